@@ -1,0 +1,134 @@
+"""ctypes binding of the oracle (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module; the product (shrewd_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "librv64se.so")
+
+OUTCOME_DT = np.dtype([("cls", "u1"), ("sub", "u1"), ("exit_code", "u1"), ("flags", "u1"),
+                       ("detail", "<u4"), ("ninst", "<u8")])
+SITE_DT = np.dtype([("inst", "<u8"), ("mask", "<u8"), ("addr", "<u8"), ("target", "<u4"), ("trial", "<u4")])
+
+
+class Golden(C.Structure):
+    _fields_ = [("ninst", C.c_uint64), ("ncycles", C.c_uint64), ("exit_code", C.c_uint32), ("cls", C.c_uint32),
+                ("stdout_len", C.c_uint64), ("stderr_len", C.c_uint64),
+                ("fetch_bytes", C.c_uint64), ("data_bytes", C.c_uint64)]
+
+
+class Probe(C.Structure):
+    _fields_ = [("rd_value", C.c_uint64), ("npc", C.c_uint64), ("fault", C.c_int32), ("rd", C.c_int32),
+                ("len", C.c_uint32), ("op", C.c_uint32)]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        L.or_create.restype = C.c_void_p
+        L.or_create.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p]
+        L.or_destroy.argtypes = [C.c_void_p]
+        L.or_error.restype = C.c_char_p
+        L.or_error.argtypes = [C.c_void_p]
+        L.or_golden.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(Golden)]
+        L.or_golden_stdout.restype = C.c_uint64
+        L.or_golden_stdout.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64]
+        L.or_sample.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]
+        L.or_run_trials.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]
+        L.or_run_one_capture.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
+                                         C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.or_probe.argtypes = [C.c_uint32, C.c_uint64, C.c_void_p, C.POINTER(Probe)]
+        L.or_mnemonic.restype = C.c_char_p
+        L.or_mnemonic.argtypes = [C.c_uint32]
+        L.or_sys_class.argtypes = [C.c_int]
+        _lib = L
+    return _lib
+
+
+class Oracle:
+    def __init__(self, elf: bytes, argv0: str):
+        self.L = lib()
+        self.h = self.L.or_create(elf, len(elf), argv0.encode())
+        err = self.L.or_error(self.h).decode()
+        if err:
+            raise RuntimeError(err)
+        self.golden = None
+
+    def close(self):
+        if self.h:
+            self.L.or_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def run_golden(self, max_inst=1 << 32) -> Golden:
+        g = Golden()
+        if self.L.or_golden(self.h, max_inst, C.byref(g)) != 0:
+            raise RuntimeError(self.L.or_error(self.h).decode())
+        self.golden = g
+        return g
+
+    def golden_stdout(self) -> bytes:
+        buf = C.create_string_buffer(1 << 20)
+        n = self.L.or_golden_stdout(self.h, buf, 1 << 20)
+        return buf.raw[:n]
+
+    def sample(self, seed, first, n, structures, burst=1) -> np.ndarray:
+        sites = np.zeros(n, SITE_DT)
+        if self.L.or_sample(self.h, seed, first, n, structures, burst, sites.ctypes.data) != 0:
+            raise RuntimeError(self.L.or_error(self.h).decode())
+        return sites
+
+    def run_trials(self, sites: np.ndarray, protect_mask=0, hang_x16=0, threads=None) -> np.ndarray:
+        sites = np.ascontiguousarray(sites, SITE_DT)
+        out = np.zeros(len(sites), OUTCOME_DT)
+        threads = threads or os.cpu_count() or 1
+        if self.L.or_run_trials(self.h, sites.ctypes.data, len(sites), protect_mask, hang_x16,
+                                out.ctypes.data, threads) != 0:
+            raise RuntimeError(self.L.or_error(self.h).decode())
+        return out
+
+    def run_one(self, site=None, protect_mask=0, hang_x16=0):
+        out = np.zeros(1, OUTCOME_DT)
+        buf = C.create_string_buffer(1 << 16)
+        n = C.c_uint64()
+        sp = None
+        if site is not None:
+            s = np.ascontiguousarray(np.array([site], SITE_DT))
+            sp = s.ctypes.data
+        self.L.or_run_one_capture(self.h, sp, protect_mask, hang_x16, out.ctypes.data, buf, 1 << 16, C.byref(n))
+        return out[0], buf.raw[:min(n.value, 1 << 16)]
+
+
+def probe(inst: int, pc: int, regs) -> Probe:
+    r = (C.c_uint64 * 32)(*[int(x) & (2**64 - 1) for x in regs])
+    p = Probe()
+    lib().or_probe(inst & 0xFFFFFFFF, pc, r, C.byref(p))
+    return p
+
+
+def mnemonic(inst: int) -> str:
+    return lib().or_mnemonic(inst & 0xFFFFFFFF).decode()
+
+
+def sys_class(num: int) -> int:
+    return lib().or_sys_class(num)

@@ -1,0 +1,1293 @@
+/*
+ * rv64se.c -- TEST INFRASTRUCTURE ONLY (see rv64se.h).
+ *
+ * Plain-C restatement of gem5's RISC-V AtomicSimpleCPU in SE mode, limited to
+ * what a fault-injection trial of a static RV64 Linux binary exercises.  The
+ * per-tick loop, decoder state machine, instruction semantics, SE memory
+ * fixups, syscall subset and fault disposition each cite the reference
+ * location they follow.  Everything outside the modelled subset is reported as
+ * an explicit ESCAPE outcome, never guessed.
+ */
+#define _GNU_SOURCE
+#include "rv64se.h"
+
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define PAGE 4096ULL
+#define PAGE_MASK (~(PAGE - 1))
+/* RiscvProcess64 ctor, arch/riscv/process.cc:71-82 */
+#define STACK_BASE 0x7FFFFFFFFFFFFFFFULL
+#define MAX_STACK (8ULL * 1024 * 1024)
+/* Process params defaults, sim/Process.py:61-67 */
+#define PID 100
+#define PPID 0
+#define UID 100
+#define GID 100
+
+typedef uint64_t u64;
+typedef int64_t s64;
+typedef uint32_t u32;
+typedef int32_t s32;
+
+/* ------------------------------------------------------------------ pages */
+typedef struct {
+    u64 vpn;     /* page number; UINT64_MAX = empty */
+    uint8_t *data;
+    int owned;   /* 1 = private copy, 0 = shared image page */
+} pte_t;
+
+typedef struct {
+    pte_t *tab;
+    u64 cap, n;
+} pmap_t;
+
+static u64 hash_vpn(u64 v) { v ^= v >> 29; v *= 0xBF58476D1CE4E5B9ULL; v ^= v >> 32; return v; }
+
+static void pm_init(pmap_t *m, u64 cap) {
+    m->cap = cap; m->n = 0;
+    m->tab = (pte_t *)malloc(sizeof(pte_t) * cap);
+    for (u64 i = 0; i < cap; i++) { m->tab[i].vpn = UINT64_MAX; m->tab[i].data = NULL; m->tab[i].owned = 0; }
+}
+static pte_t *pm_find(pmap_t *m, u64 vpn) {
+    u64 i = hash_vpn(vpn) & (m->cap - 1);
+    for (;;) {
+        if (m->tab[i].vpn == vpn) return &m->tab[i];
+        if (m->tab[i].vpn == UINT64_MAX) return NULL;
+        i = (i + 1) & (m->cap - 1);
+    }
+}
+static pte_t *pm_insert(pmap_t *m, u64 vpn, uint8_t *data, int owned);
+static void pm_grow(pmap_t *m) {
+    pmap_t n2; pm_init(&n2, m->cap * 2);
+    for (u64 i = 0; i < m->cap; i++)
+        if (m->tab[i].vpn != UINT64_MAX) pm_insert(&n2, m->tab[i].vpn, m->tab[i].data, m->tab[i].owned);
+    free(m->tab); *m = n2;
+}
+static pte_t *pm_insert(pmap_t *m, u64 vpn, uint8_t *data, int owned) {
+    if ((m->n + 1) * 2 > m->cap) pm_grow(m);
+    u64 i = hash_vpn(vpn) & (m->cap - 1);
+    while (m->tab[i].vpn != UINT64_MAX && m->tab[i].vpn != vpn) i = (i + 1) & (m->cap - 1);
+    if (m->tab[i].vpn == UINT64_MAX) m->n++;
+    m->tab[i].vpn = vpn; m->tab[i].data = data; m->tab[i].owned = owned;
+    return &m->tab[i];
+}
+static void pm_free(pmap_t *m) {
+    for (u64 i = 0; i < m->cap; i++)
+        if (m->tab[i].vpn != UINT64_MAX && m->tab[i].owned) free(m->tab[i].data);
+    free(m->tab);
+}
+
+/* ------------------------------------------------------------- campaign */
+typedef struct { uint8_t *buf; u64 len, cap; } bytes_t;
+static void by_push(bytes_t *b, const uint8_t *p, u64 n) {
+    if (b->len + n > b->cap) {
+        u64 nc = b->cap ? b->cap : 256;
+        while (nc < b->len + n) nc *= 2;
+        b->buf = (uint8_t *)realloc(b->buf, nc); b->cap = nc;
+    }
+    memcpy(b->buf + b->len, p, n); b->len += n;
+}
+
+struct or_campaign {
+    pmap_t image;          /* initial process image pages (shared, read-only) */
+    u64 entry, sp0, stack_min0;
+    u64 stack_vma_lo, stack_vma_hi;  /* the "stack" VMA created by argsInit */
+    u64 brk0;
+    u64 *mem_pages;        /* writable pages at process start (memory fault candidates) */
+    u64 n_mem_pages;
+    /* golden */
+    int have_golden;
+    or_golden_t golden;
+    bytes_t gout, gerr;
+    char err[256];
+};
+
+const char *or_error(or_campaign_t *c) { return c ? c->err : "null campaign"; }
+
+/* ---------------------------------------------------------------- machine */
+typedef struct {
+    u64 x[32];
+    u64 pc, npc;
+    u64 num_inst, num_cycles;
+    /* decoder state machine, arch/riscv/decoder.cc:54-116 */
+    int mid; u32 emi; int inst_done;
+    u64 fetch_offset; int stay_at_pc;
+    pmap_t mem;
+    u64 stack_min;
+    bytes_t out, err;
+    /* fault injection */
+    const or_site_t *site; int injected; int watch; /* watch = protected flipped reg, -1 none */
+    u64 protect_mask;
+    /* termination */
+    int done; or_outcome_t res;
+    /* counters for the roofline bookkeeping */
+    u64 fetch_bytes, data_bytes;
+    const or_campaign_t *c;
+} mach_t;
+
+enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_ESCAPE = 5, F_PGFAULT = 6 };
+
+/* -------------------------------------------------------------- decode */
+/* Op ids.  Names follow gem5's mnemonics (arch/riscv/isa/decoder.isa). */
+#define OPS(X) \
+    X(UNKNOWN) X(ESC_FP) X(ESC_VEC) X(ESC_AMO) X(ESC_SYS) X(ESC_CRYPTO) X(ESC_CBO) X(ESC_CMP) X(ESC_M5) X(ESC_HYP) \
+    X(c_addi4spn) X(c_lw) X(c_ld) X(c_lbu) X(c_lhu) X(c_lh) X(c_sb) X(c_sh) X(c_sw) X(c_sd) \
+    X(c_addi) X(c_addiw) X(c_li) X(c_addi16sp) X(c_lui) X(c_srli) X(c_srai) X(c_andi) \
+    X(c_sub) X(c_xor) X(c_or) X(c_and) X(c_subw) X(c_addw) X(c_mul) \
+    X(c_zext_b) X(c_sext_b) X(c_zext_h) X(c_sext_h) X(c_zext_w) X(c_not) \
+    X(c_j) X(c_beqz) X(c_bnez) X(c_slli) X(c_lwsp) X(c_ldsp) X(c_jr) X(c_mv) X(c_ebreak) X(c_jalr) X(c_add) \
+    X(c_swsp) X(c_sdsp) \
+    X(lb) X(lh) X(lw) X(ld) X(lbu) X(lhu) X(lwu) X(fence) X(fence_i) \
+    X(slli) X(bseti) X(bclri) X(binvi) X(clz) X(ctz) X(cpop) X(sext_b) X(sext_h) \
+    X(addi) X(slti) X(sltiu) X(xori) X(srli) X(orc_b) X(srai) X(bexti) X(rori) X(rev8) \
+    X(prefetch_i) X(prefetch_r) X(prefetch_w) X(ori_hint) X(ori) X(andi) X(auipc) \
+    X(addiw) X(slliw) X(slli_uw) X(clzw) X(ctzw) X(cpopw) X(srliw) X(sraiw) X(roriw) \
+    X(sb) X(sh) X(sw) X(sd) \
+    X(add) X(sub) X(mul) X(sll) X(mulh) X(clmul) X(bset) X(bclr) X(rol) X(binv) \
+    X(slt) X(mulhsu) X(clmulr) X(sh1add) X(sltu) X(mulhu) X(clmulh) \
+    X(xor_) X(div_) X(pack) X(min_) X(sh2add) X(xnor) \
+    X(srl) X(divu) X(czero_eqz) X(sra) X(minu) X(bext) X(ror) \
+    X(or_) X(rem) X(max_) X(sh3add) X(orn) \
+    X(and_) X(remu) X(packh) X(maxu) X(czero_nez) X(andn) \
+    X(lui) X(addw) X(mulw) X(add_uw) X(subw) X(sllw) X(rolw) X(sh1add_uw) \
+    X(divw) X(packw) X(sh2add_uw) X(srlw) X(divuw) X(sraw) X(rorw) X(remw) X(sh3add_uw) X(remuw) \
+    X(beq) X(bne) X(blt) X(bge) X(bltu) X(bgeu) X(jalr) X(jal) \
+    X(ecall) X(ebreak) X(csr)
+
+enum {
+#define X(n) OP_##n,
+    OPS(X)
+#undef X
+    OP_COUNT
+};
+static const char *op_names[] = {
+#define X(n) #n,
+    OPS(X)
+#undef X
+};
+
+typedef struct {
+    u32 raw; u32 len;
+    int op;
+    int rd, rs1, rs2;     /* -1 = not used */
+    s64 imm;
+    u32 csr, funct3;
+} dec_t;
+
+static inline u32 bits(u32 v, int hi, int lo) { return (v >> lo) & ((hi - lo == 31) ? 0xFFFFFFFFu : ((1u << (hi - lo + 1)) - 1)); }
+static inline s64 sext(u64 v, int n) { return (s64)(v << (64 - n)) >> (64 - n); }
+
+/* Decode one instruction (16- or 32-bit in the low bits of raw) following the
+ * decode tree of arch/riscv/isa/decoder.isa for rv_type=RV64, enable_zcd=1
+ * (RiscvISA.py:95,121-127).  Field definitions: isa/bitfields.isa:36-130. */
+static void decode(u32 raw, dec_t *d) {
+    memset(d, 0, sizeof(*d));
+    d->raw = raw; d->rd = d->rs1 = d->rs2 = -1; d->op = OP_UNKNOWN;
+    u32 q = raw & 3;
+    if (q != 3) {  /* compressed: decoder.isa:43-536 */
+        raw &= 0xFFFF; d->raw = raw; d->len = 2;
+        u32 cop = bits(raw, 15, 13);
+        u32 rp1 = 8 + bits(raw, 9, 7), rp2 = 8 + bits(raw, 4, 2);
+        u32 rc1 = bits(raw, 11, 7), rc2 = bits(raw, 6, 2);
+        u32 cimm5 = bits(raw, 6, 2), cimm1 = bits(raw, 12, 12), cimm3 = bits(raw, 12, 10), cimm2 = bits(raw, 6, 5);
+        u32 cimm6 = bits(raw, 12, 7), cimm8 = bits(raw, 12, 5);
+        if (q == 0) {
+            switch (cop) {
+            case 0: d->op = OP_c_addi4spn; d->rd = rp2; d->rs1 = 2;
+                d->imm = (bits(cimm8, 1, 1) << 2) | (bits(cimm8, 0, 0) << 3) | (bits(cimm8, 7, 6) << 4) | (bits(cimm8, 5, 2) << 6);
+                return;
+            case 1: d->op = OP_ESC_FP; return;                        /* c_fld (ENABLE_ZCD=1) */
+            case 2: d->op = OP_c_lw; d->rd = rp2; d->rs1 = rp1;
+                d->imm = (bits(cimm2, 1, 1) << 2) | (cimm3 << 3) | (bits(cimm2, 0, 0) << 6); return;
+            case 3: d->op = OP_c_ld; d->rd = rp2; d->rs1 = rp1; d->imm = (cimm3 << 3) | (cimm2 << 6); return;
+            case 4:
+                switch (bits(raw, 12, 10)) {
+                case 0: d->op = OP_c_lbu; d->rd = rp2; d->rs1 = rp1; d->imm = (bits(cimm2, 0, 0) << 1) | bits(cimm2, 1, 1); return;
+                case 1: d->op = bits(raw, 6, 6) ? OP_c_lh : OP_c_lhu; d->rd = rp2; d->rs1 = rp1; d->imm = bits(cimm2, 0, 0) << 1; return;
+                case 2: d->op = OP_c_sb; d->rs1 = rp1; d->rs2 = rp2; d->imm = (bits(cimm2, 0, 0) << 1) | bits(cimm2, 1, 1); return;
+                case 3: d->op = OP_c_sh; d->rs1 = rp1; d->rs2 = rp2; d->imm = bits(cimm2, 0, 0) << 1; return;
+                default: return;
+                }
+            case 5: d->op = OP_ESC_FP; return;                        /* c_fsd */
+            case 6: d->op = OP_c_sw; d->rs1 = rp1; d->rs2 = rp2;
+                d->imm = (bits(cimm2, 1, 1) << 2) | (cimm3 << 3) | (bits(cimm2, 0, 0) << 6); return;
+            case 7: d->op = OP_c_sd; d->rs1 = rp1; d->rs2 = rp2; d->imm = (cimm3 << 3) | (cimm2 << 6); return;
+            }
+        } else if (q == 1) {
+            switch (cop) {
+            case 0: d->op = OP_c_addi; d->rd = d->rs1 = rc1; d->imm = sext(cimm5 | (cimm1 << 5), 6); return;
+            case 1: d->op = OP_c_addiw; d->rd = d->rs1 = rc1; d->imm = sext(cimm5 | (cimm1 << 5), 6); return;
+            case 2: d->op = OP_c_li; d->rd = rc1; d->imm = sext(cimm5 | (cimm1 << 5), 6); return;
+            case 3:
+                if (rc1 == 2) {
+                    d->op = OP_c_addi16sp; d->rd = d->rs1 = 2;
+                    d->imm = sext((bits(cimm5, 4, 4) << 4) | (bits(cimm5, 0, 0) << 5) | (bits(cimm5, 3, 3) << 6) |
+                                  (bits(cimm5, 2, 1) << 7) | (cimm1 << 9), 10);
+                } else {
+                    d->op = OP_c_lui; d->rd = rc1; d->imm = sext(cimm5 | (cimm1 << 5), 6) * 4096;
+                }
+                return;
+            case 4:
+                switch (bits(raw, 11, 10)) {
+                case 0: d->op = OP_c_srli; d->rd = d->rs1 = rp1; d->imm = cimm5 | (cimm1 << 5); return;
+                case 1: d->op = OP_c_srai; d->rd = d->rs1 = rp1; d->imm = cimm5 | (cimm1 << 5); return;
+                case 2: d->op = OP_c_andi; d->rd = d->rs1 = rp1; d->imm = sext(cimm5 | (cimm1 << 5), 6); return;
+                case 3: {
+                    u32 f2 = bits(raw, 6, 5);
+                    d->rd = d->rs1 = rp1; d->rs2 = rp2;
+                    if (!cimm1) {
+                        static const int o[4] = {OP_c_sub, OP_c_xor, OP_c_or, OP_c_and};
+                        d->op = o[f2]; return;
+                    }
+                    switch (f2) {
+                    case 0: d->op = OP_c_subw; return;
+                    case 1: d->op = OP_c_addw; return;
+                    case 2: d->op = OP_c_mul; return;
+                    case 3:
+                        d->rs2 = -1;
+                        switch (bits(raw, 4, 2)) {
+                        case 0: d->op = OP_c_zext_b; return;
+                        case 1: d->op = OP_c_sext_b; return;
+                        case 2: d->op = OP_c_zext_h; return;
+                        case 3: d->op = OP_c_sext_h; return;
+                        case 4: d->op = OP_c_zext_w; return;
+                        case 5: d->op = OP_c_not; return;
+                        default: d->rd = d->rs1 = -1; d->op = OP_UNKNOWN; return;
+                        }
+                    }
+                }
+                }
+                return;
+            case 5: d->op = OP_c_j;
+                d->imm = sext((bits(raw, 5, 3) << 1) | (bits(raw, 11, 11) << 4) | (bits(raw, 2, 2) << 5) |
+                              (bits(raw, 7, 7) << 6) | (bits(raw, 6, 6) << 7) | (bits(raw, 10, 9) << 8) |
+                              (bits(raw, 8, 8) << 10) | (bits(raw, 12, 12) << 11), 12);
+                return;
+            case 6: case 7:
+                d->op = cop == 6 ? OP_c_beqz : OP_c_bnez; d->rs1 = rp1;
+                d->imm = sext((bits(cimm5, 2, 1) << 1) | (bits(cimm3, 1, 0) << 3) | (bits(cimm5, 0, 0) << 5) |
+                              (bits(cimm5, 4, 3) << 6) | (bits(cimm3, 2, 2) << 8), 9);
+                return;
+            }
+        } else { /* q == 2 */
+            switch (cop) {
+            case 0: d->op = OP_c_slli; d->rd = d->rs1 = rc1; d->imm = cimm5 | (cimm1 << 5); return;
+            case 1: d->op = OP_ESC_FP; return;                        /* c_fldsp */
+            case 2: d->op = OP_c_lwsp; d->rd = rc1; d->rs1 = 2;
+                d->imm = (bits(cimm5, 4, 2) << 2) | (cimm1 << 5) | (bits(cimm5, 1, 0) << 6); return;
+            case 3: d->op = OP_c_ldsp; d->rd = rc1; d->rs1 = 2;
+                d->imm = (bits(cimm5, 4, 3) << 3) | (cimm1 << 5) | (bits(cimm5, 2, 0) << 6); return;
+            case 4:
+                if (!cimm1) {
+                    if (rc2 == 0) { d->op = OP_c_jr; d->rs1 = rc1; }
+                    else { d->op = OP_c_mv; d->rd = rc1; d->rs2 = rc2; }
+                } else {
+                    if (rc2 == 0) {
+                        if (rc1 == 0) d->op = OP_c_ebreak;
+                        else { d->op = OP_c_jalr; d->rd = 1; d->rs1 = rc1; }
+                    } else { d->op = OP_c_add; d->rd = d->rs1 = rc1; d->rs2 = rc2; }
+                }
+                return;
+            case 5: d->op = OP_ESC_FP; return;                        /* c_fsdsp (ENABLE_ZCD=1) */
+            case 6: d->op = OP_c_swsp; d->rs1 = 2; d->rs2 = rc2; d->imm = (bits(cimm6, 5, 2) << 2) | (bits(cimm6, 1, 0) << 6); return;
+            case 7: d->op = OP_c_sdsp; d->rs1 = 2; d->rs2 = rc2; d->imm = (bits(cimm6, 5, 3) << 3) | (bits(cimm6, 2, 0) << 6); return;
+            }
+        }
+        return;
+    }
+    /* 32-bit: decoder.isa:537-6365 */
+    d->len = 4;
+    u32 opc = bits(raw, 6, 2), f3 = bits(raw, 14, 12), f7 = bits(raw, 31, 25);
+    u32 rd = bits(raw, 11, 7), rs1 = bits(raw, 19, 15), rs2 = bits(raw, 24, 20);
+    u32 fs3 = bits(raw, 31, 27);   /* FS3 <31:27> */
+    s64 imm_i = sext(bits(raw, 31, 20), 12);
+    s64 imm_s = sext((bits(raw, 31, 25) << 5) | bits(raw, 11, 7), 12);
+    s64 imm_b = sext((bits(raw, 31, 31) << 12) | (bits(raw, 7, 7) << 11) | (bits(raw, 30, 25) << 5) | (bits(raw, 11, 8) << 1), 13);
+    s64 imm_j = sext((bits(raw, 31, 31) << 20) | (bits(raw, 19, 12) << 12) | (bits(raw, 20, 20) << 11) | (bits(raw, 30, 21) << 1), 21);
+    d->funct3 = f3;
+    switch (opc) {
+    case 0x00: {  /* LOAD :538-566 */
+        static const int o[8] = {OP_lb, OP_lh, OP_lw, OP_ld, OP_lbu, OP_lhu, OP_lwu, OP_UNKNOWN};
+        d->op = o[f3];
+        if (d->op != OP_UNKNOWN) { d->rd = rd; d->rs1 = rs1; d->imm = imm_i; }
+        return;
+    }
+    case 0x01: d->op = OP_ESC_FP; return;      /* LOAD-FP / vector loads */
+    case 0x03:  /* MISC-MEM :1336-1433 */
+        if (f3 == 0) { d->op = OP_fence; return; }
+        if (f3 == 1) { d->op = OP_fence_i; return; }
+        if (f3 == 2 && rd == 0) {
+            u32 f12 = bits(raw, 31, 20);
+            if (f12 == 0 || f12 == 1 || f12 == 2 || f12 == 4) { d->op = OP_ESC_CBO; return; }
+        }
+        return;
+    case 0x04:  /* OP-IMM :1435-1670 */
+        d->rd = rd; d->rs1 = rs1;
+        switch (f3) {
+        case 0: d->op = OP_addi; d->imm = imm_i; return;
+        case 1:
+            switch (fs3) {
+            case 0x00: d->op = OP_slli; d->imm = bits(raw, 25, 20); return;
+            case 0x02:
+                if (rs2 <= 9) { d->op = OP_ESC_CRYPTO; return; }   /* sha256/sha512/sm3 */
+                break;
+            case 0x05: d->op = OP_bseti; d->imm = bits(raw, 25, 20); return;
+            case 0x06: d->op = OP_ESC_CRYPTO; return;             /* aes64im / aes64ks1i (RV64) */
+            case 0x09: d->op = OP_bclri; d->imm = bits(raw, 25, 20); return;
+            case 0x0d: d->op = OP_binvi; d->imm = bits(raw, 25, 20); return;
+            case 0x0c:
+                switch (rs2) {
+                case 0: d->op = OP_clz; return;
+                case 1: d->op = OP_ctz; return;
+                case 2: d->op = OP_cpop; return;
+                case 4: d->op = OP_sext_b; return;
+                case 5: d->op = OP_sext_h; return;
+                }
+                break;
+            }
+            break;
+        case 2: d->op = OP_slti; d->imm = imm_i; return;
+        case 3: d->op = OP_sltiu; d->imm = imm_i; return;
+        case 4: d->op = OP_xori; d->imm = imm_i; return;
+        case 5:
+            switch (fs3) {
+            case 0x0: d->op = OP_srli; d->imm = bits(raw, 25, 20); return;
+            case 0x5: d->op = OP_orc_b; d->imm = bits(raw, 25, 20); return;
+            case 0x8: d->op = OP_srai; d->imm = bits(raw, 25, 20); return;
+            case 0x9: d->op = OP_bexti; d->imm = bits(raw, 25, 20); return;
+            case 0xc: d->op = OP_rori; d->imm = bits(raw, 25, 20); return;
+            case 0xd:
+                if (rs2 == 0x18) { d->op = OP_rev8; return; }
+                if (rs2 == 0x07) { d->op = OP_ESC_CRYPTO; return; }   /* brev8 */
+                break;
+            }
+            break;
+        case 6:
+            if (rd == 0) {
+                if (rs2 == 0) { d->op = OP_prefetch_i; d->rd = -1; d->imm = bits(raw, 31, 25) << 5; return; }
+                if (rs2 == 1) { d->op = OP_prefetch_r; d->rd = -1; d->imm = bits(raw, 31, 25) << 5; return; }
+                if (rs2 == 3) { d->op = OP_prefetch_w; d->rd = -1; d->imm = bits(raw, 31, 25) << 5; return; }
+                d->op = OP_ori_hint; d->imm = imm_i; return;
+            }
+            d->op = OP_ori; d->imm = imm_i; return;
+        case 7: d->op = OP_andi; d->imm = imm_i; return;
+        }
+        d->rd = d->rs1 = -1; d->op = OP_UNKNOWN; return;
+    case 0x05: d->op = OP_auipc; d->rd = rd; d->imm = sext(bits(raw, 31, 12), 20) * 4096; return;
+    case 0x06:  /* OP-IMM-32 :1676-1720 */
+        d->rd = rd; d->rs1 = rs1;
+        if (f3 == 0) { d->op = OP_addiw; d->imm = imm_i; return; }
+        if (f3 == 1) {
+            if (fs3 == 0x0) { d->op = OP_slliw; d->imm = bits(raw, 24, 20); return; }
+            if (fs3 == 0x1) { d->op = OP_slli_uw; d->imm = bits(raw, 25, 20); return; }
+            if (fs3 == 0xc) {
+                if (rs2 == 0) { d->op = OP_clzw; return; }
+                if (rs2 == 1) { d->op = OP_ctzw; return; }
+                if (rs2 == 2) { d->op = OP_cpopw; return; }
+            }
+        }
+        if (f3 == 5) {
+            if (fs3 == 0x0) { d->op = OP_srliw; d->imm = bits(raw, 24, 20); return; }
+            if (fs3 == 0x8) { d->op = OP_sraiw; d->imm = bits(raw, 24, 20); return; }
+            if (fs3 == 0xc) { d->op = OP_roriw; d->imm = bits(raw, 24, 20); return; }
+        }
+        d->rd = d->rs1 = -1; d->op = OP_UNKNOWN; return;
+    case 0x08: {  /* STORE :1722-1739 */
+        static const int o[8] = {OP_sb, OP_sh, OP_sw, OP_sd, OP_UNKNOWN, OP_UNKNOWN, OP_UNKNOWN, OP_UNKNOWN};
+        d->op = o[f3];
+        if (d->op != OP_UNKNOWN) { d->rs1 = rs1; d->rs2 = rs2; d->imm = imm_s; }
+        return;
+    }
+    case 0x09: d->op = OP_ESC_FP; return;      /* STORE-FP / vector stores */
+    case 0x0b: d->op = OP_ESC_AMO; return;     /* AMO :2067-2283 */
+    case 0x0c: {  /* OP :2285-2613 */
+        d->rd = rd; d->rs1 = rs1; d->rs2 = rs2;
+        u32 kf5 = bits(raw, 29, 25), bs = bits(raw, 31, 30);
+        switch (f3) {
+        case 0:
+            if (kf5 == 0x00) { if (bs == 0) { d->op = OP_add; return; } if (bs == 1) { d->op = OP_sub; return; } break; }
+            if (kf5 == 0x01) { if (bs == 0) { d->op = OP_mul; return; } break; }
+            if (kf5 == 0x11 || kf5 == 0x13 || kf5 == 0x15 || kf5 == 0x17) break;   /* RV32-only aes32* */
+            if (kf5 == 0x08 || kf5 == 0x09 || kf5 == 0x0a || kf5 == 0x0b || kf5 == 0x0e || kf5 == 0x0f) break; /* RV32 sha512 */
+            if (kf5 == 0x18 || kf5 == 0x1a) { d->op = OP_ESC_CRYPTO; return; }     /* sm4ed / sm4ks */
+            if (kf5 == 0x19 || kf5 == 0x1b || kf5 == 0x1d) { if (bs == 0) { d->op = OP_ESC_CRYPTO; return; } break; }
+            if (kf5 == 0x1f) { if (bs <= 1) { d->op = OP_ESC_CRYPTO; return; } break; }
+            break;
+        case 1:
+            switch (f7) { case 0x0: d->op = OP_sll; return; case 0x1: d->op = OP_mulh; return; case 0x5: d->op = OP_clmul; return;
+            case 0x14: d->op = OP_bset; return; case 0x24: d->op = OP_bclr; return; case 0x30: d->op = OP_rol; return;
+            case 0x34: d->op = OP_binv; return; }
+            break;
+        case 2:
+            switch (f7) { case 0x0: d->op = OP_slt; return; case 0x1: d->op = OP_mulhsu; return; case 0x5: d->op = OP_clmulr; return;
+            case 0x10: d->op = OP_sh1add; return; case 0x14: d->op = OP_ESC_CRYPTO; return; }
+            break;
+        case 3:
+            switch (f7) { case 0x0: d->op = OP_sltu; return; case 0x1: d->op = OP_mulhu; return; case 0x5: d->op = OP_clmulh; return; }
+            break;
+        case 4:
+            switch (f7) { case 0x0: d->op = OP_xor_; return; case 0x1: d->op = OP_div_; return; case 0x4: d->op = OP_pack; return;
+            case 0x5: d->op = OP_min_; return; case 0x10: d->op = OP_sh2add; return; case 0x14: d->op = OP_ESC_CRYPTO; return;
+            case 0x20: d->op = OP_xnor; return; }
+            break;
+        case 5:
+            switch (f7) { case 0x0: d->op = OP_srl; return; case 0x1: d->op = OP_divu; return; case 0x7: d->op = OP_czero_eqz; return;
+            case 0x20: d->op = OP_sra; return; case 0x5: d->op = OP_minu; return; case 0x24: d->op = OP_bext; return;
+            case 0x30: d->op = OP_ror; return; }
+            break;
+        case 6:
+            switch (f7) { case 0x0: d->op = OP_or_; return; case 0x1: d->op = OP_rem; return; case 0x5: d->op = OP_max_; return;
+            case 0x10: d->op = OP_sh3add; return; case 0x20: d->op = OP_orn; return; }
+            break;
+        case 7:
+            switch (f7) { case 0x0: d->op = OP_and_; return; case 0x1: d->op = OP_remu; return; case 0x4: d->op = OP_packh; return;
+            case 0x5: d->op = OP_maxu; return; case 0x7: d->op = OP_czero_nez; return; case 0x20: d->op = OP_andn; return; }
+            break;
+        }
+        d->rd = d->rs1 = d->rs2 = -1; d->op = OP_UNKNOWN; return;
+    }
+    case 0x0d: d->op = OP_lui; d->rd = rd; d->imm = sext(bits(raw, 31, 12), 20) * 4096; return;
+    case 0x0e:  /* OP-32 :2620-2692 */
+        d->rd = rd; d->rs1 = rs1; d->rs2 = rs2;
+        switch (f3) {
+        case 0: switch (f7) { case 0x0: d->op = OP_addw; return; case 0x1: d->op = OP_mulw; return;
+                case 0x4: d->op = OP_add_uw; return; case 0x20: d->op = OP_subw; return; } break;
+        case 1: switch (f7) { case 0x0: d->op = OP_sllw; return; case 0x30: d->op = OP_rolw; return; } break;
+        case 2: if (f7 == 0x10) { d->op = OP_sh1add_uw; return; } break;
+        case 4: switch (f7) { case 0x1: d->op = OP_divw; return; case 0x4: d->op = OP_packw; return;
+                case 0x10: d->op = OP_sh2add_uw; return; } break;
+        case 5: switch (f7) { case 0x0: d->op = OP_srlw; return; case 0x1: d->op = OP_divuw; return;
+                case 0x20: d->op = OP_sraw; return; case 0x30: d->op = OP_rorw; return; } break;
+        case 6: switch (f7) { case 0x1: d->op = OP_remw; return; case 0x10: d->op = OP_sh3add_uw; return; } break;
+        case 7: d->op = OP_remuw; return;          /* decoded on FUNCT3 alone (:2687-2689) */
+        }
+        d->rd = d->rs1 = d->rs2 = -1; d->op = OP_UNKNOWN; return;
+    case 0x10: case 0x11: case 0x12: case 0x13: case 0x14: d->op = OP_ESC_FP; return;
+    case 0x15: d->op = OP_ESC_VEC; return;
+    case 0x18: {  /* BRANCH :5891-5936 */
+        static const int o[8] = {OP_beq, OP_bne, OP_UNKNOWN, OP_UNKNOWN, OP_blt, OP_bge, OP_bltu, OP_bgeu};
+        d->op = o[f3];
+        if (d->op != OP_UNKNOWN) { d->rs1 = rs1; d->rs2 = rs2; d->imm = imm_b; }
+        return;
+    }
+    case 0x19:  /* JALR :5938-5943 */
+        if (f3 == 0) { d->op = OP_jalr; d->rd = rd; d->rs1 = rs1; d->imm = imm_i; }
+        return;
+    case 0x1b: d->op = OP_jal; d->rd = rd; d->imm = imm_j; return;   /* :5945-5948 */
+    case 0x1c:  /* SYSTEM :5950-6300 */
+        if (f3 == 0) {
+            if (f7 == 0) {
+                if (rs2 == 0) { d->op = OP_ecall; return; }
+                if (rs2 == 1) { d->op = OP_ebreak; return; }
+                return;
+            }
+            d->op = OP_ESC_SYS; return;
+        }
+        if (f3 == 4) { d->op = OP_ESC_HYP; return; }
+        d->op = OP_csr; d->rd = rd; d->rs1 = (f3 >= 5) ? -1 : (int)rs1; d->csr = bits(raw, 31, 20);
+        d->imm = rs1;  /* uimm for csrr*i */
+        return;
+    case 0x1e: d->op = OP_ESC_M5; return;      /* M5Op :6363 */
+    default: return;
+    }
+}
+
+const char *or_mnemonic(u32 inst) {
+    dec_t d; decode(inst, &d);
+    static __thread char buf[64];
+    if (d.op == OP_UNKNOWN) return "unknown";
+    if (d.op < OP_c_addi4spn) { snprintf(buf, sizeof buf, "escape:%s", op_names[d.op]); return buf; }
+    if (d.op == OP_csr) {
+        static const char *cn[8] = {"?", "csrrw", "csrrs", "csrrc", "?", "csrrwi", "csrrsi", "csrrci"};
+        return cn[d.funct3];
+    }
+    const char *n = op_names[d.op];
+    size_t l = strlen(n);
+    if (l && n[l - 1] == '_') { snprintf(buf, sizeof buf, "%.*s", (int)(l - 1), n); return buf; }
+    return n;
+}
+
+/* ---------------------------------------------------------- memory access */
+/* SE translation: arch/riscv/tlb.cc:573-604 -> EmulationPageTable::translate
+ * (mem/page_table.cc:143-153).  Returns page data or NULL (page-table fault). */
+static uint8_t *translate(mach_t *m, u64 vaddr) {
+    pte_t *p = pm_find(&m->mem, vaddr >> 12);
+    return p ? p->data : NULL;
+}
+static uint8_t *translate_w(mach_t *m, u64 vaddr) {
+    pte_t *p = pm_find(&m->mem, vaddr >> 12);
+    if (!p) return NULL;
+    if (!p->owned) {
+        uint8_t *n = (uint8_t *)malloc(PAGE);
+        memcpy(n, p->data, PAGE);
+        p->data = n; p->owned = 1;
+    }
+    return p->data;
+}
+
+/* Process::allocateMem for one page, zero-filled (sim/process.cc:318-343). */
+static void alloc_page(mach_t *m, u64 vaddr) {
+    u64 vpn = vaddr >> 12;
+    if (pm_find(&m->mem, vpn)) return;
+    uint8_t *n = (uint8_t *)calloc(1, PAGE);
+    pm_insert(&m->mem, vpn, n, 1);
+}
+
+/* MemState::fixupFault, sim/mem_state.cc:387-447.  Returns 1 handled, 0 not
+ * handled (panic), -1 fatal("Maximum stack size exceeded"). */
+static int fixup_fault(mach_t *m, u64 vaddr) {
+    const or_campaign_t *c = m->c;
+    if (vaddr >= c->stack_vma_lo && vaddr < c->stack_vma_hi) { alloc_page(m, vaddr & PAGE_MASK); return 1; }
+    if (vaddr >= m->stack_min && vaddr < STACK_BASE) { alloc_page(m, vaddr & PAGE_MASK); return 1; }
+    if (vaddr < m->stack_min && vaddr >= STACK_BASE - MAX_STACK) {
+        while (vaddr < m->stack_min) {
+            m->stack_min -= PAGE;
+            if (STACK_BASE - m->stack_min > MAX_STACK) return -1;
+            alloc_page(m, m->stack_min);
+        }
+        return 1;
+    }
+    return 0;
+}
+
+/* AtomicSimpleCPU::readMem: fragments split at 64-byte lines, each translated
+ * separately; the first fragment that faults aborts the access
+ * (cpu/simple/atomic.cc:331-434).  fault_va receives the faulting fragment. */
+static int mem_read(mach_t *m, u64 addr, unsigned size, u64 *val, u64 *fault_va) {
+    uint8_t buf[8];
+    unsigned done = 0;
+    u64 a = addr;
+    while (done < size) {
+        unsigned frag = 64 - (unsigned)(a & 63);
+        if (frag > size - done) frag = size - done;
+        if (a + frag - 1 < a) { *fault_va = a; return F_PGFAULT; }   /* tlb.cc:589-590 */
+        uint8_t *pg = translate(m, a);
+        if (!pg) { *fault_va = a; return F_PGFAULT; }
+        for (unsigned i = 0; i < frag; i++) {
+            u64 b = a + i;   /* fragment lies within one page (64-byte line) */
+            buf[done + i] = pg[b & (PAGE - 1)];
+        }
+        done += frag; a += frag;
+    }
+    u64 v = 0;
+    for (unsigned i = 0; i < size; i++) v |= (u64)buf[i] << (8 * i);
+    *val = v;
+    m->data_bytes += size;
+    return F_NONE;
+}
+/* AtomicSimpleCPU::writeMem (atomic.cc:437-544): fragments written in order,
+ * a faulting second fragment leaves the first one written. */
+static int mem_write(mach_t *m, u64 addr, unsigned size, u64 val, u64 *fault_va) {
+    unsigned done = 0;
+    u64 a = addr;
+    while (done < size) {
+        unsigned frag = 64 - (unsigned)(a & 63);
+        if (frag > size - done) frag = size - done;
+        if (a + frag - 1 < a) { *fault_va = a; return F_PGFAULT; }
+        uint8_t *pg = translate_w(m, a);
+        if (!pg) { *fault_va = a; return F_PGFAULT; }
+        for (unsigned i = 0; i < frag; i++) pg[(a + i) & (PAGE - 1)] = (uint8_t)(val >> (8 * (done + i)));
+        done += frag; a += frag;
+    }
+    m->data_bytes += size;
+    return F_NONE;
+}
+
+/* ------------------------------------------------------------- terminate */
+static void finish(mach_t *m, int cls, int sub, int exit_code) {
+    m->done = 1;
+    m->res.cls = (uint8_t)cls; m->res.sub = (uint8_t)sub; m->res.exit_code = (uint8_t)exit_code;
+    m->res.flags = (uint8_t)(m->injected ? 1 : 0);
+    m->res.detail = (u32)m->pc;
+    m->res.ninst = m->num_inst;
+}
+
+/* ------------------------------------------------------------- syscalls */
+/* Classification of the RV64 Linux syscall table (arch/riscv/linux/
+ * se_workload.cc:529-895; pinned by tests/golden/syscalls_rv64.json):
+ *   0 absent (fatal "out of range", syscall_desc.hh:204-214)
+ *   1 present without a handler (unimplementedFunc -> fatal, syscall_emul.cc:77)
+ *   2 ignoreFunc / ignoreWarnOnceFunc (returns 0, syscall_emul.cc:84-104)
+ *   3 a real gem5 handler this engine does not model (escape)
+ *   4 modelled here (write, exit, exit_group, get*id) */
+static const uint16_t sys_impl_escape[] = {
+    17, 23, 25, 29, 33, 34, 35, 38, 43, 44, 45, 46, 47, 48, 49, 52, 55, 56, 57, 59, 61, 62, 63, 66, 67, 68,
+    78, 79, 80, 96, 98, 113, 114, 121, 123, 131, 153, 154, 160, 163, 165, 166, 168, 169, 179, 198, 199, 200,
+    201, 202, 203, 204, 205, 206, 207, 208, 209, 210, 211, 212, 214, 215, 216, 220, 221, 222, 258, 260, 261,
+    278, 435, 1024, 1025, 1026, 1027, 1028, 1029, 1030, 1031, 1033, 1034, 1035, 1036, 1037, 1038, 1039, 1040,
+    1041, 1044, 1047, 1048, 1049, 1050, 1051, 1052, 1054, 1055, 1056, 1057, 1058, 1060, 1062, 1065, 1067, 1068};
+int or_sys_class(int num) {
+    if (num == 64 || num == 93 || num == 94 || (num >= 172 && num <= 178)) return 4;
+    int present = (num >= 0 && num <= 64) || (num >= 66 && num <= 243) || num == 258 ||
+                  (num >= 260 && num <= 287) || (num >= 424 && num <= 450) || (num >= 1024 && num <= 1079) ||
+                  num == 2011;
+    if (!present) return 0;
+    if (num == 99 || num == 100 || num == 101 || num == 124 || (num >= 133 && num <= 139) || num == 146 ||
+        num == 164 || (num >= 226 && num <= 233) || num == 235)
+        return 2;
+    for (size_t i = 0; i < sizeof(sys_impl_escape) / sizeof(sys_impl_escape[0]); i++)
+        if (sys_impl_escape[i] == num) return 3;
+    return 1;
+}
+
+static void do_syscall(mach_t *m) {
+    /* EmuLinux::syscall: num = (int) a7 (se_workload.cc:95-106, syscall_desc.hh:204) */
+    int num = (int)(s32)(u32)m->x[17];
+    int cls = or_sys_class(num);
+    if (cls == 0) { finish(m, OR_CRASH, OR_CRASH_SYSCALL_RANGE, 1); m->res.detail = (u32)num; return; }
+    if (cls == 1) { finish(m, OR_CRASH, OR_CRASH_SYSCALL_UNIMPL, 1); m->res.detail = (u32)num; return; }
+    if (cls == 3) { finish(m, OR_ESCAPE, OR_ESC_SYSCALL, 0); m->res.detail = (u32)num; return; }
+    if (cls == 2) { m->x[10] = 0; return; }
+    switch (num) {
+    case 93: case 94: {   /* exitImpl -> exitSimLoop(status & 0xff) (syscall_emul.cc:120-248) */
+        int status = (int)(s32)(u32)m->x[10];
+        int code = status & 0xff;
+        const or_campaign_t *c = m->c;
+        int same = c->have_golden && code == (int)c->golden.exit_code &&
+                   m->out.len == c->gout.len && m->err.len == c->gerr.len &&
+                   (m->out.len == 0 || !memcmp(m->out.buf, c->gout.buf, m->out.len)) &&
+                   (m->err.len == 0 || !memcmp(m->err.buf, c->gerr.buf, m->err.len));
+        finish(m, same ? OR_MASKED : OR_SDC, 0, code);
+        return;
+    }
+    case 172: m->x[10] = PID; return;     /* getpid -> tgid (syscall_emul.cc:822-826) */
+    case 173: m->x[10] = PPID; return;
+    case 174: case 175: m->x[10] = UID; return;
+    case 176: case 177: m->x[10] = GID; return;
+    case 178: m->x[10] = PID; return;     /* gettid -> pid */
+    case 64: {  /* writeFunc<RiscvLinux64>(int fd, VPtr buf, size_t n) syscall_emul.hh:2826-2860 */
+        int fd = (int)(s32)(u32)m->x[10];
+        u64 buf = m->x[11], n = m->x[12];
+        if (fd < 0 || fd >= 1024) { finish(m, OR_CRASH, OR_CRASH_FD_ASSERT, 134); return; }  /* fd_array.cc:322 */
+        if (fd == 0) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* host stdin poll/write */
+        if (fd > 2) { m->x[10] = (u64)(s64)-9; return; }                  /* -EBADF */
+        if (n > (1ULL << 31)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; } /* host allocation */
+        /* BufferArg::copyIn -> readBlob: fatal if any byte is unmapped (no fixup on reads) */
+        for (u64 a = buf & PAGE_MASK; n && a < buf + n; a += PAGE) {
+            if (a + PAGE < a) break;
+            if (!translate(m, a)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+            if (buf + n < buf) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        }
+        bytes_t *dst = fd == 1 ? &m->out : &m->err;
+        for (u64 i = 0; i < n; i++) {
+            uint8_t *pg = translate(m, buf + i);
+            uint8_t ch = pg[(buf + i) & (PAGE - 1)];
+            by_push(dst, &ch, 1);
+        }
+        m->x[10] = n;
+        return;
+    }
+    }
+}
+
+/* ------------------------------------------------------------ execute */
+static inline u64 rdreg(mach_t *m, int r) { return r <= 0 ? 0 : m->x[r]; }
+static inline void wrreg(mach_t *m, int r, u64 v) { if (r > 0) m->x[r] = v; }
+
+static inline u64 mulhu64(u64 a, u64 b) { return (u64)(((unsigned __int128)a * b) >> 64); }
+static inline s64 mulh64(s64 a, s64 b) { return (s64)(((__int128)a * b) >> 64); }
+static inline s64 mulhsu64(s64 a, u64 b) { return (s64)(((__int128)a * (__int128)b) >> 64); }
+static inline s64 div64(s64 a, s64 b) { if (b == 0) return -1; if (a == INT64_MIN && b == -1) return INT64_MIN; return a / b; }
+static inline u64 divu64(u64 a, u64 b) { return b == 0 ? UINT64_MAX : a / b; }
+static inline s64 rem64(s64 a, s64 b) { if (b == 0) return a; if (a == INT64_MIN && b == -1) return 0; return a % b; }
+static inline u64 remu64(u64 a, u64 b) { return b == 0 ? a : a % b; }
+static inline s32 div32(s32 a, s32 b) { if (b == 0) return -1; if (a == INT32_MIN && b == -1) return INT32_MIN; return a / b; }
+static inline u32 divu32(u32 a, u32 b) { return b == 0 ? UINT32_MAX : a / b; }
+static inline s32 rem32(s32 a, s32 b) { if (b == 0) return a; if (a == INT32_MIN && b == -1) return 0; return a % b; }
+static inline u32 remu32(u32 a, u32 b) { return b == 0 ? a : a % b; }
+static inline int clz64(u64 v) { return v ? __builtin_clzll(v) : 64; }
+static inline int ctz64(u64 v) { return v ? __builtin_ctzll(v) : 64; }
+static inline int clz32(u32 v) { return v ? __builtin_clz(v) : 32; }
+static inline int ctz32(u32 v) { return v ? __builtin_ctz(v) : 32; }
+static inline u64 sx32(u64 v) { return (u64)(s64)(s32)(u32)v; }
+
+/* U-mode CSR accessibility (formats/standard.isa:325-447, regs/misc.hh:604-1241):
+ * returns 1 if the access would reach the CSR data path (escape), 0 if it
+ * raises IllegalInstFault. */
+static int csr_u_accessible(u32 csr) {
+    if (bits(csr, 9, 8) != 0) return 0;     /* lowestAllowedMode > U */
+    if (csr >= 0x001 && csr <= 0x003) return 1;
+    if (csr >= 0x008 && csr <= 0x00A) return 1;
+    if (csr == 0x00F || csr == 0x017) return 1;
+    if (csr >= 0xC00 && csr <= 0xC1F) return 1;
+    if (csr >= 0xC20 && csr <= 0xC22) return 1;
+    return 0;                              /* absent from CSRData, or RV32-only *H */
+}
+
+/* Execute one decoded instruction (the generated StaticInst::execute bodies of
+ * decoder.isa).  Returns a fault kind; on F_NONE the caller commits npc. */
+static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
+    u64 pc = m->pc;
+    u64 a = rdreg(m, d->rs1), b = rdreg(m, d->rs2);
+    s64 imm = d->imm;
+    u64 v = 0, t;
+    int r;
+    /* detected-by-replica: a protected flipped register read before being
+     * overwritten (build-defined SHREWD semantics). */
+    if (m->watch > 0 && (d->rs1 == m->watch || d->rs2 == m->watch)) return 100;
+    if (m->watch > 0 && d->op == OP_ecall && (m->watch == 17 || (m->watch >= 10 && m->watch <= 15))) return 100;
+    switch (d->op) {
+    case OP_UNKNOWN: return F_UNKNOWN;
+    case OP_ESC_FP: case OP_ESC_VEC: case OP_ESC_AMO: case OP_ESC_SYS: case OP_ESC_CRYPTO: case OP_ESC_CBO:
+    case OP_ESC_CMP: case OP_ESC_M5: case OP_ESC_HYP:
+        return F_ESCAPE;
+    /* ---- compressed */
+    case OP_c_addi4spn: if (imm == 0) return F_ILLEGAL; v = a + imm; break;
+    case OP_c_lw: case OP_lw: case OP_c_lwsp:
+        if (d->op == OP_c_lwsp && d->rd == 0) return F_ILLEGAL;
+        r = mem_read(m, a + imm, 4, &t, fault_va); if (r) return r; v = sx32(t); break;
+    case OP_c_ld: case OP_ld: case OP_c_ldsp:
+        if (d->op == OP_c_ldsp && d->rd == 0) return F_ILLEGAL;
+        r = mem_read(m, a + imm, 8, &t, fault_va); if (r) return r; v = t; break;
+    case OP_c_lbu: case OP_lbu: r = mem_read(m, a + imm, 1, &t, fault_va); if (r) return r; v = t; break;
+    case OP_c_lhu: case OP_lhu: r = mem_read(m, a + imm, 2, &t, fault_va); if (r) return r; v = t; break;
+    case OP_c_lh: case OP_lh: r = mem_read(m, a + imm, 2, &t, fault_va); if (r) return r; v = (u64)sext(t, 16); break;
+    case OP_lb: r = mem_read(m, a + imm, 1, &t, fault_va); if (r) return r; v = (u64)sext(t, 8); break;
+    case OP_lwu: r = mem_read(m, a + imm, 4, &t, fault_va); if (r) return r; v = t; break;
+    case OP_c_sb: case OP_sb: r = mem_write(m, a + imm, 1, b, fault_va); if (r) return r; goto no_rd;
+    case OP_c_sh: case OP_sh: r = mem_write(m, a + imm, 2, b, fault_va); if (r) return r; goto no_rd;
+    case OP_c_sw: case OP_sw: case OP_c_swsp: r = mem_write(m, a + imm, 4, b, fault_va); if (r) return r; goto no_rd;
+    case OP_c_sd: case OP_sd: case OP_c_sdsp: r = mem_write(m, a + imm, 8, b, fault_va); if (r) return r; goto no_rd;
+    case OP_c_addi: case OP_addi: v = a + imm; break;
+    case OP_c_addiw: if (d->rd == 0) return F_ILLEGAL; v = sx32(a + imm); break;
+    case OP_addiw: v = sx32(a + imm); break;
+    case OP_c_li: v = imm; break;
+    case OP_c_addi16sp: if (imm == 0) return F_ILLEGAL; v = a + imm; break;
+    case OP_c_lui: if (imm == 0) return F_ILLEGAL; v = imm; break;
+    case OP_c_srli: case OP_srli: v = a >> imm; break;
+    case OP_c_srai: case OP_srai: v = (u64)((s64)a >> imm); break;
+    case OP_c_andi: case OP_andi: v = a & (u64)imm; break;
+    case OP_c_sub: case OP_sub: v = a - b; break;
+    case OP_c_xor: case OP_xor_: v = a ^ b; break;
+    case OP_c_or: case OP_or_: v = a | b; break;
+    case OP_c_and: case OP_and_: v = a & b; break;
+    case OP_c_subw: case OP_subw: v = sx32((u32)a - (u32)b); break;
+    case OP_c_addw: case OP_addw: v = sx32((u32)a + (u32)b); break;
+    case OP_c_mul: case OP_mul: v = a * b; break;
+    case OP_c_zext_b: v = a & 0xFF; break;
+    case OP_c_sext_b: case OP_sext_b: v = (u64)sext(a & 0xFF, 8); break;
+    case OP_c_zext_h: v = a & 0xFFFF; break;
+    case OP_c_sext_h: case OP_sext_h: v = (u64)sext(a & 0xFFFF, 16); break;
+    case OP_c_zext_w: v = a & 0xFFFFFFFFULL; break;
+    case OP_c_not: v = ~a; break;
+    case OP_c_j: m->npc = pc + imm; goto no_rd;
+    case OP_c_beqz: if (a == 0) m->npc = pc + imm; goto no_rd;
+    case OP_c_bnez: if (a != 0) m->npc = pc + imm; goto no_rd;
+    case OP_c_slli: case OP_slli: v = a << imm; break;
+    case OP_c_jr: if (d->rs1 == 0) return F_ILLEGAL; m->npc = a & ~1ULL; goto no_rd;
+    case OP_c_mv: v = b; break;
+    case OP_c_ebreak: case OP_ebreak: return F_BREAK;
+    case OP_c_jalr: v = m->npc; m->npc = a & ~1ULL; break;
+    case OP_c_add: case OP_add: v = a + b; break;
+    /* ---- 32-bit */
+    case OP_fence: case OP_fence_i: goto no_rd;
+    case OP_bseti: v = a | (1ULL << (imm & 63)); break;
+    case OP_bclri: v = a & ~(1ULL << (imm & 63)); break;
+    case OP_binvi: v = a ^ (1ULL << (imm & 63)); break;
+    case OP_clz: v = clz64(a); break;
+    case OP_ctz: v = ctz64(a); break;
+    case OP_cpop: v = __builtin_popcountll(a); break;
+    case OP_slti: v = (s64)a < imm ? 1 : 0; break;
+    case OP_sltiu: v = a < (u64)imm ? 1 : 0; break;
+    case OP_xori: v = a ^ (u64)imm; break;
+    case OP_orc_b: v = 0; for (int i = 0; i < 8; i++) if ((a >> (8 * i)) & 0xFF) v |= 0xFFULL << (8 * i); break;
+    case OP_bexti: v = (a >> (imm & 63)) & 1; break;
+    case OP_rori: v = (a >> imm) | (a << ((64 - imm) & 63)); break;
+    case OP_rev8: v = __builtin_bswap64(a); break;
+    case OP_prefetch_i: case OP_prefetch_r: case OP_prefetch_w: goto no_rd;   /* faults suppressed (atomic.cc:604) */
+    case OP_ori_hint: case OP_ori: v = a | (u64)imm; break;
+    case OP_auipc: v = pc + imm; break;
+    case OP_slliw: v = sx32((u32)a << imm); break;
+    case OP_slli_uw: v = (a & 0xFFFFFFFFULL) << imm; break;
+    case OP_clzw: v = clz32((u32)a); break;
+    case OP_ctzw: v = ctz32((u32)a); break;
+    case OP_cpopw: v = __builtin_popcount((u32)a); break;
+    case OP_srliw: v = sx32((u32)a >> imm); break;
+    case OP_sraiw: v = (u64)(s64)((s32)(u32)a >> imm); break;
+    case OP_roriw: { u32 x = (u32)a; v = sx32((x >> imm) | (x << ((32 - imm) & 31))); break; }
+    case OP_sll: v = a << (b & 63); break;
+    case OP_mulh: v = (u64)mulh64((s64)a, (s64)b); break;
+    case OP_clmul: v = 0; for (int i = 0; i < 64; i++) if ((b >> i) & 1) v ^= a << i; break;
+    case OP_bset: v = a | (1ULL << (b & 63)); break;
+    case OP_bclr: v = a & ~(1ULL << (b & 63)); break;
+    case OP_rol: { int s = (int)(b & 63); v = (a << s) | (a >> ((64 - s) & 63)); break; }
+    case OP_binv: v = a ^ (1ULL << (b & 63)); break;
+    case OP_slt: v = (s64)a < (s64)b ? 1 : 0; break;
+    case OP_mulhsu: v = (u64)mulhsu64((s64)a, b); break;
+    case OP_clmulr: v = 0; for (int i = 0; i < 64; i++) if ((b >> i) & 1) v ^= a >> (64 - i - 1); break;
+    case OP_sh1add: v = (a << 1) + b; break;
+    case OP_sltu: v = a < b ? 1 : 0; break;
+    case OP_mulhu: v = mulhu64(a, b); break;
+    case OP_clmulh: v = 0; for (int i = 1; i < 64; i++) if ((b >> i) & 1) v ^= a >> (64 - i); break;
+    case OP_div_: v = (u64)div64((s64)a, (s64)b); break;
+    case OP_pack: v = (b << 32) | (a & 0xFFFFFFFFULL); break;
+    case OP_min_: v = (s64)a < (s64)b ? a : b; break;
+    case OP_sh2add: v = (a << 2) + b; break;
+    case OP_xnor: v = ~(a ^ b); break;
+    case OP_srl: v = a >> (b & 63); break;
+    case OP_divu: v = divu64(a, b); break;
+    case OP_czero_eqz: v = b == 0 ? 0 : a; break;
+    case OP_sra: v = (u64)((s64)a >> (b & 63)); break;
+    case OP_minu: v = a < b ? a : b; break;
+    case OP_bext: v = (a >> (b & 63)) & 1; break;
+    case OP_ror: { int s = (int)(b & 63); v = (a >> s) | (a << ((64 - s) & 63)); break; }
+    case OP_rem: v = (u64)rem64((s64)a, (s64)b); break;
+    case OP_max_: v = (s64)a > (s64)b ? a : b; break;
+    case OP_sh3add: v = (a << 3) + b; break;
+    case OP_orn: v = a | ~b; break;
+    case OP_remu: v = remu64(a, b); break;
+    case OP_packh: v = ((b & 0xFF) << 8) | (a & 0xFF); break;
+    case OP_maxu: v = a > b ? a : b; break;
+    case OP_czero_nez: v = b != 0 ? 0 : a; break;
+    case OP_andn: v = a & ~b; break;
+    case OP_lui: v = imm; break;
+    case OP_mulw: v = sx32((u32)a * (u32)b); break;
+    case OP_add_uw: v = (a & 0xFFFFFFFFULL) + b; break;
+    case OP_sllw: v = sx32((u32)a << (b & 31)); break;
+    case OP_rolw: { u32 x = (u32)a; int s = (int)(b & 31); v = sx32((x << s) | (x >> ((32 - s) & 31))); break; }
+    case OP_sh1add_uw: v = ((a & 0xFFFFFFFFULL) << 1) + b; break;
+    case OP_divw: v = (u64)(s64)div32((s32)a, (s32)b); break;
+    case OP_packw: v = sx32(((b & 0xFFFF) << 16) | (a & 0xFFFF)); break;
+    case OP_sh2add_uw: v = ((a & 0xFFFFFFFFULL) << 2) + b; break;
+    case OP_srlw: v = sx32((u32)a >> (b & 31)); break;
+    case OP_divuw: v = sx32(divu32((u32)a, (u32)b)); break;
+    case OP_sraw: v = (u64)(s64)((s32)(u32)a >> (b & 31)); break;
+    case OP_rorw: { u32 x = (u32)a; int s = (int)(b & 31); v = sx32((x >> s) | (x << ((32 - s) & 31))); break; }
+    case OP_remw: v = (u64)(s64)rem32((s32)a, (s32)b); break;
+    case OP_sh3add_uw: v = ((a & 0xFFFFFFFFULL) << 3) + b; break;
+    case OP_remuw: v = sx32(remu32((u32)a, (u32)b)); break;
+    case OP_beq: if (a == b) m->npc = pc + imm; goto no_rd;
+    case OP_bne: if (a != b) m->npc = pc + imm; goto no_rd;
+    case OP_blt: if ((s64)a < (s64)b) m->npc = pc + imm; goto no_rd;
+    case OP_bge: if ((s64)a >= (s64)b) m->npc = pc + imm; goto no_rd;
+    case OP_bltu: if (a < b) m->npc = pc + imm; goto no_rd;
+    case OP_bgeu: if (a >= b) m->npc = pc + imm; goto no_rd;
+    case OP_jalr: v = m->npc; m->npc = (a + imm) & ~1ULL; break;
+    case OP_jal: v = m->npc; m->npc = pc + imm; break;
+    case OP_ecall: return F_SYSCALL;
+    case OP_csr: return csr_u_accessible(d->csr) ? F_ESCAPE + 100 : F_ILLEGAL;
+    default: return F_UNKNOWN;
+    }
+    wrreg(m, d->rd, v);
+    if (m->watch > 0 && d->rd == m->watch) m->watch = -1;   /* overwritten before read */
+    return F_NONE;
+no_rd:
+    return F_NONE;
+}
+
+/* --------------------------------------------------------- inject / tick */
+static void inject(mach_t *m) {
+    const or_site_t *s = m->site;
+    m->injected = 1;
+    if (s->target >= 1 && s->target <= 31) {
+        m->x[s->target] ^= s->mask;
+        if ((m->protect_mask >> s->target) & 1) m->watch = (int)s->target;
+    } else if (s->target == OR_T_PC) {
+        m->pc ^= s->mask;
+        if ((m->protect_mask >> 32) & 1) { finish(m, OR_DETECTED, 0, 0); }
+    } else if (s->target == OR_T_MEM) {
+        /* flip the 8-byte word if its page is mapped at inject time */
+        uint8_t *pg = translate_w(m, s->addr);
+        if (pg) {
+            u64 off = s->addr & (PAGE - 1);
+            for (int i = 0; i < 8; i++) pg[off + i] ^= (uint8_t)(s->mask >> (8 * i));
+        } else {
+            m->injected = 2;
+        }
+    }
+}
+
+/* RiscvFault::invoke / invokeSE dispositions, arch/riscv/faults.cc:286-333 and
+ * sim/faults.cc:95-105. */
+static void invoke_fault(mach_t *m, int f, u64 fault_va, const dec_t *d) {
+    switch (f) {
+    case F_SYSCALL:
+        /* SyscallFault::invokeSE advances the PC first (faults.cc:325-333) */
+        m->pc = m->pc + d->len;
+        do_syscall(m);
+        return;
+    case F_BREAK: finish(m, OR_CRASH, OR_CRASH_SIGTRAP, 133); return;
+    case F_ILLEGAL: finish(m, OR_CRASH, OR_CRASH_ILLEGAL_INST, 134); return;
+    case F_UNKNOWN: finish(m, OR_CRASH, OR_CRASH_UNKNOWN_INST, 134); return;
+    case F_ESCAPE: finish(m, OR_ESCAPE, OR_ESC_INST, 0); m->res.detail = d->raw; return;
+    case F_ESCAPE + 100: finish(m, OR_ESCAPE, OR_ESC_CSR, 0); m->res.detail = d->raw; return;
+    case 100: finish(m, OR_DETECTED, 0, 0); return;
+    case F_PGFAULT: {
+        int h = fixup_fault(m, fault_va);
+        if (h == 1) return;   /* retried next tick */
+        if (h == -1) { finish(m, OR_CRASH, OR_CRASH_STACK_LIMIT, 1); return; }
+        finish(m, OR_CRASH, OR_CRASH_PAGE_FAULT, 134);
+        m->res.detail = (u32)fault_va;
+        return;
+    }
+    }
+}
+
+/* One AtomicSimpleCPU::tick() with width=1 (cpu/simple/atomic.cc:611-739). */
+static void tick(mach_t *m, u64 cap) {
+    m->num_cycles++;
+    /* serviceInstCountEvents (base.cc:321-325): fault injection and the
+     * max-insts exit both fire at the top of the first tick with numInst >= n */
+    if (m->site && !m->injected && m->num_inst >= m->site->inst) {
+        inject(m);
+        if (m->done) return;
+    }
+    if (m->num_inst >= cap) { finish(m, OR_HANG, OR_HANG_INSTS, 0); return; }
+    /* setupFetchRequest: 4 bytes at (pc & ~3) + fetchOffset (base.cc:304-318) */
+    u64 fetch_pc = (m->pc & ~3ULL) + m->fetch_offset;
+    uint8_t *pg = translate(m, fetch_pc);
+    int f = F_NONE; u64 fva = 0;
+    dec_t d; memset(&d, 0, sizeof d);
+    int have_inst = 0;
+    if (!pg) {
+        f = F_PGFAULT; fva = fetch_pc;
+    } else {
+        const uint8_t *w = pg + (fetch_pc & (PAGE - 1));
+        u32 word = (u32)w[0] | ((u32)w[1] << 8) | ((u32)w[2] << 16) | ((u32)w[3] << 24);
+        m->fetch_bytes += 4;
+        /* Decoder::moreBytes (decoder.cc:63-116) */
+        int aligned = (m->pc % 4) == 0;
+        if (aligned) {
+            m->emi = word;
+            if ((word & 3) != 3) m->emi = word & 0xFFFF;
+            m->inst_done = 1;
+        } else if (m->mid) {
+            m->emi = (m->emi & 0xFFFF) | ((word & 0xFFFF) << 16);
+            m->mid = 0; m->inst_done = 1;
+        } else {
+            m->emi = word >> 16;
+            m->mid = (m->emi & 3) == 3;
+            m->inst_done = !m->mid;
+        }
+        /* preExecute / Decoder::decode (base.cc:328-409, decoder.cc:135-173) */
+        if (m->inst_done) {
+            m->inst_done = 0;
+            decode(m->emi, &d);
+            m->npc = m->pc + d.len;
+            m->stay_at_pc = 0;
+            have_inst = 1;
+        } else {
+            m->stay_at_pc = 1;
+            m->fetch_offset += 4;
+        }
+        if (have_inst) {
+            f = execute(m, &d, &fva);
+            if (f == F_NONE) m->num_inst++;   /* countInst only on NoFault (atomic.cc:687-689) */
+        }
+    }
+    /* advancePC (base.cc:493-512) */
+    if (f != F_NONE || !m->stay_at_pc) {
+        m->fetch_offset = 0;
+        if (f != F_NONE) {
+            m->mid = 0; m->inst_done = 0; m->emi = 0;   /* decoder->reset() */
+            invoke_fault(m, f, fva, &d);
+        } else {
+            m->pc = m->npc;
+        }
+    }
+}
+
+/* --------------------------------------------------------- ELF + image */
+static int rd16(const uint8_t *p) { return p[0] | (p[1] << 8); }
+static u32 rd32(const uint8_t *p) { return (u32)p[0] | ((u32)p[1] << 8) | ((u32)p[2] << 16) | ((u32)p[3] << 24); }
+static u64 rd64(const uint8_t *p) { return (u64)rd32(p) | ((u64)rd32(p + 4) << 32); }
+
+static void image_write(or_campaign_t *c, u64 addr, const uint8_t *src, u64 n) {
+    /* Process::initState -> image.write through an allocating proxy (process.cc:289-306) */
+    for (u64 i = 0; i < n; i++) {
+        u64 a = addr + i;
+        pte_t *p = pm_find(&c->image, a >> 12);
+        if (!p) p = pm_insert(&c->image, a >> 12, (uint8_t *)calloc(1, PAGE), 1);
+        p->data[a & (PAGE - 1)] = src ? src[i] : 0;
+    }
+}
+
+/* gem5 Random: std::mt19937_64 seeded with the global seed 5489
+ * (base/random.hh:211-217, random.cc:79); random(0,0xFF) = gen() % 256. */
+typedef struct { u64 mt[312]; int idx; } mt64_t;
+static void mt_seed(mt64_t *s, u64 seed) {
+    s->mt[0] = seed;
+    for (int i = 1; i < 312; i++) s->mt[i] = 6364136223846793005ULL * (s->mt[i - 1] ^ (s->mt[i - 1] >> 62)) + (u64)i;
+    s->idx = 312;
+}
+static u64 mt_next(mt64_t *s) {
+    if (s->idx >= 312) {
+        for (int i = 0; i < 312; i++) {
+            u64 x = (s->mt[i] & 0xFFFFFFFF80000000ULL) | (s->mt[(i + 1) % 312] & 0x7FFFFFFFULL);
+            u64 xa = x >> 1;
+            if (x & 1) xa ^= 0xB5026F5AA96619E9ULL;
+            s->mt[i] = s->mt[(i + 156) % 312] ^ xa;
+        }
+        s->idx = 0;
+    }
+    u64 y = s->mt[s->idx++];
+    y ^= (y >> 29) & 0x5555555555555555ULL;
+    y ^= (y << 17) & 0x71D67FFFEDA60000ULL;
+    y ^= (y << 37) & 0xFFF7EEE000000000ULL;
+    y ^= y >> 43;
+    return y;
+}
+
+static void push64(or_campaign_t *c, u64 *sp, u64 v) {
+    uint8_t b[8];
+    for (int i = 0; i < 8; i++) b[i] = (uint8_t)(v >> (8 * i));
+    image_write(c, *sp, b, 8);
+    *sp += 8;
+}
+
+or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
+    or_campaign_t *c = (or_campaign_t *)calloc(1, sizeof(*c));
+    pm_init(&c->image, 64);
+    if (len < 64 || memcmp(elf, "\x7f" "ELF", 4) || elf[4] != 2 || elf[5] != 1 || rd16(elf + 18) != 243) {
+        snprintf(c->err, sizeof c->err, "not an ELF64 LE RISC-V file"); return c;
+    }
+    c->entry = rd64(elf + 24);
+    u64 phoff = rd64(elf + 32);
+    int phentsize = rd16(elf + 54), phnum = rd16(elf + 56);
+    u64 max_addr = 0, phdr_vaddr = 0;
+    u64 wpages[4096]; u64 nw = 0;
+    for (int i = 0; i < phnum; i++) {
+        const uint8_t *ph = elf + phoff + (u64)i * phentsize;
+        if (rd32(ph) != 1) continue;                   /* PT_LOAD */
+        u32 flags = rd32(ph + 4);
+        u64 off = rd64(ph + 8), vaddr = rd64(ph + 16), paddr = rd64(ph + 24);
+        u64 filesz = rd64(ph + 32), memsz = rd64(ph + 40);
+        if (memsz == 0) continue;                      /* elf_object.cc:378-381 */
+        /* segments are loaded at p_paddr, bss zero-filled (elf_object.cc:383-392) */
+        image_write(c, paddr, elf + off, filesz);
+        if (memsz > filesz) image_write(c, paddr + filesz, NULL, memsz - filesz);
+        if (paddr + memsz > max_addr) max_addr = paddr + memsz;
+        if (off <= phoff && off + filesz > phoff) phdr_vaddr = vaddr + (phoff - off);   /* :396-402 */
+        if (flags & 2)
+            for (u64 pg = paddr & PAGE_MASK; pg < paddr + memsz && nw < 4096; pg += PAGE) wpages[nw++] = pg;
+    }
+    /* RiscvProcess64 ctor: brk = roundUp(image.maxAddr(), 4096) (process.cc:76) */
+    c->brk0 = (max_addr + PAGE - 1) & PAGE_MASK;
+
+    /* RiscvProcess::argsInit<uint64_t> (process.cc:134-261), argv = {argv0}, envp = {} */
+    const size_t alen = strlen(argv0);
+    u64 stack_min = STACK_BASE;
+    u64 stack_top = stack_min - 16 - (alen + 1);
+    stack_top &= ~7ULL;
+    const int nauxv = 8;
+    stack_top -= (1 + 1) * 8 + (1 + 0) * 8 + 8 + 2 * 8 * nauxv;
+    stack_top &= ~15ULL;
+    u64 stack_size = STACK_BASE - stack_top;
+    c->stack_vma_lo = stack_top & PAGE_MASK;
+    c->stack_vma_hi = c->stack_vma_lo + ((stack_size + PAGE - 1) & PAGE_MASK);
+    /* AT_RANDOM */
+    stack_min -= 16;
+    mt64_t mt; mt_seed(&mt, 5489);
+    uint8_t rnd[16];
+    for (int i = 0; i < 16; i++) rnd[i] = (uint8_t)(mt_next(&mt) % 256);
+    image_write(c, stack_min, rnd, 16);
+    /* argv string */
+    stack_min -= alen + 1;
+    image_write(c, stack_min, (const uint8_t *)argv0, alen + 1);
+    u64 argp = stack_min;
+    stack_min &= ~7ULL;
+    stack_min -= (1 + 1) * 8 + (1 + 0) * 8 + 8 + 2 * 8 * nauxv;
+    stack_min &= ~15ULL;
+    u64 sp = stack_min;
+    push64(c, &sp, 1);            /* argc */
+    push64(c, &sp, argp); push64(c, &sp, 0);
+    push64(c, &sp, 0);            /* envp terminator */
+    const u64 aux[8][2] = {{9, c->entry}, {5, (u64)phnum}, {4, (u64)phentsize}, {3, phdr_vaddr},
+                           {6, PAGE}, {23, 0}, {25, stack_top}, {0, 0}};
+    for (int i = 0; i < nauxv; i++) { push64(c, &sp, aux[i][0]); push64(c, &sp, aux[i][1]); }
+    c->sp0 = stack_min;
+    c->stack_min0 = stack_min & PAGE_MASK;
+    /* writable pages at start: ELF writable segments + initial stack pages */
+    for (u64 pg = c->stack_min0; pg != 0 && pg <= (STACK_BASE & PAGE_MASK); pg += PAGE) {
+        if (nw < 4096) wpages[nw++] = pg;
+        if (pg == (STACK_BASE & PAGE_MASK)) break;
+    }
+    c->n_mem_pages = nw;
+    c->mem_pages = (u64 *)malloc(sizeof(u64) * (nw ? nw : 1));
+    memcpy(c->mem_pages, wpages, sizeof(u64) * nw);
+    return c;
+}
+
+void or_destroy(or_campaign_t *c) {
+    if (!c) return;
+    pm_free(&c->image);
+    free(c->mem_pages); free(c->gout.buf); free(c->gerr.buf);
+    free(c);
+}
+
+static void mach_init(mach_t *m, const or_campaign_t *c) {
+    memset(m, 0, sizeof(*m));
+    m->c = c;
+    pm_init(&m->mem, 64);
+    for (u64 i = 0; i < c->image.cap; i++)
+        if (c->image.tab[i].vpn != UINT64_MAX) pm_insert(&m->mem, c->image.tab[i].vpn, c->image.tab[i].data, 0);
+    m->x[2] = c->sp0;
+    m->pc = c->entry;
+    m->stack_min = c->stack_min0;
+    m->watch = -1;
+}
+static void mach_free(mach_t *m) { pm_free(&m->mem); free(m->out.buf); free(m->err.buf); }
+
+static void run(mach_t *m, u64 cap) {
+    while (!m->done) tick(m, cap);
+}
+
+int or_golden(or_campaign_t *c, u64 max_inst, or_golden_t *out) {
+    if (c->err[0]) return -1;
+    mach_t m; mach_init(&m, c);
+    run(&m, max_inst);
+    if (m.res.cls != OR_MASKED && m.res.cls != OR_SDC) {
+        snprintf(c->err, sizeof c->err, "golden run did not exit (cls %d sub %d pc %#lx)", m.res.cls, m.res.sub,
+                 (unsigned long)m.pc);
+        mach_free(&m); return -1;
+    }
+    c->golden.ninst = m.num_inst; c->golden.ncycles = m.num_cycles;
+    c->golden.exit_code = m.res.exit_code; c->golden.cls = 0;
+    c->golden.stdout_len = m.out.len; c->golden.stderr_len = m.err.len;
+    c->golden.fetch_bytes = m.fetch_bytes; c->golden.data_bytes = m.data_bytes;
+    free(c->gout.buf); free(c->gerr.buf);
+    c->gout = m.out; c->gerr = m.err; m.out.buf = m.err.buf = NULL;
+    c->have_golden = 1;
+    mach_free(&m);
+    if (out) *out = c->golden;
+    return 0;
+}
+
+uint64_t or_golden_stdout(or_campaign_t *c, uint8_t *buf, uint64_t cap) {
+    u64 n = c->gout.len < cap ? c->gout.len : cap;
+    if (n) memcpy(buf, c->gout.buf, n);
+    return c->gout.len;
+}
+
+/* ------------------------------------------------------------- sampler */
+/* SplitMix64 (Steele et al. 2014); site = f(seed, trial) only, so it is
+ * shard-invariant.  Same definition as shrewd_amd/csrc/hip/sampler. */
+static u64 splitmix(u64 *s) {
+    u64 z = (*s += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+static u64 mulhi(u64 a, u64 b) { return (u64)(((unsigned __int128)a * b) >> 64); }
+
+int or_sample(or_campaign_t *c, u64 seed, u64 first, u64 n, u64 structures, u32 burst, or_site_t *sites) {
+    if (!c->have_golden) { snprintf(c->err, sizeof c->err, "golden run required before sampling"); return -1; }
+    if (burst < 1 || burst > 64) burst = 1;
+    structures &= ~1ULL;                        /* x0 is not a fault site */
+    if (c->n_mem_pages == 0) structures &= ~(1ULL << OR_T_MEM);
+    int nt = __builtin_popcountll(structures);
+    if (nt == 0) { snprintf(c->err, sizeof c->err, "no fault structures"); return -1; }
+    for (u64 i = 0; i < n; i++) {
+        u64 id = first + i;
+        u64 st = seed ^ (id * 0xD6E8FEB86659FD93ULL);
+        u64 r0 = splitmix(&st), r1 = splitmix(&st), r2 = splitmix(&st), r3 = splitmix(&st);
+        or_site_t *s = &sites[i];
+        s->inst = mulhi(r0, c->golden.ninst);
+        u64 k = mulhi(r1, (u64)nt);
+        u64 m = structures;
+        for (u64 j = 0; j < k; j++) m &= m - 1;
+        s->target = (u32)__builtin_ctzll(m);
+        u64 b = mulhi(r2, 65 - burst);
+        s->mask = (burst == 64 ? ~0ULL : ((1ULL << burst) - 1)) << b;
+        s->addr = 0;
+        if (s->target == OR_T_MEM) {
+            u64 w = mulhi(r3, c->n_mem_pages * 512);
+            s->addr = c->mem_pages[w / 512] + (w % 512) * 8;
+        }
+        s->trial = (u32)id;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------- trials */
+static u64 hang_cap(const or_campaign_t *c, u64 f16) {
+    if (f16 == 0) f16 = 32;   /* default cap: 2x golden instructions */
+    return (c->golden.ninst * f16) / 16 + 1000;
+}
+
+static void run_trial(const or_campaign_t *c, const or_site_t *s, u64 protect, u64 cap, or_outcome_t *o,
+                      bytes_t *cap_out) {
+    mach_t m; mach_init(&m, c);
+    m.site = s; m.protect_mask = protect;
+    run(&m, cap);
+    *o = m.res;
+    if (cap_out) { *cap_out = m.out; m.out.buf = NULL; }
+    mach_free(&m);
+}
+
+typedef struct {
+    const or_campaign_t *c; const or_site_t *sites; u64 n; u64 protect; u64 cap;
+    or_outcome_t *out; int tid, nth;
+} job_t;
+
+static void *worker(void *arg) {
+    job_t *j = (job_t *)arg;
+    for (u64 i = (u64)j->tid; i < j->n; i += (u64)j->nth)
+        run_trial(j->c, &j->sites[i], j->protect, j->cap, &j->out[i], NULL);
+    return NULL;
+}
+
+int or_run_trials(or_campaign_t *c, const or_site_t *sites, u64 n, u64 protect, u64 f16, or_outcome_t *out,
+                  int nth) {
+    if (!c->have_golden) { snprintf(c->err, sizeof c->err, "golden run required"); return -1; }
+    u64 cap = hang_cap(c, f16);
+    if (nth <= 1) {
+        for (u64 i = 0; i < n; i++) run_trial(c, &sites[i], protect, cap, &out[i], NULL);
+        return 0;
+    }
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nth);
+    job_t *jobs = (job_t *)malloc(sizeof(job_t) * nth);
+    for (int t = 0; t < nth; t++) {
+        jobs[t] = (job_t){c, sites, n, protect, cap, out, t, nth};
+        pthread_create(&th[t], NULL, worker, &jobs[t]);
+    }
+    for (int t = 0; t < nth; t++) pthread_join(th[t], NULL);
+    free(th); free(jobs);
+    return 0;
+}
+
+int or_run_one_capture(or_campaign_t *c, const or_site_t *site, u64 protect, u64 f16, or_outcome_t *out,
+                       uint8_t *buf, u64 capn, u64 *len) {
+    if (!c->have_golden && site) { snprintf(c->err, sizeof c->err, "golden run required"); return -1; }
+    bytes_t b = {0};
+    u64 cap = c->have_golden ? hang_cap(c, f16) : (u64)1 << 40;
+    run_trial(c, site, protect, cap, out, &b);
+    u64 n = b.len < capn ? b.len : capn;
+    if (n) memcpy(buf, b.buf, n);
+    *len = b.len;
+    free(b.buf);
+    return 0;
+}
+
+/* ------------------------------------------------------------- probe */
+int or_probe(u32 inst, u64 pc, const u64 regs[32], or_probe_t *o) {
+    static or_campaign_t dummy;   /* stack VMA empty: no fixups */
+    mach_t m; memset(&m, 0, sizeof m);
+    m.c = &dummy;
+    pm_init(&m.mem, 64);
+    for (int i = 0; i < 32; i++) m.x[i] = regs[i];
+    m.x[0] = 0;
+    m.pc = pc; m.watch = -1; m.stack_min = STACK_BASE;
+    dec_t d; decode(inst, &d);
+    m.npc = pc + d.len;
+    /* memory: every page the access touches is mapped zero (probe semantics) */
+    if (d.rs1 >= 0) {
+        u64 ea = rdreg(&m, d.rs1) + d.imm;
+        alloc_page(&m, ea & PAGE_MASK);
+        alloc_page(&m, (ea + 7) & PAGE_MASK);
+    }
+    u64 fva = 0;
+    int f = execute(&m, &d, &fva);
+    o->fault = f == F_NONE ? 0 : f == F_SYSCALL ? 1 : f == F_BREAK ? 2 : f == F_ILLEGAL ? 3 :
+               f == F_UNKNOWN ? 4 : f == F_PGFAULT ? 6 : 5;
+    o->rd = d.rd;
+    o->rd_value = d.rd > 0 ? m.x[d.rd] : 0;
+    o->npc = m.npc;
+    o->len = d.len;
+    o->op = (u32)d.op;
+    pm_free(&m.mem);
+    return 0;
+}

@@ -1,0 +1,124 @@
+/*
+ * rv64se.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement ("oracle") of gem5 v25 RISC-V AtomicSimpleCPU SE-mode
+ * semantics for the fault-injection campaign path, used as the parity checker
+ * for the MI355X engine in shrewd_amd/.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it.  The product never links it.
+ *
+ * Each function in rv64se.c cites the reference file:line it restates
+ * (paths relative to the gem5/SHREWD tree).  Parity status: instruction
+ * decode + integer semantics are pinned by vectors generated from gem5's own
+ * ISA parser (tools/oracle/gen_isa_vectors.py -> tests/golden/); process
+ * image, syscalls and crash taxonomy are restated from the cited code and
+ * are "parity unpinned" against a live gem5.opt (unbuildable here: no SCons).
+ */
+#ifndef SHREWD_ORACLE_RV64SE_H
+#define SHREWD_ORACLE_RV64SE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Outcome classes and sub-codes.  Must stay identical to include/fi_engine.h. */
+enum {
+    OR_MASKED = 0, OR_SDC = 1, OR_CRASH = 2, OR_HANG = 3, OR_DETECTED = 4, OR_ESCAPE = 5
+};
+enum {
+    OR_CRASH_UNKNOWN_INST = 1,  /* panic: UnknownInstFault        faults.cc:286-291 */
+    OR_CRASH_ILLEGAL_INST = 2,  /* panic: IllegalInstFault        faults.cc:294-301 */
+    OR_CRASH_PAGE_FAULT   = 3,  /* panic: GenericPageTableFault   sim/faults.cc:95-105 */
+    OR_CRASH_SYSCALL_RANGE = 4, /* fatal: syscall out of range    syscall_desc.hh:204-214 */
+    OR_CRASH_SYSCALL_UNIMPL = 5,/* fatal: unimplementedFunc       syscall_emul.cc:77-80 */
+    OR_CRASH_PROXY = 6,         /* fatal: readBlob failed         port_proxy.hh:182-196 */
+    OR_CRASH_FD_ASSERT = 7,     /* abort: FDArray assert          fd_array.cc:320-323 */
+    OR_CRASH_SIGTRAP = 8,       /* ebreak -> kill(SIGTRAP)        faults.cc:317-322, debug.cc:64-70 */
+    OR_CRASH_STACK_LIMIT = 9    /* fatal: Maximum stack size      mem_state.cc:440 */
+};
+enum {
+    OR_ESC_INST = 1,            /* instruction gem5 decodes but the engine does not model */
+    OR_ESC_SYSCALL = 2,         /* syscall gem5 implements but the engine does not model */
+    OR_ESC_CSR = 3,             /* U-mode-accessible CSR */
+    OR_ESC_HOST = 4,            /* behaviour that depends on the host (fd 0, huge buffers) */
+    OR_ESC_RESOURCE = 5         /* engine resource limit (private pages) -- device only */
+};
+enum { OR_HANG_INSTS = 1 };
+
+/* structure ids for fault sites */
+enum { OR_T_PC = 32, OR_T_MEM = 33 };
+
+typedef struct {
+    uint8_t cls, sub, exit_code, flags;
+    uint32_t detail;
+    uint64_t ninst;
+} or_outcome_t;                              /* 16 bytes == fi_outcome */
+
+typedef struct {
+    uint64_t inst;      /* numInst at whose tick-top the flip is applied */
+    uint64_t mask;      /* xor mask */
+    uint64_t addr;      /* memory fault: 8-byte aligned guest address */
+    uint32_t target;    /* 1..31 = x reg, 32 = pc, 33 = memory word */
+    uint32_t trial;     /* trial id (informational) */
+} or_site_t;                                 /* 32 bytes == fi_site */
+
+typedef struct {
+    uint64_t ninst, ncycles;
+    uint32_t exit_code, cls;
+    uint64_t stdout_len, stderr_len;
+    uint64_t fetch_bytes, data_bytes;   /* algorithmic byte counters of the golden run */
+} or_golden_t;
+
+typedef struct or_campaign or_campaign_t;
+
+/* Build the initial process image exactly as gem5 SE would for
+ * cmd=[argv0] (RiscvProcess64::argsInit, arch/riscv/process.cc:134-261). */
+or_campaign_t *or_create(const uint8_t *elf, size_t elf_len, const char *argv0);
+void or_destroy(or_campaign_t *c);
+const char *or_error(or_campaign_t *c);
+
+/* Fault-free run; records golden stdout/stderr/exit code/instruction count. */
+int or_golden(or_campaign_t *c, uint64_t max_inst, or_golden_t *out);
+/* copies golden stdout into buf (up to cap bytes); returns length */
+uint64_t or_golden_stdout(or_campaign_t *c, uint8_t *buf, uint64_t cap);
+
+/* Counter-based site sampler: SplitMix64 keyed by (seed, trial).  structures
+ * is a bitmask over {bit r = x_r (1..31), bit 32 = pc, bit 33 = memory}. */
+int or_sample(or_campaign_t *c, uint64_t seed, uint64_t first_trial, uint64_t n,
+              uint64_t structures, uint32_t burst, or_site_t *sites);
+
+/* Run trials from scratch (no golden snapshots, no early exit): the plain
+ * serial semantics the GPU engine must reproduce bit for bit. */
+int or_run_trials(or_campaign_t *c, const or_site_t *sites, uint64_t n,
+                  uint64_t protect_mask, uint64_t hang_factor_x16,
+                  or_outcome_t *out, int n_threads);
+
+/* Diagnostics: run one trial and return its full stdout in buf. */
+int or_run_one_capture(or_campaign_t *c, const or_site_t *site, uint64_t protect_mask,
+                       uint64_t hang_factor_x16, or_outcome_t *out,
+                       uint8_t *stdout_buf, uint64_t cap, uint64_t *stdout_len);
+
+/* Single-instruction semantic probe used by the ISA-vector tests: executes
+ * inst at pc with the given x[rs1]/x[rs2] values in a scratch machine whose
+ * memory is one zero page at 0x1000 (loads/stores clamp there) and reports
+ * the value written to rd, the next pc and the fault kind. */
+typedef struct {
+    uint64_t rd_value, npc;
+    int32_t fault;      /* 0 none, 1 syscall, 2 breakpoint, 3 illegal, 4 unknown, 5 escape, 6 pagefault */
+    int32_t rd;         /* destination register written, -1 none */
+    uint32_t len;
+    uint32_t op;        /* oracle-internal op id */
+} or_probe_t;
+int or_probe(uint32_t inst, uint64_t pc, const uint64_t regs[32], or_probe_t *out);
+/* decode-only probe: returns a stable mnemonic string for inst ("unknown" for
+ * gem5 Unknown, "escape:<name>" for modelled-as-escape encodings) */
+const char *or_mnemonic(uint32_t inst);
+/* syscall classification (0 absent,1 unimpl,2 ignore,3 escape,4 modelled) */
+int or_sys_class(int num);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
