@@ -1,0 +1,166 @@
+/*
+ * fi_engine.h -- C ABI of the MI355X fault-injection campaign engine.
+ *
+ * This is the drop-in boundary for SHREWD/gem5's fault-injection campaign
+ * path.  A gem5 `FaultCampaign` SimObject
+ * (src/gem5ext/fault_campaign.cc) or a plain ctypes caller
+ * (configs/fi_campaign.py, shrewd_amd/fi.py) drives it.  What each entry point
+ * replaces in the reference:
+ *
+ *   fi_load_elf    Process ctor + Process::initState + RiscvProcess64::argsInit
+ *                  (src/sim/process.cc:113-165,289-306;
+ *                   src/arch/riscv/process.cc:71-82,98-113,134-261): builds the
+ *                  initial SE process image of the workload binary.
+ *   fi_golden_run  one fault-free `m5.simulate()` of the workload under
+ *                  AtomicSimpleCPU (src/cpu/simple/atomic.cc:611-739), i.e. the
+ *                  run a campaign compares every trial against.
+ *   fi_run_trials  N independent gem5 runs, each with a BaseCPU::scheduleInstStop-
+ *                  style instruction-count event (src/cpu/base.cc:764-770,
+ *                  src/cpu/simple/base.cc:321-325) that flips the sampled bit(s),
+ *                  followed by exit-code/stdout comparison against the golden run.
+ *                  The per-trial loop is the AtomicSimpleCPU::tick loop, executed
+ *                  on the GPU one trial per lane.
+ *   fi_set_protect setEnableShrewd-style runtime knob (src/cpu/o3/BaseO3CPU.py:69-72,
+ *                  src/cpu/o3/cpu.hh:298-302): the selective-replication mask.
+ *
+ * Conventions: opaque handle; caller-owned host output buffers; integer status
+ * (0 = ok) plus a per-engine last-error string; one engine per host thread,
+ * bound to one HIP device; never aborts the host process -- a guest "crash" is
+ * a classified outcome.  There is no CPU execution path behind this ABI: if
+ * the HIP device or kernels are unavailable every call fails with
+ * FI_E_NODEVICE.
+ */
+#ifndef SHREWD_FI_ENGINE_H
+#define SHREWD_FI_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t fi_status;
+#define FI_OK 0
+#define FI_E_ARG -1
+#define FI_E_NODEVICE -2
+#define FI_E_HIP -3
+#define FI_E_ELF -4
+#define FI_E_STATE -5
+#define FI_E_GOLDEN -6
+
+/* Outcome classes (masked / SDC / crash / hang / detected-by-replica) plus
+ * ESCAPE: behaviour gem5 has that the engine does not model -- reported, never
+ * guessed. */
+#define FI_MASKED 0
+#define FI_SDC 1
+#define FI_CRASH 2
+#define FI_HANG 3
+#define FI_DETECTED 4
+#define FI_ESCAPE 5
+#define FI_N_CLASS 6
+
+/* FI_CRASH sub-codes: the gem5 process outcome */
+#define FI_CRASH_UNKNOWN_INST 1   /* panic  UnknownInstFault      arch/riscv/faults.cc:286-291 */
+#define FI_CRASH_ILLEGAL_INST 2   /* panic  IllegalInstFault      arch/riscv/faults.cc:294-301 */
+#define FI_CRASH_PAGE_FAULT 3     /* panic  GenericPageTableFault sim/faults.cc:95-105 */
+#define FI_CRASH_SYSCALL_RANGE 4  /* fatal  syscall out of range  sim/syscall_desc.hh:204-214 */
+#define FI_CRASH_SYSCALL_UNIMPL 5 /* fatal  unimplementedFunc     sim/syscall_emul.cc:77-80 */
+#define FI_CRASH_PROXY 6          /* fatal  readBlob failed       mem/port_proxy.hh:182-196 */
+#define FI_CRASH_FD_ASSERT 7      /* abort  FDArray assert        sim/fd_array.cc:320-323 */
+#define FI_CRASH_SIGTRAP 8        /* ebreak -> SIGTRAP            arch/riscv/faults.cc:317-322 */
+#define FI_CRASH_STACK_LIMIT 9    /* fatal  max stack exceeded    sim/mem_state.cc:440 */
+/* FI_ESCAPE sub-codes */
+#define FI_ESC_INST 1
+#define FI_ESC_SYSCALL 2
+#define FI_ESC_CSR 3
+#define FI_ESC_HOST 4
+#define FI_ESC_RESOURCE 5
+
+/* Fault-site structures: 1..31 = x1..x31, 32 = pc, 33 = 8-byte memory word */
+#define FI_T_PC 32
+#define FI_T_MEM 33
+#define FI_N_STRUCT 34
+
+typedef struct {
+    uint8_t cls, sub, exit_code, flags;  /* flags bit0: injected, bit1: memory site unmapped at t */
+    uint32_t detail;                     /* low 32 bits of pc at termination / fault va / syscall # */
+    uint64_t ninst;                      /* committed guest instructions (numInst) at termination */
+} fi_outcome;
+
+typedef struct {
+    uint64_t inst;    /* numInst at whose tick the flip is applied */
+    uint64_t mask;    /* xor mask (burst of adjacent bits) */
+    uint64_t addr;    /* memory sites: 8-byte aligned guest virtual address */
+    uint32_t target;  /* FI_T_* */
+    uint32_t trial;   /* trial id */
+} fi_site;
+
+typedef struct {
+    int32_t device;                 /* HIP device ordinal */
+    uint32_t private_pages;         /* copy-on-write pages per trial (0 -> 16) */
+    uint32_t hang_factor_x16;       /* hang cap = golden_ninst * f / 16 + 1000 (0 -> 32) */
+    uint32_t max_trials_per_launch; /* 0 -> 65536 */
+} fi_config;
+
+typedef struct {
+    uint64_t ninst, ncycles;
+    uint32_t exit_code, pad;
+    uint64_t stdout_len, stderr_len;
+    uint64_t fetch_bytes, data_bytes;
+} fi_golden_info;
+
+typedef struct {
+    uint64_t counts[FI_N_STRUCT][64][FI_N_CLASS]; /* [structure][first flipped bit][class] */
+    uint64_t crash_sub[16];
+    uint64_t escape_sub[8];
+    uint64_t trials;
+    uint64_t guest_insts;   /* sum of committed instructions over trials */
+    uint64_t fetch_bytes;   /* algorithmic bytes: instruction fetch */
+    uint64_t data_bytes;    /* algorithmic bytes: loads + stores */
+    uint64_t cow_pages;     /* private pages materialised (copy-on-write / zero-fill) */
+} fi_histogram;
+
+typedef struct fi_engine fi_engine;
+
+fi_status fi_create(const fi_config *cfg, fi_engine **out);
+void fi_destroy(fi_engine *e);
+const char *fi_last_error(fi_engine *e);
+
+/* argv/envp are NULL-terminated; argv[0] is the path string gem5 was given
+ * (it shapes the initial stack exactly as in RiscvProcess64::argsInit). */
+fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *const *argv,
+                      const char *const *envp);
+fi_status fi_golden_run(fi_engine *e, fi_golden_info *out);
+/* copies up to cap bytes of golden stdout; returns the full length in *len */
+fi_status fi_golden_stdout(fi_engine *e, uint8_t *buf, uint64_t cap, uint64_t *len);
+
+/* Campaign definition: SplitMix64 sites keyed by (seed, trial id); structures
+ * is a bitmask (bit r = x_r, bit 32 = pc, bit 33 = memory); burst = adjacent
+ * bits flipped (1..64). */
+fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint32_t burst);
+/* selective-replication mask over x0..x31 (bits 0..31) and pc (bit 32) */
+fi_status fi_set_protect(fi_engine *e, uint64_t protect_mask);
+
+fi_status fi_sample_sites(fi_engine *e, uint64_t first_trial, uint64_t n, fi_site *out);
+/* out (n entries, trial order) and hist may be NULL. hist is accumulated into (+=). */
+fi_status fi_run_trials(fi_engine *e, uint64_t first_trial, uint64_t n, fi_outcome *out, fi_histogram *hist);
+/* Explicit sites (parity tests, replay of a gem5-side site list). */
+fi_status fi_run_sites(fi_engine *e, const fi_site *sites, uint64_t n, fi_outcome *out, fi_histogram *hist);
+
+/* Device-resident variant for multi-GPU drivers: d_out (n fi_outcome) and
+ * d_hist (one fi_histogram, accumulated) are device pointers; stream is a
+ * hipStream_t (NULL = engine stream).  Asynchronous: nothing is copied back. */
+fi_status fi_run_trials_device(fi_engine *e, uint64_t first_trial, uint64_t n, void *d_out, void *d_hist,
+                               void *stream);
+/* Synchronise the engine stream. */
+fi_status fi_sync(fi_engine *e);
+
+/* Timing of the last fi_run_* call's interpreter kernel(s), measured with
+ * hipEvents on the engine stream (milliseconds). */
+double fi_last_kernel_ms(fi_engine *e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

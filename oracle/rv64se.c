@@ -183,7 +183,13 @@ static inline s64 sext(u64 v, int n) { return (s64)(v << (64 - n)) >> (64 - n); 
 /* Decode one instruction (16- or 32-bit in the low bits of raw) following the
  * decode tree of arch/riscv/isa/decoder.isa for rv_type=RV64, enable_zcd=1
  * (RiscvISA.py:95,121-127).  Field definitions: isa/bitfields.isa:36-130. */
+static void decode_tree(u32 raw, dec_t *d);
+/* Unknown and escape encodings read and write no registers. */
 static void decode(u32 raw, dec_t *d) {
+    decode_tree(raw, d);
+    if (d->op < OP_c_addi4spn) d->rd = d->rs1 = d->rs2 = -1;
+}
+static void decode_tree(u32 raw, dec_t *d) {
     memset(d, 0, sizeof(*d));
     d->raw = raw; d->rd = d->rs1 = d->rs2 = -1; d->op = OP_UNKNOWN;
     u32 q = raw & 3;
@@ -600,7 +606,7 @@ static int mem_write(mach_t *m, u64 addr, unsigned size, u64 val, u64 *fault_va)
 static void finish(mach_t *m, int cls, int sub, int exit_code) {
     m->done = 1;
     m->res.cls = (uint8_t)cls; m->res.sub = (uint8_t)sub; m->res.exit_code = (uint8_t)exit_code;
-    m->res.flags = (uint8_t)(m->injected ? 1 : 0);
+    m->res.flags = (uint8_t)((m->injected ? 1 : 0) | (m->injected == 2 ? 2 : 0));
     m->res.detail = (u32)m->pc;
     m->res.ninst = m->num_inst;
 }
@@ -666,10 +672,11 @@ static void do_syscall(mach_t *m) {
         if (fd > 2) { m->x[10] = (u64)(s64)-9; return; }                  /* -EBADF */
         if (n > (1ULL << 31)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; } /* host allocation */
         /* BufferArg::copyIn -> readBlob: fatal if any byte is unmapped (no fixup on reads) */
-        for (u64 a = buf & PAGE_MASK; n && a < buf + n; a += PAGE) {
-            if (a + PAGE < a) break;
-            if (!translate(m, a)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
-            if (buf + n < buf) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        if (n) {
+            u64 last = buf + n - 1;
+            if (last < buf) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+            for (u64 v = buf >> 12; v <= (last >> 12); v++)
+                if (!pm_find(&m->mem, v)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
         }
         bytes_t *dst = fd == 1 ? &m->out : &m->err;
         for (u64 i = 0; i < n; i++) {
@@ -1072,6 +1079,7 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
     u64 stack_min = STACK_BASE;
     u64 stack_top = stack_min - 16 - (alen + 1);
     stack_top &= ~7ULL;
+    const u64 at_random = stack_top;   /* auxv Random is taken here (process.cc:150-159) */
     const int nauxv = 8;
     stack_top -= (1 + 1) * 8 + (1 + 0) * 8 + 8 + 2 * 8 * nauxv;
     stack_top &= ~15ULL;
@@ -1096,7 +1104,7 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
     push64(c, &sp, argp); push64(c, &sp, 0);
     push64(c, &sp, 0);            /* envp terminator */
     const u64 aux[8][2] = {{9, c->entry}, {5, (u64)phnum}, {4, (u64)phentsize}, {3, phdr_vaddr},
-                           {6, PAGE}, {23, 0}, {25, stack_top}, {0, 0}};
+                           {6, PAGE}, {23, 0}, {25, at_random}, {0, 0}};
     for (int i = 0; i < nauxv; i++) { push64(c, &sp, aux[i][0]); push64(c, &sp, aux[i][1]); }
     c->sp0 = stack_min;
     c->stack_min0 = stack_min & PAGE_MASK;
@@ -1105,6 +1113,12 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
         if (nw < 4096) wpages[nw++] = pg;
         if (pg == (STACK_BASE & PAGE_MASK)) break;
     }
+    /* sorted, unique */
+    for (u64 i = 1; i < nw; i++)
+        for (u64 j = i; j > 0 && wpages[j - 1] > wpages[j]; j--) { u64 t = wpages[j]; wpages[j] = wpages[j - 1]; wpages[j - 1] = t; }
+    u64 u = 0;
+    for (u64 i = 0; i < nw; i++) if (u == 0 || wpages[u - 1] != wpages[i]) wpages[u++] = wpages[i];
+    nw = u;
     c->n_mem_pages = nw;
     c->mem_pages = (u64 *)malloc(sizeof(u64) * (nw ? nw : 1));
     memcpy(c->mem_pages, wpages, sizeof(u64) * nw);

@@ -1,0 +1,600 @@
+// fi_engine.cpp -- host side of the MI355X fault-injection engine (C ABI in
+// include/fi_engine.h).
+//
+// Host responsibilities are the ones gem5 performs once per run before the
+// tick loop starts: load the static ELF and build the SE process image
+// (src/base/loader/elf_object.cc:374-404, src/sim/process.cc:289-306,
+// src/arch/riscv/process.cc:71-261), then hand everything to the device.
+// Every guest instruction -- golden run included -- executes in the HIP
+// kernels (hip/fi_kernels.hip).  There is no CPU interpreter here.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "fi_types.h"
+
+namespace fi {
+hipError_t launch_sample(const SampleCtx &c, uint64_t n, fi_site *sites, uint64_t *keys, uint32_t *perm,
+                         hipStream_t st);
+hipError_t launch_keys(const fi_site *sites, uint64_t n, uint64_t *keys, uint32_t *perm, hipStream_t st);
+hipError_t launch_predecode(const uint8_t *text, uint64_t text_lo, uint64_t nhalf, PreInst *pre, hipStream_t st);
+hipError_t launch_debug_decode(const uint32_t *raws, uint64_t n, PreInst *out, hipStream_t st);
+hipError_t launch_trials(const DevCtx &c, hipStream_t st);
+hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, fi_histogram *h,
+                       const unsigned long long *stats, hipStream_t st);
+hipError_t sort_pairs_bytes(uint64_t n, size_t &bytes);
+hipError_t sort_pairs(void *tmp, size_t bytes, const uint64_t *kin, uint64_t *kout, const uint32_t *vin,
+                      uint32_t *vout, uint64_t n, int end_bit, hipStream_t st);
+}  // namespace fi
+
+using namespace fi;
+
+struct fi_engine {
+    fi_config cfg{};
+    std::string err;
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_ms = 0;
+
+    // process image (host copy)
+    bool loaded = false;
+    std::map<uint64_t, std::vector<uint8_t>> pages;   // vpn -> 4 KiB
+    uint64_t entry = 0, sp0 = 0, stack_min0 = 0, svma_lo = 0, svma_hi = 0;
+    uint64_t text_lo = 0, text_hi = 0;
+    std::vector<uint64_t> mem_pages;   // memory fault candidates (sorted)
+
+    // device image
+    PreInst *d_pre = nullptr;
+    uint64_t *d_base_vpn = nullptr;
+    uint32_t *d_base_frame = nullptr;
+    uint8_t *d_frames = nullptr, *d_zero = nullptr, *d_text = nullptr;
+    uint64_t *d_mem_pages = nullptr;
+    uint32_t n_base = 0;
+
+    // golden
+    bool have_golden = false;
+    fi_golden_info golden{};
+    std::vector<uint8_t> gout, gerr;
+    uint8_t *d_gout = nullptr, *d_gerr = nullptr;
+
+    // campaign
+    uint64_t seed = 0x5EED0001ULL, structures = 0;
+    uint32_t burst = 1;
+    uint64_t protect = 0;
+
+    // work buffers, sized for `cap` trials per launch
+    uint64_t cap = 0;
+    fi_site *d_sites = nullptr;
+    uint64_t *d_keys = nullptr, *d_keys2 = nullptr;
+    uint32_t *d_perm = nullptr, *d_perm2 = nullptr;
+    void *d_tmp = nullptr;
+    size_t tmp_bytes = 0;
+    fi_outcome *d_out = nullptr;
+    fi_histogram *d_hist = nullptr;
+    unsigned long long *d_stats = nullptr;
+    uint8_t *d_priv = nullptr;
+    uint64_t *d_priv_vpn = nullptr;
+};
+
+static fi_status fail(fi_engine *e, fi_status code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (e) e->err = buf;
+    return code;
+}
+
+#define HIPCHK(call)                                                                          \
+    do {                                                                                      \
+        hipError_t _e = (call);                                                               \
+        if (_e != hipSuccess) return fail(e, FI_E_HIP, "%s: %s", #call, hipGetErrorString(_e)); \
+    } while (0)
+
+template <typename T>
+static void dfree(T *&p) {
+    if (p) { (void)hipFree((void *)p); p = nullptr; }
+}
+
+extern "C" {
+
+fi_status fi_create(const fi_config *cfg, fi_engine **out) {
+    if (!out) return FI_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return FI_E_NODEVICE;
+    fi_engine *e = new fi_engine();
+    if (cfg) e->cfg = *cfg;
+    if (e->cfg.private_pages == 0) e->cfg.private_pages = 16;
+    if (e->cfg.hang_factor_x16 == 0) e->cfg.hang_factor_x16 = 32;
+    if (e->cfg.max_trials_per_launch == 0) e->cfg.max_trials_per_launch = 65536;
+    e->dev = e->cfg.device;
+    if (e->dev < 0 || e->dev >= n) { delete e; return FI_E_ARG; }
+    if (hipSetDevice(e->dev) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
+        delete e;
+        return FI_E_HIP;
+    }
+    *out = e;
+    return FI_OK;
+}
+
+static void free_work(fi_engine *e) {
+    dfree(e->d_sites); dfree(e->d_keys); dfree(e->d_keys2); dfree(e->d_perm); dfree(e->d_perm2);
+    dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_priv); dfree(e->d_priv_vpn);
+    e->cap = 0;
+}
+static void free_image(fi_engine *e) {
+    dfree(e->d_pre); dfree(e->d_base_vpn); dfree(e->d_base_frame); dfree(e->d_frames); dfree(e->d_zero);
+    dfree(e->d_text); dfree(e->d_mem_pages); dfree(e->d_gout); dfree(e->d_gerr);
+    e->have_golden = false;
+    e->loaded = false;
+}
+
+void fi_destroy(fi_engine *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->dev);
+    free_work(e);
+    free_image(e);
+    if (e->ev0) (void)hipEventDestroy(e->ev0);
+    if (e->ev1) (void)hipEventDestroy(e->ev1);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+const char *fi_last_error(fi_engine *e) { return e ? e->err.c_str() : "null engine"; }
+
+// ------------------------------------------------------------------ image
+static uint16_t le16(const uint8_t *p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static uint32_t le32(const uint8_t *p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24); }
+static uint64_t le64(const uint8_t *p) { return (uint64_t)le32(p) | ((uint64_t)le32(p + 4) << 32); }
+
+// SETranslatingPortProxy(Always) write: allocates pages on demand.
+static void img_write(fi_engine *e, uint64_t addr, const uint8_t *src, uint64_t n) {
+    for (uint64_t i = 0; i < n;) {
+        const uint64_t a = addr + i;
+        auto &pg = e->pages[a >> 12];
+        if (pg.empty()) pg.assign(kPage, 0);
+        const uint64_t off = a & (kPage - 1);
+        const uint64_t k = std::min<uint64_t>(n - i, kPage - off);
+        if (src) memcpy(pg.data() + off, src + i, k);
+        else memset(pg.data() + off, 0, k);
+        i += k;
+    }
+}
+static void img_push64(fi_engine *e, uint64_t &sp, uint64_t v) {
+    uint8_t b[8];
+    for (int i = 0; i < 8; i++) b[i] = (uint8_t)(v >> (8 * i));
+    img_write(e, sp, b, 8);
+    sp += 8;
+}
+
+// std::mt19937_64 with gem5's global seed 5489 (src/base/random.hh:211-217):
+// AT_RANDOM byte i = gen() % 256 (RiscvProcess::argsInit, process.cc:171-175).
+struct Mt64 {
+    uint64_t mt[312];
+    int idx;
+    explicit Mt64(uint64_t seed) {
+        mt[0] = seed;
+        for (int i = 1; i < 312; i++) mt[i] = 6364136223846793005ULL * (mt[i - 1] ^ (mt[i - 1] >> 62)) + (uint64_t)i;
+        idx = 312;
+    }
+    uint64_t operator()() {
+        if (idx >= 312) {
+            for (int i = 0; i < 312; i++) {
+                const uint64_t x = (mt[i] & 0xFFFFFFFF80000000ULL) | (mt[(i + 1) % 312] & 0x7FFFFFFFULL);
+                uint64_t xa = x >> 1;
+                if (x & 1) xa ^= 0xB5026F5AA96619E9ULL;
+                mt[i] = mt[(i + 156) % 312] ^ xa;
+            }
+            idx = 0;
+        }
+        uint64_t y = mt[idx++];
+        y ^= (y >> 29) & 0x5555555555555555ULL;
+        y ^= (y << 17) & 0x71D67FFFEDA60000ULL;
+        y ^= (y << 37) & 0xFFF7EEE000000000ULL;
+        y ^= y >> 43;
+        return y;
+    }
+};
+
+fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *const *argv, const char *const *envp) {
+    if (!e || !elf || !argv || !argv[0]) return fail(e, FI_E_ARG, "fi_load_elf: elf and argv[0] required");
+    HIPCHK(hipSetDevice(e->dev));
+    free_image(e);
+    e->pages.clear();
+    e->mem_pages.clear();
+    if (len < 64 || memcmp(elf, "\x7f" "ELF", 4) || elf[4] != 2 || elf[5] != 1 || le16(elf + 18) != 243)
+        return fail(e, FI_E_ELF, "not an ELF64 little-endian RISC-V executable");
+    e->entry = le64(elf + 24);
+    const uint64_t phoff = le64(elf + 32);
+    const uint32_t phentsize = le16(elf + 54), phnum = le16(elf + 56);
+    if (phoff + (uint64_t)phentsize * phnum > len) return fail(e, FI_E_ELF, "program headers out of file");
+    uint64_t max_addr = 0, phdr_vaddr = 0;
+    uint64_t xlo = ~0ULL, xhi = 0;
+    std::vector<uint64_t> wpages;
+    for (uint32_t i = 0; i < phnum; i++) {
+        const uint8_t *ph = elf + phoff + (uint64_t)i * phentsize;
+        if (le32(ph) != 1) continue;   // PT_LOAD
+        const uint32_t flags = le32(ph + 4);
+        const uint64_t off = le64(ph + 8), vaddr = le64(ph + 16), paddr = le64(ph + 24);
+        const uint64_t filesz = le64(ph + 32), memsz = le64(ph + 40);
+        if (memsz == 0) continue;                       // elf_object.cc:378-381
+        if (off + filesz > len) return fail(e, FI_E_ELF, "segment %u beyond file", i);
+        img_write(e, paddr, elf + off, filesz);          // loaded at p_paddr (elf_object.cc:383)
+        if (memsz > filesz) img_write(e, paddr + filesz, nullptr, memsz - filesz);
+        max_addr = std::max(max_addr, paddr + memsz);
+        if (off <= phoff && off + filesz > phoff) phdr_vaddr = vaddr + (phoff - off);
+        if (flags & 1) { xlo = std::min(xlo, paddr & ~(kPage - 1)); xhi = std::max(xhi, (paddr + memsz + kPage - 1) & ~(kPage - 1)); }
+        if (flags & 2)
+            for (uint64_t pg = paddr & ~(kPage - 1); pg < paddr + memsz; pg += kPage) wpages.push_back(pg);
+    }
+    if (xlo == ~0ULL) return fail(e, FI_E_ELF, "no executable segment");
+    e->text_lo = xlo;
+    e->text_hi = xhi;
+
+    // RiscvProcess::argsInit<uint64_t> (src/arch/riscv/process.cc:134-261)
+    std::vector<std::string> av, ev;
+    for (int i = 0; argv[i]; i++) av.emplace_back(argv[i]);
+    for (int i = 0; envp && envp[i]; i++) ev.emplace_back(envp[i]);
+    const int nauxv = 8;
+    uint64_t stack_min = kStackBase;
+    uint64_t stack_top = stack_min - 16;
+    for (auto &s : av) stack_top -= s.size() + 1;
+    for (auto &s : ev) stack_top -= s.size() + 1;
+    stack_top &= ~7ULL;
+    const uint64_t at_random = stack_top;   // AT_RANDOM points here (process.cc:156)
+    const uint64_t arrays = (1 + av.size()) * 8 + (1 + ev.size()) * 8 + 8 + 2 * 8 * nauxv;
+    stack_top -= arrays;
+    stack_top &= ~15ULL;
+    const uint64_t stack_size = kStackBase - stack_top;
+    e->svma_lo = stack_top & ~(kPage - 1);
+    e->svma_hi = e->svma_lo + ((stack_size + kPage - 1) & ~(kPage - 1));
+    stack_min -= 16;
+    Mt64 rng(5489);
+    uint8_t rnd[16];
+    for (int i = 0; i < 16; i++) rnd[i] = (uint8_t)(rng() % 256);
+    img_write(e, stack_min, rnd, 16);
+    std::vector<uint64_t> argp, envptr;
+    for (auto &s : av) { stack_min -= s.size() + 1; img_write(e, stack_min, (const uint8_t *)s.c_str(), s.size() + 1); argp.push_back(stack_min); }
+    for (auto &s : ev) { stack_min -= s.size() + 1; img_write(e, stack_min, (const uint8_t *)s.c_str(), s.size() + 1); envptr.push_back(stack_min); }
+    stack_min &= ~7ULL;
+    stack_min -= arrays;
+    stack_min &= ~15ULL;
+    uint64_t sp = stack_min;
+    img_push64(e, sp, av.size());
+    for (uint64_t p : argp) img_push64(e, sp, p);
+    img_push64(e, sp, 0);
+    for (uint64_t p : envptr) img_push64(e, sp, p);
+    img_push64(e, sp, 0);
+    const uint64_t aux[8][2] = {{9, e->entry}, {5, phnum}, {4, phentsize}, {3, phdr_vaddr},
+                                {6, kPage}, {23, 0}, {25, at_random}, {0, 0}};
+    for (auto &a : aux) { img_push64(e, sp, a[0]); img_push64(e, sp, a[1]); }
+    e->sp0 = stack_min;
+    e->stack_min0 = stack_min & ~(kPage - 1);
+    for (uint64_t pg = e->stack_min0;; pg += kPage) {
+        wpages.push_back(pg);
+        if (pg == (kStackBase & ~(kPage - 1))) break;
+    }
+    std::sort(wpages.begin(), wpages.end());
+    wpages.erase(std::unique(wpages.begin(), wpages.end()), wpages.end());
+    e->mem_pages = wpages;
+    (void)max_addr;   // brk = roundUp(maxAddr) is not needed: brk() is an escape
+
+    // ---- upload: frames sorted by vpn, text pre-decode
+    std::vector<uint64_t> vpns;
+    std::vector<uint32_t> fidx;
+    std::vector<uint8_t> frames;
+    for (auto &kv : e->pages) {
+        vpns.push_back(kv.first);
+        fidx.push_back((uint32_t)(frames.size() / kPage));
+        frames.insert(frames.end(), kv.second.begin(), kv.second.end());
+    }
+    e->n_base = (uint32_t)vpns.size();
+    HIPCHK(hipMalloc(&e->d_base_vpn, vpns.size() * 8));
+    HIPCHK(hipMalloc(&e->d_base_frame, fidx.size() * 4));
+    HIPCHK(hipMalloc(&e->d_frames, frames.size()));
+    HIPCHK(hipMalloc(&e->d_zero, kPage));
+    HIPCHK(hipMalloc(&e->d_mem_pages, std::max<size_t>(1, wpages.size()) * 8));
+    HIPCHK(hipMemcpy(e->d_base_vpn, vpns.data(), vpns.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->d_base_frame, fidx.data(), fidx.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->d_frames, frames.data(), frames.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(e->d_zero, 0, kPage));
+    if (!wpages.empty()) HIPCHK(hipMemcpy(e->d_mem_pages, wpages.data(), wpages.size() * 8, hipMemcpyHostToDevice));
+    const uint64_t tbytes = e->text_hi - e->text_lo;
+    std::vector<uint8_t> text(tbytes, 0);
+    for (uint64_t a = e->text_lo; a < e->text_hi; a += kPage) {
+        auto it = e->pages.find(a >> 12);
+        if (it != e->pages.end()) memcpy(text.data() + (a - e->text_lo), it->second.data(), kPage);
+    }
+    HIPCHK(hipMalloc(&e->d_text, tbytes));
+    HIPCHK(hipMemcpy(e->d_text, text.data(), tbytes, hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&e->d_pre, (tbytes / 2) * sizeof(PreInst)));
+    HIPCHK(launch_predecode(e->d_text, e->text_lo, tbytes / 2, e->d_pre, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    e->loaded = true;
+    return FI_OK;
+}
+
+// ------------------------------------------------------------------ work buffers
+static fi_status ensure_work(fi_engine *e, uint64_t n) {
+    if (n <= e->cap) return FI_OK;
+    free_work(e);
+    const uint64_t c = n;
+    HIPCHK(hipMalloc(&e->d_sites, c * sizeof(fi_site)));
+    HIPCHK(hipMalloc(&e->d_keys, c * 8));
+    HIPCHK(hipMalloc(&e->d_keys2, c * 8));
+    HIPCHK(hipMalloc(&e->d_perm, c * 4));
+    HIPCHK(hipMalloc(&e->d_perm2, c * 4));
+    HIPCHK(sort_pairs_bytes(c, e->tmp_bytes));
+    HIPCHK(hipMalloc(&e->d_tmp, std::max<size_t>(e->tmp_bytes, 16)));
+    HIPCHK(hipMalloc(&e->d_out, c * sizeof(fi_outcome)));
+    HIPCHK(hipMalloc(&e->d_hist, sizeof(fi_histogram)));
+    HIPCHK(hipMalloc(&e->d_stats, 8 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&e->d_priv, c * e->cfg.private_pages * kPage));
+    HIPCHK(hipMalloc(&e->d_priv_vpn, c * e->cfg.private_pages * 8));
+    e->cap = c;
+    return FI_OK;
+}
+
+static DevCtx base_ctx(fi_engine *e) {
+    DevCtx c{};
+    c.pre = e->d_pre; c.text_lo = e->text_lo; c.text_hi = e->text_hi;
+    c.base_vpn = e->d_base_vpn; c.base_frame = e->d_base_frame; c.frames = e->d_frames; c.zero_page = e->d_zero;
+    c.n_base = e->n_base;
+    c.entry = e->entry; c.sp0 = e->sp0; c.stack_min0 = e->stack_min0;
+    c.stack_vma_lo = e->svma_lo; c.stack_vma_hi = e->svma_hi;
+    c.gout = e->d_gout; c.gerr = e->d_gerr; c.gout_len = e->gout.size(); c.gerr_len = e->gerr.size();
+    c.gexit = e->golden.exit_code;
+    c.priv_pages = e->cfg.private_pages;
+    c.hang_cap = e->golden.ninst * e->cfg.hang_factor_x16 / 16 + 1000;
+    c.protect_mask = e->protect;
+    c.priv_frames = e->d_priv; c.priv_vpn = e->d_priv_vpn;
+    c.stats = e->d_stats;
+    return c;
+}
+
+fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
+    if (!e) return FI_E_ARG;
+    if (!e->loaded) return fail(e, FI_E_STATE, "fi_golden_run: no workload loaded");
+    HIPCHK(hipSetDevice(e->dev));
+    fi_status st = ensure_work(e, 64);
+    if (st) return st;
+    const uint64_t rec_cap = 1 << 24;
+    uint8_t *d_rec_out = nullptr, *d_rec_err = nullptr;
+    HIPCHK(hipMalloc(&d_rec_out, rec_cap));
+    HIPCHK(hipMalloc(&d_rec_err, rec_cap));
+    DevCtx c = base_ctx(e);
+    c.record = 1;
+    c.rec_out = d_rec_out; c.rec_err = d_rec_err; c.rec_cap = rec_cap;
+    c.hang_cap = 1ULL << 30;   // golden safety cap
+    c.out = e->d_out;
+    c.n = 1;
+    c.sites = nullptr; c.perm = nullptr;
+    HIPCHK(hipMemsetAsync(e->d_stats, 0, 8 * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipEventRecord(e->ev0, e->stream));
+    HIPCHK(launch_trials(c, e->stream));
+    HIPCHK(hipEventRecord(e->ev1, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    e->last_ms = ms;
+    fi_outcome o;
+    unsigned long long stats[8];
+    HIPCHK(hipMemcpy(&o, e->d_out, sizeof o, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(stats, e->d_stats, sizeof stats, hipMemcpyDeviceToHost));
+    if (o.cls != FI_MASKED) {
+        (void)hipFree(d_rec_out); (void)hipFree(d_rec_err);
+        return fail(e, FI_E_GOLDEN, "golden run did not exit normally (class %u sub %u detail %#x after %llu insts)",
+                    o.cls, o.sub, o.detail, (unsigned long long)o.ninst);
+    }
+    const uint64_t ol = stats[4], el = stats[5];
+    if (ol > rec_cap || el > rec_cap) return fail(e, FI_E_GOLDEN, "golden output exceeds %llu bytes", (unsigned long long)rec_cap);
+    e->gout.assign(ol, 0);
+    e->gerr.assign(el, 0);
+    if (ol) HIPCHK(hipMemcpy(e->gout.data(), d_rec_out, ol, hipMemcpyDeviceToHost));
+    if (el) HIPCHK(hipMemcpy(e->gerr.data(), d_rec_err, el, hipMemcpyDeviceToHost));
+    (void)hipFree(d_rec_out);
+    (void)hipFree(d_rec_err);
+    dfree(e->d_gout); dfree(e->d_gerr);
+    HIPCHK(hipMalloc(&e->d_gout, std::max<uint64_t>(ol, 1)));
+    HIPCHK(hipMalloc(&e->d_gerr, std::max<uint64_t>(el, 1)));
+    if (ol) HIPCHK(hipMemcpy(e->d_gout, e->gout.data(), ol, hipMemcpyHostToDevice));
+    if (el) HIPCHK(hipMemcpy(e->d_gerr, e->gerr.data(), el, hipMemcpyHostToDevice));
+    e->golden.ninst = o.ninst;
+    e->golden.ncycles = stats[3];
+    e->golden.exit_code = o.exit_code;
+    e->golden.stdout_len = ol;
+    e->golden.stderr_len = el;
+    e->golden.fetch_bytes = stats[0];
+    e->golden.data_bytes = stats[1];
+    e->have_golden = true;
+    if (out) *out = e->golden;
+    return FI_OK;
+}
+
+fi_status fi_golden_stdout(fi_engine *e, uint8_t *buf, uint64_t cap, uint64_t *len) {
+    if (!e || !e->have_golden) return fail(e, FI_E_STATE, "no golden run");
+    if (buf && cap) memcpy(buf, e->gout.data(), std::min<uint64_t>(cap, e->gout.size()));
+    if (len) *len = e->gout.size();
+    return FI_OK;
+}
+
+fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint32_t burst) {
+    if (!e) return FI_E_ARG;
+    structures &= ~1ULL;
+    structures &= (1ULL << FI_N_STRUCT) - 1;
+    if (!structures) return fail(e, FI_E_ARG, "no fault structures selected");
+    if (burst < 1 || burst > 64) return fail(e, FI_E_ARG, "burst must be 1..64");
+    e->seed = seed; e->structures = structures; e->burst = burst;
+    return FI_OK;
+}
+
+fi_status fi_set_protect(fi_engine *e, uint64_t protect_mask) {
+    if (!e) return FI_E_ARG;
+    e->protect = protect_mask;
+    return FI_OK;
+}
+
+static SampleCtx sample_ctx(fi_engine *e, uint64_t first) {
+    SampleCtx s{};
+    s.seed = e->seed;
+    s.structures = e->structures;
+    if (e->mem_pages.empty()) s.structures &= ~(1ULL << FI_T_MEM);
+    s.golden_ninst = e->golden.ninst;
+    s.first = first;
+    s.burst = e->burst;
+    s.n_struct = (uint32_t)__builtin_popcountll(s.structures);
+    s.mem_pages = e->d_mem_pages;
+    s.n_mem_pages = e->mem_pages.size();
+    return s;
+}
+
+fi_status fi_sample_sites(fi_engine *e, uint64_t first, uint64_t n, fi_site *out) {
+    if (!e || !out) return FI_E_ARG;
+    if (!e->have_golden) return fail(e, FI_E_STATE, "golden run required before sampling");
+    if (!e->structures) return fail(e, FI_E_STATE, "fi_set_campaign first");
+    HIPCHK(hipSetDevice(e->dev));
+    const uint64_t chunk = e->cfg.max_trials_per_launch;
+    fi_status st = ensure_work(e, std::min<uint64_t>(std::max<uint64_t>(n, 1), chunk));
+    if (st) return st;
+    for (uint64_t done = 0; done < n;) {
+        const uint64_t k = std::min<uint64_t>(n - done, e->cap);
+        HIPCHK(launch_sample(sample_ctx(e, first + done), k, e->d_sites, e->d_keys, e->d_perm, e->stream));
+        HIPCHK(hipMemcpyAsync(out + done, e->d_sites, k * sizeof(fi_site), hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream));
+        done += k;
+    }
+    return FI_OK;
+}
+
+// One launch: d_sites[0..k) holds the sites in trial order, keys/perm set.
+static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histogram *d_hist, hipStream_t st) {
+    int end_bit = 64 - __builtin_clzll(std::max<uint64_t>(e->golden.ninst, 1));
+    HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_keys, e->d_keys2, e->d_perm, e->d_perm2, k, end_bit, st));
+    DevCtx c = base_ctx(e);
+    c.sites = e->d_sites;
+    c.perm = e->d_perm2;
+    c.out = d_out;
+    c.n = k;
+    HIPCHK(hipMemsetAsync(e->d_stats, 0, 8 * sizeof(unsigned long long), st));
+    HIPCHK(hipEventRecord(e->ev0, st));
+    HIPCHK(launch_trials(c, st));
+    HIPCHK(hipEventRecord(e->ev1, st));
+    HIPCHK(launch_hist(e->d_sites, d_out, k, d_hist, e->d_stats, st));
+    return FI_OK;
+}
+
+static fi_status finish_chunk(fi_engine *e, hipStream_t st, double &ms_acc) {
+    HIPCHK(hipStreamSynchronize(st));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
+    ms_acc += ms;
+    return FI_OK;
+}
+
+static void hist_add(fi_histogram *dst, const fi_histogram *src) {
+    const uint64_t *s = (const uint64_t *)src;
+    uint64_t *d = (uint64_t *)dst;
+    for (size_t i = 0; i < sizeof(fi_histogram) / 8; i++) d[i] += s[i];
+}
+
+static fi_status run_common(fi_engine *e, uint64_t first, const fi_site *sites, uint64_t n, fi_outcome *out,
+                            fi_histogram *hist) {
+    if (!e) return FI_E_ARG;
+    if (!e->have_golden) return fail(e, FI_E_STATE, "golden run required");
+    if (!sites && !e->structures) return fail(e, FI_E_STATE, "fi_set_campaign first");
+    HIPCHK(hipSetDevice(e->dev));
+    const uint64_t chunk = e->cfg.max_trials_per_launch;
+    fi_status s = ensure_work(e, std::min<uint64_t>(std::max<uint64_t>(n, 1), chunk));
+    if (s) return s;
+    HIPCHK(hipMemsetAsync(e->d_hist, 0, sizeof(fi_histogram), e->stream));
+    double ms = 0;
+    for (uint64_t done = 0; done < n;) {
+        const uint64_t k = std::min<uint64_t>(n - done, e->cap);
+        if (sites) {
+            HIPCHK(hipMemcpyAsync(e->d_sites, sites + done, k * sizeof(fi_site), hipMemcpyHostToDevice, e->stream));
+            HIPCHK(launch_keys(e->d_sites, k, e->d_keys, e->d_perm, e->stream));
+        } else {
+            HIPCHK(launch_sample(sample_ctx(e, first + done), k, e->d_sites, e->d_keys, e->d_perm, e->stream));
+        }
+        s = run_chunk(e, k, e->d_out, e->d_hist, e->stream);
+        if (s) return s;
+        if (out) HIPCHK(hipMemcpyAsync(out + done, e->d_out, k * sizeof(fi_outcome), hipMemcpyDeviceToHost, e->stream));
+        s = finish_chunk(e, e->stream, ms);
+        if (s) return s;
+        done += k;
+    }
+    e->last_ms = ms;
+    if (hist) {
+        fi_histogram h;
+        HIPCHK(hipMemcpy(&h, e->d_hist, sizeof h, hipMemcpyDeviceToHost));
+        hist_add(hist, &h);
+    }
+    return FI_OK;
+}
+
+fi_status fi_run_trials(fi_engine *e, uint64_t first, uint64_t n, fi_outcome *out, fi_histogram *hist) {
+    return run_common(e, first, nullptr, n, out, hist);
+}
+
+fi_status fi_run_sites(fi_engine *e, const fi_site *sites, uint64_t n, fi_outcome *out, fi_histogram *hist) {
+    if (!sites && n) return FI_E_ARG;
+    return run_common(e, 0, sites, n, out, hist);
+}
+
+fi_status fi_run_trials_device(fi_engine *e, uint64_t first, uint64_t n, void *d_out, void *d_hist, void *stream) {
+    if (!e || !d_out || !d_hist) return FI_E_ARG;
+    if (!e->have_golden) return fail(e, FI_E_STATE, "golden run required");
+    if (!e->structures) return fail(e, FI_E_STATE, "fi_set_campaign first");
+    HIPCHK(hipSetDevice(e->dev));
+    hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+    const uint64_t chunk = e->cfg.max_trials_per_launch;
+    fi_status s = ensure_work(e, std::min<uint64_t>(std::max<uint64_t>(n, 1), chunk));
+    if (s) return s;
+    for (uint64_t done = 0; done < n;) {
+        const uint64_t k = std::min<uint64_t>(n - done, e->cap);
+        HIPCHK(launch_sample(sample_ctx(e, first + done), k, e->d_sites, e->d_keys, e->d_perm, st));
+        s = run_chunk(e, k, (fi_outcome *)d_out + done, (fi_histogram *)d_hist, st);
+        if (s) return s;
+        done += k;
+    }
+    return FI_OK;
+}
+
+fi_status fi_sync(fi_engine *e) {
+    if (!e) return FI_E_ARG;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, e->ev0, e->ev1) == hipSuccess) e->last_ms = ms;
+    return FI_OK;
+}
+
+double fi_last_kernel_ms(fi_engine *e) { return e ? e->last_ms : 0.0; }
+
+// ------------------------------------------------------------------ debug hooks (tests)
+fi_status fi_debug_decode(fi_engine *e, const uint32_t *raws, uint64_t n, void *out16) {
+    if (!e || !raws || !out16) return FI_E_ARG;
+    HIPCHK(hipSetDevice(e->dev));
+    uint32_t *d_raw = nullptr;
+    PreInst *d_o = nullptr;
+    HIPCHK(hipMalloc(&d_raw, n * 4));
+    HIPCHK(hipMalloc(&d_o, n * sizeof(PreInst)));
+    HIPCHK(hipMemcpy(d_raw, raws, n * 4, hipMemcpyHostToDevice));
+    HIPCHK(launch_debug_decode(d_raw, n, d_o, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(out16, d_o, n * sizeof(PreInst), hipMemcpyDeviceToHost));
+    (void)hipFree(d_raw);
+    (void)hipFree(d_o);
+    return FI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,361 @@
+// rv64_isa.h -- RV64 decode for the CDNA4 interpreter.
+//
+// Decode follows the decode tree of gem5's src/arch/riscv/isa/decoder.isa for
+// rv_type = RV64 and enable_zcd = 1 (src/arch/riscv/RiscvISA.py:95,121-127);
+// bitfields from isa/bitfields.isa:36-130.  Encodings gem5 decodes to an
+// instruction this engine does not model (FP, vector, AMO, crypto, privileged
+// SYSTEM, cbo, M5 ops, hypervisor loads) map to ESC_* ops and end the trial as
+// an explicit ESCAPE outcome; encodings gem5 decodes to Unknown map to UNKNOWN.
+// The function is evaluated on wave-uniform (scalar) operands by the
+// pre-decode kernel and on the slow fetch path.
+#pragma once
+#include <stdint.h>
+
+#define FI_OPS(X) \
+    X(UNKNOWN) X(ESC_FP) X(ESC_VEC) X(ESC_AMO) X(ESC_SYS) X(ESC_CRYPTO) X(ESC_CBO) X(ESC_CMP) X(ESC_M5) X(ESC_HYP) \
+    X(c_addi4spn) X(c_lw) X(c_ld) X(c_lbu) X(c_lhu) X(c_lh) X(c_sb) X(c_sh) X(c_sw) X(c_sd) \
+    X(c_addi) X(c_addiw) X(c_li) X(c_addi16sp) X(c_lui) X(c_srli) X(c_srai) X(c_andi) \
+    X(c_sub) X(c_xor) X(c_or) X(c_and) X(c_subw) X(c_addw) X(c_mul) \
+    X(c_zext_b) X(c_sext_b) X(c_zext_h) X(c_sext_h) X(c_zext_w) X(c_not) \
+    X(c_j) X(c_beqz) X(c_bnez) X(c_slli) X(c_lwsp) X(c_ldsp) X(c_jr) X(c_mv) X(c_ebreak) X(c_jalr) X(c_add) \
+    X(c_swsp) X(c_sdsp) \
+    X(lb) X(lh) X(lw) X(ld) X(lbu) X(lhu) X(lwu) X(fence) X(fence_i) \
+    X(slli) X(bseti) X(bclri) X(binvi) X(clz) X(ctz) X(cpop) X(sext_b) X(sext_h) \
+    X(addi) X(slti) X(sltiu) X(xori) X(srli) X(orc_b) X(srai) X(bexti) X(rori) X(rev8) \
+    X(prefetch_i) X(prefetch_r) X(prefetch_w) X(ori_hint) X(ori) X(andi) X(auipc) \
+    X(addiw) X(slliw) X(slli_uw) X(clzw) X(ctzw) X(cpopw) X(srliw) X(sraiw) X(roriw) \
+    X(sb) X(sh) X(sw) X(sd) \
+    X(add) X(sub) X(mul) X(sll) X(mulh) X(clmul) X(bset) X(bclr) X(rol) X(binv) \
+    X(slt) X(mulhsu) X(clmulr) X(sh1add) X(sltu) X(mulhu) X(clmulh) \
+    X(xor_) X(div_) X(pack) X(min_) X(sh2add) X(xnor) \
+    X(srl) X(divu) X(czero_eqz) X(sra) X(minu) X(bext) X(ror) \
+    X(or_) X(rem) X(max_) X(sh3add) X(orn) \
+    X(and_) X(remu) X(packh) X(maxu) X(czero_nez) X(andn) \
+    X(lui) X(addw) X(mulw) X(add_uw) X(subw) X(sllw) X(rolw) X(sh1add_uw) \
+    X(divw) X(packw) X(sh2add_uw) X(srlw) X(divuw) X(sraw) X(rorw) X(remw) X(sh3add_uw) X(remuw) \
+    X(beq) X(bne) X(blt) X(bge) X(bltu) X(bgeu) X(jalr) X(jal) \
+    X(ecall) X(ebreak) X(csr)
+
+namespace fi {
+
+enum Op : uint8_t {
+#define FI_X(n) OP_##n,
+    FI_OPS(FI_X)
+#undef FI_X
+    OP_COUNT
+};
+
+struct Dec {
+    uint32_t raw;
+    int32_t imm;
+    uint8_t op, rd, rs1, rs2, len, flags;  // flags: kPreRs1|kPreRs2|kPreRd
+    uint16_t aux;
+};
+
+__host__ __device__ inline uint32_t fbits(uint32_t v, int hi, int lo) {
+    return (v >> lo) & ((1u << (hi - lo + 1)) - 1u);
+}
+__host__ __device__ inline int32_t fsext(uint32_t v, int n) { return (int32_t)(v << (32 - n)) >> (32 - n); }
+
+#define D_RD(r) (d.rd = (uint8_t)(r), d.flags |= 16)
+#define D_RS1(r) (d.rs1 = (uint8_t)(r), d.flags |= 4)
+#define D_RS2(r) (d.rs2 = (uint8_t)(r), d.flags |= 8)
+
+__host__ __device__ inline Dec rv_decode(uint32_t raw) {
+    Dec d;
+    d.raw = raw; d.imm = 0; d.op = OP_UNKNOWN; d.rd = d.rs1 = d.rs2 = 0; d.flags = 0; d.aux = 0;
+    const uint32_t q = raw & 3;
+    if (q != 3) {  // compressed, decoder.isa:43-536
+        raw &= 0xFFFF; d.raw = raw; d.len = 2;
+        const uint32_t cop = fbits(raw, 15, 13);
+        const uint32_t rp1 = 8 + fbits(raw, 9, 7), rp2 = 8 + fbits(raw, 4, 2);
+        const uint32_t rc1 = fbits(raw, 11, 7), rc2 = fbits(raw, 6, 2);
+        const uint32_t cimm5 = fbits(raw, 6, 2), cimm1 = fbits(raw, 12, 12), cimm3 = fbits(raw, 12, 10);
+        const uint32_t cimm2 = fbits(raw, 6, 5), cimm6 = fbits(raw, 12, 7), cimm8 = fbits(raw, 12, 5);
+        if (q == 0) {
+            switch (cop) {
+            case 0: d.op = OP_c_addi4spn; D_RD(rp2); D_RS1(2);
+                d.imm = (fbits(cimm8, 1, 1) << 2) | (fbits(cimm8, 0, 0) << 3) | (fbits(cimm8, 7, 6) << 4) |
+                        (fbits(cimm8, 5, 2) << 6);
+                return d;
+            case 1: d.op = OP_ESC_FP; return d;
+            case 2: d.op = OP_c_lw; D_RD(rp2); D_RS1(rp1);
+                d.imm = (fbits(cimm2, 1, 1) << 2) | (cimm3 << 3) | (fbits(cimm2, 0, 0) << 6); return d;
+            case 3: d.op = OP_c_ld; D_RD(rp2); D_RS1(rp1); d.imm = (cimm3 << 3) | (cimm2 << 6); return d;
+            case 4:
+                switch (fbits(raw, 12, 10)) {
+                case 0: d.op = OP_c_lbu; D_RD(rp2); D_RS1(rp1); d.imm = (fbits(cimm2, 0, 0) << 1) | fbits(cimm2, 1, 1); return d;
+                case 1: d.op = fbits(raw, 6, 6) ? OP_c_lh : OP_c_lhu; D_RD(rp2); D_RS1(rp1); d.imm = fbits(cimm2, 0, 0) << 1; return d;
+                case 2: d.op = OP_c_sb; D_RS1(rp1); D_RS2(rp2); d.imm = (fbits(cimm2, 0, 0) << 1) | fbits(cimm2, 1, 1); return d;
+                case 3: d.op = OP_c_sh; D_RS1(rp1); D_RS2(rp2); d.imm = fbits(cimm2, 0, 0) << 1; return d;
+                default: return d;
+                }
+            case 5: d.op = OP_ESC_FP; return d;
+            case 6: d.op = OP_c_sw; D_RS1(rp1); D_RS2(rp2);
+                d.imm = (fbits(cimm2, 1, 1) << 2) | (cimm3 << 3) | (fbits(cimm2, 0, 0) << 6); return d;
+            default: d.op = OP_c_sd; D_RS1(rp1); D_RS2(rp2); d.imm = (cimm3 << 3) | (cimm2 << 6); return d;
+            }
+        }
+        if (q == 1) {
+            switch (cop) {
+            case 0: d.op = OP_c_addi; D_RD(rc1); D_RS1(rc1); d.imm = fsext(cimm5 | (cimm1 << 5), 6); return d;
+            case 1: d.op = OP_c_addiw; D_RD(rc1); D_RS1(rc1); d.imm = fsext(cimm5 | (cimm1 << 5), 6); return d;
+            case 2: d.op = OP_c_li; D_RD(rc1); d.imm = fsext(cimm5 | (cimm1 << 5), 6); return d;
+            case 3:
+                if (rc1 == 2) {
+                    d.op = OP_c_addi16sp; D_RD(2); D_RS1(2);
+                    d.imm = fsext((fbits(cimm5, 4, 4) << 4) | (fbits(cimm5, 0, 0) << 5) | (fbits(cimm5, 3, 3) << 6) |
+                                  (fbits(cimm5, 2, 1) << 7) | (cimm1 << 9), 10);
+                } else {
+                    d.op = OP_c_lui; D_RD(rc1); d.imm = fsext(cimm5 | (cimm1 << 5), 6) * 4096;
+                }
+                return d;
+            case 4:
+                switch (fbits(raw, 11, 10)) {
+                case 0: d.op = OP_c_srli; D_RD(rp1); D_RS1(rp1); d.imm = cimm5 | (cimm1 << 5); return d;
+                case 1: d.op = OP_c_srai; D_RD(rp1); D_RS1(rp1); d.imm = cimm5 | (cimm1 << 5); return d;
+                case 2: d.op = OP_c_andi; D_RD(rp1); D_RS1(rp1); d.imm = fsext(cimm5 | (cimm1 << 5), 6); return d;
+                default: {
+                    const uint32_t f2 = fbits(raw, 6, 5);
+                    if (!cimm1) {
+                        const uint8_t o[4] = {OP_c_sub, OP_c_xor, OP_c_or, OP_c_and};
+                        d.op = o[f2]; D_RD(rp1); D_RS1(rp1); D_RS2(rp2); return d;
+                    }
+                    if (f2 < 3) {
+                        const uint8_t o[3] = {OP_c_subw, OP_c_addw, OP_c_mul};
+                        d.op = o[f2]; D_RD(rp1); D_RS1(rp1); D_RS2(rp2); return d;
+                    }
+                    const uint32_t sel = fbits(raw, 4, 2);
+                    if (sel > 5) return d;
+                    const uint8_t o[6] = {OP_c_zext_b, OP_c_sext_b, OP_c_zext_h, OP_c_sext_h, OP_c_zext_w, OP_c_not};
+                    d.op = o[sel]; D_RD(rp1); D_RS1(rp1); return d;
+                }
+                }
+            case 5:
+                d.op = OP_c_j;
+                d.imm = fsext((fbits(raw, 5, 3) << 1) | (fbits(raw, 11, 11) << 4) | (fbits(raw, 2, 2) << 5) |
+                              (fbits(raw, 7, 7) << 6) | (fbits(raw, 6, 6) << 7) | (fbits(raw, 10, 9) << 8) |
+                              (fbits(raw, 8, 8) << 10) | (fbits(raw, 12, 12) << 11), 12);
+                return d;
+            default:
+                d.op = cop == 6 ? OP_c_beqz : OP_c_bnez; D_RS1(rp1);
+                d.imm = fsext((fbits(cimm5, 2, 1) << 1) | (fbits(cimm3, 1, 0) << 3) | (fbits(cimm5, 0, 0) << 5) |
+                              (fbits(cimm5, 4, 3) << 6) | (fbits(cimm3, 2, 2) << 8), 9);
+                return d;
+            }
+        }
+        switch (cop) {  // q == 2
+        case 0: d.op = OP_c_slli; D_RD(rc1); D_RS1(rc1); d.imm = cimm5 | (cimm1 << 5); return d;
+        case 1: d.op = OP_ESC_FP; return d;
+        case 2: d.op = OP_c_lwsp; D_RD(rc1); D_RS1(2);
+            d.imm = (fbits(cimm5, 4, 2) << 2) | (cimm1 << 5) | (fbits(cimm5, 1, 0) << 6); return d;
+        case 3: d.op = OP_c_ldsp; D_RD(rc1); D_RS1(2);
+            d.imm = (fbits(cimm5, 4, 3) << 3) | (cimm1 << 5) | (fbits(cimm5, 2, 0) << 6); return d;
+        case 4:
+            if (!cimm1) {
+                if (rc2 == 0) { d.op = OP_c_jr; D_RS1(rc1); }
+                else { d.op = OP_c_mv; D_RD(rc1); D_RS2(rc2); }
+            } else if (rc2 == 0) {
+                if (rc1 == 0) d.op = OP_c_ebreak;
+                else { d.op = OP_c_jalr; D_RD(1); D_RS1(rc1); }
+            } else { d.op = OP_c_add; D_RD(rc1); D_RS1(rc1); D_RS2(rc2); }
+            return d;
+        case 5: d.op = OP_ESC_FP; return d;
+        case 6: d.op = OP_c_swsp; D_RS1(2); D_RS2(rc2); d.imm = (fbits(cimm6, 5, 2) << 2) | (fbits(cimm6, 1, 0) << 6); return d;
+        default: d.op = OP_c_sdsp; D_RS1(2); D_RS2(rc2); d.imm = (fbits(cimm6, 5, 3) << 3) | (fbits(cimm6, 2, 0) << 6); return d;
+        }
+    }
+    // 32-bit, decoder.isa:537-6365
+    d.len = 4;
+    const uint32_t opc = fbits(raw, 6, 2), f3 = fbits(raw, 14, 12), f7 = fbits(raw, 31, 25);
+    const uint32_t rd = fbits(raw, 11, 7), rs1 = fbits(raw, 19, 15), rs2 = fbits(raw, 24, 20);
+    const uint32_t fs3 = fbits(raw, 31, 27);
+    const int32_t imm_i = fsext(fbits(raw, 31, 20), 12);
+    const int32_t imm_s = fsext((fbits(raw, 31, 25) << 5) | fbits(raw, 11, 7), 12);
+    const int32_t imm_b = fsext((fbits(raw, 31, 31) << 12) | (fbits(raw, 7, 7) << 11) | (fbits(raw, 30, 25) << 5) |
+                                (fbits(raw, 11, 8) << 1), 13);
+    const int32_t imm_j = fsext((fbits(raw, 31, 31) << 20) | (fbits(raw, 19, 12) << 12) | (fbits(raw, 20, 20) << 11) |
+                                (fbits(raw, 30, 21) << 1), 21);
+    const int32_t imm_u = (int32_t)(raw & 0xFFFFF000u);
+    const uint32_t sh6 = fbits(raw, 25, 20), sh5 = fbits(raw, 24, 20);
+    d.aux = (uint16_t)f3;
+#define RI(o, im) do { d.op = (o); D_RD(rd); D_RS1(rs1); d.imm = (im); return d; } while (0)
+#define RR(o) do { d.op = (o); D_RD(rd); D_RS1(rs1); D_RS2(rs2); return d; } while (0)
+    switch (opc) {
+    case 0x00: {  // LOAD :538-566
+        if (f3 == 7) return d;
+        const uint8_t o[7] = {OP_lb, OP_lh, OP_lw, OP_ld, OP_lbu, OP_lhu, OP_lwu};
+        RI(o[f3], imm_i);
+    }
+    case 0x01: d.op = OP_ESC_FP; return d;
+    case 0x03:  // MISC-MEM :1336-1433
+        if (f3 == 0) { d.op = OP_fence; return d; }
+        if (f3 == 1) { d.op = OP_fence_i; return d; }
+        if (f3 == 2 && rd == 0) {
+            const uint32_t f12 = fbits(raw, 31, 20);
+            if (f12 == 0 || f12 == 1 || f12 == 2 || f12 == 4) d.op = OP_ESC_CBO;
+        }
+        return d;
+    case 0x04:  // OP-IMM :1435-1670
+        switch (f3) {
+        case 0: RI(OP_addi, imm_i);
+        case 1:
+            if (fs3 == 0x00) RI(OP_slli, sh6);
+            if (fs3 == 0x02 && rs2 <= 9) { d.op = OP_ESC_CRYPTO; return d; }
+            if (fs3 == 0x05) RI(OP_bseti, sh6);
+            if (fs3 == 0x06) { d.op = OP_ESC_CRYPTO; return d; }
+            if (fs3 == 0x09) RI(OP_bclri, sh6);
+            if (fs3 == 0x0d) RI(OP_binvi, sh6);
+            if (fs3 == 0x0c) {
+                if (rs2 == 0) RI(OP_clz, 0);
+                if (rs2 == 1) RI(OP_ctz, 0);
+                if (rs2 == 2) RI(OP_cpop, 0);
+                if (rs2 == 4) RI(OP_sext_b, 0);
+                if (rs2 == 5) RI(OP_sext_h, 0);
+            }
+            return d;
+        case 2: RI(OP_slti, imm_i);
+        case 3: RI(OP_sltiu, imm_i);
+        case 4: RI(OP_xori, imm_i);
+        case 5:
+            if (fs3 == 0x0) RI(OP_srli, sh6);
+            if (fs3 == 0x5) RI(OP_orc_b, sh6);
+            if (fs3 == 0x8) RI(OP_srai, sh6);
+            if (fs3 == 0x9) RI(OP_bexti, sh6);
+            if (fs3 == 0xc) RI(OP_rori, sh6);
+            if (fs3 == 0xd && rs2 == 0x18) RI(OP_rev8, 0);
+            if (fs3 == 0xd && rs2 == 0x07) { d.op = OP_ESC_CRYPTO; return d; }
+            return d;
+        case 6:
+            if (rd == 0) {
+                if (rs2 == 0 || rs2 == 1 || rs2 == 3) {
+                    d.op = rs2 == 0 ? OP_prefetch_i : rs2 == 1 ? OP_prefetch_r : OP_prefetch_w;
+                    D_RS1(rs1); d.imm = (int32_t)(fbits(raw, 31, 25) << 5);
+                    return d;
+                }
+                RI(OP_ori_hint, imm_i);
+            }
+            RI(OP_ori, imm_i);
+        default: RI(OP_andi, imm_i);
+        }
+    case 0x05: d.op = OP_auipc; D_RD(rd); d.imm = imm_u; return d;
+    case 0x06:  // OP-IMM-32 :1676-1720
+        if (f3 == 0) RI(OP_addiw, imm_i);
+        if (f3 == 1) {
+            if (fs3 == 0x0) RI(OP_slliw, sh5);
+            if (fs3 == 0x1) RI(OP_slli_uw, sh6);
+            if (fs3 == 0xc && rs2 == 0) RI(OP_clzw, 0);
+            if (fs3 == 0xc && rs2 == 1) RI(OP_ctzw, 0);
+            if (fs3 == 0xc && rs2 == 2) RI(OP_cpopw, 0);
+        }
+        if (f3 == 5) {
+            if (fs3 == 0x0) RI(OP_srliw, sh5);
+            if (fs3 == 0x8) RI(OP_sraiw, sh5);
+            if (fs3 == 0xc) RI(OP_roriw, sh5);
+        }
+        return d;
+    case 0x08: {  // STORE :1722-1739
+        if (f3 > 3) return d;
+        const uint8_t o[4] = {OP_sb, OP_sh, OP_sw, OP_sd};
+        d.op = o[f3]; D_RS1(rs1); D_RS2(rs2); d.imm = imm_s; return d;
+    }
+    case 0x09: d.op = OP_ESC_FP; return d;
+    case 0x0b: d.op = OP_ESC_AMO; return d;
+    case 0x0c: {  // OP :2285-2613
+        const uint32_t kf5 = fbits(raw, 29, 25), bs = fbits(raw, 31, 30);
+        switch (f3) {
+        case 0:
+            if (kf5 == 0x00 && bs == 0) RR(OP_add);
+            if (kf5 == 0x00 && bs == 1) RR(OP_sub);
+            if (kf5 == 0x01 && bs == 0) RR(OP_mul);
+            if (kf5 == 0x18 || kf5 == 0x1a) { d.op = OP_ESC_CRYPTO; return d; }
+            if ((kf5 == 0x19 || kf5 == 0x1b || kf5 == 0x1d) && bs == 0) { d.op = OP_ESC_CRYPTO; return d; }
+            if (kf5 == 0x1f && bs <= 1) { d.op = OP_ESC_CRYPTO; return d; }
+            return d;
+        case 1:
+            switch (f7) {
+            case 0x00: RR(OP_sll); case 0x01: RR(OP_mulh); case 0x05: RR(OP_clmul); case 0x14: RR(OP_bset);
+            case 0x24: RR(OP_bclr); case 0x30: RR(OP_rol); case 0x34: RR(OP_binv);
+            }
+            return d;
+        case 2:
+            switch (f7) {
+            case 0x00: RR(OP_slt); case 0x01: RR(OP_mulhsu); case 0x05: RR(OP_clmulr); case 0x10: RR(OP_sh1add);
+            case 0x14: d.op = OP_ESC_CRYPTO; return d;
+            }
+            return d;
+        case 3:
+            switch (f7) { case 0x00: RR(OP_sltu); case 0x01: RR(OP_mulhu); case 0x05: RR(OP_clmulh); }
+            return d;
+        case 4:
+            switch (f7) {
+            case 0x00: RR(OP_xor_); case 0x01: RR(OP_div_); case 0x04: RR(OP_pack); case 0x05: RR(OP_min_);
+            case 0x10: RR(OP_sh2add); case 0x14: d.op = OP_ESC_CRYPTO; return d; case 0x20: RR(OP_xnor);
+            }
+            return d;
+        case 5:
+            switch (f7) {
+            case 0x00: RR(OP_srl); case 0x01: RR(OP_divu); case 0x07: RR(OP_czero_eqz); case 0x20: RR(OP_sra);
+            case 0x05: RR(OP_minu); case 0x24: RR(OP_bext); case 0x30: RR(OP_ror);
+            }
+            return d;
+        case 6:
+            switch (f7) {
+            case 0x00: RR(OP_or_); case 0x01: RR(OP_rem); case 0x05: RR(OP_max_); case 0x10: RR(OP_sh3add);
+            case 0x20: RR(OP_orn);
+            }
+            return d;
+        default:
+            switch (f7) {
+            case 0x00: RR(OP_and_); case 0x01: RR(OP_remu); case 0x04: RR(OP_packh); case 0x05: RR(OP_maxu);
+            case 0x07: RR(OP_czero_nez); case 0x20: RR(OP_andn);
+            }
+            return d;
+        }
+    }
+    case 0x0d: d.op = OP_lui; D_RD(rd); d.imm = imm_u; return d;
+    case 0x0e:  // OP-32 :2620-2692
+        switch (f3) {
+        case 0: switch (f7) { case 0x00: RR(OP_addw); case 0x01: RR(OP_mulw); case 0x04: RR(OP_add_uw); case 0x20: RR(OP_subw); } return d;
+        case 1: switch (f7) { case 0x00: RR(OP_sllw); case 0x30: RR(OP_rolw); } return d;
+        case 2: if (f7 == 0x10) RR(OP_sh1add_uw); return d;
+        case 4: switch (f7) { case 0x01: RR(OP_divw); case 0x04: RR(OP_packw); case 0x10: RR(OP_sh2add_uw); } return d;
+        case 5: switch (f7) { case 0x00: RR(OP_srlw); case 0x01: RR(OP_divuw); case 0x20: RR(OP_sraw); case 0x30: RR(OP_rorw); } return d;
+        case 6: switch (f7) { case 0x01: RR(OP_remw); case 0x10: RR(OP_sh3add_uw); } return d;
+        case 7: RR(OP_remuw);   // decoded on FUNCT3 alone (:2687-2689)
+        default: return d;
+        }
+    case 0x10: case 0x11: case 0x12: case 0x13: case 0x14: d.op = OP_ESC_FP; return d;
+    case 0x15: d.op = OP_ESC_VEC; return d;
+    case 0x18: {  // BRANCH :5891-5936
+        if (f3 == 2 || f3 == 3) return d;
+        const uint8_t o[8] = {OP_beq, OP_bne, 0, 0, OP_blt, OP_bge, OP_bltu, OP_bgeu};
+        d.op = o[f3]; D_RS1(rs1); D_RS2(rs2); d.imm = imm_b; return d;
+    }
+    case 0x19: if (f3 == 0) RI(OP_jalr, imm_i); return d;   // :5938-5943
+    case 0x1b: d.op = OP_jal; D_RD(rd); d.imm = imm_j; return d;
+    case 0x1c:  // SYSTEM :5950-6300
+        if (f3 == 0) {
+            if (f7 == 0) {
+                if (rs2 == 0) d.op = OP_ecall;
+                else if (rs2 == 1) d.op = OP_ebreak;
+                return d;
+            }
+            d.op = OP_ESC_SYS; return d;
+        }
+        if (f3 == 4) { d.op = OP_ESC_HYP; return d; }
+        d.op = OP_csr; D_RD(rd);
+        if (f3 < 5) D_RS1(rs1);
+        d.imm = (int32_t)rs1; d.aux = (uint16_t)fbits(raw, 31, 20);
+        return d;
+    case 0x1e: d.op = OP_ESC_M5; return d;
+    default: return d;
+    }
+#undef RI
+#undef RR
+}
+#undef D_RD
+#undef D_RS1
+#undef D_RS2
+
+}  // namespace fi

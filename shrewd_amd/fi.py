@@ -1,0 +1,262 @@
+"""Host-side mirror of the gem5 `FaultCampaign` SimObject over the C ABI.
+
+`FaultCampaign` keeps the parameter names and meaning of the SimObject
+declared in src/gem5ext/FaultCampaign.py (a gem5 SimObject in the style of
+src/cpu/o3/BaseO3CPU.py:64-72,226-227 of the reference) so a config script can
+drive the engine with or without gem5 present.  Every call goes to
+libshrewd_fi.so (HIP kernels); there is no CPU execution path -- when no
+MI355X is visible the engine refuses to start (FI_E_NODEVICE).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import build as _build
+
+FI_OK, FI_E_ARG, FI_E_NODEVICE, FI_E_HIP, FI_E_ELF, FI_E_STATE, FI_E_GOLDEN = 0, -1, -2, -3, -4, -5, -6
+CLASS_NAMES = ["masked", "sdc", "crash", "hang", "detected", "escape"]
+CRASH_NAMES = {1: "panic_unknown_inst", 2: "panic_illegal_inst", 3: "panic_page_fault",
+               4: "fatal_syscall_range", 5: "fatal_syscall_unimpl", 6: "fatal_proxy", 7: "abort_fd_assert",
+               8: "sigtrap", 9: "fatal_stack_limit"}
+ESCAPE_NAMES = {1: "inst", 2: "syscall", 3: "csr", 4: "host", 5: "resource"}
+T_PC, T_MEM, N_STRUCT = 32, 33, 34
+
+OUTCOME_DT = np.dtype([("cls", "u1"), ("sub", "u1"), ("exit_code", "u1"), ("flags", "u1"),
+                       ("detail", "<u4"), ("ninst", "<u8")])
+SITE_DT = np.dtype([("inst", "<u8"), ("mask", "<u8"), ("addr", "<u8"), ("target", "<u4"), ("trial", "<u4")])
+HIST_DT = np.dtype([("counts", "<u8", (N_STRUCT, 64, 6)), ("crash_sub", "<u8", (16,)), ("escape_sub", "<u8", (8,)),
+                    ("trials", "<u8"), ("guest_insts", "<u8"), ("fetch_bytes", "<u8"), ("data_bytes", "<u8"),
+                    ("cow_pages", "<u8")])
+
+ABI_NAMES = {"zero": 0, "ra": 1, "sp": 2, "gp": 3, "tp": 4, "t0": 5, "t1": 6, "t2": 7, "s0": 8, "fp": 8, "s1": 9,
+             **{f"a{i}": 10 + i for i in range(8)}, **{f"s{i}": 16 + i for i in range(2, 12)},
+             "t3": 28, "t4": 29, "t5": 30, "t6": 31}
+
+
+def structures_mask(structures: Iterable[str] | int) -> int:
+    """'int_reg' (x1..x31), 'pc', 'mem', or register names ('x5', 'a0', 'sp') -> bitmask."""
+    if isinstance(structures, int):
+        return structures
+    m = 0
+    for s in structures:
+        s = s.strip().lower()
+        if s in ("int_reg", "intreg", "regs", "regfile"):
+            m |= ((1 << 32) - 1) & ~1
+        elif s == "pc":
+            m |= 1 << T_PC
+        elif s in ("mem", "memory"):
+            m |= 1 << T_MEM
+        elif s in ABI_NAMES:
+            m |= 1 << ABI_NAMES[s]
+        elif s.startswith("x") and s[1:].isdigit() and 0 <= int(s[1:]) < 32:
+            m |= 1 << int(s[1:])
+        else:
+            raise ValueError(f"unknown fault structure {s!r}")
+    return m & ~1
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class _Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("private_pages", C.c_uint32), ("hang_factor_x16", C.c_uint32),
+                ("max_trials_per_launch", C.c_uint32)]
+
+
+class GoldenInfo(C.Structure):
+    _fields_ = [("ninst", C.c_uint64), ("ncycles", C.c_uint64), ("exit_code", C.c_uint32), ("pad", C.c_uint32),
+                ("stdout_len", C.c_uint64), ("stderr_len", C.c_uint64), ("fetch_bytes", C.c_uint64),
+                ("data_bytes", C.c_uint64)]
+
+
+_lib = None
+
+
+def library_path() -> str:
+    return _build.OUT
+
+
+def build_library(force: bool = False) -> str:
+    return _build.build(force=force)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        path = library_path()
+        if not os.path.exists(path):
+            raise EngineError(f"{path} missing: run `python -m shrewd_amd.build` (hipcc, gfx950)")
+        L = C.CDLL(path)
+        vp = C.c_void_p
+        L.fi_create.argtypes = [C.POINTER(_Config), C.POINTER(vp)]
+        L.fi_destroy.argtypes = [vp]
+        L.fi_last_error.restype = C.c_char_p
+        L.fi_last_error.argtypes = [vp]
+        L.fi_load_elf.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]
+        L.fi_golden_run.argtypes = [vp, C.POINTER(GoldenInfo)]
+        L.fi_golden_stdout.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.fi_set_campaign.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32]
+        L.fi_set_protect.argtypes = [vp, C.c_uint64]
+        L.fi_sample_sites.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
+        L.fi_run_trials.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp]
+        L.fi_run_sites.argtypes = [vp, vp, C.c_uint64, vp, vp]
+        L.fi_run_trials_device.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp, vp]
+        L.fi_sync.argtypes = [vp]
+        L.fi_last_kernel_ms.restype = C.c_double
+        L.fi_last_kernel_ms.argtypes = [vp]
+        L.fi_debug_decode.argtypes = [vp, vp, C.c_uint64, vp]
+        _lib = L
+    return _lib
+
+
+def _cstrs(items: Sequence[str] | None):
+    items = list(items or [])
+    arr = (C.c_char_p * (len(items) + 1))()
+    for i, s in enumerate(items):
+        arr[i] = s.encode()
+    arr[len(items)] = None
+    return arr
+
+
+class Engine:
+    """Thin RAII wrapper of one fi_engine (one HIP device)."""
+
+    def __init__(self, device: int = 0, private_pages: int = 16, hang_factor_x16: int = 32,
+                 max_trials_per_launch: int = 65536):
+        self.L = lib()
+        cfg = _Config(device, private_pages, hang_factor_x16, max_trials_per_launch)
+        h = C.c_void_p()
+        st = self.L.fi_create(C.byref(cfg), C.byref(h))
+        if st == FI_E_NODEVICE:
+            raise EngineError("no HIP device visible: the engine has no CPU path")
+        if st != FI_OK:
+            raise EngineError(f"fi_create failed ({st})")
+        self.h = h
+        self.golden: GoldenInfo | None = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.fi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def _chk(self, st: int, what: str):
+        if st != FI_OK:
+            raise EngineError(f"{what}: {self.L.fi_last_error(self.h).decode()} ({st})")
+
+    def load_elf(self, elf: bytes, argv: Sequence[str], envp: Sequence[str] | None = None):
+        self._chk(self.L.fi_load_elf(self.h, elf, len(elf), _cstrs(argv), _cstrs(envp)), "fi_load_elf")
+
+    def golden_run(self) -> GoldenInfo:
+        g = GoldenInfo()
+        self._chk(self.L.fi_golden_run(self.h, C.byref(g)), "fi_golden_run")
+        self.golden = g
+        return g
+
+    def golden_stdout(self) -> bytes:
+        n = C.c_uint64()
+        buf = C.create_string_buffer(1 << 20)
+        self._chk(self.L.fi_golden_stdout(self.h, buf, 1 << 20, C.byref(n)), "fi_golden_stdout")
+        return buf.raw[:n.value]
+
+    def set_campaign(self, seed: int, structures, burst: int = 1):
+        self._chk(self.L.fi_set_campaign(self.h, seed & (2**64 - 1), structures_mask(structures), burst),
+                  "fi_set_campaign")
+
+    def set_protect(self, mask: int):
+        self._chk(self.L.fi_set_protect(self.h, mask), "fi_set_protect")
+
+    def sample(self, first: int, n: int) -> np.ndarray:
+        out = np.zeros(n, SITE_DT)
+        self._chk(self.L.fi_sample_sites(self.h, first, n, out.ctypes.data), "fi_sample_sites")
+        return out
+
+    def run_trials(self, first: int, n: int, want_outcomes: bool = True):
+        out = np.zeros(n, OUTCOME_DT) if want_outcomes else None
+        hist = np.zeros(1, HIST_DT)
+        self._chk(self.L.fi_run_trials(self.h, first, n, out.ctypes.data if out is not None else None,
+                                       hist.ctypes.data), "fi_run_trials")
+        return out, hist[0]
+
+    def run_sites(self, sites: np.ndarray):
+        sites = np.ascontiguousarray(sites, SITE_DT)
+        out = np.zeros(len(sites), OUTCOME_DT)
+        hist = np.zeros(1, HIST_DT)
+        self._chk(self.L.fi_run_sites(self.h, sites.ctypes.data, len(sites), out.ctypes.data, hist.ctypes.data),
+                  "fi_run_sites")
+        return out, hist[0]
+
+    def run_trials_device(self, first: int, n: int, d_out: int, d_hist: int, stream: int | None = None):
+        self._chk(self.L.fi_run_trials_device(self.h, first, n, d_out, d_hist, stream), "fi_run_trials_device")
+
+    def sync(self):
+        self._chk(self.L.fi_sync(self.h), "fi_sync")
+
+    def last_kernel_ms(self) -> float:
+        return self.L.fi_last_kernel_ms(self.h)
+
+    def debug_decode(self, raws: np.ndarray) -> np.ndarray:
+        raws = np.ascontiguousarray(raws, np.uint32)
+        dt = np.dtype([("raw", "<u4"), ("op", "u1"), ("rd", "u1"), ("rs1", "u1"), ("rs2", "u1"), ("imm", "<i4"),
+                       ("len", "u1"), ("flags", "u1"), ("aux", "<u2")])
+        out = np.zeros(len(raws), dt)
+        self._chk(self.L.fi_debug_decode(self.h, raws.ctypes.data, len(raws), out.ctypes.data), "fi_debug_decode")
+        return out
+
+
+class FaultCampaign:
+    """Mirror of the gem5 `FaultCampaign` SimObject (src/gem5ext/FaultCampaign.py).
+
+    Params (same names/meaning as the SimObject): workload (binary path), cmd
+    (argv, cmd[0] defaults to workload), env, trials, seed, structures,
+    burst, protect_mask, num_gpus, max_insts_factor, output.
+    """
+
+    def __init__(self, workload: str, cmd: Sequence[str] | None = None, env: Sequence[str] | None = None,
+                 trials: int = 1000, seed: int = 0x5EED0001, structures=("int_reg",), burst: int = 1,
+                 protect_mask: int = 0, num_gpus: int = 1, max_insts_factor: float = 2.0, output: str = "",
+                 device: int = 0, private_pages: int = 16):
+        self.workload, self.cmd, self.env = workload, list(cmd or [workload]), list(env or [])
+        self.trials, self.seed, self.structures, self.burst = trials, seed, structures, burst
+        self.protect_mask, self.num_gpus, self.output = protect_mask, num_gpus, output
+        self.max_insts_factor = max_insts_factor
+        self.engine = Engine(device=device, private_pages=private_pages,
+                             hang_factor_x16=max(1, int(round(max_insts_factor * 16))))
+        with open(workload, "rb") as f:
+            self.engine.load_elf(f.read(), self.cmd, self.env)
+        self.golden = self.engine.golden_run()
+        self.engine.set_campaign(seed, structures, burst)
+        self.engine.set_protect(protect_mask)
+        self._hist = None
+        self.outcomes = None
+
+    # PyBindMethod("setProtectMask") analogue of setEnableShrewd (BaseO3CPU.py:69-72)
+    def setProtectMask(self, mask: int):
+        self.protect_mask = mask
+        self.engine.set_protect(mask)
+
+    def run(self, first_trial: int = 0, n: int | None = None):
+        n = self.trials if n is None else n
+        self.outcomes, self._hist = self.engine.run_trials(first_trial, n)
+        if self.output:
+            np.save(self.output, self.outcomes)
+        return self.outcomes
+
+    def histogram(self):
+        return self._hist
+
+    def summary(self) -> dict:
+        h = self._hist
+        cls = h["counts"].sum(axis=(0, 1))
+        return {"trials": int(h["trials"]), **{CLASS_NAMES[i]: int(cls[i]) for i in range(6)},
+                "crash": {CRASH_NAMES.get(i, str(i)): int(h["crash_sub"][i]) for i in range(16) if h["crash_sub"][i]},
+                "escape": {ESCAPE_NAMES.get(i, str(i)): int(h["escape_sub"][i]) for i in range(8)
+                           if h["escape_sub"][i]},
+                "guest_insts": int(h["guest_insts"])}

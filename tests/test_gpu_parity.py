@@ -1,0 +1,166 @@
+"""GPU parity: the HIP engine against the oracle, through the C ABI.
+
+Bar: bit-exact per-trial outcomes (class, sub-code, exit code, flags, detail,
+committed-instruction count) on the same seeded sites.
+"""
+import numpy as np
+import pytest
+
+from conftest import WORKLOADS, workload_elf
+
+pytestmark = pytest.mark.gpu
+
+REGS = (1 << 32) - 2
+PC = 1 << 32
+MEM = 1 << 33
+
+
+def oracle_for(oracle_mod, name, argv0=None):
+    o = oracle_mod.Oracle(workload_elf(name), argv0 or name)
+    o.run_golden()
+    return o
+
+
+def compare(dev, ref, sites):
+    bad = np.nonzero(dev != ref)[0]
+    if len(bad):
+        i = bad[0]
+        raise AssertionError(f"{len(bad)} of {len(sites)} outcomes differ; first: site={sites[i]} "
+                             f"gpu={dev[i]} oracle={ref[i]}")
+
+
+def test_decode_parity_compressed(engine_factory, oracle_mod):
+    e = engine_factory("hello")
+    raws = np.arange(0x10000, dtype=np.uint32)
+    raws = raws[(raws & 3) != 3]
+    d = e.debug_decode(raws)
+    names = [oracle_mod.mnemonic(int(r)) for r in raws]
+    _check_decode(d, raws, names, oracle_mod)
+
+
+def test_decode_parity_32bit(engine_factory, oracle_mod):
+    e = engine_factory("hello")
+    rng = np.random.default_rng(1)
+    raws = (rng.integers(0, 2**32, 200000, dtype=np.uint64).astype(np.uint32) | 3)
+    d = e.debug_decode(raws)
+    names = [oracle_mod.mnemonic(int(r)) for r in raws]
+    _check_decode(d, raws, names, oracle_mod)
+
+
+def _check_decode(d, raws, names, oracle_mod):
+    # device op ids share the oracle's op list order; compare through the
+    # oracle probe (op id, rd, len) for every encoding
+    for i in range(0, len(raws), max(1, len(raws) // 20000)):
+        p = oracle_mod.probe(int(raws[i]), 0x10000, [0] * 32)
+        assert d["op"][i] == p.op, (hex(int(raws[i])), names[i], int(d["op"][i]), p.op)
+        assert d["len"][i] == p.len
+        if p.rd > 0:
+            assert d["rd"][i] == p.rd, (hex(int(raws[i])), names[i])
+
+
+@pytest.mark.parametrize("name", WORKLOADS)
+def test_golden_run_matches_oracle(engine_factory, oracle_mod, name):
+    e = engine_factory(name)
+    o = oracle_for(oracle_mod, name)
+    g, og = e.golden, o.golden
+    assert (g.ninst, g.ncycles, g.exit_code) == (og.ninst, og.ncycles, og.exit_code)
+    assert e.golden_stdout() == o.golden_stdout()
+
+
+@pytest.mark.parametrize("name", ["crc32", "qsort"])
+def test_sampler_matches_oracle(engine_factory, oracle_mod, name):
+    e = engine_factory(name)
+    o = oracle_for(oracle_mod, name)
+    for structs, burst in ((REGS | PC, 1), (MEM, 1), (MEM, 4), (REGS | PC | MEM, 8)):
+        e.set_campaign(0xABCDEF, structs, burst)
+        dev = e.sample(1000, 3000)
+        ref = o.sample(0xABCDEF, 1000, 3000, structs, burst)
+        assert np.array_equal(dev, ref)
+
+
+@pytest.mark.parametrize("name,structs,burst,n", [
+    ("hello", REGS | PC, 1, 1000),        # C1: 1k regfile flips
+    ("crc32", REGS | PC, 1, 6000),        # C2 (sampled)
+    ("qsort", REGS | PC, 1, 6000),        # C2 (sampled)
+    ("crc32", MEM, 1, 3000),              # C4 memory words
+    ("qsort", MEM, 4, 3000),              # C4 bursts
+    ("qsort", REGS | PC | MEM, 8, 2000),
+    ("intmix", REGS | PC, 1, 600),        # C3 kernel (sampled)
+])
+def test_trials_bit_exact(engine_factory, oracle_mod, name, structs, burst, n):
+    e = engine_factory(name)
+    o = oracle_for(oracle_mod, name)
+    e.set_campaign(0x5EED0001 + n, structs, burst)
+    e.set_protect(0)
+    sites = e.sample(0, n)
+    dev, hist = e.run_sites(sites)
+    ref = o.run_trials(sites, protect_mask=0)
+    compare(dev, ref, sites)
+    assert int(hist["trials"]) == n
+    assert int(hist["counts"].sum()) == n
+
+
+@pytest.mark.parametrize("mask", [0, (1 << 1) | (1 << 2) | (1 << 3) | (1 << 4),
+                                  sum(1 << r for r in range(10, 18)), (1 << 32) - 2 | (1 << 32)])
+def test_protect_mask_bit_exact(engine_factory, oracle_mod, mask):
+    """C5: selective-replication sweep -- detected-by-replica classification."""
+    e = engine_factory("crc32")
+    o = oracle_for(oracle_mod, "crc32")
+    e.set_campaign(99, REGS | PC, 1)
+    e.set_protect(mask)
+    sites = e.sample(0, 3000)
+    dev, hist = e.run_sites(sites)
+    ref = o.run_trials(sites, protect_mask=mask)
+    e.set_protect(0)
+    compare(dev, ref, sites)
+    if mask:
+        assert (dev["cls"] == 4).sum() > 0
+
+
+def test_run_trials_equals_run_sites(engine_factory):
+    e = engine_factory("crc32")
+    e.set_campaign(4242, REGS | PC, 1)
+    out1, h1 = e.run_trials(100, 5000)
+    sites = e.sample(100, 5000)
+    out2, h2 = e.run_sites(sites)
+    assert np.array_equal(out1, out2)
+    assert np.array_equal(h1["counts"], h2["counts"])
+
+
+def test_chunking_invariance(engine_factory):
+    """Launch size must not change any outcome (shard invariance)."""
+    small = engine_factory("qsort", max_trials_per_launch=1000)
+    big = engine_factory("qsort")
+    for e in (small, big):
+        e.set_campaign(77, REGS | PC | MEM, 2)
+    a, ha = small.run_trials(0, 5000)
+    b, hb = big.run_trials(0, 5000)
+    assert np.array_equal(a, b)
+    assert np.array_equal(ha["counts"], hb["counts"])
+
+
+def test_argv_shapes_stack(engine_factory, oracle_mod):
+    """argv[0] length moves sp (argsInit); golden + trials still agree."""
+    e = engine_factory("crc32", argv0="/some/much/longer/path/to/crc32")
+    o = oracle_for(oracle_mod, "crc32", "/some/much/longer/path/to/crc32")
+    e.set_campaign(5, REGS | PC | MEM, 1)
+    sites = e.sample(0, 2000)
+    dev, _ = e.run_sites(sites)
+    compare(dev, o.run_trials(sites), sites)
+
+
+def test_full_size_properties(engine_factory):
+    """C2 at full size (100k trials): size-independent properties."""
+    e = engine_factory("crc32")
+    e.set_campaign(0x5EED0002, REGS | PC, 1)
+    out, h = e.run_trials(0, 100_000)
+    g = e.golden
+    assert int(h["trials"]) == 100_000
+    assert int(h["guest_insts"]) == int(out["ninst"].sum())
+    cls = np.bincount(out["cls"], minlength=6)
+    assert cls[0] > 50_000 and cls[2] > 0
+    masked = out[out["cls"] == 0]
+    assert (masked["exit_code"] == g.exit_code).all()
+    # flips of x0..: the PC-flip crash share is large, register flips mostly masked
+    out2, _ = e.run_trials(0, 100_000)
+    assert np.array_equal(out, out2)   # deterministic
