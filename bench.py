@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""bench.py -- fault-injection campaign throughput on MI355X.
+
+Metric (BASELINE.json): fault-injection trials/sec (whole node) and guest
+inst/sec.  Workload (configs[1]): the RV64 MiBench-style CRC32 kernel,
+100k register-file + PC single-bit trials per GPU, seeded sites.
+
+One step = one campaign pass over a batch of `--trials` trials per GPU:
+device-side site sampling, sort by inject time, the interpreter kernel (all
+trials from process start to exit/crash/hang), outcome histogram, and the
+RCCL all-reduce of the histogram (the campaign's only exchange; N > 1).
+Trials shard by id across ranks (weak scaling: per-GPU work fixed).
+
+Launch: python bench.py [--gpus 1] [--steps 5] [--warmup 1]
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+REGS_PC = ((1 << 32) - 2) | (1 << 32)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="crc32")
+    ap.add_argument("--trials", type=int, default=100_000, help="trials per GPU per step")
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(elf: bytes, argv0: str, seed: int, budget_s: float):
+    """The oracle (plain-C restatement of gem5 RV64 SE, test infrastructure)
+    on the host cores, same campaign, bounded sample."""
+    from oracle.pyoracle import Oracle
+    threads = max(1, min(16, os.cpu_count() or 1))
+    o = Oracle(elf, argv0)
+    o.run_golden()
+    calib = o.sample(seed, 0, 64 * threads, REGS_PC, 1)
+    t0 = time.perf_counter()
+    o.run_trials(calib, threads=threads)
+    dt = max(time.perf_counter() - t0, 1e-3)
+    n = int(min(2_000_000, max(len(calib), len(calib) * budget_s / dt)))
+    sites = o.sample(seed, 0, n, REGS_PC, 1)
+    t0 = time.perf_counter()
+    out = o.run_trials(sites, threads=threads)
+    dt = time.perf_counter() - t0
+    insts = int(out["ninst"].sum())
+    o.close()
+    return {"value": n / dt, "unit": "trials/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} trials of the same {argv0} campaign (seed {seed:#x}, regs+pc), "
+                      f"oracle/rv64se.c with {threads} pthreads, {dt:.1f}s wall",
+            "guest_inst_per_s": insts / dt}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from shrewd_amd import HIST_DT, Engine
+    with open(os.path.join(ROOT, "workloads", f"{a.workload}.elf"), "rb") as f:
+        elf = f.read()
+    eng = Engine(device=local, max_trials_per_launch=max(a.trials, 1024))
+    t0 = time.perf_counter()
+    eng.load_elf(elf, [a.workload])
+    g = eng.golden_run()
+    golden_s = time.perf_counter() - t0
+    eng.set_campaign(a.seed, REGS_PC, 1)
+
+    T = a.trials
+    d_out = torch.empty(T * 16, dtype=torch.uint8, device=dev)
+    hist_words = HIST_DT.itemsize // 8
+    d_hist = torch.zeros(hist_words, dtype=torch.int64, device=dev)
+    d_hist_node = torch.zeros_like(d_hist)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        d_hist.zero_()
+        eng.run_trials_device(rank * T, T, d_out.data_ptr(), d_hist.data_ptr(), stream)
+        d_hist_node.copy_(d_hist)
+        if world > 1:
+            dist.all_reduce(d_hist_node)      # RCCL over xGMI: outcome histogram only
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    eng.kernel_timer_reset()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms, launches = eng.kernel_timer_read()
+
+    local_h = np.frombuffer(d_hist.cpu().numpy().tobytes(), HIST_DT)[0]
+    node_h = np.frombuffer(d_hist_node.cpu().numpy().tobytes(), HIST_DT)[0]
+
+    if rank == 0:
+        trials_total = world * T * a.steps
+        value = trials_total / elapsed
+        guest_ips = int(node_h["guest_insts"]) * a.steps / elapsed
+        # roofline of the dominant kernel (fi_trial_kernel), per launch:
+        # algorithmic bytes = fetched instruction bytes + load/store bytes of all
+        # executed guest instructions + 264 B initial state + 16 B outcome per
+        # trial + 4096 B per copy-on-write page
+        per_launch_bytes = (int(local_h["fetch_bytes"]) + int(local_h["data_bytes"]) + T * (264 + 16)
+                            + 4096 * int(local_h["cow_pages"]))
+        avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
+        achieved = per_launch_bytes / avg_kernel_s / 1e9
+        traffic = None
+        if os.path.exists(a.traffic_json):
+            try:
+                with open(a.traffic_json) as f:
+                    tj = json.load(f)
+                if tj.get("workload") == a.workload and tj.get("trials") == T:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        cls = node_h["counts"].sum(axis=(0, 1))
+        res = {
+            "metric": "fault-injection trials/sec (whole node)",
+            "value": value,
+            "unit": "trials/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (seeded SplitMix64 fault sites over a hand-assembled RV64 ELF)",
+            "config": {"workload": f"{a.workload} (RV64 MiBench-style, {g.ninst} golden insts), "
+                                   f"{T} single-bit x1..x31+pc trials per GPU per step",
+                       "trials_per_gpu": T, "seed": hex(a.seed), "structures": "x1-x31,pc", "burst": 1,
+                       "parallelism": f"trial-sharded x{world}, RCCL histogram all-reduce"},
+            "guest_inst_per_s": guest_ips,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "fi_trial_kernel", "avg_kernel_ms": avg_kernel_s * 1e3,
+                         "algorithmic_bytes_per_launch": per_launch_bytes},
+            "outcomes": {n: int(cls[i]) for i, n in enumerate(["masked", "sdc", "crash", "hang", "detected",
+                                                                 "escape"])},
+            "golden_s": golden_s,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(elf, a.workload, a.seed, a.cpu_seconds)
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -159,6 +159,10 @@ fi_status fi_sync(fi_engine *e);
 /* Timing of the last fi_run_* call's interpreter kernel(s), measured with
  * hipEvents on the engine stream (milliseconds). */
 double fi_last_kernel_ms(fi_engine *e);
+/* Accumulating per-launch timer of the interpreter kernel (HIP event pairs
+ * recorded on the launch stream around every fi_trial_kernel launch). */
+fi_status fi_kernel_timer_reset(fi_engine *e);
+fi_status fi_kernel_timer_read(fi_engine *e, double *total_ms, uint32_t *launches);
 
 #ifdef __cplusplus
 }

@@ -42,6 +42,9 @@ struct fi_engine {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_ms = 0;
+    // per-launch timing of the interpreter kernel (bench roofline)
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> tpool;
+    size_t tused = 0;
 
     // process image (host copy)
     bool loaded = false;
@@ -144,6 +147,7 @@ void fi_destroy(fi_engine *e) {
     (void)hipSetDevice(e->dev);
     free_work(e);
     free_image(e);
+    for (auto &tp : e->tpool) { (void)hipEventDestroy(tp.first); (void)hipEventDestroy(tp.second); }
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -486,8 +490,17 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     c.out = d_out;
     c.n = k;
     HIPCHK(hipMemsetAsync(e->d_stats, 0, 8 * sizeof(unsigned long long), st));
+    if (e->tused == e->tpool.size()) {
+        hipEvent_t a, b;
+        HIPCHK(hipEventCreate(&a));
+        HIPCHK(hipEventCreate(&b));
+        e->tpool.emplace_back(a, b);
+    }
+    auto &tp = e->tpool[e->tused++];
     HIPCHK(hipEventRecord(e->ev0, st));
+    HIPCHK(hipEventRecord(tp.first, st));
     HIPCHK(launch_trials(c, st));
+    HIPCHK(hipEventRecord(tp.second, st));
     HIPCHK(hipEventRecord(e->ev1, st));
     HIPCHK(launch_hist(e->d_sites, d_out, k, d_hist, e->d_stats, st));
     return FI_OK;
@@ -573,12 +586,33 @@ fi_status fi_run_trials_device(fi_engine *e, uint64_t first, uint64_t n, void *d
 fi_status fi_sync(fi_engine *e) {
     if (!e) return FI_E_ARG;
     HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipEventSynchronize(e->ev1));
     float ms = 0;
     if (hipEventElapsedTime(&ms, e->ev0, e->ev1) == hipSuccess) e->last_ms = ms;
     return FI_OK;
 }
 
 double fi_last_kernel_ms(fi_engine *e) { return e ? e->last_ms : 0.0; }
+
+fi_status fi_kernel_timer_reset(fi_engine *e) {
+    if (!e) return FI_E_ARG;
+    e->tused = 0;
+    return FI_OK;
+}
+
+fi_status fi_kernel_timer_read(fi_engine *e, double *total_ms, uint32_t *launches) {
+    if (!e) return FI_E_ARG;
+    double t = 0;
+    for (size_t i = 0; i < e->tused; i++) {
+        HIPCHK(hipEventSynchronize(e->tpool[i].second));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, e->tpool[i].first, e->tpool[i].second));
+        t += ms;
+    }
+    if (total_ms) *total_ms = t;
+    if (launches) *launches = (uint32_t)e->tused;
+    return FI_OK;
+}
 
 // ------------------------------------------------------------------ debug hooks (tests)
 fi_status fi_debug_decode(fi_engine *e, const uint32_t *raws, uint64_t n, void *out16) {

@@ -110,6 +110,8 @@ def lib():
         L.fi_last_kernel_ms.restype = C.c_double
         L.fi_last_kernel_ms.argtypes = [vp]
         L.fi_debug_decode.argtypes = [vp, vp, C.c_uint64, vp]
+        L.fi_kernel_timer_reset.argtypes = [vp]
+        L.fi_kernel_timer_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
 
@@ -201,6 +203,14 @@ class Engine:
 
     def last_kernel_ms(self) -> float:
         return self.L.fi_last_kernel_ms(self.h)
+
+    def kernel_timer_reset(self):
+        self._chk(self.L.fi_kernel_timer_reset(self.h), "fi_kernel_timer_reset")
+
+    def kernel_timer_read(self):
+        ms, n = C.c_double(), C.c_uint32()
+        self._chk(self.L.fi_kernel_timer_read(self.h, C.byref(ms), C.byref(n)), "fi_kernel_timer_read")
+        return ms.value, n.value
 
     def debug_decode(self, raws: np.ndarray) -> np.ndarray:
         raws = np.ascontiguousarray(raws, np.uint32)
