@@ -99,7 +99,10 @@ def main():
     hist_words = HIST_DT.itemsize // 8
     d_hist = torch.zeros(hist_words, dtype=torch.int64, device=dev)
     d_hist_node = torch.zeros_like(d_hist)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    # one dedicated stream for engine kernels, histogram copies and RCCL
+    tstream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(tstream)
+    stream = tstream.cuda_stream
 
     def step():
         d_hist.zero_()

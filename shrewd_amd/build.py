@@ -25,6 +25,8 @@ def build(force: bool = False, out: str = OUT, extra: list[str] | None = None) -
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17", "-Wall",
+           # keep wave-uniform branch trees as scalar branches (no flow-block chains)
+           "-mllvm", "-structurizecfg-skip-uniform-regions=true",
            "-o", out + ".tmp"] + (extra or []) + SRCS
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)

@@ -342,7 +342,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_tmp, std::max<size_t>(e->tmp_bytes, 16)));
     HIPCHK(hipMalloc(&e->d_out, c * sizeof(fi_outcome)));
     HIPCHK(hipMalloc(&e->d_hist, sizeof(fi_histogram)));
-    HIPCHK(hipMalloc(&e->d_stats, 8 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&e->d_stats, 32 * sizeof(unsigned long long)));
     HIPCHK(hipMalloc(&e->d_priv, c * e->cfg.private_pages * kPage));
     HIPCHK(hipMalloc(&e->d_priv_vpn, c * e->cfg.private_pages * 8));
     e->cap = c;
@@ -383,7 +383,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     c.out = e->d_out;
     c.n = 1;
     c.sites = nullptr; c.perm = nullptr;
-    HIPCHK(hipMemsetAsync(e->d_stats, 0, 8 * sizeof(unsigned long long), e->stream));
+    HIPCHK(hipMemsetAsync(e->d_stats, 0, 32 * sizeof(unsigned long long), e->stream));
     HIPCHK(hipEventRecord(e->ev0, e->stream));
     HIPCHK(launch_trials(c, e->stream));
     HIPCHK(hipEventRecord(e->ev1, e->stream));
@@ -392,7 +392,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
     e->last_ms = ms;
     fi_outcome o;
-    unsigned long long stats[8];
+    unsigned long long stats[32];
     HIPCHK(hipMemcpy(&o, e->d_out, sizeof o, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(stats, e->d_stats, sizeof stats, hipMemcpyDeviceToHost));
     if (o.cls != FI_MASKED) {
@@ -489,7 +489,7 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     c.perm = e->d_perm2;
     c.out = d_out;
     c.n = k;
-    HIPCHK(hipMemsetAsync(e->d_stats, 0, 8 * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(e->d_stats, 0, 32 * sizeof(unsigned long long), st));
     if (e->tused == e->tpool.size()) {
         hipEvent_t a, b;
         HIPCHK(hipEventCreate(&a));
@@ -593,6 +593,13 @@ fi_status fi_sync(fi_engine *e) {
 }
 
 double fi_last_kernel_ms(fi_engine *e) { return e ? e->last_ms : 0.0; }
+
+fi_status fi_debug_stats(fi_engine *e, uint64_t *out16) {
+    if (!e || !out16) return FI_E_ARG;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(out16, e->d_stats, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return FI_OK;
+}
 
 fi_status fi_kernel_timer_reset(fi_engine *e) {
     if (!e) return FI_E_ARG;

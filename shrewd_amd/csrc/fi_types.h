@@ -61,7 +61,8 @@ struct DevCtx {
     const uint32_t *perm;            // launch slot -> index into sites/out (sorted by site.inst)
     fi_outcome *out;
     uint64_t n;                      // trials in this launch
-    unsigned long long *stats;       // [0] fetch bytes [1] data bytes [2] pages [3] ncycles(golden)
+    unsigned long long *stats;       // [0] fetch B [1] data B [2] pages [3..5] golden ncycles/out/err
+                                     // [6] loop iterations [7] lane-insts [8] slow fetches [9] min-PC [10] max iter/wave
 };
 
 struct SampleCtx {

@@ -34,6 +34,10 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
     return ((uint64_t)hi << 32) | lo;
 }
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+    return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
+}
 __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -119,8 +123,9 @@ __global__ void fi_predecode_kernel(const uint8_t *text, uint64_t text_lo, uint6
     }
     if (ok) {
         Dec d = rv_decode(raw);
+        const uint16_t u = uop_of(d);   // may normalise d.imm (c.zext.b/h, c.not)
         p.raw = d.raw; p.op = d.op; p.rd = d.rd; p.rs1 = d.rs1; p.rs2 = d.rs2; p.imm = d.imm; p.len = d.len;
-        p.aux = d.aux;
+        p.aux = u;
         p.flags = (uint8_t)(kPreValid | (straddle ? kPreStraddle : 0) | d.flags);
     }
     pre[h] = p;
@@ -242,6 +247,23 @@ __device__ int mem_access(const DevCtx &c, LaneMem &m, uint64_t slot, uint64_t e
     return F_NONE;
 }
 
+// Fast-path translation: succeeds only if every fragment's page is mapped and,
+// for a store, already private -- anything else is left to the general path.
+__device__ __forceinline__ bool mem_probe(const DevCtx &c, LaneMem &m, uint64_t slot, uint64_t ea, uint32_t size,
+                                          bool wr, const uint8_t *&p1, const uint8_t *&p2, uint32_t &n1) {
+    n1 = 64 - (uint32_t)(ea & 63);
+    if (n1 > size) n1 = size;
+    if (ea + size - 1 < ea) return false;
+    const int k1 = lookup(c, m, slot, ea >> 12, p1);
+    if (!k1 || (wr && k1 != 2)) return false;
+    p2 = p1;
+    if (n1 < size) {
+        const int k2 = lookup(c, m, slot, (ea + n1) >> 12, p2);
+        if (!k2 || (wr && k2 != 2)) return false;
+    }
+    return true;
+}
+
 // Slow-path fetch of one lane: Decoder::moreBytes + setupFetchRequest
 // (src/arch/riscv/decoder.cc:63-116, src/cpu/simple/base.cc:304-318).
 // Returns 0 ok, or F_PGFAULT with the faulting fetch address and the number of
@@ -326,9 +348,25 @@ __device__ __forceinline__ void finish(Lane &L, int cls, int sub, int code, uint
 
 #define RREG(r) R[(uint32_t)(r) * 64u + lane]
 
+// Diagnostic build only (-DFI_STAMPS): per-wave cycle accounting of the loop
+// segments with s_memtime (never compiled into the shipped library).
+#ifdef FI_STAMPS
+#define STAMP(k)                                                  \
+    do {                                                          \
+        __builtin_amdgcn_sched_barrier(0);                        \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();         \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                       \
+        tacc[k] += _t - tlast;                                    \
+        tlast = _t;                                               \
+        __builtin_amdgcn_sched_barrier(0);                        \
+    } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
 // The syscall path of one lane: EmuLinux::syscall (se_workload.cc:95-106)
 // with the golden-output comparator folded into write().
-__device__ void do_syscall(const DevCtx &c, Lane &L, LaneMem &m, uint64_t slot, uint64_t *R, uint32_t lane) {
+__device__ __forceinline__ void do_syscall(const DevCtx &c, Lane &L, LaneMem &m, uint64_t slot, uint64_t *R, uint32_t lane) {
     const int num = (int)(uint32_t)RREG(17);
     const int cls = sys_class(num);
     if (cls == 0) { finish(L, FI_CRASH, FI_CRASH_SYSCALL_RANGE, 1, (uint32_t)num); return; }
@@ -411,6 +449,11 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
     m.stack_min = c.stack_min0; m.tlb_vpn = kNone; m.tlb_page = nullptr; m.req_vpn = kNone; m.req_src = nullptr;
     m.n_priv = 0; m.tlb_w = false; m.code_dirty = false;
     uint64_t pages_made = 0;
+    uint32_t n_iter = 0, n_slow = 0, n_min = 0, n_exec = 0;   // per-wave loop counters (uniform)
+#ifdef FI_STAMPS
+    uint64_t tacc[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t tlast = __builtin_amdgcn_s_memtime();
+#endif
 
     for (;;) {
         // ---- A. materialise requested pages, whole wave cooperating
@@ -442,6 +485,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
                 m.tlb_vpn = kNone;
             }
         }
+        STAMP(0);
         // ---- B. tick-top events: fault injection and the max-insts (hang)
         // exit both fire in serviceInstCountEvents at the first tick with
         // numInst >= n (src/cpu/simple/base.cc:321-325, src/cpu/base.cc:764-770)
@@ -478,27 +522,178 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
             if (__ballot(!L.done) == 0) break;
             continue;
         }
+        STAMP(1);
         // ---- C. leader PC: first ready lane, or min-PC if the lanes diverged
         const int leader = __ffsll((unsigned long long)act) - 1;
         uint64_t lpc = readlane64(L.pc, leader);
-        if (__ballot(ready && L.pc == lpc) != act) lpc = wave_min64(ready ? L.pc : kNone);
+        n_iter++;
+        if (__ballot(ready && L.pc == lpc) != act) { lpc = wave_min64(ready ? L.pc : kNone); n_min++; }
+        lpc = uni64(lpc);   // wave-uniform: keeps fetch/decode/dispatch on the scalar unit
         bool mine = ready && L.pc == lpc;
+        // lanes of other groups wait; the group keeps the wave only while its PC
+        // stays below theirs (min-PC order, so groups merge when they meet)
+        const uint64_t wait_min = (__ballot(mine) != act) ? uni64(wave_min64((ready && !mine) ? L.pc : kNone)) : kNone;
+        // next instruction-count event of this lane (injection or hang cap)
+        const uint64_t next_ev = (!L.injected && s.inst < c.hang_cap) ? s.inst : c.hang_cap;
 
+        // ---- FAST PATH: the group is converged on golden text with nothing
+        // watched or modified -- run pre-decoded micro-ops with PC, instruction,
+        // cycle and byte counts in SGPRs until an event is due, the group
+        // diverges, meets another group, or hits something the general path owns
+        // (K_SLOW op, fault, page request, syscall).  Nothing commits unless the
+        // whole instruction commits for every group lane.
+        if (lpc >= c.text_lo && lpc < c.text_hi && __ballot(mine && (m.code_dirty || L.watch > 0)) == 0) {
+            const uint64_t gm = __ballot(mine);
+            const int glane = __ffsll((unsigned long long)gm) - 1;
+            const uint64_t budget = uni64(wave_min64(mine ? next_ev - L.ninst : kNone));
+            uint64_t spc = lpc, steps = 0, cyc = 0, fbytes = 0, dbytes = 0;
+            bool div = false;
+            typedef __attribute__((address_space(4))) const uint32_t const_u32;
+            for (;;) {
+                spc = uni64(spc);   // keep the guest PC in SGPRs: s_load of the entry, scalar dispatch
+                const uint64_t key = (spc & 3) ? ((spc & ~3ULL) | 2) : spc;
+                if (key < c.text_lo || key >= c.text_hi) break;
+                const const_u32 *q = (const const_u32 *)(uintptr_t)(c.pre + ((key - c.text_lo) >> 1));
+                const uint32_t q1 = uni32(q[1]), q2 = uni32(q[2]), q3 = uni32(q[3]);
+                const uint32_t aux = q3 >> 16, kind = aux & 63;
+                if (!((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
+                const uint32_t rd = q1 >> 8 & 0xFF, rs1 = q1 >> 16 & 0xFF, rs2 = q1 >> 24;
+                const int64_t imm = (int32_t)q2;
+                const uint32_t len = q3 & 0xFF, ticks = ((q3 >> 8) & kPreStraddle) ? 2 : 1;
+                const uint64_t a0 = RREG(rs1), b0 = RREG(rs2);
+                const uint64_t av = (aux & U_APC) ? spc : a0;
+                const uint64_t bv = (aux & U_BIMM) ? (uint64_t)imm : b0;
+                const bool w32 = aux & U_W32;
+                const uint32_t shm = w32 ? 31 : 63;
+                uint64_t v = 0, npc = spc + len;
+                uint32_t msz = 0;
+                bool wr = true;
+                switch (kind) {
+                case K_ADD: v = av + bv; break;
+                case K_SUB: v = av - bv; break;
+                case K_AND: v = av & bv; break;
+                case K_OR: v = av | bv; break;
+                case K_XOR: v = av ^ bv; break;
+                case K_SLT: v = (int64_t)av < (int64_t)bv ? 1 : 0; break;
+                case K_SLTU: v = av < bv ? 1 : 0; break;
+                case K_SLL: v = av << (bv & shm); break;
+                case K_SRL: v = (w32 ? (av & 0xFFFFFFFFULL) : av) >> (bv & shm); break;
+                case K_SRA: v = (uint64_t)((w32 ? (int64_t)(int32_t)av : (int64_t)av) >> (bv & shm)); break;
+                case K_MUL: v = av * bv; break;
+                case K_NOP: wr = false; break;
+                case K_JAL: v = npc; npc = spc + imm; break;
+                case K_JALR: {
+                    v = npc;
+                    const uint64_t t = (a0 + imm) & ~1ULL;
+                    const uint64_t t0 = readlane64(t, glane);
+                    if (__ballot(mine && t != t0) == 0) npc = uni64(t0);
+                    else { div = true; if (mine) L.pc = t; }
+                    break;
+                }
+                case K_BEQ: case K_BNE: case K_BLT: case K_BGE: case K_BLTU: case K_BGEU: {
+                    wr = false;
+                    bool cnd;
+                    switch (kind) {
+                    case K_BEQ: cnd = a0 == b0; break;
+                    case K_BNE: cnd = a0 != b0; break;
+                    case K_BLT: cnd = (int64_t)a0 < (int64_t)b0; break;
+                    case K_BGE: cnd = (int64_t)a0 >= (int64_t)b0; break;
+                    case K_BLTU: cnd = a0 < b0; break;
+                    default: cnd = a0 >= b0; break;
+                    }
+                    const uint64_t tk = __ballot(mine && cnd);
+                    if (tk == gm) npc = spc + imm;
+                    else if (tk != 0) { div = true; if (mine) L.pc = cnd ? spc + imm : npc; }
+                    break;
+                }
+                default: {   // K_LOAD / K_STORE
+                    const bool st = kind == K_STORE;
+                    msz = 1u << ((aux >> 12) & 3);
+                    const uint64_t ea = a0 + imm;
+                    const uint8_t *p1 = nullptr, *p2 = nullptr;
+                    uint32_t n1 = 0;
+                    bool ok = true;
+                    if (mine) ok = mem_probe(c, m, slot, ea, msz, st, p1, p2, n1);
+                    if (__ballot(mine && !ok) != 0) { msz = 0xFFFFFFFFu; break; }   // bail: general path
+                    if (mine) {
+                        const uint32_t off = (uint32_t)(ea & 4095);
+                        if (st) {
+                            uint8_t *w1 = const_cast<uint8_t *>(p1);
+                            if (n1 == msz && (off & (msz - 1)) == 0) {
+                                switch (msz) {
+                                case 1: w1[off] = (uint8_t)b0; break;
+                                case 2: *(uint16_t *)(w1 + off) = (uint16_t)b0; break;
+                                case 4: *(uint32_t *)(w1 + off) = (uint32_t)b0; break;
+                                default: *(uint64_t *)(w1 + off) = b0; break;
+                                }
+                            } else {
+                                uint8_t *w2 = const_cast<uint8_t *>(p2);
+                                for (uint32_t i = 0; i < msz; i++) (i < n1 ? w1 : w2)[(ea + i) & 4095] = (uint8_t)(b0 >> (8 * i));
+                            }
+                        } else {
+                            uint64_t t = 0;
+                            if (n1 == msz && (off & (msz - 1)) == 0) {
+                                switch (msz) {
+                                case 1: t = p1[off]; break;
+                                case 2: t = *(const uint16_t *)(p1 + off); break;
+                                case 4: t = *(const uint32_t *)(p1 + off); break;
+                                default: t = *(const uint64_t *)(p1 + off); break;
+                                }
+                            } else {
+                                for (uint32_t i = 0; i < msz; i++) t |= (uint64_t)(i < n1 ? p1 : p2)[(ea + i) & 4095] << (8 * i);
+                            }
+                            v = (aux & U_SEXT) ? (uint64_t)sext64(t, 8 * msz) : t;
+                        }
+                    }
+                    if (st) wr = false;
+                    break;
+                }
+                }
+                if (msz == 0xFFFFFFFFu) break;            // nothing committed for this instruction
+                if (w32) v = sx32(v);
+                if (wr && rd && mine) RREG(rd) = v;
+                steps++; cyc += ticks; fbytes += len; dbytes += msz;
+                if (div) break;
+                spc = npc;
+                if (steps >= budget || spc >= wait_min) break;
+            }
+            if (steps) {
+                if (mine) {
+                    L.ninst += steps; L.ncyc += cyc; L.fetch_b += fbytes; L.data_b += dbytes;
+                    if (!div) L.pc = spc;
+                }
+                n_iter += (uint32_t)steps;
+                n_exec += (uint32_t)(steps * __popcll(gm));
+                continue;
+            }
+        }
+
+        // ---- inner loop: one guest instruction per iteration while the group
+        // stays converged, with no event due and no page request pending
+        for (;;) {
+        STAMP(2);
         // ---- D. fetch + decode (wave-uniform)
         Dec d;
         uint32_t ticks = 1;
         bool fast = false;
         const uint64_t key = (lpc & 3) ? ((lpc & ~3ULL) | 2) : lpc;
         if (key >= c.text_lo && key < c.text_hi && __ballot(mine && m.code_dirty) == 0) {
-            const PreInst p = c.pre[(key - c.text_lo) >> 1];
-            if (p.flags & kPreValid) {
+            // one s_load_dwordx4 through the constant address space: the
+            // pre-decoded table is read-only for the whole launch
+            typedef __attribute__((address_space(4))) const uint32_t const_u32;
+            const const_u32 *q = (const const_u32 *)(uintptr_t)(c.pre + ((key - c.text_lo) >> 1));
+            const uint32_t q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+            const uint32_t pflags = (q3 >> 8) & 0xFF;
+            if (pflags & kPreValid) {
                 fast = true;
-                d.raw = p.raw; d.op = p.op; d.rd = p.rd; d.rs1 = p.rs1; d.rs2 = p.rs2; d.imm = p.imm; d.len = p.len;
-                d.flags = p.flags; d.aux = p.aux;
-                ticks = (p.flags & kPreStraddle) ? 2 : 1;
+                d.raw = q0; d.op = (uint8_t)q1; d.rd = (uint8_t)(q1 >> 8); d.rs1 = (uint8_t)(q1 >> 16);
+                d.rs2 = (uint8_t)(q1 >> 24); d.imm = (int32_t)q2; d.len = (uint8_t)q3;
+                d.flags = (uint8_t)pflags; d.aux = (uint16_t)(q3 >> 16);
+                ticks = (pflags & kPreStraddle) ? 2 : 1;
             }
         }
         if (!fast) {
+            n_slow++;
             uint32_t raw = 0, t = 1;
             uint64_t fva = 0;
             if (mine) {
@@ -518,7 +713,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
                 }
             }
             const uint64_t okm = __ballot(mine);
-            if (okm == 0) continue;
+            if (okm == 0) break;
             const int ld = __ffsll((unsigned long long)okm) - 1;
             const uint32_t lraw = (uint32_t)__builtin_amdgcn_readlane((int)raw, ld);
             const uint32_t lt = (uint32_t)__builtin_amdgcn_readlane((int)t, ld);
@@ -526,8 +721,17 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
             d = rv_decode(lraw);
             ticks = lt;
         }
-        if (!mine) continue;
-
+        // force every decoded field into SGPRs: the op switch below must be a
+        // scalar branch tree, never a per-lane waterfall
+        d.op = (uint8_t)uni32(d.op); d.rd = (uint8_t)uni32(d.rd); d.rs1 = (uint8_t)uni32(d.rs1);
+        d.rs2 = (uint8_t)uni32(d.rs2); d.len = (uint8_t)uni32(d.len); d.flags = (uint8_t)uni32(d.flags);
+        d.imm = (int32_t)uni32((uint32_t)d.imm); d.aux = (uint16_t)uni32(d.aux); d.raw = uni32(d.raw);
+        ticks = uni32(ticks);
+        const uint64_t gmask = __ballot(mine);
+        n_exec += (uint32_t)__popcll(gmask);
+        STAMP(3);
+        int f = F_NONE;
+        if (mine) {
         // ---- E. execute: the generated StaticInst::execute bodies of
         // src/arch/riscv/isa/decoder.isa for the modelled subset
         const uint64_t pc = L.pc;
@@ -535,8 +739,9 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
         const int64_t imm = d.imm;
         uint64_t npc = pc + d.len;
         uint64_t v = 0, fva = 0, t = 0;
-        int f = F_NONE;
         bool wrd = true;
+        uint32_t msz = 0, mext = 0;   // memory access size / sign-extension width (uniform)
+        bool mst = false;
         // detected-by-replica: the flipped protected register is read before
         // being overwritten (build-defined SHREWD semantics)
         if (L.watch > 0 &&
@@ -549,19 +754,21 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
             case OP_ESC_FP: case OP_ESC_VEC: case OP_ESC_AMO: case OP_ESC_SYS: case OP_ESC_CRYPTO: case OP_ESC_CBO:
             case OP_ESC_CMP: case OP_ESC_M5: case OP_ESC_HYP: f = F_ESCAPE; break;
             case OP_c_addi4spn: if (imm == 0) f = F_ILLEGAL; else v = a + imm; break;
-            case OP_c_lwsp: if (d.rd == 0) { f = F_ILLEGAL; break; }   // fallthrough
-            case OP_c_lw: case OP_lw: f = mem_access(c, m, slot, a + imm, 4, false, t, fva); v = sx32(t); L.data_b += 4; break;
-            case OP_c_ldsp: if (d.rd == 0) { f = F_ILLEGAL; break; }   // fallthrough
-            case OP_c_ld: case OP_ld: f = mem_access(c, m, slot, a + imm, 8, false, t, fva); v = t; L.data_b += 8; break;
-            case OP_c_lbu: case OP_lbu: f = mem_access(c, m, slot, a + imm, 1, false, t, fva); v = t; L.data_b += 1; break;
-            case OP_c_lhu: case OP_lhu: f = mem_access(c, m, slot, a + imm, 2, false, t, fva); v = t; L.data_b += 2; break;
-            case OP_c_lh: case OP_lh: f = mem_access(c, m, slot, a + imm, 2, false, t, fva); v = (uint64_t)sext64(t, 16); L.data_b += 2; break;
-            case OP_lb: f = mem_access(c, m, slot, a + imm, 1, false, t, fva); v = (uint64_t)sext64(t, 8); L.data_b += 1; break;
-            case OP_lwu: f = mem_access(c, m, slot, a + imm, 4, false, t, fva); v = t; L.data_b += 4; break;
-            case OP_c_sb: case OP_sb: t = b; f = mem_access(c, m, slot, a + imm, 1, true, t, fva); wrd = false; L.data_b += 1; break;
-            case OP_c_sh: case OP_sh: t = b; f = mem_access(c, m, slot, a + imm, 2, true, t, fva); wrd = false; L.data_b += 2; break;
-            case OP_c_sw: case OP_sw: case OP_c_swsp: t = b; f = mem_access(c, m, slot, a + imm, 4, true, t, fva); wrd = false; L.data_b += 4; break;
-            case OP_c_sd: case OP_sd: case OP_c_sdsp: t = b; f = mem_access(c, m, slot, a + imm, 8, true, t, fva); wrd = false; L.data_b += 8; break;
+            // loads/stores only describe the access here; the single access site
+            // after the switch keeps the hot loop small (one inlined copy)
+            case OP_c_lwsp: if (d.rd == 0) { f = F_ILLEGAL; break; } msz = 4; mext = 32; break;
+            case OP_c_lw: case OP_lw: msz = 4; mext = 32; break;
+            case OP_c_ldsp: if (d.rd == 0) { f = F_ILLEGAL; break; } msz = 8; break;
+            case OP_c_ld: case OP_ld: msz = 8; break;
+            case OP_c_lbu: case OP_lbu: msz = 1; break;
+            case OP_c_lhu: case OP_lhu: msz = 2; break;
+            case OP_c_lh: case OP_lh: msz = 2; mext = 16; break;
+            case OP_lb: msz = 1; mext = 8; break;
+            case OP_lwu: msz = 4; break;
+            case OP_c_sb: case OP_sb: msz = 1; mst = true; wrd = false; break;
+            case OP_c_sh: case OP_sh: msz = 2; mst = true; wrd = false; break;
+            case OP_c_sw: case OP_sw: case OP_c_swsp: msz = 4; mst = true; wrd = false; break;
+            case OP_c_sd: case OP_sd: case OP_c_sdsp: msz = 8; mst = true; wrd = false; break;
             case OP_c_addi: case OP_addi: v = a + imm; break;
             case OP_c_addiw: if (d.rd == 0) f = F_ILLEGAL; else v = sx32(a + imm); break;
             case OP_addiw: v = sx32(a + imm); break;
@@ -700,13 +907,22 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
             case OP_jalr: v = npc; npc = (a + imm) & ~1ULL; break;
             case OP_jal: v = npc; npc = pc + imm; break;
             case OP_ecall: f = F_SYSCALL; break;
-            case OP_csr: f = csr_u_accessible(d.aux) ? F_ESCCSR : F_ILLEGAL; break;
+            case OP_csr: f = csr_u_accessible(d.raw >> 20) ? F_ESCCSR : F_ILLEGAL; break;
             default: f = F_UNKNOWN; break;
             }
         }
-        if (f == F_NEEDPAGE) continue;      // copy-on-write first; the tick is retried
+        STAMP(4);
+        if (msz && f == F_NONE) {
+            t = b;
+            f = mem_access(c, m, slot, a + imm, msz, mst, t, fva);
+            L.data_b += msz;
+            if (!mst) v = mext ? (uint64_t)sext64(t, mext) : t;
+        }
+        STAMP(5);
+        // F_NEEDPAGE: copy-on-write first; the tick is retried (no commit)
         // ---- F. commit: countInst only on NoFault (atomic.cc:687-689), then
         // advancePC (src/cpu/simple/base.cc:493-512)
+        if (f != F_NEEDPAGE) {
         L.ncyc += ticks;
         L.fetch_b += d.len;
         if (f == F_NONE) {
@@ -714,8 +930,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
             if (wrd && L.watch > 0 && (d.flags & kPreRd) && d.rd == L.watch) L.watch = -1;
             L.ninst++;
             L.pc = npc;
-            continue;
-        }
+        } else {
         switch (f) {
         case F_SYSCALL:   // SyscallFault::invokeSE advances the PC first (arch/riscv/faults.cc:325-333)
             L.pc = pc + d.len;
@@ -738,6 +953,20 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
             break;
         default: break;
         }
+        }   // fault disposition
+        }   // f != F_NEEDPAGE
+        }   // mine
+        // ---- stay in the inner loop? every group lane committed, none reached
+        // its next event, all at one PC that is still the wave's minimum
+        const bool cont = mine && f == F_NONE && L.ninst < next_ev;
+        const uint64_t cm = __ballot(cont);
+        if (cm != gmask) break;
+        const uint64_t npc0 = uni64(readlane64(L.pc, __ffsll((unsigned long long)cm) - 1));
+        if (__ballot(cont && L.pc == npc0) != cm || npc0 >= wait_min) break;
+        lpc = npc0;
+        mine = cont;
+        n_iter++;
+        }   // inner loop
     }
 
     if (live) c.out[c.record ? 0 : sidx] = L.res;
@@ -751,6 +980,14 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx c) {
         atomicAdd(&c.stats[0], (unsigned long long)fb);
         atomicAdd(&c.stats[1], (unsigned long long)db);
         atomicAdd(&c.stats[2], (unsigned long long)pm);
+        atomicAdd(&c.stats[6], (unsigned long long)n_iter);
+        atomicAdd(&c.stats[7], (unsigned long long)n_exec);
+        atomicAdd(&c.stats[8], (unsigned long long)n_slow);
+        atomicAdd(&c.stats[9], (unsigned long long)n_min);
+        atomicMax(&c.stats[10], (unsigned long long)n_iter);
+#ifdef FI_STAMPS
+        for (int k = 0; k < 6; k++) atomicAdd(&c.stats[16 + k], (unsigned long long)tacc[k]);
+#endif
     }
 }
 

@@ -117,18 +117,12 @@ __host__ __device__ inline Dec rv_decode(uint32_t raw) {
                 case 2: d.op = OP_c_andi; D_RD(rp1); D_RS1(rp1); d.imm = fsext(cimm5 | (cimm1 << 5), 6); return d;
                 default: {
                     const uint32_t f2 = fbits(raw, 6, 5);
-                    if (!cimm1) {
-                        const uint8_t o[4] = {OP_c_sub, OP_c_xor, OP_c_or, OP_c_and};
-                        d.op = o[f2]; D_RD(rp1); D_RS1(rp1); D_RS2(rp2); return d;
-                    }
-                    if (f2 < 3) {
-                        const uint8_t o[3] = {OP_c_subw, OP_c_addw, OP_c_mul};
-                        d.op = o[f2]; D_RD(rp1); D_RS1(rp1); D_RS2(rp2); return d;
-                    }
+                    // (no local lookup arrays: they would live in scratch memory)
+                    if (!cimm1) { d.op = (uint8_t)(OP_c_sub + f2); D_RD(rp1); D_RS1(rp1); D_RS2(rp2); return d; }
+                    if (f2 < 3) { d.op = (uint8_t)(OP_c_subw + f2); D_RD(rp1); D_RS1(rp1); D_RS2(rp2); return d; }
                     const uint32_t sel = fbits(raw, 4, 2);
                     if (sel > 5) return d;
-                    const uint8_t o[6] = {OP_c_zext_b, OP_c_sext_b, OP_c_zext_h, OP_c_sext_h, OP_c_zext_w, OP_c_not};
-                    d.op = o[sel]; D_RD(rp1); D_RS1(rp1); return d;
+                    d.op = (uint8_t)(OP_c_zext_b + sel); D_RD(rp1); D_RS1(rp1); return d;
                 }
                 }
             case 5:
@@ -184,8 +178,7 @@ __host__ __device__ inline Dec rv_decode(uint32_t raw) {
     switch (opc) {
     case 0x00: {  // LOAD :538-566
         if (f3 == 7) return d;
-        const uint8_t o[7] = {OP_lb, OP_lh, OP_lw, OP_ld, OP_lbu, OP_lhu, OP_lwu};
-        RI(o[f3], imm_i);
+        RI((uint8_t)(OP_lb + f3), imm_i);
     }
     case 0x01: d.op = OP_ESC_FP; return d;
     case 0x03:  // MISC-MEM :1336-1433
@@ -256,8 +249,7 @@ __host__ __device__ inline Dec rv_decode(uint32_t raw) {
         return d;
     case 0x08: {  // STORE :1722-1739
         if (f3 > 3) return d;
-        const uint8_t o[4] = {OP_sb, OP_sh, OP_sw, OP_sd};
-        d.op = o[f3]; D_RS1(rs1); D_RS2(rs2); d.imm = imm_s; return d;
+        d.op = (uint8_t)(OP_sb + f3); D_RS1(rs1); D_RS2(rs2); d.imm = imm_s; return d;
     }
     case 0x09: d.op = OP_ESC_FP; return d;
     case 0x0b: d.op = OP_ESC_AMO; return d;
@@ -329,8 +321,7 @@ __host__ __device__ inline Dec rv_decode(uint32_t raw) {
     case 0x15: d.op = OP_ESC_VEC; return d;
     case 0x18: {  // BRANCH :5891-5936
         if (f3 == 2 || f3 == 3) return d;
-        const uint8_t o[8] = {OP_beq, OP_bne, 0, 0, OP_blt, OP_bge, OP_bltu, OP_bgeu};
-        d.op = o[f3]; D_RS1(rs1); D_RS2(rs2); d.imm = imm_b; return d;
+        d.op = (uint8_t)(OP_beq + (f3 < 4 ? f3 : f3 - 2)); D_RS1(rs1); D_RS2(rs2); d.imm = imm_b; return d;
     }
     case 0x19: if (f3 == 0) RI(OP_jalr, imm_i); return d;   // :5938-5943
     case 0x1b: d.op = OP_jal; D_RD(rd); d.imm = imm_j; return d;
@@ -357,5 +348,86 @@ __host__ __device__ inline Dec rv_decode(uint32_t raw) {
 #undef D_RD
 #undef D_RS1
 #undef D_RS2
+
+// ---------------------------------------------------------------- micro-ops
+// The fast path executes a normalised micro-op instead of the 170 gem5 ops:
+// aux = kind | U_* flags | log2(size) << 12.  Every op whose semantics are not a
+// plain ALU/load/store/branch/jump (M-extension beyond mul, bitmanip, system,
+// unknown, escapes, and the encodings that raise IllegalInst at execute) is
+// K_SLOW and goes through the full per-op switch of the general path.
+enum Kind : uint8_t {
+    K_SLOW = 0, K_ADD, K_SUB, K_AND, K_OR, K_XOR, K_SLT, K_SLTU, K_SLL, K_SRL, K_SRA, K_MUL,
+    K_LOAD, K_STORE, K_BEQ, K_BNE, K_BLT, K_BGE, K_BLTU, K_BGEU, K_JAL, K_JALR, K_NOP
+};
+constexpr uint16_t U_BIMM = 1u << 8, U_APC = 1u << 9, U_W32 = 1u << 10, U_SEXT = 1u << 11;
+
+__host__ __device__ inline uint16_t uop_of(Dec &d) {
+    auto ls = [](uint8_t k, int lg, bool sx) -> uint16_t {
+        return (uint16_t)(k | (lg << 12) | (sx ? U_SEXT : 0));
+    };
+    switch (d.op) {
+    case OP_c_addi4spn: return d.imm ? (uint16_t)(K_ADD | U_BIMM) : K_SLOW;
+    case OP_c_lwsp: if (d.rd == 0) return K_SLOW; return ls(K_LOAD, 2, true);
+    case OP_c_lw: case OP_lw: return ls(K_LOAD, 2, true);
+    case OP_c_ldsp: if (d.rd == 0) return K_SLOW; return ls(K_LOAD, 3, false);
+    case OP_c_ld: case OP_ld: return ls(K_LOAD, 3, false);
+    case OP_c_lbu: case OP_lbu: return ls(K_LOAD, 0, false);
+    case OP_c_lhu: case OP_lhu: return ls(K_LOAD, 1, false);
+    case OP_c_lh: case OP_lh: return ls(K_LOAD, 1, true);
+    case OP_lb: return ls(K_LOAD, 0, true);
+    case OP_lwu: return ls(K_LOAD, 2, false);
+    case OP_c_sb: case OP_sb: return ls(K_STORE, 0, false);
+    case OP_c_sh: case OP_sh: return ls(K_STORE, 1, false);
+    case OP_c_sw: case OP_sw: case OP_c_swsp: return ls(K_STORE, 2, false);
+    case OP_c_sd: case OP_sd: case OP_c_sdsp: return ls(K_STORE, 3, false);
+    case OP_c_addi: case OP_addi: case OP_c_li: case OP_lui: return K_ADD | U_BIMM;
+    case OP_c_addiw: if (d.rd == 0) return K_SLOW; return K_ADD | U_BIMM | U_W32;
+    case OP_addiw: return K_ADD | U_BIMM | U_W32;
+    case OP_c_addi16sp: case OP_c_lui: return d.imm ? (uint16_t)(K_ADD | U_BIMM) : K_SLOW;
+    case OP_c_srli: case OP_srli: return K_SRL | U_BIMM;
+    case OP_c_srai: case OP_srai: return K_SRA | U_BIMM;
+    case OP_c_slli: case OP_slli: return K_SLL | U_BIMM;
+    case OP_c_andi: case OP_andi: return K_AND | U_BIMM;
+    case OP_xori: return K_XOR | U_BIMM;
+    case OP_ori: case OP_ori_hint: return K_OR | U_BIMM;
+    case OP_slti: return K_SLT | U_BIMM;
+    case OP_sltiu: return K_SLTU | U_BIMM;
+    case OP_c_sub: case OP_sub: return K_SUB;
+    case OP_c_xor: case OP_xor_: return K_XOR;
+    case OP_c_or: case OP_or_: return K_OR;
+    case OP_c_and: case OP_and_: return K_AND;
+    case OP_c_subw: case OP_subw: return K_SUB | U_W32;
+    case OP_c_addw: case OP_addw: return K_ADD | U_W32;
+    case OP_c_mul: case OP_mul: return K_MUL;
+    case OP_mulw: return K_MUL | U_W32;
+    case OP_c_zext_b: d.imm = 0xFF; return K_AND | U_BIMM;
+    case OP_c_zext_h: d.imm = 0xFFFF; return K_AND | U_BIMM;
+    case OP_c_not: d.imm = -1; return K_XOR | U_BIMM;
+    case OP_c_j: case OP_jal: return K_JAL;
+    case OP_c_beqz: case OP_beq: return K_BEQ;
+    case OP_c_bnez: case OP_bne: return K_BNE;
+    case OP_blt: return K_BLT;
+    case OP_bge: return K_BGE;
+    case OP_bltu: return K_BLTU;
+    case OP_bgeu: return K_BGEU;
+    case OP_c_jr: return d.rs1 ? (uint16_t)K_JALR : K_SLOW;
+    case OP_c_jalr: case OP_jalr: return K_JALR;
+    case OP_c_mv: case OP_c_add: case OP_add: return K_ADD;
+    case OP_sll: return K_SLL;
+    case OP_srl: return K_SRL;
+    case OP_sra: return K_SRA;
+    case OP_slt: return K_SLT;
+    case OP_sltu: return K_SLTU;
+    case OP_sllw: return K_SLL | U_W32;
+    case OP_srlw: return K_SRL | U_W32;
+    case OP_sraw: return K_SRA | U_W32;
+    case OP_slliw: return K_SLL | U_BIMM | U_W32;
+    case OP_srliw: return K_SRL | U_BIMM | U_W32;
+    case OP_sraiw: return K_SRA | U_BIMM | U_W32;
+    case OP_auipc: return K_ADD | U_BIMM | U_APC;
+    case OP_fence: case OP_fence_i: case OP_prefetch_i: case OP_prefetch_r: case OP_prefetch_w: return K_NOP;
+    default: return K_SLOW;
+    }
+}
 
 }  // namespace fi

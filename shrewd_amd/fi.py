@@ -78,7 +78,7 @@ _lib = None
 
 
 def library_path() -> str:
-    return _build.OUT
+    return os.environ.get("SHREWD_FI_LIB", _build.OUT)
 
 
 def build_library(force: bool = False) -> str:
@@ -111,6 +111,7 @@ def lib():
         L.fi_last_kernel_ms.argtypes = [vp]
         L.fi_debug_decode.argtypes = [vp, vp, C.c_uint64, vp]
         L.fi_kernel_timer_reset.argtypes = [vp]
+        L.fi_debug_stats.argtypes = [vp, vp]
         L.fi_kernel_timer_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
         _lib = L
     return _lib
@@ -203,6 +204,11 @@ class Engine:
 
     def last_kernel_ms(self) -> float:
         return self.L.fi_last_kernel_ms(self.h)
+
+    def debug_stats(self) -> np.ndarray:
+        out = np.zeros(32, np.uint64)
+        self._chk(self.L.fi_debug_stats(self.h, out.ctypes.data), "fi_debug_stats")
+        return out
 
     def kernel_timer_reset(self):
         self._chk(self.L.fi_kernel_timer_reset(self.h), "fi_kernel_timer_reset")
