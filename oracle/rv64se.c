@@ -10,6 +10,7 @@
  */
 #define _GNU_SOURCE
 #include "rv64se.h"
+#include "../shrewd_amd/csrc/gem5_decode_table.h"
 
 #include <pthread.h>
 #include <stdio.h>
@@ -184,9 +185,30 @@ static inline s64 sext(u64 v, int n) { return (s64)(v << (64 - n)) >> (64 - n); 
  * decode tree of arch/riscv/isa/decoder.isa for rv_type=RV64, enable_zcd=1
  * (RiscvISA.py:95,121-127).  Field definitions: isa/bitfields.isa:36-130. */
 static void decode_tree(u32 raw, dec_t *d);
+/* Which 32-bit encodings of the non-executed opcode groups (FP, vector, AMO,
+ * privileged SYSTEM) gem5 decodes to a real instruction rather than Unknown:
+ * first-match rows generated from decoder.isa by
+ * tools/oracle/gen_decode_vectors.py (shrewd_amd/csrc/gem5_decode_table.h). */
+typedef struct { u32 mask, match; uint8_t known; } dec_row_t;
+#define ROW(m, v, k) {m, v, k},
+static const dec_row_t gem5_rows[FI_GEM5_DEC_ROWS] = { FI_GEM5_DEC_TABLE(ROW) };
+#undef ROW
+static int gem5_known(u32 raw) {
+    u32 op5 = (raw >> 2) & 31;
+#define IDX(o, first, cnt) \
+    if (op5 == (o)) { for (int i = (first); i < (first) + (cnt); i++) \
+                          if ((raw & gem5_rows[i].mask) == gem5_rows[i].match) return gem5_rows[i].known; \
+                      return 0; }
+    FI_GEM5_DEC_INDEX(IDX)
+#undef IDX
+    return 1;
+}
 /* Unknown and escape encodings read and write no registers. */
 static void decode(u32 raw, dec_t *d) {
     decode_tree(raw, d);
+    if ((raw & 3) == 3 && (d->op == OP_ESC_FP || d->op == OP_ESC_VEC || d->op == OP_ESC_AMO ||
+                           d->op == OP_ESC_SYS || d->op == OP_ESC_HYP) && !gem5_known(raw))
+        d->op = OP_UNKNOWN;
     if (d->op < OP_c_addi4spn) d->rd = d->rs1 = d->rs2 = -1;
 }
 static void decode_tree(u32 raw, dec_t *d) {

@@ -5,7 +5,9 @@ hand-written HIP kernels behind the C ABI in include/fi_engine.h; this package
 is the host-side mirror of the gem5 FaultCampaign SimObject interface.
 """
 from .fi import (CLASS_NAMES, CRASH_NAMES, ESCAPE_NAMES, FaultCampaign, Engine, EngineError, HIST_DT,
-                 OUTCOME_DT, SITE_DT, build_library, library_path, structures_mask)
+                 OUTCOME_DT, SITE_DT, allreduce_histogram, build_library, library_path, shard_range,
+                 structures_mask)
 
 __all__ = ["FaultCampaign", "Engine", "EngineError", "OUTCOME_DT", "SITE_DT", "HIST_DT", "CLASS_NAMES",
-           "CRASH_NAMES", "ESCAPE_NAMES", "build_library", "library_path", "structures_mask"]
+           "CRASH_NAMES", "ESCAPE_NAMES", "allreduce_histogram", "build_library", "library_path",
+           "shard_range", "structures_mask"]

@@ -109,20 +109,31 @@ static void dfree(T *&p) {
 
 extern "C" {
 
+// errors of calls that have no engine yet (fi_create), per host thread
+static thread_local std::string g_create_err;
+
 fi_status fi_create(const fi_config *cfg, fi_engine **out) {
-    if (!out) return FI_E_ARG;
+    if (!out) { g_create_err = "fi_create: out is NULL"; return FI_E_ARG; }
     *out = nullptr;
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return FI_E_NODEVICE;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        g_create_err = "fi_create: no HIP device visible (the engine has no CPU fallback)";
+        return FI_E_NODEVICE;
+    }
     fi_engine *e = new fi_engine();
     if (cfg) e->cfg = *cfg;
     if (e->cfg.private_pages == 0) e->cfg.private_pages = 16;
     if (e->cfg.hang_factor_x16 == 0) e->cfg.hang_factor_x16 = 32;
     if (e->cfg.max_trials_per_launch == 0) e->cfg.max_trials_per_launch = 65536;
     e->dev = e->cfg.device;
-    if (e->dev < 0 || e->dev >= n) { delete e; return FI_E_ARG; }
+    if (e->dev < 0 || e->dev >= n) {
+        g_create_err = "fi_create: device " + std::to_string(e->dev) + " out of range (" + std::to_string(n) + " visible)";
+        delete e;
+        return FI_E_ARG;
+    }
     if (hipSetDevice(e->dev) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
+        g_create_err = "fi_create: HIP stream/event creation failed on device " + std::to_string(e->dev);
         delete e;
         return FI_E_HIP;
     }
@@ -154,7 +165,7 @@ void fi_destroy(fi_engine *e) {
     delete e;
 }
 
-const char *fi_last_error(fi_engine *e) { return e ? e->err.c_str() : "null engine"; }
+const char *fi_last_error(fi_engine *e) { return e ? e->err.c_str() : g_create_err.c_str(); }
 
 // ------------------------------------------------------------------ image
 static uint16_t le16(const uint8_t *p) { return (uint16_t)(p[0] | (p[1] << 8)); }

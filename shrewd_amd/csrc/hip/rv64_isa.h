@@ -11,6 +11,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "../gem5_decode_table.h"
+
 #define FI_OPS(X) \
     X(UNKNOWN) X(ESC_FP) X(ESC_VEC) X(ESC_AMO) X(ESC_SYS) X(ESC_CRYPTO) X(ESC_CBO) X(ESC_CMP) X(ESC_M5) X(ESC_HYP) \
     X(c_addi4spn) X(c_lw) X(c_ld) X(c_lbu) X(c_lhu) X(c_lh) X(c_sb) X(c_sh) X(c_sw) X(c_sd) \
@@ -61,7 +63,7 @@ __host__ __device__ inline int32_t fsext(uint32_t v, int n) { return (int32_t)(v
 #define D_RS1(r) (d.rs1 = (uint8_t)(r), d.flags |= 4)
 #define D_RS2(r) (d.rs2 = (uint8_t)(r), d.flags |= 8)
 
-__host__ __device__ inline Dec rv_decode(uint32_t raw) {
+__device__ inline Dec rv_decode_tree(uint32_t raw) {
     Dec d;
     d.raw = raw; d.imm = 0; d.op = OP_UNKNOWN; d.rd = d.rs1 = d.rs2 = 0; d.flags = 0; d.aux = 0;
     const uint32_t q = raw & 3;
@@ -344,6 +346,33 @@ __host__ __device__ inline Dec rv_decode(uint32_t raw) {
     }
 #undef RI
 #undef RR
+}
+
+// gem5's known-vs-Unknown split for the opcode groups the engine does not
+// execute; rows generated from decoder.isa (../gem5_decode_table.h).
+struct DecRow { uint32_t mask, match, known; };
+#define FI_ROW(m, v, k) {m, v, k},
+__constant__ const DecRow kGem5Rows[FI_GEM5_DEC_ROWS] = { FI_GEM5_DEC_TABLE(FI_ROW) };
+#undef FI_ROW
+
+__device__ inline bool gem5_known(uint32_t raw) {
+    const uint32_t op5 = (raw >> 2) & 31;
+    int first = -1, cnt = 0;
+#define FI_IDX(o, f, c) if (op5 == (o)) { first = (f); cnt = (c); }
+    FI_GEM5_DEC_INDEX(FI_IDX)
+#undef FI_IDX
+    if (first < 0) return true;
+    for (int i = first; i < first + cnt; i++)
+        if ((raw & kGem5Rows[i].mask) == kGem5Rows[i].match) return kGem5Rows[i].known != 0;
+    return false;
+}
+
+__device__ inline Dec rv_decode(uint32_t raw) {
+    Dec d = rv_decode_tree(raw);
+    if ((raw & 3) == 3 && (d.op == OP_ESC_FP || d.op == OP_ESC_VEC || d.op == OP_ESC_AMO ||
+                           d.op == OP_ESC_SYS || d.op == OP_ESC_HYP) && !gem5_known(raw))
+        d.op = OP_UNKNOWN;
+    return d;
 }
 #undef D_RD
 #undef D_RS1

@@ -227,6 +227,29 @@ class Engine:
         return out
 
 
+def shard_range(trials: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous trial-id block of `rank`: [r*T/G, (r+1)*T/G).
+    Sites are counter-based on (seed, trial id), so any sharding runs the same
+    trials."""
+    lo = trials * rank // world
+    hi = trials * (rank + 1) // world
+    return lo, hi - lo
+
+
+def allreduce_histogram(hist, device=None, group=None):
+    """Sum an outcome histogram (HIST_DT record) over all ranks: the campaign's
+    only exchange.  RCCL over xGMI when `device` is a GPU and the process group
+    is "nccl"; any torch.distributed backend works (gloo in CPU tests)."""
+    import torch
+    import torch.distributed as dist
+    words = np.frombuffer(np.asarray(hist, HIST_DT).tobytes(), np.int64).copy()
+    t = torch.from_numpy(words)
+    if device is not None:
+        t = t.to(device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return np.frombuffer(t.cpu().numpy().tobytes(), HIST_DT)[0].copy()
+
+
 class FaultCampaign:
     """Mirror of the gem5 `FaultCampaign` SimObject (src/gem5ext/FaultCampaign.py).
 
@@ -259,10 +282,24 @@ class FaultCampaign:
         self.engine.set_protect(mask)
 
     def run(self, first_trial: int = 0, n: int | None = None):
+        """Run the campaign.  Under torch.distributed with num_gpus > 1 (one
+        process per GPU), this rank runs its contiguous shard of the trial ids
+        and the outcome histogram is all-reduced; per-trial outcomes stay per
+        rank (written to `output` with a `.rankR` suffix)."""
         n = self.trials if n is None else n
-        self.outcomes, self._hist = self.engine.run_trials(first_trial, n)
+        rank, world = 0, 1
+        if self.num_gpus > 1:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                rank, world = dist.get_rank(), dist.get_world_size()
+        lo, cnt = shard_range(n, world, rank)
+        self.first = first_trial + lo
+        self.outcomes, self._hist = self.engine.run_trials(self.first, cnt)
+        if world > 1:
+            import torch
+            self._hist = allreduce_histogram(self._hist, torch.device("cuda", torch.cuda.current_device()))
         if self.output:
-            np.save(self.output, self.outcomes)
+            np.save(self.output if world == 1 else f"{self.output}.rank{rank}", self.outcomes)
         return self.outcomes
 
     def histogram(self):

@@ -1,0 +1,41 @@
+# FaultCampaign SimObject -- drop-in campaign front end for gem5.
+#
+# Declared the way gem5 declares SimObjects (type / cxx_header / cxx_class /
+# Param.*; pattern of src/cpu/o3/BaseO3CPU.py:64-72) with Python-callable
+# methods exported through cxx_exports (src/cpu/BaseCPU.py:68-77, the same
+# mechanism SHREWD uses for setEnableShrewd).  Built into gem5 out of tree with
+#   scons build/RISCV/gem5.opt EXTRAS=/path/to/this/repo/src/gem5ext
+# (SConstruct:882-897).  The C++ side (fault_campaign.{hh,cc}) drives the
+# MI355X engine through the C ABI include/fi_engine.h via src/campaign/.
+from m5.params import *
+from m5.SimObject import PyBindMethod, SimObject
+
+
+class FaultCampaign(SimObject):
+    type = "FaultCampaign"
+    cxx_header = "gem5ext/fault_campaign.hh"
+    cxx_class = "gem5::FaultCampaign"
+    cxx_exports = [
+        PyBindMethod("run"),
+        PyBindMethod("summaryJson"),
+        PyBindMethod("setProtectMask"),
+        PyBindMethod("trialsRun"),
+    ]
+
+    workload = Param.String("RV64 static ELF run in SE mode")
+    cmd = VectorParam.String([], "argv of the workload (cmd[0] defaults to workload)")
+    env = VectorParam.String([], "environment of the workload")
+    trials = Param.UInt64(1000, "number of fault-injection trials")
+    first_trial = Param.UInt64(0, "first trial id (sites are keyed by (seed, trial id))")
+    seed = Param.UInt64(0x5EED0001, "campaign seed")
+    structures = VectorParam.String(
+        ["int_reg"], "fault targets: int_reg, pc, mem, xN or ABI register names")
+    burst = Param.UInt32(1, "adjacent bits flipped per fault (1..64)")
+    protect_mask = Param.UInt64(
+        0, "selective replication: protected x0..x31 (bits 0-31) and pc (bit 32)")
+    num_gpus = Param.UInt32(1, "MI355X devices used by this process")
+    first_gpu = Param.UInt32(0, "first HIP device ordinal")
+    max_insts_factor = Param.Float(
+        2.0, "hang cap: golden committed instructions x factor + 1000")
+    private_pages = Param.UInt32(16, "copy-on-write guest pages per trial")
+    output = Param.String("", "prefix for outcome/histogram files (empty: none)")

@@ -1,0 +1,69 @@
+#include "gem5ext/fault_campaign.hh"
+
+#include <stdexcept>
+
+#include "base/logging.hh"
+#include "campaign/campaign.hh"
+
+namespace gem5 {
+
+FaultCampaign::FaultCampaign(const Params &p) : SimObject(p) {}
+
+FaultCampaign::~FaultCampaign() = default;
+
+void
+FaultCampaign::init()
+{
+    SimObject::init();
+    shrewd::CampaignParams cp;
+    cp.workload = params().workload;
+    cp.cmd = params().cmd;
+    cp.env = params().env;
+    cp.trials = params().trials;
+    cp.first_trial = params().first_trial;
+    cp.seed = params().seed;
+    cp.structures = params().structures;
+    cp.burst = params().burst;
+    cp.protect_mask = params().protect_mask;
+    cp.num_gpus = params().num_gpus;
+    cp.first_device = params().first_gpu;
+    cp.max_insts_factor = params().max_insts_factor;
+    cp.private_pages = params().private_pages;
+    cp.output = params().output;
+    try {
+        campaign = std::make_unique<shrewd::Campaign>(cp);
+    } catch (const std::exception &e) {
+        // gem5 reports configuration/user errors with fatal() (base/logging.hh)
+        fatal("FaultCampaign %s: %s", name(), e.what());
+    }
+}
+
+void
+FaultCampaign::run()
+{
+    try {
+        campaign->run();
+    } catch (const std::exception &e) {
+        fatal("FaultCampaign %s: %s", name(), e.what());
+    }
+}
+
+std::string
+FaultCampaign::summaryJson() const
+{
+    return campaign->summaryJson();
+}
+
+void
+FaultCampaign::setProtectMask(uint64_t mask)
+{
+    campaign->setProtectMask(mask);
+}
+
+uint64_t
+FaultCampaign::trialsRun() const
+{
+    return campaign->histogram().trials;
+}
+
+} // namespace gem5

@@ -48,3 +48,23 @@ def engine_factory():
     yield make
     for e in cache.values():
         e.close()
+
+
+def np_histogram(sites, outcomes):
+    """Host restatement of fi_hist_kernel (test-side checker only)."""
+    import numpy as np
+    from shrewd_amd.fi import HIST_DT, N_STRUCT
+    h = np.zeros(1, HIST_DT)[0]
+    t = np.where(sites["target"] < N_STRUCT, sites["target"], 0).astype(np.int64)
+    m = sites["mask"].astype(np.uint64)
+    bit = np.zeros(len(m), np.int64)
+    nz = m != 0
+    low = m[nz] & (~m[nz] + np.uint64(1))
+    bit[nz] = np.log2(low.astype(np.float64)).round().astype(np.int64)
+    cls = np.where(outcomes["cls"] < 6, outcomes["cls"], 5).astype(np.int64)
+    np.add.at(h["counts"], (t, bit, cls), 1)
+    np.add.at(h["crash_sub"], (outcomes["sub"][cls == 2] & 15).astype(np.int64), 1)
+    np.add.at(h["escape_sub"], (outcomes["sub"][cls == 5] & 7).astype(np.int64), 1)
+    h["trials"] = len(sites)
+    h["guest_insts"] = int(outcomes["ninst"].astype(np.uint64).sum())
+    return h

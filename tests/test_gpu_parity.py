@@ -3,10 +3,12 @@
 Bar: bit-exact per-trial outcomes (class, sub-code, exit code, flags, detail,
 committed-instruction count) on the same seeded sites.
 """
+import os
+
 import numpy as np
 import pytest
 
-from conftest import WORKLOADS, workload_elf
+from conftest import ROOT, WORKLOADS, workload_elf
 
 pytestmark = pytest.mark.gpu
 
@@ -45,6 +47,20 @@ def test_decode_parity_32bit(engine_factory, oracle_mod):
     d = e.debug_decode(raws)
     names = [oracle_mod.mnemonic(int(r)) for r in raws]
     _check_decode(d, raws, names, oracle_mod)
+
+
+def test_decode_parity_gem5_vectors(engine_factory, oracle_mod):
+    """Device decoder against the oracle on every word of the gem5-decoder
+    fixture (the oracle itself is checked against it in test_oracle.py)."""
+    from test_oracle import load_decode_vectors
+    raws = load_decode_vectors()[0]
+    e = engine_factory("hello")
+    d = e.debug_decode(raws)
+    for i in range(len(raws)):
+        p = oracle_mod.probe(int(raws[i]), 0x10000, [0] * 32)
+        assert (d["op"][i], d["len"][i]) == (p.op, p.len), (hex(int(raws[i])), oracle_mod.mnemonic(int(raws[i])))
+        if p.rd > 0:
+            assert d["rd"][i] == p.rd, hex(int(raws[i]))
 
 
 def _check_decode(d, raws, names, oracle_mod):
@@ -164,3 +180,26 @@ def test_full_size_properties(engine_factory):
     # flips of x0..: the PC-flip crash share is large, register flips mostly masked
     out2, _ = e.run_trials(0, 100_000)
     assert np.array_equal(out, out2)   # deterministic
+
+
+def test_native_driver_matches_engine(engine_factory, tmp_path):
+    """src/campaign (the FaultCampaign SimObject's core) over the C ABI gives the
+    same per-trial outcomes and histogram as the Python binding."""
+    import subprocess
+    from shrewd_amd import HIST_DT, OUTCOME_DT
+    from shrewd_amd import build as b
+    exe = b.build_cli()
+    n, seed = 3000, 0x5EED0003
+    prefix = str(tmp_path / "camp")
+    r = subprocess.run([exe, "--workload", os.path.join(ROOT, "workloads", "crc32.elf"), "--cmd", "crc32",
+                        "--trials", str(n), "--seed", hex(seed), "--structures", "int_reg,pc,mem",
+                        "--output", prefix], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = np.fromfile(prefix + ".outcomes.bin", OUTCOME_DT)
+    hist = np.fromfile(prefix + ".hist.bin", HIST_DT)[0]
+    e = engine_factory("crc32")
+    e.set_campaign(seed, (1 << 34) - 2, 1)
+    e.set_protect(0)
+    ref, rh = e.run_trials(0, n)
+    assert out.tobytes() == ref.tobytes()
+    assert hist["counts"].tobytes() == rh["counts"].tobytes()

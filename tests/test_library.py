@@ -49,3 +49,23 @@ def test_structures_mask():
     assert structures_mask(["int_reg"]) == ((1 << 32) - 2)
     assert structures_mask(["pc", "mem"]) == (1 << 32) | (1 << 33)
     assert structures_mask(["a0", "sp", "x5"]) == (1 << 10) | (1 << 2) | (1 << 5)
+
+
+def test_native_driver_refuses_without_device():
+    """The C++ campaign driver (src/campaign) builds, links the engine and, with
+    no GPU visible, fails loudly instead of computing anything on the CPU."""
+    import subprocess
+    import torch
+    from shrewd_amd import build as b
+    if torch.cuda.is_available():
+        pytest.skip("GPU visible")
+    exe = b.build_cli()
+    r = subprocess.run([exe, "--workload", os.path.join(ROOT, "workloads", "hello.elf"), "--trials", "8"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 1 and "no HIP device" in r.stderr
+
+
+def test_structures_mask_names():
+    from shrewd_amd import structures_mask
+    assert structures_mask(["int_reg", "pc"]) == 0x1FFFFFFFE
+    assert structures_mask(["a0", "x5", "mem"]) == (1 << 10) | (1 << 5) | (1 << 33)

@@ -144,3 +144,35 @@ def test_unapplied_memory_site(oracle_mod):
     site["inst"], site["mask"], site["addr"], site["target"] = 10, 1, 0x100000000, 33
     res, out = o.run_one(site)
     assert res["cls"] == 0 and res["flags"] == 3
+
+
+def load_decode_vectors():
+    """tests/golden/decode_rv64.npz: instruction words and the class gem5's own
+    decoder (decoder.isa through the reference isa_parser) gives each; made by
+    tools/oracle/gen_decode_vectors.py."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "decode_rv64.npz"))
+    return z["raw"], z["leaf"], z["cls"], z["fmt"], z["mnem"]
+
+
+def test_decode_matches_gem5_decoder(oracle_mod):
+    raw, leaf, cls, fmt, mnem = load_decode_vectors()
+    assert len(raw) > 250_000 and len(cls) > 800
+    seen = {}
+    for r, lf in zip(raw.tolist(), leaf.tolist()):
+        seen.setdefault(lf, set()).add(oracle_mod.mnemonic(r))
+    executed = set()
+    for lf, names in seen.items():
+        # every gem5 class maps to exactly one oracle op ...
+        assert len(names) == 1, (cls[lf], names)
+        name = names.pop()
+        if cls[lf] == "Unknown":
+            assert name == "unknown"
+        elif name.startswith("escape:"):
+            # ... a class the engine does not execute ends the trial as an escape
+            assert name != "escape:UNKNOWN"
+        else:
+            # ... and an executed class carries gem5's own mnemonic
+            assert name == str(mnem[lf]), (cls[lf], name)
+            executed.add(name)
+    assert {"c_addi4spn", "addi", "ld", "sd", "jalr", "mulhsu", "sh3add_uw", "czero_nez",
+            "csrrw", "csrrci", "ecall", "fence_i", "prefetch_w"} <= executed

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Summarise a tools/gpu_profile.sh run into profiles/.
+
+Reads gpurun_out/{bench,prof_trace,prof_fetch,prof_write,prof_sq}_TAG and writes
+  profiles/TAG_bench.json           the bench JSON line
+  profiles/TAG_kernel_stats.csv     rocprofv3 --kernel-trace --stats summary
+  profiles/TAG_pmc.json             per-launch PMC values of fi_trial_kernel
+  profiles/pmc_traffic.json         HBM bytes per launch (read by bench.py)
+
+HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950
+FETCH_SIZE reports half the bytes of coalesced reads (MI355X_MICROARCH.md,
+"HBM [CDNA4]").  Only the campaign launches (grid > 64 lanes) are averaged;
+the one-lane golden run is excluded.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "fi_trial_kernel"
+
+
+def rows(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def per_launch(path, counter):
+    vals = [float(r["Counter_Value"]) for r in rows(path)
+            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter and int(r["Grid_Size"]) > 64]
+    return sum(vals) / len(vals) if vals else None, len(vals)
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    g = os.path.join(ROOT, "gpurun_out")
+    p = os.path.join(ROOT, "profiles")
+    os.makedirs(p, exist_ok=True)
+    with open(os.path.join(g, f"bench_{tag}.json")) as f:
+        bench = json.loads(f.read().strip().splitlines()[-1])
+    with open(os.path.join(p, f"{tag}_bench.json"), "w") as f:
+        json.dump(bench, f, indent=1)
+    shutil.copy(os.path.join(g, f"prof_trace_{tag}", "trace_kernel_stats.csv"),
+                os.path.join(p, f"{tag}_kernel_stats.csv"))
+    fetch, nf = per_launch(os.path.join(g, f"prof_fetch_{tag}", "fetch_counter_collection.csv"), "FETCH_SIZE")
+    write, nw = per_launch(os.path.join(g, f"prof_write_{tag}", "write_counter_collection.csv"), "WRITE_SIZE")
+    sq = {}
+    sqp = os.path.join(g, f"prof_sq_{tag}", "sq_counter_collection.csv")
+    for name in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
+                 "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"):
+        sq[name] = per_launch(sqp, name)[0]
+    trace = rows(os.path.join(g, f"prof_trace_{tag}", "trace_kernel_trace.csv"))
+    durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace
+            if KERNEL in r["Kernel_Name"] and int(r["Grid_Size_X"]) > 64]
+    hbm = (2 * fetch + write) * 1024 if fetch is not None and write is not None else None
+    wl = bench["config"]["workload"].split()[0]
+    pmc = {"tag": tag, "kernel": KERNEL, "launches_fetch": nf, "launches_write": nw,
+           "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write, "hbm_bytes_per_launch": hbm,
+           "trace_avg_ms": sum(durs) / len(durs) / 1e6 if durs else None, "trace_launches": len(durs),
+           "bench_avg_kernel_ms": bench["roofline"]["avg_kernel_ms"],
+           "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"], "sq": sq}
+    with open(os.path.join(p, f"{tag}_pmc.json"), "w") as f:
+        json.dump(pmc, f, indent=1)
+    with open(os.path.join(p, "pmc_traffic.json"), "w") as f:
+        json.dump({"tag": tag, "workload": wl, "trials": bench["config"]["trials_per_gpu"],
+                   "hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}_pmc.json"}, f, indent=1)
+    print(json.dumps(pmc, indent=1))
+
+
+if __name__ == "__main__":
+    main()
