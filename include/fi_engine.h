@@ -101,13 +101,21 @@ typedef struct {
     uint32_t private_pages;         /* copy-on-write pages per trial (0 -> 16) */
     uint32_t hang_factor_x16;       /* hang cap = golden_ninst * f / 16 + 1000 (0 -> 32) */
     uint32_t max_trials_per_launch; /* 0 -> 65536 */
+    uint32_t snapshot_interval;     /* golden snapshot every N committed insts (0 -> auto, >= 256) */
+    uint32_t flags;                 /* FI_CFG_* */
 } fi_config;
+/* fi_config.flags: trials start from process start / run to their natural end
+ * (the plain serial semantics, for A/B checks; outcomes are identical) */
+#define FI_CFG_NO_SNAPSHOT_START 1u
+#define FI_CFG_NO_EARLY_EXIT 2u
 
 typedef struct {
     uint64_t ninst, ncycles;
     uint32_t exit_code, pad;
     uint64_t stdout_len, stderr_len;
     uint64_t fetch_bytes, data_bytes;
+    uint64_t snapshots, snapshot_interval; /* golden snapshots kept on the device */
+    uint64_t snapshot_frames;              /* distinct 4 KiB frames behind them */
 } fi_golden_info;
 
 typedef struct {

@@ -5,8 +5,10 @@ import os
 import subprocess
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-SRCS = [os.path.join(ROOT, "csrc", "hip", "fi_kernels.hip"), os.path.join(ROOT, "csrc", "fi_engine.cpp")]
+SRCS = [os.path.join(ROOT, "csrc", "hip", "fi_kernels.hip"), os.path.join(ROOT, "csrc", "hip", "fi_trial.hip"),
+        os.path.join(ROOT, "csrc", "fi_engine.cpp")]
 DEPS = SRCS + [os.path.join(ROOT, "csrc", "fi_types.h"), os.path.join(ROOT, "csrc", "hip", "rv64_isa.h"),
+               os.path.join(ROOT, "csrc", "hip", "fi_device.h"),
                os.path.join(ROOT, "csrc", "gem5_decode_table.h"),
                os.path.join(os.path.dirname(ROOT), "include", "fi_engine.h")]
 REPO = os.path.dirname(ROOT)

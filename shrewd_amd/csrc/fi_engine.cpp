@@ -53,17 +53,25 @@ struct fi_engine {
     uint64_t text_lo = 0, text_hi = 0;
     std::vector<uint64_t> mem_pages;   // memory fault candidates (sorted)
 
-    // device image
+    // device image: snapshot 0 = the process-start image; the golden run
+    // appends snapshots 1..n-1
     PreInst *d_pre = nullptr;
-    uint64_t *d_base_vpn = nullptr;
-    uint32_t *d_base_frame = nullptr;
-    uint8_t *d_frames = nullptr, *d_zero = nullptr, *d_text = nullptr;
+    uint8_t *d_zero = nullptr, *d_text = nullptr;
     uint64_t *d_mem_pages = nullptr;
-    uint32_t n_base = 0;
+    std::vector<SnapState> snaps;
+    std::vector<PageEnt> tab;
+    std::vector<uint8_t> pool;            // host copy of the snapshot frames
+    uint32_t n_start_frames = 0;          // frames [0, n) = process-start pages
+    SnapState *d_snaps = nullptr;
+    PageEnt *d_tab = nullptr;
+    uint8_t *d_pool = nullptr;
+    uint64_t snap_I = 1ULL << 62;
+    bool pre_ok = true;
 
     // golden
     bool have_golden = false;
     fi_golden_info golden{};
+    uint32_t gdetail = 0;
     std::vector<uint8_t> gout, gerr;
     uint8_t *d_gout = nullptr, *d_gerr = nullptr;
 
@@ -146,9 +154,11 @@ static void free_work(fi_engine *e) {
     dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_priv); dfree(e->d_priv_vpn);
     e->cap = 0;
 }
+static void free_snaps(fi_engine *e) { dfree(e->d_snaps); dfree(e->d_tab); dfree(e->d_pool); }
 static void free_image(fi_engine *e) {
-    dfree(e->d_pre); dfree(e->d_base_vpn); dfree(e->d_base_frame); dfree(e->d_frames); dfree(e->d_zero);
+    dfree(e->d_pre); dfree(e->d_zero);
     dfree(e->d_text); dfree(e->d_mem_pages); dfree(e->d_gout); dfree(e->d_gerr);
+    free_snaps(e);
     e->have_golden = false;
     e->loaded = false;
 }
@@ -221,6 +231,18 @@ struct Mt64 {
     }
 };
 
+static fi_status upload_snaps(fi_engine *e) {
+    free_snaps(e);
+    HIPCHK(hipMalloc(&e->d_snaps, e->snaps.size() * sizeof(SnapState)));
+    HIPCHK(hipMalloc(&e->d_tab, std::max<size_t>(1, e->tab.size()) * sizeof(PageEnt)));
+    HIPCHK(hipMalloc(&e->d_pool, std::max<size_t>(kPage, e->pool.size())));
+    HIPCHK(hipMemcpy(e->d_snaps, e->snaps.data(), e->snaps.size() * sizeof(SnapState), hipMemcpyHostToDevice));
+    if (!e->tab.empty())
+        HIPCHK(hipMemcpy(e->d_tab, e->tab.data(), e->tab.size() * sizeof(PageEnt), hipMemcpyHostToDevice));
+    if (!e->pool.empty()) HIPCHK(hipMemcpy(e->d_pool, e->pool.data(), e->pool.size(), hipMemcpyHostToDevice));
+    return FI_OK;
+}
+
 fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *const *argv, const char *const *envp) {
     if (!e || !elf || !argv || !argv[0]) return fail(e, FI_E_ARG, "fi_load_elf: elf and argv[0] required");
     HIPCHK(hipSetDevice(e->dev));
@@ -253,6 +275,7 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
             for (uint64_t pg = paddr & ~(kPage - 1); pg < paddr + memsz; pg += kPage) wpages.push_back(pg);
     }
     if (xlo == ~0ULL) return fail(e, FI_E_ELF, "no executable segment");
+    if ((xlo >> 32) != ((xhi - 1) >> 32)) return fail(e, FI_E_ELF, "executable segments cross a 4 GiB boundary");
     e->text_lo = xlo;
     e->text_hi = xhi;
 
@@ -304,24 +327,35 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
     e->mem_pages = wpages;
     (void)max_addr;   // brk = roundUp(maxAddr) is not needed: brk() is an escape
 
-    // ---- upload: frames sorted by vpn, text pre-decode
-    std::vector<uint64_t> vpns;
-    std::vector<uint32_t> fidx;
-    std::vector<uint8_t> frames;
+    // ---- snapshot 0: the process-start image (frames sorted by vpn) and the
+    // initial architectural state (RiscvProcess::argsInit leaves every
+    // register 0 but sp; pc = e_entry)
+    e->pool.clear();
+    e->tab.clear();
+    e->snaps.clear();
     for (auto &kv : e->pages) {
-        vpns.push_back(kv.first);
-        fidx.push_back((uint32_t)(frames.size() / kPage));
-        frames.insert(frames.end(), kv.second.begin(), kv.second.end());
+        PageEnt pe{};
+        pe.vpn = kv.first;
+        pe.frame = (uint32_t)(e->pool.size() / kPage);
+        e->tab.push_back(pe);
+        e->pool.insert(e->pool.end(), kv.second.begin(), kv.second.end());
     }
-    e->n_base = (uint32_t)vpns.size();
-    HIPCHK(hipMalloc(&e->d_base_vpn, vpns.size() * 8));
-    HIPCHK(hipMalloc(&e->d_base_frame, fidx.size() * 4));
-    HIPCHK(hipMalloc(&e->d_frames, frames.size()));
+    e->n_start_frames = (uint32_t)e->tab.size();
+    SnapState s0{};
+    s0.regs[2] = e->sp0;
+    s0.pc = e->entry;
+    s0.stack_min = e->stack_min0;
+    s0.tab_off = 0;
+    s0.tab_n = (uint32_t)e->tab.size();
+    e->snaps.push_back(s0);
+    e->snap_I = 1ULL << 62;
+    e->pre_ok = true;
+    {
+        fi_status st = upload_snaps(e);
+        if (st) return st;
+    }
     HIPCHK(hipMalloc(&e->d_zero, kPage));
     HIPCHK(hipMalloc(&e->d_mem_pages, std::max<size_t>(1, wpages.size()) * 8));
-    HIPCHK(hipMemcpy(e->d_base_vpn, vpns.data(), vpns.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(e->d_base_frame, fidx.data(), fidx.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(e->d_frames, frames.data(), frames.size(), hipMemcpyHostToDevice));
     HIPCHK(hipMemset(e->d_zero, 0, kPage));
     if (!wpages.empty()) HIPCHK(hipMemcpy(e->d_mem_pages, wpages.data(), wpages.size() * 8, hipMemcpyHostToDevice));
     const uint64_t tbytes = e->text_hi - e->text_lo;
@@ -362,13 +396,18 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
 
 static DevCtx base_ctx(fi_engine *e) {
     DevCtx c{};
-    c.pre = e->d_pre; c.text_lo = e->text_lo; c.text_hi = e->text_hi;
-    c.base_vpn = e->d_base_vpn; c.base_frame = e->d_base_frame; c.frames = e->d_frames; c.zero_page = e->d_zero;
-    c.n_base = e->n_base;
-    c.entry = e->entry; c.sp0 = e->sp0; c.stack_min0 = e->stack_min0;
-    c.stack_vma_lo = e->svma_lo; c.stack_vma_hi = e->svma_hi;
+    c.pre = e->d_pre; c.text_lo = e->text_lo; c.text_hi = e->text_hi; c.pre_ok = e->pre_ok ? 1 : 0;
+    c.text_bytes = (uint32_t)(e->text_hi - e->text_lo);
+    c.snaps = e->d_snaps; c.snap_tab = e->d_tab; c.pool = e->d_pool; c.zero_page = e->d_zero;
+    const bool start = !(e->cfg.flags & FI_CFG_NO_SNAPSHOT_START);
+    c.n_snap = (uint32_t)e->snaps.size();
+    c.snap_start = start ? 1 : 0;
+    c.snap_interval = e->snap_I;
+    c.early_exit = (!(e->cfg.flags & FI_CFG_NO_EARLY_EXIT) && e->snaps.size() > 1) ? 1 : 0;
     c.gout = e->d_gout; c.gerr = e->d_gerr; c.gout_len = e->gout.size(); c.gerr_len = e->gerr.size();
     c.gexit = e->golden.exit_code;
+    c.gdetail = e->gdetail;
+    c.gninst = e->golden.ninst;
     c.priv_pages = e->cfg.private_pages;
     c.hang_cap = e->golden.ninst * e->cfg.hang_factor_x16 / 16 + 1000;
     c.protect_mask = e->protect;
@@ -377,53 +416,94 @@ static DevCtx base_ctx(fi_engine *e) {
     return c;
 }
 
+// One golden (fault-free, record-mode) launch: a single lane from snapshot 0.
+// P private pages; rec_* capture snapshots every rec_I instructions (0 = off).
+static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_t rec_max, SnapState *d_rs,
+                               uint8_t *d_rp, uint64_t *d_rv, uint32_t *d_trace, uint32_t trace_cap, uint8_t *d_ro,
+                               uint8_t *d_re, uint64_t rec_cap, fi_outcome &o, unsigned long long *stats) {
+    uint8_t *d_gpriv = nullptr;
+    uint64_t *d_gvpn = nullptr;
+    HIPCHK(hipMalloc(&d_gpriv, (uint64_t)P * kPage));
+    HIPCHK(hipMalloc(&d_gvpn, (uint64_t)P * 8));
+    DevCtx c = base_ctx(e);
+    c.record = 1;
+    c.early_exit = 0;
+    c.snap_start = 0;
+    c.rec_out = d_ro; c.rec_err = d_re; c.rec_cap = rec_cap;
+    c.hang_cap = 1ULL << 30;   // golden safety cap
+    c.priv_pages = P; c.priv_frames = d_gpriv; c.priv_vpn = d_gvpn;
+    c.rec_snaps = d_rs; c.rec_pages = d_rp; c.rec_vpns = d_rv; c.rec_interval = rec_I; c.rec_max_snaps = rec_max;
+    c.rec_trace = d_trace; c.rec_trace_cap = d_trace ? trace_cap : 0;
+    c.out = e->d_out;
+    c.n = 1;
+    c.sites = nullptr; c.perm = nullptr;
+    hipError_t err = hipMemsetAsync(e->d_stats, 0, 32 * sizeof(unsigned long long), e->stream);
+    if (err == hipSuccess) err = hipEventRecord(e->ev0, e->stream);
+    if (err == hipSuccess) err = launch_trials(c, e->stream);
+    if (err == hipSuccess) err = hipEventRecord(e->ev1, e->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(e->stream);
+    float ms = 0;
+    if (err == hipSuccess) err = hipEventElapsedTime(&ms, e->ev0, e->ev1);
+    if (err == hipSuccess) err = hipMemcpy(&o, e->d_out, sizeof o, hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(stats, e->d_stats, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    (void)hipFree(d_gpriv);
+    (void)hipFree(d_gvpn);
+    if (err != hipSuccess) return fail(e, FI_E_HIP, "golden launch: %s", hipGetErrorString(err));
+    e->last_ms = ms;
+    if (o.cls != FI_MASKED)
+        return fail(e, FI_E_GOLDEN, "golden run did not exit normally (class %u sub %u detail %#x after %llu insts)",
+                    o.cls, o.sub, o.detail, (unsigned long long)o.ninst);
+    return FI_OK;
+}
+
 fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     if (!e) return FI_E_ARG;
     if (!e->loaded) return fail(e, FI_E_STATE, "fi_golden_run: no workload loaded");
     HIPCHK(hipSetDevice(e->dev));
     fi_status st = ensure_work(e, 64);
     if (st) return st;
+    // back to the process-start image only
+    e->snaps.resize(1);
+    e->tab.resize(e->n_start_frames);
+    e->pool.resize((uint64_t)e->n_start_frames * kPage);
+    e->snap_I = 1ULL << 62;
+    e->pre_ok = true;
+    e->have_golden = false;
+    st = upload_snaps(e);
+    if (st) return st;
+
+    // ---- pass 1: the golden run itself (output, instruction count, footprint)
     const uint64_t rec_cap = 1 << 24;
+    const uint32_t kGoldenPages = 4096;   // 16 MiB of written pages
     uint8_t *d_rec_out = nullptr, *d_rec_err = nullptr;
     HIPCHK(hipMalloc(&d_rec_out, rec_cap));
     HIPCHK(hipMalloc(&d_rec_err, rec_cap));
-    DevCtx c = base_ctx(e);
-    c.record = 1;
-    c.rec_out = d_rec_out; c.rec_err = d_rec_err; c.rec_cap = rec_cap;
-    c.hang_cap = 1ULL << 30;   // golden safety cap
-    c.out = e->d_out;
-    c.n = 1;
-    c.sites = nullptr; c.perm = nullptr;
-    HIPCHK(hipMemsetAsync(e->d_stats, 0, 32 * sizeof(unsigned long long), e->stream));
-    HIPCHK(hipEventRecord(e->ev0, e->stream));
-    HIPCHK(launch_trials(c, e->stream));
-    HIPCHK(hipEventRecord(e->ev1, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
-    e->last_ms = ms;
     fi_outcome o;
     unsigned long long stats[32];
-    HIPCHK(hipMemcpy(&o, e->d_out, sizeof o, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(stats, e->d_stats, sizeof stats, hipMemcpyDeviceToHost));
-    if (o.cls != FI_MASKED) {
-        (void)hipFree(d_rec_out); (void)hipFree(d_rec_err);
-        return fail(e, FI_E_GOLDEN, "golden run did not exit normally (class %u sub %u detail %#x after %llu insts)",
-                    o.cls, o.sub, o.detail, (unsigned long long)o.ninst);
-    }
+    st = golden_launch(e, kGoldenPages, 0, 0, nullptr, nullptr, nullptr, nullptr, 0, d_rec_out, d_rec_err, rec_cap, o,
+                       stats);
+    if (st) { (void)hipFree(d_rec_out); (void)hipFree(d_rec_err); return st; }
+    const double golden_ms = e->last_ms;
     const uint64_t ol = stats[4], el = stats[5];
-    if (ol > rec_cap || el > rec_cap) return fail(e, FI_E_GOLDEN, "golden output exceeds %llu bytes", (unsigned long long)rec_cap);
+    const uint64_t gpages = stats[2];
+    if (ol > rec_cap || el > rec_cap) {
+        (void)hipFree(d_rec_out); (void)hipFree(d_rec_err);
+        return fail(e, FI_E_GOLDEN, "golden output exceeds %llu bytes", (unsigned long long)rec_cap);
+    }
+    if (gpages >= kGoldenPages) {
+        (void)hipFree(d_rec_out); (void)hipFree(d_rec_err);
+        return fail(e, FI_E_GOLDEN, "golden run writes more than %u pages", kGoldenPages);
+    }
     e->gout.assign(ol, 0);
     e->gerr.assign(el, 0);
     if (ol) HIPCHK(hipMemcpy(e->gout.data(), d_rec_out, ol, hipMemcpyDeviceToHost));
     if (el) HIPCHK(hipMemcpy(e->gerr.data(), d_rec_err, el, hipMemcpyDeviceToHost));
-    (void)hipFree(d_rec_out);
-    (void)hipFree(d_rec_err);
     dfree(e->d_gout); dfree(e->d_gerr);
     HIPCHK(hipMalloc(&e->d_gout, std::max<uint64_t>(ol, 1)));
     HIPCHK(hipMalloc(&e->d_gerr, std::max<uint64_t>(el, 1)));
     if (ol) HIPCHK(hipMemcpy(e->d_gout, e->gout.data(), ol, hipMemcpyHostToDevice));
     if (el) HIPCHK(hipMemcpy(e->d_gerr, e->gerr.data(), el, hipMemcpyHostToDevice));
+    e->golden = fi_golden_info{};
     e->golden.ninst = o.ninst;
     e->golden.ncycles = stats[3];
     e->golden.exit_code = o.exit_code;
@@ -431,6 +511,126 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     e->golden.stderr_len = el;
     e->golden.fetch_bytes = stats[0];
     e->golden.data_bytes = stats[1];
+    e->gdetail = o.detail;
+
+    // ---- pass 2: the same run again, capturing a snapshot every I committed
+    // instructions (state + every page written so far), within ~1 GiB
+    uint64_t I = std::max<uint64_t>(e->cfg.snapshot_interval ? e->cfg.snapshot_interval : 256, 16);
+    const uint32_t P = (uint32_t)std::max<uint64_t>(gpages, 1);
+    while (o.ninst / I + 2 > 65536 || (o.ninst / I + 2) * P * kPage > (1ULL << 30)) I *= 2;
+    const uint32_t rec_max = (uint32_t)(o.ninst / I + 2);
+    SnapState *d_rs = nullptr;
+    uint8_t *d_rp = nullptr;
+    uint64_t *d_rv = nullptr;
+    HIPCHK(hipMalloc(&d_rs, (uint64_t)rec_max * sizeof(SnapState)));
+    HIPCHK(hipMalloc(&d_rp, (uint64_t)rec_max * P * kPage));
+    HIPCHK(hipMalloc(&d_rv, (uint64_t)rec_max * P * 8));
+    // golden trace for the register liveness pass: one entry per committed
+    // instruction and ecall (capped; without it every register counts as live)
+    const uint32_t trace_cap = (uint32_t)std::min<uint64_t>(o.ninst + 4096, 1ULL << 26);
+    uint32_t *d_trace = nullptr;
+    HIPCHK(hipMalloc(&d_trace, (uint64_t)trace_cap * 4));
+    fi_outcome o2;
+    st = golden_launch(e, P, I, rec_max, d_rs, d_rp, d_rv, d_trace, trace_cap, d_rec_out, d_rec_err, rec_cap, o2,
+                       stats);
+    (void)hipFree(d_rec_out);
+    (void)hipFree(d_rec_err);
+    std::vector<SnapState> rs;
+    std::vector<uint8_t> rp;
+    std::vector<uint64_t> rv;
+    std::vector<uint32_t> trace;
+    std::vector<PreInst> pre;
+    uint32_t ns = 0;
+    const uint64_t n_events = stats[15];
+    if (!st && n_events <= trace_cap) {
+        trace.resize(n_events);
+        pre.resize((e->text_hi - e->text_lo) / 2);
+        hipError_t err = hipMemcpy(trace.data(), d_trace, n_events * 4, hipMemcpyDeviceToHost);
+        if (err == hipSuccess) err = hipMemcpy(pre.data(), e->d_pre, pre.size() * sizeof(PreInst), hipMemcpyDeviceToHost);
+        if (err != hipSuccess) st = fail(e, FI_E_HIP, "trace download: %s", hipGetErrorString(err));
+    }
+    (void)hipFree(d_trace);
+    if (!st) {
+        ns = (uint32_t)std::min<unsigned long long>(stats[13], rec_max);
+        rs.resize(ns);
+        rp.resize((uint64_t)ns * P * kPage);
+        rv.resize((uint64_t)ns * P);
+        hipError_t err = hipMemcpy(rs.data(), d_rs, ns * sizeof(SnapState), hipMemcpyDeviceToHost);
+        if (err == hipSuccess) err = hipMemcpy(rp.data(), d_rp, rp.size(), hipMemcpyDeviceToHost);
+        if (err == hipSuccess) err = hipMemcpy(rv.data(), d_rv, rv.size() * 8, hipMemcpyDeviceToHost);
+        if (err != hipSuccess) st = fail(e, FI_E_HIP, "snapshot download: %s", hipGetErrorString(err));
+    }
+    (void)hipFree(d_rs); (void)hipFree(d_rp); (void)hipFree(d_rv);
+    if (st) return st;
+    if (o2.ninst != o.ninst || o2.detail != o.detail || stats[13] != o.ninst / I + 1)
+        return fail(e, FI_E_GOLDEN, "golden capture pass diverged from the golden run");
+
+    // ---- host: deduplicate frames and build one sorted page table per snapshot
+    std::map<uint64_t, uint32_t> cur;   // vpn -> frame of its latest version
+    for (uint32_t i = 0; i < e->n_start_frames; i++) cur[e->tab[i].vpn] = e->tab[i].frame;
+    std::vector<SnapState> snaps;
+    std::vector<PageEnt> tab;
+    for (uint32_t k = 0; k < ns; k++) {
+        SnapState S = rs[k];
+        for (uint32_t i = 0; i < S.tab_n; i++) {
+            const uint64_t vpn = rv[(uint64_t)k * P + i];
+            const uint8_t *pg = rp.data() + (((uint64_t)k * P + i) << 12);
+            auto it = cur.find(vpn);
+            if (it != cur.end() && !memcmp(e->pool.data() + ((uint64_t)it->second << 12), pg, kPage)) continue;
+            const uint32_t f = (uint32_t)(e->pool.size() / kPage);
+            e->pool.insert(e->pool.end(), pg, pg + kPage);
+            cur[vpn] = f;
+            // the pre-decoded text stays valid only if the golden run never rewrites it
+            if ((vpn << 12) >= e->text_lo && (vpn << 12) < e->text_hi) {
+                auto org = e->pages.find(vpn);
+                if (org == e->pages.end() || memcmp(org->second.data(), pg, kPage)) e->pre_ok = false;
+            }
+        }
+        S.tab_off = (uint32_t)tab.size();
+        S.tab_n = (uint32_t)cur.size();
+        for (auto &kv : cur) {
+            PageEnt pe{};
+            pe.vpn = kv.first;
+            pe.frame = kv.second;
+            tab.push_back(pe);
+        }
+        snaps.push_back(S);
+    }
+    // ---- register liveness at each snapshot: backward over the golden trace,
+    // live = (live - writes) | reads; an ecall reads a0..a7.  Unknown entries
+    // (trace overflow, pc outside the pre-decoded text) leave every register live.
+    bool live_ok = !trace.empty() || n_events == 0;
+    std::vector<uint32_t> rmask(trace.size()), wmask(trace.size());
+    for (size_t i = 0; live_ok && i < trace.size(); i++) {
+        const uint32_t h = trace[i] & 0x7FFFFFFFu;
+        if (h >= pre.size() || !(pre[h].flags & kPreValid)) { live_ok = false; break; }
+        const PreInst &p = pre[h];
+        uint32_t r = 0, w = 0;
+        if ((p.flags & kPreRs1) && p.rs1) r |= 1u << p.rs1;
+        if ((p.flags & kPreRs2) && p.rs2) r |= 1u << p.rs2;
+        if (trace[i] & 0x80000000u) r |= 0x3FC00u;   // x10..x17
+        else if ((p.flags & kPreRd) && p.rd) w |= 1u << p.rd;
+        rmask[i] = r;
+        wmask[i] = w;
+    }
+    {
+        uint32_t live = 0;
+        int64_t ev = (int64_t)trace.size() - 1;
+        for (int64_t k = (int64_t)snaps.size() - 1; k >= 0; k--) {
+            if (!live_ok) { snaps[k].live = 0xFFFFFFFEu; continue; }
+            for (; ev >= (int64_t)snaps[k].trace_pos; ev--) live = (live & ~wmask[ev]) | rmask[ev];
+            snaps[k].live = live & ~1u;
+        }
+    }
+    e->snaps = snaps;
+    e->tab = tab;
+    e->snap_I = I;
+    st = upload_snaps(e);
+    if (st) return st;
+    e->last_ms = golden_ms;
+    e->golden.snapshots = e->snaps.size();
+    e->golden.snapshot_interval = I;
+    e->golden.snapshot_frames = e->pool.size() / kPage;
     e->have_golden = true;
     if (out) *out = e->golden;
     return FI_OK;

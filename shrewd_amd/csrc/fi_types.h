@@ -29,33 +29,67 @@ struct PreInst {
 static_assert(sizeof(PreInst) == 16, "PreInst must stay 16 bytes (one s_load_dwordx4)");
 constexpr uint8_t kPreValid = 1, kPreStraddle = 2, kPreRs1 = 4, kPreRs2 = 8, kPreRd = 16;
 
+// Golden snapshot: the architectural state at the top of the first tick with
+// numInst == k * snap_interval, plus the page table of the whole guest address
+// space at that point (process-start pages overlaid with the golden run's
+// written pages).  Trials start from the snapshot at or before their inject
+// time, and a trial whose state equals a later snapshot is masked (its future
+// is the golden future; deterministic machine).
+struct SnapState {
+    uint64_t regs[32];               // x0..x31 (x0 = 0)
+    uint64_t pc, ninst, ncyc, out_pos, err_pos, stack_min;
+    uint32_t tab_off, tab_n;         // entries [tab_off, tab_off + tab_n) of DevCtx::snap_tab
+    uint32_t live;                   // x_r whose value here the golden future reads before writing
+    uint32_t trace_pos;              // record mode: golden trace events before this snapshot
+};
+static_assert(sizeof(SnapState) == 320, "SnapState layout");
+// One mapped guest page of a snapshot: vpn -> frame in the snapshot pool.
+struct PageEnt {
+    uint64_t vpn;
+    uint32_t frame;                  // page index into DevCtx::pool
+    uint32_t pad;
+};
+
 // Everything one launch of the trial kernel needs.  Passed by value as the
 // kernel argument (lives in the kernarg segment -> scalar loads).
 struct DevCtx {
-    // golden text, pre-decoded
+    // golden text, pre-decoded (pre_ok = 0 if the golden run rewrote its text)
     const PreInst *pre;
     uint64_t text_lo, text_hi;       // page-aligned executable range
-    // base (process-start) image: sorted vpns -> frame index into frames
-    const uint64_t *base_vpn;
-    const uint32_t *base_frame;
-    const uint8_t *frames;
+    uint32_t pre_ok;
+    uint32_t text_bytes;             // text_hi - text_lo (< 4 GiB)
+    uint32_t record;                 // 1 = golden run: record output (and snapshots) instead of comparing
+    // snapshots: [0] is the process-start state (SE process image)
+    const SnapState *snaps;
+    const PageEnt *snap_tab;
+    const uint8_t *pool;             // snapshot frames, 4 KiB each
     const uint8_t *zero_page;
-    uint32_t n_base;
-    uint32_t record;                 // 1 = golden run: record output instead of comparing
-    // process start state
-    uint64_t entry, sp0, stack_min0, stack_vma_lo, stack_vma_hi;
+    uint64_t snap_interval;          // I: snapshot k is at numInst == k * I
+    uint32_t n_snap;
+    uint32_t early_exit;             // compare with snapshots after the injection
     // golden reference output (or record buffers in golden mode)
     const uint8_t *gout, *gerr;
     uint64_t gout_len, gerr_len;
     uint8_t *rec_out, *rec_err;
     uint64_t rec_cap;
-    uint32_t gexit;
+    uint32_t gexit, gdetail;         // golden exit code and final pc (low 32 bits)
+    uint64_t gninst;                 // golden numInst at exit
     uint32_t priv_pages;             // P
+    uint32_t snap_start;             // 1 = a wave starts at the snapshot before its earliest inject time
     uint64_t hang_cap;
     uint64_t protect_mask;
     // per-trial private (copy-on-write) pages: frames [slot][P][4096], vpns [P][n]
     uint8_t *priv_frames;
     uint64_t *priv_vpn;
+    // record mode: snapshot capture at numInst == k * rec_interval
+    SnapState *rec_snaps;            // [rec_max_snaps]
+    uint8_t *rec_pages;              // [rec_max_snaps][priv_pages][4096]
+    uint64_t *rec_vpns;              // [rec_max_snaps][priv_pages]
+    uint64_t rec_interval;
+    uint32_t rec_max_snaps;
+    uint32_t rec_trace_cap;          // entries of rec_trace
+    uint32_t *rec_trace;             // halfword index (pc - text_lo) / 2 of every committed instruction and
+                                     // ecall of the golden run, for the host's register liveness pass
     // the work
     const fi_site *sites;            // in trial order
     const uint32_t *perm;            // launch slot -> index into sites/out (sorted by site.inst)
@@ -63,6 +97,8 @@ struct DevCtx {
     uint64_t n;                      // trials in this launch
     unsigned long long *stats;       // [0] fetch B [1] data B [2] pages [3..5] golden ncycles/out/err
                                      // [6] loop iterations [7] lane-insts [8] slow fetches [9] min-PC [10] max iter/wave
+                                     // [11] early-exit checks [12] early exits [13] snapshots captured [14] start-inst sum
+                                     // [15] golden trace events [20] wave-0 s_memtime delta [21] s_memrealtime delta
 };
 
 struct SampleCtx {

@@ -1,0 +1,1124 @@
+// fi_trial.hip -- the batched RV64 interpreter of the fault-injection campaign
+// (CDNA4 / gfx950).  One trial per lane; a 64-lane wave runs 64 trials that
+// are sorted by inject time.  The loop body is AtomicSimpleCPU::tick
+// (src/cpu/simple/atomic.cc:611-739) with the golden-trace comparator and the
+// outcome classifier folded into the syscall/exit path.
+//
+//   * Golden snapshots: a wave starts at the golden snapshot at
+//     or before the earliest inject time of its lanes instead of at process
+//     start, and a lane whose whole architectural state (pc, x1..x31, output
+//     positions, stack limit, every mapped page) equals the golden state at a
+//     later snapshot is classified masked on the spot: the machine is
+//     deterministic, so its future is the golden future.  Both are exact; the
+//     oracle (oracle/rv64se.c) runs every trial from process start.
+//   * Registers live in LDS as R[row][lane] (row 32 = write sink for
+//     instructions without a destination, so the write is unconditional).
+//   * Guest memory: read-only snapshot frames shared by the whole launch +
+//     per-trial copy-on-write pages; a 4-entry per-lane TLB in VGPRs in front
+//     of the lane's private-page list and the snapshot's page table.
+//   * Fast path: while a group of lanes is converged on the pre-decoded golden
+//     text, the guest PC lives in SGPRs and each instruction is one scalar
+//     dispatch; the pre-decoded entries of both successors are prefetched with
+//     scalar loads while the current instruction executes.
+#include <hip/hip_runtime.h>
+
+#include "../fi_types.h"
+#include "fi_device.h"
+#include "rv64_isa.h"
+
+namespace fi {
+
+constexpr uint64_t kNone = ~0ULL;
+constexpr uint32_t kSinkRow = 32;
+constexpr uint32_t kRows = 33;
+
+// The launch context is read through an opaque pointer into the kernarg
+// segment (constant address space -> scalar loads) at each use instead of
+// being held in SGPRs for the whole kernel: the interpreter's hot loop needs
+// those SGPRs, and spilling them forced a wait on every prefetch.
+typedef __attribute__((address_space(4))) const DevCtx KCtx;
+__device__ __forceinline__ KCtx *opq(KCtx *p) {
+    asm volatile("" : "+s"(p));
+    return p;
+}
+
+// ------------------------------------------------------------------ memory
+struct LaneMem {
+    uint64_t stack_min;
+    uint64_t tv0, tv1, tv2, tv3;   // TLB vpns (kNone = empty)
+    uint64_t tp0, tp1, tp2, tp3;   // page address | 1 if the page is the lane's private copy
+    uint32_t tnext;
+    uint32_t n_priv;
+    uint64_t req_vpn;              // pending copy-on-write, kNone = none
+    const uint8_t *req_src;
+    bool code_dirty;
+};
+
+// The start snapshot's page table (wave-uniform).
+struct WaveMem {
+    const PageEnt *tab;
+    uint32_t tab_n;
+};
+
+__device__ __forceinline__ uint8_t *priv_frame(KCtx *c, uint64_t slot, uint32_t i) {
+    return c->priv_frames + ((slot * c->priv_pages + i) << 12);
+}
+
+__device__ __forceinline__ uint64_t tlb_find(const LaneMem &m, uint64_t vpn) {
+    uint64_t r = 0;
+    r = m.tv0 == vpn ? m.tp0 : r;
+    r = m.tv1 == vpn ? m.tp1 : r;
+    r = m.tv2 == vpn ? m.tp2 : r;
+    r = m.tv3 == vpn ? m.tp3 : r;
+    return r;
+}
+__device__ __forceinline__ void tlb_flush(LaneMem &m) { m.tv0 = m.tv1 = m.tv2 = m.tv3 = kNone; }
+__device__ __forceinline__ void tlb_insert(LaneMem &m, uint64_t vpn, uint64_t p) {
+    const uint32_t k = m.tnext & 3;
+    m.tv0 = k == 0 ? vpn : m.tv0; m.tp0 = k == 0 ? p : m.tp0;
+    m.tv1 = k == 1 ? vpn : m.tv1; m.tp1 = k == 1 ? p : m.tp1;
+    m.tv2 = k == 2 ? vpn : m.tv2; m.tp2 = k == 2 ? p : m.tp2;
+    m.tv3 = k == 3 ? vpn : m.tv3; m.tp3 = k == 3 ? p : m.tp3;
+    m.tnext++;
+}
+
+// Binary search of a snapshot page table (sorted by vpn): frame or -1.
+__device__ __forceinline__ int64_t tab_find(const PageEnt *t, uint32_t n, uint64_t vpn) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (t[mid].vpn < vpn) lo = mid + 1; else hi = mid;
+    }
+    return (lo < n && t[lo].vpn == vpn) ? (int64_t)t[lo].frame : -1;
+}
+
+// SE translation = EmulationPageTable::translate (src/mem/page_table.cc:143-153)
+// over the lane's page set: its private pages, then the start snapshot's
+// pages, then the stack pages [stack_min, top] that MemState::fixupFault
+// (src/sim/mem_state.cc:387-447) has mapped and nobody has written (zero).
+// Returns the page address | 1 for a private (writable) page, 0 if unmapped.
+__device__ uint64_t lookup_full(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t vpn) {
+    uint64_t p = 0;
+    for (uint32_t i = 0; i < m.n_priv; i++) {
+        if (c->priv_vpn[(uint64_t)i * c->n + slot] == vpn) { p = (uint64_t)priv_frame(c, slot, i) | 1; break; }
+    }
+    if (!p) {
+        const int64_t f = tab_find(w.tab, w.tab_n, vpn);
+        if (f >= 0) p = (uint64_t)(c->pool + ((uint64_t)f << 12));
+        else if (vpn >= (m.stack_min >> 12) && vpn <= kStackTopVpn) p = (uint64_t)c->zero_page;
+    }
+    if (p) tlb_insert(m, vpn, p);
+    return p;
+}
+__device__ __forceinline__ uint64_t lookup(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot,
+                                           uint64_t vpn) {
+    const uint64_t p = tlb_find(m, vpn);
+    return p ? p : lookup_full(c, w, m, slot, vpn);
+}
+__device__ __forceinline__ const uint8_t *page_of(uint64_t p) { return (const uint8_t *)(p & ~1ULL); }
+
+enum { F_NONE = 0, F_SYSCALL, F_BREAK, F_ILLEGAL, F_UNKNOWN, F_ESCAPE, F_ESCCSR, F_PGFAULT, F_NEEDPAGE, F_DETECT };
+
+// AtomicSimpleCPU::readMem/writeMem (atomic.cc:331-544): the access is split
+// at 64-byte line boundaries, each fragment translated on its own; faults are
+// raised in fragment order.  Writes to a shared page request a copy-on-write
+// page first (not a gem5 event: the tick is retried).
+__device__ int mem_access(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t ea,
+                          uint32_t size, bool wr, uint64_t &val, uint64_t &fva) {
+    uint32_t n1 = 64 - (uint32_t)(ea & 63);
+    if (n1 > size) n1 = size;
+    if (ea + n1 - 1 < ea) { fva = ea; return F_PGFAULT; }
+    const uint64_t p1 = lookup(c, w, m, slot, ea >> 12);
+    if (!p1) { fva = ea; return F_PGFAULT; }
+    const uint64_t ea2 = ea + n1;
+    uint64_t p2 = p1;
+    if (n1 < size) {
+        if (ea2 + (size - n1) - 1 < ea2) { fva = ea2; return F_PGFAULT; }
+        p2 = lookup(c, w, m, slot, ea2 >> 12);
+        if (!p2) { fva = ea2; return F_PGFAULT; }
+    }
+    const uint32_t off = (uint32_t)(ea & 4095);
+    if (wr) {
+        if (!(p1 & 1)) { m.req_vpn = ea >> 12; m.req_src = page_of(p1); return F_NEEDPAGE; }
+        if (!(p2 & 1)) { m.req_vpn = ea2 >> 12; m.req_src = page_of(p2); return F_NEEDPAGE; }
+        uint8_t *w1 = const_cast<uint8_t *>(page_of(p1));
+        if (n1 == size && (off & (size - 1)) == 0) {
+            switch (size) {
+            case 1: w1[off] = (uint8_t)val; break;
+            case 2: *(uint16_t *)(w1 + off) = (uint16_t)val; break;
+            case 4: *(uint32_t *)(w1 + off) = (uint32_t)val; break;
+            default: *(uint64_t *)(w1 + off) = val; break;
+            }
+        } else {
+            uint8_t *w2 = const_cast<uint8_t *>(page_of(p2));
+            for (uint32_t i = 0; i < size; i++) (i < n1 ? w1 : w2)[(ea + i) & 4095] = (uint8_t)(val >> (8 * i));
+        }
+    } else {
+        const uint8_t *r1 = page_of(p1);
+        uint64_t v = 0;
+        if (n1 == size && (off & (size - 1)) == 0) {
+            switch (size) {
+            case 1: v = r1[off]; break;
+            case 2: v = *(const uint16_t *)(r1 + off); break;
+            case 4: v = *(const uint32_t *)(r1 + off); break;
+            default: v = *(const uint64_t *)(r1 + off); break;
+            }
+        } else {
+            const uint8_t *r2 = page_of(p2);
+            for (uint32_t i = 0; i < size; i++) v |= (uint64_t)(i < n1 ? r1 : r2)[(ea + i) & 4095] << (8 * i);
+        }
+        val = v;
+    }
+    return F_NONE;
+}
+
+// Slow-path fetch of one lane: Decoder::moreBytes + setupFetchRequest
+// (src/arch/riscv/decoder.cc:63-116, src/cpu/simple/base.cc:304-318).
+// Returns 0 ok, or F_PGFAULT with the faulting fetch address and the number of
+// ticks consumed (1 if the first word faulted, 2 if the second did).
+__device__ int fetch_lane(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t pc, uint32_t &raw,
+                          uint32_t &ticks, uint64_t &fva) {
+    const uint64_t w0 = pc & ~3ULL;
+    ticks = 1;
+    const uint64_t p0 = lookup(c, w, m, slot, w0 >> 12);
+    if (!p0) { fva = w0; return F_PGFAULT; }
+    const uint32_t word = *(const uint32_t *)(page_of(p0) + (w0 & 4095));
+    if ((pc & 3) == 0) {
+        raw = ((word & 3) != 3) ? (word & 0xFFFF) : word;
+        return F_NONE;
+    }
+    const uint32_t half = word >> 16;
+    if ((half & 3) != 3) { raw = half; return F_NONE; }
+    ticks = 2;
+    const uint64_t w1 = w0 + 4;
+    const uint64_t p1 = lookup(c, w, m, slot, w1 >> 12);
+    if (!p1) { fva = w1; return F_PGFAULT; }
+    const uint32_t word2 = *(const uint32_t *)(page_of(p1) + (w1 & 4095));
+    raw = half | ((word2 & 0xFFFF) << 16);
+    return F_NONE;
+}
+
+// ------------------------------------------------------------------ syscalls
+// RV64 Linux SE syscall table classification (src/arch/riscv/linux/
+// se_workload.cc:529-895); 0 absent, 1 unimplemented, 2 ignore, 3 escape,
+// 4 modelled.
+__device__ int sys_class(int num) {
+    if (num == 64 || num == 93 || num == 94 || (num >= 172 && num <= 178)) return 4;
+    const bool present = (num >= 0 && num <= 64) || (num >= 66 && num <= 243) || num == 258 ||
+                         (num >= 260 && num <= 287) || (num >= 424 && num <= 450) ||
+                         (num >= 1024 && num <= 1079) || num == 2011;
+    if (!present) return 0;
+    if (num == 99 || num == 100 || num == 101 || num == 124 || (num >= 133 && num <= 139) || num == 146 ||
+        num == 164 || (num >= 226 && num <= 233) || num == 235)
+        return 2;
+    switch (num) {   // gem5 handlers not modelled on the device (escape)
+    case 17: case 23: case 25: case 29: case 33: case 34: case 35: case 38: case 43: case 44: case 45: case 46:
+    case 47: case 48: case 49: case 52: case 55: case 56: case 57: case 59: case 61: case 62: case 63: case 66:
+    case 67: case 68: case 78: case 79: case 80: case 96: case 98: case 113: case 114: case 121: case 123:
+    case 131: case 153: case 154: case 160: case 163: case 165: case 166: case 168: case 169: case 179:
+    case 198: case 199: case 200: case 201: case 202: case 203: case 204: case 205: case 206: case 207:
+    case 208: case 209: case 210: case 211: case 212: case 214: case 215: case 216: case 220: case 221:
+    case 222: case 258: case 260: case 261: case 278: case 435:
+    case 1024: case 1025: case 1026: case 1027: case 1028: case 1029: case 1030: case 1031: case 1033:
+    case 1034: case 1035: case 1036: case 1037: case 1038: case 1039: case 1040: case 1041: case 1044:
+    case 1047: case 1048: case 1049: case 1050: case 1051: case 1052: case 1054: case 1055: case 1056:
+    case 1057: case 1058: case 1060: case 1062: case 1065: case 1067: case 1068:
+        return 3;
+    default:
+        return 1;
+    }
+}
+
+// U-mode CSR reachability (CSRExecute, src/arch/riscv/isa/formats/standard.isa:
+// 325-447 and the CSRData map, src/arch/riscv/regs/misc.hh:604-1241).
+__device__ __forceinline__ bool csr_u_accessible(uint32_t csr) {
+    if ((csr >> 8) & 3) return false;
+    return (csr >= 0x001 && csr <= 0x003) || (csr >= 0x008 && csr <= 0x00A) || csr == 0x00F || csr == 0x017 ||
+           (csr >= 0xC00 && csr <= 0xC1F) || (csr >= 0xC20 && csr <= 0xC22);
+}
+
+struct Lane {
+    uint64_t pc, ninst, ncyc;
+    uint64_t out_pos, err_pos;
+    uint64_t fetch_b, data_b;
+    uint64_t next_chk;            // next snapshot boundary to compare at (kNone = none)
+    uint32_t nfail;               // failed comparisons (back-off)
+    int watch;
+    bool out_bad, done;
+    uint8_t injected;
+    fi_outcome res;
+};
+
+__device__ __forceinline__ void finish(Lane &L, int cls, int sub, int code, uint32_t detail) {
+    L.done = true;
+    L.res.cls = (uint8_t)cls; L.res.sub = (uint8_t)sub; L.res.exit_code = (uint8_t)code;
+    L.res.flags = (uint8_t)((L.injected ? 1 : 0) | (L.injected == 2 ? 2 : 0));
+    L.res.detail = detail;
+    L.res.ninst = L.ninst;
+}
+
+#define RREG(r) R[(uint32_t)(r) * 64u + lane]
+
+// The syscall path of one lane: EmuLinux::syscall (se_workload.cc:95-106)
+// with the golden-output comparator folded into write().
+__device__ __forceinline__ void do_syscall(KCtx *c, const WaveMem &w, Lane &L, LaneMem &m, uint64_t slot,
+                                           uint64_t *R, uint32_t lane) {
+    const int num = (int)(uint32_t)RREG(17);
+    const int cls = sys_class(num);
+    if (cls == 0) { finish(L, FI_CRASH, FI_CRASH_SYSCALL_RANGE, 1, (uint32_t)num); return; }
+    if (cls == 1) { finish(L, FI_CRASH, FI_CRASH_SYSCALL_UNIMPL, 1, (uint32_t)num); return; }
+    if (cls == 3) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, (uint32_t)num); return; }
+    if (cls == 2) { RREG(10) = 0; return; }
+    switch (num) {
+    case 93: case 94: {  // exitImpl -> exitSimLoop(status & 0xff), sim/syscall_emul.cc:120-248
+        const int code = (int)(uint32_t)RREG(10) & 0xff;
+        if (c->record) {
+            finish(L, FI_MASKED, 0, code, (uint32_t)L.pc);
+            return;
+        }
+        const bool same = !L.out_bad && L.out_pos == c->gout_len && L.err_pos == c->gerr_len && code == (int)c->gexit;
+        finish(L, same ? FI_MASKED : FI_SDC, 0, code, (uint32_t)L.pc);
+        return;
+    }
+    case 172: case 178: RREG(10) = kPid; return;
+    case 173: RREG(10) = kPpid; return;
+    case 174: case 175: RREG(10) = kUid; return;
+    case 176: case 177: RREG(10) = kGid; return;
+    default: break;   // 64: write
+    }
+    // writeFunc (src/sim/syscall_emul.hh:2826-2860): int fd, buffer copied in
+    // through a non-allocating proxy (fatal on an unmapped byte), then compared
+    // with the golden stream at the current position.
+    const int fd = (int)(uint32_t)RREG(10);
+    const uint64_t buf = RREG(11), n = RREG(12);
+    if (fd < 0 || fd >= 1024) { finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, (uint32_t)L.pc); return; }
+    if (fd == 0) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, (uint32_t)L.pc); return; }
+    if (fd > 2) { RREG(10) = (uint64_t)(int64_t)-9; return; }
+    if (n > (1ULL << 31)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, (uint32_t)L.pc); return; }
+    if (n) {
+        const uint64_t last = buf + n - 1;
+        if (last < buf) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, (uint32_t)L.pc); return; }
+        for (uint64_t v = buf >> 12; v <= (last >> 12); v++) {
+            if (!lookup(c, w, m, slot, v)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, (uint32_t)L.pc); return; }
+        }
+        uint64_t &pos = fd == 1 ? L.out_pos : L.err_pos;
+        const uint8_t *gold = fd == 1 ? c->gout : c->gerr;
+        const uint64_t glen = fd == 1 ? c->gout_len : c->gerr_len;
+        uint8_t *rec = fd == 1 ? c->rec_out : c->rec_err;
+        uint64_t cur_vpn = kNone;
+        const uint8_t *pg = nullptr;
+        for (uint64_t i = 0; i < n; i++) {
+            const uint64_t a = buf + i;
+            if ((a >> 12) != cur_vpn) { cur_vpn = a >> 12; pg = page_of(lookup(c, w, m, slot, cur_vpn)); }
+            const uint8_t ch = pg[a & 4095];
+            const uint64_t p = pos + i;
+            if (c->record) {
+                if (p < c->rec_cap) rec[p] = ch;
+            } else if (p >= glen || gold[p] != ch) {
+                L.out_bad = true;
+            }
+        }
+        pos += n;
+    }
+    RREG(10) = n;
+}
+
+// ------------------------------------------------------------------ snapshots
+// Wave-cooperative 4 KiB comparison (all 64 lanes active): each lane compares
+// 64 bytes.
+__device__ __forceinline__ bool page_eq(const uint8_t *a, const uint8_t *b, uint32_t lane) {
+    if (a == b) return true;
+    const uint4 *x = (const uint4 *)a, *y = (const uint4 *)b;
+    bool eq = true;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint4 u = x[lane + 64 * k], v = y[lane + 64 * k];
+        eq = eq && u.x == v.x && u.y == v.y && u.z == v.z && u.w == v.w;
+    }
+    return __ballot(!eq) == 0;
+}
+
+// Is lane l's memory equal to the golden memory of snapshot S?  (wave-uniform
+// arguments, all lanes active).  The lane's page set is its private pages
+// over the start snapshot's table over zero stack pages; the golden one is
+// S's table over zero stack pages.  Called only once pc, registers, output
+// positions and stack limit already match, so the stack ranges agree.
+__device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32_t np, const SnapState *S,
+                               uint32_t lane) {
+    const PageEnt *tk = c->snap_tab + S->tab_off;
+    const uint32_t nk = S->tab_n;
+    const uint64_t smin = S->stack_min >> 12;
+    for (uint32_t i = 0; i < np; i++) {   // every page the lane has written
+        const uint64_t v = uni64(c->priv_vpn[(uint64_t)i * c->n + lslot]);
+        const int64_t f = tab_find(tk, nk, v);
+        const uint8_t *g = f >= 0 ? c->pool + ((uint64_t)f << 12)
+                                  : ((v >= smin && v <= kStackTopVpn) ? c->zero_page : nullptr);
+        if (!g) return false;
+        if (!page_eq(priv_frame(c, lslot, i), g, lane)) return false;
+    }
+    for (uint32_t e = 0; e < nk; e++) {   // golden pages the lane still sees through its start snapshot
+        const uint64_t v = uni64(tk[e].vpn);
+        const uint32_t f = uni32(tk[e].frame);
+        bool priv = false;
+        for (uint32_t i = 0; i < np; i++) priv = priv || c->priv_vpn[(uint64_t)i * c->n + lslot] == v;
+        if (priv) continue;
+        const int64_t fj = tab_find(w.tab, w.tab_n, v);
+        const uint8_t *lv = fj >= 0 ? c->pool + ((uint64_t)fj << 12)
+                                    : ((v >= smin && v <= kStackTopVpn) ? c->zero_page : nullptr);
+        if (!lv) return false;
+        if (!page_eq(lv, c->pool + ((uint64_t)f << 12), lane)) return false;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------ trial kernel
+// Diagnostic build only (-DFI_PROF): s_memtime stamps at the phase boundaries
+// of the fast loop, summed per wave into stats[24..27] (never in the shipped
+// library; a stamp waits for outstanding scalar/LDS loads, so it also shows
+// which phase absorbs those waits).
+#ifdef FI_PROF
+#define PSTAMP(k)                                               \
+    do {                                                        \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();       \
+        pacc[k] += _t - plast;                                  \
+        plast = _t;                                             \
+    } while (0)
+#else
+#define PSTAMP(k) do { } while (0)
+#endif
+
+typedef __attribute__((address_space(4))) const uint32_t const_u32;
+struct Pre4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ Pre4 pre_load(const PreInst *p) {
+    const const_u32 *q = (const const_u32 *)(uintptr_t)p;
+    Pre4 r;
+    r.x = q[0]; r.y = q[1]; r.z = q[2]; r.w = q[3];
+    return r;
+}
+
+// Pre-decoded entry of the instruction at pc: one unconditional scalar load,
+// and a separate in-text flag, so that a prefetch is not waited for until its
+// entry is used.  Odd pcs fetch like pc | 2 of their word:
+// key = (pc & ~1) | ((pc & 1) << 1).  The host guarantees that the text does
+// not cross a 4 GiB boundary (32-bit compares only: SALU has no 64-bit <).
+struct PreRef { Pre4 e; bool in; };
+struct TextRef { const PreInst *pre; uint32_t lo, hi, bytes; };
+__device__ __forceinline__ PreRef pre_entry(const TextRef &t, uint64_t pc) {
+    const uint32_t klo = ((uint32_t)pc & ~1u) | (((uint32_t)pc & 1u) << 1);
+    const uint32_t off = klo - t.lo;
+    PreRef r;
+    r.in = (uint32_t)(pc >> 32) == t.hi && off < t.bytes;
+    r.e = pre_load(t.pre + (r.in ? (off >> 1) : 0u));
+    return r;
+}
+
+// a < b for wave-uniform 64-bit values on the scalar unit (SALU compares are 32-bit)
+__device__ __forceinline__ bool ult64(uint64_t a, uint64_t b) {
+    const uint32_t ah = (uint32_t)(a >> 32), bh = (uint32_t)(b >> 32);
+    return ah < bh || (ah == bh && (uint32_t)a < (uint32_t)b);
+}
+
+__global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
+    (void)ctx_arg;
+    KCtx *const kc = (KCtx *)__builtin_amdgcn_kernarg_segment_ptr();
+#define CX (opq(kc))
+    __shared__ uint64_t R[kRows * 64];
+    const uint64_t t_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
+    const uint32_t lane = threadIdx.x;
+    const uint64_t slot = (uint64_t)blockIdx.x * 64 + lane;
+    const bool live = slot < CX->n;
+    fi_site s;
+    s.inst = kNone; s.mask = 0; s.addr = 0; s.target = 0; s.trial = 0;
+    uint32_t sidx = 0;
+    if (live && !CX->record) { sidx = CX->perm[slot]; s = CX->sites[sidx]; }
+
+    // ---- start snapshot: the last one at or before the wave's earliest
+    // inject time (lane 0 holds it: slots are sorted by inject time)
+    uint32_t j = 0;
+    if (!CX->record && CX->snap_start && CX->n_snap > 1) {
+        const uint64_t t0 = uni64(CX->sites[CX->perm[(uint64_t)blockIdx.x * 64]].inst);
+        const uint64_t k = t0 / CX->snap_interval;
+        j = (uint32_t)(k < CX->n_snap ? k : CX->n_snap - 1);
+    }
+    const SnapState *S0 = CX->snaps + j;
+    WaveMem w;
+    w.tab = CX->snap_tab + S0->tab_off;
+    w.tab_n = S0->tab_n;
+#pragma unroll
+    for (int r = 0; r < 32; r++) RREG(r) = S0->regs[r];
+    RREG(kSinkRow) = 0;
+
+    Lane L;
+    L.pc = S0->pc; L.ninst = S0->ninst; L.ncyc = S0->ncyc; L.out_pos = S0->out_pos; L.err_pos = S0->err_pos;
+    L.fetch_b = L.data_b = 0;
+    L.next_chk = kNone;
+    L.nfail = 0;
+    L.watch = -1; L.out_bad = false; L.done = !live; L.injected = (CX->record || !live) ? 1 : 0;
+    L.res.cls = 0; L.res.sub = 0; L.res.exit_code = 0; L.res.flags = 0; L.res.detail = 0; L.res.ninst = 0;
+    LaneMem m;
+    m.stack_min = S0->stack_min;
+    tlb_flush(m);
+    m.tp0 = m.tp1 = m.tp2 = m.tp3 = 0;
+    m.tnext = 0; m.n_priv = 0; m.req_vpn = kNone; m.req_src = nullptr; m.code_dirty = false;
+    const uint64_t start_inst = live ? L.ninst : 0;
+    uint64_t pages_made = 0;
+    uint64_t next_snap = (CX->record && CX->rec_interval) ? 0 : kNone;   // record mode: capture points
+    uint32_t snaps_taken = 0;
+    uint32_t tpos = 0;   // record mode: golden trace events so far (uniform)
+#ifdef FI_PROF
+    uint64_t pacc[4] = {0, 0, 0, 0};
+    uint64_t plast = __builtin_amdgcn_s_memtime();
+#endif
+    uint32_t n_iter = 0, n_slow = 0, n_min = 0, n_exec = 0, n_chk = 0, n_early = 0;   // per-wave (uniform)
+
+    for (;;) {
+        // ---- A. materialise requested pages, whole wave cooperating
+        const uint64_t want = __ballot(!L.done && m.req_vpn != kNone);
+        if (want) {
+            uint64_t wl = want;
+            while (wl) {
+                const int l = __ffsll((unsigned long long)wl) - 1;
+                wl &= wl - 1;
+                const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)m.n_priv, l);
+                if (np >= CX->priv_pages) continue;
+                const uint64_t lslot = readlane64(slot, l);
+                const uint4 *src = (const uint4 *)readlane64((uint64_t)m.req_src, l);
+                uint4 *dst = (uint4 *)priv_frame(CX, lslot, np);
+#pragma unroll
+                for (int k = 0; k < 4; k++) dst[lane + 64 * k] = src[lane + 64 * k];
+            }
+            __syncthreads();
+            if (!L.done && m.req_vpn != kNone) {
+                if (m.n_priv >= CX->priv_pages) {
+                    finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, (uint32_t)L.pc);
+                } else {
+                    CX->priv_vpn[(uint64_t)m.n_priv * CX->n + slot] = m.req_vpn;
+                    if ((m.req_vpn << 12) >= CX->text_lo && (m.req_vpn << 12) < CX->text_hi) m.code_dirty = true;
+                    m.n_priv++;
+                    pages_made++;
+                }
+                m.req_vpn = kNone;
+                tlb_flush(m);
+            }
+        }
+        // ---- B. tick-top events: fault injection and the max-insts (hang)
+        // exit both fire in serviceInstCountEvents at the first tick with
+        // numInst >= n (src/cpu/simple/base.cc:321-325, src/cpu/base.cc:764-770)
+        if (!L.done && !L.injected && L.ninst >= s.inst) {
+            if (s.target >= 1 && s.target <= 31) {
+                RREG(s.target) ^= s.mask;
+                if ((CX->protect_mask >> s.target) & 1) L.watch = (int)s.target;
+                L.injected = 1;
+            } else if (s.target == FI_T_PC) {
+                L.pc ^= s.mask;
+                L.injected = 1;
+                if ((CX->protect_mask >> 32) & 1) finish(L, FI_DETECTED, 0, 0, (uint32_t)L.pc);
+            } else if (s.target == FI_T_MEM) {
+                const uint64_t p = lookup(CX, w, m, slot, s.addr >> 12);
+                if (!p) {
+                    L.injected = 2;    // page not mapped at t: nothing to flip
+                } else if (!(p & 1)) {
+                    m.req_vpn = s.addr >> 12; m.req_src = page_of(p);   // copy-on-write first, flip next iteration
+                } else {
+                    uint64_t *wp = (uint64_t *)(const_cast<uint8_t *>(page_of(p)) + (s.addr & 4095));
+                    *wp ^= s.mask;
+                    L.injected = 1;
+                }
+            } else {
+                L.injected = 1;
+            }
+            if (L.injected && CX->early_exit) {
+                const uint64_t k = L.ninst / CX->snap_interval + 1;
+                L.next_chk = k < CX->n_snap ? k * CX->snap_interval : kNone;
+            }
+        }
+        if (!L.done && L.ninst >= CX->hang_cap) finish(L, FI_HANG, 1, 0, (uint32_t)L.pc);
+
+        // ---- B'. golden comparator at snapshot boundaries (exact early exit)
+        if (CX->early_exit) {
+            uint64_t pend = __ballot(!L.done && m.req_vpn == kNone && L.ninst == L.next_chk);
+            if (pend) __syncthreads();   // the lanes' own stores are complete before others read them
+            while (pend) {
+                const int ld = __ffsll((unsigned long long)pend) - 1;
+                const uint64_t kn = uni64(readlane64(L.ninst, ld));
+                const bool grp = !L.done && m.req_vpn == kNone && L.ninst == L.next_chk && L.ninst == kn;
+                pend &= ~__ballot(grp);
+                const SnapState *S = CX->snaps + (uint32_t)(kn / CX->snap_interval);
+                bool eq = grp && L.pc == S->pc && L.out_pos == S->out_pos && L.err_pos == S->err_pos && !L.out_bad &&
+                          m.stack_min == S->stack_min;
+                if (__ballot(eq)) {
+                    // a register the golden future writes before reading it cannot
+                    // influence the outcome (liveness from the golden trace)
+                    const uint32_t lv = S->live;
+#pragma unroll
+                    for (int r = 1; r < 32; r++) eq = eq && (RREG(r) == S->regs[r] || !((lv >> r) & 1));
+                }
+                n_chk += (uint32_t)__popcll(__ballot(grp));
+                uint64_t mm = __ballot(eq);
+                while (mm) {
+                    const int l = __ffsll((unsigned long long)mm) - 1;
+                    mm &= mm - 1;
+                    const bool same = lane_mem_equal(CX, w, readlane64(slot, l),
+                                                     (uint32_t)__builtin_amdgcn_readlane((int)m.n_priv, l), S, lane);
+                    if ((int)lane == l) eq = same;
+                }
+                if (grp) {
+                    if (eq) {
+                        finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
+                        L.res.ninst = CX->gninst;
+                    } else {
+                        // back off after repeated mismatches (any schedule is exact)
+                        const uint32_t sh = L.nfail < 4 ? 0 : (L.nfail < 7 ? L.nfail - 3 : 4);
+                        L.nfail++;
+                        const uint64_t nx = L.next_chk + (CX->snap_interval << sh);
+                        L.next_chk = nx / CX->snap_interval < CX->n_snap ? nx : kNone;
+                    }
+                }
+                n_early += (uint32_t)__popcll(__ballot(grp && eq));
+            }
+        }
+
+        // ---- B''. record mode: capture a golden snapshot (one live lane)
+        if (CX->record && uni64(readlane64(L.ninst, 0)) == next_snap && !__builtin_amdgcn_readlane((int)L.done, 0)) {
+            if (snaps_taken < CX->rec_max_snaps) {
+                SnapState *S = CX->rec_snaps + snaps_taken;
+                const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)m.n_priv, 0);
+                if (lane == 0) {
+#pragma unroll
+                    for (int r = 0; r < 32; r++) S->regs[r] = RREG(r);
+                    S->pc = L.pc; S->ninst = L.ninst; S->ncyc = L.ncyc; S->out_pos = L.out_pos; S->err_pos = L.err_pos;
+                    S->stack_min = m.stack_min; S->tab_off = 0; S->tab_n = np;
+                    S->live = 0; S->trace_pos = tpos;
+                }
+                for (uint32_t i = 0; i < np; i++) {
+                    if (lane == 0) CX->rec_vpns[(uint64_t)snaps_taken * CX->priv_pages + i] = CX->priv_vpn[i * CX->n];
+                    const uint4 *src = (const uint4 *)priv_frame(CX, 0, i);
+                    uint4 *dst = (uint4 *)(CX->rec_pages + (((uint64_t)snaps_taken * CX->priv_pages + i) << 12));
+#pragma unroll
+                    for (int k = 0; k < 4; k++) dst[lane + 64 * k] = src[lane + 64 * k];
+                }
+            }
+            snaps_taken++;
+            next_snap += CX->rec_interval;
+        }
+
+        const bool ready = !L.done && m.req_vpn == kNone;
+        const uint64_t act = __ballot(ready);
+        if (act == 0) {
+            if (__ballot(!L.done) == 0) break;
+            continue;
+        }
+        // ---- C. leader PC: first ready lane, or min-PC if the lanes diverged
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        uint64_t lpc = readlane64(L.pc, leader);
+        n_iter++;
+        if (__ballot(ready && L.pc == lpc) != act) { lpc = wave_min64(ready ? L.pc : kNone); n_min++; }
+        lpc = uni64(lpc);   // wave-uniform: keeps fetch/decode/dispatch on the scalar unit
+        bool mine = ready && L.pc == lpc;
+        // lanes of other groups wait; the group keeps the wave only while its PC
+        // stays below theirs (min-PC order, so groups merge when they meet)
+        const uint64_t wait_min = (__ballot(mine) != act) ? uni64(wave_min64((ready && !mine) ? L.pc : kNone)) : kNone;
+        // next instruction-count event of this lane: injection, snapshot
+        // comparison, hang cap, or (record mode) snapshot capture
+        uint64_t next_ev = CX->hang_cap;
+        if (!L.injected) next_ev = s.inst < next_ev ? s.inst : next_ev;
+        if (L.next_chk < next_ev) next_ev = L.next_chk;
+        if (next_snap < next_ev) next_ev = next_snap;
+
+        // ---- FAST PATH: the group is converged on golden text with nothing
+        // watched or modified -- run pre-decoded micro-ops with PC, instruction,
+        // cycle and byte counts in SGPRs until an event is due, the group
+        // diverges, meets another group, or hits something the general path owns
+        // (K_SLOW op, fault, page request, syscall).  Nothing commits unless the
+        // whole instruction commits for every group lane.
+        if (CX->pre_ok && lpc >= CX->text_lo && lpc < CX->text_hi &&
+            __ballot(mine && (m.code_dirty || L.watch > 0)) == 0) {
+            const uint64_t gm = __ballot(mine);
+            const int glane = __ffsll((unsigned long long)gm) - 1;
+            uint64_t budget64 = uni64(wave_min64(mine ? next_ev - L.ninst : kNone));
+            const uint32_t budget = budget64 > (1u << 30) ? (1u << 30) : (uint32_t)budget64;
+            uint64_t spc = lpc;
+            uint32_t steps = 0, xticks = 0, fbytes = 0, dbytes = 0;
+            bool div = false;
+            TextRef tx;
+            tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
+            tx.bytes = CX->text_bytes;
+            PreRef E = pre_entry(tx, spc);
+            while (budget) {
+                PSTAMP(3);
+                spc = uni64(spc);
+                const uint32_t q1 = uni32(E.e.y), q2 = uni32(E.e.z), q3 = uni32(E.e.w);
+                const uint32_t aux = q3 >> 16, kind = aux & 63;
+                if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
+                const uint32_t rd = q1 >> 8 & 0xFF, rs1 = q1 >> 16 & 0xFF, rs2 = q1 >> 24;
+                const int64_t imm = (int32_t)q2;
+                const uint32_t len = q3 & 0xFF, straddle = ((q3 >> 8) & kPreStraddle) ? 1 : 0;
+                const uint64_t a0 = RREG(rs1), b0 = RREG(rs2);
+                // prefetch the successors' entries while this instruction executes
+                const uint64_t ft = spc + len;
+                const PreRef Eft = pre_entry(tx, ft);
+                const PreRef Etg = pre_entry(tx, spc + imm);   // unconditional: no phi, no early wait
+                const uint64_t av = (aux & U_APC) ? spc : a0;
+                const uint64_t bv = (aux & U_BIMM) ? (uint64_t)imm : b0;
+#ifdef FI_PROF
+                asm volatile("" :: "v"(av), "v"(bv));
+                PSTAMP(0);
+#endif
+                const bool w32 = aux & U_W32;
+                const uint32_t shm = w32 ? 31 : 63;
+                uint64_t v = 0, npc = ft;
+                uint32_t msz = 0;
+                bool wr = true, took = false, ind = false;
+                switch (kind) {
+                case K_ADD: v = av + bv; break;
+                case K_SUB: v = av - bv; break;
+                case K_AND: v = av & bv; break;
+                case K_OR: v = av | bv; break;
+                case K_XOR: v = av ^ bv; break;
+                case K_SLT: v = (int64_t)av < (int64_t)bv ? 1 : 0; break;
+                case K_SLTU: v = av < bv ? 1 : 0; break;
+                case K_SLL: v = av << (bv & shm); break;
+                case K_SRL: v = (w32 ? (av & 0xFFFFFFFFULL) : av) >> (bv & shm); break;
+                case K_SRA: v = (uint64_t)((w32 ? (int64_t)(int32_t)av : (int64_t)av) >> (bv & shm)); break;
+                case K_MUL: v = av * bv; break;
+                case K_NOP: wr = false; break;
+                case K_JAL: v = ft; npc = spc + imm; took = true; break;
+                case K_JALR: {
+                    v = ft;
+                    const uint64_t t = (a0 + imm) & ~1ULL;
+                    const uint64_t t0 = readlane64(t, glane);
+                    if (__ballot(mine && t != t0) == 0) { npc = uni64(t0); ind = true; }
+                    else { div = true; if (mine) L.pc = t; }
+                    break;
+                }
+                case K_BEQ: case K_BNE: case K_BLT: case K_BGE: case K_BLTU: case K_BGEU: {
+                    wr = false;
+                    bool cnd;
+                    switch (kind) {
+                    case K_BEQ: cnd = a0 == b0; break;
+                    case K_BNE: cnd = a0 != b0; break;
+                    case K_BLT: cnd = (int64_t)a0 < (int64_t)b0; break;
+                    case K_BGE: cnd = (int64_t)a0 >= (int64_t)b0; break;
+                    case K_BLTU: cnd = a0 < b0; break;
+                    default: cnd = a0 >= b0; break;
+                    }
+                    const uint64_t tk = __ballot(mine && cnd);
+                    if (tk == gm) { npc = spc + imm; took = true; }
+                    else if (tk != 0) { div = true; if (mine) L.pc = cnd ? spc + imm : ft; }
+                    break;
+                }
+                default: {   // K_LOAD / K_STORE: the whole access inside one mapped page
+                    const bool st = kind == K_STORE;
+                    msz = 1u << ((aux >> 12) & 3);
+                    const uint64_t ea = a0 + imm;
+                    const uint32_t off = (uint32_t)(ea & 4095);
+                    uint64_t p = 0;
+                    if (mine) {
+                        p = tlb_find(m, ea >> 12);
+                        if (!p) p = lookup_full(CX, w, m, slot, ea >> 12);
+                    }
+                    const bool ok = p && (!st || (p & 1)) && off + msz <= 4096;
+                    if (__ballot(mine && !ok) != 0) { msz = 0xFFFFFFFFu; break; }   // bail: general path
+                    if (mine) {
+                        uint8_t *pg = const_cast<uint8_t *>(page_of(p));
+                        const bool al = (off & (msz - 1)) == 0;
+                        if (st) {
+                            if (al) {
+                                switch (msz) {
+                                case 1: pg[off] = (uint8_t)b0; break;
+                                case 2: *(uint16_t *)(pg + off) = (uint16_t)b0; break;
+                                case 4: *(uint32_t *)(pg + off) = (uint32_t)b0; break;
+                                default: *(uint64_t *)(pg + off) = b0; break;
+                                }
+                            } else {
+                                for (uint32_t i = 0; i < msz; i++) pg[off + i] = (uint8_t)(b0 >> (8 * i));
+                            }
+                        } else {
+                            uint64_t t = 0;
+                            if (al) {
+                                switch (msz) {
+                                case 1: t = pg[off]; break;
+                                case 2: t = *(const uint16_t *)(pg + off); break;
+                                case 4: t = *(const uint32_t *)(pg + off); break;
+                                default: t = *(const uint64_t *)(pg + off); break;
+                                }
+                            } else {
+                                for (uint32_t i = 0; i < msz; i++) t |= (uint64_t)pg[off + i] << (8 * i);
+                            }
+                            v = (aux & U_SEXT) ? (uint64_t)sext64(t, 8 * msz) : t;
+                        }
+                    }
+                    if (st) wr = false;
+                    break;
+                }
+                }
+                if (msz == 0xFFFFFFFFu) break;            // nothing committed for this instruction
+#ifdef FI_PROF
+                asm volatile("" :: "v"(v));
+                PSTAMP(1);
+#endif
+                if (w32) v = sx32(v);
+                const uint32_t row = (wr && rd) ? rd : kSinkRow;
+                if (mine) RREG(row) = v;
+                if (CX->record) {   // golden trace for the liveness pass (one lane, uniform)
+                    if (tpos < CX->rec_trace_cap && lane == 0)
+                        CX->rec_trace[tpos] = (((uint32_t)spc & ~1u) | (((uint32_t)spc & 1u) << 1)) - tx.lo >> 1;
+                    tpos++;
+                }
+                steps++; xticks += straddle; fbytes += len; dbytes += msz;
+                if (div) break;
+                spc = npc;
+                E = ind ? pre_entry(tx, npc) : (took ? Etg : Eft);
+                PSTAMP(2);
+                if (steps >= budget || !ult64(spc, wait_min)) break;
+            }
+            if (steps) {
+                if (mine) {
+                    L.ninst += steps; L.ncyc += steps + xticks; L.fetch_b += fbytes; L.data_b += dbytes;
+                    if (!div) L.pc = spc;
+                }
+                n_iter += steps;
+                n_exec += steps * (uint32_t)__popcll(gm);
+                continue;
+            }
+        }
+
+        // ---- inner loop: one guest instruction per iteration while the group
+        // stays converged, with no event due and no page request pending
+        for (;;) {
+        // ---- D. fetch + decode (wave-uniform)
+        Dec d;
+        uint32_t ticks = 1;
+        bool fast = false;
+        const uint64_t key = (lpc & 3) ? ((lpc & ~3ULL) | 2) : lpc;
+        if (CX->pre_ok && key >= CX->text_lo && key < CX->text_hi && __ballot(mine && m.code_dirty) == 0) {
+            const Pre4 q = pre_load(CX->pre + ((key - CX->text_lo) >> 1));
+            const uint32_t pflags = (q.w >> 8) & 0xFF;
+            if (pflags & kPreValid) {
+                fast = true;
+                d.raw = q.x; d.op = (uint8_t)q.y; d.rd = (uint8_t)(q.y >> 8); d.rs1 = (uint8_t)(q.y >> 16);
+                d.rs2 = (uint8_t)(q.y >> 24); d.imm = (int32_t)q.z; d.len = (uint8_t)q.w;
+                d.flags = (uint8_t)pflags; d.aux = (uint16_t)(q.w >> 16);
+                ticks = (pflags & kPreStraddle) ? 2 : 1;
+            }
+        }
+        if (!fast) {
+            n_slow++;
+            uint32_t raw = 0, t = 1;
+            uint64_t fva = 0;
+            if (mine) {
+                const int fr = fetch_lane(CX, w, m, slot, L.pc, raw, t, fva);
+                if (fr) {
+                    // the faulting tick(s) count, nothing commits; decoder reset;
+                    // GenericPageTableFault::invoke -> fixupFault (sim/faults.cc:95-105)
+                    L.ncyc += t;
+                    mine = false;
+                    if (fva < m.stack_min && fva >= kStackBase - kMaxStack) {
+                        const uint64_t nm = fva & ~4095ULL;
+                        if (kStackBase - nm > kMaxStack) finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, (uint32_t)L.pc);
+                        else m.stack_min = nm;
+                    } else {
+                        finish(L, FI_CRASH, FI_CRASH_PAGE_FAULT, 134, (uint32_t)fva);
+                    }
+                }
+            }
+            const uint64_t okm = __ballot(mine);
+            if (okm == 0) break;
+            const int ld = __ffsll((unsigned long long)okm) - 1;
+            const uint32_t lraw = (uint32_t)__builtin_amdgcn_readlane((int)raw, ld);
+            const uint32_t lt = (uint32_t)__builtin_amdgcn_readlane((int)t, ld);
+            mine = mine && raw == lraw;
+            d = rv_decode(lraw);
+            ticks = lt;
+        }
+        // force every decoded field into SGPRs: the op switch below must be a
+        // scalar branch tree, never a per-lane waterfall
+        d.op = (uint8_t)uni32(d.op); d.rd = (uint8_t)uni32(d.rd); d.rs1 = (uint8_t)uni32(d.rs1);
+        d.rs2 = (uint8_t)uni32(d.rs2); d.len = (uint8_t)uni32(d.len); d.flags = (uint8_t)uni32(d.flags);
+        d.imm = (int32_t)uni32((uint32_t)d.imm); d.aux = (uint16_t)uni32(d.aux); d.raw = uni32(d.raw);
+        ticks = uni32(ticks);
+        const uint64_t gmask = __ballot(mine);
+        n_exec += (uint32_t)__popcll(gmask);
+        int f = F_NONE;
+        if (mine) {
+        // ---- E. execute: the generated StaticInst::execute bodies of
+        // src/arch/riscv/isa/decoder.isa for the modelled subset
+        const uint64_t pc = L.pc;
+        const uint64_t a = RREG(d.rs1), b = RREG(d.rs2);
+        const int64_t imm = d.imm;
+        uint64_t npc = pc + d.len;
+        uint64_t v = 0, fva = 0, t = 0;
+        bool wrd = true;
+        uint32_t msz = 0, mext = 0;   // memory access size / sign-extension width (uniform)
+        bool mst = false;
+        // detected-by-replica: the flipped protected register is read before
+        // being overwritten (build-defined SHREWD semantics)
+        if (L.watch > 0 &&
+            (((d.flags & kPreRs1) && d.rs1 == L.watch) || ((d.flags & kPreRs2) && d.rs2 == L.watch) ||
+             (d.op == OP_ecall && (L.watch == 17 || (L.watch >= 10 && L.watch <= 15))))) {
+            f = F_DETECT;
+        } else {
+            switch (d.op) {
+            case OP_UNKNOWN: f = F_UNKNOWN; break;
+            case OP_ESC_FP: case OP_ESC_VEC: case OP_ESC_AMO: case OP_ESC_SYS: case OP_ESC_CRYPTO: case OP_ESC_CBO:
+            case OP_ESC_CMP: case OP_ESC_M5: case OP_ESC_HYP: f = F_ESCAPE; break;
+            case OP_c_addi4spn: if (imm == 0) f = F_ILLEGAL; else v = a + imm; break;
+            // loads/stores only describe the access here; the single access site
+            // after the switch keeps the hot loop small (one inlined copy)
+            case OP_c_lwsp: if (d.rd == 0) { f = F_ILLEGAL; break; } msz = 4; mext = 32; break;
+            case OP_c_lw: case OP_lw: msz = 4; mext = 32; break;
+            case OP_c_ldsp: if (d.rd == 0) { f = F_ILLEGAL; break; } msz = 8; break;
+            case OP_c_ld: case OP_ld: msz = 8; break;
+            case OP_c_lbu: case OP_lbu: msz = 1; break;
+            case OP_c_lhu: case OP_lhu: msz = 2; break;
+            case OP_c_lh: case OP_lh: msz = 2; mext = 16; break;
+            case OP_lb: msz = 1; mext = 8; break;
+            case OP_lwu: msz = 4; break;
+            case OP_c_sb: case OP_sb: msz = 1; mst = true; wrd = false; break;
+            case OP_c_sh: case OP_sh: msz = 2; mst = true; wrd = false; break;
+            case OP_c_sw: case OP_sw: case OP_c_swsp: msz = 4; mst = true; wrd = false; break;
+            case OP_c_sd: case OP_sd: case OP_c_sdsp: msz = 8; mst = true; wrd = false; break;
+            case OP_c_addi: case OP_addi: v = a + imm; break;
+            case OP_c_addiw: if (d.rd == 0) f = F_ILLEGAL; else v = sx32(a + imm); break;
+            case OP_addiw: v = sx32(a + imm); break;
+            case OP_c_li: case OP_lui: v = (uint64_t)imm; break;
+            case OP_c_addi16sp: if (imm == 0) f = F_ILLEGAL; else v = a + imm; break;
+            case OP_c_lui: if (imm == 0) f = F_ILLEGAL; else v = (uint64_t)imm; break;
+            case OP_c_srli: case OP_srli: v = a >> imm; break;
+            case OP_c_srai: case OP_srai: v = (uint64_t)((int64_t)a >> imm); break;
+            case OP_c_andi: case OP_andi: v = a & (uint64_t)imm; break;
+            case OP_c_sub: case OP_sub: v = a - b; break;
+            case OP_c_xor: case OP_xor_: v = a ^ b; break;
+            case OP_c_or: case OP_or_: v = a | b; break;
+            case OP_c_and: case OP_and_: v = a & b; break;
+            case OP_c_subw: case OP_subw: v = sx32((uint32_t)a - (uint32_t)b); break;
+            case OP_c_addw: case OP_addw: v = sx32((uint32_t)a + (uint32_t)b); break;
+            case OP_c_mul: case OP_mul: v = a * b; break;
+            case OP_c_zext_b: v = a & 0xFF; break;
+            case OP_c_sext_b: case OP_sext_b: v = (uint64_t)sext64(a & 0xFF, 8); break;
+            case OP_c_zext_h: v = a & 0xFFFF; break;
+            case OP_c_sext_h: case OP_sext_h: v = (uint64_t)sext64(a & 0xFFFF, 16); break;
+            case OP_c_zext_w: v = a & 0xFFFFFFFFULL; break;
+            case OP_c_not: v = ~a; break;
+            case OP_c_j: npc = pc + imm; wrd = false; break;
+            case OP_c_beqz: if (a == 0) npc = pc + imm; wrd = false; break;
+            case OP_c_bnez: if (a != 0) npc = pc + imm; wrd = false; break;
+            case OP_c_slli: case OP_slli: v = a << imm; break;
+            case OP_c_jr: if (d.rs1 == 0) f = F_ILLEGAL; else npc = a & ~1ULL; wrd = false; break;
+            case OP_c_mv: v = b; break;
+            case OP_c_ebreak: case OP_ebreak: f = F_BREAK; break;
+            case OP_c_jalr: v = npc; npc = a & ~1ULL; break;
+            case OP_c_add: case OP_add: v = a + b; break;
+            case OP_fence: case OP_fence_i: wrd = false; break;
+            case OP_bseti: v = a | (1ULL << (imm & 63)); break;
+            case OP_bclri: v = a & ~(1ULL << (imm & 63)); break;
+            case OP_binvi: v = a ^ (1ULL << (imm & 63)); break;
+            case OP_clz: v = a ? __builtin_clzll(a) : 64; break;
+            case OP_ctz: v = a ? __builtin_ctzll(a) : 64; break;
+            case OP_cpop: v = __builtin_popcountll(a); break;
+            case OP_slti: v = (int64_t)a < imm ? 1 : 0; break;
+            case OP_sltiu: v = a < (uint64_t)imm ? 1 : 0; break;
+            case OP_xori: v = a ^ (uint64_t)imm; break;
+            case OP_orc_b: {
+                v = 0;
+#pragma unroll
+                for (int i = 0; i < 8; i++) if ((a >> (8 * i)) & 0xFF) v |= 0xFFULL << (8 * i);
+                break;
+            }
+            case OP_bexti: v = (a >> (imm & 63)) & 1; break;
+            case OP_rori: v = (a >> imm) | (a << ((64 - imm) & 63)); break;
+            case OP_rev8: v = __builtin_bswap64(a); break;
+            case OP_prefetch_i: case OP_prefetch_r: case OP_prefetch_w: wrd = false; break;
+            case OP_ori_hint: case OP_ori: v = a | (uint64_t)imm; break;
+            case OP_auipc: v = pc + imm; break;
+            case OP_slliw: v = sx32((uint32_t)a << imm); break;
+            case OP_slli_uw: v = (a & 0xFFFFFFFFULL) << imm; break;
+            case OP_clzw: v = (uint32_t)a ? __builtin_clz((uint32_t)a) : 32; break;
+            case OP_ctzw: v = (uint32_t)a ? __builtin_ctz((uint32_t)a) : 32; break;
+            case OP_cpopw: v = __builtin_popcount((uint32_t)a); break;
+            case OP_srliw: v = sx32((uint32_t)a >> imm); break;
+            case OP_sraiw: v = (uint64_t)(int64_t)((int32_t)(uint32_t)a >> imm); break;
+            case OP_roriw: { const uint32_t x = (uint32_t)a; v = sx32((x >> imm) | (x << ((32 - imm) & 31))); break; }
+            case OP_sll: v = a << (b & 63); break;
+            case OP_mulh: v = (uint64_t)__mul64hi((int64_t)a, (int64_t)b); break;
+            case OP_clmul: { v = 0; for (int i = 0; i < 64; i++) if ((b >> i) & 1) v ^= a << i; break; }
+            case OP_bset: v = a | (1ULL << (b & 63)); break;
+            case OP_bclr: v = a & ~(1ULL << (b & 63)); break;
+            case OP_rol: { const int sh = (int)(b & 63); v = (a << sh) | (a >> ((64 - sh) & 63)); break; }
+            case OP_binv: v = a ^ (1ULL << (b & 63)); break;
+            case OP_slt: v = (int64_t)a < (int64_t)b ? 1 : 0; break;
+            case OP_mulhsu: v = __umul64hi(a, b) - (((int64_t)a < 0) ? b : 0); break;
+            case OP_clmulr: { v = 0; for (int i = 0; i < 64; i++) if ((b >> i) & 1) v ^= a >> (63 - i); break; }
+            case OP_sh1add: v = (a << 1) + b; break;
+            case OP_sltu: v = a < b ? 1 : 0; break;
+            case OP_mulhu: v = __umul64hi(a, b); break;
+            case OP_clmulh: { v = 0; for (int i = 1; i < 64; i++) if ((b >> i) & 1) v ^= a >> (64 - i); break; }
+            case OP_div_: {
+                const int64_t x = (int64_t)a, y = (int64_t)b;
+                v = y == 0 ? ~0ULL : (x == INT64_MIN && y == -1) ? (uint64_t)x : (uint64_t)(x / y);
+                break;
+            }
+            case OP_pack: v = (b << 32) | (a & 0xFFFFFFFFULL); break;
+            case OP_min_: v = (int64_t)a < (int64_t)b ? a : b; break;
+            case OP_sh2add: v = (a << 2) + b; break;
+            case OP_xnor: v = ~(a ^ b); break;
+            case OP_srl: v = a >> (b & 63); break;
+            case OP_divu: v = b == 0 ? ~0ULL : a / b; break;
+            case OP_czero_eqz: v = b == 0 ? 0 : a; break;
+            case OP_sra: v = (uint64_t)((int64_t)a >> (b & 63)); break;
+            case OP_minu: v = a < b ? a : b; break;
+            case OP_bext: v = (a >> (b & 63)) & 1; break;
+            case OP_ror: { const int sh = (int)(b & 63); v = (a >> sh) | (a << ((64 - sh) & 63)); break; }
+            case OP_rem: {
+                const int64_t x = (int64_t)a, y = (int64_t)b;
+                v = y == 0 ? a : (x == INT64_MIN && y == -1) ? 0 : (uint64_t)(x % y);
+                break;
+            }
+            case OP_max_: v = (int64_t)a > (int64_t)b ? a : b; break;
+            case OP_sh3add: v = (a << 3) + b; break;
+            case OP_orn: v = a | ~b; break;
+            case OP_remu: v = b == 0 ? a : a % b; break;
+            case OP_packh: v = ((b & 0xFF) << 8) | (a & 0xFF); break;
+            case OP_maxu: v = a > b ? a : b; break;
+            case OP_czero_nez: v = b != 0 ? 0 : a; break;
+            case OP_andn: v = a & ~b; break;
+            case OP_mulw: v = sx32((uint32_t)a * (uint32_t)b); break;
+            case OP_add_uw: v = (a & 0xFFFFFFFFULL) + b; break;
+            case OP_sllw: v = sx32((uint32_t)a << (b & 31)); break;
+            case OP_rolw: { const uint32_t x = (uint32_t)a; const int sh = (int)(b & 31); v = sx32((x << sh) | (x >> ((32 - sh) & 31))); break; }
+            case OP_sh1add_uw: v = ((a & 0xFFFFFFFFULL) << 1) + b; break;
+            case OP_divw: {
+                const int32_t x = (int32_t)a, y = (int32_t)b;
+                const int32_t q = y == 0 ? -1 : (x == INT32_MIN && y == -1) ? x : x / y;
+                v = (uint64_t)(int64_t)q;
+                break;
+            }
+            case OP_packw: v = sx32(((b & 0xFFFF) << 16) | (a & 0xFFFF)); break;
+            case OP_sh2add_uw: v = ((a & 0xFFFFFFFFULL) << 2) + b; break;
+            case OP_srlw: v = sx32((uint32_t)a >> (b & 31)); break;
+            case OP_divuw: v = (uint32_t)b == 0 ? ~0ULL : sx32((uint32_t)a / (uint32_t)b); break;
+            case OP_sraw: v = (uint64_t)(int64_t)((int32_t)(uint32_t)a >> (b & 31)); break;
+            case OP_rorw: { const uint32_t x = (uint32_t)a; const int sh = (int)(b & 31); v = sx32((x >> sh) | (x << ((32 - sh) & 31))); break; }
+            case OP_remw: {
+                const int32_t x = (int32_t)a, y = (int32_t)b;
+                const int32_t r = y == 0 ? x : (x == INT32_MIN && y == -1) ? 0 : x % y;
+                v = (uint64_t)(int64_t)r;
+                break;
+            }
+            case OP_sh3add_uw: v = ((a & 0xFFFFFFFFULL) << 3) + b; break;
+            case OP_remuw: v = (uint32_t)b == 0 ? sx32(a) : sx32((uint32_t)a % (uint32_t)b); break;
+            case OP_beq: if (a == b) npc = pc + imm; wrd = false; break;
+            case OP_bne: if (a != b) npc = pc + imm; wrd = false; break;
+            case OP_blt: if ((int64_t)a < (int64_t)b) npc = pc + imm; wrd = false; break;
+            case OP_bge: if ((int64_t)a >= (int64_t)b) npc = pc + imm; wrd = false; break;
+            case OP_bltu: if (a < b) npc = pc + imm; wrd = false; break;
+            case OP_bgeu: if (a >= b) npc = pc + imm; wrd = false; break;
+            case OP_jalr: v = npc; npc = (a + imm) & ~1ULL; break;
+            case OP_jal: v = npc; npc = pc + imm; break;
+            case OP_ecall: f = F_SYSCALL; break;
+            case OP_csr: f = csr_u_accessible(d.raw >> 20) ? F_ESCCSR : F_ILLEGAL; break;
+            default: f = F_UNKNOWN; break;
+            }
+        }
+        if (msz && f == F_NONE) {
+            t = b;
+            f = mem_access(CX, w, m, slot, a + imm, msz, mst, t, fva);
+            L.data_b += msz;
+            if (!mst) v = mext ? (uint64_t)sext64(t, mext) : t;
+        }
+        // F_NEEDPAGE: copy-on-write first; the tick is retried (no commit)
+        // ---- F. commit: countInst only on NoFault (atomic.cc:687-689), then
+        // advancePC (src/cpu/simple/base.cc:493-512)
+        if (f != F_NEEDPAGE) {
+        L.ncyc += ticks;
+        L.fetch_b += d.len;
+        if (CX->record && (f == F_NONE || f == F_SYSCALL)) {
+            const uint64_t ho = ((pc & ~1ULL) | ((pc & 1) << 1)) - CX->text_lo;
+            const uint32_t ev = ho < CX->text_bytes ? (uint32_t)(ho >> 1) : 0x7FFFFFFFu;
+            if (tpos < CX->rec_trace_cap) CX->rec_trace[tpos] = ev | (f == F_SYSCALL ? 0x80000000u : 0u);
+            tpos++;
+        }
+        if (f == F_NONE) {
+            if (wrd && d.rd) RREG(d.rd) = v;
+            if (wrd && L.watch > 0 && (d.flags & kPreRd) && d.rd == L.watch) L.watch = -1;
+            L.ninst++;
+            L.pc = npc;
+        } else {
+        switch (f) {
+        case F_SYSCALL:   // SyscallFault::invokeSE advances the PC first (arch/riscv/faults.cc:325-333)
+            L.pc = pc + d.len;
+            do_syscall(CX, w, L, m, slot, R, lane);
+            break;
+        case F_BREAK: finish(L, FI_CRASH, FI_CRASH_SIGTRAP, 133, (uint32_t)pc); break;
+        case F_ILLEGAL: finish(L, FI_CRASH, FI_CRASH_ILLEGAL_INST, 134, (uint32_t)pc); break;
+        case F_UNKNOWN: finish(L, FI_CRASH, FI_CRASH_UNKNOWN_INST, 134, (uint32_t)pc); break;
+        case F_ESCAPE: finish(L, FI_ESCAPE, FI_ESC_INST, 0, d.raw); break;
+        case F_ESCCSR: finish(L, FI_ESCAPE, FI_ESC_CSR, 0, d.raw); break;
+        case F_DETECT: finish(L, FI_DETECTED, 0, 0, (uint32_t)pc); break;
+        case F_PGFAULT:
+            if (fva < m.stack_min && fva >= kStackBase - kMaxStack) {
+                const uint64_t nm = fva & ~4095ULL;
+                if (kStackBase - nm > kMaxStack) finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, (uint32_t)pc);
+                else m.stack_min = nm;
+            } else {
+                finish(L, FI_CRASH, FI_CRASH_PAGE_FAULT, 134, (uint32_t)fva);
+            }
+            break;
+        default: break;
+        }
+        }   // fault disposition
+        }   // f != F_NEEDPAGE
+        }   // mine
+        // ---- stay in the inner loop? every group lane committed, none reached
+        // its next event, all at one PC that is still the wave's minimum
+        const bool cont = mine && f == F_NONE && L.ninst < next_ev;
+        const uint64_t cm = __ballot(cont);
+        if (cm != gmask) break;
+        const uint64_t npc0 = uni64(readlane64(L.pc, __ffsll((unsigned long long)cm) - 1));
+        if (__ballot(cont && L.pc == npc0) != cm || npc0 >= wait_min) break;
+        lpc = npc0;
+        mine = cont;
+        n_iter++;
+        }   // inner loop
+    }
+
+    if (live) CX->out[CX->record ? 0 : sidx] = L.res;
+    if (CX->record && live) {
+        CX->stats[3] = L.ncyc;
+        CX->stats[4] = L.out_pos;
+        CX->stats[5] = L.err_pos;
+        CX->stats[13] = snaps_taken;
+        CX->stats[15] = tpos;
+    }
+#ifdef FI_PROF
+    if (lane == 0)
+        for (int k = 0; k < 4; k++) atomicAdd(&CX->stats[24 + k], (unsigned long long)pacc[k]);
+#endif
+    if (blockIdx.x == 0 && lane == 0) {
+        CX->stats[20] = __builtin_amdgcn_s_memtime() - t_start;
+        CX->stats[21] = __builtin_amdgcn_s_memrealtime() - rt_start;
+    }
+    const uint64_t fb = wave_sum64(L.fetch_b), db = wave_sum64(L.data_b), pm = wave_sum64(pages_made);
+    const uint64_t si = wave_sum64(start_inst);
+    if (lane == 0) {
+        atomicAdd(&CX->stats[0], (unsigned long long)fb);
+        atomicAdd(&CX->stats[1], (unsigned long long)db);
+        atomicAdd(&CX->stats[2], (unsigned long long)pm);
+        atomicAdd(&CX->stats[6], (unsigned long long)n_iter);
+        atomicAdd(&CX->stats[7], (unsigned long long)n_exec);
+        atomicAdd(&CX->stats[8], (unsigned long long)n_slow);
+        atomicAdd(&CX->stats[9], (unsigned long long)n_min);
+        atomicMax(&CX->stats[10], (unsigned long long)n_iter);
+        atomicAdd(&CX->stats[11], (unsigned long long)n_chk);
+        atomicAdd(&CX->stats[12], (unsigned long long)n_early);
+        atomicAdd(&CX->stats[14], (unsigned long long)si);
+    }
+}
+
+hipError_t launch_trials(const DevCtx &c, hipStream_t st) {
+    hipLaunchKernelGGL(fi_trial_kernel, dim3((unsigned)((c.n + 63) / 64)), dim3(64), 0, st, c);
+    return hipGetLastError();
+}
+
+}  // namespace fi

@@ -65,13 +65,18 @@ class EngineError(RuntimeError):
 
 class _Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("private_pages", C.c_uint32), ("hang_factor_x16", C.c_uint32),
-                ("max_trials_per_launch", C.c_uint32)]
+                ("max_trials_per_launch", C.c_uint32), ("snapshot_interval", C.c_uint32), ("flags", C.c_uint32)]
+
+
+CFG_NO_SNAPSHOT_START = 1
+CFG_NO_EARLY_EXIT = 2
 
 
 class GoldenInfo(C.Structure):
     _fields_ = [("ninst", C.c_uint64), ("ncycles", C.c_uint64), ("exit_code", C.c_uint32), ("pad", C.c_uint32),
                 ("stdout_len", C.c_uint64), ("stderr_len", C.c_uint64), ("fetch_bytes", C.c_uint64),
-                ("data_bytes", C.c_uint64)]
+                ("data_bytes", C.c_uint64), ("snapshots", C.c_uint64), ("snapshot_interval", C.c_uint64),
+                ("snapshot_frames", C.c_uint64)]
 
 
 _lib = None
@@ -130,9 +135,9 @@ class Engine:
     """Thin RAII wrapper of one fi_engine (one HIP device)."""
 
     def __init__(self, device: int = 0, private_pages: int = 16, hang_factor_x16: int = 32,
-                 max_trials_per_launch: int = 65536):
+                 max_trials_per_launch: int = 65536, snapshot_interval: int = 0, flags: int = 0):
         self.L = lib()
-        cfg = _Config(device, private_pages, hang_factor_x16, max_trials_per_launch)
+        cfg = _Config(device, private_pages, hang_factor_x16, max_trials_per_launch, snapshot_interval, flags)
         h = C.c_void_p()
         st = self.L.fi_create(C.byref(cfg), C.byref(h))
         if st == FI_E_NODEVICE:

@@ -1,21 +1,38 @@
-"""Interpreter diagnostics on the GPU: per-wave loop counters and timings."""
-import sys, os, time, json
+"""Interpreter diagnostics on the GPU: per-wave loop counters and timings.
+
+python tools/diag.py [workload] [--trials N] [--flags F]
+"""
+import argparse
+import json
+import os
+import sys
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np
-import torch  # noqa
-from shrewd_amd import Engine
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401
+from shrewd_amd import Engine  # noqa: E402
 
 REGS_PC = ((1 << 32) - 2) | (1 << 32)
-name = sys.argv[1] if len(sys.argv) > 1 else "crc32"
-e = Engine(max_trials_per_launch=200000)
+ap = argparse.ArgumentParser()
+ap.add_argument("workload", nargs="?", default="crc32")
+ap.add_argument("--trials", type=int, nargs="*", default=[64, 6400, 100000])
+ap.add_argument("--flags", type=int, default=0)
+ap.add_argument("--interval", type=int, default=0)
+a = ap.parse_args()
+name = a.workload
+e = Engine(max_trials_per_launch=200000, flags=a.flags, snapshot_interval=a.interval)
 e.load_elf(open(f"workloads/{name}.elf", "rb").read(), [name])
 g = e.golden_run()
+gms = e.last_kernel_ms()
 st = e.debug_stats()
-print(json.dumps({"golden_ninst": g.ninst, "golden_ms": e.last_kernel_ms(), "golden_iters": int(st[6]),
-                  "golden_ns_per_iter": e.last_kernel_ms() * 1e6 / max(1, int(st[6]))}))
+clk = int(st[20]) / max(1, int(st[21])) * 100.0
+print(json.dumps({"golden_ninst": g.ninst, "golden_ms": gms, "golden_ns_per_inst": gms * 1e6 / max(1, g.ninst),
+                  "snapshots": g.snapshots, "interval": g.snapshot_interval, "frames": g.snapshot_frames, "capture_pass_clock_mhz": round(clk, 1),
+                  "cycles_per_inst_capture_pass": int(st[20]) / max(1, g.ninst),
+                  "prof_cycles_per_inst": [round(int(st[24 + k]) / max(1, g.ninst), 1) for k in range(4)]}),
+      flush=True)
 e.set_campaign(0x5EED0002, REGS_PC, 1)
-for n in (64, 6400, 100000):
-    # trials whose site lies beyond the end: pure golden lanes, no divergence
+for n in a.trials:
     sites = e.sample(0, n)
     nofault = sites.copy(); nofault["inst"] = 1 << 40
     for label, s in (("nofault", nofault), ("faults", sites)):
@@ -23,19 +40,13 @@ for n in (64, 6400, 100000):
         st = e.debug_stats()
         ms = e.last_kernel_ms()
         waves = (n + 63) // 64
-        print(json.dumps({"n": n, "kind": label, "kernel_ms": ms, "iters": int(st[6]), "max_iter_wave": int(st[10]),
-                          "iters_per_wave": int(st[6]) / waves, "lane_insts": int(st[7]),
-                          "lanes_per_iter": int(st[7]) / max(1, int(st[6])), "slow": int(st[8]), "minpc": int(st[9]),
-                          "ns_per_iter_slowest_wave": ms * 1e6 / max(1, int(st[10])),
-                          "classes": np.bincount(out["cls"], minlength=6).tolist()}))
-
-if os.environ.get("SHREWD_FI_LIB", "").endswith("_diag.so"):
-    e.set_campaign(0x5EED0002, REGS_PC, 1)
-    g = e.golden_run()
-    st = e.debug_stats()
-    seg = ["A_requests", "B_events", "C_leader", "D_fetch_decode", "E_execute", "F_memaccess"]
-    it = max(1, int(st[6]))
-    print(json.dumps({"golden_cycles_per_iter_by_segment": {seg[k]: int(st[16 + k]) / it for k in range(6)}}))
-    sites = e.sample(0, 100000); nof = sites.copy(); nof["inst"] = 1 << 40
-    e.run_sites(nof); st = e.debug_stats(); it = max(1, int(st[6]))
-    print(json.dumps({"nofault100k_cycles_per_iter_by_segment": {seg[k]: int(st[16 + k]) / it for k in range(6)}}))
+        print(json.dumps({"n": n, "kind": label, "kernel_ms": round(ms, 3), "trials_per_s": n / ms * 1e3,
+                          "iters_per_wave": int(st[6]) / waves, "max_iter_wave": int(st[10]),
+                          "lane_insts": int(st[7]), "lanes_per_iter": round(int(st[7]) / max(1, int(st[6])), 2),
+                          "slow": int(st[8]), "minpc": int(st[9]), "checks": int(st[11]), "early": int(st[12]),
+                          "skipped_prefix": int(st[14]), "cow_pages": int(st[2]),
+                          "ns_per_iter_slowest_wave": round(ms * 1e6 / max(1, int(st[10])), 1),
+                          "clock_mhz": round(int(st[20]) / max(1, int(st[21])) * 100.0, 1),
+                          "wave0_cycles": int(st[20]),
+                          "prof_cycles_per_iter": [round(int(st[24 + k]) / max(1, int(st[6])), 1) for k in range(4)],
+                          "classes": np.bincount(out["cls"], minlength=6).tolist()}), flush=True)
