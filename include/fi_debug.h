@@ -11,12 +11,23 @@ extern "C" {
  * the interpreter's pre-decode and slow fetch path use); out receives n
  * 16-byte records {u32 raw; u8 op, rd, rs1, rs2; i32 imm; u8 len, flags; u16 aux}. */
 fi_status fi_debug_decode(fi_engine *e, const uint32_t *raws, uint64_t n, void *out);
-/* Counters of the last interpreter launch: [0] fetch bytes [1] data bytes
- * [2] private pages [3..5] golden ncycles/stdout/stderr [6] wave-loop
- * iterations [7] lane-instructions executed [8] slow-path fetches [9] min-PC
- * reductions [10] max iterations of one wave; [16..21] diagnostic builds
- * only: s_memtime cycles per loop segment. */
+/* Counters of the last interpreter launch (layout: DevCtx::stats in
+ * shrewd_amd/csrc/fi_types.h): fetch/data bytes, private pages, golden
+ * cycles/output, loop iterations, lane-instructions, slow fetches, min-PC
+ * reductions, snapshot comparisons and early exits, translated instructions
+ * and entries, the slowest wave, wave-0 clock; [24..27] -DFI_PROF builds only. */
 fi_status fi_debug_stats(fi_engine *e, uint64_t *out32);
+/* Per wave of the last launch: {s_memtime cycles, loop iterations,
+ * translated instructions, slow fetches} (4 x u64 each). */
+fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves);
+/* The C++ generated for the golden blocks by the last fi_golden_run
+ * (fi_translate.cpp); *len = its length, buf gets up to cap-1 bytes + NUL. */
+fi_status fi_debug_translation(fi_engine *e, char *buf, uint64_t cap, uint64_t *len);
+/* hipRTC build of the trial kernel with `body` as its translated blocks, no
+ * device needed; code (cap bytes) receives the code object, *len its size,
+ * err the hipRTC log on failure. */
+fi_status fi_debug_jit_compile(const char *body, const char *arch, void *code, uint64_t cap, uint64_t *len,
+                               char *err, uint64_t err_cap);
 #ifdef __cplusplus
 }
 #endif

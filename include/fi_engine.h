@@ -33,8 +33,10 @@
 #ifndef SHREWD_FI_ENGINE_H
 #define SHREWD_FI_ENGINE_H
 
+#ifndef __HIPCC_RTC__
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -108,6 +110,8 @@ typedef struct {
  * (the plain serial semantics, for A/B checks; outcomes are identical) */
 #define FI_CFG_NO_SNAPSHOT_START 1u
 #define FI_CFG_NO_EARLY_EXIT 2u
+/* interpreter only: no load-time translation of the golden blocks (hipRTC) */
+#define FI_CFG_NO_TRANSLATE 4u
 
 typedef struct {
     uint64_t ninst, ncycles;
@@ -116,6 +120,9 @@ typedef struct {
     uint64_t fetch_bytes, data_bytes;
     uint64_t snapshots, snapshot_interval; /* golden snapshots kept on the device */
     uint64_t snapshot_frames;              /* distinct 4 KiB frames behind them */
+    uint64_t translated_blocks;            /* golden basic blocks compiled to straight-line code (0: interpreter only) */
+    uint64_t translated_insts;
+    uint64_t translate_us;                 /* translation + hipRTC build (0 if the code object was cached) */
 } fi_golden_info;
 
 typedef struct {
@@ -163,6 +170,9 @@ fi_status fi_run_trials_device(fi_engine *e, uint64_t first_trial, uint64_t n, v
                                void *stream);
 /* Synchronise the engine stream. */
 fi_status fi_sync(fi_engine *e);
+
+/* Why the translated path is off for this workload ("" when it is on). */
+const char *fi_translate_status(fi_engine *e);
 
 /* Timing of the last fi_run_* call's interpreter kernel(s), measured with
  * hipEvents on the engine stream (milliseconds). */

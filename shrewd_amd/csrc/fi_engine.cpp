@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -23,12 +24,17 @@ namespace fi {
 hipError_t launch_sample(const SampleCtx &c, uint64_t n, fi_site *sites, uint64_t *keys, uint32_t *perm,
                          hipStream_t st);
 hipError_t launch_keys(const fi_site *sites, uint64_t n, uint64_t *keys, uint32_t *perm, hipStream_t st);
-hipError_t launch_predecode(const uint8_t *text, uint64_t text_lo, uint64_t nhalf, PreInst *pre, hipStream_t st);
+hipError_t launch_predecode(const uint8_t *text, uint64_t code_off, uint64_t code_end, uint64_t nhalf, PreInst *pre,
+                           hipStream_t st);
 hipError_t launch_debug_decode(const uint32_t *raws, uint64_t n, PreInst *out, hipStream_t st);
 hipError_t launch_trials(const DevCtx &c, hipStream_t st);
 hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, fi_histogram *h,
                        const unsigned long long *stats, hipStream_t st);
 hipError_t sort_pairs_bytes(uint64_t n, size_t &bytes);
+std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
+                             const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
+                             uint32_t &n_insts);
+std::string jit_compile(const std::string &body, const char *arch, std::vector<char> &code, bool &cached);
 hipError_t sort_pairs(void *tmp, size_t bytes, const uint64_t *kin, uint64_t *kout, const uint32_t *vin,
                       uint32_t *vout, uint64_t n, int end_bit, hipStream_t st);
 }  // namespace fi
@@ -50,13 +56,13 @@ struct fi_engine {
     bool loaded = false;
     std::map<uint64_t, std::vector<uint8_t>> pages;   // vpn -> 4 KiB
     uint64_t entry = 0, sp0 = 0, stack_min0 = 0, svma_lo = 0, svma_hi = 0;
-    uint64_t text_lo = 0, text_hi = 0;
+    uint64_t text_lo = 0, text_hi = 0, code_lo = 0, code_hi = 0;
     std::vector<uint64_t> mem_pages;   // memory fault candidates (sorted)
 
     // device image: snapshot 0 = the process-start image; the golden run
     // appends snapshots 1..n-1
     PreInst *d_pre = nullptr;
-    uint8_t *d_zero = nullptr, *d_text = nullptr;
+    uint8_t *d_zero = nullptr, *d_text = nullptr, *d_sink = nullptr;
     uint64_t *d_mem_pages = nullptr;
     std::vector<SnapState> snaps;
     std::vector<PageEnt> tab;
@@ -67,6 +73,11 @@ struct fi_engine {
     uint8_t *d_pool = nullptr;
     uint64_t snap_I = 1ULL << 62;
     bool pre_ok = true;
+    // load-time build of the trial kernel with the translated golden blocks
+    hipModule_t tx_mod = nullptr;
+    hipFunction_t tx_fn = nullptr;
+    std::string tx_status = "no golden run";
+    std::string tx_body;   // last generated translation (diagnostics)
 
     // golden
     bool have_golden = false;
@@ -90,6 +101,7 @@ struct fi_engine {
     fi_outcome *d_out = nullptr;
     fi_histogram *d_hist = nullptr;
     unsigned long long *d_stats = nullptr;
+    uint64_t *d_wave_dbg = nullptr;
     uint8_t *d_priv = nullptr;
     uint64_t *d_priv_vpn = nullptr;
 };
@@ -151,14 +163,20 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
 
 static void free_work(fi_engine *e) {
     dfree(e->d_sites); dfree(e->d_keys); dfree(e->d_keys2); dfree(e->d_perm); dfree(e->d_perm2);
-    dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_priv); dfree(e->d_priv_vpn);
+    dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg); dfree(e->d_priv); dfree(e->d_priv_vpn);
     e->cap = 0;
 }
 static void free_snaps(fi_engine *e) { dfree(e->d_snaps); dfree(e->d_tab); dfree(e->d_pool); }
+static void free_tx(fi_engine *e) {
+    if (e->tx_mod) (void)hipModuleUnload(e->tx_mod);
+    e->tx_mod = nullptr;
+    e->tx_fn = nullptr;
+}
 static void free_image(fi_engine *e) {
-    dfree(e->d_pre); dfree(e->d_zero);
+    dfree(e->d_pre); dfree(e->d_zero); dfree(e->d_sink);
     dfree(e->d_text); dfree(e->d_mem_pages); dfree(e->d_gout); dfree(e->d_gerr);
     free_snaps(e);
+    free_tx(e);
     e->have_golden = false;
     e->loaded = false;
 }
@@ -256,7 +274,7 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
     const uint32_t phentsize = le16(elf + 54), phnum = le16(elf + 56);
     if (phoff + (uint64_t)phentsize * phnum > len) return fail(e, FI_E_ELF, "program headers out of file");
     uint64_t max_addr = 0, phdr_vaddr = 0;
-    uint64_t xlo = ~0ULL, xhi = 0;
+    uint64_t xlo = ~0ULL, xhi = 0, clo = ~0ULL, chi = 0;
     std::vector<uint64_t> wpages;
     for (uint32_t i = 0; i < phnum; i++) {
         const uint8_t *ph = elf + phoff + (uint64_t)i * phentsize;
@@ -270,7 +288,12 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
         if (memsz > filesz) img_write(e, paddr + filesz, nullptr, memsz - filesz);
         max_addr = std::max(max_addr, paddr + memsz);
         if (off <= phoff && off + filesz > phoff) phdr_vaddr = vaddr + (phoff - off);
-        if (flags & 1) { xlo = std::min(xlo, paddr & ~(kPage - 1)); xhi = std::max(xhi, (paddr + memsz + kPage - 1) & ~(kPage - 1)); }
+        if (flags & 1) {
+            xlo = std::min(xlo, paddr & ~(kPage - 1));
+            xhi = std::max(xhi, (paddr + memsz + kPage - 1) & ~(kPage - 1));
+            clo = std::min(clo, paddr);
+            chi = std::max(chi, paddr + memsz);
+        }
         if (flags & 2)
             for (uint64_t pg = paddr & ~(kPage - 1); pg < paddr + memsz; pg += kPage) wpages.push_back(pg);
     }
@@ -278,6 +301,8 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
     if ((xlo >> 32) != ((xhi - 1) >> 32)) return fail(e, FI_E_ELF, "executable segments cross a 4 GiB boundary");
     e->text_lo = xlo;
     e->text_hi = xhi;
+    e->code_lo = clo;
+    e->code_hi = chi;
 
     // RiscvProcess::argsInit<uint64_t> (src/arch/riscv/process.cc:134-261)
     std::vector<std::string> av, ev;
@@ -355,6 +380,7 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
         if (st) return st;
     }
     HIPCHK(hipMalloc(&e->d_zero, kPage));
+    HIPCHK(hipMalloc(&e->d_sink, kPage));
     HIPCHK(hipMalloc(&e->d_mem_pages, std::max<size_t>(1, wpages.size()) * 8));
     HIPCHK(hipMemset(e->d_zero, 0, kPage));
     if (!wpages.empty()) HIPCHK(hipMemcpy(e->d_mem_pages, wpages.data(), wpages.size() * 8, hipMemcpyHostToDevice));
@@ -367,7 +393,8 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
     HIPCHK(hipMalloc(&e->d_text, tbytes));
     HIPCHK(hipMemcpy(e->d_text, text.data(), tbytes, hipMemcpyHostToDevice));
     HIPCHK(hipMalloc(&e->d_pre, (tbytes / 2) * sizeof(PreInst)));
-    HIPCHK(launch_predecode(e->d_text, e->text_lo, tbytes / 2, e->d_pre, e->stream));
+    HIPCHK(launch_predecode(e->d_text, e->code_lo - e->text_lo, e->code_hi - e->text_lo, tbytes / 2, e->d_pre,
+                            e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     e->loaded = true;
     return FI_OK;
@@ -388,6 +415,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_out, c * sizeof(fi_outcome)));
     HIPCHK(hipMalloc(&e->d_hist, sizeof(fi_histogram)));
     HIPCHK(hipMalloc(&e->d_stats, 32 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&e->d_wave_dbg, ((c + 63) / 64) * 4 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&e->d_priv, c * e->cfg.private_pages * kPage));
     HIPCHK(hipMalloc(&e->d_priv_vpn, c * e->cfg.private_pages * 8));
     e->cap = c;
@@ -398,6 +426,7 @@ static DevCtx base_ctx(fi_engine *e) {
     DevCtx c{};
     c.pre = e->d_pre; c.text_lo = e->text_lo; c.text_hi = e->text_hi; c.pre_ok = e->pre_ok ? 1 : 0;
     c.text_bytes = (uint32_t)(e->text_hi - e->text_lo);
+    c.code_lo = e->code_lo; c.code_hi = e->code_hi;
     c.snaps = e->d_snaps; c.snap_tab = e->d_tab; c.pool = e->d_pool; c.zero_page = e->d_zero;
     const bool start = !(e->cfg.flags & FI_CFG_NO_SNAPSHOT_START);
     c.n_snap = (uint32_t)e->snaps.size();
@@ -412,6 +441,8 @@ static DevCtx base_ctx(fi_engine *e) {
     c.hang_cap = e->golden.ninst * e->cfg.hang_factor_x16 / 16 + 1000;
     c.protect_mask = e->protect;
     c.priv_frames = e->d_priv; c.priv_vpn = e->d_priv_vpn;
+    c.tx_sink = e->d_sink;
+    c.wave_dbg = e->d_wave_dbg;
     c.stats = e->d_stats;
     return c;
 }
@@ -547,6 +578,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         pre.resize((e->text_hi - e->text_lo) / 2);
         hipError_t err = hipMemcpy(trace.data(), d_trace, n_events * 4, hipMemcpyDeviceToHost);
         if (err == hipSuccess) err = hipMemcpy(pre.data(), e->d_pre, pre.size() * sizeof(PreInst), hipMemcpyDeviceToHost);
+        for (auto &p : pre) p.flags &= (uint8_t)~kPreLeader;
         if (err != hipSuccess) st = fail(e, FI_E_HIP, "trace download: %s", hipGetErrorString(err));
     }
     (void)hipFree(d_trace);
@@ -581,9 +613,12 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
             e->pool.insert(e->pool.end(), pg, pg + kPage);
             cur[vpn] = f;
             // the pre-decoded text stays valid only if the golden run never rewrites it
-            if ((vpn << 12) >= e->text_lo && (vpn << 12) < e->text_hi) {
+            const uint64_t va = vpn << 12;
+            if (va < e->code_hi && va + kPage > e->code_lo) {   // bytes of the code range in this page
+                const uint64_t a = std::max(va, e->code_lo), b = std::min(va + kPage, e->code_hi);
                 auto org = e->pages.find(vpn);
-                if (org == e->pages.end() || memcmp(org->second.data(), pg, kPage)) e->pre_ok = false;
+                if (org == e->pages.end() || memcmp(org->second.data() + (a - va), pg + (a - va), b - a))
+                    e->pre_ok = false;
             }
         }
         S.tab_off = (uint32_t)tab.size();
@@ -627,6 +662,44 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     e->snap_I = I;
     st = upload_snaps(e);
     if (st) return st;
+
+    // ---- translate the golden basic blocks and build the trial kernel with
+    // them (hipRTC); the static kernel stays the fallback
+    free_tx(e);
+    if (e->cfg.flags & FI_CFG_NO_TRANSLATE) e->tx_status = "disabled (FI_CFG_NO_TRANSLATE)";
+    else if (!e->pre_ok) e->tx_status = "golden run rewrites its text";
+    else if (!live_ok || trace.empty()) e->tx_status = "golden trace unavailable";
+    else {
+        const auto t0 = std::chrono::steady_clock::now();
+        // (snapshot pcs are not leaders: they fall all over the hot loops and
+        // would cut the blocks into single instructions; a wave that starts
+        // mid-block steps to the next leader in the interpreter)
+        const std::vector<uint64_t> pcs;
+        std::vector<uint32_t> leaders;
+        uint32_t n_tx = 0;
+        const std::string body = translate_blocks(pre, e->text_lo, trace, pcs, leaders, n_tx);
+        e->tx_body = body;
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, e->dev));
+        std::vector<char> code;
+        bool cached = false;
+        const std::string err = jit_compile(body, prop.gcnArchName, code, cached);
+        if (!err.empty()) {
+            e->tx_status = err;
+        } else if (hipModuleLoadData(&e->tx_mod, code.data()) != hipSuccess ||
+                   hipModuleGetFunction(&e->tx_fn, e->tx_mod, "fi_trial_kernel_tx") != hipSuccess) {
+            free_tx(e);
+            e->tx_status = "code object did not load";
+        } else {
+            for (uint32_t h : leaders) pre[h].flags |= kPreLeader;
+            HIPCHK(hipMemcpy(e->d_pre, pre.data(), pre.size() * sizeof(PreInst), hipMemcpyHostToDevice));
+            e->tx_status = "";
+            e->golden.translated_blocks = leaders.size();
+            e->golden.translated_insts = n_tx;
+            e->golden.translate_us = cached ? 0 : (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+                                                          std::chrono::steady_clock::now() - t0).count();
+        }
+    }
     e->last_ms = golden_ms;
     e->golden.snapshots = e->snaps.size();
     e->golden.snapshot_interval = I;
@@ -691,6 +764,14 @@ fi_status fi_sample_sites(fi_engine *e, uint64_t first, uint64_t n, fi_site *out
     return FI_OK;
 }
 
+// The trial kernel: the load-time build with translated blocks when there is
+// one, else the static (interpreter-only) kernel.
+static hipError_t launch_trial_kernel(fi_engine *e, DevCtx &c, hipStream_t st) {
+    if (!e->tx_fn) return launch_trials(c, st);
+    void *args[] = {&c};
+    return hipModuleLaunchKernel(e->tx_fn, (unsigned)((c.n + 63) / 64), 1, 1, 64, 1, 1, 0, st, args, nullptr);
+}
+
 // One launch: d_sites[0..k) holds the sites in trial order, keys/perm set.
 static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histogram *d_hist, hipStream_t st) {
     int end_bit = 64 - __builtin_clzll(std::max<uint64_t>(e->golden.ninst, 1));
@@ -710,7 +791,7 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     auto &tp = e->tpool[e->tused++];
     HIPCHK(hipEventRecord(e->ev0, st));
     HIPCHK(hipEventRecord(tp.first, st));
-    HIPCHK(launch_trials(c, st));
+    HIPCHK(launch_trial_kernel(e, c, st));
     HIPCHK(hipEventRecord(tp.second, st));
     HIPCHK(hipEventRecord(e->ev1, st));
     HIPCHK(launch_hist(e->d_sites, d_out, k, d_hist, e->d_stats, st));
@@ -804,6 +885,45 @@ fi_status fi_sync(fi_engine *e) {
 }
 
 double fi_last_kernel_ms(fi_engine *e) { return e ? e->last_ms : 0.0; }
+
+const char *fi_translate_status(fi_engine *e) { return e ? e->tx_status.c_str() : "no engine"; }
+
+// hipRTC build of the trial kernel with `body` as translated blocks, no
+// device needed (tests; inspecting generated code offline).
+fi_status fi_debug_jit_compile(const char *body, const char *arch, void *code, uint64_t cap, uint64_t *len,
+                               char *err, uint64_t err_cap) {
+    std::vector<char> co;
+    bool cached = false;
+    const std::string msg = jit_compile(body ? body : "", arch ? arch : "gfx950", co, cached);
+    if (err && err_cap) {
+        const uint64_t n = std::min<uint64_t>(err_cap - 1, msg.size());
+        memcpy(err, msg.data(), n);
+        err[n] = 0;
+    }
+    if (!msg.empty()) return FI_E_HIP;
+    if (code && cap) memcpy(code, co.data(), std::min<uint64_t>(cap, co.size()));
+    if (len) *len = co.size();
+    return FI_OK;
+}
+
+fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves) {
+    if (!e || !out) return FI_E_ARG;
+    if (n_waves > (e->cap + 63) / 64) return fail(e, FI_E_ARG, "more waves than the work buffers hold");
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(out, e->d_wave_dbg, n_waves * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return FI_OK;
+}
+
+fi_status fi_debug_translation(fi_engine *e, char *buf, uint64_t cap, uint64_t *len) {
+    if (!e) return FI_E_ARG;
+    if (buf && cap) {
+        const uint64_t n = std::min<uint64_t>(cap - 1, e->tx_body.size());
+        memcpy(buf, e->tx_body.data(), n);
+        buf[n] = 0;
+    }
+    if (len) *len = e->tx_body.size();
+    return FI_OK;
+}
 
 fi_status fi_debug_stats(fi_engine *e, uint64_t *out16) {
     if (!e || !out16) return FI_E_ARG;

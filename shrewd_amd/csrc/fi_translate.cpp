@@ -1,0 +1,392 @@
+// fi_translate.cpp -- load-time translation of the golden run's basic blocks
+// into straight-line HIP code.
+//
+// The interpreter (hip/fi_trial.hip) pays a scalar dispatch tree, ballots and
+// a dozen branches per guest instruction (~20 cycles per scalar branch on
+// gfx950, tools/microbench).  Here each block of the golden text that the
+// golden run executed becomes a run of C statements on 31 locals X1..X31 --
+// the guest registers, in VGPRs with static indices -- with one ballot-driven
+// uniform branch at its end.  The generated code is compiled into the trial
+// kernel with hipRTC (fi_jit.cpp) and entered at block leaders; whatever it
+// does not cover (ecall, CSR, escapes, illegal encodings, TLB misses,
+// copy-on-write, misaligned accesses, divergence, events, untranslated pcs)
+// leaves to the interpreter before the instruction, with every counter
+// (numInst, cycles, fetch and data bytes) exact.
+//
+// Semantics follow the interpreter's general path op for op, i.e. the
+// generated StaticInst::execute bodies of src/arch/riscv/isa/decoder.isa.
+#include <cctype>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "fi_types.h"
+#include "rv64_isa.h"
+
+namespace fi {
+
+namespace {
+
+struct Gen {
+    const std::vector<PreInst> &pre;
+    uint64_t text_lo;
+    const std::set<uint32_t> &leaders;
+    const std::set<uint32_t> &executed;
+    std::string out;
+
+    void put(const char *fmt, ...) __attribute__((format(printf, 2, 3))) {
+        char buf[1024];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        out += buf;
+    }
+    static std::string R(uint32_t r) { return r ? "X" + std::to_string(r) : std::string("0ULL"); }
+    uint64_t pc_of(uint32_t h) const { return text_lo + 2ULL * h; }
+    // jump to the block at pc, or leave at pc if it is not translated
+    std::string go(uint64_t pc) const {
+        char buf[96];
+        const uint64_t off = pc - text_lo;
+        if (pc >= text_lo && !(off & 1) && off / 2 < pre.size() && leaders.count((uint32_t)(off / 2)))
+            snprintf(buf, sizeof buf, "goto B_%u;", (uint32_t)(off / 2));
+        else
+            snprintf(buf, sizeof buf, "{ spc = 0x%llxULL; goto tx_out; }", (unsigned long long)pc);
+        return buf;
+    }
+};
+
+enum Cls { C_STOP, C_ALU, C_NOP, C_LOAD, C_STORE, C_BR, C_JAL, C_JALR };
+
+// Classify an instruction and, for ALU ops, produce its value expression in
+// terms of A (rs1), B (rs2), IMM and PC.  Every case mirrors the general path
+// of fi_trial_kernel; the encodings that raise IllegalInst there are C_STOP.
+Cls classify(const PreInst &p, std::string &expr, uint32_t &size, int &sext, const char *&cond) {
+    const int64_t imm = p.imm;
+    size = 0; sext = 0; cond = nullptr;
+    switch (p.op) {
+    case OP_c_addi4spn: if (imm == 0) return C_STOP; expr = "A + IMM"; return C_ALU;
+    case OP_c_lwsp: if (p.rd == 0) return C_STOP; size = 4; sext = 32; return C_LOAD;
+    case OP_c_lw: case OP_lw: size = 4; sext = 32; return C_LOAD;
+    case OP_c_ldsp: if (p.rd == 0) return C_STOP; size = 8; return C_LOAD;
+    case OP_c_ld: case OP_ld: size = 8; return C_LOAD;
+    case OP_c_lbu: case OP_lbu: size = 1; return C_LOAD;
+    case OP_c_lhu: case OP_lhu: size = 2; return C_LOAD;
+    case OP_c_lh: case OP_lh: size = 2; sext = 16; return C_LOAD;
+    case OP_lb: size = 1; sext = 8; return C_LOAD;
+    case OP_lwu: size = 4; return C_LOAD;
+    case OP_c_sb: case OP_sb: size = 1; return C_STORE;
+    case OP_c_sh: case OP_sh: size = 2; return C_STORE;
+    case OP_c_sw: case OP_sw: case OP_c_swsp: size = 4; return C_STORE;
+    case OP_c_sd: case OP_sd: case OP_c_sdsp: size = 8; return C_STORE;
+    case OP_c_addi: case OP_addi: expr = "A + IMM"; return C_ALU;
+    case OP_c_addiw: if (p.rd == 0) return C_STOP; expr = "sx32(A + IMM)"; return C_ALU;
+    case OP_addiw: expr = "sx32(A + IMM)"; return C_ALU;
+    case OP_c_li: case OP_lui: expr = "IMM"; return C_ALU;
+    case OP_c_addi16sp: if (imm == 0) return C_STOP; expr = "A + IMM"; return C_ALU;
+    case OP_c_lui: if (imm == 0) return C_STOP; expr = "IMM"; return C_ALU;
+    case OP_c_srli: case OP_srli: expr = "A >> IMM"; return C_ALU;
+    case OP_c_srai: case OP_srai: expr = "(uint64_t)((int64_t)A >> IMM)"; return C_ALU;
+    case OP_c_andi: case OP_andi: expr = "A & IMM"; return C_ALU;
+    case OP_c_sub: case OP_sub: expr = "A - B"; return C_ALU;
+    case OP_c_xor: case OP_xor_: expr = "A ^ B"; return C_ALU;
+    case OP_c_or: case OP_or_: expr = "A | B"; return C_ALU;
+    case OP_c_and: case OP_and_: expr = "A & B"; return C_ALU;
+    case OP_c_subw: case OP_subw: expr = "sx32((uint32_t)A - (uint32_t)B)"; return C_ALU;
+    case OP_c_addw: case OP_addw: expr = "sx32((uint32_t)A + (uint32_t)B)"; return C_ALU;
+    case OP_c_mul: case OP_mul: expr = "A * B"; return C_ALU;
+    case OP_c_zext_b: expr = "A & 0xFFULL"; return C_ALU;
+    case OP_c_sext_b: case OP_sext_b: expr = "(uint64_t)sext64(A & 0xFF, 8)"; return C_ALU;
+    case OP_c_zext_h: expr = "A & 0xFFFFULL"; return C_ALU;
+    case OP_c_sext_h: case OP_sext_h: expr = "(uint64_t)sext64(A & 0xFFFF, 16)"; return C_ALU;
+    case OP_c_zext_w: expr = "A & 0xFFFFFFFFULL"; return C_ALU;
+    case OP_c_not: expr = "~A"; return C_ALU;
+    case OP_c_j: return C_JAL;
+    case OP_c_beqz: cond = "A == 0"; return C_BR;
+    case OP_c_bnez: cond = "A != 0"; return C_BR;
+    case OP_c_slli: case OP_slli: expr = "A << IMM"; return C_ALU;
+    case OP_c_jr: if (p.rs1 == 0) return C_STOP; return C_JALR;
+    case OP_c_mv: expr = "B"; return C_ALU;
+    case OP_c_jalr: return C_JALR;
+    case OP_c_add: case OP_add: expr = "A + B"; return C_ALU;
+    case OP_fence: case OP_fence_i: case OP_prefetch_i: case OP_prefetch_r: case OP_prefetch_w: return C_NOP;
+    case OP_bseti: expr = "A | (1ULL << (IMM & 63))"; return C_ALU;
+    case OP_bclri: expr = "A & ~(1ULL << (IMM & 63))"; return C_ALU;
+    case OP_binvi: expr = "A ^ (1ULL << (IMM & 63))"; return C_ALU;
+    case OP_clz: expr = "(A ? (uint64_t)__builtin_clzll(A) : 64ULL)"; return C_ALU;
+    case OP_ctz: expr = "(A ? (uint64_t)__builtin_ctzll(A) : 64ULL)"; return C_ALU;
+    case OP_cpop: expr = "(uint64_t)__builtin_popcountll(A)"; return C_ALU;
+    case OP_slti: expr = "((int64_t)A < (int64_t)IMM ? 1ULL : 0ULL)"; return C_ALU;
+    case OP_sltiu: expr = "(A < IMM ? 1ULL : 0ULL)"; return C_ALU;
+    case OP_xori: expr = "A ^ IMM"; return C_ALU;
+    case OP_orc_b: expr = "orc_b(A)"; return C_ALU;
+    case OP_bexti: expr = "(A >> (IMM & 63)) & 1"; return C_ALU;
+    case OP_rori: expr = "(A >> IMM) | (A << ((64 - IMM) & 63))"; return C_ALU;
+    case OP_rev8: expr = "__builtin_bswap64(A)"; return C_ALU;
+    case OP_ori_hint: case OP_ori: expr = "A | IMM"; return C_ALU;
+    case OP_auipc: expr = "PC + IMM"; return C_ALU;
+    case OP_slliw: expr = "sx32((uint32_t)A << IMM)"; return C_ALU;
+    case OP_slli_uw: expr = "(A & 0xFFFFFFFFULL) << IMM"; return C_ALU;
+    case OP_clzw: expr = "((uint32_t)A ? (uint64_t)__builtin_clz((uint32_t)A) : 32ULL)"; return C_ALU;
+    case OP_ctzw: expr = "((uint32_t)A ? (uint64_t)__builtin_ctz((uint32_t)A) : 32ULL)"; return C_ALU;
+    case OP_cpopw: expr = "(uint64_t)__builtin_popcount((uint32_t)A)"; return C_ALU;
+    case OP_srliw: expr = "sx32((uint32_t)A >> IMM)"; return C_ALU;
+    case OP_sraiw: expr = "(uint64_t)(int64_t)((int32_t)(uint32_t)A >> IMM)"; return C_ALU;
+    case OP_roriw: expr = "sx32(((uint32_t)A >> IMM) | ((uint32_t)A << ((32 - IMM) & 31)))"; return C_ALU;
+    case OP_sll: expr = "A << (B & 63)"; return C_ALU;
+    case OP_mulh: expr = "(uint64_t)__mul64hi((int64_t)A, (int64_t)B)"; return C_ALU;
+    case OP_clmul: expr = "clmul(A, B)"; return C_ALU;
+    case OP_bset: expr = "A | (1ULL << (B & 63))"; return C_ALU;
+    case OP_bclr: expr = "A & ~(1ULL << (B & 63))"; return C_ALU;
+    case OP_rol: expr = "((A << (B & 63)) | (A >> ((64 - (B & 63)) & 63)))"; return C_ALU;
+    case OP_binv: expr = "A ^ (1ULL << (B & 63))"; return C_ALU;
+    case OP_slt: expr = "((int64_t)A < (int64_t)B ? 1ULL : 0ULL)"; return C_ALU;
+    case OP_mulhsu: expr = "(__umul64hi(A, B) - (((int64_t)A < 0) ? B : 0ULL))"; return C_ALU;
+    case OP_clmulr: expr = "clmulr(A, B)"; return C_ALU;
+    case OP_sh1add: expr = "(A << 1) + B"; return C_ALU;
+    case OP_sltu: expr = "(A < B ? 1ULL : 0ULL)"; return C_ALU;
+    case OP_mulhu: expr = "__umul64hi(A, B)"; return C_ALU;
+    case OP_clmulh: expr = "clmulh(A, B)"; return C_ALU;
+    case OP_div_: expr = "div64(A, B)"; return C_ALU;
+    case OP_pack: expr = "(B << 32) | (A & 0xFFFFFFFFULL)"; return C_ALU;
+    case OP_min_: expr = "((int64_t)A < (int64_t)B ? A : B)"; return C_ALU;
+    case OP_sh2add: expr = "(A << 2) + B"; return C_ALU;
+    case OP_xnor: expr = "~(A ^ B)"; return C_ALU;
+    case OP_srl: expr = "A >> (B & 63)"; return C_ALU;
+    case OP_divu: expr = "(B == 0 ? ~0ULL : A / B)"; return C_ALU;
+    case OP_czero_eqz: expr = "(B == 0 ? 0ULL : A)"; return C_ALU;
+    case OP_sra: expr = "(uint64_t)((int64_t)A >> (B & 63))"; return C_ALU;
+    case OP_minu: expr = "(A < B ? A : B)"; return C_ALU;
+    case OP_bext: expr = "(A >> (B & 63)) & 1"; return C_ALU;
+    case OP_ror: expr = "((A >> (B & 63)) | (A << ((64 - (B & 63)) & 63)))"; return C_ALU;
+    case OP_rem: expr = "rem64(A, B)"; return C_ALU;
+    case OP_max_: expr = "((int64_t)A > (int64_t)B ? A : B)"; return C_ALU;
+    case OP_sh3add: expr = "(A << 3) + B"; return C_ALU;
+    case OP_orn: expr = "A | ~B"; return C_ALU;
+    case OP_remu: expr = "(B == 0 ? A : A % B)"; return C_ALU;
+    case OP_packh: expr = "((B & 0xFF) << 8) | (A & 0xFF)"; return C_ALU;
+    case OP_maxu: expr = "(A > B ? A : B)"; return C_ALU;
+    case OP_czero_nez: expr = "(B != 0 ? 0ULL : A)"; return C_ALU;
+    case OP_andn: expr = "A & ~B"; return C_ALU;
+    case OP_mulw: expr = "sx32((uint32_t)A * (uint32_t)B)"; return C_ALU;
+    case OP_add_uw: expr = "(A & 0xFFFFFFFFULL) + B"; return C_ALU;
+    case OP_sllw: expr = "sx32((uint32_t)A << (B & 31))"; return C_ALU;
+    case OP_rolw: expr = "rolw(A, B)"; return C_ALU;
+    case OP_sh1add_uw: expr = "((A & 0xFFFFFFFFULL) << 1) + B"; return C_ALU;
+    case OP_divw: expr = "divw(A, B)"; return C_ALU;
+    case OP_packw: expr = "sx32(((B & 0xFFFF) << 16) | (A & 0xFFFF))"; return C_ALU;
+    case OP_sh2add_uw: expr = "((A & 0xFFFFFFFFULL) << 2) + B"; return C_ALU;
+    case OP_srlw: expr = "sx32((uint32_t)A >> (B & 31))"; return C_ALU;
+    case OP_divuw: expr = "((uint32_t)B == 0 ? ~0ULL : sx32((uint32_t)A / (uint32_t)B))"; return C_ALU;
+    case OP_sraw: expr = "(uint64_t)(int64_t)((int32_t)(uint32_t)A >> (B & 31))"; return C_ALU;
+    case OP_rorw: expr = "rorw(A, B)"; return C_ALU;
+    case OP_remw: expr = "remw(A, B)"; return C_ALU;
+    case OP_sh3add_uw: expr = "((A & 0xFFFFFFFFULL) << 3) + B"; return C_ALU;
+    case OP_remuw: expr = "((uint32_t)B == 0 ? sx32(A) : sx32((uint32_t)A % (uint32_t)B))"; return C_ALU;
+    case OP_beq: cond = "A == B"; return C_BR;
+    case OP_bne: cond = "A != B"; return C_BR;
+    case OP_blt: cond = "(int64_t)A < (int64_t)B"; return C_BR;
+    case OP_bge: cond = "(int64_t)A >= (int64_t)B"; return C_BR;
+    case OP_bltu: cond = "A < B"; return C_BR;
+    case OP_bgeu: cond = "A >= B"; return C_BR;
+    case OP_jalr: return C_JALR;
+    case OP_jal: return C_JAL;
+    default: return C_STOP;   // ecall, ebreak, CSR, escapes, unknown
+    }
+}
+
+// Substitute A, B, IMM, PC in an expression template (whole tokens only).
+std::string subst(const std::string &t, const std::string &a, const std::string &b, const std::string &imm,
+                  const std::string &pc) {
+    std::string r;
+    for (size_t i = 0; i < t.size();) {
+        auto tok = [&](const char *w) {
+            const size_t n = strlen(w);
+            if (t.compare(i, n, w) != 0) return false;
+            const bool lb = i == 0 || !(isalnum((unsigned char)t[i - 1]) || t[i - 1] == '_');
+            const bool rb = i + n >= t.size() || !(isalnum((unsigned char)t[i + n]) || t[i + n] == '_');
+            return lb && rb;
+        };
+        if (tok("IMM")) { r += imm; i += 3; }
+        else if (tok("PC")) { r += pc; i += 2; }
+        else if (tok("A")) { r += a; i += 1; }
+        else if (tok("B")) { r += b; i += 1; }
+        else r += t[i++];
+    }
+    return r;
+}
+
+const char *ltype(uint32_t size) {
+    return size == 1 ? "uint8_t" : size == 2 ? "uint16_t" : size == 4 ? "uint32_t" : "uint64_t";
+}
+
+}  // namespace
+
+// Leaders: the first executed instruction, every instruction the golden run
+// reached other than by falling through, the successor of every executed
+// control transfer or ecall, and the extra pcs (snapshot pcs: where waves
+// start).  trace = halfword index per golden event (bit 31: ecall).
+std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
+                             const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
+                             uint32_t &n_insts) {
+    std::set<uint32_t> executed, leaders;
+    auto valid = [&](uint32_t h) { return h < pre.size() && (pre[h].flags & kPreValid); };
+    for (size_t i = 0; i < trace.size(); i++) {
+        const uint32_t h = trace[i] & 0x7FFFFFFFu;
+        if (!valid(h)) continue;
+        executed.insert(h);
+        const bool is_ecall = trace[i] & 0x80000000u;
+        if (i == 0) leaders.insert(h);
+        if (i + 1 < trace.size()) {
+            const uint32_t nh = trace[i + 1] & 0x7FFFFFFFu;
+            if (is_ecall || nh != h + pre[h].len / 2u) leaders.insert(nh);
+        }
+    }
+    for (uint32_t h : executed) {   // successors of control transfers
+        std::string e;
+        uint32_t sz;
+        int sx;
+        const char *cond;
+        const Cls k = classify(pre[h], e, sz, sx, cond);
+        if ((k == C_BR || k == C_JAL || k == C_JALR) && executed.count(h + pre[h].len / 2u))
+            leaders.insert(h + pre[h].len / 2u);
+    }
+    for (uint64_t pc : extra_pcs) {
+        if (pc < text_lo || ((pc - text_lo) & 1)) continue;
+        const uint64_t h = (pc - text_lo) / 2;
+        if (h < pre.size() && executed.count((uint32_t)h)) leaders.insert((uint32_t)h);
+    }
+    // drop leaders whose first instruction is not translatable (no block)
+    for (auto it = leaders.begin(); it != leaders.end();) {
+        std::string e;
+        uint32_t sz;
+        int sx;
+        const char *cond;
+        if (!valid(*it) || classify(pre[*it], e, sz, sx, cond) == C_STOP) it = leaders.erase(it);
+        else ++it;
+    }
+
+    Gen g{pre, text_lo, leaders, executed, {}};
+    n_insts = 0;
+    g.put("tx_dispatch: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", (unsigned long long)text_lo);
+    g.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto tx_out;\n  switch ((uint32_t)off_ >> 1) {\n");
+    for (uint32_t h : leaders) g.put("  case %u: goto B_%u;\n", h, h);
+    g.put("  default: goto tx_out;\n  }\n}\n");
+
+    for (uint32_t h0 : leaders) {
+        // the block: instructions from h0 until a control transfer (inclusive),
+        // an untranslatable or unexecuted instruction, or the next leader
+        std::vector<uint32_t> insts;
+        uint32_t h = h0;
+        bool term = false;
+        for (;;) {
+            if (!valid(h) || !executed.count(h)) break;
+            if (h != h0 && leaders.count(h)) break;
+            std::string e;
+            uint32_t sz;
+            int sx;
+            const char *cond;
+            const Cls k = classify(pre[h], e, sz, sx, cond);
+            if (k == C_STOP) break;
+            insts.push_back(h);
+            if (k == C_BR || k == C_JAL || k == C_JALR) { term = true; break; }
+            h += pre[h].len / 2u;
+        }
+        const uint32_t n = (uint32_t)insts.size();
+        n_insts += n;
+        const uint64_t pc0 = g.pc_of(h0);
+        g.put("B_%u: { // pc 0x%llx, %u insts\n", h0, (unsigned long long)pc0, n);
+        g.put("  if (budget - steps < %uu || !ult64(0x%llxULL, wait_min)) { spc = 0x%llxULL; goto tx_out; }\n", n,
+              (unsigned long long)pc0, (unsigned long long)pc0);
+        uint32_t k_st = 0, k_xt = 0, k_fb = 0, k_db = 0;   // committed so far in this block
+        auto commit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
+            std::string s = "steps += " + std::to_string(st) + "u; ";
+            if (xt) s += "xticks += " + std::to_string(xt) + "u; ";
+            s += "fbytes += " + std::to_string(fb) + "u; ";
+            if (db) s += "dbytes += " + std::to_string(db) + "u; ";
+            return s;
+        };
+        for (uint32_t i = 0; i < n; i++) {
+            const PreInst &p = pre[insts[i]];
+            const uint64_t pc = g.pc_of(insts[i]);
+            const uint64_t ft = pc + p.len;
+            std::string e;
+            uint32_t sz;
+            int sx;
+            const char *cond;
+            const Cls k = classify(p, e, sz, sx, cond);
+            const std::string A = Gen::R(p.rs1), B = Gen::R(p.rs2);
+            char immb[48], pcb[32], ftb[32];
+            snprintf(immb, sizeof immb, "((uint64_t)(int64_t)%dLL)", p.imm);
+            snprintf(pcb, sizeof pcb, "0x%llxULL", (unsigned long long)pc);
+            snprintf(ftb, sizeof ftb, "0x%llxULL", (unsigned long long)ft);
+            const uint32_t xt = (p.flags & kPreStraddle) ? 1 : 0;
+            const std::string leave_here = "{ " + commit(k_st, k_xt, k_fb, k_db) + "spc = " + pcb + "; goto tx_out; }";
+            switch (k) {
+            case C_ALU:
+                if (p.rd) g.put("  X%u = %s;\n", p.rd, subst(e, A, B, immb, pcb).c_str());
+                break;
+            case C_NOP:
+                break;
+            case C_LOAD:
+                g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, false, p_, tx);\n", A.c_str(), immb, sz);
+                g.put("    if (__ballot(mine && !ok_)) %s\n", leave_here.c_str());
+                if (p.rd) {
+                    g.put("    p_ = ok_ ? p_ : const_cast<uint8_t *>(zp);\n");
+                    if (sx) g.put("    X%u = (uint64_t)(int64_t)(int%d_t)*(const %s *)p_; }\n", p.rd, sx, ltype(sz));
+                    else g.put("    X%u = (uint64_t)*(const %s *)p_; }\n", p.rd, ltype(sz));
+                } else {
+                    g.put("  }\n");
+                }
+                break;
+            case C_STORE:
+                g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, true, p_, tx);\n", A.c_str(), immb, sz);
+                g.put("    if (__ballot(mine && !ok_)) %s\n", leave_here.c_str());
+                g.put("    p_ = (mine && ok_) ? p_ : sink; *(%s *)p_ = (%s)%s; }\n", ltype(sz), ltype(sz), B.c_str());
+                break;
+            case C_BR: {
+                const std::string c = subst(cond, A, B, immb, pcb);
+                const uint64_t tgt = pc + (int64_t)p.imm;
+                g.put("  { const bool c_ = %s; const uint64_t tk_ = __ballot(mine && c_);\n", c.c_str());
+                g.put("    %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
+                g.put("    if (tk_ == gm) %s\n", g.go(tgt).c_str());
+                g.put("    if (tk_ == 0) %s\n", g.go(ft).c_str());
+                g.put("    dpc = c_ ? 0x%llxULL : %s; div = true; goto tx_out; }\n", (unsigned long long)tgt, ftb);
+                break;
+            }
+            case C_JAL: {
+                const uint64_t tgt = pc + (int64_t)p.imm;
+                if (p.rd) g.put("  X%u = %s;\n", p.rd, ftb);
+                g.put("  %s %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), g.go(tgt).c_str());
+                break;
+            }
+            case C_JALR: {
+                const int64_t im = (p.op == OP_jalr) ? p.imm : 0;
+                const uint32_t rd = (p.op == OP_c_jalr) ? 1 : (p.op == OP_c_jr ? 0 : p.rd);
+                g.put("  { const uint64_t t_ = (%s + (uint64_t)(int64_t)%lldLL) & ~1ULL;\n", A.c_str(), (long long)im);
+                if (rd) g.put("    X%u = %s;\n", rd, ftb);
+                g.put("    %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
+                g.put("    const uint64_t t0_ = readlane64(t_, glane);\n");
+                g.put("    if (__ballot(mine && t_ != t0_)) { dpc = t_; div = true; goto tx_out; }\n");
+                g.put("    spc = uni64(t0_); goto tx_dispatch; }\n");
+                break;
+            }
+            default:
+                break;
+            }
+            k_st += 1; k_xt += xt; k_fb += p.len; k_db += (k == C_LOAD || k == C_STORE) ? sz : 0;
+        }
+        if (!term) {   // fell into the next leader, or stops before an instruction it does not cover
+            const uint64_t nxt = n ? g.pc_of(insts[n - 1]) + pre[insts[n - 1]].len : pc0;
+            g.put("  %s %s\n", commit(k_st, k_xt, k_fb, k_db).c_str(), g.go(nxt).c_str());
+        }
+        g.put("}\n");
+    }
+    leaders_out.assign(leaders.begin(), leaders.end());
+    return g.out;
+}
+
+}  // namespace fi

@@ -2,9 +2,8 @@
 // CDNA4 kernels (hip/fi_kernels.hip).  Internal; the public ABI is
 // include/fi_engine.h.
 #pragma once
-#include <stdint.h>
-
-#include "../../include/fi_engine.h"
+#include "fi_rtc.h"
+#include "fi_engine.h"
 
 namespace fi {
 
@@ -28,6 +27,7 @@ struct PreInst {
 };
 static_assert(sizeof(PreInst) == 16, "PreInst must stay 16 bytes (one s_load_dwordx4)");
 constexpr uint8_t kPreValid = 1, kPreStraddle = 2, kPreRs1 = 4, kPreRs2 = 8, kPreRd = 16;
+constexpr uint8_t kPreLeader = 32;   // a translated golden basic block starts here (load-time build)
 
 // Golden snapshot: the architectural state at the top of the first tick with
 // numInst == k * snap_interval, plus the page table of the whole guest address
@@ -56,6 +56,8 @@ struct DevCtx {
     // golden text, pre-decoded (pre_ok = 0 if the golden run rewrote its text)
     const PreInst *pre;
     uint64_t text_lo, text_hi;       // page-aligned executable range
+    uint64_t code_lo, code_hi;       // exact byte range of the executable segments: pre-decoded entries are valid
+                                     // inside it only, and a lane's store into it makes its text "dirty"
     uint32_t pre_ok;
     uint32_t text_bytes;             // text_hi - text_lo (< 4 GiB)
     uint32_t record;                 // 1 = golden run: record output (and snapshots) instead of comparing
@@ -81,6 +83,7 @@ struct DevCtx {
     // per-trial private (copy-on-write) pages: frames [slot][P][4096], vpns [P][n]
     uint8_t *priv_frames;
     uint64_t *priv_vpn;
+    uint8_t *tx_sink;                // translated code: stores of lanes outside the running group land here
     // record mode: snapshot capture at numInst == k * rec_interval
     SnapState *rec_snaps;            // [rec_max_snaps]
     uint8_t *rec_pages;              // [rec_max_snaps][priv_pages][4096]
@@ -95,10 +98,13 @@ struct DevCtx {
     const uint32_t *perm;            // launch slot -> index into sites/out (sorted by site.inst)
     fi_outcome *out;
     uint64_t n;                      // trials in this launch
+    uint64_t *wave_dbg;              // per wave: {s_memtime cycles, loop iterations, translated insts, slow fetches}
     unsigned long long *stats;       // [0] fetch B [1] data B [2] pages [3..5] golden ncycles/out/err
                                      // [6] loop iterations [7] lane-insts [8] slow fetches [9] min-PC [10] max iter/wave
                                      // [11] early-exit checks [12] early exits [13] snapshots captured [14] start-inst sum
-                                     // [15] golden trace events [20] wave-0 s_memtime delta [21] s_memrealtime delta
+                                     // [15] golden trace events [16] translated insts [17] translated entries
+                                     // [18] slowest wave: iters<<32 | tx permille<<20 | entries [19] iters<<32 | slow
+                                     // [20] wave-0 s_memtime delta [21] s_memrealtime delta
 };
 
 struct SampleCtx {

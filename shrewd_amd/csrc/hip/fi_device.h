@@ -1,7 +1,6 @@
 // fi_device.h -- wave-level helpers shared by the CDNA4 kernels.
 #pragma once
-#include <hip/hip_runtime.h>
-#include <stdint.h>
+#include "fi_rtc.h"
 
 namespace fi {
 

@@ -10,7 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
-#include "../fi_types.h"
+#include "fi_types.h"
 #include "fi_device.h"
 #include "rv64_isa.h"
 
@@ -63,7 +63,8 @@ __global__ void fi_keys_kernel(const fi_site *sites, uint64_t n, uint64_t *keys,
 // pc & ~3; pc % 4 != 0 takes its upper half; a 32-bit instruction starting in
 // an upper half needs a second fetch tick (the "straddle").  Odd PCs behave
 // like pc | 2 of the same word (handled by the caller's key computation).
-__global__ void fi_predecode_kernel(const uint8_t *text, uint64_t text_lo, uint64_t nhalf, PreInst *pre) {
+__global__ void fi_predecode_kernel(const uint8_t *text, uint64_t code_off, uint64_t code_end, uint64_t nhalf,
+                                    PreInst *pre) {
     const uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= nhalf) return;
     const uint64_t off = h * 2;
@@ -83,6 +84,9 @@ __global__ void fi_predecode_kernel(const uint8_t *text, uint64_t text_lo, uint6
             else raw |= ((uint32_t)text[off + 2] << 16) | ((uint32_t)text[off + 3] << 24);
         }
     }
+    // only instructions whose bytes lie inside the executable segments: a
+    // lane's stores elsewhere in the text pages do not invalidate the table
+    if (off < code_off || off + ((raw & 3) == 3 ? 4 : 2) > code_end) ok = false;
     if (ok) {
         Dec d = rv_decode(raw);
         const uint16_t u = uop_of(d);   // may normalise d.imm (c.zext.b/h, c.not)
@@ -91,7 +95,6 @@ __global__ void fi_predecode_kernel(const uint8_t *text, uint64_t text_lo, uint6
         p.flags = (uint8_t)(kPreValid | (straddle ? kPreStraddle : 0) | d.flags);
     }
     pre[h] = p;
-    (void)text_lo;
 }
 
 __global__ void fi_debug_decode_kernel(const uint32_t *raws, uint64_t n, PreInst *out) {
@@ -140,8 +143,10 @@ hipError_t launch_keys(const fi_site *sites, uint64_t n, uint64_t *keys, uint32_
     hipLaunchKernelGGL(fi_keys_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, sites, n, keys, perm);
     return hipGetLastError();
 }
-hipError_t launch_predecode(const uint8_t *text, uint64_t text_lo, uint64_t nhalf, PreInst *pre, hipStream_t st) {
-    hipLaunchKernelGGL(fi_predecode_kernel, dim3(nblk(nhalf, 256)), dim3(256), 0, st, text, text_lo, nhalf, pre);
+hipError_t launch_predecode(const uint8_t *text, uint64_t code_off, uint64_t code_end, uint64_t nhalf, PreInst *pre,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(fi_predecode_kernel, dim3(nblk(nhalf, 256)), dim3(256), 0, st, text, code_off, code_end, nhalf,
+                       pre);
     return hipGetLastError();
 }
 hipError_t launch_debug_decode(const uint32_t *raws, uint64_t n, PreInst *out, hipStream_t st) {

@@ -20,9 +20,8 @@
 //     text, the guest PC lives in SGPRs and each instruction is one scalar
 //     dispatch; the pre-decoded entries of both successors are prefetched with
 //     scalar loads while the current instruction executes.
-#include <hip/hip_runtime.h>
-
-#include "../fi_types.h"
+#include "fi_rtc.h"
+#include "fi_types.h"
 #include "fi_device.h"
 #include "rv64_isa.h"
 
@@ -40,6 +39,60 @@ typedef __attribute__((address_space(4))) const DevCtx KCtx;
 __device__ __forceinline__ KCtx *opq(KCtx *p) {
     asm volatile("" : "+s"(p));
     return p;
+}
+
+// ------------------------------------------------------------------ semantics
+// Integer helpers of the generated StaticInst::execute bodies
+// (src/arch/riscv/isa/decoder.isa; div/rem edge cases src/arch/riscv/utility.hh:
+// 191-231), shared by the general path below and the translated blocks.
+__device__ __forceinline__ uint64_t orc_b(uint64_t a) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) if ((a >> (8 * i)) & 0xFF) v |= 0xFFULL << (8 * i);
+    return v;
+}
+__device__ __forceinline__ uint64_t clmul(uint64_t a, uint64_t b) {
+    uint64_t v = 0;
+    for (int i = 0; i < 64; i++) if ((b >> i) & 1) v ^= a << i;
+    return v;
+}
+__device__ __forceinline__ uint64_t clmulr(uint64_t a, uint64_t b) {
+    uint64_t v = 0;
+    for (int i = 0; i < 64; i++) if ((b >> i) & 1) v ^= a >> (63 - i);
+    return v;
+}
+__device__ __forceinline__ uint64_t clmulh(uint64_t a, uint64_t b) {
+    uint64_t v = 0;
+    for (int i = 1; i < 64; i++) if ((b >> i) & 1) v ^= a >> (64 - i);
+    return v;
+}
+__device__ __forceinline__ uint64_t div64(uint64_t a, uint64_t b) {
+    const int64_t x = (int64_t)a, y = (int64_t)b;
+    return y == 0 ? ~0ULL : (x == INT64_MIN && y == -1) ? (uint64_t)x : (uint64_t)(x / y);
+}
+__device__ __forceinline__ uint64_t rem64(uint64_t a, uint64_t b) {
+    const int64_t x = (int64_t)a, y = (int64_t)b;
+    return y == 0 ? a : (x == INT64_MIN && y == -1) ? 0 : (uint64_t)(x % y);
+}
+__device__ __forceinline__ uint64_t divw(uint64_t a, uint64_t b) {
+    const int32_t x = (int32_t)a, y = (int32_t)b;
+    const int32_t q = y == 0 ? -1 : (x == INT32_MIN && y == -1) ? x : x / y;
+    return (uint64_t)(int64_t)q;
+}
+__device__ __forceinline__ uint64_t remw(uint64_t a, uint64_t b) {
+    const int32_t x = (int32_t)a, y = (int32_t)b;
+    const int32_t r = y == 0 ? x : (x == INT32_MIN && y == -1) ? 0 : x % y;
+    return (uint64_t)(int64_t)r;
+}
+__device__ __forceinline__ uint64_t rolw(uint64_t a, uint64_t b) {
+    const uint32_t x = (uint32_t)a;
+    const int sh = (int)(b & 31);
+    return sx32((x << sh) | (x >> ((32 - sh) & 31)));
+}
+__device__ __forceinline__ uint64_t rorw(uint64_t a, uint64_t b) {
+    const uint32_t x = (uint32_t)a;
+    const int sh = (int)(b & 31);
+    return sx32((x >> sh) | (x << ((32 - sh) & 31)));
 }
 
 // ------------------------------------------------------------------ memory
@@ -141,6 +194,7 @@ __device__ int mem_access(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, 
     if (wr) {
         if (!(p1 & 1)) { m.req_vpn = ea >> 12; m.req_src = page_of(p1); return F_NEEDPAGE; }
         if (!(p2 & 1)) { m.req_vpn = ea2 >> 12; m.req_src = page_of(p2); return F_NEEDPAGE; }
+        if (ea < c->code_hi && ea + size > c->code_lo) m.code_dirty = true;   // the lane rewrote its code
         uint8_t *w1 = const_cast<uint8_t *>(page_of(p1));
         if (n1 == size && (off & (size - 1)) == 0) {
             switch (size) {
@@ -371,6 +425,20 @@ __device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32
     return true;
 }
 
+// The pre-decoded text (uniform): table, text range, exact code range.
+struct TextRef { const PreInst *pre; uint32_t lo, hi, bytes; uint64_t clo, chi; };
+
+// Translated-code memory access: the page must be in the lane's TLB (and be
+// its private copy for a store) and the access naturally aligned; anything
+// else leaves the translated code before the instruction (the interpreter
+// handles misses, copy-on-write, faults and misaligned accesses).
+__device__ __forceinline__ bool tx_probe(const LaneMem &m, uint64_t ea, uint32_t size, bool st, uint8_t *&p,
+                                         const TextRef &t) {
+    const uint64_t e = tlb_find(m, ea >> 12);
+    p = const_cast<uint8_t *>(page_of(e)) + (ea & 4095);
+    return e && (!st || ((e & 1) && (ea >= t.chi || ea + size <= t.clo))) && (ea & (size - 1)) == 0;
+}
+
 // ------------------------------------------------------------------ trial kernel
 // Diagnostic build only (-DFI_PROF): s_memtime stamps at the phase boundaries
 // of the fast loop, summed per wave into stats[24..27] (never in the shipped
@@ -403,7 +471,6 @@ __device__ __forceinline__ Pre4 pre_load(const PreInst *p) {
 // key = (pc & ~1) | ((pc & 1) << 1).  The host guarantees that the text does
 // not cross a 4 GiB boundary (32-bit compares only: SALU has no 64-bit <).
 struct PreRef { Pre4 e; bool in; };
-struct TextRef { const PreInst *pre; uint32_t lo, hi, bytes; };
 __device__ __forceinline__ PreRef pre_entry(const TextRef &t, uint64_t pc) {
     const uint32_t klo = ((uint32_t)pc & ~1u) | (((uint32_t)pc & 1u) << 1);
     const uint32_t off = klo - t.lo;
@@ -419,7 +486,11 @@ __device__ __forceinline__ bool ult64(uint64_t a, uint64_t b) {
     return ah < bh || (ah == bh && (uint32_t)a < (uint32_t)b);
 }
 
+#ifdef __HIPCC_RTC__
+extern "C" __global__ void __launch_bounds__(64) fi_trial_kernel_tx(DevCtx ctx_arg) {
+#else
 __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
+#endif
     (void)ctx_arg;
     KCtx *const kc = (KCtx *)__builtin_amdgcn_kernarg_segment_ptr();
 #define CX (opq(kc))
@@ -471,6 +542,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     uint64_t plast = __builtin_amdgcn_s_memtime();
 #endif
     uint32_t n_iter = 0, n_slow = 0, n_min = 0, n_exec = 0, n_chk = 0, n_early = 0;   // per-wave (uniform)
+    uint32_t n_tx = 0, n_txin = 0;   // instructions run in translated blocks, entries into them
 
     for (;;) {
         // ---- A. materialise requested pages, whole wave cooperating
@@ -494,7 +566,6 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                     finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, (uint32_t)L.pc);
                 } else {
                     CX->priv_vpn[(uint64_t)m.n_priv * CX->n + slot] = m.req_vpn;
-                    if ((m.req_vpn << 12) >= CX->text_lo && (m.req_vpn << 12) < CX->text_hi) m.code_dirty = true;
                     m.n_priv++;
                     pages_made++;
                 }
@@ -523,6 +594,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 } else {
                     uint64_t *wp = (uint64_t *)(const_cast<uint8_t *>(page_of(p)) + (s.addr & 4095));
                     *wp ^= s.mask;
+                    if (s.addr < CX->code_hi && s.addr + 8 > CX->code_lo) m.code_dirty = true;
                     L.injected = 1;
                 }
             } else {
@@ -626,6 +698,57 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         if (L.next_chk < next_ev) next_ev = L.next_chk;
         if (next_snap < next_ev) next_ev = next_snap;
 
+#ifdef FI_TX
+        // ---- TRANSLATED PATH (load-time build only): the golden run's basic
+        // blocks compiled to straight-line code with the guest registers in
+        // VGPRs.  Entered at a block leader by a converged group
+        // with nothing watched or modified; leaves at anything the blocks do
+        // not cover (events, divergence, faults, copy-on-write, syscalls,
+        // TLB misses, untranslated pcs), with every counter exact.  The code
+        // runs in uniform control flow with every lane active: lanes outside
+        // the group compute on their own copies, read the zero page, store to
+        // a sink, and write nothing back.
+        if (!CX->record) {
+            TextRef tx;
+            tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
+            tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
+            const PreRef E0 = pre_entry(tx, lpc);
+            if (!(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader) &&
+                __ballot(mine && (m.code_dirty || L.watch > 0)) == 0) {
+                const uint64_t gm = __ballot(mine);
+                const int glane = __ffsll((unsigned long long)gm) - 1;
+                const uint64_t budget64 = uni64(wave_min64(mine ? next_ev - L.ninst : kNone));
+                const uint32_t budget = budget64 > (1u << 30) ? (1u << 30) : (uint32_t)budget64;
+                const uint8_t *const zp = CX->zero_page;
+                uint8_t *const sink = CX->tx_sink + 8 * lane;
+                uint32_t steps = 0, xticks = 0, fbytes = 0, dbytes = 0;
+                uint64_t spc = lpc, dpc = 0;
+                bool div = false;
+#define TXR(r) uint64_t X##r = RREG(r);
+                TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
+                TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
+                TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
+#undef TXR
+                goto tx_dispatch;
+                /*@TX_BODY@*/
+            tx_out:
+                if (mine) {
+#define TXW(r) RREG(r) = X##r;
+                    TXW(1) TXW(2) TXW(3) TXW(4) TXW(5) TXW(6) TXW(7) TXW(8) TXW(9) TXW(10) TXW(11) TXW(12) TXW(13)
+                    TXW(14) TXW(15) TXW(16) TXW(17) TXW(18) TXW(19) TXW(20) TXW(21) TXW(22) TXW(23) TXW(24) TXW(25)
+                    TXW(26) TXW(27) TXW(28) TXW(29) TXW(30) TXW(31)
+#undef TXW
+                    L.ninst += steps; L.ncyc += steps + xticks; L.fetch_b += fbytes; L.data_b += dbytes;
+                    L.pc = div ? dpc : spc;
+                }
+                n_iter += steps;
+                n_tx += steps;
+                n_txin++;
+                if (steps) continue;
+            }
+        }
+#endif
+
         // ---- FAST PATH: the group is converged on golden text with nothing
         // watched or modified -- run pre-decoded micro-ops with PC, instruction,
         // cycle and byte counts in SGPRs until an event is due, the group
@@ -643,7 +766,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             bool div = false;
             TextRef tx;
             tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
-            tx.bytes = CX->text_bytes;
+            tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
             PreRef E = pre_entry(tx, spc);
             while (budget) {
                 PSTAMP(3);
@@ -651,6 +774,9 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 const uint32_t q1 = uni32(E.e.y), q2 = uni32(E.e.z), q3 = uni32(E.e.w);
                 const uint32_t aux = q3 >> 16, kind = aux & 63;
                 if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
+#ifdef FI_TX
+                if (steps && ((q3 >> 8) & kPreLeader)) break;   // translated blocks take over here
+#endif
                 const uint32_t rd = q1 >> 8 & 0xFF, rs1 = q1 >> 16 & 0xFF, rs2 = q1 >> 24;
                 const int64_t imm = (int32_t)q2;
                 const uint32_t len = q3 & 0xFF, straddle = ((q3 >> 8) & kPreStraddle) ? 1 : 0;
@@ -718,7 +844,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                         p = tlb_find(m, ea >> 12);
                         if (!p) p = lookup_full(CX, w, m, slot, ea >> 12);
                     }
-                    const bool ok = p && (!st || (p & 1)) && off + msz <= 4096;
+                    const bool ok = p && (!st || ((p & 1) && (ea >= tx.chi || ea + msz <= tx.clo))) && off + msz <= 4096;
                     if (__ballot(mine && !ok) != 0) { msz = 0xFFFFFFFFu; break; }   // bail: general path
                     if (mine) {
                         uint8_t *pg = const_cast<uint8_t *>(page_of(p));
@@ -920,12 +1046,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             case OP_slti: v = (int64_t)a < imm ? 1 : 0; break;
             case OP_sltiu: v = a < (uint64_t)imm ? 1 : 0; break;
             case OP_xori: v = a ^ (uint64_t)imm; break;
-            case OP_orc_b: {
-                v = 0;
-#pragma unroll
-                for (int i = 0; i < 8; i++) if ((a >> (8 * i)) & 0xFF) v |= 0xFFULL << (8 * i);
-                break;
-            }
+            case OP_orc_b: v = orc_b(a); break;
             case OP_bexti: v = (a >> (imm & 63)) & 1; break;
             case OP_rori: v = (a >> imm) | (a << ((64 - imm) & 63)); break;
             case OP_rev8: v = __builtin_bswap64(a); break;
@@ -942,23 +1063,19 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             case OP_roriw: { const uint32_t x = (uint32_t)a; v = sx32((x >> imm) | (x << ((32 - imm) & 31))); break; }
             case OP_sll: v = a << (b & 63); break;
             case OP_mulh: v = (uint64_t)__mul64hi((int64_t)a, (int64_t)b); break;
-            case OP_clmul: { v = 0; for (int i = 0; i < 64; i++) if ((b >> i) & 1) v ^= a << i; break; }
+            case OP_clmul: v = clmul(a, b); break;
             case OP_bset: v = a | (1ULL << (b & 63)); break;
             case OP_bclr: v = a & ~(1ULL << (b & 63)); break;
             case OP_rol: { const int sh = (int)(b & 63); v = (a << sh) | (a >> ((64 - sh) & 63)); break; }
             case OP_binv: v = a ^ (1ULL << (b & 63)); break;
             case OP_slt: v = (int64_t)a < (int64_t)b ? 1 : 0; break;
             case OP_mulhsu: v = __umul64hi(a, b) - (((int64_t)a < 0) ? b : 0); break;
-            case OP_clmulr: { v = 0; for (int i = 0; i < 64; i++) if ((b >> i) & 1) v ^= a >> (63 - i); break; }
+            case OP_clmulr: v = clmulr(a, b); break;
             case OP_sh1add: v = (a << 1) + b; break;
             case OP_sltu: v = a < b ? 1 : 0; break;
             case OP_mulhu: v = __umul64hi(a, b); break;
-            case OP_clmulh: { v = 0; for (int i = 1; i < 64; i++) if ((b >> i) & 1) v ^= a >> (64 - i); break; }
-            case OP_div_: {
-                const int64_t x = (int64_t)a, y = (int64_t)b;
-                v = y == 0 ? ~0ULL : (x == INT64_MIN && y == -1) ? (uint64_t)x : (uint64_t)(x / y);
-                break;
-            }
+            case OP_clmulh: v = clmulh(a, b); break;
+            case OP_div_: v = div64(a, b); break;
             case OP_pack: v = (b << 32) | (a & 0xFFFFFFFFULL); break;
             case OP_min_: v = (int64_t)a < (int64_t)b ? a : b; break;
             case OP_sh2add: v = (a << 2) + b; break;
@@ -970,11 +1087,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             case OP_minu: v = a < b ? a : b; break;
             case OP_bext: v = (a >> (b & 63)) & 1; break;
             case OP_ror: { const int sh = (int)(b & 63); v = (a >> sh) | (a << ((64 - sh) & 63)); break; }
-            case OP_rem: {
-                const int64_t x = (int64_t)a, y = (int64_t)b;
-                v = y == 0 ? a : (x == INT64_MIN && y == -1) ? 0 : (uint64_t)(x % y);
-                break;
-            }
+            case OP_rem: v = rem64(a, b); break;
             case OP_max_: v = (int64_t)a > (int64_t)b ? a : b; break;
             case OP_sh3add: v = (a << 3) + b; break;
             case OP_orn: v = a | ~b; break;
@@ -986,26 +1099,16 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             case OP_mulw: v = sx32((uint32_t)a * (uint32_t)b); break;
             case OP_add_uw: v = (a & 0xFFFFFFFFULL) + b; break;
             case OP_sllw: v = sx32((uint32_t)a << (b & 31)); break;
-            case OP_rolw: { const uint32_t x = (uint32_t)a; const int sh = (int)(b & 31); v = sx32((x << sh) | (x >> ((32 - sh) & 31))); break; }
+            case OP_rolw: v = rolw(a, b); break;
             case OP_sh1add_uw: v = ((a & 0xFFFFFFFFULL) << 1) + b; break;
-            case OP_divw: {
-                const int32_t x = (int32_t)a, y = (int32_t)b;
-                const int32_t q = y == 0 ? -1 : (x == INT32_MIN && y == -1) ? x : x / y;
-                v = (uint64_t)(int64_t)q;
-                break;
-            }
+            case OP_divw: v = divw(a, b); break;
             case OP_packw: v = sx32(((b & 0xFFFF) << 16) | (a & 0xFFFF)); break;
             case OP_sh2add_uw: v = ((a & 0xFFFFFFFFULL) << 2) + b; break;
             case OP_srlw: v = sx32((uint32_t)a >> (b & 31)); break;
             case OP_divuw: v = (uint32_t)b == 0 ? ~0ULL : sx32((uint32_t)a / (uint32_t)b); break;
             case OP_sraw: v = (uint64_t)(int64_t)((int32_t)(uint32_t)a >> (b & 31)); break;
-            case OP_rorw: { const uint32_t x = (uint32_t)a; const int sh = (int)(b & 31); v = sx32((x >> sh) | (x << ((32 - sh) & 31))); break; }
-            case OP_remw: {
-                const int32_t x = (int32_t)a, y = (int32_t)b;
-                const int32_t r = y == 0 ? x : (x == INT32_MIN && y == -1) ? 0 : x % y;
-                v = (uint64_t)(int64_t)r;
-                break;
-            }
+            case OP_rorw: v = rorw(a, b); break;
+            case OP_remw: v = remw(a, b); break;
             case OP_sh3add_uw: v = ((a & 0xFFFFFFFFULL) << 3) + b; break;
             case OP_remuw: v = (uint32_t)b == 0 ? sx32(a) : sx32((uint32_t)a % (uint32_t)b); break;
             case OP_beq: if (a == b) npc = pc + imm; wrd = false; break;
@@ -1077,6 +1180,16 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         if (cm != gmask) break;
         const uint64_t npc0 = uni64(readlane64(L.pc, __ffsll((unsigned long long)cm) - 1));
         if (__ballot(cont && L.pc == npc0) != cm || npc0 >= wait_min) break;
+        if (CX->pre_ok) {   // back to the fast path (or translated blocks) when they can take the next one
+            TextRef tn;
+            tn.pre = CX->pre; tn.lo = (uint32_t)CX->text_lo; tn.hi = (uint32_t)(CX->text_lo >> 32);
+            tn.bytes = CX->text_bytes; tn.clo = CX->code_lo; tn.chi = CX->code_hi;
+            const PreRef En = pre_entry(tn, npc0);
+            const uint32_t wn = uni32(En.e.w);
+            if (En.in && ((wn >> 8) & kPreValid) && ((wn >> 16) & 63) != K_SLOW &&
+                __ballot(cont && (m.code_dirty || L.watch > 0)) == 0)
+                break;
+        }
         lpc = npc0;
         mine = cont;
         n_iter++;
@@ -1095,6 +1208,13 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     if (lane == 0)
         for (int k = 0; k < 4; k++) atomicAdd(&CX->stats[24 + k], (unsigned long long)pacc[k]);
 #endif
+    if (lane == 0 && CX->wave_dbg) {
+        uint64_t *wd = CX->wave_dbg + 4 * (uint64_t)blockIdx.x;
+        wd[0] = __builtin_amdgcn_s_memtime() - t_start;
+        wd[1] = n_iter;
+        wd[2] = n_tx;
+        wd[3] = n_slow;
+    }
     if (blockIdx.x == 0 && lane == 0) {
         CX->stats[20] = __builtin_amdgcn_s_memtime() - t_start;
         CX->stats[21] = __builtin_amdgcn_s_memrealtime() - rt_start;
@@ -1113,12 +1233,21 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         atomicAdd(&CX->stats[11], (unsigned long long)n_chk);
         atomicAdd(&CX->stats[12], (unsigned long long)n_early);
         atomicAdd(&CX->stats[14], (unsigned long long)si);
+        atomicAdd(&CX->stats[16], (unsigned long long)n_tx);
+        atomicAdd(&CX->stats[17], (unsigned long long)n_txin);
+        // the slowest wave: iterations, translated permille, entries (packed)
+        atomicMax(&CX->stats[18], ((unsigned long long)n_iter << 32) |
+                                      ((unsigned long long)(n_iter ? (uint64_t)n_tx * 1000 / n_iter : 0) << 20) |
+                                      (n_txin < (1u << 20) ? n_txin : (1u << 20) - 1));
+        atomicMax(&CX->stats[19], ((unsigned long long)n_iter << 32) | (n_slow < 0xFFFFFFFFu ? n_slow : 0xFFFFFFFFu));
     }
 }
 
+#ifndef __HIPCC_RTC__
 hipError_t launch_trials(const DevCtx &c, hipStream_t st) {
     hipLaunchKernelGGL(fi_trial_kernel, dim3((unsigned)((c.n + 63) / 64)), dim3(64), 0, st, c);
     return hipGetLastError();
 }
+#endif
 
 }  // namespace fi

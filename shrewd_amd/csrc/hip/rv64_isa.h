@@ -9,9 +9,8 @@
 // The function is evaluated on wave-uniform (scalar) operands by the
 // pre-decode kernel and on the slow fetch path.
 #pragma once
-#include <stdint.h>
-
-#include "../gem5_decode_table.h"
+#include "fi_rtc.h"
+#include "gem5_decode_table.h"
 
 #define FI_OPS(X) \
     X(UNKNOWN) X(ESC_FP) X(ESC_VEC) X(ESC_AMO) X(ESC_SYS) X(ESC_CRYPTO) X(ESC_CBO) X(ESC_CMP) X(ESC_M5) X(ESC_HYP) \

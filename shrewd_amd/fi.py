@@ -70,13 +70,15 @@ class _Config(C.Structure):
 
 CFG_NO_SNAPSHOT_START = 1
 CFG_NO_EARLY_EXIT = 2
+CFG_NO_TRANSLATE = 4
 
 
 class GoldenInfo(C.Structure):
     _fields_ = [("ninst", C.c_uint64), ("ncycles", C.c_uint64), ("exit_code", C.c_uint32), ("pad", C.c_uint32),
                 ("stdout_len", C.c_uint64), ("stderr_len", C.c_uint64), ("fetch_bytes", C.c_uint64),
                 ("data_bytes", C.c_uint64), ("snapshots", C.c_uint64), ("snapshot_interval", C.c_uint64),
-                ("snapshot_frames", C.c_uint64)]
+                ("snapshot_frames", C.c_uint64), ("translated_blocks", C.c_uint64),
+                ("translated_insts", C.c_uint64), ("translate_us", C.c_uint64)]
 
 
 _lib = None
@@ -118,6 +120,10 @@ def lib():
         L.fi_kernel_timer_reset.argtypes = [vp]
         L.fi_debug_stats.argtypes = [vp, vp]
         L.fi_kernel_timer_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
+        L.fi_debug_waves.argtypes = [vp, vp, C.c_uint64]
+        L.fi_debug_translation.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.fi_translate_status.restype = C.c_char_p
+        L.fi_translate_status.argtypes = [vp]
         _lib = L
     return _lib
 
@@ -206,6 +212,22 @@ class Engine:
 
     def sync(self):
         self._chk(self.L.fi_sync(self.h), "fi_sync")
+
+    def translate_status(self) -> str:
+        """"" when the translated path is on, else why not."""
+        return self.L.fi_translate_status(self.h).decode()
+
+    def debug_waves(self, n_waves: int) -> np.ndarray:
+        out = np.zeros((n_waves, 4), np.uint64)
+        self._chk(self.L.fi_debug_waves(self.h, out.ctypes.data, n_waves), "fi_debug_waves")
+        return out
+
+    def debug_translation(self) -> str:
+        n = C.c_uint64()
+        self.L.fi_debug_translation(self.h, None, 0, C.byref(n))
+        buf = C.create_string_buffer(n.value + 1)
+        self.L.fi_debug_translation(self.h, buf, n.value + 1, C.byref(n))
+        return buf.value.decode()
 
     def last_kernel_ms(self) -> float:
         return self.L.fi_last_kernel_ms(self.h)

@@ -1,0 +1,36 @@
+"""Offline hipRTC build + disassembly of a translated-block body (no GPU).
+
+python tools/jit_inspect.py gpurun_out/tx_crc32.inc [out.s]
+Prints the kernel's resource use (VGPRs, SGPRs, spills, scratch)."""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from shrewd_amd.fi import lib  # noqa: E402
+
+L = lib()
+L.fi_debug_jit_compile.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64),
+                                   C.c_char_p, C.c_uint64]
+body = open(sys.argv[1]).read().encode() if len(sys.argv) > 1 else b""
+n = C.c_uint64()
+err = C.create_string_buffer(8192)
+st = L.fi_debug_jit_compile(body, b"gfx950", None, 0, C.byref(n), err, 8192)
+if st:
+    sys.exit("compile failed:\n" + err.value.decode())
+buf = C.create_string_buffer(n.value)
+L.fi_debug_jit_compile(body, b"gfx950", buf, n.value, C.byref(n), err, 8192)
+co = "/tmp/fi_jit_inspect.co"
+open(co, "wb").write(buf.raw[:n.value])
+notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co], capture_output=True, text=True).stdout
+for key in (".vgpr_count", ".sgpr_count", ".vgpr_spill_count", ".sgpr_spill_count", ".private_segment_fixed_size"):
+    for line in notes.splitlines():
+        if key + ":" in line:
+            print(line.strip())
+            break
+if len(sys.argv) > 2:
+    dis = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "-d", co], capture_output=True, text=True).stdout
+    open(sys.argv[2], "w").write(dis)
+    print("disassembly ->", sys.argv[2])
