@@ -20,6 +20,16 @@ fi_status fi_debug_stats(fi_engine *e, uint64_t *out32);
 /* Per wave of the last launch: {s_memtime cycles, loop iterations,
  * translated instructions, slow fetches} (4 x u64 each). */
 fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves);
+/* Lanes suspended at the end of each epoch of the last chunk (16 x u32). */
+fi_status fi_debug_epochs(fi_engine *e, uint32_t *out16);
+/* The translator's inputs of the last fi_golden_run: the pre-decoded text
+ * (16-byte records, see fi_debug_decode) and the golden trace (halfword index
+ * per committed instruction or ecall, bit 31 = ecall). */
+fi_status fi_debug_golden_trace(fi_engine *e, void *pre_out, uint64_t pre_cap, uint64_t *n_pre, uint32_t *trace_out,
+                                uint64_t trace_cap, uint64_t *n_trace, uint64_t *text_lo);
+/* Run the translator on given inputs (no device): the generated C++. */
+fi_status fi_debug_translate(const void *pre, uint64_t n_pre, uint64_t text_lo, const uint32_t *trace,
+                             uint64_t n_trace, char *out, uint64_t cap, uint64_t *len);
 /* The C++ generated for the golden blocks by the last fi_golden_run
  * (fi_translate.cpp); *len = its length, buf gets up to cap-1 bytes + NUL. */
 fi_status fi_debug_translation(fi_engine *e, char *buf, uint64_t cap, uint64_t *len);

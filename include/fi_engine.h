@@ -105,6 +105,7 @@ typedef struct {
     uint32_t max_trials_per_launch; /* 0 -> 65536 */
     uint32_t snapshot_interval;     /* golden snapshot every N committed insts (0 -> auto, >= 256) */
     uint32_t flags;                 /* FI_CFG_* */
+    uint32_t epoch_iters;           /* first epoch's loop iterations per wave (0 -> 4096; then x4, x16, unbounded) */
 } fi_config;
 /* fi_config.flags: trials start from process start / run to their natural end
  * (the plain serial semantics, for A/B checks; outcomes are identical) */
@@ -112,6 +113,8 @@ typedef struct {
 #define FI_CFG_NO_EARLY_EXIT 2u
 /* interpreter only: no load-time translation of the golden blocks (hipRTC) */
 #define FI_CFG_NO_TRANSLATE 4u
+/* one launch per chunk, every wave to completion (no suspend / compact / resume) */
+#define FI_CFG_NO_EPOCHS 8u
 
 typedef struct {
     uint64_t ninst, ncycles;

@@ -31,6 +31,8 @@ hipError_t launch_trials(const DevCtx &c, hipStream_t st);
 hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, fi_histogram *h,
                        const unsigned long long *stats, hipStream_t st);
 hipError_t sort_pairs_bytes(uint64_t n, size_t &bytes);
+hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
+                            uint64_t *keys, uint32_t *vals, hipStream_t st);
 std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
                              const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
                              uint32_t &n_insts);
@@ -78,6 +80,8 @@ struct fi_engine {
     hipFunction_t tx_fn = nullptr;
     std::string tx_status = "no golden run";
     std::string tx_body;   // last generated translation (diagnostics)
+    std::vector<PreInst> tx_pre;     // its inputs: the pre-decoded text and the golden trace
+    std::vector<uint32_t> tx_trace;
 
     // golden
     bool have_golden = false;
@@ -104,6 +108,12 @@ struct fi_engine {
     uint64_t *d_wave_dbg = nullptr;
     uint8_t *d_priv = nullptr;
     uint64_t *d_priv_vpn = nullptr;
+    // epochs: suspended lanes, survivor lists, counts, sort buffers
+    LaneSave *d_save = nullptr;
+    uint32_t *d_surv[2] = {nullptr, nullptr};
+    uint32_t *d_cnt = nullptr;
+    uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;
+    uint32_t *d_svals = nullptr, *d_svals2 = nullptr;
 };
 
 static fi_status fail(fi_engine *e, fi_status code, const char *fmt, ...) {
@@ -163,7 +173,9 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
 
 static void free_work(fi_engine *e) {
     dfree(e->d_sites); dfree(e->d_keys); dfree(e->d_keys2); dfree(e->d_perm); dfree(e->d_perm2);
-    dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg); dfree(e->d_priv); dfree(e->d_priv_vpn);
+    dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg);
+    dfree(e->d_save); dfree(e->d_surv[0]); dfree(e->d_surv[1]); dfree(e->d_cnt);
+    dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_priv); dfree(e->d_priv_vpn);
     e->cap = 0;
 }
 static void free_snaps(fi_engine *e) { dfree(e->d_snaps); dfree(e->d_tab); dfree(e->d_pool); }
@@ -418,6 +430,14 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_wave_dbg, ((c + 63) / 64) * 4 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&e->d_priv, c * e->cfg.private_pages * kPage));
     HIPCHK(hipMalloc(&e->d_priv_vpn, c * e->cfg.private_pages * 8));
+    HIPCHK(hipMalloc(&e->d_save, c * sizeof(LaneSave)));
+    HIPCHK(hipMalloc(&e->d_surv[0], c * 4));
+    HIPCHK(hipMalloc(&e->d_surv[1], c * 4));
+    HIPCHK(hipMalloc(&e->d_cnt, 16 * 4));
+    HIPCHK(hipMalloc(&e->d_skeys, c * 8));
+    HIPCHK(hipMalloc(&e->d_skeys2, c * 8));
+    HIPCHK(hipMalloc(&e->d_svals, c * 4));
+    HIPCHK(hipMalloc(&e->d_svals2, c * 4));
     e->cap = c;
     return FI_OK;
 }
@@ -467,6 +487,7 @@ static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_
     c.rec_trace = d_trace; c.rec_trace_cap = d_trace ? trace_cap : 0;
     c.out = e->d_out;
     c.n = 1;
+    c.n_slots = 1;
     c.sites = nullptr; c.perm = nullptr;
     hipError_t err = hipMemsetAsync(e->d_stats, 0, 32 * sizeof(unsigned long long), e->stream);
     if (err == hipSuccess) err = hipEventRecord(e->ev0, e->stream);
@@ -679,6 +700,8 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         uint32_t n_tx = 0;
         const std::string body = translate_blocks(pre, e->text_lo, trace, pcs, leaders, n_tx);
         e->tx_body = body;
+        e->tx_pre = pre;
+        e->tx_trace = trace;
         hipDeviceProp_t prop;
         HIPCHK(hipGetDeviceProperties(&prop, e->dev));
         std::vector<char> code;
@@ -781,7 +804,21 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     c.perm = e->d_perm2;
     c.out = d_out;
     c.n = k;
+    c.n_slots = (uint32_t)k;
+    c.save = e->d_save;
     HIPCHK(hipMemsetAsync(e->d_stats, 0, 32 * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(e->d_cnt, 0, 16 * 4, st));
+    // epochs: each wave runs a bounded number of loop
+    // iterations, then its live lanes are suspended, sorted by pc and resumed
+    // densely packed; the last epoch runs to completion.  All asynchronous:
+    // resume grids are sized for every slot and surplus waves exit at once.
+    std::vector<uint32_t> budgets;
+    if (e->cfg.flags & FI_CFG_NO_EPOCHS) {
+        budgets = {0};
+    } else {
+        const uint32_t b = e->cfg.epoch_iters ? e->cfg.epoch_iters : 4096;
+        budgets = {b, 4 * b, 16 * b, 0};
+    }
     if (e->tused == e->tpool.size()) {
         hipEvent_t a, b;
         HIPCHK(hipEventCreate(&a));
@@ -791,7 +828,21 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     auto &tp = e->tpool[e->tused++];
     HIPCHK(hipEventRecord(e->ev0, st));
     HIPCHK(hipEventRecord(tp.first, st));
-    HIPCHK(launch_trial_kernel(e, c, st));
+    for (size_t ep = 0; ep < budgets.size(); ep++) {
+        c.wave_budget = budgets[ep];
+        c.surv = e->d_surv[ep & 1];
+        c.surv_n = e->d_cnt + ep;
+        if (ep == 0) {
+            c.resume = nullptr;
+            c.resume_n = nullptr;
+        } else {
+            HIPCHK(launch_surv_keys(e->d_save, e->d_surv[(ep - 1) & 1], e->d_cnt + ep - 1, k, e->d_skeys, e->d_svals, st));
+            HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_skeys, e->d_skeys2, e->d_svals, e->d_svals2, k, 64, st));
+            c.resume = e->d_svals2;
+            c.resume_n = e->d_cnt + ep - 1;
+        }
+        HIPCHK(launch_trial_kernel(e, c, st));
+    }
     HIPCHK(hipEventRecord(tp.second, st));
     HIPCHK(hipEventRecord(e->ev1, st));
     HIPCHK(launch_hist(e->d_sites, d_out, k, d_hist, e->d_stats, st));
@@ -911,6 +962,41 @@ fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves) {
     if (n_waves > (e->cap + 63) / 64) return fail(e, FI_E_ARG, "more waves than the work buffers hold");
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipMemcpy(out, e->d_wave_dbg, n_waves * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return FI_OK;
+}
+
+fi_status fi_debug_epochs(fi_engine *e, uint32_t *out16) {
+    if (!e || !out16 || !e->d_cnt) return FI_E_ARG;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(out16, e->d_cnt, 16 * 4, hipMemcpyDeviceToHost));
+    return FI_OK;
+}
+
+fi_status fi_debug_golden_trace(fi_engine *e, void *pre_out, uint64_t pre_cap, uint64_t *n_pre, uint32_t *trace_out,
+                                uint64_t trace_cap, uint64_t *n_trace, uint64_t *text_lo) {
+    if (!e) return FI_E_ARG;
+    if (pre_out) memcpy(pre_out, e->tx_pre.data(), std::min<uint64_t>(pre_cap, e->tx_pre.size()) * sizeof(PreInst));
+    if (trace_out) memcpy(trace_out, e->tx_trace.data(), std::min<uint64_t>(trace_cap, e->tx_trace.size()) * 4);
+    if (n_pre) *n_pre = e->tx_pre.size();
+    if (n_trace) *n_trace = e->tx_trace.size();
+    if (text_lo) *text_lo = e->text_lo;
+    return FI_OK;
+}
+
+fi_status fi_debug_translate(const void *pre, uint64_t n_pre, uint64_t text_lo, const uint32_t *trace,
+                             uint64_t n_trace, char *out, uint64_t cap, uint64_t *len) {
+    if (!pre || !trace) return FI_E_ARG;
+    std::vector<PreInst> p((const PreInst *)pre, (const PreInst *)pre + n_pre);
+    std::vector<uint32_t> t(trace, trace + n_trace);
+    std::vector<uint32_t> leaders;
+    uint32_t n_tx = 0;
+    const std::string body = translate_blocks(p, text_lo, t, {}, leaders, n_tx);
+    if (out && cap) {
+        const uint64_t n = std::min<uint64_t>(cap - 1, body.size());
+        memcpy(out, body.data(), n);
+        out[n] = 0;
+    }
+    if (len) *len = body.size();
     return FI_OK;
 }
 

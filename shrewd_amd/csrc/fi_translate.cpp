@@ -47,14 +47,21 @@ struct Gen {
     }
     static std::string R(uint32_t r) { return r ? "X" + std::to_string(r) : std::string("0ULL"); }
     uint64_t pc_of(uint32_t h) const { return text_lo + 2ULL * h; }
-    // jump to the block at pc, or leave at pc if it is not translated
-    std::string go(uint64_t pc) const {
+    // Jump from the block at `from` to the block at pc, or leave at pc if it
+    // is not translated.  Only forward edges and self-loops are direct: every
+    // cycle then passes through tx_dispatch, the single header, and the CFG
+    // stays reducible (with direct backward edges every block of a loop would
+    // be one of its entries, and the compiler's irreducible-control-flow fix
+    // routes every transition through a linear guard chain).
+    std::string go(uint64_t pc, uint32_t from) const {
         char buf[96];
         const uint64_t off = pc - text_lo;
-        if (pc >= text_lo && !(off & 1) && off / 2 < pre.size() && leaders.count((uint32_t)(off / 2)))
-            snprintf(buf, sizeof buf, "goto B_%u;", (uint32_t)(off / 2));
-        else
+        if (pc >= text_lo && !(off & 1) && off / 2 < pre.size() && leaders.count((uint32_t)(off / 2))) {
+            if ((uint32_t)(off / 2) >= from) snprintf(buf, sizeof buf, "goto B_%u;", (uint32_t)(off / 2));
+            else snprintf(buf, sizeof buf, "{ spc = 0x%llxULL; goto tx_dispatch; }", (unsigned long long)pc);
+        } else {
             snprintf(buf, sizeof buf, "{ spc = 0x%llxULL; goto tx_out; }", (unsigned long long)pc);
+        }
         return buf;
     }
 };
@@ -219,6 +226,10 @@ std::string subst(const std::string &t, const std::string &a, const std::string 
     return r;
 }
 
+const char *gtype(uint32_t size) {
+    return size == 1 ? "u8" : size == 2 ? "u16" : size == 4 ? "u32" : "u64";
+}
+
 const char *ltype(uint32_t size) {
     return size == 1 ? "uint8_t" : size == 2 ? "uint16_t" : size == 4 ? "uint32_t" : "uint64_t";
 }
@@ -299,15 +310,19 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         n_insts += n;
         const uint64_t pc0 = g.pc_of(h0);
         g.put("B_%u: { // pc 0x%llx, %u insts\n", h0, (unsigned long long)pc0, n);
-        g.put("  if (budget - steps < %uu || !ult64(0x%llxULL, wait_min)) { spc = 0x%llxULL; goto tx_out; }\n", n,
-              (unsigned long long)pc0, (unsigned long long)pc0);
+        g.put("  if (!ult64(0x%llxULL, wmin)) { spc = 0x%llxULL; goto tx_sched; }\n", (unsigned long long)pc0,
+              (unsigned long long)pc0);
+        g.put("  if (wst + %uu > wbud || TXB(mine && rem - lst < %uu)) { spc = 0x%llxULL; goto tx_out; }\n", n, n,
+              (unsigned long long)pc0);
         uint32_t k_st = 0, k_xt = 0, k_fb = 0, k_db = 0;   // committed so far in this block
         auto commit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
-            std::string s = "steps += " + std::to_string(st) + "u; ";
-            if (xt) s += "xticks += " + std::to_string(xt) + "u; ";
-            s += "fbytes += " + std::to_string(fb) + "u; ";
-            if (db) s += "dbytes += " + std::to_string(db) + "u; ";
-            return s;
+            // per-lane counters of the running lanes (zero terms omitted), wave iterations
+            if (!st) return std::string();
+            std::string r = "{ const uint32_t mm_ = mine ? 0xFFFFFFFFu : 0u; lst += " + std::to_string(st) + "u & mm_; ";
+            if (xt) r += "lxt += " + std::to_string(xt) + "u & mm_; ";
+            if (fb) r += "lfb += " + std::to_string(fb) + "u & mm_; ";
+            if (db) r += "ldb += " + std::to_string(db) + "u & mm_; ";
+            return r + "wst = uni32(wst + " + std::to_string(st) + "u); } ";
         };
         for (uint32_t i = 0; i < n; i++) {
             const PreInst &p = pre[insts[i]];
@@ -327,50 +342,64 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             const std::string leave_here = "{ " + commit(k_st, k_xt, k_fb, k_db) + "spc = " + pcb + "; goto tx_out; }";
             switch (k) {
             case C_ALU:
-                if (p.rd) g.put("  X%u = %s;\n", p.rd, subst(e, A, B, immb, pcb).c_str());
+                if (p.rd) g.put("  TXSET(%u, %s);\n", p.rd, subst(e, A, B, immb, pcb).c_str());
                 break;
             case C_NOP:
                 break;
             case C_LOAD:
                 g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, false, p_, tx);\n", A.c_str(), immb, sz);
-                g.put("    if (__ballot(mine && !ok_)) %s\n", leave_here.c_str());
+                g.put("    if (TXB(mine && !ok_)) %s\n", leave_here.c_str());
                 if (p.rd) {
                     g.put("    p_ = ok_ ? p_ : const_cast<uint8_t *>(zp);\n");
-                    if (sx) g.put("    X%u = (uint64_t)(int64_t)(int%d_t)*(const %s *)p_; }\n", p.rd, sx, ltype(sz));
-                    else g.put("    X%u = (uint64_t)*(const %s *)p_; }\n", p.rd, ltype(sz));
+                    if (sx) g.put("    TXSET(%u, (int64_t)(int%d_t)*(const g_%s *)p_); }\n", p.rd, sx, gtype(sz));
+                    else g.put("    TXSET(%u, *(const g_%s *)p_); }\n", p.rd, gtype(sz));
                 } else {
                     g.put("  }\n");
                 }
                 break;
             case C_STORE:
                 g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, true, p_, tx);\n", A.c_str(), immb, sz);
-                g.put("    if (__ballot(mine && !ok_)) %s\n", leave_here.c_str());
-                g.put("    p_ = (mine && ok_) ? p_ : sink; *(%s *)p_ = (%s)%s; }\n", ltype(sz), ltype(sz), B.c_str());
+                g.put("    if (TXB(mine && !ok_)) %s\n", leave_here.c_str());
+                g.put("    p_ = (mine && ok_) ? p_ : sink; *(g_%s *)p_ = (%s)%s; }\n", gtype(sz), ltype(sz), B.c_str());
                 break;
             case C_BR: {
                 const std::string c = subst(cond, A, B, immb, pcb);
                 const uint64_t tgt = pc + (int64_t)p.imm;
-                g.put("  { const bool c_ = %s; const uint64_t tk_ = __ballot(mine && c_);\n", c.c_str());
+                g.put("  { const bool c_ = %s; const uint64_t tk_ = uni64(TXB(mine && c_));\n", c.c_str());
                 g.put("    %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
-                g.put("    if (tk_ == gm) %s\n", g.go(tgt).c_str());
-                g.put("    if (tk_ == 0) %s\n", g.go(ft).c_str());
-                g.put("    dpc = c_ ? 0x%llxULL : %s; div = true; goto tx_out; }\n", (unsigned long long)tgt, ftb);
+                g.put("    if (tk_ == gmr) %s\n", g.go(tgt, h0).c_str());
+                g.put("    if (tk_ == 0) %s\n", g.go(ft, h0).c_str());
+                // divergent: the lanes bound for the higher pc park, the others run on
+                if (tgt > ft) {
+                    g.put("    lp = (mine && c_) ? 0x%llxULL : lp; pend = uni64(pend | tk_); mine = mine && !c_;"
+                          " gmr = uni64(gmr & ~tk_);\n", (unsigned long long)tgt);
+                    g.put("    pmin = uni64(ult64(0x%llxULL, pmin) ? 0x%llxULL : pmin);"
+                          " wmin = uni64(ult64(pmin, owm) ? pmin : owm);\n",
+                          (unsigned long long)tgt, (unsigned long long)tgt);
+                    g.put("    %s }\n", g.go(ft, h0).c_str());
+                } else {
+                    g.put("    lp = (mine && !c_) ? %s : lp; pend = uni64(pend | (gmr & ~tk_)); mine = mine && c_;"
+                          " gmr = uni64(tk_);\n", ftb);
+                    g.put("    pmin = uni64(ult64(%s, pmin) ? %s : pmin); wmin = uni64(ult64(pmin, owm) ? pmin : owm);\n",
+                          ftb, ftb);
+                    g.put("    %s }\n", g.go(tgt, h0).c_str());
+                }
                 break;
             }
             case C_JAL: {
                 const uint64_t tgt = pc + (int64_t)p.imm;
-                if (p.rd) g.put("  X%u = %s;\n", p.rd, ftb);
-                g.put("  %s %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), g.go(tgt).c_str());
+                if (p.rd) g.put("  TXSET(%u, %s);\n", p.rd, ftb);
+                g.put("  %s %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), g.go(tgt, h0).c_str());
                 break;
             }
             case C_JALR: {
                 const int64_t im = (p.op == OP_jalr) ? p.imm : 0;
                 const uint32_t rd = (p.op == OP_c_jalr) ? 1 : (p.op == OP_c_jr ? 0 : p.rd);
                 g.put("  { const uint64_t t_ = (%s + (uint64_t)(int64_t)%lldLL) & ~1ULL;\n", A.c_str(), (long long)im);
-                if (rd) g.put("    X%u = %s;\n", rd, ftb);
+                if (rd) g.put("    TXSET(%u, %s);\n", rd, ftb);
                 g.put("    %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
-                g.put("    const uint64_t t0_ = readlane64(t_, glane);\n");
-                g.put("    if (__ballot(mine && t_ != t0_)) { dpc = t_; div = true; goto tx_out; }\n");
+                g.put("    const uint64_t t0_ = readlane64(t_, __ffsll((unsigned long long)gmr) - 1);\n");
+                g.put("    if (TXB(mine && t_ != t0_)) { dpc = t_; jdiv = mine; goto tx_out; }\n");
                 g.put("    spc = uni64(t0_); goto tx_dispatch; }\n");
                 break;
             }
@@ -381,7 +410,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         }
         if (!term) {   // fell into the next leader, or stops before an instruction it does not cover
             const uint64_t nxt = n ? g.pc_of(insts[n - 1]) + pre[insts[n - 1]].len : pc0;
-            g.put("  %s %s\n", commit(k_st, k_xt, k_fb, k_db).c_str(), g.go(nxt).c_str());
+            g.put("  %s %s\n", commit(k_st, k_xt, k_fb, k_db).c_str(), g.go(nxt, h0).c_str());
         }
         g.put("}\n");
     }

@@ -50,6 +50,18 @@ struct PageEnt {
     uint32_t pad;
 };
 
+// A suspended lane (epochs): everything a resumed lane needs
+// besides its site, private pages (still in place under its slot) and the
+// golden data.
+struct LaneSave {
+    uint64_t regs[32];
+    uint64_t pc, ninst, ncyc, out_pos, err_pos, stack_min, next_chk;
+    int32_t watch;
+    uint32_t nfail, n_priv, snap_j;
+    uint32_t flags;                  // bit 0 out_bad, bits 1-2 injected, bit 3 code_dirty
+    uint32_t pad;
+};
+
 // Everything one launch of the trial kernel needs.  Passed by value as the
 // kernel argument (lives in the kernarg segment -> scalar loads).
 struct DevCtx {
@@ -93,6 +105,15 @@ struct DevCtx {
     uint32_t rec_trace_cap;          // entries of rec_trace
     uint32_t *rec_trace;             // halfword index (pc - text_lo) / 2 of every committed instruction and
                                      // ecall of the golden run, for the host's register liveness pass
+    // epochs: a wave suspends its live lanes after wave_budget loop iterations
+    // (0 = run to completion); a resume launch takes its lanes from resume[]
+    uint32_t wave_budget;
+    uint32_t n_slots;                // slots of the chunk (stride of priv_vpn)
+    const uint32_t *resume;          // NULL = fresh launch: lane slot = global lane index
+    const uint32_t *resume_n;        // number of entries in resume[]
+    uint32_t *surv;                  // suspended lanes' slots are appended here
+    uint32_t *surv_n;
+    LaneSave *save;                  // [n_slots]
     // the work
     const fi_site *sites;            // in trial order
     const uint32_t *perm;            // launch slot -> index into sites/out (sorted by site.inst)

@@ -123,6 +123,22 @@ __global__ void fi_hist_kernel(const fi_site *sites, const fi_outcome *out, uint
     atomicAdd((unsigned long long *)&h->guest_insts, (unsigned long long)o.ninst);
 }
 
+// Epochs: sort keys of the suspended lanes (their pc: lanes of one loop end
+// up in the same wave); entries past the survivor count sort last.
+__global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
+                                    uint64_t *keys, uint32_t *vals) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cap) return;
+    if (i < *cnt) {
+        const uint32_t sl = list[i];
+        keys[i] = save[sl].pc;
+        vals[i] = sl;
+    } else {
+        keys[i] = ~0ULL;
+        vals[i] = 0;
+    }
+}
+
 __global__ void fi_hist_stats_kernel(const unsigned long long *stats, fi_histogram *h) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         h->fetch_bytes += stats[0];
@@ -157,6 +173,11 @@ hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, 
                        const unsigned long long *stats, hipStream_t st) {
     hipLaunchKernelGGL(fi_hist_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, sites, out, n, h);
     hipLaunchKernelGGL(fi_hist_stats_kernel, dim3(1), dim3(64), 0, st, stats, h);
+    return hipGetLastError();
+}
+hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
+                            uint64_t *keys, uint32_t *vals, hipStream_t st) {
+    hipLaunchKernelGGL(fi_surv_keys_kernel, dim3(nblk(cap, 256)), dim3(256), 0, st, save, list, cnt, cap, keys, vals);
     return hipGetLastError();
 }
 hipError_t sort_pairs_bytes(uint64_t n, size_t &bytes) {

@@ -107,7 +107,8 @@ struct LaneMem {
     bool code_dirty;
 };
 
-// The start snapshot's page table (wave-uniform).
+// The lane's start-snapshot page table (uniform in a fresh launch; per lane
+// after a resume).
 struct WaveMem {
     const PageEnt *tab;
     uint32_t tab_n;
@@ -153,7 +154,7 @@ __device__ __forceinline__ int64_t tab_find(const PageEnt *t, uint32_t n, uint64
 __device__ uint64_t lookup_full(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t vpn) {
     uint64_t p = 0;
     for (uint32_t i = 0; i < m.n_priv; i++) {
-        if (c->priv_vpn[(uint64_t)i * c->n + slot] == vpn) { p = (uint64_t)priv_frame(c, slot, i) | 1; break; }
+        if (c->priv_vpn[(uint64_t)i * c->n_slots + slot] == vpn) { p = (uint64_t)priv_frame(c, slot, i) | 1; break; }
     }
     if (!p) {
         const int64_t f = tab_find(w.tab, w.tab_n, vpn);
@@ -403,7 +404,7 @@ __device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32
     const uint32_t nk = S->tab_n;
     const uint64_t smin = S->stack_min >> 12;
     for (uint32_t i = 0; i < np; i++) {   // every page the lane has written
-        const uint64_t v = uni64(c->priv_vpn[(uint64_t)i * c->n + lslot]);
+        const uint64_t v = uni64(c->priv_vpn[(uint64_t)i * c->n_slots + lslot]);
         const int64_t f = tab_find(tk, nk, v);
         const uint8_t *g = f >= 0 ? c->pool + ((uint64_t)f << 12)
                                   : ((v >= smin && v <= kStackTopVpn) ? c->zero_page : nullptr);
@@ -414,7 +415,7 @@ __device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32
         const uint64_t v = uni64(tk[e].vpn);
         const uint32_t f = uni32(tk[e].frame);
         bool priv = false;
-        for (uint32_t i = 0; i < np; i++) priv = priv || c->priv_vpn[(uint64_t)i * c->n + lslot] == v;
+        for (uint32_t i = 0; i < np; i++) priv = priv || c->priv_vpn[(uint64_t)i * c->n_slots + lslot] == v;
         if (priv) continue;
         const int64_t fj = tab_find(w.tab, w.tab_n, v);
         const uint8_t *lv = fj >= 0 ? c->pool + ((uint64_t)fj << 12)
@@ -424,6 +425,23 @@ __device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32
     }
     return true;
 }
+
+// Guest memory through the global address space (global_load/store, not flat).
+typedef __attribute__((address_space(1))) uint8_t g_u8;
+typedef __attribute__((address_space(1))) uint16_t g_u16;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) uint64_t g_u64;
+// Translated code: the wave mask of a lane predicate (no int round trip), and
+// a value pinned in a VGPR so that `mine ? v : X` stays a select (a select on
+// a load's result is otherwise turned into a divergent branch around the load,
+// which makes the whole region divergent).
+#define TXB(x) __builtin_amdgcn_ballot_w64(x)
+#define TXSET(r, e)                         \
+    do {                                    \
+        uint64_t t_ = (uint64_t)(e);        \
+        __asm__ volatile("" : "+v"(t_));    \
+        X##r = mine ? t_ : X##r;            \
+    } while (0)
 
 // The pre-decoded text (uniform): table, text range, exact code range.
 struct TextRef { const PreInst *pre; uint32_t lo, hi, bytes; uint64_t clo, chi; };
@@ -436,7 +454,9 @@ __device__ __forceinline__ bool tx_probe(const LaneMem &m, uint64_t ea, uint32_t
                                          const TextRef &t) {
     const uint64_t e = tlb_find(m, ea >> 12);
     p = const_cast<uint8_t *>(page_of(e)) + (ea & 4095);
-    return e && (!st || ((e & 1) && (ea >= t.chi || ea + size <= t.clo))) && (ea & (size - 1)) == 0;
+    // bitwise, not short-circuit: a && here becomes a divergent branch
+    const bool code_ok = (ea >= t.chi) | (ea + size <= t.clo);
+    return (e != 0) & (!st | (((e & 1) != 0) & code_ok)) & ((ea & (size - 1)) == 0);
 }
 
 // ------------------------------------------------------------------ trial kernel
@@ -497,8 +517,12 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     __shared__ uint64_t R[kRows * 64];
     const uint64_t t_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
     const uint32_t lane = threadIdx.x;
-    const uint64_t slot = (uint64_t)blockIdx.x * 64 + lane;
-    const bool live = slot < CX->n;
+    // ---- the lane's slot: a fresh launch takes slot = global lane index, a
+    // resume launch (epochs) the slots of suspended lanes, sorted by pc
+    const uint64_t gidx = (uint64_t)blockIdx.x * 64 + lane;
+    const bool resume = CX->resume != nullptr;
+    const bool live = resume ? gidx < *CX->resume_n : gidx < CX->n;
+    const uint64_t slot = resume ? (live ? CX->resume[gidx] : 0) : gidx;
     fi_site s;
     s.inst = kNone; s.mask = 0; s.addr = 0; s.target = 0; s.trial = 0;
     uint32_t sidx = 0;
@@ -507,17 +531,24 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     // ---- start snapshot: the last one at or before the wave's earliest
     // inject time (lane 0 holds it: slots are sorted by inject time)
     uint32_t j = 0;
-    if (!CX->record && CX->snap_start && CX->n_snap > 1) {
+    if (!resume && !CX->record && CX->snap_start && CX->n_snap > 1) {
         const uint64_t t0 = uni64(CX->sites[CX->perm[(uint64_t)blockIdx.x * 64]].inst);
         const uint64_t k = t0 / CX->snap_interval;
         j = (uint32_t)(k < CX->n_snap ? k : CX->n_snap - 1);
     }
+    const LaneSave *SV = CX->save + slot;
+    if (resume) j = live ? SV->snap_j : 0;
     const SnapState *S0 = CX->snaps + j;
-    WaveMem w;
+    WaveMem w;   // per lane: resumed lanes come from different start snapshots
     w.tab = CX->snap_tab + S0->tab_off;
     w.tab_n = S0->tab_n;
+    if (resume) {
 #pragma unroll
-    for (int r = 0; r < 32; r++) RREG(r) = S0->regs[r];
+        for (int r = 0; r < 32; r++) RREG(r) = live ? SV->regs[r] : 0;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 32; r++) RREG(r) = S0->regs[r];
+    }
     RREG(kSinkRow) = 0;
 
     Lane L;
@@ -532,7 +563,14 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     tlb_flush(m);
     m.tp0 = m.tp1 = m.tp2 = m.tp3 = 0;
     m.tnext = 0; m.n_priv = 0; m.req_vpn = kNone; m.req_src = nullptr; m.code_dirty = false;
-    const uint64_t start_inst = live ? L.ninst : 0;
+    if (resume && live) {
+        L.pc = SV->pc; L.ninst = SV->ninst; L.ncyc = SV->ncyc; L.out_pos = SV->out_pos; L.err_pos = SV->err_pos;
+        L.next_chk = SV->next_chk; L.nfail = SV->nfail; L.watch = SV->watch;
+        L.out_bad = SV->flags & 1; L.injected = (uint8_t)((SV->flags >> 1) & 3);
+        m.stack_min = SV->stack_min; m.n_priv = SV->n_priv; m.code_dirty = (SV->flags >> 3) & 1;
+    }
+    bool suspended = false;
+    const uint64_t start_inst = (live && !resume) ? L.ninst : 0;
     uint64_t pages_made = 0;
     uint64_t next_snap = (CX->record && CX->rec_interval) ? 0 : kNone;   // record mode: capture points
     uint32_t snaps_taken = 0;
@@ -545,6 +583,23 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     uint32_t n_tx = 0, n_txin = 0;   // instructions run in translated blocks, entries into them
 
     for (;;) {
+        // ---- epochs: after wave_budget iterations the wave suspends its live
+        // lanes (a pending copy-on-write is dropped: its tick simply retries)
+        if (CX->wave_budget && n_iter >= CX->wave_budget) {
+            if (!L.done) {
+                LaneSave *sv = CX->save + slot;
+#pragma unroll
+                for (int r = 0; r < 32; r++) sv->regs[r] = RREG(r);
+                sv->pc = L.pc; sv->ninst = L.ninst; sv->ncyc = L.ncyc; sv->out_pos = L.out_pos; sv->err_pos = L.err_pos;
+                sv->stack_min = m.stack_min; sv->next_chk = L.next_chk; sv->watch = L.watch; sv->nfail = L.nfail;
+                sv->n_priv = m.n_priv; sv->snap_j = j;
+                sv->flags = (L.out_bad ? 1u : 0u) | ((uint32_t)L.injected << 1) | (m.code_dirty ? 8u : 0u);
+                CX->surv[atomicAdd(CX->surv_n, 1u)] = (uint32_t)slot;
+                suspended = true;
+                L.done = true;
+            }
+            break;
+        }
         // ---- A. materialise requested pages, whole wave cooperating
         const uint64_t want = __ballot(!L.done && m.req_vpn != kNone);
         if (want) {
@@ -565,7 +620,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 if (m.n_priv >= CX->priv_pages) {
                     finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, (uint32_t)L.pc);
                 } else {
-                    CX->priv_vpn[(uint64_t)m.n_priv * CX->n + slot] = m.req_vpn;
+                    CX->priv_vpn[(uint64_t)m.n_priv * CX->n_slots + slot] = m.req_vpn;
                     m.n_priv++;
                     pages_made++;
                 }
@@ -631,7 +686,10 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 while (mm) {
                     const int l = __ffsll((unsigned long long)mm) - 1;
                     mm &= mm - 1;
-                    const bool same = lane_mem_equal(CX, w, readlane64(slot, l),
+                    WaveMem wl;
+                    wl.tab = (const PageEnt *)readlane64((uint64_t)w.tab, l);
+                    wl.tab_n = (uint32_t)__builtin_amdgcn_readlane((int)w.tab_n, l);
+                    const bool same = lane_mem_equal(CX, wl, readlane64(slot, l),
                                                      (uint32_t)__builtin_amdgcn_readlane((int)m.n_priv, l), S, lane);
                     if ((int)lane == l) eq = same;
                 }
@@ -664,7 +722,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                     S->live = 0; S->trace_pos = tpos;
                 }
                 for (uint32_t i = 0; i < np; i++) {
-                    if (lane == 0) CX->rec_vpns[(uint64_t)snaps_taken * CX->priv_pages + i] = CX->priv_vpn[i * CX->n];
+                    if (lane == 0) CX->rec_vpns[(uint64_t)snaps_taken * CX->priv_pages + i] = CX->priv_vpn[i * CX->n_slots];
                     const uint4 *src = (const uint4 *)priv_frame(CX, 0, i);
                     uint4 *dst = (uint4 *)(CX->rec_pages + (((uint64_t)snaps_taken * CX->priv_pages + i) << 12));
 #pragma unroll
@@ -702,12 +760,17 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         // ---- TRANSLATED PATH (load-time build only): the golden run's basic
         // blocks compiled to straight-line code with the guest registers in
         // VGPRs.  Entered at a block leader by a converged group
-        // with nothing watched or modified; leaves at anything the blocks do
-        // not cover (events, divergence, faults, copy-on-write, syscalls,
-        // TLB misses, untranslated pcs), with every counter exact.  The code
-        // runs in uniform control flow with every lane active: lanes outside
-        // the group compute on their own copies, read the zero page, store to
-        // a sink, and write nothing back.
+        // with nothing watched or modified.  Divergence is handled inside, by
+        // the same min-PC rule as the interpreter: at a divergent branch the
+        // lanes bound for the higher pc park (lp) and the others run on; a
+        // block entered at or past the lowest parked pc merges or switches
+        // groups (tx_sched).  Everything runs in uniform control flow with
+        // every lane active: register writes are selects on `mine`, lanes
+        // outside the running group read the zero page and store to a sink.
+        // It leaves (tx_out) at anything the blocks do not cover (events,
+        // faults, copy-on-write, syscalls, TLB misses, divergent jalr,
+        // untranslated pcs, lanes outside the entry group), every counter
+        // exact and per lane.
         if (!CX->record) {
             TextRef tx;
             tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
@@ -715,36 +778,71 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             const PreRef E0 = pre_entry(tx, lpc);
             if (!(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader) &&
                 __ballot(mine && (m.code_dirty || L.watch > 0)) == 0) {
-                const uint64_t gm = __ballot(mine);
-                const int glane = __ffsll((unsigned long long)gm) - 1;
-                const uint64_t budget64 = uni64(wave_min64(mine ? next_ev - L.ninst : kNone));
-                const uint32_t budget = budget64 > (1u << 30) ? (1u << 30) : (uint32_t)budget64;
+                const uint64_t gm = __ballot(mine);      // the entry group
+                uint64_t gmr = gm;                        // the running group
+                uint64_t pend = 0, pmin = kNone;          // parked lanes, their lowest pc
+                const uint64_t owm = wait_min;            // lanes outside the entry group
+                uint64_t wmin = owm;                      // min(pmin, owm)
+                const uint64_t rem64 = mine ? next_ev - L.ninst : 0;
+                const uint32_t rem = rem64 > (1u << 30) ? (1u << 30) : (uint32_t)rem64;
+                // n_iter is uniform in value but not provably so (divergent updates
+                // elsewhere in the loop); a divergent bound here would make every
+                // branch of the translated code divergent
+                const uint32_t wbud = uni32(CX->wave_budget ? CX->wave_budget - n_iter : (1u << 30));
                 const uint8_t *const zp = CX->zero_page;
                 uint8_t *const sink = CX->tx_sink + 8 * lane;
-                uint32_t steps = 0, xticks = 0, fbytes = 0, dbytes = 0;
-                uint64_t spc = lpc, dpc = 0;
-                bool div = false;
+                uint32_t lst = 0, lxt = 0, lfb = 0, ldb = 0;   // per lane: insts, straddles, fetch/data bytes
+                uint32_t wst = 0;                              // wave iterations
+                uint64_t spc = lpc, lp = 0, dpc = 0;
+                bool jdiv = false;
 #define TXR(r) uint64_t X##r = RREG(r);
                 TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
                 TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
                 TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
 #undef TXR
+#define TXC(st, xt, fb, db)                                                               \
+    do {                                                                                  \
+        const uint32_t mm_ = mine ? 0xFFFFFFFFu : 0u;                                     \
+        lst += (st) & mm_; lxt += (xt) & mm_; lfb += (fb) & mm_; ldb += (db) & mm_;       \
+        wst += (st);                                                                      \
+    } while (0)
                 goto tx_dispatch;
                 /*@TX_BODY@*/
+#undef TXC
+            tx_sched:   // spc >= wmin: merge with the parked group, switch to it, or leave
+                if (!ult64(pmin, owm)) goto tx_out;   // lanes outside run first (or no parked lanes)
+                if (spc == pmin) {
+                    const bool jn = ((pend >> lane) & 1) && lp == spc;
+                    const uint64_t b = TXB(jn);
+                    mine = mine || jn;
+                    gmr = uni64(gmr | b);
+                    pend = uni64(pend & ~b);
+                } else {
+                    lp = mine ? spc : lp;
+                    pend = uni64(pend | gmr);
+                    const bool jn = ((pend >> lane) & 1) && lp == pmin;
+                    mine = jn;
+                    gmr = uni64(TXB(jn));
+                    pend = uni64(pend & ~gmr);
+                    spc = pmin;
+                }
+                pmin = uni64(pend ? wave_min64(((pend >> lane) & 1) ? lp : kNone) : kNone);
+                wmin = uni64(ult64(pmin, owm) ? pmin : owm);
+                goto tx_dispatch;
             tx_out:
-                if (mine) {
+                if ((gm >> lane) & 1) {
 #define TXW(r) RREG(r) = X##r;
                     TXW(1) TXW(2) TXW(3) TXW(4) TXW(5) TXW(6) TXW(7) TXW(8) TXW(9) TXW(10) TXW(11) TXW(12) TXW(13)
                     TXW(14) TXW(15) TXW(16) TXW(17) TXW(18) TXW(19) TXW(20) TXW(21) TXW(22) TXW(23) TXW(24) TXW(25)
                     TXW(26) TXW(27) TXW(28) TXW(29) TXW(30) TXW(31)
 #undef TXW
-                    L.ninst += steps; L.ncyc += steps + xticks; L.fetch_b += fbytes; L.data_b += dbytes;
-                    L.pc = div ? dpc : spc;
+                    L.ninst += lst; L.ncyc += lst + lxt; L.fetch_b += lfb; L.data_b += ldb;
+                    L.pc = ((pend >> lane) & 1) ? lp : (jdiv ? dpc : spc);
                 }
-                n_iter += steps;
-                n_tx += steps;
+                n_iter += wst;
+                n_tx += wst;
                 n_txin++;
-                if (steps) continue;
+                if (wst) continue;
             }
         }
 #endif
@@ -760,6 +858,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             const uint64_t gm = __ballot(mine);
             const int glane = __ffsll((unsigned long long)gm) - 1;
             uint64_t budget64 = uni64(wave_min64(mine ? next_ev - L.ninst : kNone));
+            if (CX->wave_budget && budget64 > CX->wave_budget - n_iter) budget64 = CX->wave_budget - n_iter;
             const uint32_t budget = budget64 > (1u << 30) ? (1u << 30) : (uint32_t)budget64;
             uint64_t spc = lpc;
             uint32_t steps = 0, xticks = 0, fbytes = 0, dbytes = 0;
@@ -1180,6 +1279,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         if (cm != gmask) break;
         const uint64_t npc0 = uni64(readlane64(L.pc, __ffsll((unsigned long long)cm) - 1));
         if (__ballot(cont && L.pc == npc0) != cm || npc0 >= wait_min) break;
+        if (CX->wave_budget && n_iter + 1 >= CX->wave_budget) break;
         if (CX->pre_ok) {   // back to the fast path (or translated blocks) when they can take the next one
             TextRef tn;
             tn.pre = CX->pre; tn.lo = (uint32_t)CX->text_lo; tn.hi = (uint32_t)(CX->text_lo >> 32);
@@ -1196,7 +1296,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         }   // inner loop
     }
 
-    if (live) CX->out[CX->record ? 0 : sidx] = L.res;
+    if (live && !suspended) CX->out[CX->record ? 0 : sidx] = L.res;
     if (CX->record && live) {
         CX->stats[3] = L.ncyc;
         CX->stats[4] = L.out_pos;

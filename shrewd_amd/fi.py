@@ -65,12 +65,14 @@ class EngineError(RuntimeError):
 
 class _Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("private_pages", C.c_uint32), ("hang_factor_x16", C.c_uint32),
-                ("max_trials_per_launch", C.c_uint32), ("snapshot_interval", C.c_uint32), ("flags", C.c_uint32)]
+                ("max_trials_per_launch", C.c_uint32), ("snapshot_interval", C.c_uint32), ("flags", C.c_uint32),
+                ("epoch_iters", C.c_uint32)]
 
 
 CFG_NO_SNAPSHOT_START = 1
 CFG_NO_EARLY_EXIT = 2
 CFG_NO_TRANSLATE = 4
+CFG_NO_EPOCHS = 8
 
 
 class GoldenInfo(C.Structure):
@@ -121,6 +123,11 @@ def lib():
         L.fi_debug_stats.argtypes = [vp, vp]
         L.fi_kernel_timer_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
         L.fi_debug_waves.argtypes = [vp, vp, C.c_uint64]
+        L.fi_debug_epochs.argtypes = [vp, vp]
+        L.fi_debug_golden_trace.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), vp, C.c_uint64,
+                                            C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.fi_debug_translate.argtypes = [vp, C.c_uint64, C.c_uint64, vp, C.c_uint64, C.c_char_p, C.c_uint64,
+                                         C.POINTER(C.c_uint64)]
         L.fi_debug_translation.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.fi_translate_status.restype = C.c_char_p
         L.fi_translate_status.argtypes = [vp]
@@ -141,9 +148,11 @@ class Engine:
     """Thin RAII wrapper of one fi_engine (one HIP device)."""
 
     def __init__(self, device: int = 0, private_pages: int = 16, hang_factor_x16: int = 32,
-                 max_trials_per_launch: int = 65536, snapshot_interval: int = 0, flags: int = 0):
+                 max_trials_per_launch: int = 65536, snapshot_interval: int = 0, flags: int = 0,
+                 epoch_iters: int = 0):
         self.L = lib()
-        cfg = _Config(device, private_pages, hang_factor_x16, max_trials_per_launch, snapshot_interval, flags)
+        cfg = _Config(device, private_pages, hang_factor_x16, max_trials_per_launch, snapshot_interval, flags,
+                      epoch_iters)
         h = C.c_void_p()
         st = self.L.fi_create(C.byref(cfg), C.byref(h))
         if st == FI_E_NODEVICE:
@@ -221,6 +230,21 @@ class Engine:
         out = np.zeros((n_waves, 4), np.uint64)
         self._chk(self.L.fi_debug_waves(self.h, out.ctypes.data, n_waves), "fi_debug_waves")
         return out
+
+    def debug_epochs(self) -> list:
+        out = np.zeros(16, np.uint32)
+        self._chk(self.L.fi_debug_epochs(self.h, out.ctypes.data), "fi_debug_epochs")
+        return out.tolist()
+
+    def debug_golden_trace(self):
+        """(pre-decoded text as uint8[n,16], golden trace uint32[m], text_lo)"""
+        npre, ntr, lo = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self.L.fi_debug_golden_trace(self.h, None, 0, C.byref(npre), None, 0, C.byref(ntr), C.byref(lo))
+        pre = np.zeros((npre.value, 16), np.uint8)
+        tr = np.zeros(ntr.value, np.uint32)
+        self.L.fi_debug_golden_trace(self.h, pre.ctypes.data, npre.value, C.byref(npre), tr.ctypes.data, ntr.value,
+                                     C.byref(ntr), C.byref(lo))
+        return pre, tr, lo.value
 
     def debug_translation(self) -> str:
         n = C.c_uint64()

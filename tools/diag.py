@@ -18,10 +18,11 @@ ap.add_argument("workload", nargs="?", default="crc32")
 ap.add_argument("--trials", type=int, nargs="*", default=[64, 6400, 100000])
 ap.add_argument("--flags", type=int, default=0)
 ap.add_argument("--interval", type=int, default=0)
+ap.add_argument("--epoch", type=int, default=0)
 ap.add_argument("--converged", action="store_true", help="also time one converged wave from process start")
 a = ap.parse_args()
 name = a.workload
-e = Engine(max_trials_per_launch=200000, flags=a.flags, snapshot_interval=a.interval)
+e = Engine(max_trials_per_launch=200000, flags=a.flags, snapshot_interval=a.interval, epoch_iters=a.epoch)
 e.load_elf(open(f"workloads/{name}.elf", "rb").read(), [name])
 g = e.golden_run()
 gms = e.last_kernel_ms()
@@ -37,6 +38,8 @@ print(json.dumps({"golden_ninst": g.ninst, "golden_ms": gms, "golden_ns_per_inst
 os.makedirs("gpurun_out", exist_ok=True)
 with open(f"gpurun_out/tx_{name}.inc", "w") as f:
     f.write(e.debug_translation())
+_pre, _tr, _lo = e.debug_golden_trace()
+np.savez(f"gpurun_out/golden_{name}.npz", pre=_pre, trace=_tr, text_lo=np.uint64(_lo))
 e.set_campaign(0x5EED0002, REGS_PC, 1)
 for n in a.trials:
     sites = e.sample(0, n)
@@ -53,7 +56,7 @@ for n in a.trials:
                           "skipped_prefix": int(st[14]), "cow_pages": int(st[2]),
                           "ns_per_iter_slowest_wave": round(ms * 1e6 / max(1, int(st[10])), 1),
                           "clock_mhz": round(int(st[20]) / max(1, int(st[21])) * 100.0, 1),
-                          "wave0_cycles": int(st[20]),
+                          "wave0_cycles": int(st[20]), "survivors": e.debug_epochs()[:4],
                           "tx_insts": int(st[16]), "tx_entries": int(st[17]),
                           "slowest": {"iters": int(st[18]) >> 32, "tx_permille": (int(st[18]) >> 20) & 0xFFF,
                                       "tx_entries": int(st[18]) & 0xFFFFF, "slow": int(st[19]) & 0xFFFFFFFF},

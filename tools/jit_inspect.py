@@ -1,11 +1,14 @@
-"""Offline hipRTC build + disassembly of a translated-block body (no GPU).
+"""Offline translation + hipRTC build + disassembly (no GPU).
 
-python tools/jit_inspect.py gpurun_out/tx_crc32.inc [out.s]
+python tools/jit_inspect.py gpurun_out/golden_crc32.npz [out.s]   # translate the saved golden inputs
+python tools/jit_inspect.py gpurun_out/tx_crc32.inc [out.s]       # a saved body as is
 Prints the kernel's resource use (VGPRs, SGPRs, spills, scratch)."""
 import ctypes as C
 import os
 import subprocess
 import sys
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -14,11 +17,22 @@ from shrewd_amd.fi import lib  # noqa: E402
 L = lib()
 L.fi_debug_jit_compile.argtypes = [C.c_char_p, C.c_char_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64),
                                    C.c_char_p, C.c_uint64]
-body = open(sys.argv[1]).read().encode() if len(sys.argv) > 1 else b""
+src = sys.argv[1]
+if src.endswith(".npz"):
+    z = np.load(src)
+    pre, tr = np.ascontiguousarray(z["pre"]), np.ascontiguousarray(z["trace"])
+    n = C.c_uint64()
+    L.fi_debug_translate(pre.ctypes.data, len(pre), int(z["text_lo"]), tr.ctypes.data, len(tr), None, 0, C.byref(n))
+    buf = C.create_string_buffer(n.value + 1)
+    L.fi_debug_translate(pre.ctypes.data, len(pre), int(z["text_lo"]), tr.ctypes.data, len(tr), buf, n.value + 1,
+                         C.byref(n))
+    body = buf.value
+    open("/tmp/fi_jit_inspect.inc", "wb").write(body)
+else:
+    body = open(src, "rb").read()
 n = C.c_uint64()
 err = C.create_string_buffer(8192)
-st = L.fi_debug_jit_compile(body, b"gfx950", None, 0, C.byref(n), err, 8192)
-if st:
+if L.fi_debug_jit_compile(body, b"gfx950", None, 0, C.byref(n), err, 8192):
     sys.exit("compile failed:\n" + err.value.decode())
 buf = C.create_string_buffer(n.value)
 L.fi_debug_jit_compile(body, b"gfx950", buf, n.value, C.byref(n), err, 8192)
