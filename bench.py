@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lanes", type=int, default=0, help="trials per 64-lane wave (0: engine default)")
+    ap.add_argument("--epoch-iters", type=int, default=0, help="first epoch's iterations per wave (0: default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -87,7 +89,9 @@ def main():
     from shrewd_amd import HIST_DT, Engine
     with open(os.path.join(ROOT, "workloads", f"{a.workload}.elf"), "rb") as f:
         elf = f.read()
-    eng = Engine(device=local, max_trials_per_launch=max(a.trials, 1024))
+    eng = Engine(device=local, max_trials_per_launch=max(a.trials, 1024), lanes_per_wave=a.lanes,
+                 epoch_iters=a.epoch_iters)
+    lanes = eng.config()["lanes_per_wave"]
     t0 = time.perf_counter()
     eng.load_elf(elf, [a.workload])
     g = eng.golden_run()
@@ -143,8 +147,11 @@ def main():
         # algorithmic bytes = fetched instruction bytes + load/store bytes of all
         # executed guest instructions + 264 B initial state + 16 B outcome per
         # trial + 4096 B per copy-on-write page
-        per_launch_bytes = (int(local_h["fetch_bytes"]) + int(local_h["data_bytes"]) + T * (264 + 16)
-                            + 4096 * int(local_h["cow_pages"]))
+        # a step runs one chunk = one dispatch per epoch; every step does the
+        # same work, so bytes per dispatch = bytes per step x steps / dispatches
+        per_step_bytes = (int(local_h["fetch_bytes"]) + int(local_h["data_bytes"]) + T * (264 + 16)
+                          + 4096 * int(local_h["cow_pages"]))
+        per_launch_bytes = per_step_bytes * a.steps // max(launches, 1)
         avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
         achieved = per_launch_bytes / avg_kernel_s / 1e9
         traffic = None
@@ -152,7 +159,8 @@ def main():
             try:
                 with open(a.traffic_json) as f:
                     tj = json.load(f)
-                if tj.get("workload") == a.workload and tj.get("trials") == T:
+                if (tj.get("workload") == a.workload and tj.get("trials") == T
+                        and tj.get("lanes_per_wave", 64) == lanes):
                     traffic = tj.get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
@@ -173,11 +181,13 @@ def main():
             "config": {"workload": f"{a.workload} (RV64 MiBench-style, {g.ninst} golden insts), "
                                    f"{T} single-bit x1..x31+pc trials per GPU per step",
                        "trials_per_gpu": T, "seed": hex(a.seed), "structures": "x1-x31,pc", "burst": 1,
+                       "lanes_per_wave": lanes,
                        "parallelism": f"trial-sharded x{world}, RCCL histogram all-reduce"},
             "guest_inst_per_s": guest_ips,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "fi_trial_kernel", "avg_kernel_ms": avg_kernel_s * 1e3,
+                         "dispatches_per_step": launches / a.steps,
                          "algorithmic_bytes_per_launch": per_launch_bytes},
             "outcomes": {n: int(cls[i]) for i, n in enumerate(["masked", "sdc", "crash", "hang", "detected",
                                                                  "escape"])},

@@ -106,6 +106,8 @@ typedef struct {
     uint32_t snapshot_interval;     /* golden snapshot every N committed insts (0 -> auto, >= 256) */
     uint32_t flags;                 /* FI_CFG_* */
     uint32_t epoch_iters;           /* first epoch's loop iterations per wave (0 -> 4096; then x4, x16, unbounded) */
+    uint32_t lanes_per_wave;        /* trials per 64-lane wave: 8, 16, 32 or 64 (0 -> default); fewer trials per wave
+                                       = more waves in flight to hide the interpreter's dependent-issue latency */
 } fi_config;
 /* fi_config.flags: trials start from process start / run to their natural end
  * (the plain serial semantics, for A/B checks; outcomes are identical) */
@@ -180,9 +182,12 @@ const char *fi_translate_status(fi_engine *e);
 /* Timing of the last fi_run_* call's interpreter kernel(s), measured with
  * hipEvents on the engine stream (milliseconds). */
 double fi_last_kernel_ms(fi_engine *e);
-/* Accumulating per-launch timer of the interpreter kernel (HIP event pairs
- * recorded on the launch stream around every fi_trial_kernel launch). */
+/* Accumulating per-dispatch timer of the interpreter kernel (HIP event pairs
+ * recorded on the launch stream around every fi_trial_kernel dispatch: a chunk
+ * is one dispatch per epoch); launches = dispatches timed. */
 fi_status fi_kernel_timer_reset(fi_engine *e);
+/* The effective configuration (defaults resolved). */
+fi_status fi_get_config(fi_engine *e, fi_config *out);
 fi_status fi_kernel_timer_read(fi_engine *e, double *total_ms, uint32_t *launches);
 
 #ifdef __cplusplus

@@ -43,6 +43,9 @@ hipError_t sort_pairs(void *tmp, size_t bytes, const uint64_t *kin, uint64_t *ko
 
 using namespace fi;
 
+// trials per wave when fi_config.lanes_per_wave is 0
+static constexpr uint32_t kDefaultLanes = 64;
+
 struct fi_engine {
     fi_config cfg{};
     std::string err;
@@ -155,6 +158,13 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
     if (e->cfg.private_pages == 0) e->cfg.private_pages = 16;
     if (e->cfg.hang_factor_x16 == 0) e->cfg.hang_factor_x16 = 32;
     if (e->cfg.max_trials_per_launch == 0) e->cfg.max_trials_per_launch = 65536;
+    if (e->cfg.lanes_per_wave == 0) e->cfg.lanes_per_wave = kDefaultLanes;
+    if (e->cfg.lanes_per_wave != 8 && e->cfg.lanes_per_wave != 16 && e->cfg.lanes_per_wave != 32 &&
+        e->cfg.lanes_per_wave != 64) {
+        g_create_err = "fi_create: lanes_per_wave must be 8, 16, 32 or 64";
+        delete e;
+        return FI_E_ARG;
+    }
     e->dev = e->cfg.device;
     if (e->dev < 0 || e->dev >= n) {
         g_create_err = "fi_create: device " + std::to_string(e->dev) + " out of range (" + std::to_string(n) + " visible)";
@@ -427,7 +437,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_out, c * sizeof(fi_outcome)));
     HIPCHK(hipMalloc(&e->d_hist, sizeof(fi_histogram)));
     HIPCHK(hipMalloc(&e->d_stats, 32 * sizeof(unsigned long long)));
-    HIPCHK(hipMalloc(&e->d_wave_dbg, ((c + 63) / 64) * 4 * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&e->d_wave_dbg, ((c + 7) / 8) * 4 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&e->d_priv, c * e->cfg.private_pages * kPage));
     HIPCHK(hipMalloc(&e->d_priv_vpn, c * e->cfg.private_pages * 8));
     HIPCHK(hipMalloc(&e->d_save, c * sizeof(LaneSave)));
@@ -464,6 +474,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.tx_sink = e->d_sink;
     c.wave_dbg = e->d_wave_dbg;
     c.stats = e->d_stats;
+    c.lanes = e->cfg.lanes_per_wave;
     return c;
 }
 
@@ -792,7 +803,8 @@ fi_status fi_sample_sites(fi_engine *e, uint64_t first, uint64_t n, fi_site *out
 static hipError_t launch_trial_kernel(fi_engine *e, DevCtx &c, hipStream_t st) {
     if (!e->tx_fn) return launch_trials(c, st);
     void *args[] = {&c};
-    return hipModuleLaunchKernel(e->tx_fn, (unsigned)((c.n + 63) / 64), 1, 1, 64, 1, 1, 0, st, args, nullptr);
+    return hipModuleLaunchKernel(e->tx_fn, (unsigned)((c.n + c.lanes - 1) / c.lanes), 1, 1, 64, 1, 1, 0, st, args,
+                                 nullptr);
 }
 
 // One launch: d_sites[0..k) holds the sites in trial order, keys/perm set.
@@ -819,15 +831,7 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
         const uint32_t b = e->cfg.epoch_iters ? e->cfg.epoch_iters : 4096;
         budgets = {b, 4 * b, 16 * b, 0};
     }
-    if (e->tused == e->tpool.size()) {
-        hipEvent_t a, b;
-        HIPCHK(hipEventCreate(&a));
-        HIPCHK(hipEventCreate(&b));
-        e->tpool.emplace_back(a, b);
-    }
-    auto &tp = e->tpool[e->tused++];
     HIPCHK(hipEventRecord(e->ev0, st));
-    HIPCHK(hipEventRecord(tp.first, st));
     for (size_t ep = 0; ep < budgets.size(); ep++) {
         c.wave_budget = budgets[ep];
         c.surv = e->d_surv[ep & 1];
@@ -841,9 +845,19 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
             c.resume = e->d_svals2;
             c.resume_n = e->d_cnt + ep - 1;
         }
+        // every dispatch of the trial kernel is bracketed by its own event
+        // pair on the launch stream (the bench's per-dispatch kernel time)
+        if (e->tused == e->tpool.size()) {
+            hipEvent_t a, b;
+            HIPCHK(hipEventCreate(&a));
+            HIPCHK(hipEventCreate(&b));
+            e->tpool.emplace_back(a, b);
+        }
+        auto &tp = e->tpool[e->tused++];
+        HIPCHK(hipEventRecord(tp.first, st));
         HIPCHK(launch_trial_kernel(e, c, st));
+        HIPCHK(hipEventRecord(tp.second, st));
     }
-    HIPCHK(hipEventRecord(tp.second, st));
     HIPCHK(hipEventRecord(e->ev1, st));
     HIPCHK(launch_hist(e->d_sites, d_out, k, d_hist, e->d_stats, st));
     return FI_OK;
@@ -959,7 +973,7 @@ fi_status fi_debug_jit_compile(const char *body, const char *arch, void *code, u
 
 fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves) {
     if (!e || !out) return FI_E_ARG;
-    if (n_waves > (e->cap + 63) / 64) return fail(e, FI_E_ARG, "more waves than the work buffers hold");
+    if (n_waves > (e->cap + 7) / 8) return fail(e, FI_E_ARG, "more waves than the work buffers hold");
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipMemcpy(out, e->d_wave_dbg, n_waves * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return FI_OK;
@@ -1015,6 +1029,12 @@ fi_status fi_debug_stats(fi_engine *e, uint64_t *out16) {
     if (!e || !out16) return FI_E_ARG;
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipMemcpy(out16, e->d_stats, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return FI_OK;
+}
+
+fi_status fi_get_config(fi_engine *e, fi_config *out) {
+    if (!e || !out) return FI_E_ARG;
+    *out = e->cfg;
     return FI_OK;
 }
 

@@ -109,6 +109,8 @@ struct DevCtx {
     // (0 = run to completion); a resume launch takes its lanes from resume[]
     uint32_t wave_budget;
     uint32_t n_slots;                // slots of the chunk (stride of priv_vpn)
+    uint32_t lanes;                  // trials per wave (lanes >= this are idle): 8, 16, 32 or 64
+    uint32_t pad_lanes;
     const uint32_t *resume;          // NULL = fresh launch: lane slot = global lane index
     const uint32_t *resume_n;        // number of entries in resume[]
     uint32_t *surv;                  // suspended lanes' slots are appended here

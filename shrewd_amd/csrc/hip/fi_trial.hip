@@ -519,10 +519,11 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     const uint32_t lane = threadIdx.x;
     // ---- the lane's slot: a fresh launch takes slot = global lane index, a
     // resume launch (epochs) the slots of suspended lanes, sorted by pc
-    const uint64_t gidx = (uint64_t)blockIdx.x * 64 + lane;
+    const uint32_t nlw = CX->lanes;
+    const uint64_t gidx = (uint64_t)blockIdx.x * nlw + lane;
     const bool resume = CX->resume != nullptr;
-    const bool live = resume ? gidx < *CX->resume_n : gidx < CX->n;
-    const uint64_t slot = resume ? (live ? CX->resume[gidx] : 0) : gidx;
+    const bool live = lane < nlw && (resume ? gidx < *CX->resume_n : gidx < CX->n);
+    const uint64_t slot = live ? (resume ? CX->resume[gidx] : gidx) : (uint64_t)CX->n_slots + lane;
     fi_site s;
     s.inst = kNone; s.mask = 0; s.addr = 0; s.target = 0; s.trial = 0;
     uint32_t sidx = 0;
@@ -532,7 +533,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     // inject time (lane 0 holds it: slots are sorted by inject time)
     uint32_t j = 0;
     if (!resume && !CX->record && CX->snap_start && CX->n_snap > 1) {
-        const uint64_t t0 = uni64(CX->sites[CX->perm[(uint64_t)blockIdx.x * 64]].inst);
+        const uint64_t t0 = uni64(CX->sites[CX->perm[(uint64_t)blockIdx.x * nlw]].inst);
         const uint64_t k = t0 / CX->snap_interval;
         j = (uint32_t)(k < CX->n_snap ? k : CX->n_snap - 1);
     }
@@ -1345,7 +1346,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
 
 #ifndef __HIPCC_RTC__
 hipError_t launch_trials(const DevCtx &c, hipStream_t st) {
-    hipLaunchKernelGGL(fi_trial_kernel, dim3((unsigned)((c.n + 63) / 64)), dim3(64), 0, st, c);
+    hipLaunchKernelGGL(fi_trial_kernel, dim3((unsigned)((c.n + c.lanes - 1) / c.lanes)), dim3(64), 0, st, c);
     return hipGetLastError();
 }
 #endif

@@ -66,7 +66,7 @@ class EngineError(RuntimeError):
 class _Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("private_pages", C.c_uint32), ("hang_factor_x16", C.c_uint32),
                 ("max_trials_per_launch", C.c_uint32), ("snapshot_interval", C.c_uint32), ("flags", C.c_uint32),
-                ("epoch_iters", C.c_uint32)]
+                ("epoch_iters", C.c_uint32), ("lanes_per_wave", C.c_uint32)]
 
 
 CFG_NO_SNAPSHOT_START = 1
@@ -120,6 +120,7 @@ def lib():
         L.fi_last_kernel_ms.argtypes = [vp]
         L.fi_debug_decode.argtypes = [vp, vp, C.c_uint64, vp]
         L.fi_kernel_timer_reset.argtypes = [vp]
+        L.fi_get_config.argtypes = [vp, C.POINTER(_Config)]
         L.fi_debug_stats.argtypes = [vp, vp]
         L.fi_kernel_timer_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
         L.fi_debug_waves.argtypes = [vp, vp, C.c_uint64]
@@ -149,10 +150,10 @@ class Engine:
 
     def __init__(self, device: int = 0, private_pages: int = 16, hang_factor_x16: int = 32,
                  max_trials_per_launch: int = 65536, snapshot_interval: int = 0, flags: int = 0,
-                 epoch_iters: int = 0):
+                 epoch_iters: int = 0, lanes_per_wave: int = 0):
         self.L = lib()
         cfg = _Config(device, private_pages, hang_factor_x16, max_trials_per_launch, snapshot_interval, flags,
-                      epoch_iters)
+                      epoch_iters, lanes_per_wave)
         h = C.c_void_p()
         st = self.L.fi_create(C.byref(cfg), C.byref(h))
         if st == FI_E_NODEVICE:
@@ -260,6 +261,11 @@ class Engine:
         out = np.zeros(32, np.uint64)
         self._chk(self.L.fi_debug_stats(self.h, out.ctypes.data), "fi_debug_stats")
         return out
+
+    def config(self) -> dict:
+        cfg = _Config()
+        self._chk(self.L.fi_get_config(self.h, C.byref(cfg)), "fi_get_config")
+        return {n: getattr(cfg, n) for n, _ in _Config._fields_}
 
     def kernel_timer_reset(self):
         self._chk(self.L.fi_kernel_timer_reset(self.h), "fi_kernel_timer_reset")

@@ -9,6 +9,7 @@ TAG=${1:-r01}
 STEPS=${STEPS:-5}
 mkdir -p $O
 export TMPDIR=/tmp
+export SHREWD_FI_JIT_CACHE=$O/jitcache
 cd /tmp
 timeout -k 10 400 python $R/bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_trace_$TAG -o trace --output-format csv -- \

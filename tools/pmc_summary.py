@@ -65,6 +65,7 @@ def main():
         json.dump(pmc, f, indent=1)
     with open(os.path.join(p, "pmc_traffic.json"), "w") as f:
         json.dump({"tag": tag, "workload": wl, "trials": bench["config"]["trials_per_gpu"],
+                   "lanes_per_wave": bench["config"].get("lanes_per_wave", 64),
                    "hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}_pmc.json"}, f, indent=1)
     print(json.dumps(pmc, indent=1))
 
