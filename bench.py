@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lanes", type=int, default=0, help="trials per 64-lane wave (0: engine default)")
+    ap.add_argument("--resume-lanes", type=int, default=0, help="trials per wave in resumed epochs (0: default)")
+    ap.add_argument("--epochs", type=int, default=0, help="epochs per chunk (0: default)")
     ap.add_argument("--epoch-iters", type=int, default=0, help="first epoch's iterations per wave (0: default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
@@ -90,7 +92,8 @@ def main():
     with open(os.path.join(ROOT, "workloads", f"{a.workload}.elf"), "rb") as f:
         elf = f.read()
     eng = Engine(device=local, max_trials_per_launch=max(a.trials, 1024), lanes_per_wave=a.lanes,
-                 epoch_iters=a.epoch_iters)
+                 resume_lanes=a.resume_lanes, epoch_iters=a.epoch_iters,
+                 epochs=a.epochs)
     lanes = eng.config()["lanes_per_wave"]
     t0 = time.perf_counter()
     eng.load_elf(elf, [a.workload])

@@ -72,6 +72,7 @@ typedef int32_t fi_status;
 #define FI_CRASH_FD_ASSERT 7      /* abort  FDArray assert        sim/fd_array.cc:320-323 */
 #define FI_CRASH_SIGTRAP 8        /* ebreak -> SIGTRAP            arch/riscv/faults.cc:317-322 */
 #define FI_CRASH_STACK_LIMIT 9    /* fatal  max stack exceeded    sim/mem_state.cc:440 */
+#define FI_CRASH_AMO_LINE 10      /* panic  AMO across a cache line cpu/simple/atomic.cc:569-570 */
 /* FI_ESCAPE sub-codes */
 #define FI_ESC_INST 1
 #define FI_ESC_SYSCALL 2
@@ -106,8 +107,10 @@ typedef struct {
     uint32_t snapshot_interval;     /* golden snapshot every N committed insts (0 -> auto, >= 256) */
     uint32_t flags;                 /* FI_CFG_* */
     uint32_t epoch_iters;           /* first epoch's loop iterations per wave (0 -> 4096; then x4, x16, unbounded) */
-    uint32_t lanes_per_wave;        /* trials per 64-lane wave: 8, 16, 32 or 64 (0 -> default); fewer trials per wave
-                                       = more waves in flight to hide the interpreter's dependent-issue latency */
+    uint32_t lanes_per_wave;        /* trials per 64-lane wave in the first epoch: 1, 2, 4, ..., 64 (0 -> 64) */
+    uint32_t resume_lanes;          /* trials per wave in resumed epochs (0 -> default): survivors have diverged, and
+                                       a wave serialises its lanes' distinct control flows, so fewer per wave */
+    uint32_t epochs;                /* epochs per chunk (0 -> 4): budgets b, 4b, 16b, 16b, ..., unbounded */
 } fi_config;
 /* fi_config.flags: trials start from process start / run to their natural end
  * (the plain serial semantics, for A/B checks; outcomes are identical) */

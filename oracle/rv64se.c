@@ -111,6 +111,7 @@ const char *or_error(or_campaign_t *c) { return c ? c->err : "null campaign"; }
 /* ---------------------------------------------------------------- machine */
 typedef struct {
     u64 x[32];
+    u64 f[32];            /* FP registers (raw bits; zero at process start) */
     u64 pc, npc;
     u64 num_inst, num_cycles;
     /* decoder state machine, arch/riscv/decoder.cc:54-116 */
@@ -129,7 +130,7 @@ typedef struct {
     const or_campaign_t *c;
 } mach_t;
 
-enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_ESCAPE = 5, F_PGFAULT = 6 };
+enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_ESCAPE = 5, F_PGFAULT = 6, F_AMOLINE = 7 };
 
 /* -------------------------------------------------------------- decode */
 /* Op ids.  Names follow gem5's mnemonics (arch/riscv/isa/decoder.isa). */
@@ -156,7 +157,13 @@ enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_E
     X(lui) X(addw) X(mulw) X(add_uw) X(subw) X(sllw) X(rolw) X(sh1add_uw) \
     X(divw) X(packw) X(sh2add_uw) X(srlw) X(divuw) X(sraw) X(rorw) X(remw) X(sh3add_uw) X(remuw) \
     X(beq) X(bne) X(blt) X(bge) X(bltu) X(bgeu) X(jalr) X(jal) \
-    X(ecall) X(ebreak) X(csr)
+    X(ecall) X(ebreak) X(csr) \
+    X(flh) X(flw) X(fld) X(fsh) X(fsw) X(fsd) X(c_fld) X(c_fsd) X(c_fldsp) X(c_fsdsp) \
+    X(fmv_x_w) X(fmv_x_d) X(fmv_x_h) X(fmv_w_x) X(fmv_d_x) X(fmv_h_x) \
+    X(fsgnj_s) X(fsgnjn_s) X(fsgnjx_s) X(fsgnj_d) X(fsgnjn_d) X(fsgnjx_d) X(fsgnj_h) X(fsgnjn_h) X(fsgnjx_h) \
+    X(fclass_s) X(fclass_d) X(fclass_h) \
+    X(amoadd_w) X(amoswap_w) X(amoxor_w) X(amoor_w) X(amoand_w) X(amomin_w) X(amomax_w) X(amominu_w) X(amomaxu_w) \
+    X(amoadd_d) X(amoswap_d) X(amoxor_d) X(amoor_d) X(amoand_d) X(amomin_d) X(amomax_d) X(amominu_d) X(amomaxu_d)
 
 enum {
 #define X(n) OP_##n,
@@ -173,7 +180,8 @@ static const char *op_names[] = {
 typedef struct {
     u32 raw; u32 len;
     int op;
-    int rd, rs1, rs2;     /* -1 = not used */
+    int rd, rs1, rs2;     /* integer registers, -1 = not used */
+    int frd, frs1, frs2;  /* floating-point registers, -1 = not used */
     s64 imm;
     u32 csr, funct3;
 } dec_t;
@@ -204,16 +212,57 @@ static int gem5_known(u32 raw) {
     return 1;
 }
 /* Unknown and escape encodings read and write no registers. */
+static void refine_fp_amo(u32 raw, dec_t *d);
 static void decode(u32 raw, dec_t *d) {
     decode_tree(raw, d);
     if ((raw & 3) == 3 && (d->op == OP_ESC_FP || d->op == OP_ESC_VEC || d->op == OP_ESC_AMO ||
                            d->op == OP_ESC_SYS || d->op == OP_ESC_HYP) && !gem5_known(raw))
         d->op = OP_UNKNOWN;
-    if (d->op < OP_c_addi4spn) d->rd = d->rs1 = d->rs2 = -1;
+    if ((raw & 3) == 3 && (d->op == OP_ESC_FP || d->op == OP_ESC_AMO)) refine_fp_amo(raw, d);
+    if (d->op < OP_c_addi4spn) d->rd = d->rs1 = d->rs2 = d->frd = d->frs1 = d->frs2 = -1;
+}
+/* The executed members of the LOAD-FP / STORE-FP / OP-FP / AMO groups, among
+ * the encodings gem5 decodes to a known class (decoder.isa:567-591 flh/flw/fld,
+ * :1741-1763 fsh/fsw/fsd, :2067-2283 AMOs, :2896-2942 fsgnj*, :3500-3544
+ * fmv.x.* / fclass.*, :3545-3548 fmv.w.x, :3593-3598 fmv.d.x, :3648-3652
+ * fmv.h.x).  Everything else in those groups stays an escape. */
+static void refine_fp_amo(u32 raw, dec_t *d) {
+    u32 opc = bits(raw, 6, 2), f3 = bits(raw, 14, 12), f7 = bits(raw, 31, 25);
+    int rd = (int)bits(raw, 11, 7), rs1 = (int)bits(raw, 19, 15), rs2 = (int)bits(raw, 24, 20);
+    s64 imm_i = sext(bits(raw, 31, 20), 12), imm_s = sext((bits(raw, 31, 25) << 5) | bits(raw, 11, 7), 12);
+    if (opc == 0x01 && f3 >= 1 && f3 <= 3) {
+        d->op = OP_flh + (int)(f3 - 1); d->frd = rd; d->rs1 = rs1; d->imm = imm_i; return;
+    }
+    if (opc == 0x09 && f3 >= 1 && f3 <= 3) {
+        d->op = OP_fsh + (int)(f3 - 1); d->frs2 = rs2; d->rs1 = rs1; d->imm = imm_s; return;
+    }
+    if (opc == 0x0b && (f3 == 2 || f3 == 3)) {
+        static const int w[32] = {[0x00] = OP_amoadd_w, [0x01] = OP_amoswap_w, [0x04] = OP_amoxor_w,
+                                  [0x08] = OP_amoor_w, [0x0c] = OP_amoand_w, [0x10] = OP_amomin_w,
+                                  [0x14] = OP_amomax_w, [0x18] = OP_amominu_w, [0x1c] = OP_amomaxu_w};
+        int o = w[bits(raw, 31, 27)];
+        if (!o) return;   /* lr / sc: escape */
+        d->op = f3 == 2 ? o : o + (OP_amoadd_d - OP_amoadd_w);
+        d->rd = rd; d->rs1 = rs1; d->rs2 = rs2; d->imm = 0;
+        d->funct3 = bits(raw, 26, 25);   /* aq << 1 | rl: the macro-op's fence micro-ops */
+        return;
+    }
+    if (opc != 0x14) return;
+    if ((f7 == 0x10 || f7 == 0x11 || f7 == 0x12) && f3 <= 2) {
+        d->op = (f7 == 0x10 ? OP_fsgnj_s : f7 == 0x11 ? OP_fsgnj_d : OP_fsgnj_h) + (int)f3;
+        d->frd = rd; d->frs1 = rs1; d->frs2 = rs2; return;
+    }
+    if (f7 == 0x70 && f3 <= 1) { d->op = f3 ? OP_fclass_s : OP_fmv_x_w; d->rd = rd; d->frs1 = rs1; return; }
+    if (f7 == 0x71 && f3 == 1) { d->op = OP_fclass_d; d->rd = rd; d->frs1 = rs1; return; }
+    if (f7 == 0x71 && f3 == 0 && rs2 == 0) { d->op = OP_fmv_x_d; d->rd = rd; d->frs1 = rs1; return; }
+    if (f7 == 0x72 && f3 <= 1) { d->op = f3 ? OP_fclass_h : OP_fmv_x_h; d->rd = rd; d->frs1 = rs1; return; }
+    if (f7 == 0x78 && f3 == 0 && rs2 == 0) { d->op = OP_fmv_w_x; d->frd = rd; d->rs1 = rs1; return; }
+    if (f7 == 0x79 && rs2 == 0) { d->op = OP_fmv_d_x; d->frd = rd; d->rs1 = rs1; return; }
+    if (f7 == 0x7a && rs2 == 0) { d->op = OP_fmv_h_x; d->frd = rd; d->rs1 = rs1; return; }
 }
 static void decode_tree(u32 raw, dec_t *d) {
     memset(d, 0, sizeof(*d));
-    d->raw = raw; d->rd = d->rs1 = d->rs2 = -1; d->op = OP_UNKNOWN;
+    d->raw = raw; d->rd = d->rs1 = d->rs2 = -1; d->frd = d->frs1 = d->frs2 = -1; d->op = OP_UNKNOWN;
     u32 q = raw & 3;
     if (q != 3) {  /* compressed: decoder.isa:43-536 */
         raw &= 0xFFFF; d->raw = raw; d->len = 2;
@@ -227,7 +276,7 @@ static void decode_tree(u32 raw, dec_t *d) {
             case 0: d->op = OP_c_addi4spn; d->rd = rp2; d->rs1 = 2;
                 d->imm = (bits(cimm8, 1, 1) << 2) | (bits(cimm8, 0, 0) << 3) | (bits(cimm8, 7, 6) << 4) | (bits(cimm8, 5, 2) << 6);
                 return;
-            case 1: d->op = OP_ESC_FP; return;                        /* c_fld (ENABLE_ZCD=1) */
+            case 1: d->op = OP_c_fld; d->frd = rp2; d->rs1 = rp1; d->imm = (cimm3 << 3) | (cimm2 << 6); return;  /* :57-68 */
             case 2: d->op = OP_c_lw; d->rd = rp2; d->rs1 = rp1;
                 d->imm = (bits(cimm2, 1, 1) << 2) | (cimm3 << 3) | (bits(cimm2, 0, 0) << 6); return;
             case 3: d->op = OP_c_ld; d->rd = rp2; d->rs1 = rp1; d->imm = (cimm3 << 3) | (cimm2 << 6); return;
@@ -239,7 +288,7 @@ static void decode_tree(u32 raw, dec_t *d) {
                 case 3: d->op = OP_c_sh; d->rs1 = rp1; d->rs2 = rp2; d->imm = bits(cimm2, 0, 0) << 1; return;
                 default: return;
                 }
-            case 5: d->op = OP_ESC_FP; return;                        /* c_fsd */
+            case 5: d->op = OP_c_fsd; d->frs2 = rp2; d->rs1 = rp1; d->imm = (cimm3 << 3) | (cimm2 << 6); return;  /* :146-156 */
             case 6: d->op = OP_c_sw; d->rs1 = rp1; d->rs2 = rp2;
                 d->imm = (bits(cimm2, 1, 1) << 2) | (cimm3 << 3) | (bits(cimm2, 0, 0) << 6); return;
             case 7: d->op = OP_c_sd; d->rs1 = rp1; d->rs2 = rp2; d->imm = (cimm3 << 3) | (cimm2 << 6); return;
@@ -303,7 +352,8 @@ static void decode_tree(u32 raw, dec_t *d) {
         } else { /* q == 2 */
             switch (cop) {
             case 0: d->op = OP_c_slli; d->rd = d->rs1 = rc1; d->imm = cimm5 | (cimm1 << 5); return;
-            case 1: d->op = OP_ESC_FP; return;                        /* c_fldsp */
+            case 1: d->op = OP_c_fldsp; d->frd = rc1; d->rs1 = 2;                                   /* :372-383 */
+                d->imm = (bits(cimm5, 4, 3) << 3) | (cimm1 << 5) | (bits(cimm5, 2, 0) << 6); return;
             case 2: d->op = OP_c_lwsp; d->rd = rc1; d->rs1 = 2;
                 d->imm = (bits(cimm5, 4, 2) << 2) | (cimm1 << 5) | (bits(cimm5, 1, 0) << 6); return;
             case 3: d->op = OP_c_ldsp; d->rd = rc1; d->rs1 = 2;
@@ -319,7 +369,8 @@ static void decode_tree(u32 raw, dec_t *d) {
                     } else { d->op = OP_c_add; d->rd = d->rs1 = rc1; d->rs2 = rc2; }
                 }
                 return;
-            case 5: d->op = OP_ESC_FP; return;                        /* c_fsdsp (ENABLE_ZCD=1) */
+            case 5: d->op = OP_c_fsdsp; d->frs2 = rc2; d->rs1 = 2;                                  /* :493-503 */
+                d->imm = (bits(cimm6, 5, 3) << 3) | (bits(cimm6, 2, 0) << 6); return;
             case 6: d->op = OP_c_swsp; d->rs1 = 2; d->rs2 = rc2; d->imm = (bits(cimm6, 5, 2) << 2) | (bits(cimm6, 1, 0) << 6); return;
             case 7: d->op = OP_c_sdsp; d->rs1 = 2; d->rs2 = rc2; d->imm = (bits(cimm6, 5, 3) << 3) | (bits(cimm6, 2, 0) << 6); return;
             }
@@ -736,6 +787,42 @@ static inline u64 sx32(u64 v) { return (u64)(s64)(s32)(u32)v; }
 /* U-mode CSR accessibility (formats/standard.isa:325-447, regs/misc.hh:604-1241):
  * returns 1 if the access would reach the CSR data path (escape), 0 if it
  * raises IllegalInstFault. */
+/* NaN-boxing, arch/riscv/regs/float.hh:72-94 (RISC-V default NaNs 0x7e00 /
+ * 0x7fc00000, ext/softfloat/specialize.h) */
+static inline u64 unbox32(u64 v) { return (v >> 32) == 0xFFFFFFFFULL ? (v & 0xFFFFFFFFULL) : 0x7FC00000ULL; }
+static inline u64 unbox16(u64 v) { return (v >> 16) == 0xFFFFFFFFFFFFULL ? (v & 0xFFFF) : 0x7E00; }
+static inline u64 box32(u64 v) { return 0xFFFFFFFF00000000ULL | (v & 0xFFFFFFFFULL); }
+static inline u64 box16(u64 v) { return 0xFFFFFFFFFFFF0000ULL | (v & 0xFFFF); }
+/* f16/f32/f64_classify, ext/softfloat/f32_classify.c (same shape for 16/64) */
+static u64 fclassify(u64 ui, int ebits, int fbits) {
+    u64 emax = (1ULL << ebits) - 1;
+    u64 e = (ui >> fbits) & emax, fr = ui & ((1ULL << fbits) - 1);
+    int sign = (int)((ui >> (ebits + fbits)) & 1);
+    int inf_nan = e == emax, sub_zero = e == 0, frac_zero = fr == 0;
+    int is_nan = inf_nan && !frac_zero, is_snan = is_nan && !((fr >> (fbits - 1)) & 1);
+    return (u64)(sign && inf_nan && frac_zero) << 0 | (u64)(sign && !inf_nan && !sub_zero) << 1 |
+           (u64)(sign && sub_zero && !frac_zero) << 2 | (u64)(sign && sub_zero && frac_zero) << 3 |
+           (u64)(!sign && inf_nan && frac_zero) << 7 | (u64)(!sign && !inf_nan && !sub_zero) << 6 |
+           (u64)(!sign && sub_zero && !frac_zero) << 5 | (u64)(!sign && sub_zero && frac_zero) << 4 |
+           (u64)(is_nan && is_snan) << 8 | (u64)(is_nan && !is_snan) << 9;
+}
+/* AtomicMemOp RMW (decoder.isa:2067-2283 lambdas), w = 32-bit form */
+static u64 amo_apply(int op, u64 mem, u64 src, int w) {
+    if (w) { mem &= 0xFFFFFFFFULL; src &= 0xFFFFFFFFULL; }
+    s64 sm = w ? (s64)(s32)(u32)mem : (s64)mem, ss = w ? (s64)(s32)(u32)src : (s64)src;
+    switch (op) {
+    case 0: return mem + src;                       /* add  */
+    case 1: return src;                             /* swap */
+    case 2: return mem ^ src;                       /* xor  */
+    case 3: return mem | src;                       /* or   */
+    case 4: return mem & src;                       /* and  */
+    case 5: return ss < sm ? src : mem;             /* min  */
+    case 6: return ss > sm ? src : mem;             /* max  */
+    case 7: return src < mem ? src : mem;           /* minu */
+    default: return src > mem ? src : mem;          /* maxu */
+    }
+}
+
 static int csr_u_accessible(u32 csr) {
     if (bits(csr, 9, 8) != 0) return 0;     /* lowestAllowedMode > U */
     if (csr >= 0x001 && csr <= 0x003) return 1;
@@ -898,6 +985,71 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
     case OP_jal: v = m->npc; m->npc = pc + imm; break;
     case OP_ecall: return F_SYSCALL;
     case OP_csr: return csr_u_accessible(d->csr) ? F_ESCAPE + 100 : F_ILLEGAL;
+    /* ---- F/D/Zfh loads and stores (Load/Store formats, formats/mem.isa:123-207):
+     * the access first, then the FPU-status update (never off in SE: fs is
+     * INITIAL from ISA::resetThread, isa.cc:390); loads NaN-box (float.hh:104-107) */
+    case OP_flh: case OP_flw: case OP_fld: case OP_c_fld: case OP_c_fldsp: {
+        unsigned sz = d->op == OP_flh ? 2 : d->op == OP_flw ? 4 : 8;
+        r = mem_read(m, a + imm, sz, &t, fault_va); if (r) return r;
+        m->f[d->frd] = sz == 2 ? box16(t) : sz == 4 ? box32(t) : t;
+        goto no_rd;
+    }
+    case OP_fsh: case OP_fsw: case OP_fsd: case OP_c_fsd: case OP_c_fsdsp: {
+        unsigned sz = d->op == OP_fsh ? 2 : d->op == OP_fsw ? 4 : 8;
+        r = mem_write(m, a + imm, sz, m->f[d->frs2], fault_va); if (r) return r;
+        goto no_rd;
+    }
+    /* ---- moves, sign injection, classify (no rounding, no exception flags) */
+    case OP_fmv_x_w: v = sx32(m->f[d->frs1]); break;
+    case OP_fmv_x_d: v = m->f[d->frs1]; break;
+    case OP_fmv_x_h: v = (u64)sext(m->f[d->frs1] & 0xFFFF, 16); break;
+    case OP_fmv_w_x: m->f[d->frd] = box32(a); goto no_rd;
+    case OP_fmv_d_x: m->f[d->frd] = a; goto no_rd;
+    case OP_fmv_h_x: m->f[d->frd] = box16(a); goto no_rd;
+    case OP_fsgnj_s: case OP_fsgnjn_s: case OP_fsgnjx_s: {
+        u64 x = unbox32(m->f[d->frs1]), y = unbox32(m->f[d->frs2]);
+        u64 sg = d->op == OP_fsgnj_s ? y : d->op == OP_fsgnjn_s ? ~y : (x ^ y);
+        m->f[d->frd] = box32((x & 0x7FFFFFFFULL) | (sg & 0x80000000ULL));
+        goto no_rd;
+    }
+    case OP_fsgnj_d: case OP_fsgnjn_d: case OP_fsgnjx_d: {
+        u64 x = m->f[d->frs1], y = m->f[d->frs2];
+        u64 sg = d->op == OP_fsgnj_d ? y : d->op == OP_fsgnjn_d ? ~y : (x ^ y);
+        m->f[d->frd] = (x & 0x7FFFFFFFFFFFFFFFULL) | (sg & 0x8000000000000000ULL);
+        goto no_rd;
+    }
+    case OP_fsgnj_h: case OP_fsgnjn_h: case OP_fsgnjx_h: {
+        u64 x = unbox16(m->f[d->frs1]), y = unbox16(m->f[d->frs2]);
+        u64 sg = d->op == OP_fsgnj_h ? y : d->op == OP_fsgnjn_h ? ~y : (x ^ y);
+        m->f[d->frd] = box16((x & 0x7FFF) | (sg & 0x8000));
+        goto no_rd;
+    }
+    case OP_fclass_s: v = fclassify(unbox32(m->f[d->frs1]), 8, 23); break;
+    case OP_fclass_d: v = fclassify(m->f[d->frs1], 11, 52); break;
+    case OP_fclass_h: v = fclassify(unbox16(m->f[d->frs1]), 5, 10); break;
+    /* ---- AMOs: AtomicSimpleCPU::amoMem (atomic.cc:546-608) panics on an
+     * access that crosses a 64-byte line before translating; no alignment
+     * check in SE (tlb.cc:573-604).  Rd = the old value (sign-extended .w). */
+    case OP_amoadd_w: case OP_amoswap_w: case OP_amoxor_w: case OP_amoor_w: case OP_amoand_w:
+    case OP_amomin_w: case OP_amomax_w: case OP_amominu_w: case OP_amomaxu_w:
+    case OP_amoadd_d: case OP_amoswap_d: case OP_amoxor_d: case OP_amoor_d: case OP_amoand_d:
+    case OP_amomin_d: case OP_amomax_d: case OP_amominu_d: case OP_amomaxu_d: {
+        int w = d->op <= OP_amomaxu_w;
+        unsigned sz = w ? 4 : 8;
+        u64 ea = a;
+        if (((ea + sz - 1) & ~63ULL) > ea) return F_AMOLINE;
+        if (ea + sz - 1 < ea) { *fault_va = ea; return F_PGFAULT; }
+        uint8_t *pg = translate_w(m, ea);
+        if (!pg) { *fault_va = ea; return F_PGFAULT; }
+        u64 old = 0;
+        for (unsigned i = 0; i < sz; i++) old |= (u64)pg[(ea + i) & (PAGE - 1)] << (8 * i);
+        u64 nw = amo_apply(d->op - (w ? OP_amoadd_w : OP_amoadd_d), old, b, w);
+        for (unsigned i = 0; i < sz; i++) pg[(ea + i) & (PAGE - 1)] = (uint8_t)(nw >> (8 * i));
+        m->data_bytes += 2 * sz;
+        m->num_cycles += (d->funct3 & 1) + (d->funct3 >> 1);   /* rl / aq fence micro-ops: one tick each */
+        v = w ? sx32(old) : old;
+        break;
+    }
     default: return F_UNKNOWN;
     }
     wrreg(m, d->rd, v);
@@ -943,6 +1095,7 @@ static void invoke_fault(mach_t *m, int f, u64 fault_va, const dec_t *d) {
     case F_UNKNOWN: finish(m, OR_CRASH, OR_CRASH_UNKNOWN_INST, 134); return;
     case F_ESCAPE: finish(m, OR_ESCAPE, OR_ESC_INST, 0); m->res.detail = d->raw; return;
     case F_ESCAPE + 100: finish(m, OR_ESCAPE, OR_ESC_CSR, 0); m->res.detail = d->raw; return;
+    case F_AMOLINE: finish(m, OR_CRASH, OR_CRASH_AMO_LINE, 134); return;
     case 100: finish(m, OR_DETECTED, 0, 0); return;
     case F_PGFAULT: {
         int h = fixup_fault(m, fault_va);

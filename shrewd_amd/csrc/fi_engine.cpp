@@ -45,6 +45,7 @@ using namespace fi;
 
 // trials per wave when fi_config.lanes_per_wave is 0
 static constexpr uint32_t kDefaultLanes = 64;
+static constexpr uint32_t kDefaultResumeLanes = 8;   // measured: profiles/README.md (r01b sweep)
 
 struct fi_engine {
     fi_config cfg{};
@@ -109,6 +110,8 @@ struct fi_engine {
     fi_histogram *d_hist = nullptr;
     unsigned long long *d_stats = nullptr;
     uint64_t *d_wave_dbg = nullptr;
+    uint64_t *d_fregs = nullptr;     // FP registers of the work slots
+    bool golden_fp = false;          // the golden run wrote FP state: no snapshot start / early exit
     uint8_t *d_priv = nullptr;
     uint64_t *d_priv_vpn = nullptr;
     // epochs: suspended lanes, survivor lists, counts, sort buffers
@@ -159,11 +162,13 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
     if (e->cfg.hang_factor_x16 == 0) e->cfg.hang_factor_x16 = 32;
     if (e->cfg.max_trials_per_launch == 0) e->cfg.max_trials_per_launch = 65536;
     if (e->cfg.lanes_per_wave == 0) e->cfg.lanes_per_wave = kDefaultLanes;
-    if (e->cfg.lanes_per_wave != 8 && e->cfg.lanes_per_wave != 16 && e->cfg.lanes_per_wave != 32 &&
-        e->cfg.lanes_per_wave != 64) {
-        g_create_err = "fi_create: lanes_per_wave must be 8, 16, 32 or 64";
-        delete e;
-        return FI_E_ARG;
+    if (e->cfg.resume_lanes == 0) e->cfg.resume_lanes = kDefaultResumeLanes;
+    for (uint32_t l : {e->cfg.lanes_per_wave, e->cfg.resume_lanes}) {
+        if (l > 64 || (l & (l - 1))) {
+            g_create_err = "fi_create: lanes_per_wave / resume_lanes must be a power of two <= 64";
+            delete e;
+            return FI_E_ARG;
+        }
     }
     e->dev = e->cfg.device;
     if (e->dev < 0 || e->dev >= n) {
@@ -183,7 +188,7 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
 
 static void free_work(fi_engine *e) {
     dfree(e->d_sites); dfree(e->d_keys); dfree(e->d_keys2); dfree(e->d_perm); dfree(e->d_perm2);
-    dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg);
+    dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg); dfree(e->d_fregs);
     dfree(e->d_save); dfree(e->d_surv[0]); dfree(e->d_surv[1]); dfree(e->d_cnt);
     dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_priv); dfree(e->d_priv_vpn);
     e->cap = 0;
@@ -437,10 +442,11 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_out, c * sizeof(fi_outcome)));
     HIPCHK(hipMalloc(&e->d_hist, sizeof(fi_histogram)));
     HIPCHK(hipMalloc(&e->d_stats, 32 * sizeof(unsigned long long)));
-    HIPCHK(hipMalloc(&e->d_wave_dbg, ((c + 7) / 8) * 4 * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&e->d_wave_dbg, c * 4 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&e->d_priv, c * e->cfg.private_pages * kPage));
     HIPCHK(hipMalloc(&e->d_priv_vpn, c * e->cfg.private_pages * 8));
     HIPCHK(hipMalloc(&e->d_save, c * sizeof(LaneSave)));
+    HIPCHK(hipMalloc(&e->d_fregs, c * 32 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&e->d_surv[0], c * 4));
     HIPCHK(hipMalloc(&e->d_surv[1], c * 4));
     HIPCHK(hipMalloc(&e->d_cnt, 16 * 4));
@@ -460,9 +466,9 @@ static DevCtx base_ctx(fi_engine *e) {
     c.snaps = e->d_snaps; c.snap_tab = e->d_tab; c.pool = e->d_pool; c.zero_page = e->d_zero;
     const bool start = !(e->cfg.flags & FI_CFG_NO_SNAPSHOT_START);
     c.n_snap = (uint32_t)e->snaps.size();
-    c.snap_start = start ? 1 : 0;
+    c.snap_start = (start && !e->golden_fp) ? 1 : 0;
     c.snap_interval = e->snap_I;
-    c.early_exit = (!(e->cfg.flags & FI_CFG_NO_EARLY_EXIT) && e->snaps.size() > 1) ? 1 : 0;
+    c.early_exit = (!(e->cfg.flags & FI_CFG_NO_EARLY_EXIT) && e->snaps.size() > 1 && !e->golden_fp) ? 1 : 0;
     c.gout = e->d_gout; c.gerr = e->d_gerr; c.gout_len = e->gout.size(); c.gerr_len = e->gerr.size();
     c.gexit = e->golden.exit_code;
     c.gdetail = e->gdetail;
@@ -472,6 +478,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.protect_mask = e->protect;
     c.priv_frames = e->d_priv; c.priv_vpn = e->d_priv_vpn;
     c.tx_sink = e->d_sink;
+    c.fregs = e->d_fregs;
     c.wave_dbg = e->d_wave_dbg;
     c.stats = e->d_stats;
     c.lanes = e->cfg.lanes_per_wave;
@@ -487,7 +494,10 @@ static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_
     uint64_t *d_gvpn = nullptr;
     HIPCHK(hipMalloc(&d_gpriv, (uint64_t)P * kPage));
     HIPCHK(hipMalloc(&d_gvpn, (uint64_t)P * 8));
+    uint64_t *d_gfregs = nullptr;
+    HIPCHK(hipMalloc(&d_gfregs, 32 * sizeof(uint64_t)));
     DevCtx c = base_ctx(e);
+    c.fregs = d_gfregs;
     c.record = 1;
     c.early_exit = 0;
     c.snap_start = 0;
@@ -510,6 +520,7 @@ static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_
     if (err == hipSuccess) err = hipMemcpy(&o, e->d_out, sizeof o, hipMemcpyDeviceToHost);
     if (err == hipSuccess) err = hipMemcpy(stats, e->d_stats, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
     (void)hipFree(d_gpriv);
+    (void)hipFree(d_gfregs);
     (void)hipFree(d_gvpn);
     if (err != hipSuccess) return fail(e, FI_E_HIP, "golden launch: %s", hipGetErrorString(err));
     e->last_ms = ms;
@@ -575,6 +586,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     e->golden.fetch_bytes = stats[0];
     e->golden.data_bytes = stats[1];
     e->gdetail = o.detail;
+    e->golden_fp = stats[22] != 0;
 
     // ---- pass 2: the same run again, capturing a snapshot every I committed
     // instructions (state + every page written so far), within ~1 GiB
@@ -829,13 +841,16 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
         budgets = {0};
     } else {
         const uint32_t b = e->cfg.epoch_iters ? e->cfg.epoch_iters : 4096;
-        budgets = {b, 4 * b, 16 * b, 0};
+        const uint32_t n_ep = e->cfg.epochs ? std::max(2u, std::min(e->cfg.epochs, 14u)) : 4u;
+        for (uint32_t i = 0; i + 1 < n_ep; i++) budgets.push_back(b << (2 * std::min(i, 2u)));
+        budgets.push_back(0);
     }
     HIPCHK(hipEventRecord(e->ev0, st));
     for (size_t ep = 0; ep < budgets.size(); ep++) {
         c.wave_budget = budgets[ep];
         c.surv = e->d_surv[ep & 1];
         c.surv_n = e->d_cnt + ep;
+        c.lanes = ep == 0 ? e->cfg.lanes_per_wave : e->cfg.resume_lanes;
         if (ep == 0) {
             c.resume = nullptr;
             c.resume_n = nullptr;
@@ -973,7 +988,7 @@ fi_status fi_debug_jit_compile(const char *body, const char *arch, void *code, u
 
 fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves) {
     if (!e || !out) return FI_E_ARG;
-    if (n_waves > (e->cap + 7) / 8) return fail(e, FI_E_ARG, "more waves than the work buffers hold");
+    if (n_waves > e->cap) return fail(e, FI_E_ARG, "more waves than the work buffers hold");
     HIPCHK(hipStreamSynchronize(e->stream));
     HIPCHK(hipMemcpy(out, e->d_wave_dbg, n_waves * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return FI_OK;

@@ -96,6 +96,7 @@ struct DevCtx {
     uint8_t *priv_frames;
     uint64_t *priv_vpn;
     uint8_t *tx_sink;                // translated code: stores of lanes outside the running group land here
+    uint64_t *fregs;                 // FP registers [32][n_slots] (written only by a lane's FP data-movement ops)
     // record mode: snapshot capture at numInst == k * rec_interval
     SnapState *rec_snaps;            // [rec_max_snaps]
     uint8_t *rec_pages;              // [rec_max_snaps][priv_pages][4096]

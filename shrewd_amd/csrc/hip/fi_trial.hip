@@ -171,7 +171,8 @@ __device__ __forceinline__ uint64_t lookup(KCtx *c, const WaveMem &w, LaneMem &m
 }
 __device__ __forceinline__ const uint8_t *page_of(uint64_t p) { return (const uint8_t *)(p & ~1ULL); }
 
-enum { F_NONE = 0, F_SYSCALL, F_BREAK, F_ILLEGAL, F_UNKNOWN, F_ESCAPE, F_ESCCSR, F_PGFAULT, F_NEEDPAGE, F_DETECT };
+enum { F_NONE = 0, F_SYSCALL, F_BREAK, F_ILLEGAL, F_UNKNOWN, F_ESCAPE, F_ESCCSR, F_PGFAULT, F_NEEDPAGE, F_DETECT,
+       F_AMOLINE };
 
 // AtomicSimpleCPU::readMem/writeMem (atomic.cc:331-544): the access is split
 // at 64-byte line boundaries, each fragment translated on its own; faults are
@@ -300,9 +301,52 @@ struct Lane {
     uint32_t nfail;               // failed comparisons (back-off)
     int watch;
     bool out_bad, done;
+    bool fp;                      // FP registers materialised (else all zero, as at process start)
     uint8_t injected;
     fi_outcome res;
 };
+
+// ------------------------------------------------------------------ F/D/Zfh + A
+// FP registers live in HBM, [32][n_slots] (lane-coalesced), touched only by the
+// FP data-movement ops of the general path; a lane that never wrote one reads
+// zeros (RegFile is zeroed at process start).  NaN-boxing follows
+// src/arch/riscv/regs/float.hh:72-107 (default NaNs 0x7e00 / 0x7fc00000).
+__device__ __forceinline__ uint64_t fp_unbox32(uint64_t v) {
+    return (v >> 32) == 0xFFFFFFFFULL ? (v & 0xFFFFFFFFULL) : 0x7FC00000ULL;
+}
+__device__ __forceinline__ uint64_t fp_unbox16(uint64_t v) {
+    return (v >> 16) == 0xFFFFFFFFFFFFULL ? (v & 0xFFFF) : 0x7E00ULL;
+}
+// f16/f32/f64_classify (ext/softfloat/f32_classify.c, same shape per width)
+__device__ __forceinline__ uint64_t fp_classify(uint64_t ui, int eb, int fb) {
+    const uint64_t emax = (1ULL << eb) - 1, e = (ui >> fb) & emax, fr = ui & ((1ULL << fb) - 1);
+    const bool sg = (ui >> (eb + fb)) & 1, infnan = e == emax, subz = e == 0, fz = fr == 0;
+    const bool nan = infnan && !fz, snan = nan && !((fr >> (fb - 1)) & 1);
+    int k;
+    if (nan) k = snan ? 8 : 9;
+    else if (infnan) k = sg ? 0 : 7;
+    else if (subz) k = fz ? (sg ? 3 : 4) : (sg ? 2 : 5);
+    else k = sg ? 1 : 6;
+    return 1ULL << k;
+}
+// AtomicMemOp read-modify-write bodies (decoder.isa:2067-2283), op = 0 add,
+// 1 swap, 2 xor, 3 or, 4 and, 5 min, 6 max, 7 minu, 8 maxu
+__device__ __forceinline__ uint64_t amo_apply(int op, uint64_t mem, uint64_t src, bool w) {
+    if (w) { mem &= 0xFFFFFFFFULL; src &= 0xFFFFFFFFULL; }
+    const int64_t sm = w ? (int64_t)(int32_t)(uint32_t)mem : (int64_t)mem;
+    const int64_t ss = w ? (int64_t)(int32_t)(uint32_t)src : (int64_t)src;
+    switch (op) {
+    case 0: return mem + src;
+    case 1: return src;
+    case 2: return mem ^ src;
+    case 3: return mem | src;
+    case 4: return mem & src;
+    case 5: return ss < sm ? src : mem;
+    case 6: return ss > sm ? src : mem;
+    case 7: return src < mem ? src : mem;
+    default: return src > mem ? src : mem;
+    }
+}
 
 __device__ __forceinline__ void finish(Lane &L, int cls, int sub, int code, uint32_t detail) {
     L.done = true;
@@ -557,7 +601,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     L.fetch_b = L.data_b = 0;
     L.next_chk = kNone;
     L.nfail = 0;
-    L.watch = -1; L.out_bad = false; L.done = !live; L.injected = (CX->record || !live) ? 1 : 0;
+    L.watch = -1; L.out_bad = false; L.fp = false; L.done = !live; L.injected = (CX->record || !live) ? 1 : 0;
     L.res.cls = 0; L.res.sub = 0; L.res.exit_code = 0; L.res.flags = 0; L.res.detail = 0; L.res.ninst = 0;
     LaneMem m;
     m.stack_min = S0->stack_min;
@@ -567,7 +611,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     if (resume && live) {
         L.pc = SV->pc; L.ninst = SV->ninst; L.ncyc = SV->ncyc; L.out_pos = SV->out_pos; L.err_pos = SV->err_pos;
         L.next_chk = SV->next_chk; L.nfail = SV->nfail; L.watch = SV->watch;
-        L.out_bad = SV->flags & 1; L.injected = (uint8_t)((SV->flags >> 1) & 3);
+        L.out_bad = SV->flags & 1; L.injected = (uint8_t)((SV->flags >> 1) & 3); L.fp = (SV->flags >> 4) & 1;
         m.stack_min = SV->stack_min; m.n_priv = SV->n_priv; m.code_dirty = (SV->flags >> 3) & 1;
     }
     bool suspended = false;
@@ -594,7 +638,8 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 sv->pc = L.pc; sv->ninst = L.ninst; sv->ncyc = L.ncyc; sv->out_pos = L.out_pos; sv->err_pos = L.err_pos;
                 sv->stack_min = m.stack_min; sv->next_chk = L.next_chk; sv->watch = L.watch; sv->nfail = L.nfail;
                 sv->n_priv = m.n_priv; sv->snap_j = j;
-                sv->flags = (L.out_bad ? 1u : 0u) | ((uint32_t)L.injected << 1) | (m.code_dirty ? 8u : 0u);
+                sv->flags = (L.out_bad ? 1u : 0u) | ((uint32_t)L.injected << 1) | (m.code_dirty ? 8u : 0u) |
+                            (L.fp ? 16u : 0u);
                 CX->surv[atomicAdd(CX->surv_n, 1u)] = (uint32_t)slot;
                 suspended = true;
                 L.done = true;
@@ -674,7 +719,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 pend &= ~__ballot(grp);
                 const SnapState *S = CX->snaps + (uint32_t)(kn / CX->snap_interval);
                 bool eq = grp && L.pc == S->pc && L.out_pos == S->out_pos && L.err_pos == S->err_pos && !L.out_bad &&
-                          m.stack_min == S->stack_min;
+                          m.stack_min == S->stack_min && !L.fp;
                 if (__ballot(eq)) {
                     // a register the golden future writes before reading it cannot
                     // influence the outcome (liveness from the golden trace)
@@ -1078,6 +1123,12 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         bool wrd = true;
         uint32_t msz = 0, mext = 0;   // memory access size / sign-extension width (uniform)
         bool mst = false;
+        uint64_t sval = b;            // store data (an FP register for FP stores)
+        uint64_t fval = 0;            // FP destination value
+        uint32_t fbox = 0;            // FP destination: 0 none, 1 fval, 16/32/64 loaded (NaN-boxed) width
+        uint32_t xticks = 0;          // extra micro-op ticks (AMO fences)
+        int amo = -1;                 // AMO read-modify-write op (amo_apply), -1 none
+#define FREG_RD(r) (L.fp ? CX->fregs[(uint64_t)(r) * CX->n_slots + slot] : 0ULL)
         // detected-by-replica: the flipped protected register is read before
         // being overwritten (build-defined SHREWD semantics)
         if (L.watch > 0 &&
@@ -1221,14 +1272,80 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             case OP_jal: v = npc; npc = pc + imm; break;
             case OP_ecall: f = F_SYSCALL; break;
             case OP_csr: f = csr_u_accessible(d.raw >> 20) ? F_ESCCSR : F_ILLEGAL; break;
+            // ---- F/D/Zfh data movement: loads/stores through the single access
+            // site below (access first, then the FPU-status update, which never
+            // faults in SE: fs = INITIAL, isa.cc:390)
+            case OP_flh: msz = 2; fbox = 16; wrd = false; break;
+            case OP_flw: msz = 4; fbox = 32; wrd = false; break;
+            case OP_fld: case OP_c_fld: case OP_c_fldsp: msz = 8; fbox = 64; wrd = false; break;
+            case OP_fsh: msz = 2; mst = true; wrd = false; sval = FREG_RD(d.rs2); break;
+            case OP_fsw: msz = 4; mst = true; wrd = false; sval = FREG_RD(d.rs2); break;
+            case OP_fsd: case OP_c_fsd: case OP_c_fsdsp: msz = 8; mst = true; wrd = false; sval = FREG_RD(d.rs2); break;
+            case OP_fmv_x_w: v = sx32(FREG_RD(d.rs1)); break;
+            case OP_fmv_x_d: v = FREG_RD(d.rs1); break;
+            case OP_fmv_x_h: v = (uint64_t)sext64(FREG_RD(d.rs1) & 0xFFFF, 16); break;
+            case OP_fmv_w_x: fval = 0xFFFFFFFF00000000ULL | (a & 0xFFFFFFFFULL); fbox = 1; wrd = false; break;
+            case OP_fmv_d_x: fval = a; fbox = 1; wrd = false; break;
+            case OP_fmv_h_x: fval = 0xFFFFFFFFFFFF0000ULL | (a & 0xFFFF); fbox = 1; wrd = false; break;
+            case OP_fsgnj_s: case OP_fsgnjn_s: case OP_fsgnjx_s: {
+                const uint64_t x = fp_unbox32(FREG_RD(d.rs1)), y = fp_unbox32(FREG_RD(d.rs2));
+                const uint64_t sg = d.op == OP_fsgnj_s ? y : d.op == OP_fsgnjn_s ? ~y : (x ^ y);
+                fval = 0xFFFFFFFF00000000ULL | (x & 0x7FFFFFFFULL) | (sg & 0x80000000ULL); fbox = 1; wrd = false;
+                break;
+            }
+            case OP_fsgnj_d: case OP_fsgnjn_d: case OP_fsgnjx_d: {
+                const uint64_t x = FREG_RD(d.rs1), y = FREG_RD(d.rs2);
+                const uint64_t sg = d.op == OP_fsgnj_d ? y : d.op == OP_fsgnjn_d ? ~y : (x ^ y);
+                fval = (x & 0x7FFFFFFFFFFFFFFFULL) | (sg & 0x8000000000000000ULL); fbox = 1; wrd = false;
+                break;
+            }
+            case OP_fsgnj_h: case OP_fsgnjn_h: case OP_fsgnjx_h: {
+                const uint64_t x = fp_unbox16(FREG_RD(d.rs1)), y = fp_unbox16(FREG_RD(d.rs2));
+                const uint64_t sg = d.op == OP_fsgnj_h ? y : d.op == OP_fsgnjn_h ? ~y : (x ^ y);
+                fval = 0xFFFFFFFFFFFF0000ULL | (x & 0x7FFF) | (sg & 0x8000); fbox = 1; wrd = false;
+                break;
+            }
+            case OP_fclass_s: v = fp_classify(fp_unbox32(FREG_RD(d.rs1)), 8, 23); break;
+            case OP_fclass_d: v = fp_classify(FREG_RD(d.rs1), 11, 52); break;
+            case OP_fclass_h: v = fp_classify(fp_unbox16(FREG_RD(d.rs1)), 5, 10); break;
+            // ---- A-extension RMW: AtomicSimpleCPU::amoMem (atomic.cc:546-608)
+            // panics on a 64-byte-line crossing before translating; one
+            // translation, then read-modify-write; rl/aq fences are extra
+            // micro-op ticks (amo.isa macro-op constructors)
+            case OP_amoadd_w: case OP_amoswap_w: case OP_amoxor_w: case OP_amoor_w: case OP_amoand_w:
+            case OP_amomin_w: case OP_amomax_w: case OP_amominu_w: case OP_amomaxu_w:
+            case OP_amoadd_d: case OP_amoswap_d: case OP_amoxor_d: case OP_amoor_d: case OP_amoand_d:
+            case OP_amomin_d: case OP_amomax_d: case OP_amominu_d: case OP_amomaxu_d: {
+                const bool w32 = d.op <= OP_amomaxu_w;
+                msz = w32 ? 4 : 8;
+                if (((a + msz - 1) & ~63ULL) > a) { f = F_AMOLINE; msz = 0; break; }
+                amo = (int)d.op - (w32 ? OP_amoadd_w : OP_amoadd_d);
+                xticks = ((d.raw >> 25) & 1) + ((d.raw >> 26) & 1);   // rl, aq (pre-decoded aux holds the micro-op)
+                break;
+            }
             default: f = F_UNKNOWN; break;
             }
         }
         if (msz && f == F_NONE) {
-            t = b;
-            f = mem_access(CX, w, m, slot, a + imm, msz, mst, t, fva);
-            L.data_b += msz;
-            if (!mst) v = mext ? (uint64_t)sext64(t, mext) : t;
+            // one call site (an AMO reads, then writes, in a second pass): a
+            // second inlined copy of mem_access puts the lane state in scratch
+            const uint64_t ea = amo >= 0 ? a : a + imm;
+            uint64_t old = 0;
+#pragma unroll 1
+            for (int pass = 0; pass < (amo >= 0 ? 2 : 1); pass++) {
+                t = pass ? amo_apply(amo, old, b, msz == 4) : (amo >= 0 ? 0 : sval);
+                f = mem_access(CX, w, m, slot, ea, msz, pass ? true : mst, t, fva);
+                if (f != F_NONE) break;
+                if (!pass) old = t;
+            }
+            if (f == F_NONE) {
+                L.data_b += amo >= 0 ? 2 * msz : msz;
+                if (amo >= 0) v = msz == 4 ? sx32(old) : old;
+                else if (!mst) {
+                    if (fbox) fval = fbox == 16 ? (0xFFFFFFFFFFFF0000ULL | t) : fbox == 32 ? (0xFFFFFFFF00000000ULL | t) : t;
+                    else v = mext ? (uint64_t)sext64(t, mext) : t;
+                }
+            }
         }
         // F_NEEDPAGE: copy-on-write first; the tick is retried (no commit)
         // ---- F. commit: countInst only on NoFault (atomic.cc:687-689), then
@@ -1243,6 +1360,15 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             tpos++;
         }
         if (f == F_NONE) {
+            if (fbox) {   // FP destination: materialise the lane's FP file on its first write
+                if (!L.fp) {
+                    for (int r = 0; r < 32; r++) CX->fregs[(uint64_t)r * CX->n_slots + slot] = 0;
+                    L.fp = true;
+                    if (CX->record) CX->stats[22] = 1;   // the golden run uses FP state (host disables snapshots)
+                }
+                CX->fregs[(uint64_t)d.rd * CX->n_slots + slot] = fval;
+            }
+            L.ncyc += xticks;
             if (wrd && d.rd) RREG(d.rd) = v;
             if (wrd && L.watch > 0 && (d.flags & kPreRd) && d.rd == L.watch) L.watch = -1;
             L.ninst++;
@@ -1259,6 +1385,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         case F_ESCAPE: finish(L, FI_ESCAPE, FI_ESC_INST, 0, d.raw); break;
         case F_ESCCSR: finish(L, FI_ESCAPE, FI_ESC_CSR, 0, d.raw); break;
         case F_DETECT: finish(L, FI_DETECTED, 0, 0, (uint32_t)pc); break;
+        case F_AMOLINE: finish(L, FI_CRASH, FI_CRASH_AMO_LINE, 134, (uint32_t)pc); break;
         case F_PGFAULT:
             if (fva < m.stack_min && fva >= kStackBase - kMaxStack) {
                 const uint64_t nm = fva & ~4095ULL;

@@ -35,7 +35,13 @@
     X(lui) X(addw) X(mulw) X(add_uw) X(subw) X(sllw) X(rolw) X(sh1add_uw) \
     X(divw) X(packw) X(sh2add_uw) X(srlw) X(divuw) X(sraw) X(rorw) X(remw) X(sh3add_uw) X(remuw) \
     X(beq) X(bne) X(blt) X(bge) X(bltu) X(bgeu) X(jalr) X(jal) \
-    X(ecall) X(ebreak) X(csr)
+    X(ecall) X(ebreak) X(csr) \
+    X(flh) X(flw) X(fld) X(fsh) X(fsw) X(fsd) X(c_fld) X(c_fsd) X(c_fldsp) X(c_fsdsp) \
+    X(fmv_x_w) X(fmv_x_d) X(fmv_x_h) X(fmv_w_x) X(fmv_d_x) X(fmv_h_x) \
+    X(fsgnj_s) X(fsgnjn_s) X(fsgnjx_s) X(fsgnj_d) X(fsgnjn_d) X(fsgnjx_d) X(fsgnj_h) X(fsgnjn_h) X(fsgnjx_h) \
+    X(fclass_s) X(fclass_d) X(fclass_h) \
+    X(amoadd_w) X(amoswap_w) X(amoxor_w) X(amoor_w) X(amoand_w) X(amomin_w) X(amomax_w) X(amominu_w) X(amomaxu_w) \
+    X(amoadd_d) X(amoswap_d) X(amoxor_d) X(amoor_d) X(amoand_d) X(amomin_d) X(amomax_d) X(amominu_d) X(amomaxu_d)
 
 namespace fi {
 
@@ -79,7 +85,7 @@ __device__ inline Dec rv_decode_tree(uint32_t raw) {
                 d.imm = (fbits(cimm8, 1, 1) << 2) | (fbits(cimm8, 0, 0) << 3) | (fbits(cimm8, 7, 6) << 4) |
                         (fbits(cimm8, 5, 2) << 6);
                 return d;
-            case 1: d.op = OP_ESC_FP; return d;
+            case 1: d.op = OP_c_fld; d.rd = (uint8_t)rp2; D_RS1(rp1); d.imm = (cimm3 << 3) | (cimm2 << 6); return d;
             case 2: d.op = OP_c_lw; D_RD(rp2); D_RS1(rp1);
                 d.imm = (fbits(cimm2, 1, 1) << 2) | (cimm3 << 3) | (fbits(cimm2, 0, 0) << 6); return d;
             case 3: d.op = OP_c_ld; D_RD(rp2); D_RS1(rp1); d.imm = (cimm3 << 3) | (cimm2 << 6); return d;
@@ -91,7 +97,7 @@ __device__ inline Dec rv_decode_tree(uint32_t raw) {
                 case 3: d.op = OP_c_sh; D_RS1(rp1); D_RS2(rp2); d.imm = fbits(cimm2, 0, 0) << 1; return d;
                 default: return d;
                 }
-            case 5: d.op = OP_ESC_FP; return d;
+            case 5: d.op = OP_c_fsd; d.rs2 = (uint8_t)rp2; D_RS1(rp1); d.imm = (cimm3 << 3) | (cimm2 << 6); return d;
             case 6: d.op = OP_c_sw; D_RS1(rp1); D_RS2(rp2);
                 d.imm = (fbits(cimm2, 1, 1) << 2) | (cimm3 << 3) | (fbits(cimm2, 0, 0) << 6); return d;
             default: d.op = OP_c_sd; D_RS1(rp1); D_RS2(rp2); d.imm = (cimm3 << 3) | (cimm2 << 6); return d;
@@ -141,7 +147,8 @@ __device__ inline Dec rv_decode_tree(uint32_t raw) {
         }
         switch (cop) {  // q == 2
         case 0: d.op = OP_c_slli; D_RD(rc1); D_RS1(rc1); d.imm = cimm5 | (cimm1 << 5); return d;
-        case 1: d.op = OP_ESC_FP; return d;
+        case 1: d.op = OP_c_fldsp; d.rd = (uint8_t)rc1; D_RS1(2);
+            d.imm = (fbits(cimm5, 4, 3) << 3) | (cimm1 << 5) | (fbits(cimm5, 2, 0) << 6); return d;
         case 2: d.op = OP_c_lwsp; D_RD(rc1); D_RS1(2);
             d.imm = (fbits(cimm5, 4, 2) << 2) | (cimm1 << 5) | (fbits(cimm5, 1, 0) << 6); return d;
         case 3: d.op = OP_c_ldsp; D_RD(rc1); D_RS1(2);
@@ -155,7 +162,8 @@ __device__ inline Dec rv_decode_tree(uint32_t raw) {
                 else { d.op = OP_c_jalr; D_RD(1); D_RS1(rc1); }
             } else { d.op = OP_c_add; D_RD(rc1); D_RS1(rc1); D_RS2(rc2); }
             return d;
-        case 5: d.op = OP_ESC_FP; return d;
+        case 5: d.op = OP_c_fsdsp; d.rs2 = (uint8_t)rc2; D_RS1(2);
+            d.imm = (fbits(cimm6, 5, 3) << 3) | (fbits(cimm6, 2, 0) << 6); return d;
         case 6: d.op = OP_c_swsp; D_RS1(2); D_RS2(rc2); d.imm = (fbits(cimm6, 5, 2) << 2) | (fbits(cimm6, 1, 0) << 6); return d;
         default: d.op = OP_c_sdsp; D_RS1(2); D_RS2(rc2); d.imm = (fbits(cimm6, 5, 3) << 3) | (fbits(cimm6, 2, 0) << 6); return d;
         }
@@ -366,11 +374,56 @@ __device__ inline bool gem5_known(uint32_t raw) {
     return false;
 }
 
+// The executed members of the LOAD-FP / STORE-FP / OP-FP / AMO groups among
+// the encodings gem5 knows (decoder.isa:567-591, :1741-1763, :2067-2283,
+// :2896-2942, :3500-3548, :3593-3598, :3648-3652).  FP register indices sit in
+// rd / rs1 / rs2 WITHOUT the integer-register flags (liveness and the replica
+// watch only see integer operands).
+__device__ inline void rv_refine_fp_amo(uint32_t raw, Dec &d) {
+    const uint32_t opc = fbits(raw, 6, 2), f3 = fbits(raw, 14, 12), f7 = fbits(raw, 31, 25);
+    const uint32_t rd = fbits(raw, 11, 7), rs1 = fbits(raw, 19, 15), rs2 = fbits(raw, 24, 20);
+    if (opc == 0x01 && f3 >= 1 && f3 <= 3) {
+        d.op = (uint8_t)(OP_flh + f3 - 1); d.rd = (uint8_t)rd; D_RS1(rs1); d.imm = fsext(fbits(raw, 31, 20), 12);
+        return;
+    }
+    if (opc == 0x09 && f3 >= 1 && f3 <= 3) {
+        d.op = (uint8_t)(OP_fsh + f3 - 1); d.rs2 = (uint8_t)rs2; D_RS1(rs1);
+        d.imm = fsext((fbits(raw, 31, 25) << 5) | fbits(raw, 11, 7), 12);
+        return;
+    }
+    if (opc == 0x0b && (f3 == 2 || f3 == 3)) {
+        int o;
+        switch (fbits(raw, 31, 27)) {
+        case 0x00: o = OP_amoadd_w; break;  case 0x01: o = OP_amoswap_w; break; case 0x04: o = OP_amoxor_w; break;
+        case 0x08: o = OP_amoor_w; break;   case 0x0c: o = OP_amoand_w; break;  case 0x10: o = OP_amomin_w; break;
+        case 0x14: o = OP_amomax_w; break;  case 0x18: o = OP_amominu_w; break; case 0x1c: o = OP_amomaxu_w; break;
+        default: return;   // lr / sc stay escapes
+        }
+        d.op = (uint8_t)(f3 == 2 ? o : o + (OP_amoadd_d - OP_amoadd_w));
+        D_RD(rd); D_RS1(rs1); D_RS2(rs2); d.imm = 0;
+        return;
+    }
+    if (opc != 0x14) return;
+    if ((f7 == 0x10 || f7 == 0x11 || f7 == 0x12) && f3 <= 2) {
+        d.op = (uint8_t)((f7 == 0x10 ? OP_fsgnj_s : f7 == 0x11 ? OP_fsgnj_d : OP_fsgnj_h) + f3);
+        d.rd = (uint8_t)rd; d.rs1 = (uint8_t)rs1; d.rs2 = (uint8_t)rs2;
+        return;
+    }
+    if (f7 == 0x70 && f3 <= 1) { d.op = f3 ? OP_fclass_s : OP_fmv_x_w; D_RD(rd); d.rs1 = (uint8_t)rs1; return; }
+    if (f7 == 0x71 && f3 == 1) { d.op = OP_fclass_d; D_RD(rd); d.rs1 = (uint8_t)rs1; return; }
+    if (f7 == 0x71 && f3 == 0 && rs2 == 0) { d.op = OP_fmv_x_d; D_RD(rd); d.rs1 = (uint8_t)rs1; return; }
+    if (f7 == 0x72 && f3 <= 1) { d.op = f3 ? OP_fclass_h : OP_fmv_x_h; D_RD(rd); d.rs1 = (uint8_t)rs1; return; }
+    if (f7 == 0x78 && f3 == 0 && rs2 == 0) { d.op = OP_fmv_w_x; d.rd = (uint8_t)rd; D_RS1(rs1); return; }
+    if (f7 == 0x79 && rs2 == 0) { d.op = OP_fmv_d_x; d.rd = (uint8_t)rd; D_RS1(rs1); return; }
+    if (f7 == 0x7a && rs2 == 0) { d.op = OP_fmv_h_x; d.rd = (uint8_t)rd; D_RS1(rs1); return; }
+}
+
 __device__ inline Dec rv_decode(uint32_t raw) {
     Dec d = rv_decode_tree(raw);
     if ((raw & 3) == 3 && (d.op == OP_ESC_FP || d.op == OP_ESC_VEC || d.op == OP_ESC_AMO ||
                            d.op == OP_ESC_SYS || d.op == OP_ESC_HYP) && !gem5_known(raw))
         d.op = OP_UNKNOWN;
+    if ((raw & 3) == 3 && (d.op == OP_ESC_FP || d.op == OP_ESC_AMO)) rv_refine_fp_amo(raw, d);
     return d;
 }
 #undef D_RD

@@ -66,7 +66,8 @@ class EngineError(RuntimeError):
 class _Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("private_pages", C.c_uint32), ("hang_factor_x16", C.c_uint32),
                 ("max_trials_per_launch", C.c_uint32), ("snapshot_interval", C.c_uint32), ("flags", C.c_uint32),
-                ("epoch_iters", C.c_uint32), ("lanes_per_wave", C.c_uint32)]
+                ("epoch_iters", C.c_uint32), ("lanes_per_wave", C.c_uint32),
+                ("resume_lanes", C.c_uint32), ("epochs", C.c_uint32)]
 
 
 CFG_NO_SNAPSHOT_START = 1
@@ -150,10 +151,11 @@ class Engine:
 
     def __init__(self, device: int = 0, private_pages: int = 16, hang_factor_x16: int = 32,
                  max_trials_per_launch: int = 65536, snapshot_interval: int = 0, flags: int = 0,
-                 epoch_iters: int = 0, lanes_per_wave: int = 0):
+                 epoch_iters: int = 0, lanes_per_wave: int = 0, resume_lanes: int = 0,
+                 epochs: int = 0):
         self.L = lib()
         cfg = _Config(device, private_pages, hang_factor_x16, max_trials_per_launch, snapshot_interval, flags,
-                      epoch_iters, lanes_per_wave)
+                      epoch_iters, lanes_per_wave, resume_lanes, epochs)
         h = C.c_void_p()
         st = self.L.fi_create(C.byref(cfg), C.byref(h))
         if st == FI_E_NODEVICE:

@@ -102,6 +102,8 @@ def test_sampler_matches_oracle(engine_factory, oracle_mod, name):
     ("qsort", MEM, 4, 3000),              # C4 bursts
     ("qsort", REGS | PC | MEM, 8, 2000),
     ("intmix", REGS | PC, 1, 600),        # C3 kernel (sampled)
+    ("fpamo", REGS | PC | MEM, 1, 4000),  # F/D data movement + AMOs (the golden run has FP state)
+    ("fpamo", REGS | PC, 3, 2000),
 ])
 def test_trials_bit_exact(engine_factory, oracle_mod, name, structs, burst, n):
     e = engine_factory(name)

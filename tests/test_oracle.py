@@ -51,7 +51,100 @@ def ref_intmix():
     return b"%016x\n" % t
 
 
-EXPECTED = {"hello": b"Hello world!\n", "crc32": ref_crc32(), "qsort": ref_qsort(), "intmix": ref_intmix()}
+def _fclass(ui, eb, fb):
+    """RISC-V fclass bit (the ISA manual's table), from the raw encoding"""
+    e, f, s = (ui >> fb) & ((1 << eb) - 1), ui & ((1 << fb) - 1), (ui >> (eb + fb)) & 1
+    emax = (1 << eb) - 1
+    if e == emax:
+        if f == 0:
+            return 1 << (0 if s else 7)
+        return 1 << (9 if (f >> (fb - 1)) & 1 else 8)
+    if e == 0:
+        return 1 << ((3 if s else 4) if f == 0 else (2 if s else 5))
+    return 1 << (1 if s else 6)
+
+
+def ref_fpamo():
+    """workloads/fpamo.s: F/D/Zfh moves + AMOs folded into an FNV-style hash"""
+    h = 0x1234567
+
+    def mix(v):
+        nonlocal h
+        h = ((h ^ (v % M64)) * 0x100000001B3) % M64
+
+    sx = lambda v, n: (v & ((1 << n) - 1)) - ((v >> (n - 1) & 1) << n)  # noqa: E731
+    box32 = lambda v: 0xFFFFFFFF00000000 | (v & 0xFFFFFFFF)  # noqa: E731
+    unbox32 = lambda v: v & 0xFFFFFFFF if v >> 32 == 0xFFFFFFFF else 0x7FC00000  # noqa: E731
+    S = 1 << 63
+    dvals = [0x3ff0000000000000, 0xbff8000000000000, 0x7ff0000000000000, 0x1,
+             0x7ff4000000000000, 0x8000000000000000, 0x7ff8000000000000, 0xffefffffffffffff]
+    f1 = 0
+    for d in dvals:
+        f1 = d
+        mix(_fclass(d, 11, 52))
+        f2 = (d & ~S) | (~d & S)
+        mix(f2)
+        f3 = (d & ~S) | ((d ^ f2) & S)
+        mix(f3)
+        x = unbox32(d)
+        mix(sx(box32(x) & 0xFFFFFFFF, 32))
+    fvals = [0x3f800000, 0xff800000, 0x7fa00000, 0x80000001]
+    for v in fvals:
+        f5 = box32(v)
+        mix(_fclass(v, 8, 23))
+        mix(sx(v & 0x7FFFFFFF, 32))
+        a0 = sx(v, 32) % M64
+        mix(a0)
+        mix(box32(a0))
+    f5 = box32(fvals[-1])
+    f8 = 0xFFFFFFFFFFFF0000 | 0x3c00
+    mix(_fclass(0x3c00, 5, 10))
+    mix(0x3c00)
+    mix(0xFFFFFFFFFFFF0000 | 0xbc00)
+    mem = bytearray(struct.pack("<QQQQQ", 0x0123456789abcdef, 0xfedcba9876543210, 0x0000000500000005, 0, 0))
+
+    def amo(off, size, fn):
+        old = int.from_bytes(mem[off:off + size], "little")
+        new = fn(old) % (1 << (8 * size))
+        mem[off:off + size] = new.to_bytes(size, "little")
+        return sx(old, 32) % M64 if size == 4 else old
+
+    s32 = lambda v: sx(v, 32)  # noqa: E731
+    s64 = lambda v: sx(v, 64)  # noqa: E731
+    mix(amo(0, 4, lambda m: m + 0x11))
+    b = -5 % M64
+    mix(amo(0, 4, lambda m: b if s32(b) < s32(m) else m))
+    mix(amo(0, 4, lambda m: max(b & 0xFFFFFFFF, m)))
+    b = 0x0f0f
+    mix(amo(8, 8, lambda m: m ^ b))
+    mix(amo(8, 8, lambda m: m | b))
+    mix(amo(8, 8, lambda m: m & b))
+    mix(amo(8, 8, lambda m: 7))
+    b = -9 % M64
+    mix(amo(8, 8, lambda m: b if s64(b) > s64(m) else m))
+    mix(amo(8, 8, lambda m: min(b, m)))
+    mix(amo(8, 8, lambda m: b if s64(b) < s64(m) else m))
+    b = 3
+    mix(amo(17, 4, lambda m: m + b))
+    amo(17, 4, lambda m: b)
+    mix(amo(17, 4, lambda m: b if s32(b) > s32(m) else m))
+    mix(amo(17, 4, lambda m: min(b, m)))
+    mix(amo(17, 4, lambda m: m | b))
+    mix(amo(17, 4, lambda m: m & b))
+    mix(amo(17, 4, lambda m: m ^ b))
+    for off in (0, 8, 16):
+        mix(int.from_bytes(mem[off:off + 8], "little"))
+    mem[24:32] = f1.to_bytes(8, "little")
+    mem[32:36] = (f5 & 0xFFFFFFFF).to_bytes(4, "little")
+    mem[36:38] = (f8 & 0xFFFF).to_bytes(2, "little")
+    mix(int.from_bytes(mem[24:32], "little"))
+    mix(int.from_bytes(mem[32:40], "little"))
+    mix(0xFFFFFFFFFFFF0000 | int.from_bytes(mem[36:38], "little"))
+    return b"%016x\n" % h
+
+
+EXPECTED = {"hello": b"Hello world!\n", "crc32": ref_crc32(), "qsort": ref_qsort(), "intmix": ref_intmix(),
+            "fpamo": ref_fpamo()}
 
 
 @pytest.mark.parametrize("name", list(EXPECTED))

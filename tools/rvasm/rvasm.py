@@ -37,6 +37,20 @@ REG_ALIASES = {
 for _i in range(32):
     REG_ALIASES[f"x{_i}"] = _i
 
+FREG = {f"f{_i}": _i for _i in range(32)}
+FREG.update({n: i for i, n in enumerate(
+    ["ft0", "ft1", "ft2", "ft3", "ft4", "ft5", "ft6", "ft7", "fs0", "fs1", "fa0", "fa1", "fa2", "fa3", "fa4",
+     "fa5", "fa6", "fa7", "fs2", "fs3", "fs4", "fs5", "fs6", "fs7", "fs8", "fs9", "fs10", "fs11", "ft8", "ft9",
+     "ft10", "ft11"])})
+
+
+def freg(tok: str) -> int:
+    tok = tok.strip()
+    if tok not in FREG:
+        raise AsmError(f"bad FP register {tok!r}")
+    return FREG[tok]
+
+
 TEXT_BASE = 0x10000
 PAGE = 0x1000
 
@@ -129,6 +143,29 @@ SHIFT_OPS = {  # name: (opcode, funct3, funct6/7 high bits, shamt bits)
 LOADS = {"lb": 0, "lh": 1, "lw": 2, "ld": 3, "lbu": 4, "lhu": 5, "lwu": 6}
 STORES = {"sb": 0, "sh": 1, "sw": 2, "sd": 3}
 BRANCHES = {"beq": 0, "bne": 1, "blt": 4, "bge": 5, "bltu": 6, "bgeu": 7}
+# F/D/Zfh subset without rounding: loads/stores, moves, sign injection, classify
+FLOADS = {"flh": 1, "flw": 2, "fld": 3}
+FSTORES = {"fsh": 1, "fsw": 2, "fsd": 3}
+F_RR = {  # name: (funct7, funct3) -- fd, fs1, fs2
+    "fsgnj.s": (0x10, 0), "fsgnjn.s": (0x10, 1), "fsgnjx.s": (0x10, 2),
+    "fsgnj.d": (0x11, 0), "fsgnjn.d": (0x11, 1), "fsgnjx.d": (0x11, 2),
+    "fsgnj.h": (0x12, 0), "fsgnjn.h": (0x12, 1), "fsgnjx.h": (0x12, 2)}
+F_TO_X = {"fmv.x.w": (0x70, 0), "fclass.s": (0x70, 1), "fmv.x.d": (0x71, 0), "fclass.d": (0x71, 1),
+          "fmv.x.h": (0x72, 0), "fclass.h": (0x72, 1)}   # rd, fs1
+X_TO_F = {"fmv.w.x": 0x78, "fmv.d.x": 0x79, "fmv.h.x": 0x7A}   # fd, rs1
+AMO_F5 = {"amoadd": 0x00, "amoswap": 0x01, "lr": 0x02, "sc": 0x03, "amoxor": 0x04, "amoor": 0x08, "amoand": 0x0C,
+          "amomin": 0x10, "amomax": 0x14, "amominu": 0x18, "amomaxu": 0x1C}
+
+
+def amo_parse(name):
+    """amoadd.w / amoswap.d.aqrl / lr.w.aq -> (funct5, funct3, aq, rl) or None"""
+    p = name.split(".")
+    if len(p) < 2 or p[0] not in AMO_F5 or p[1] not in ("w", "d"):
+        return None
+    sfx = p[2] if len(p) > 2 else ""
+    if sfx not in ("", "aq", "rl", "aqrl"):
+        return None
+    return AMO_F5[p[0]], 2 if p[1] == "w" else 3, int("aq" in sfx), int("rl" in sfx)
 
 
 # ---------------------------------------------------------------- compressed encodings
@@ -229,6 +266,15 @@ def try_compress(name, ops):
                 return (f3 << 13) | (((off >> 3) & 7) << 10) | ((base - 8) << 7) | (((off >> 2) & 1) << 6) | \
                     (((off >> 6) & 1) << 5) | ((r - 8) << 2)
         return None
+    if name in ("fld", "fsd"):
+        # c.fld / c.fsd / c.fldsp / c.fsdsp: the c.ld / c.sd layouts with funct3 1 / 5
+        r, off, base = ops
+        c = try_compress("ld" if name == "fld" else "sd", (max(r, 1) if base == 2 else r, off, base))
+        if c is None:
+            return None
+        if base == 2 and name == "fld":
+            c = (c & ~(0x1F << 7)) | (r << 7)
+        return (c & 0x1FFF) | ((1 if name == "fld" else 5) << 13)
     if name == "jalr":
         rd, rs1, imm = ops
         if imm == 0 and rs1 != 0 and rd in (0, 1):
@@ -422,6 +468,23 @@ class Assembler:
             return [(n, (reg(a[0]), parse_int(a[1]), reg(a[2])))]
         if n == ".insn16" or n == ".insn32":
             return [(n, (parse_int(a[0]),))]
+        if n in FLOADS or n in FSTORES:
+            off, base = parse_mem(a[1])
+            return [(n, (freg(a[0]), parse_int(off), base))]
+        if n in F_RR:
+            return [(n, (freg(a[0]), freg(a[1]), freg(a[2])))]
+        if n in F_TO_X:
+            return [(n, (reg(a[0]), freg(a[1])))]
+        if n in X_TO_F:
+            return [(n, (freg(a[0]), reg(a[1])))]
+        if amo_parse(n) is not None:
+            # amoadd.w rd, rs2, (rs1)   lr.w rd, (rs1)
+            f5 = amo_parse(n)[0]
+            if f5 == 0x02:
+                _, base = parse_mem(a[1])
+                return [(n, (reg(a[0]), 0, base))]
+            _, base = parse_mem(a[2])
+            return [(n, (reg(a[0]), reg(a[1]), base))]
         raise AsmError(f"line {it.line}: unknown instruction {n!r}")
 
     @staticmethod
@@ -563,6 +626,24 @@ class Assembler:
             w = 0x0FF0000F
         elif name == "fence.i":
             w = 0x0000100F
+        elif name in FLOADS:
+            fd, off, base = ops
+            w = enc_i(0x07, FLOADS[name], fd, base, off)
+        elif name in FSTORES:
+            fs2, off, base = ops
+            w = enc_s(0x27, FSTORES[name], base, fs2, off)
+        elif name in F_RR:
+            f7, f3 = F_RR[name]
+            w = enc_r(0x53, f3, f7, *ops)
+        elif name in F_TO_X:
+            f7, f3 = F_TO_X[name]
+            w = enc_r(0x53, f3, f7, ops[0], ops[1], 0)
+        elif name in X_TO_F:
+            w = enc_r(0x53, 0, X_TO_F[name], ops[0], ops[1], 0)
+        elif amo_parse(name) is not None:
+            f5, f3, aq, rl = amo_parse(name)
+            rd, rs2, base = ops
+            w = enc_r(0x2F, f3, (f5 << 2) | (aq << 1) | rl, rd, base, rs2)
         elif name in ("csrrw", "csrrs", "csrrc"):
             rd, csr, rs1 = ops
             w = (csr << 20) | (rs1 << 15) | ({"csrrw": 1, "csrrs": 2, "csrrc": 3}[name] << 12) | (rd << 7) | 0x73
