@@ -314,6 +314,11 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
               (unsigned long long)pc0);
         g.put("  if (wst + %uu > wbud || TXB(mine && rem - lst < %uu)) { spc = 0x%llxULL; goto tx_out; }\n", n, n,
               (unsigned long long)pc0);
+        {   // a lane that rewrote one of this block's instruction bytes leaves before it
+            const uint64_t blo = pc0 & ~3ULL, bhi = g.pc_of(insts.empty() ? h0 : insts.back()) + 6;
+            g.put("  if (wdirty && TXB(mine && ldlo < 0x%llxULL && ldhi > 0x%llxULL)) { spc = 0x%llxULL; goto tx_out; }\n",
+                  (unsigned long long)bhi, (unsigned long long)blo, (unsigned long long)pc0);
+        }
         uint32_t k_st = 0, k_xt = 0, k_fb = 0, k_db = 0;   // committed so far in this block
         auto commit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
             // per-lane counters of the running lanes (zero terms omitted), wave iterations

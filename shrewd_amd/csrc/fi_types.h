@@ -58,7 +58,8 @@ struct LaneSave {
     uint64_t pc, ninst, ncyc, out_pos, err_pos, stack_min, next_chk;
     int32_t watch;
     uint32_t nfail, n_priv, snap_j;
-    uint32_t flags;                  // bit 0 out_bad, bits 1-2 injected, bit 3 code_dirty
+    uint32_t flags;                  // bit 0 out_bad, bits 1-2 injected, bit 3 code_dirty, bit 4 FP state
+    uint32_t dlo, dhi;               // rewritten code bytes [code_lo + dlo, code_lo + dhi) (if code_dirty)
     uint32_t pad;
 };
 

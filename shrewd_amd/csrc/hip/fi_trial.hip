@@ -105,7 +105,19 @@ struct LaneMem {
     uint64_t req_vpn;              // pending copy-on-write, kNone = none
     const uint8_t *req_src;
     bool code_dirty;
+    uint64_t dlo, dhi;             // bounding range of the code bytes the lane rewrote (valid if code_dirty)
 };
+
+// The golden pre-decode of the instruction at pc is stale for this lane only if
+// the lane rewrote one of its bytes (conservatively [pc & ~3, pc + 6)).
+__device__ __forceinline__ bool dirty_at(const LaneMem &m, uint64_t pc) {
+    return m.code_dirty && (pc & ~3ULL) < m.dhi && pc + 6 > m.dlo;
+}
+__device__ __forceinline__ void mark_dirty(LaneMem &m, uint64_t lo, uint64_t hi) {
+    m.dlo = m.code_dirty ? (lo < m.dlo ? lo : m.dlo) : lo;
+    m.dhi = m.code_dirty ? (hi > m.dhi ? hi : m.dhi) : hi;
+    m.code_dirty = true;
+}
 
 // The lane's start-snapshot page table (uniform in a fresh launch; per lane
 // after a resume).
@@ -196,7 +208,7 @@ __device__ int mem_access(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, 
     if (wr) {
         if (!(p1 & 1)) { m.req_vpn = ea >> 12; m.req_src = page_of(p1); return F_NEEDPAGE; }
         if (!(p2 & 1)) { m.req_vpn = ea2 >> 12; m.req_src = page_of(p2); return F_NEEDPAGE; }
-        if (ea < c->code_hi && ea + size > c->code_lo) m.code_dirty = true;   // the lane rewrote its code
+        if (ea < c->code_hi && ea + size > c->code_lo) mark_dirty(m, ea, ea + size);   // the lane rewrote its code
         uint8_t *w1 = const_cast<uint8_t *>(page_of(p1));
         if (n1 == size && (off & (size - 1)) == 0) {
             switch (size) {
@@ -608,11 +620,13 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     tlb_flush(m);
     m.tp0 = m.tp1 = m.tp2 = m.tp3 = 0;
     m.tnext = 0; m.n_priv = 0; m.req_vpn = kNone; m.req_src = nullptr; m.code_dirty = false;
+    m.dlo = m.dhi = 0;
     if (resume && live) {
         L.pc = SV->pc; L.ninst = SV->ninst; L.ncyc = SV->ncyc; L.out_pos = SV->out_pos; L.err_pos = SV->err_pos;
         L.next_chk = SV->next_chk; L.nfail = SV->nfail; L.watch = SV->watch;
         L.out_bad = SV->flags & 1; L.injected = (uint8_t)((SV->flags >> 1) & 3); L.fp = (SV->flags >> 4) & 1;
         m.stack_min = SV->stack_min; m.n_priv = SV->n_priv; m.code_dirty = (SV->flags >> 3) & 1;
+        m.dlo = CX->code_lo + SV->dlo; m.dhi = CX->code_lo + SV->dhi;
     }
     bool suspended = false;
     const uint64_t start_inst = (live && !resume) ? L.ninst : 0;
@@ -638,6 +652,8 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 sv->pc = L.pc; sv->ninst = L.ninst; sv->ncyc = L.ncyc; sv->out_pos = L.out_pos; sv->err_pos = L.err_pos;
                 sv->stack_min = m.stack_min; sv->next_chk = L.next_chk; sv->watch = L.watch; sv->nfail = L.nfail;
                 sv->n_priv = m.n_priv; sv->snap_j = j;
+                sv->dlo = m.code_dirty ? (uint32_t)(m.dlo > CX->code_lo ? m.dlo - CX->code_lo : 0) : 0;
+                sv->dhi = m.code_dirty ? (uint32_t)((m.dhi < CX->code_hi ? m.dhi : CX->code_hi) - CX->code_lo) : 0;
                 sv->flags = (L.out_bad ? 1u : 0u) | ((uint32_t)L.injected << 1) | (m.code_dirty ? 8u : 0u) |
                             (L.fp ? 16u : 0u);
                 CX->surv[atomicAdd(CX->surv_n, 1u)] = (uint32_t)slot;
@@ -695,7 +711,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 } else {
                     uint64_t *wp = (uint64_t *)(const_cast<uint8_t *>(page_of(p)) + (s.addr & 4095));
                     *wp ^= s.mask;
-                    if (s.addr < CX->code_hi && s.addr + 8 > CX->code_lo) m.code_dirty = true;
+                    if (s.addr < CX->code_hi && s.addr + 8 > CX->code_lo) mark_dirty(m, s.addr, s.addr + 8);
                     L.injected = 1;
                 }
             } else {
@@ -823,7 +839,10 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
             const PreRef E0 = pre_entry(tx, lpc);
             if (!(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader) &&
-                __ballot(mine && (m.code_dirty || L.watch > 0)) == 0) {
+                __ballot(mine && L.watch > 0) == 0) {
+                // lanes that rewrote code: every block checks its bytes against their range
+                const bool wdirty = uni32(__ballot(m.code_dirty) != 0);
+                const uint64_t ldlo = m.code_dirty ? m.dlo : kNone, ldhi = m.code_dirty ? m.dhi : 0;
                 const uint64_t gm = __ballot(mine);      // the entry group
                 uint64_t gmr = gm;                        // the running group
                 uint64_t pend = 0, pmin = kNone;          // parked lanes, their lowest pc
@@ -900,7 +919,9 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         // (K_SLOW op, fault, page request, syscall).  Nothing commits unless the
         // whole instruction commits for every group lane.
         if (CX->pre_ok && lpc >= CX->text_lo && lpc < CX->text_hi &&
-            __ballot(mine && (m.code_dirty || L.watch > 0)) == 0) {
+            __ballot(mine && L.watch > 0) == 0) {
+            // lanes that rewrote code run here too, until they reach a rewritten instruction
+            const bool any_dirty = __ballot(mine && m.code_dirty) != 0;
             const uint64_t gm = __ballot(mine);
             const int glane = __ffsll((unsigned long long)gm) - 1;
             uint64_t budget64 = uni64(wave_min64(mine ? next_ev - L.ninst : kNone));
@@ -919,6 +940,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 const uint32_t q1 = uni32(E.e.y), q2 = uni32(E.e.z), q3 = uni32(E.e.w);
                 const uint32_t aux = q3 >> 16, kind = aux & 63;
                 if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
+                if (any_dirty && __ballot(mine && dirty_at(m, spc)) != 0) break;
 #ifdef FI_TX
                 if (steps && ((q3 >> 8) & kPreLeader)) break;   // translated blocks take over here
 #endif
@@ -1063,7 +1085,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         uint32_t ticks = 1;
         bool fast = false;
         const uint64_t key = (lpc & 3) ? ((lpc & ~3ULL) | 2) : lpc;
-        if (CX->pre_ok && key >= CX->text_lo && key < CX->text_hi && __ballot(mine && m.code_dirty) == 0) {
+        if (CX->pre_ok && key >= CX->text_lo && key < CX->text_hi && __ballot(mine && dirty_at(m, lpc)) == 0) {
             const Pre4 q = pre_load(CX->pre + ((key - CX->text_lo) >> 1));
             const uint32_t pflags = (q.w >> 8) & 0xFF;
             if (pflags & kPreValid) {
@@ -1415,7 +1437,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             const PreRef En = pre_entry(tn, npc0);
             const uint32_t wn = uni32(En.e.w);
             if (En.in && ((wn >> 8) & kPreValid) && ((wn >> 16) & 63) != K_SLOW &&
-                __ballot(cont && (m.code_dirty || L.watch > 0)) == 0)
+                __ballot(cont && (dirty_at(m, npc0) || L.watch > 0)) == 0)
                 break;
         }
         lpc = npc0;

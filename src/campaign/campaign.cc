@@ -18,7 +18,7 @@ namespace {
 
 const char *kClass[FI_N_CLASS] = {"masked", "sdc", "crash", "hang", "detected", "escape"};
 const char *kCrash[] = {"", "unknown_inst", "illegal_inst", "page_fault", "syscall_range", "syscall_unimpl",
-                        "proxy", "fd_assert", "sigtrap", "stack_limit"};
+                        "proxy", "fd_assert", "sigtrap", "stack_limit", "amo_line"};
 const char *kEscape[] = {"", "inst", "syscall", "csr", "host", "resource"};
 
 void check(fi_engine *e, fi_status s, const char *what) {
@@ -161,7 +161,7 @@ std::string Campaign::summaryJson() const {
     for (int c = 0; c < FI_N_CLASS; c++) o << ", \"" << kClass[c] << "\": " << cls[c];
     o << ", \"crash_sub\": {";
     bool first = true;
-    for (int i = 1; i < 10; i++)
+    for (int i = 1; i < 11; i++)
         if (hist_.crash_sub[i]) { o << (first ? "" : ", ") << "\"" << kCrash[i] << "\": " << hist_.crash_sub[i]; first = false; }
     o << "}, \"escape_sub\": {";
     first = true;

@@ -118,6 +118,21 @@ def test_trials_bit_exact(engine_factory, oracle_mod, name, structs, burst, n):
     assert int(hist["counts"].sum()) == n
 
 
+def test_rewritten_code_bit_exact(engine_factory, oracle_mod):
+    """Trials whose stores land in the text (a flipped pointer in crc32's fill
+    loop): pre-decoded and translated code stay in use for every instruction
+    whose bytes the lane did not rewrite; the rewritten ones decode from the
+    lane's own pages."""
+    e = engine_factory("crc32")
+    o = oracle_for(oracle_mod, "crc32")
+    e.set_campaign(0x5EED0003, REGS | PC, 1)
+    sites = e.sample(0, 100_000)
+    sites = sites[(sites["target"] == 7) | (sites["target"] == 8)][:4000]   # t2 / s0: the fill loop's pointers
+    dev, _ = e.run_sites(sites)
+    ref = o.run_trials(sites)
+    compare(dev, ref, sites)
+
+
 @pytest.mark.parametrize("mask", [0, (1 << 1) | (1 << 2) | (1 << 3) | (1 << 4),
                                   sum(1 << r for r in range(10, 18)), (1 << 32) - 2 | (1 << 32)])
 def test_protect_mask_bit_exact(engine_factory, oracle_mod, mask):

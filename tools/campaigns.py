@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Run the BASELINE.json campaign configs C1-C5 on one MI355X and write one
+JSON summary (profiles/TAG_campaigns.json).  Each line: trials, seconds of
+device time (sample + sort + interpreter + histogram, inputs resident),
+trials/s, outcome classes, crash/escape sub-codes.
+
+  C1 hello, 1k regfile flips
+  C2 crc32 / qsort, 100k regfile+PC single-bit trials
+  C3 intmix, one GPU's shard of the 1M-trial 8-GPU campaign (125k trials)
+  C4 memory-word faults, bursts k = 1, 2, 4, 8 (copy-on-write guest pages)
+  C5 SHREWD selective-replication sweep on crc32: protected register masks vs
+     residual SDC rate (a fault on a protected register that is read before
+     being overwritten is detected-by-replica)
+python tools/campaigns.py [TAG]
+"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from shrewd_amd import Engine  # noqa: E402
+from shrewd_amd.fi import CLASS_NAMES, CRASH_NAMES, ESCAPE_NAMES  # noqa: E402
+
+REGS = (1 << 32) - 2
+PC = 1 << 32
+MEM = 1 << 33
+# ABI register groups (x-register numbers)
+MASKS = {"none": 0, "sp_ra_gp_tp": (1 << 1) | (1 << 2) | (1 << 3) | (1 << 4),
+         "a0-a7": sum(1 << r for r in range(10, 18)),
+         "s0-s11": sum(1 << r for r in (8, 9, *range(18, 28))),
+         "t0-t6": sum(1 << r for r in (5, 6, 7, 28, 29, 30, 31)),
+         "all+pc": REGS | PC}
+
+_engines = {}
+
+
+def engine(name):
+    if name not in _engines:
+        e = Engine(max_trials_per_launch=131072)
+        e.load_elf(open(os.path.join(ROOT, "workloads", f"{name}.elf"), "rb").read(), [name])
+        e.golden_run()
+        _engines[name] = e
+    return _engines[name]
+
+
+def run(cfg, name, n, structs, burst=1, protect=0, seed=0x5EED0003):
+    e = engine(name)
+    e.set_campaign(seed, structs, burst)
+    e.set_protect(protect)
+    e.run_trials(0, n)   # warm: code objects and work buffers sized for n
+    t0 = time.perf_counter()
+    out, h = e.run_trials(0, n)
+    dt = time.perf_counter() - t0
+    e.set_protect(0)
+    cls = h["counts"].sum(axis=(0, 1))
+    rec = {"config": cfg, "workload": name, "golden_ninst": int(e.golden.ninst), "trials": n,
+           "structures": hex(structs), "burst": burst, "protect_mask": hex(protect), "seconds": dt,
+           "trials_per_s": n / dt, **{CLASS_NAMES[i]: int(cls[i]) for i in range(6)},
+           "crash_sub": {CRASH_NAMES.get(i, str(i)): int(h["crash_sub"][i]) for i in range(16) if h["crash_sub"][i]},
+           "escape_sub": {ESCAPE_NAMES.get(i, str(i)): int(h["escape_sub"][i]) for i in range(8)
+                          if h["escape_sub"][i]},
+           "sdc_rate": int(cls[1]) / n}
+    print(json.dumps(rec), flush=True)
+    return rec, out
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    recs = []
+    # C1 (its bit-exactness against the oracle: tests/test_gpu_parity.py)
+    recs.append(run("C1", "hello", 1000, REGS, seed=0x5EED0001)[0])
+    for w in ("crc32", "qsort"):
+        recs.append(run("C2", w, 100_000, REGS | PC)[0])
+    recs.append(run("C3", "intmix", 125_000, REGS | PC)[0])
+    for w in ("crc32", "qsort"):
+        for k in (1, 2, 4, 8):
+            recs.append(run("C4", w, 100_000, MEM, burst=k)[0])
+    for label, m in MASKS.items():
+        r = run("C5", "crc32", 100_000, REGS | PC, protect=m)[0]
+        r["mask_name"] = label
+        recs.append(r)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", f"{tag}_campaigns.json"), "w") as f:
+        json.dump(recs, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -19,6 +19,7 @@ ap.add_argument("--trials", type=int, nargs="*", default=[64, 6400, 100000])
 ap.add_argument("--flags", type=int, default=0)
 ap.add_argument("--interval", type=int, default=0)
 ap.add_argument("--epoch", type=int, default=0)
+ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
 ap.add_argument("--converged", action="store_true", help="also time one converged wave from process start")
 a = ap.parse_args()
 name = a.workload
@@ -40,7 +41,7 @@ with open(f"gpurun_out/tx_{name}.inc", "w") as f:
     f.write(e.debug_translation())
 _pre, _tr, _lo = e.debug_golden_trace()
 np.savez(f"gpurun_out/golden_{name}.npz", pre=_pre, trace=_tr, text_lo=np.uint64(_lo))
-e.set_campaign(0x5EED0002, REGS_PC, 1)
+e.set_campaign(a.seed, REGS_PC, 1)
 for n in a.trials:
     sites = e.sample(0, n)
     nofault = sites.copy(); nofault["inst"] = 1 << 40
