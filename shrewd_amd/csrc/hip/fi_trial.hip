@@ -635,7 +635,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     uint32_t snaps_taken = 0;
     uint32_t tpos = 0;   // record mode: golden trace events so far (uniform)
 #ifdef FI_PROF
-    uint64_t pacc[4] = {0, 0, 0, 0};
+    uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t plast = __builtin_amdgcn_s_memtime();
 #endif
     uint32_t n_iter = 0, n_slow = 0, n_min = 0, n_exec = 0, n_chk = 0, n_early = 0;   // per-wave (uniform)
@@ -1097,6 +1097,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             }
         }
         if (!fast) {
+            PSTAMP(4);
             n_slow++;
             uint32_t raw = 0, t = 1;
             uint64_t fva = 0;
@@ -1122,8 +1123,13 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             const uint32_t lraw = (uint32_t)__builtin_amdgcn_readlane((int)raw, ld);
             const uint32_t lt = (uint32_t)__builtin_amdgcn_readlane((int)t, ld);
             mine = mine && raw == lraw;
+            PSTAMP(5);
             d = rv_decode(lraw);
             ticks = lt;
+#ifdef FI_PROF
+            asm volatile("" :: "s"((uint32_t)d.op), "s"((uint32_t)d.imm));
+#endif
+            PSTAMP(6);
         }
         // force every decoded field into SGPRs: the op switch below must be a
         // scalar branch tree, never a per-lane waterfall
@@ -1134,7 +1140,8 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         const uint64_t gmask = __ballot(mine);
         n_exec += (uint32_t)__popcll(gmask);
         int f = F_NONE;
-        if (mine) {
+        {   // every lane evaluates the (uniform) op: the switch stays a scalar
+            // branch tree in uniform control flow; only group lanes commit
         // ---- E. execute: the generated StaticInst::execute bodies of
         // src/arch/riscv/isa/decoder.isa for the modelled subset
         const uint64_t pc = L.pc;
@@ -1153,11 +1160,10 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
 #define FREG_RD(r) (L.fp ? CX->fregs[(uint64_t)(r) * CX->n_slots + slot] : 0ULL)
         // detected-by-replica: the flipped protected register is read before
         // being overwritten (build-defined SHREWD semantics)
-        if (L.watch > 0 &&
+        const bool detect = L.watch > 0 &&
             (((d.flags & kPreRs1) && d.rs1 == L.watch) || ((d.flags & kPreRs2) && d.rs2 == L.watch) ||
-             (d.op == OP_ecall && (L.watch == 17 || (L.watch >= 10 && L.watch <= 15))))) {
-            f = F_DETECT;
-        } else {
+             (d.op == OP_ecall && (L.watch == 17 || (L.watch >= 10 && L.watch <= 15))));
+        {
             switch (d.op) {
             case OP_UNKNOWN: f = F_UNKNOWN; break;
             case OP_ESC_FP: case OP_ESC_VEC: case OP_ESC_AMO: case OP_ESC_SYS: case OP_ESC_CRYPTO: case OP_ESC_CBO:
@@ -1348,6 +1354,8 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             default: f = F_UNKNOWN; break;
             }
         }
+        if (detect) f = F_DETECT;   // the op does not execute
+        if (mine) {
         if (msz && f == F_NONE) {
             // one call site (an AMO reads, then writes, in a second pass): a
             // second inlined copy of mem_access puts the lane state in scratch
@@ -1421,7 +1429,11 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         }
         }   // fault disposition
         }   // f != F_NEEDPAGE
-        }   // mine
+        }   // mine (commit)
+        }   // execute
+#ifdef FI_PROF
+        if (!fast) PSTAMP(7);
+#endif
         // ---- stay in the inner loop? every group lane committed, none reached
         // its next event, all at one PC that is still the wave's minimum
         const bool cont = mine && f == F_NONE && L.ninst < next_ev;
@@ -1456,7 +1468,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     }
 #ifdef FI_PROF
     if (lane == 0)
-        for (int k = 0; k < 4; k++) atomicAdd(&CX->stats[24 + k], (unsigned long long)pacc[k]);
+        for (int k = 0; k < 8; k++) atomicAdd(&CX->stats[24 + k], (unsigned long long)pacc[k]);
 #endif
     if (lane == 0 && CX->wave_dbg) {
         uint64_t *wd = CX->wave_dbg + 4 * (uint64_t)blockIdx.x;

@@ -62,6 +62,7 @@ for n in a.trials:
                           "slowest": {"iters": int(st[18]) >> 32, "tx_permille": (int(st[18]) >> 20) & 0xFFF,
                                       "tx_entries": int(st[18]) & 0xFFFFF, "slow": int(st[19]) & 0xFFFFFFFF},
                           "prof_cycles_per_iter": [round(int(st[24 + k]) / max(1, int(st[6])), 1) for k in range(4)],
+                          "prof_slow_cycles_per_slow": [round(int(st[24 + k]) / max(1, int(st[8])), 1) for k in range(4, 8)],
                           "classes": np.bincount(out["cls"], minlength=6).tolist()}), flush=True)
         wv = e.debug_waves(waves).astype(np.int64)
         top = np.argsort(-wv[:, 0])[:4]
