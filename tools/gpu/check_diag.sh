@@ -10,3 +10,5 @@ timeout -k 10 300 python -u bench.py --no-cpu-baseline --seed 0x5EED0003 > gpuru
 python -c "import json;b=json.load(open('gpurun_out/bench3.json'));print('bench seed3', round(b['value']), b['ms_per_step'], b['outcomes'])"
 timeout -k 10 300 python -u bench.py --no-cpu-baseline --workload qsort --steps 2 > gpurun_out/benchq.json 2> gpurun_out/benchq.err || exit 1
 python -c "import json;b=json.load(open('gpurun_out/benchq.json'));print('bench qsort', round(b['value']), b['ms_per_step'], b['outcomes'])"
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --workload intmix --steps 1 > gpurun_out/benchi.json 2> gpurun_out/benchi.err || exit 1
+python -c "import json;b=json.load(open('gpurun_out/benchi.json'));print('bench intmix', round(b['value']), b['ms_per_step'], b['outcomes'])"
