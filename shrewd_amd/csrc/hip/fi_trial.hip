@@ -919,9 +919,12 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
         // (K_SLOW op, fault, page request, syscall).  Nothing commits unless the
         // whole instruction commits for every group lane.
         if (CX->pre_ok && lpc >= CX->text_lo && lpc < CX->text_hi &&
-            __ballot(mine && L.watch > 0) == 0) {
-            // lanes that rewrote code run here too, until they reach a rewritten instruction
+            true) {
+            // lanes that rewrote code run here too, until they reach a rewritten
+            // instruction; lanes watching a protected flipped register, until an
+            // instruction reads it (the general path classifies the detection)
             const bool any_dirty = __ballot(mine && m.code_dirty) != 0;
+            const bool any_watch = __ballot(mine && L.watch > 0) != 0;
             const uint64_t gm = __ballot(mine);
             const int glane = __ffsll((unsigned long long)gm) - 1;
             uint64_t budget64 = uni64(wave_min64(mine ? next_ev - L.ninst : kNone));
@@ -945,6 +948,12 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 if (steps && ((q3 >> 8) & kPreLeader)) break;   // translated blocks take over here
 #endif
                 const uint32_t rd = q1 >> 8 & 0xFF, rs1 = q1 >> 16 & 0xFF, rs2 = q1 >> 24;
+                if (any_watch) {
+                    const uint32_t fl = q3 >> 8;
+                    const bool rw = L.watch > 0 && (((fl & kPreRs1) && rs1 == (uint32_t)L.watch) ||
+                                                    ((fl & kPreRs2) && rs2 == (uint32_t)L.watch));
+                    if (__ballot(mine && rw) != 0) break;
+                }
                 const int64_t imm = (int32_t)q2;
                 const uint32_t len = q3 & 0xFF, straddle = ((q3 >> 8) & kPreStraddle) ? 1 : 0;
                 const uint64_t a0 = RREG(rs1), b0 = RREG(rs2);
@@ -1054,6 +1063,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 if (w32) v = sx32(v);
                 const uint32_t row = (wr && rd) ? rd : kSinkRow;
                 if (mine) RREG(row) = v;
+                if (any_watch && mine && row == (uint32_t)L.watch) L.watch = -1;   // overwritten before read
                 if (CX->record) {   // golden trace for the liveness pass (one lane, uniform)
                     if (tpos < CX->rec_trace_cap && lane == 0)
                         CX->rec_trace[tpos] = (((uint32_t)spc & ~1u) | (((uint32_t)spc & 1u) << 1)) - tx.lo >> 1;
@@ -1449,7 +1459,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             const PreRef En = pre_entry(tn, npc0);
             const uint32_t wn = uni32(En.e.w);
             if (En.in && ((wn >> 8) & kPreValid) && ((wn >> 16) & 63) != K_SLOW &&
-                __ballot(cont && (dirty_at(m, npc0) || L.watch > 0)) == 0)
+                __ballot(cont && dirty_at(m, npc0)) == 0)
                 break;
         }
         lpc = npc0;
