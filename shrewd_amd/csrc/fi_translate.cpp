@@ -15,6 +15,7 @@
 //
 // Semantics follow the interpreter's general path op for op, i.e. the
 // generated StaticInst::execute bodies of src/arch/riscv/isa/decoder.isa.
+#include <cstdlib>
 #include <cctype>
 #include <cstdarg>
 #include <cstdio>
@@ -343,6 +344,18 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
               (unsigned long long)pc0);
         g.put("  if (wst + %uu > wbud || TXB(mine && rem - lst < %uu)) { spc = 0x%llxULL; goto tx_out; }\n", n, n,
               (unsigned long long)pc0);
+        {   // a lane watching a protected flipped register this block reads or writes leaves before it
+            uint32_t rw = 0;
+            for (uint32_t hh : insts) {
+                const PreInst &p = pre[hh];
+                if ((p.flags & kPreRs1) && p.rs1) rw |= 1u << p.rs1;
+                if ((p.flags & kPreRs2) && p.rs2) rw |= 1u << p.rs2;
+                if ((p.flags & kPreRd) && p.rd) rw |= 1u << p.rd;
+            }
+            static const bool tx_watch = !getenv("SHREWD_FI_TX_NOWATCH");   // A/B switch (diagnostics)
+            if (rw && tx_watch) g.put("  if (wwatch && TXB(mine && (lwm & 0x%xu) != 0)) { spc = 0x%llxULL; goto tx_out; }\n", rw,
+                          (unsigned long long)pc0);
+        }
         {   // a lane that rewrote one of this block's instruction bytes leaves before it
             const uint64_t blo = pc0 & ~3ULL, bhi = g.pc_of(insts.empty() ? h0 : insts.back()) + 6;
             g.put("  if (wdirty && TXB(mine && ldlo < 0x%llxULL && ldhi > 0x%llxULL)) { spc = 0x%llxULL; goto tx_out; }\n",

@@ -839,10 +839,13 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
             const PreRef E0 = pre_entry(tx, lpc);
             if (!(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader) &&
-                __ballot(mine && L.watch > 0) == 0) {
+                true) {
                 // lanes that rewrote code: every block checks its bytes against their range
                 const bool wdirty = uni32(__ballot(m.code_dirty) != 0);
                 const uint64_t ldlo = m.code_dirty ? m.dlo : kNone, ldhi = m.code_dirty ? m.dhi : 0;
+                // lanes watching a protected flipped register: blocks that touch it exit first
+                const bool wwatch = uni32(__ballot(L.watch > 0) != 0);
+                const uint32_t lwm = L.watch > 0 ? (1u << L.watch) : 0u;
                 const uint64_t gm = __ballot(mine);      // the entry group
                 uint64_t gmr = gm;                        // the running group
                 uint64_t pend = 0, pmin = kNone;          // parked lanes, their lowest pc
