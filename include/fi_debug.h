@@ -20,6 +20,9 @@ fi_status fi_debug_stats(fi_engine *e, uint64_t *out32);
 /* Per wave of the last launch: {s_memtime cycles, loop iterations,
  * translated instructions, slow fetches} (4 x u64 each). */
 fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves);
+/* Device time of each interpreter dispatch since fi_kernel_timer_reset, in
+ * launch order (epochs of each chunk); *n = dispatches (at most cap written). */
+fi_status fi_debug_dispatch_ms(fi_engine *e, float *ms, uint32_t cap, uint32_t *n);
 /* Lanes suspended at the end of each epoch of the last chunk (16 x u32). */
 fi_status fi_debug_epochs(fi_engine *e, uint32_t *out16);
 /* The translator's inputs of the last fi_golden_run: the pre-decoded text

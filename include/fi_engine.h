@@ -120,6 +120,10 @@ typedef struct {
 #define FI_CFG_NO_TRANSLATE 4u
 /* one launch per chunk, every wave to completion (no suspend / compact / resume) */
 #define FI_CFG_NO_EPOCHS 8u
+/* resumed epochs pack survivors by pc run: a wave takes up to 64 consecutive
+ * survivors (sorted by pc, then numInst) that stand at the same pc, instead
+ * of resume_lanes survivors of any pc */
+#define FI_CFG_PACK_RUNS 16u
 
 typedef struct {
     uint64_t ninst, ncycles;

@@ -31,7 +31,10 @@ hipError_t launch_trials(const DevCtx &c, hipStream_t st);
 hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, fi_histogram *h,
                        const unsigned long long *stats, hipStream_t st);
 hipError_t sort_pairs_bytes(uint64_t n, size_t &bytes);
+hipError_t launch_pack_runs(const uint64_t *keys, const uint32_t *cnt, uint64_t cap, uint32_t *wrange,
+                            uint32_t *n_waves, hipStream_t st);
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
+                            uint64_t text_lo,
                             uint64_t *keys, uint32_t *vals, hipStream_t st);
 std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
                              const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
@@ -120,6 +123,7 @@ struct fi_engine {
     uint32_t *d_cnt = nullptr;
     uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;
     uint32_t *d_svals = nullptr, *d_svals2 = nullptr;
+    uint32_t *d_wrange = nullptr, *d_nwaves = nullptr;   // packed resume (FI_CFG_PACK_RUNS)
 };
 
 static fi_status fail(fi_engine *e, fi_status code, const char *fmt, ...) {
@@ -190,7 +194,7 @@ static void free_work(fi_engine *e) {
     dfree(e->d_sites); dfree(e->d_keys); dfree(e->d_keys2); dfree(e->d_perm); dfree(e->d_perm2);
     dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg); dfree(e->d_fregs);
     dfree(e->d_save); dfree(e->d_surv[0]); dfree(e->d_surv[1]); dfree(e->d_cnt);
-    dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_priv); dfree(e->d_priv_vpn);
+    dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_wrange); dfree(e->d_nwaves); dfree(e->d_priv); dfree(e->d_priv_vpn);
     e->cap = 0;
 }
 static void free_snaps(fi_engine *e) { dfree(e->d_snaps); dfree(e->d_tab); dfree(e->d_pool); }
@@ -454,6 +458,8 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_skeys2, c * 8));
     HIPCHK(hipMalloc(&e->d_svals, c * 4));
     HIPCHK(hipMalloc(&e->d_svals2, c * 4));
+    HIPCHK(hipMalloc(&e->d_wrange, c * 8));
+    HIPCHK(hipMalloc(&e->d_nwaves, 16 * 4));
     e->cap = c;
     return FI_OK;
 }
@@ -832,6 +838,8 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     c.save = e->d_save;
     HIPCHK(hipMemsetAsync(e->d_stats, 0, 32 * sizeof(unsigned long long), st));
     HIPCHK(hipMemsetAsync(e->d_cnt, 0, 16 * 4, st));
+    const bool pack = (e->cfg.flags & FI_CFG_PACK_RUNS) != 0;
+    if (pack) HIPCHK(hipMemsetAsync(e->d_nwaves, 0, 16 * 4, st));
     // epochs: each wave runs a bounded number of loop
     // iterations, then its live lanes are suspended, sorted by pc and resumed
     // densely packed; the last epoch runs to completion.  All asynchronous:
@@ -851,14 +859,25 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
         c.surv = e->d_surv[ep & 1];
         c.surv_n = e->d_cnt + ep;
         c.lanes = ep == 0 ? e->cfg.lanes_per_wave : e->cfg.resume_lanes;
+        c.wrange = nullptr;
+        c.n_waves = nullptr;
         if (ep == 0) {
             c.resume = nullptr;
             c.resume_n = nullptr;
         } else {
-            HIPCHK(launch_surv_keys(e->d_save, e->d_surv[(ep - 1) & 1], e->d_cnt + ep - 1, k, e->d_skeys, e->d_svals, st));
+            HIPCHK(launch_surv_keys(e->d_save, e->d_surv[(ep - 1) & 1], e->d_cnt + ep - 1, k, c.text_lo, e->d_skeys,
+                                    e->d_svals, st));
             HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_skeys, e->d_skeys2, e->d_svals, e->d_svals2, k, 64, st));
             c.resume = e->d_svals2;
             c.resume_n = e->d_cnt + ep - 1;
+            if (pack) {
+                // one wave per same-pc run of survivors (<= 64 lanes); the grid
+                // covers the worst case (every survivor alone), surplus waves exit
+                HIPCHK(launch_pack_runs(e->d_skeys2, c.resume_n, k, e->d_wrange + 0, e->d_nwaves + ep, st));
+                c.wrange = e->d_wrange;
+                c.n_waves = e->d_nwaves + ep;
+                c.lanes = 1;
+            }
         }
         // every dispatch of the trial kernel is bracketed by its own event
         // pair on the launch stream (the bench's per-dispatch kernel time)
@@ -1074,6 +1093,16 @@ fi_status fi_kernel_timer_read(fi_engine *e, double *total_ms, uint32_t *launche
 }
 
 // ------------------------------------------------------------------ debug hooks (tests)
+fi_status fi_debug_dispatch_ms(fi_engine *e, float *ms, uint32_t cap, uint32_t *n) {
+    if (!e || (!ms && cap)) return FI_E_ARG;
+    for (size_t i = 0; i < e->tused && i < cap; i++) {
+        HIPCHK(hipEventSynchronize(e->tpool[i].second));
+        HIPCHK(hipEventElapsedTime(&ms[i], e->tpool[i].first, e->tpool[i].second));
+    }
+    if (n) *n = (uint32_t)e->tused;
+    return FI_OK;
+}
+
 fi_status fi_debug_decode(fi_engine *e, const uint32_t *raws, uint64_t n, void *out16) {
     if (!e || !raws || !out16) return FI_E_ARG;
     HIPCHK(hipSetDevice(e->dev));

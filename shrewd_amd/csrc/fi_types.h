@@ -115,6 +115,8 @@ struct DevCtx {
     uint32_t pad_lanes;
     const uint32_t *resume;          // NULL = fresh launch: lane slot = global lane index
     const uint32_t *resume_n;        // number of entries in resume[]
+    const uint32_t *wrange;          // packed resume (FI_CFG_PACK_RUNS): wave b runs resume[wrange[2b] .. wrange[2b+1])
+    const uint32_t *n_waves;         //   number of valid wrange pairs (waves b >= it exit at once)
     uint32_t *surv;                  // suspended lanes' slots are appended here
     uint32_t *surv_n;
     LaneSave *save;                  // [n_slots]

@@ -125,18 +125,39 @@ __global__ void fi_hist_kernel(const fi_site *sites, const fi_outcome *out, uint
 
 // Epochs: sort keys of the suspended lanes (their pc: lanes of one loop end
 // up in the same wave); entries past the survivor count sort last.
+// Survivor sort key: pc offset from the text base (low 32 bits) above the
+// low 32 bits of numInst, so that survivors standing at the same pc are
+// adjacent and ordered by progress.
 __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
-                                    uint64_t *keys, uint32_t *vals) {
+                                    uint64_t text_lo, uint64_t *keys, uint32_t *vals) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cap) return;
     if (i < *cnt) {
         const uint32_t sl = list[i];
-        keys[i] = save[sl].pc;
+        keys[i] = ((save[sl].pc - text_lo) << 32) | (save[sl].ninst & 0xFFFFFFFFu);
         vals[i] = sl;
     } else {
         keys[i] = ~0ULL;
         vals[i] = 0;
     }
+}
+
+// Packed resume: a wave starts at every sorted survivor whose pc differs from
+// its predecessor's, and at every 64th position; it ends at the next start.
+// Waves are numbered in atomic order (any order is correct: waves are
+// independent).
+__global__ void fi_pack_runs_kernel(const uint64_t *keys, const uint32_t *cnt, uint64_t cap, uint32_t *wrange,
+                                    uint32_t *n_waves) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = *cnt;
+    if (i >= n) return;
+    const uint32_t pc = (uint32_t)(keys[i] >> 32);
+    if (i != 0 && (i & 63) != 0 && (uint32_t)(keys[i - 1] >> 32) == pc) return;
+    uint32_t e = (uint32_t)i + 1;
+    while (e < n && (e & 63) != 0 && (uint32_t)(keys[e] >> 32) == pc) e++;
+    const uint32_t w = atomicAdd(n_waves, 1u);
+    wrange[2 * w] = (uint32_t)i;
+    wrange[2 * w + 1] = e;
 }
 
 __global__ void fi_hist_stats_kernel(const unsigned long long *stats, fi_histogram *h) {
@@ -176,8 +197,14 @@ hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, 
     return hipGetLastError();
 }
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
-                            uint64_t *keys, uint32_t *vals, hipStream_t st) {
-    hipLaunchKernelGGL(fi_surv_keys_kernel, dim3(nblk(cap, 256)), dim3(256), 0, st, save, list, cnt, cap, keys, vals);
+                            uint64_t text_lo, uint64_t *keys, uint32_t *vals, hipStream_t st) {
+    hipLaunchKernelGGL(fi_surv_keys_kernel, dim3(nblk(cap, 256)), dim3(256), 0, st, save, list, cnt, cap, text_lo,
+                       keys, vals);
+    return hipGetLastError();
+}
+hipError_t launch_pack_runs(const uint64_t *keys, const uint32_t *cnt, uint64_t cap, uint32_t *wrange,
+                            uint32_t *n_waves, hipStream_t st) {
+    hipLaunchKernelGGL(fi_pack_runs_kernel, dim3(nblk(cap, 256)), dim3(256), 0, st, keys, cnt, cap, wrange, n_waves);
     return hipGetLastError();
 }
 hipError_t sort_pairs_bytes(uint64_t n, size_t &bytes) {

@@ -113,6 +113,17 @@ struct LaneMem {
 __device__ __forceinline__ bool dirty_at(const LaneMem &m, uint64_t pc) {
     return m.code_dirty && (pc & ~3ULL) < m.dhi && pc + 6 > m.dlo;
 }
+// Does the lane's rewritten range come within kTxNear bytes after pc?  A
+// translated block that would meet it exits there (an entry and an exit for a
+// few instructions), so such lanes stay in the pre-decoded path instead.
+constexpr uint64_t kTxNear = 256;
+__device__ __forceinline__ bool dirty_near(const LaneMem &m, uint64_t pc) {
+#ifdef FI_DIRTY_NO_TX
+    return m.code_dirty;
+#else
+    return m.code_dirty && (pc & ~3ULL) < m.dhi && pc + kTxNear > m.dlo;
+#endif
+}
 __device__ __forceinline__ void mark_dirty(LaneMem &m, uint64_t lo, uint64_t hi) {
     m.dlo = m.code_dirty ? (lo < m.dlo ? lo : m.dlo) : lo;
     m.dhi = m.code_dirty ? (hi > m.dhi ? hi : m.dhi) : hi;
@@ -562,10 +573,15 @@ __device__ __forceinline__ bool ult64(uint64_t a, uint64_t b) {
     return ah < bh || (ah == bh && (uint32_t)a < (uint32_t)b);
 }
 
+// Waves per SIMD the register allocation must allow (the translated build
+// sets it per engine; see fi_jit.cpp).
+#ifndef FI_WAVES_PER_EU
+#define FI_WAVES_PER_EU 1
+#endif
 #ifdef __HIPCC_RTC__
-extern "C" __global__ void __launch_bounds__(64) fi_trial_kernel_tx(DevCtx ctx_arg) {
+extern "C" __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel_tx(DevCtx ctx_arg) {
 #else
-__global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
+__global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ctx_arg) {
 #endif
     (void)ctx_arg;
     KCtx *const kc = (KCtx *)__builtin_amdgcn_kernarg_segment_ptr();
@@ -576,9 +592,16 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
     // ---- the lane's slot: a fresh launch takes slot = global lane index, a
     // resume launch (epochs) the slots of suspended lanes, sorted by pc
     const uint32_t nlw = CX->lanes;
-    const uint64_t gidx = (uint64_t)blockIdx.x * nlw + lane;
+    uint64_t gidx = (uint64_t)blockIdx.x * nlw + lane;
     const bool resume = CX->resume != nullptr;
-    const bool live = lane < nlw && (resume ? gidx < *CX->resume_n : gidx < CX->n);
+    bool live = lane < nlw && (resume ? gidx < *CX->resume_n : gidx < CX->n);
+    if (resume && CX->wrange) {   // packed resume: this wave's same-pc run of survivors
+        const uint32_t b = blockIdx.x;
+        const bool have = b < *CX->n_waves;
+        const uint32_t ws = have ? CX->wrange[2 * b] : 0u, we = have ? CX->wrange[2 * b + 1] : 0u;
+        gidx = (uint64_t)ws + lane;
+        live = gidx < we;
+    }
     const uint64_t slot = live ? (resume ? CX->resume[gidx] : gidx) : (uint64_t)CX->n_slots + lane;
     fi_site s;
     s.inst = kNone; s.mask = 0; s.addr = 0; s.target = 0; s.trial = 0;
@@ -839,7 +862,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
             const PreRef E0 = pre_entry(tx, lpc);
             if (!(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader) &&
-                true) {
+                __ballot(mine && dirty_near(m, lpc)) == 0) {
                 // lanes that rewrote code: every block checks its bytes against their range
                 const bool wdirty = uni32(__ballot(m.code_dirty) != 0);
                 const uint64_t ldlo = m.code_dirty ? m.dlo : kNone, ldhi = m.code_dirty ? m.dhi : 0;
@@ -943,12 +966,33 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
             while (budget) {
                 PSTAMP(3);
                 spc = uni64(spc);
+                if (any_dirty && __ballot(mine && dirty_at(m, spc)) != 0) {
+                    // the group rewrote this instruction: decode the bytes the
+                    // lanes hold now (Decoder::moreBytes on their own pages) when
+                    // they all hold the same; otherwise the general path
+                    uint32_t raw = 0, t = 1;
+                    uint64_t fva = 0;
+                    int fr = 0;
+                    if (mine) fr = fetch_lane(CX, w, m, slot, spc, raw, t, fva);
+                    const uint32_t raw0 = (uint32_t)__builtin_amdgcn_readlane((int)raw, glane);
+                    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)t, glane);
+                    if (__ballot(mine && (fr != 0 || raw != raw0)) != 0) break;
+                    Dec dd = rv_decode(uni32(raw0));
+                    const uint32_t u = uop_of(dd);
+                    E.in = true;
+                    E.e.x = dd.raw;
+                    E.e.y = (uint32_t)dd.op | ((uint32_t)dd.rd << 8) | ((uint32_t)dd.rs1 << 16) | ((uint32_t)dd.rs2 << 24);
+                    E.e.z = (uint32_t)dd.imm;
+                    E.e.w = (uint32_t)dd.len |
+                            ((uint32_t)(kPreValid | (uni32(t0) == 2 ? kPreStraddle : 0) | dd.flags) << 8) | (u << 16);
+                }
                 const uint32_t q1 = uni32(E.e.y), q2 = uni32(E.e.z), q3 = uni32(E.e.w);
                 const uint32_t aux = q3 >> 16, kind = aux & 63;
                 if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
-                if (any_dirty && __ballot(mine && dirty_at(m, spc)) != 0) break;
 #ifdef FI_TX
-                if (steps && ((q3 >> 8) & kPreLeader)) break;   // translated blocks take over here
+                if (steps && ((q3 >> 8) & kPreLeader) &&   // translated blocks take over here
+                    !(any_dirty && __ballot(mine && dirty_near(m, spc)) != 0))
+                    break;
 #endif
                 const uint32_t rd = q1 >> 8 & 0xFF, rs1 = q1 >> 16 & 0xFF, rs2 = q1 >> 24;
                 if (any_watch) {
@@ -1069,7 +1113,7 @@ __global__ void __launch_bounds__(64) fi_trial_kernel(DevCtx ctx_arg) {
                 if (any_watch && mine && row == (uint32_t)L.watch) L.watch = -1;   // overwritten before read
                 if (CX->record) {   // golden trace for the liveness pass (one lane, uniform)
                     if (tpos < CX->rec_trace_cap && lane == 0)
-                        CX->rec_trace[tpos] = (((uint32_t)spc & ~1u) | (((uint32_t)spc & 1u) << 1)) - tx.lo >> 1;
+                        CX->rec_trace[tpos] = ((((uint32_t)spc & ~1u) | (((uint32_t)spc & 1u) << 1)) - tx.lo) >> 1;
                     tpos++;
                 }
                 steps++; xticks += straddle; fbytes += len; dbytes += msz;

@@ -74,6 +74,7 @@ CFG_NO_SNAPSHOT_START = 1
 CFG_NO_EARLY_EXIT = 2
 CFG_NO_TRANSLATE = 4
 CFG_NO_EPOCHS = 8
+CFG_PACK_RUNS = 16
 
 
 class GoldenInfo(C.Structure):
@@ -126,6 +127,7 @@ def lib():
         L.fi_kernel_timer_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
         L.fi_debug_waves.argtypes = [vp, vp, C.c_uint64]
         L.fi_debug_epochs.argtypes = [vp, vp]
+        L.fi_debug_dispatch_ms.argtypes = [vp, vp, C.c_uint32, C.POINTER(C.c_uint32)]
         L.fi_debug_golden_trace.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), vp, C.c_uint64,
                                             C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.fi_debug_translate.argtypes = [vp, C.c_uint64, C.c_uint64, vp, C.c_uint64, C.c_char_p, C.c_uint64,
@@ -238,6 +240,12 @@ class Engine:
         out = np.zeros(16, np.uint32)
         self._chk(self.L.fi_debug_epochs(self.h, out.ctypes.data), "fi_debug_epochs")
         return out.tolist()
+
+    def debug_dispatch_ms(self) -> list:
+        ms = np.zeros(256, np.float32)
+        n = C.c_uint32()
+        self._chk(self.L.fi_debug_dispatch_ms(self.h, ms.ctypes.data, 256, C.byref(n)), "fi_debug_dispatch_ms")
+        return [round(float(x), 3) for x in ms[:min(n.value, 256)]]
 
     def debug_golden_trace(self):
         """(pre-decoded text as uint8[n,16], golden trace uint32[m], text_lo)"""
