@@ -124,6 +124,10 @@ typedef struct {
  * survivors (sorted by pc, then numInst) that stand at the same pc, instead
  * of resume_lanes survivors of any pc */
 #define FI_CFG_PACK_RUNS 16u
+/* resumed epochs always take resume_lanes survivors per wave (by default a
+ * resumed epoch with few survivors spreads them down to one per wave, so that
+ * no two diverged survivors share a wave while SIMDs idle) */
+#define FI_CFG_FIXED_RESUME 32u
 
 typedef struct {
     uint64_t ninst, ncycles;

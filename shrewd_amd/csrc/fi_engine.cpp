@@ -821,7 +821,8 @@ fi_status fi_sample_sites(fi_engine *e, uint64_t first, uint64_t n, fi_site *out
 static hipError_t launch_trial_kernel(fi_engine *e, DevCtx &c, hipStream_t st) {
     if (!e->tx_fn) return launch_trials(c, st);
     void *args[] = {&c};
-    return hipModuleLaunchKernel(e->tx_fn, (unsigned)((c.n + c.lanes - 1) / c.lanes), 1, 1, 64, 1, 1, 0, st, args,
+    const uint32_t gl = (c.resume && c.resume_waves) ? 1u : c.lanes;   // grid for the fewest lanes per wave
+    return hipModuleLaunchKernel(e->tx_fn, (unsigned)((c.n + gl - 1) / gl), 1, 1, 64, 1, 1, 0, st, args,
                                  nullptr);
 }
 
@@ -839,6 +840,9 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     HIPCHK(hipMemsetAsync(e->d_stats, 0, 32 * sizeof(unsigned long long), st));
     HIPCHK(hipMemsetAsync(e->d_cnt, 0, 16 * 4, st));
     const bool pack = (e->cfg.flags & FI_CFG_PACK_RUNS) != 0;
+    int n_cu = 0;
+    HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->dev));
+    const uint32_t spread = (e->cfg.flags & FI_CFG_FIXED_RESUME) ? 0u : (uint32_t)std::max(1, n_cu) * 4u;   // SIMDs
     if (pack) HIPCHK(hipMemsetAsync(e->d_nwaves, 0, 16 * 4, st));
     // epochs: each wave runs a bounded number of loop
     // iterations, then its live lanes are suspended, sorted by pc and resumed
@@ -861,6 +865,7 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
         c.lanes = ep == 0 ? e->cfg.lanes_per_wave : e->cfg.resume_lanes;
         c.wrange = nullptr;
         c.n_waves = nullptr;
+        c.resume_waves = ep == 0 ? 0u : spread;
         if (ep == 0) {
             c.resume = nullptr;
             c.resume_n = nullptr;
@@ -877,6 +882,7 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
                 c.wrange = e->d_wrange;
                 c.n_waves = e->d_nwaves + ep;
                 c.lanes = 1;
+                c.resume_waves = 0;
             }
         }
         // every dispatch of the trial kernel is bracketed by its own event

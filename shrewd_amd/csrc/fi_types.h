@@ -112,7 +112,9 @@ struct DevCtx {
     uint32_t wave_budget;
     uint32_t n_slots;                // slots of the chunk (stride of priv_vpn)
     uint32_t lanes;                  // trials per wave (lanes >= this are idle): 8, 16, 32 or 64
-    uint32_t pad_lanes;
+    uint32_t resume_waves;           // resume: spread the survivors over this many waves when they
+                                     // need fewer than `lanes` per wave (power-of-two lanes per wave,
+                                     // >= 1); 0 = always `lanes` per wave
     const uint32_t *resume;          // NULL = fresh launch: lane slot = global lane index
     const uint32_t *resume_n;        // number of entries in resume[]
     const uint32_t *wrange;          // packed resume (FI_CFG_PACK_RUNS): wave b runs resume[wrange[2b] .. wrange[2b+1])

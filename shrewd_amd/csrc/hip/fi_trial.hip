@@ -591,9 +591,17 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
     const uint32_t lane = threadIdx.x;
     // ---- the lane's slot: a fresh launch takes slot = global lane index, a
     // resume launch (epochs) the slots of suspended lanes, sorted by pc
-    const uint32_t nlw = CX->lanes;
-    uint64_t gidx = (uint64_t)blockIdx.x * nlw + lane;
     const bool resume = CX->resume != nullptr;
+    uint32_t nlw = CX->lanes;
+    if (resume && CX->resume_waves) {   // few survivors: fewer per wave (the grid allows one per wave)
+        const uint32_t ns = *CX->resume_n, per = (ns + CX->resume_waves - 1) / CX->resume_waves;
+        uint32_t l = 1;
+        while (l < per && l < nlw) l <<= 1;
+        nlw = l;
+    }
+    // surplus waves of a resume grid (sized for the fewest lanes per wave) leave at once
+    if (resume && (CX->wrange ? blockIdx.x >= *CX->n_waves : (uint64_t)blockIdx.x * nlw >= *CX->resume_n)) return;
+    uint64_t gidx = (uint64_t)blockIdx.x * nlw + lane;
     bool live = lane < nlw && (resume ? gidx < *CX->resume_n : gidx < CX->n);
     if (resume && CX->wrange) {   // packed resume: this wave's same-pc run of survivors
         const uint32_t b = blockIdx.x;
@@ -985,6 +993,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                     E.e.z = (uint32_t)dd.imm;
                     E.e.w = (uint32_t)dd.len |
                             ((uint32_t)(kPreValid | (uni32(t0) == 2 ? kPreStraddle : 0) | dd.flags) << 8) | (u << 16);
+                    PSTAMP(5);
                 }
                 const uint32_t q1 = uni32(E.e.y), q2 = uni32(E.e.z), q3 = uni32(E.e.w);
                 const uint32_t aux = q3 >> 16, kind = aux & 63;
@@ -1564,7 +1573,8 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
 
 #ifndef __HIPCC_RTC__
 hipError_t launch_trials(const DevCtx &c, hipStream_t st) {
-    hipLaunchKernelGGL(fi_trial_kernel, dim3((unsigned)((c.n + c.lanes - 1) / c.lanes)), dim3(64), 0, st, c);
+    const uint32_t gl = (c.resume && c.resume_waves) ? 1u : c.lanes;   // grid for the fewest lanes per wave
+    hipLaunchKernelGGL(fi_trial_kernel, dim3((unsigned)((c.n + gl - 1) / gl)), dim3(64), 0, st, c);
     return hipGetLastError();
 }
 #endif

@@ -75,6 +75,7 @@ CFG_NO_EARLY_EXIT = 2
 CFG_NO_TRANSLATE = 4
 CFG_NO_EPOCHS = 8
 CFG_PACK_RUNS = 16
+CFG_FIXED_RESUME = 32
 
 
 class GoldenInfo(C.Structure):

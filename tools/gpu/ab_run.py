@@ -23,9 +23,11 @@ ap.add_argument("workloads", nargs="*", default=["crc32", "qsort", "intmix"])
 ap.add_argument("--resume-lanes", type=int, default=0)
 ap.add_argument("--epochs", type=int, default=0)
 ap.add_argument("--flags", type=int, default=0)
+ap.add_argument("--epoch-iters", type=int, default=0)
 a = ap.parse_args()
 for name in a.workloads:
-    e = Engine(max_trials_per_launch=131072, resume_lanes=a.resume_lanes, epochs=a.epochs, flags=a.flags)
+    e = Engine(max_trials_per_launch=131072, resume_lanes=a.resume_lanes, epochs=a.epochs, flags=a.flags,
+               epoch_iters=a.epoch_iters)
     e.load_elf(open(f"workloads/{name}.elf", "rb").read(), [name])
     e.golden_run()
     e.set_campaign(0x5EED0003, REGS_PC, 1)
