@@ -342,8 +342,10 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         g.put("B_%u: { // pc 0x%llx, %u insts\n", h0, (unsigned long long)pc0, n);
         g.put("  if (!ult64(0x%llxULL, wmin)) { spc = 0x%llxULL; goto tx_sched; }\n", (unsigned long long)pc0,
               (unsigned long long)pc0);
-        g.put("  if (wst + %uu > wbud || TXB(mine && rem - lst < %uu)) { spc = 0x%llxULL; goto tx_out; }\n", n, n,
-              (unsigned long long)pc0);
+        // ubud = min(wbud, every entry-group lane's rem) and lst <= wst, so the
+        // exact per-lane check only runs when the scalar bound is reached
+        g.put("  if (wst + %uu > ubud && (wst + %uu > wbud || TXB(mine && rem - lst < %uu))) { spc = 0x%llxULL; "
+              "goto tx_out; }\n", n, n, n, (unsigned long long)pc0);
         {   // a lane watching a protected flipped register this block reads or writes leaves before it
             uint32_t rw = 0;
             for (uint32_t hh : insts) {

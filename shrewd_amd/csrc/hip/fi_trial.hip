@@ -669,8 +669,21 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
     uint64_t pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t plast = __builtin_amdgcn_s_memtime();
 #endif
-    uint32_t n_iter = 0, n_slow = 0, n_min = 0, n_exec = 0, n_chk = 0, n_early = 0;   // per-wave (uniform)
-    uint32_t n_tx = 0, n_txin = 0;   // instructions run in translated blocks, entries into them
+    uint32_t n_iter = 0;   // per-wave loop iterations (uniform)
+    // per-wave diagnostic counters live in LDS, not SGPRs (the loop's scalar
+    // registers are scarce): slow fetches, min-PC reductions, lane-instructions,
+    // snapshot checks, early exits, translated instructions and entries.  Every
+    // lane writes the same (uniform) value.
+    __shared__ uint32_t WS[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) WS[k] = 0;
+#define n_slow WS[0]
+#define n_min WS[1]
+#define n_exec WS[2]
+#define n_chk WS[3]
+#define n_early WS[4]
+#define n_tx WS[5]
+#define n_txin WS[6]
 
     for (;;) {
         // ---- epochs: after wave_budget iterations the wave suspends its live
@@ -888,6 +901,9 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                 // elsewhere in the loop); a divergent bound here would make every
                 // branch of the translated code divergent
                 const uint32_t wbud = uni32(CX->wave_budget ? CX->wave_budget - n_iter : (1u << 30));
+                // scalar lower bound of the budget checks (translated blocks)
+                const uint32_t urem = (uint32_t)uni64(wave_min64(mine ? (uint64_t)rem : kNone));
+                const uint32_t ubud = urem < wbud ? urem : wbud;
                 const uint8_t *const zp = CX->zero_page;
                 uint8_t *const sink = CX->tx_sink + 8 * lane;
                 uint32_t lst = 0, lxt = 0, lfb = 0, ldb = 0;   // per lane: insts, straddles, fetch/data bytes
@@ -1568,6 +1584,13 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                                       ((unsigned long long)(n_iter ? (uint64_t)n_tx * 1000 / n_iter : 0) << 20) |
                                       (n_txin < (1u << 20) ? n_txin : (1u << 20) - 1));
         atomicMax(&CX->stats[19], ((unsigned long long)n_iter << 32) | (n_slow < 0xFFFFFFFFu ? n_slow : 0xFFFFFFFFu));
+#undef n_slow
+#undef n_min
+#undef n_exec
+#undef n_chk
+#undef n_early
+#undef n_tx
+#undef n_txin
     }
 }
 

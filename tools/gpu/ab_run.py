@@ -12,7 +12,8 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
 from shrewd_amd import Engine  # noqa: E402
 
 REGS_PC = ((1 << 32) - 2) | (1 << 32)
@@ -28,7 +29,7 @@ a = ap.parse_args()
 for name in a.workloads:
     e = Engine(max_trials_per_launch=131072, resume_lanes=a.resume_lanes, epochs=a.epochs, flags=a.flags,
                epoch_iters=a.epoch_iters)
-    e.load_elf(open(f"workloads/{name}.elf", "rb").read(), [name])
+    e.load_elf(open(os.path.join(ROOT, "workloads", f"{name}.elf"), "rb").read(), [name])
     e.golden_run()
     e.set_campaign(0x5EED0003, REGS_PC, 1)
     e.run_trials(0, N[name])   # warm

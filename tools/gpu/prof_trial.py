@@ -5,7 +5,8 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 from shrewd_amd import Engine  # noqa: E402
 from shrewd_amd.fi import CFG_NO_TRANSLATE  # noqa: E402
@@ -13,7 +14,7 @@ from shrewd_amd.fi import CFG_NO_TRANSLATE  # noqa: E402
 REGS_PC = ((1 << 32) - 2) | (1 << 32)
 name, seed, ids = sys.argv[1], int(sys.argv[2], 0), [int(x) for x in sys.argv[3:]]
 e = Engine(max_trials_per_launch=131072, flags=CFG_NO_TRANSLATE)
-e.load_elf(open(f"workloads/{name}.elf", "rb").read(), [name])
+e.load_elf(open(os.path.join(ROOT, "workloads", f"{name}.elf"), "rb").read(), [name])
 e.golden_run()
 e.set_campaign(seed, REGS_PC, 1)
 allsites = e.sample(0, max(ids) + 1)
