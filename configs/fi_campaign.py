@@ -29,6 +29,7 @@ def parse(argv=None):
     ap.add_argument("--structures", default="int_reg", help="comma list: int_reg,pc,mem,xN,<abi name>")
     ap.add_argument("--burst", type=int, default=1)
     ap.add_argument("--protect-mask", type=lambda s: int(s, 0), default=0)
+    ap.add_argument("--protect-opclasses", default="", help="comma list of gem5 OpClass names (IntAlu,IntMult,...)")
     ap.add_argument("--num-gpus", type=int, default=1)
     ap.add_argument("--max-insts-factor", type=float, default=2.0)
     ap.add_argument("--private-pages", type=int, default=16)
@@ -46,7 +47,7 @@ def run_gem5(a):
     camp = FaultCampaign(workload=a.workload, cmd=_split(a.cmd) or [a.workload], env=_split(a.env),
                          trials=a.trials, first_trial=a.first_trial, seed=a.seed,
                          structures=_split(a.structures), burst=a.burst, protect_mask=a.protect_mask,
-                         num_gpus=a.num_gpus, max_insts_factor=a.max_insts_factor,
+                         protect_opclasses=_split(a.protect_opclasses), num_gpus=a.num_gpus, max_insts_factor=a.max_insts_factor,
                          private_pages=a.private_pages, output=a.output)
     root = Root(full_system=False, campaign=camp)
     m5.instantiate()
@@ -70,7 +71,8 @@ def run_ctypes(a):
     c = FaultCampaign(a.workload, cmd=_split(a.cmd) or [a.workload], env=_split(a.env), trials=a.trials,
                       seed=a.seed, structures=_split(a.structures), burst=a.burst, protect_mask=a.protect_mask,
                       num_gpus=max(a.num_gpus, world), max_insts_factor=a.max_insts_factor, output=a.output,
-                      device=local, private_pages=a.private_pages)
+                      device=local, private_pages=a.private_pages,
+                      protect_opclasses=_split(a.protect_opclasses))
     t0 = time.perf_counter()
     c.run(first_trial=a.first_trial)
     dt = time.perf_counter() - t0

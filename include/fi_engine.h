@@ -80,10 +80,14 @@ typedef int32_t fi_status;
 #define FI_ESC_HOST 4
 #define FI_ESC_RESOURCE 5
 
-/* Fault-site structures: 1..31 = x1..x31, 32 = pc, 33 = 8-byte memory word */
+/* Fault-site structures: 1..31 = x1..x31, 32 = pc, 33 = 8-byte memory word,
+ * 34 = the result of an instruction: the value the first instruction that
+ * commits at or after the inject time writes to x[rd] (a transient fault in the
+ * functional unit that SHREWD's shadow execution targets) */
 #define FI_T_PC 32
 #define FI_T_MEM 33
-#define FI_N_STRUCT 34
+#define FI_T_RESULT 34
+#define FI_N_STRUCT 35
 
 typedef struct {
     uint8_t cls, sub, exit_code, flags;  /* flags bit0: injected, bit1: memory site unmapped at t */
@@ -167,11 +171,19 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out);
 fi_status fi_golden_stdout(fi_engine *e, uint8_t *buf, uint64_t cap, uint64_t *len);
 
 /* Campaign definition: SplitMix64 sites keyed by (seed, trial id); structures
- * is a bitmask (bit r = x_r, bit 32 = pc, bit 33 = memory); burst = adjacent
+ * is a bitmask (bit r = x_r, bit 32 = pc, bit 33 = memory, bit 34 = instruction
+ * result); burst = adjacent
  * bits flipped (1..64). */
 fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint32_t burst);
 /* selective-replication mask over x0..x31 (bits 0..31) and pc (bit 32) */
 fi_status fi_set_protect(fi_engine *e, uint64_t protect_mask);
+/* SHREWD selective replication by instruction class (the reference's
+ * BaseO3CPU.enableShrewd shadow issue, src/cpu/o3/inst_queue.cc:1082-1181):
+ * bit k = gem5 OpClass enum value k (src/cpu/FuncUnit.py:43).  Instructions of
+ * a protected class that has a shadow functional unit (FUPool::getUnit,
+ * src/cpu/o3/fu_pool.cc:177-301: IntAlu, IntMult, IntDiv, FloatAdd..FloatSqrt)
+ * are replicated; a result fault (FI_T_RESULT) on one is detected. */
+fi_status fi_set_protect_opclasses(fi_engine *e, uint64_t opclass_mask);
 
 fi_status fi_sample_sites(fi_engine *e, uint64_t first_trial, uint64_t n, fi_site *out);
 /* out (n entries, trial order) and hist may be NULL. hist is accumulated into (+=). */

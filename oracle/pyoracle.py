@@ -59,6 +59,7 @@ def lib():
         L.or_mnemonic.restype = C.c_char_p
         L.or_mnemonic.argtypes = [C.c_uint32]
         L.or_sys_class.argtypes = [C.c_int]
+        L.or_set_protect_opclasses.argtypes = [C.c_void_p, C.c_uint64]
         _lib = L
     return _lib
 
@@ -79,6 +80,10 @@ class Oracle:
 
     def __del__(self):
         self.close()
+
+    def set_protect_opclasses(self, mask: int):
+        """SHREWD replication set: bit k = gem5 OpClass enum value k."""
+        self.L.or_set_protect_opclasses(self.h, mask)
 
     def run_golden(self, max_inst=1 << 32) -> Golden:
         g = Golden()

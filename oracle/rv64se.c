@@ -11,6 +11,7 @@
 #define _GNU_SOURCE
 #include "rv64se.h"
 #include "../shrewd_amd/csrc/gem5_decode_table.h"
+#include "../shrewd_amd/csrc/gem5_opclass_table.h"
 
 #include <pthread.h>
 #include <stdio.h>
@@ -99,6 +100,7 @@ struct or_campaign {
     u64 brk0;
     u64 *mem_pages;        /* writable pages at process start (memory fault candidates) */
     u64 n_mem_pages;
+    u64 protect_opc;       /* SHREWD replication: OpClass mask (bit = FuncUnit.py enum value) */
     /* golden */
     int have_golden;
     or_golden_t golden;
@@ -122,6 +124,7 @@ typedef struct {
     bytes_t out, err;
     /* fault injection */
     const or_site_t *site; int injected; int watch; /* watch = protected flipped reg, -1 none */
+    int rarm, wrote;      /* result fault armed (OR_T_RESULT); the executing instruction wrote x[rd] */
     u64 protect_mask;
     /* termination */
     int done; or_outcome_t res;
@@ -1053,6 +1056,7 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
     default: return F_UNKNOWN;
     }
     wrreg(m, d->rd, v);
+    m->wrote = d->rd > 0;
     if (m->watch > 0 && d->rd == m->watch) m->watch = -1;   /* overwritten before read */
     return F_NONE;
 no_rd:
@@ -1069,6 +1073,8 @@ static void inject(mach_t *m) {
     } else if (s->target == OR_T_PC) {
         m->pc ^= s->mask;
         if ((m->protect_mask >> 32) & 1) { finish(m, OR_DETECTED, 0, 0); }
+    } else if (s->target == OR_T_RESULT) {
+        m->rarm = 1;   /* the next instruction that commits is the target */
     } else if (s->target == OR_T_MEM) {
         /* flip the 8-byte word if its page is mapped at inject time */
         uint8_t *pg = translate_w(m, s->addr);
@@ -1106,6 +1112,39 @@ static void invoke_fault(mach_t *m, int f, u64 fault_va, const dec_t *d) {
         return;
     }
     }
+}
+
+/* gem5 OpClass of an executed op (tests/golden/opclass_rv64.json, generated
+ * from the reference's ISA description) */
+static int op_class(int op) {
+    switch (op) {
+#define OPC(n, c) case OP_##n: return c;
+    FI_GEM5_OPCLASS(OPC)
+#undef OPC
+    default: return 0;
+    }
+}
+
+/* SHREWD shadow execution: FUPool::getUnit(cap, is_shadow=true) (cpu/o3/
+ * fu_pool.cc:177-301) finds a shadow unit only for IntAlu, IntMult, IntDiv and
+ * the scalar Float classes (FloatAdd..FloatSqrt, enum 1..11); every other
+ * class returns NoShadowFU.  The atomic model has no FU contention, so a
+ * shadow-capable class in the protected set is always replicated. */
+static int replicated(u64 protect_opc, int cls) {
+    return cls >= FI_OPC_INTALU && cls <= FI_OPC_FLOATSQRT && ((protect_opc >> cls) & 1);
+}
+
+/* Result fault (OR_T_RESULT): applied to the first instruction that commits
+ * at or after the inject time.  A replicated instruction's shadow disagrees
+ * with the faulty result: detected at its commit (pc = the instruction).
+ * Otherwise the value written to x[rd] is flipped; an instruction that writes
+ * no integer register leaves nothing to flip.  Returns 1 if the trial ended. */
+static int result_fault(mach_t *m, const dec_t *d) {
+    m->rarm = 0;
+    if (!m->wrote) { m->injected = 2; return 0; }
+    if (replicated(m->c->protect_opc, op_class(d->op))) { finish(m, OR_DETECTED, 0, 0); return 1; }
+    m->x[d->rd] ^= m->site->mask;
+    return 0;
 }
 
 /* One AtomicSimpleCPU::tick() with width=1 (cpu/simple/atomic.cc:611-739). */
@@ -1156,8 +1195,12 @@ static void tick(mach_t *m, u64 cap) {
             m->fetch_offset += 4;
         }
         if (have_inst) {
+            m->wrote = 0;
             f = execute(m, &d, &fva);
-            if (f == F_NONE) m->num_inst++;   /* countInst only on NoFault (atomic.cc:687-689) */
+            if (f == F_NONE) {
+                m->num_inst++;   /* countInst only on NoFault (atomic.cc:687-689) */
+                if (m->rarm && result_fault(m, &d)) return;
+            }
         }
     }
     /* advancePC (base.cc:493-512) */
@@ -1418,6 +1461,8 @@ static void *worker(void *arg) {
         run_trial(j->c, &j->sites[i], j->protect, j->cap, &j->out[i], NULL);
     return NULL;
 }
+
+void or_set_protect_opclasses(or_campaign_t *c, u64 mask) { c->protect_opc = mask; }
 
 int or_run_trials(or_campaign_t *c, const or_site_t *sites, u64 n, u64 protect, u64 f16, or_outcome_t *out,
                   int nth) {

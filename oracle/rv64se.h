@@ -49,7 +49,7 @@ enum {
 enum { OR_HANG_INSTS = 1 };
 
 /* structure ids for fault sites */
-enum { OR_T_PC = 32, OR_T_MEM = 33 };
+enum { OR_T_PC = 32, OR_T_MEM = 33, OR_T_RESULT = 34 };
 
 typedef struct {
     uint8_t cls, sub, exit_code, flags;
@@ -89,6 +89,11 @@ uint64_t or_golden_stdout(or_campaign_t *c, uint8_t *buf, uint64_t cap);
  * is a bitmask over {bit r = x_r (1..31), bit 32 = pc, bit 33 = memory}. */
 int or_sample(or_campaign_t *c, uint64_t seed, uint64_t first_trial, uint64_t n,
               uint64_t structures, uint32_t burst, or_site_t *sites);
+
+/* SHREWD selective replication by instruction class: bit k = gem5 OpClass
+ * enum value k (src/cpu/FuncUnit.py).  A result fault on a replicated
+ * instruction is detected (see rv64se.c:result_fault). */
+void or_set_protect_opclasses(or_campaign_t *c, uint64_t mask);
 
 /* Run trials from scratch (no golden snapshots, no early exit): the plain
  * serial semantics the GPU engine must reproduce bit for bit. */

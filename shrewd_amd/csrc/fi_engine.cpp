@@ -101,6 +101,7 @@ struct fi_engine {
     uint64_t seed = 0x5EED0001ULL, structures = 0;
     uint32_t burst = 1;
     uint64_t protect = 0;
+    uint64_t protect_opc = 0;   // SHREWD replication by OpClass (fi_set_protect_opclasses)
 
     // work buffers, sized for `cap` trials per launch
     uint64_t cap = 0;
@@ -482,6 +483,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.priv_pages = e->cfg.private_pages;
     c.hang_cap = e->golden.ninst * e->cfg.hang_factor_x16 / 16 + 1000;
     c.protect_mask = e->protect;
+    c.protect_opc = e->protect_opc;
     c.priv_frames = e->d_priv; c.priv_vpn = e->d_priv_vpn;
     c.tx_sink = e->d_sink;
     c.fregs = e->d_fregs;
@@ -781,6 +783,12 @@ fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint
 fi_status fi_set_protect(fi_engine *e, uint64_t protect_mask) {
     if (!e) return FI_E_ARG;
     e->protect = protect_mask;
+    return FI_OK;
+}
+
+fi_status fi_set_protect_opclasses(fi_engine *e, uint64_t opclass_mask) {
+    if (!e) return FI_E_ARG;
+    e->protect_opc = opclass_mask;
     return FI_OK;
 }
 

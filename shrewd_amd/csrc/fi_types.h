@@ -93,6 +93,7 @@ struct DevCtx {
     uint32_t snap_start;             // 1 = a wave starts at the snapshot before its earliest inject time
     uint64_t hang_cap;
     uint64_t protect_mask;
+    uint64_t protect_opc;            // SHREWD replication: protected gem5 OpClass values (bit mask)
     // per-trial private (copy-on-write) pages: frames [slot][P][4096], vpns [P][n]
     uint8_t *priv_frames;
     uint64_t *priv_vpn;

@@ -24,6 +24,7 @@
 #include "fi_types.h"
 #include "fi_device.h"
 #include "rv64_isa.h"
+#include "gem5_opclass_table.h"
 
 namespace fi {
 
@@ -325,9 +326,27 @@ struct Lane {
     int watch;
     bool out_bad, done;
     bool fp;                      // FP registers materialised (else all zero, as at process start)
-    uint8_t injected;
+    uint8_t injected;             // 0 pending, 1 applied, 2 nothing to flip, 3 result fault armed
     fi_outcome res;
 };
+
+// gem5 OpClass of an executed op (generated from the reference's ISA
+// description; tests/golden/opclass_rv64.json)
+__device__ __forceinline__ uint32_t op_class(uint32_t op) {
+    switch (op) {
+#define FI_OPC(n, c) case OP_##n: return c;
+        FI_GEM5_OPCLASS(FI_OPC)
+#undef FI_OPC
+    default: return 0;
+    }
+}
+// SHREWD shadow execution: FUPool::getUnit(cap, is_shadow) (src/cpu/o3/
+// fu_pool.cc:177-301) has a shadow unit only for IntAlu, IntMult, IntDiv and
+// FloatAdd..FloatSqrt; the atomic model has no FU contention, so a protected
+// class among them is always replicated (oracle/rv64se.c:replicated)
+__device__ __forceinline__ bool replicated(uint64_t protect_opc, uint32_t cls) {
+    return cls >= FI_OPC_INTALU && cls <= FI_OPC_FLOATSQRT && ((protect_opc >> cls) & 1);
+}
 
 // ------------------------------------------------------------------ F/D/Zfh + A
 // FP registers live in HBM, [32][n_slots] (lane-coalesced), touched only by the
@@ -746,6 +765,8 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                 L.pc ^= s.mask;
                 L.injected = 1;
                 if ((CX->protect_mask >> 32) & 1) finish(L, FI_DETECTED, 0, 0, (uint32_t)L.pc);
+            } else if (s.target == FI_T_RESULT) {
+                L.injected = 3;   // armed: the next instruction that commits (general path) is the target
             } else if (s.target == FI_T_MEM) {
                 const uint64_t p = lookup(CX, w, m, slot, s.addr >> 12);
                 if (!p) {
@@ -779,7 +800,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                 pend &= ~__ballot(grp);
                 const SnapState *S = CX->snaps + (uint32_t)(kn / CX->snap_interval);
                 bool eq = grp && L.pc == S->pc && L.out_pos == S->out_pos && L.err_pos == S->err_pos && !L.out_bad &&
-                          m.stack_min == S->stack_min && !L.fp;
+                          m.stack_min == S->stack_min && !L.fp && L.injected != 3;
                 if (__ballot(eq)) {
                     // a register the golden future writes before reading it cannot
                     // influence the outcome (liveness from the golden trace)
@@ -883,7 +904,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
             tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
             const PreRef E0 = pre_entry(tx, lpc);
             if (!(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader) &&
-                __ballot(mine && dirty_near(m, lpc)) == 0) {
+                __ballot(mine && (dirty_near(m, lpc) || L.injected == 3)) == 0) {
                 // lanes that rewrote code: every block checks its bytes against their range
                 const bool wdirty = uni32(__ballot(m.code_dirty) != 0);
                 const uint64_t ldlo = m.code_dirty ? m.dlo : kNone, ldhi = m.code_dirty ? m.dhi : 0;
@@ -969,7 +990,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
         // (K_SLOW op, fault, page request, syscall).  Nothing commits unless the
         // whole instruction commits for every group lane.
         if (CX->pre_ok && lpc >= CX->text_lo && lpc < CX->text_hi &&
-            true) {
+            __ballot(mine && L.injected == 3) == 0) {   // an armed result fault commits in the general path
             // lanes that rewrote code run here too, until they reach a rewritten
             // instruction; lanes watching a protected flipped register, until an
             // instruction reads it (the general path classifies the detection)
@@ -1481,10 +1502,17 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                 CX->fregs[(uint64_t)d.rd * CX->n_slots + slot] = fval;
             }
             L.ncyc += xticks;
+            bool rdet = false;
+            if (L.injected == 3) {   // result fault (oracle/rv64se.c:result_fault)
+                if (!(wrd && d.rd)) L.injected = 2;
+                else if (replicated(CX->protect_opc, op_class(d.op))) rdet = true;
+                else { v ^= s.mask; L.injected = 1; }
+            }
             if (wrd && d.rd) RREG(d.rd) = v;
             if (wrd && L.watch > 0 && (d.flags & kPreRd) && d.rd == L.watch) L.watch = -1;
             L.ninst++;
-            L.pc = npc;
+            if (rdet) finish(L, FI_DETECTED, 0, 0, (uint32_t)pc);   // the shadow disagrees at commit
+            else L.pc = npc;
         } else {
         switch (f) {
         case F_SYSCALL:   // SyscallFault::invokeSE advances the PC first (arch/riscv/faults.cc:325-333)
@@ -1518,7 +1546,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
 #endif
         // ---- stay in the inner loop? every group lane committed, none reached
         // its next event, all at one PC that is still the wave's minimum
-        const bool cont = mine && f == F_NONE && L.ninst < next_ev;
+        const bool cont = mine && f == F_NONE && !L.done && L.ninst < next_ev;
         const uint64_t cm = __ballot(cont);
         if (cm != gmask) break;
         const uint64_t npc0 = uni64(readlane64(L.pc, __ffsll((unsigned long long)cm) - 1));

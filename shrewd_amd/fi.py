@@ -23,7 +23,7 @@ CRASH_NAMES = {1: "panic_unknown_inst", 2: "panic_illegal_inst", 3: "panic_page_
                4: "fatal_syscall_range", 5: "fatal_syscall_unimpl", 6: "fatal_proxy", 7: "abort_fd_assert",
                8: "sigtrap", 9: "fatal_stack_limit", 10: "panic_amo_line"}
 ESCAPE_NAMES = {1: "inst", 2: "syscall", 3: "csr", 4: "host", 5: "resource"}
-T_PC, T_MEM, N_STRUCT = 32, 33, 34
+T_PC, T_MEM, T_RESULT, N_STRUCT = 32, 33, 34, 35
 
 OUTCOME_DT = np.dtype([("cls", "u1"), ("sub", "u1"), ("exit_code", "u1"), ("flags", "u1"),
                        ("detail", "<u4"), ("ninst", "<u8")])
@@ -35,6 +35,28 @@ HIST_DT = np.dtype([("counts", "<u8", (N_STRUCT, 64, 6)), ("crash_sub", "<u8", (
 ABI_NAMES = {"zero": 0, "ra": 1, "sp": 2, "gp": 3, "tp": 4, "t0": 5, "t1": 6, "t2": 7, "s0": 8, "fp": 8, "s1": 9,
              **{f"a{i}": 10 + i for i in range(8)}, **{f"s{i}": 16 + i for i in range(2, 12)},
              "t3": 28, "t4": 29, "t5": 30, "t6": 31}
+
+
+# gem5 OpClass enum (src/cpu/FuncUnit.py:43), for protect_opclasses by name
+OPCLASS_NAMES = ["No_OpClass", "IntAlu", "IntMult", "IntDiv", "FloatAdd", "FloatCmp", "FloatCvt", "FloatMult",
+                 "FloatMultAcc", "FloatDiv", "FloatMisc", "FloatSqrt"]
+OPCLASS_MEMREAD, OPCLASS_MEMWRITE, OPCLASS_FLOATMEMREAD, OPCLASS_FLOATMEMWRITE = 52, 53, 54, 55
+
+
+def opclass_mask(opclasses: Iterable[str | int] | int) -> int:
+    """gem5 OpClass names ('IntAlu', 'IntMult', ...) or enum values -> bitmask."""
+    if isinstance(opclasses, int):
+        return opclasses
+    named = dict(zip(OPCLASS_NAMES, range(len(OPCLASS_NAMES))))
+    named.update(MemRead=OPCLASS_MEMREAD, MemWrite=OPCLASS_MEMWRITE, FloatMemRead=OPCLASS_FLOATMEMREAD,
+                 FloatMemWrite=OPCLASS_FLOATMEMWRITE)
+    m = 0
+    for c in opclasses:
+        k = c if isinstance(c, int) else named[c.removesuffix("Op")]
+        if not 0 <= k < 64:
+            raise ValueError(f"OpClass {c!r} outside the 64-bit mask")
+        m |= 1 << k
+    return m
 
 
 def structures_mask(structures: Iterable[str] | int) -> int:
@@ -50,6 +72,8 @@ def structures_mask(structures: Iterable[str] | int) -> int:
             m |= 1 << T_PC
         elif s in ("mem", "memory"):
             m |= 1 << T_MEM
+        elif s in ("result", "fu", "inst_result"):
+            m |= 1 << T_RESULT
         elif s in ABI_NAMES:
             m |= 1 << ABI_NAMES[s]
         elif s.startswith("x") and s[1:].isdigit() and 0 <= int(s[1:]) < 32:
@@ -114,6 +138,7 @@ def lib():
         L.fi_golden_stdout.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.fi_set_campaign.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32]
         L.fi_set_protect.argtypes = [vp, C.c_uint64]
+        L.fi_set_protect_opclasses.argtypes = [vp, C.c_uint64]
         L.fi_sample_sites.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
         L.fi_run_trials.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp]
         L.fi_run_sites.argtypes = [vp, vp, C.c_uint64, vp, vp]
@@ -201,6 +226,9 @@ class Engine:
 
     def set_protect(self, mask: int):
         self._chk(self.L.fi_set_protect(self.h, mask), "fi_set_protect")
+
+    def set_protect_opclasses(self, opclasses):
+        self._chk(self.L.fi_set_protect_opclasses(self.h, opclass_mask(opclasses)), "fi_set_protect_opclasses")
 
     def sample(self, first: int, n: int) -> np.ndarray:
         out = np.zeros(n, SITE_DT)
@@ -323,13 +351,13 @@ class FaultCampaign:
 
     Params (same names/meaning as the SimObject): workload (binary path), cmd
     (argv, cmd[0] defaults to workload), env, trials, seed, structures,
-    burst, protect_mask, num_gpus, max_insts_factor, output.
+    burst, protect_mask, protect_opclasses, num_gpus, max_insts_factor, output.
     """
 
     def __init__(self, workload: str, cmd: Sequence[str] | None = None, env: Sequence[str] | None = None,
                  trials: int = 1000, seed: int = 0x5EED0001, structures=("int_reg",), burst: int = 1,
                  protect_mask: int = 0, num_gpus: int = 1, max_insts_factor: float = 2.0, output: str = "",
-                 device: int = 0, private_pages: int = 16):
+                 device: int = 0, private_pages: int = 16, protect_opclasses=()):
         self.workload, self.cmd, self.env = workload, list(cmd or [workload]), list(env or [])
         self.trials, self.seed, self.structures, self.burst = trials, seed, structures, burst
         self.protect_mask, self.num_gpus, self.output = protect_mask, num_gpus, output
@@ -341,6 +369,8 @@ class FaultCampaign:
         self.golden = self.engine.golden_run()
         self.engine.set_campaign(seed, structures, burst)
         self.engine.set_protect(protect_mask)
+        self.protect_opclasses = opclass_mask(protect_opclasses)
+        self.engine.set_protect_opclasses(self.protect_opclasses)
         self._hist = None
         self.outcomes = None
 
@@ -348,6 +378,11 @@ class FaultCampaign:
     def setProtectMask(self, mask: int):
         self.protect_mask = mask
         self.engine.set_protect(mask)
+
+    # PyBindMethod("setProtectOpClasses"): the op-class replication set
+    def setProtectOpClasses(self, opclasses):
+        self.protect_opclasses = opclass_mask(opclasses)
+        self.engine.set_protect_opclasses(self.protect_opclasses)
 
     def run(self, first_trial: int = 0, n: int | None = None):
         """Run the campaign.  Under torch.distributed with num_gpus > 1 (one

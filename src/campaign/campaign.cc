@@ -58,6 +58,8 @@ uint64_t structures_mask(const std::vector<std::string> &names) {
             m |= 1ULL << FI_T_PC;
         } else if (s == "mem" || s == "memory") {
             m |= 1ULL << FI_T_MEM;
+        } else if (s == "result" || s == "fu" || s == "inst_result") {
+            m |= 1ULL << FI_T_RESULT;
         } else if (abi.count(s)) {
             m |= 1ULL << abi.at(s);
         } else if (s.size() > 1 && s[0] == 'x' && s.find_first_not_of("0123456789", 1) == std::string::npos &&
@@ -68,6 +70,24 @@ uint64_t structures_mask(const std::vector<std::string> &names) {
         }
     }
     return m & ~1ULL;
+}
+
+// gem5 OpClass names (src/cpu/FuncUnit.py:43) -> mask of enum values; a bare
+// number is taken as the enum value
+uint64_t opclass_mask(const std::vector<std::string> &names) {
+    static const std::map<std::string, int> cls = {
+        {"No_OpClass", 0}, {"IntAlu", 1}, {"IntMult", 2}, {"IntDiv", 3}, {"FloatAdd", 4}, {"FloatCmp", 5},
+        {"FloatCvt", 6}, {"FloatMult", 7}, {"FloatMultAcc", 8}, {"FloatDiv", 9}, {"FloatMisc", 10},
+        {"FloatSqrt", 11}, {"MemRead", 52}, {"MemWrite", 53}, {"FloatMemRead", 54}, {"FloatMemWrite", 55}};
+    uint64_t m = 0;
+    for (std::string s : names) {
+        if (s.size() > 2 && s.compare(s.size() - 2, 2, "Op") == 0) s.resize(s.size() - 2);
+        if (cls.count(s)) m |= 1ULL << cls.at(s);
+        else if (!s.empty() && s.find_first_not_of("0123456789") == std::string::npos && std::stoi(s) < 64)
+            m |= 1ULL << std::stoi(s);
+        else throw std::runtime_error("unknown OpClass '" + s + "'");
+    }
+    return m;
 }
 
 Campaign::Campaign(const CampaignParams &p) : p_(p) {
@@ -98,6 +118,7 @@ Campaign::Campaign(const CampaignParams &p) : p_(p) {
         check(e, fi_golden_run(e, &gi), "fi_golden_run");
         check(e, fi_set_campaign(e, p_.seed, smask, p_.burst), "fi_set_campaign");
         check(e, fi_set_protect(e, p_.protect_mask), "fi_set_protect");
+        check(e, fi_set_protect_opclasses(e, opclass_mask(p_.protect_opclasses)), "fi_set_protect_opclasses");
         if (g == 0) {
             golden_.ninst = gi.ninst;
             golden_.ncycles = gi.ncycles;
@@ -115,6 +136,12 @@ Campaign::Campaign(const CampaignParams &p) : p_(p) {
 
 Campaign::~Campaign() {
     for (auto *e : engines_) fi_destroy(e);
+}
+
+void Campaign::setProtectOpClasses(const std::vector<std::string> &opclasses) {
+    p_.protect_opclasses = opclasses;
+    const uint64_t m = opclass_mask(opclasses);
+    for (auto *e : engines_) check(e, fi_set_protect_opclasses(e, m), "fi_set_protect_opclasses");
 }
 
 void Campaign::setProtectMask(uint64_t mask) {

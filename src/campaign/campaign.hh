@@ -31,6 +31,7 @@ struct CampaignParams {
     std::vector<std::string> structures{"int_reg"};
     uint32_t burst = 1;
     uint64_t protect_mask = 0;
+    std::vector<std::string> protect_opclasses;   // SHREWD replication set (gem5 OpClass names)
     uint32_t num_gpus = 1;
     uint32_t first_device = 0;
     double max_insts_factor = 2.0;        // hang cap = golden * f + 1000
@@ -41,6 +42,8 @@ struct CampaignParams {
 // 'int_reg' (x1..x31), 'pc', 'mem', 'xN' or ABI register names -> bitmask
 // (bit r = x_r, bit 32 = pc, bit 33 = memory word).  Throws on unknown names.
 uint64_t structures_mask(const std::vector<std::string> &names);
+// gem5 OpClass names ("IntAlu", "IntMultOp", ...) or enum values -> bitmask
+uint64_t opclass_mask(const std::vector<std::string> &names);
 
 struct GoldenSummary {
     uint64_t ninst = 0, ncycles = 0;
@@ -59,6 +62,7 @@ class Campaign {
     // on engine errors (the SimObject turns these into fatal()).
     void run();
     void setProtectMask(uint64_t mask);
+    void setProtectOpClasses(const std::vector<std::string> &opclasses);
 
     const fi_histogram &histogram() const { return hist_; }
     const std::vector<fi_outcome> &outcomes() const { return out_; }

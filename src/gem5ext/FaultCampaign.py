@@ -19,6 +19,7 @@ class FaultCampaign(SimObject):
         PyBindMethod("run"),
         PyBindMethod("summaryJson"),
         PyBindMethod("setProtectMask"),
+        PyBindMethod("setProtectOpClasses"),
         PyBindMethod("trialsRun"),
     ]
 
@@ -29,10 +30,13 @@ class FaultCampaign(SimObject):
     first_trial = Param.UInt64(0, "first trial id (sites are keyed by (seed, trial id))")
     seed = Param.UInt64(0x5EED0001, "campaign seed")
     structures = VectorParam.String(
-        ["int_reg"], "fault targets: int_reg, pc, mem, xN or ABI register names")
+        ["int_reg"], "fault targets: int_reg, pc, mem, result, xN or ABI register names")
     burst = Param.UInt32(1, "adjacent bits flipped per fault (1..64)")
     protect_mask = Param.UInt64(
         0, "selective replication: protected x0..x31 (bits 0-31) and pc (bit 32)")
+    protect_opclasses = VectorParam.String(
+        [], "SHREWD replication: gem5 OpClass names whose instructions get a shadow "
+        "execution (IntAlu, IntMult, IntDiv, Float*); a result fault on one is detected")
     num_gpus = Param.UInt32(1, "MI355X devices used by this process")
     first_gpu = Param.UInt32(0, "first HIP device ordinal")
     max_insts_factor = Param.Float(

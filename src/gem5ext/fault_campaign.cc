@@ -25,6 +25,7 @@ FaultCampaign::init()
     cp.structures = params().structures;
     cp.burst = params().burst;
     cp.protect_mask = params().protect_mask;
+    cp.protect_opclasses = params().protect_opclasses;
     cp.num_gpus = params().num_gpus;
     cp.first_device = params().first_gpu;
     cp.max_insts_factor = params().max_insts_factor;
@@ -58,6 +59,12 @@ void
 FaultCampaign::setProtectMask(uint64_t mask)
 {
     campaign->setProtectMask(mask);
+}
+
+void
+FaultCampaign::setProtectOpClasses(std::vector<std::string> opclasses)
+{
+    campaign->setProtectOpClasses(opclasses);
 }
 
 uint64_t

@@ -31,6 +31,7 @@ class FaultCampaign : public SimObject
     void run();
     std::string summaryJson() const;
     void setProtectMask(uint64_t mask);
+    void setProtectOpClasses(std::vector<std::string> opclasses);
     uint64_t trialsRun() const;
 
   private:

@@ -150,6 +150,32 @@ def test_protect_mask_bit_exact(engine_factory, oracle_mod, mask):
         assert (dev["cls"] == 4).sum() > 0
 
 
+RESULT = 1 << 34
+OPC_INT = (1 << 1) | (1 << 2) | (1 << 3)        # IntAlu | IntMult | IntDiv (gem5 OpClass enum)
+
+
+@pytest.mark.parametrize("name,opc,n", [
+    ("hello", 0, 500), ("crc32", 0, 4000), ("crc32", OPC_INT, 4000), ("qsort", 1 << 1, 3000),
+    ("intmix", (1 << 1) | (1 << 2), 600), ("fpamo", OPC_INT | (1 << 6) | (1 << 10), 2000),
+])
+def test_result_faults_bit_exact(engine_factory, oracle_mod, name, opc, n):
+    """Result faults (structure 34) and SHREWD replication by OpClass: the
+    first instruction committing at the inject time has its x[rd] value
+    flipped, or is detected when its class is protected and has a shadow FU."""
+    e = engine_factory(name)
+    o = oracle_for(oracle_mod, name)
+    e.set_campaign(0xFACE + n, RESULT | REGS, 1)
+    e.set_protect_opclasses(opc)
+    o.set_protect_opclasses(opc)
+    sites = e.sample(0, n)
+    dev, _ = e.run_sites(sites)
+    ref = o.run_trials(sites)
+    e.set_protect_opclasses(0)
+    compare(dev, ref, sites)
+    if opc and name != "hello":
+        assert (dev["cls"] == 4).sum() > 0
+
+
 def test_run_trials_equals_run_sites(engine_factory):
     e = engine_factory("crc32")
     e.set_campaign(4242, REGS | PC, 1)

@@ -269,3 +269,64 @@ def test_decode_matches_gem5_decoder(oracle_mod):
             executed.add(name)
     assert {"c_addi4spn", "addi", "ld", "sd", "jalr", "mulhsu", "sh3add_uw", "czero_nez",
             "csrrw", "csrrci", "ecall", "fence_i", "prefetch_w"} <= executed
+
+
+# ---------------------------------------------------------------- SHREWD op classes
+INTALU, INTMULT, INTDIV, MEMREAD, MEMWRITE = 1, 2, 3, 52, 53
+RESULT = 34
+
+
+def test_opclass_fixture_matches_table():
+    """gem5_opclass_table.h (device + oracle) carries exactly the OpClass the
+    reference's generated constructors name (tests/golden/opclass_rv64.json)."""
+    import re
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "opclass_rv64.json")))
+    enum, ops = fx["enum"], fx["ops"]
+    assert enum[:4] == ["No_OpClass", "IntAlu", "IntMult", "IntDiv"] and enum[MEMREAD] == "MemRead"
+    hdr = open(os.path.join(ROOT, "shrewd_amd", "csrc", "gem5_opclass_table.h")).read()
+    rows = dict((n, int(c)) for n, c in re.findall(r"X\((\w+), (\d+)\)", hdr))
+    assert rows == {n: enum.index(c) for n, c in ops.items()}
+    for n, c in {"add": "IntAlu", "c_addi": "IntAlu", "beq": "IntAlu", "jal": "IntAlu", "mul": "IntMult",
+                 "mulhu": "IntMult", "div_": "IntDiv", "remuw": "IntDiv", "lw": "MemRead", "c_ldsp": "MemRead",
+                 "sd": "MemWrite", "amoadd_w": "MemRead", "fmv_x_d": "FloatCvt", "ecall": "No_OpClass"}.items():
+        assert ops[n] == c, n
+
+
+def _result_site(oracle_mod, inst, mask):
+    s = np.zeros(1, oracle_mod.SITE_DT)[0]
+    s["inst"], s["mask"], s["target"] = inst, mask, RESULT
+    return s
+
+
+def test_result_fault_known_answers(oracle_mod):
+    """hello: 0 li a0,1 | 1-2 la a1 | 3 li a2,13 | 4 li a7,64 | ecall | 5 li a0,0 | 6 li a7,94 | ecall."""
+    o = oracle_mod.Oracle(workload_elf("hello"), "hello")
+    o.run_golden()
+    res, out = o.run_one(_result_site(oracle_mod, 3, 1))          # count 13 -> 12: the newline is lost
+    assert res["cls"] == 1 and out == b"Hello world!" and res["flags"] == 1
+    res, out = o.run_one(_result_site(oracle_mod, 5, 1))          # armed at the ecall, lands on li a0,0
+    assert res["cls"] == 1 and res["exit_code"] == 1 and out == b"Hello world!\n"
+    o.set_protect_opclasses(1 << INTALU)                           # the shadow ALU disagrees at commit
+    res, _ = o.run_one(_result_site(oracle_mod, 3, 1))
+    assert res["cls"] == 4 and res["ninst"] == 4
+    o.set_protect_opclasses((1 << MEMREAD) | (1 << MEMWRITE) | (1 << INTMULT))   # no shadow for li
+    res, _ = o.run_one(_result_site(oracle_mod, 3, 1))
+    assert res["cls"] == 1
+
+
+def test_result_fault_replication_properties(oracle_mod):
+    """Protecting classes only turns outcomes into detected-by-replica; the
+    classes FUPool::getUnit gives no shadow (MemRead/MemWrite) change nothing."""
+    o = oracle_mod.Oracle(workload_elf("crc32"), "crc32")
+    o.run_golden()
+    sites = o.sample(7, 0, 3000, 1 << RESULT, 1)
+    assert (sites["target"] == RESULT).all()
+    base = o.run_trials(sites)
+    assert (base["cls"] != 4).all() and ((base["flags"] & 2) != 0).any()   # stores/branches: nothing to flip
+    o.set_protect_opclasses((1 << MEMREAD) | (1 << MEMWRITE))
+    assert np.array_equal(o.run_trials(sites), base)
+    o.set_protect_opclasses((1 << INTALU) | (1 << INTMULT) | (1 << INTDIV))
+    prot = o.run_trials(sites)
+    same = prot == base
+    assert ((prot["cls"] == 4) | same).all() and (prot["cls"] == 4).sum() > 0
+    assert (base["cls"][prot["cls"] == 4] != 4).all()
