@@ -11,6 +11,9 @@ trials/s, outcome classes, crash/escape sub-codes.
   C5 SHREWD selective-replication sweep on crc32: protected register masks vs
      residual SDC rate (a fault on a protected register that is read before
      being overwritten is detected-by-replica)
+  C5b SHREWD replication by instruction class: result faults (the value an
+     instruction writes) on crc32 and qsort with protected gem5 OpClass sets
+     (a replicated instruction's shadow execution detects the fault)
 python tools/campaigns.py [TAG]
 """
 import json
@@ -26,6 +29,9 @@ from shrewd_amd.fi import CLASS_NAMES, CRASH_NAMES, ESCAPE_NAMES  # noqa: E402
 REGS = (1 << 32) - 2
 PC = 1 << 32
 MEM = 1 << 33
+RESULT = 1 << 34
+OPC = {"none": 0, "IntAlu": 1 << 1, "IntMult+IntDiv": (1 << 2) | (1 << 3), "IntAlu+IntMult+IntDiv": 0b1110,
+       "MemRead+MemWrite (no shadow FU)": (1 << 52) | (1 << 53)}
 # ABI register groups (x-register numbers)
 MASKS = {"none": 0, "sp_ra_gp_tp": (1 << 1) | (1 << 2) | (1 << 3) | (1 << 4),
          "a0-a7": sum(1 << r for r in range(10, 18)),
@@ -45,18 +51,21 @@ def engine(name):
     return _engines[name]
 
 
-def run(cfg, name, n, structs, burst=1, protect=0, seed=0x5EED0003):
+def run(cfg, name, n, structs, burst=1, protect=0, seed=0x5EED0003, opc=0):
     e = engine(name)
     e.set_campaign(seed, structs, burst)
     e.set_protect(protect)
+    e.set_protect_opclasses(opc)
     e.run_trials(0, n)   # warm: code objects and work buffers sized for n
     t0 = time.perf_counter()
     out, h = e.run_trials(0, n)
     dt = time.perf_counter() - t0
     e.set_protect(0)
+    e.set_protect_opclasses(0)
     cls = h["counts"].sum(axis=(0, 1))
     rec = {"config": cfg, "workload": name, "golden_ninst": int(e.golden.ninst), "trials": n,
-           "structures": hex(structs), "burst": burst, "protect_mask": hex(protect), "seconds": dt,
+           "structures": hex(structs), "burst": burst, "protect_mask": hex(protect), "protect_opclasses": hex(opc),
+           "seconds": dt,
            "trials_per_s": n / dt, **{CLASS_NAMES[i]: int(cls[i]) for i in range(6)},
            "crash_sub": {CRASH_NAMES.get(i, str(i)): int(h["crash_sub"][i]) for i in range(16) if h["crash_sub"][i]},
            "escape_sub": {ESCAPE_NAMES.get(i, str(i)): int(h["escape_sub"][i]) for i in range(8)
@@ -81,6 +90,11 @@ def main():
         r = run("C5", "crc32", 100_000, REGS | PC, protect=m)[0]
         r["mask_name"] = label
         recs.append(r)
+    for w in ("crc32", "qsort"):
+        for label, m in OPC.items():
+            r = run("C5b", w, 100_000, RESULT, opc=m)[0]
+            r["opclass_name"] = label
+            recs.append(r)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"{tag}_campaigns.json"), "w") as f:
         json.dump(recs, f, indent=1)
