@@ -1,0 +1,128 @@
+"""Known-answer vectors for the oracle's M-extension and shift semantics (CPU).
+
+Expected values are computed here straight from the reference's definitions:
+- div/divu/rem/remu edge cases: `src/arch/riscv/utility.hh:191-231`
+  (x/0 -> -1 or all-ones, rem x/0 -> x, INT_MIN/-1 -> INT_MIN with rem 0);
+- mulh/mulhsu/mulhu through a double-width product: `utility.hh:171-189`;
+- the W forms: `src/arch/riscv/isa/decoder.isa:2627-2689` (operands
+  truncated to 32 bits, result sign-extended from 32 bits, also for the
+  unsigned divuw/remuw);
+- shift amounts: 6 bits for sll/srl/sra (`decoder.isa:2404-2551`), 5 bits
+  for sllw/srlw/sraw (`:2638-2672`).
+Each instruction runs through `or_probe` (one instruction in a scratch
+machine), the same entry the GPU parity tests use.
+"""
+import itertools
+import os
+import random
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, os.path.join(ROOT, "tools", "rvasm"))
+from rvasm import enc_r  # noqa: E402
+
+M64 = (1 << 64) - 1
+M32 = (1 << 32) - 1
+
+
+def s64(v):
+    v &= M64
+    return v - (1 << 64) if v >> 63 else v
+
+
+def s32(v):
+    v &= M32
+    return v - (1 << 32) if v >> 31 else v
+
+
+def tdiv(a, b):   # C++ truncating division
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b >= 0) else -q
+
+
+def div(a, b, bits):
+    lo = -(1 << (bits - 1))
+    if b == 0:
+        return -1
+    if a == lo and b == -1:
+        return lo
+    return tdiv(a, b)
+
+
+def rem(a, b, bits):
+    lo = -(1 << (bits - 1))
+    if b == 0:
+        return a
+    if a == lo and b == -1:
+        return 0
+    return a - tdiv(a, b) * b
+
+
+def divu(a, b, bits):
+    return (1 << bits) - 1 if b == 0 else a // b
+
+
+def remu(a, b):
+    return a if b == 0 else a % b
+
+
+# (name, opcode, funct3, funct7, model(a, b) -> value as a Python int)
+OPS = [
+    ("mul", 0x33, 0, 1, lambda a, b: a * b),
+    ("mulh", 0x33, 1, 1, lambda a, b: (s64(a) * s64(b)) >> 64),
+    ("mulhsu", 0x33, 2, 1, lambda a, b: (s64(a) * b) >> 64),
+    ("mulhu", 0x33, 3, 1, lambda a, b: (a * b) >> 64),
+    ("div", 0x33, 4, 1, lambda a, b: div(s64(a), s64(b), 64)),
+    ("divu", 0x33, 5, 1, lambda a, b: divu(a, b, 64)),
+    ("rem", 0x33, 6, 1, lambda a, b: rem(s64(a), s64(b), 64)),
+    ("remu", 0x33, 7, 1, lambda a, b: remu(a, b)),
+    ("mulw", 0x3B, 0, 1, lambda a, b: s32(s32(a) * s32(b))),
+    ("divw", 0x3B, 4, 1, lambda a, b: s32(div(s32(a), s32(b), 32))),
+    ("divuw", 0x3B, 5, 1, lambda a, b: s32(divu(a & M32, b & M32, 32))),
+    ("remw", 0x3B, 6, 1, lambda a, b: s32(rem(s32(a), s32(b), 32))),
+    ("remuw", 0x3B, 7, 1, lambda a, b: s32(remu(a & M32, b & M32))),
+    ("sll", 0x33, 1, 0, lambda a, b: a << (b & 63)),
+    ("srl", 0x33, 5, 0, lambda a, b: a >> (b & 63)),
+    ("sra", 0x33, 5, 0x20, lambda a, b: s64(a) >> (b & 63)),
+    ("sllw", 0x3B, 1, 0, lambda a, b: s32(a << (b & 31))),
+    ("srlw", 0x3B, 5, 0, lambda a, b: s32((a & M32) >> (b & 31))),
+    ("sraw", 0x3B, 5, 0x20, lambda a, b: s32(a) >> (b & 31)),
+]
+
+EDGE = [0, 1, 2, 3, 7, M64, M64 - 1, 1 << 63, (1 << 63) - 1, 1 << 31, (1 << 31) - 1, M32, 1 << 32,
+        0xFFFFFFFF80000000, 0x8000000000000001, 0x123456789ABCDEF0, 63, 64, 31, 32]
+
+
+def vectors():
+    rng = random.Random(0x5EED)
+    pairs = list(itertools.product(EDGE, EDGE))
+    pairs += [(rng.getrandbits(64), rng.getrandbits(64)) for _ in range(200)]
+    pairs += [(rng.getrandbits(64), rng.choice([0, 1, M64, rng.getrandbits(8)])) for _ in range(100)]
+    return pairs
+
+
+@pytest.mark.parametrize("name,opc,f3,f7,model", OPS, ids=[o[0] for o in OPS])
+def test_m_extension_and_shifts(oracle_mod, name, opc, f3, f7, model):
+    inst = enc_r(opc, f3, f7, 10, 11, 12)   # name a0, a1, a2
+    bad = []
+    for a, b in vectors():
+        regs = [0] * 32
+        regs[11], regs[12] = a, b
+        p = oracle_mod.probe(inst, 0x10000, regs)
+        want = model(a, b) & M64
+        assert p.fault == 0 and p.rd == 10 and p.len == 4 and p.npc == 0x10004
+        if p.rd_value != want:
+            bad.append((hex(a), hex(b), hex(p.rd_value), hex(want)))
+    assert not bad, f"{name}: {len(bad)} mismatches, first {bad[:3]}"
+
+
+def test_x0_destination_is_dropped(oracle_mod):
+    """Writes to x0 are discarded (`regs/int.hh:65-79`, x0 = InvalidRegClass)."""
+    inst = enc_r(0x33, 0, 1, 0, 11, 12)      # mul x0, a1, a2
+    regs = [0] * 32
+    regs[11], regs[12] = 3, 5
+    p = oracle_mod.probe(inst, 0x10000, regs)
+    assert p.fault == 0 and p.rd_value == 0
