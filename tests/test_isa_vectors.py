@@ -1,4 +1,4 @@
-"""Known-answer vectors for the oracle's M-extension and shift semantics (CPU).
+"""Known-answer vectors for the oracle's M-extension, shift, bit-manipulation and Zicond semantics (CPU).
 
 Expected values are computed here straight from the reference's definitions:
 - div/divu/rem/remu edge cases: `src/arch/riscv/utility.hh:191-231`
@@ -126,3 +126,54 @@ def test_x0_destination_is_dropped(oracle_mod):
     regs[11], regs[12] = 3, 5
     p = oracle_mod.probe(inst, 0x10000, regs)
     assert p.fault == 0 and p.rd_value == 0
+
+
+def clmul128(a, b):
+    r = 0
+    for i in range(64):
+        if (b >> i) & 1:
+            r ^= a << i
+    return r
+
+
+# Zba/Zbb/Zbc/Zbs/Zicond register-register forms (OP, opcode 0x33):
+# `decoder.isa:2414-2612`.  XLEN = 64, so rvSext/rvZext are identities.
+BITMANIP = [
+    ("clmul", 1, 0x05, lambda a, b: clmul128(a, b)),
+    ("clmulr", 2, 0x05, lambda a, b: clmul128(a, b) >> 63),
+    ("clmulh", 3, 0x05, lambda a, b: clmul128(a, b) >> 64),
+    ("bset", 1, 0x14, lambda a, b: a | (1 << (b & 63))),
+    ("bclr", 1, 0x24, lambda a, b: a & ~(1 << (b & 63))),
+    ("binv", 1, 0x34, lambda a, b: a ^ (1 << (b & 63))),
+    ("bext", 5, 0x24, lambda a, b: (a >> (b & 63)) & 1),
+    ("rol", 1, 0x30, lambda a, b: (a << (b & 63)) | (a >> ((64 - (b & 63)) & 63))),
+    ("ror", 5, 0x30, lambda a, b: (a >> (b & 63)) | (a << ((64 - (b & 63)) & 63))),
+    ("sh1add", 2, 0x10, lambda a, b: (a << 1) + b),
+    ("sh2add", 4, 0x10, lambda a, b: (a << 2) + b),
+    ("sh3add", 6, 0x10, lambda a, b: (a << 3) + b),
+    ("xnor", 4, 0x20, lambda a, b: ~(a ^ b)),
+    ("orn", 6, 0x20, lambda a, b: a | ~b),
+    ("andn", 7, 0x20, lambda a, b: a & ~b),
+    ("min", 4, 0x05, lambda a, b: min(s64(a), s64(b))),
+    ("minu", 5, 0x05, lambda a, b: min(a, b)),
+    ("max", 6, 0x05, lambda a, b: max(s64(a), s64(b))),
+    ("maxu", 7, 0x05, lambda a, b: max(a, b)),
+    ("czero_eqz", 5, 0x07, lambda a, b: 0 if b == 0 else a),
+    ("czero_nez", 7, 0x07, lambda a, b: 0 if b != 0 else a),
+]
+
+
+@pytest.mark.parametrize("name,f3,f7,model", BITMANIP, ids=[o[0] for o in BITMANIP])
+def test_bitmanip_and_zicond(oracle_mod, name, f3, f7, model):
+    inst = enc_r(0x33, f3, f7, 10, 11, 12)
+    assert oracle_mod.mnemonic(inst).replace(".", "_") == name
+    bad = []
+    for a, b in vectors():
+        regs = [0] * 32
+        regs[11], regs[12] = a, b
+        p = oracle_mod.probe(inst, 0x10000, regs)
+        want = model(a, b) & M64
+        assert p.fault == 0 and p.rd == 10
+        if p.rd_value != want:
+            bad.append((hex(a), hex(b), hex(p.rd_value), hex(want)))
+    assert not bad, f"{name}: {len(bad)} mismatches, first {bad[:3]}"
