@@ -177,3 +177,82 @@ def test_bitmanip_and_zicond(oracle_mod, name, f3, f7, model):
         if p.rd_value != want:
             bad.append((hex(a), hex(b), hex(p.rd_value), hex(want)))
     assert not bad, f"{name}: {len(bad)} mismatches, first {bad[:3]}"
+
+
+# ---- the same vectors as a guest program (device known-answer workload) ----
+# Every R-type op above runs on every (a, b) pair inside one RV64 process that
+# writes the results to stdout, 8 bytes each, pair-major.  The GPU test checks
+# the device's golden stdout against the models and runs no-fault trials
+# through the pre-decoded and translated paths (tests/test_gpu_parity.py).
+ALL_OPS = [(n, opc, f3, f7, m) for (n, opc, f3, f7, m) in OPS] + \
+          [(n, 0x33, f3, f7, m) for (n, f3, f7, m) in BITMANIP]
+
+
+def program_pairs():
+    rng = random.Random(0x15A)
+    edge = EDGE[:14]
+    pairs = list(itertools.product(edge, edge))
+    pairs += [(rng.getrandbits(64), rng.getrandbits(64)) for _ in range(40)]
+    pairs += [(rng.getrandbits(64), rng.choice([0, 1, M64, rng.getrandbits(8)])) for _ in range(20)]
+    return pairs
+
+
+def program_source() -> str:
+    pairs = program_pairs()
+    body = []
+    for k, (_, opc, f3, f7, _m) in enumerate(ALL_OPS):
+        body.append(f"    .word {enc_r(opc, f3, f7, 10, 11, 12):#010x}")
+        body.append(f"    sd    a0, {8 * k}(s2)")
+    n_out = 8 * len(ALL_OPS) * len(pairs)
+    data = "\n".join(f"    .dword {a:#x}, {b:#x}" for a, b in pairs)
+    return f"""    .text
+_start:
+    la    s0, vec
+    li    s1, {len(pairs)}
+    la    s2, out
+loop:
+    ld    a1, 0(s0)
+    ld    a2, 8(s0)
+{chr(10).join(body)}
+    addi  s0, s0, 16
+    addi  s2, s2, {8 * len(ALL_OPS)}
+    addi  s1, s1, -1
+    bnez  s1, loop
+    li    a0, 1
+    la    a1, out
+    li    a2, {n_out}
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 94
+    ecall
+    .data
+    .balign 8
+vec:
+{data}
+    .bss
+    .balign 8
+out:
+    .zero {n_out}
+"""
+
+
+def program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(program_source())
+
+
+def program_expected() -> bytes:
+    out = bytearray()
+    for a, b in program_pairs():
+        for (_, _, _, _, m) in ALL_OPS:
+            out += ((m(a, b)) & M64).to_bytes(8, "little")
+    return bytes(out)
+
+
+def test_alu_program_on_oracle(oracle_mod):
+    """The guest program's stdout on the oracle equals the models."""
+    o = oracle_mod.Oracle(program_elf(), "alu")
+    g = o.run_golden()
+    assert g.exit_code == 0
+    assert o.golden_stdout() == program_expected()
