@@ -22,7 +22,7 @@ import pytest
 from conftest import ROOT
 
 sys.path.insert(0, os.path.join(ROOT, "tools", "rvasm"))
-from rvasm import enc_r  # noqa: E402
+from rvasm import enc_i, enc_r  # noqa: E402
 
 M64 = (1 << 64) - 1
 M32 = (1 << 32) - 1
@@ -179,13 +179,80 @@ def test_bitmanip_and_zicond(oracle_mod, name, f3, f7, model):
     assert not bad, f"{name}: {len(bad)} mismatches, first {bad[:3]}"
 
 
+def rot(v, n, w):
+    m = (1 << w) - 1
+    v &= m
+    n %= w
+    return ((v >> n) | (v << (w - n))) & m
+
+
+def sx(v, bits):
+    v &= (1 << bits) - 1
+    return v - (1 << bits) if v >> (bits - 1) else v
+
+
+def orc_b(a):
+    return sum(0xFF << (8 * i) for i in range(8) if (a >> (8 * i)) & 0xFF)
+
+
+# Immediate, unary and W forms, as (name, instruction word, model(a, b)):
+# `decoder.isa:1490-1716` (OP-IMM / OP-IMM-32) and `:2630-2686` (OP-32).
+# rd = a0, rs1 = a1, rs2 = a2 where the format has one.
+UNARY = [
+    ("clz", enc_i(0x13, 1, 10, 11, 0x600), lambda a, b: 64 - a.bit_length()),
+    ("ctz", enc_i(0x13, 1, 10, 11, 0x601), lambda a, b: 64 if a == 0 else (a & -a).bit_length() - 1),
+    ("cpop", enc_i(0x13, 1, 10, 11, 0x602), lambda a, b: bin(a).count("1")),
+    ("sext_b", enc_i(0x13, 1, 10, 11, 0x604), lambda a, b: sx(a, 8)),
+    ("sext_h", enc_i(0x13, 1, 10, 11, 0x605), lambda a, b: sx(a, 16)),
+    # zext.h is packw with rs2 = x0 on RV64 (gem5 decodes it as packw, `decoder.isa:2656`)
+    ("packw", enc_r(0x3B, 4, 0x04, 10, 11, 12), lambda a, b: sx(((b & 0xFFFF) << 16) | (a & 0xFFFF), 32)),
+    ("rev8", enc_i(0x13, 5, 10, 11, 0x6B8), lambda a, b: int.from_bytes(a.to_bytes(8, "little"), "big")),
+    ("orc_b", enc_i(0x13, 5, 10, 11, 0x287), lambda a, b: orc_b(a)),
+    ("rori", enc_i(0x13, 5, 10, 11, 0x600 | 13), lambda a, b: rot(a, 13, 64)),
+    ("bexti", enc_i(0x13, 5, 10, 11, 0x480 | 40), lambda a, b: (a >> 40) & 1),
+    ("bseti", enc_i(0x13, 1, 10, 11, 0x280 | 63), lambda a, b: a | (1 << 63)),
+    ("bclri", enc_i(0x13, 1, 10, 11, 0x480 | 5), lambda a, b: a & ~(1 << 5)),
+    ("binvi", enc_i(0x13, 1, 10, 11, 0x680 | 33), lambda a, b: a ^ (1 << 33)),
+    ("addiw", enc_i(0x1B, 0, 10, 11, -1), lambda a, b: sx(a - 1, 32)),
+    ("slli_uw", enc_i(0x1B, 1, 10, 11, 0x080 | 33), lambda a, b: (a & M32) << 33),
+    ("clzw", enc_i(0x1B, 1, 10, 11, 0x600), lambda a, b: 32 - (a & M32).bit_length()),
+    ("ctzw", enc_i(0x1B, 1, 10, 11, 0x601),
+     lambda a, b: 32 if a & M32 == 0 else ((a & M32) & -(a & M32)).bit_length() - 1),
+    ("cpopw", enc_i(0x1B, 1, 10, 11, 0x602), lambda a, b: bin(a & M32).count("1")),
+    ("roriw", enc_i(0x1B, 5, 10, 11, 0x600 | 7), lambda a, b: sx(rot(a, 7, 32), 32)),
+    ("addw", enc_r(0x3B, 0, 0x00, 10, 11, 12), lambda a, b: sx(a + b, 32)),
+    ("subw", enc_r(0x3B, 0, 0x20, 10, 11, 12), lambda a, b: sx(a - b, 32)),
+    ("add_uw", enc_r(0x3B, 0, 0x04, 10, 11, 12), lambda a, b: (a & M32) + b),
+    ("sh1add_uw", enc_r(0x3B, 2, 0x10, 10, 11, 12), lambda a, b: ((a & M32) << 1) + b),
+    ("sh2add_uw", enc_r(0x3B, 4, 0x10, 10, 11, 12), lambda a, b: ((a & M32) << 2) + b),
+    ("sh3add_uw", enc_r(0x3B, 6, 0x10, 10, 11, 12), lambda a, b: ((a & M32) << 3) + b),
+    ("rolw", enc_r(0x3B, 1, 0x30, 10, 11, 12), lambda a, b: sx(rot(a, 32 - (b & 31), 32), 32)),
+    ("rorw", enc_r(0x3B, 5, 0x30, 10, 11, 12), lambda a, b: sx(rot(a, b & 31, 32), 32)),
+]
+
+
+@pytest.mark.parametrize("name,word,model", UNARY, ids=[o[0] for o in UNARY])
+def test_immediate_unary_and_w_forms(oracle_mod, name, word, model):
+    assert oracle_mod.mnemonic(word).replace(".", "_") == name
+    bad = []
+    for a, b in vectors():
+        regs = [0] * 32
+        regs[11], regs[12] = a, b
+        p = oracle_mod.probe(word, 0x10000, regs)
+        want = model(a, b) & M64
+        assert p.fault == 0 and p.rd == 10
+        if p.rd_value != want:
+            bad.append((hex(a), hex(b), hex(p.rd_value), hex(want)))
+    assert not bad, f"{name}: {len(bad)} mismatches, first {bad[:3]}"
+
+
 # ---- the same vectors as a guest program (device known-answer workload) ----
 # Every R-type op above runs on every (a, b) pair inside one RV64 process that
 # writes the results to stdout, 8 bytes each, pair-major.  The GPU test checks
 # the device's golden stdout against the models and runs no-fault trials
 # through the pre-decoded and translated paths (tests/test_gpu_parity.py).
-ALL_OPS = [(n, opc, f3, f7, m) for (n, opc, f3, f7, m) in OPS] + \
-          [(n, 0x33, f3, f7, m) for (n, f3, f7, m) in BITMANIP]
+ALL_OPS = [(n, enc_r(opc, f3, f7, 10, 11, 12), m) for (n, opc, f3, f7, m) in OPS] + \
+          [(n, enc_r(0x33, f3, f7, 10, 11, 12), m) for (n, f3, f7, m) in BITMANIP] + UNARY
 
 
 def program_pairs():
@@ -200,8 +267,8 @@ def program_pairs():
 def program_source() -> str:
     pairs = program_pairs()
     body = []
-    for k, (_, opc, f3, f7, _m) in enumerate(ALL_OPS):
-        body.append(f"    .word {enc_r(opc, f3, f7, 10, 11, 12):#010x}")
+    for k, (_, word, _m) in enumerate(ALL_OPS):
+        body.append(f"    .word {word:#010x}")
         body.append(f"    sd    a0, {8 * k}(s2)")
     n_out = 8 * len(ALL_OPS) * len(pairs)
     data = "\n".join(f"    .dword {a:#x}, {b:#x}" for a, b in pairs)
@@ -245,7 +312,7 @@ def program_elf() -> bytes:
 def program_expected() -> bytes:
     out = bytearray()
     for a, b in program_pairs():
-        for (_, _, _, _, m) in ALL_OPS:
+        for (_, _, m) in ALL_OPS:
             out += ((m(a, b)) & M64).to_bytes(8, "little")
     return bytes(out)
 
