@@ -248,24 +248,27 @@ def test_native_driver_matches_engine(engine_factory, tmp_path):
     assert hist["counts"].tobytes() == rh["counts"].tobytes()
 
 
-def test_alu_known_answer_program(oracle_mod):
-    """M/shift/bit-manipulation/Zicond known answers on the device.
+@pytest.mark.parametrize("prog", ["alu", "mem"])
+def test_known_answer_programs(oracle_mod, prog):
+    """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
-    The guest program of tests/test_isa_vectors.py runs every R-type op on
-    every vector pair and writes the results to stdout.  The device golden run
-    (general interpreter) must print exactly the reference-derived models;
-    no-fault trials (pre-decoded and translated paths, from snapshots) must
-    end masked with the oracle's records; faulted trials must match the
-    oracle bit for bit."""
+    alu: every M/shift/bit-manipulation/Zicond op on every vector pair.
+    mem: sb/sh/sw/sd then all seven loads at misaligned, 64-byte-line-crossing
+    and page-crossing offsets.  The device golden run (general interpreter)
+    must print exactly the reference-derived models; no-fault trials
+    (pre-decoded and translated paths, from snapshots) must end masked with
+    the oracle's records; faulted trials must match the oracle bit for bit."""
     from shrewd_amd import Engine
-    from test_isa_vectors import program_elf, program_expected
-    elf = program_elf()
+    import test_isa_vectors as kat
+    elf, expected = {"alu": (kat.program_elf, kat.program_expected),
+                     "mem": (kat.mem_program_elf, kat.mem_program_expected)}[prog]
+    elf, expected = elf(), expected()
     e = Engine(private_pages=64)
-    e.load_elf(elf, ["alu"])
+    e.load_elf(elf, [prog])
     g = e.golden_run()
     assert g.exit_code == 0
-    assert e.golden_stdout() == program_expected()
-    o = oracle_mod.Oracle(elf, "alu")
+    assert e.golden_stdout() == expected
+    o = oracle_mod.Oracle(elf, prog)
     o.run_golden()
     e.set_campaign(0x5EED00A1, REGS | PC, 1)
     e.set_protect(0)

@@ -323,3 +323,90 @@ def test_alu_program_on_oracle(oracle_mod):
     g = o.run_golden()
     assert g.exit_code == 0
     assert o.golden_stdout() == program_expected()
+
+
+# ---- misaligned and line/page-crossing loads and stores (guest program) ----
+# SE mode has no alignment check and no read-only pages; an access is split at
+# 64-byte lines (`atomic.cc:331-545`, `tlb.cc:573-604`), little-endian.  Each
+# case stores one value with sb/sh/sw/sd at buf+off, then loads it back with
+# all seven load forms; the 8-byte results go to stdout.  buf is two pages.
+MEM_OFFS = [0, 1, 2, 3, 5, 7, 30, 57, 59, 61, 62, 63, 4033, 4039, 4089, 4091, 4093, 4094, 4095]
+STORES = [("sb", 1), ("sh", 2), ("sw", 4), ("sd", 8)]
+LOADS = [("lb", 1, True), ("lbu", 1, False), ("lh", 2, True), ("lhu", 2, False),
+         ("lw", 4, True), ("lwu", 4, False), ("ld", 8, False)]
+
+
+def mem_cases():
+    rng = random.Random(0x3E3)
+    return [(off, st, rng.getrandbits(64) | (1 << 63 if k % 2 else 0))
+            for k, (st, off) in enumerate(itertools.product(STORES, MEM_OFFS))]
+
+
+def mem_program_source() -> str:
+    # one loop per store width over MEM_OFFS (short code: the translated
+    # blocks stay small)
+    cases = mem_cases()
+    lines = []
+    for st, _ in STORES:
+        lines += [f"    li    s1, {len(MEM_OFFS)}", f"loop_{st}:", "    ld    t2, 0(s3)", "    addi  s3, s3, 8",
+                  "    ld    t0, 0(s4)", "    addi  s4, s4, 8", "    add   t1, s0, t0", f"    {st:<5} t2, 0(t1)"]
+        for k, (ld, _, _) in enumerate(LOADS):
+            lines += [f"    {ld:<5} a0, 0(t1)", f"    sd    a0, {8 * k}(s2)"]
+        lines += [f"    addi  s2, s2, {8 * len(LOADS)}", "    addi  s1, s1, -1", f"    bnez  s1, loop_{st}"]
+    n_out = 8 * len(LOADS) * len(cases)
+    vals = "\n".join(f"    .dword {v:#x}" for _, _, v in cases)
+    offs = "\n".join(f"    .dword {o}" for o, _, _ in cases)
+    return f"""    .text
+_start:
+    la    s0, buf
+    la    s2, out
+    la    s3, vals
+    la    s4, offs
+{chr(10).join(lines)}
+    li    a0, 1
+    la    a1, out
+    li    a2, {n_out}
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 94
+    ecall
+    .data
+    .balign 8
+vals:
+{vals}
+offs:
+{offs}
+    .bss
+    .balign 4096
+buf:
+    .zero 8192
+out:
+    .zero {n_out}
+"""
+
+
+def mem_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(mem_program_source())
+
+
+def mem_program_expected() -> bytes:
+    mem = bytearray(8192 + 8)
+    out = bytearray()
+    for off, (_, w), v in mem_cases():
+        mem[off:off + w] = (v & ((1 << (8 * w)) - 1)).to_bytes(w, "little")
+        for _, lw, signed in LOADS:
+            x = int.from_bytes(mem[off:off + lw], "little")
+            if signed:
+                x = sx(x, 8 * lw)
+            out += (x & M64).to_bytes(8, "little")
+    return bytes(out)
+
+
+def test_mem_program_on_oracle(oracle_mod):
+    """Misaligned, line-crossing and page-crossing accesses on the oracle."""
+    o = oracle_mod.Oracle(mem_program_elf(), "mem")
+    g = o.run_golden()
+    assert g.exit_code == 0
+    assert o.golden_stdout() == mem_program_expected()
