@@ -410,3 +410,109 @@ def test_mem_program_on_oracle(oracle_mod):
     g = o.run_golden()
     assert g.exit_code == 0
     assert o.golden_stdout() == mem_program_expected()
+
+
+# ---- compares and branches (guest program + single-instruction probes) ----
+# slt/sltu/slti/sltiu (`decoder.isa:1555-1560,2476-2500`) and the six
+# conditional branches (`:5891-5936`): a branch case stores 0 if taken, 1 if
+# not.  jalr clears bit 0 of the target (`:5938-5943`).
+CMP_OPS = [
+    ("slt", enc_r(0x33, 2, 0, 10, 11, 12), lambda a, b: int(s64(a) < s64(b))),
+    ("sltu", enc_r(0x33, 3, 0, 10, 11, 12), lambda a, b: int(a < b)),
+    ("slti", enc_i(0x13, 2, 10, 11, -1), lambda a, b: int(s64(a) < -1)),
+    ("sltiu", enc_i(0x13, 3, 10, 11, -1), lambda a, b: int(a < M64)),
+    ("slti", enc_i(0x13, 2, 10, 11, 5), lambda a, b: int(s64(a) < 5)),
+    ("sltiu", enc_i(0x13, 3, 10, 11, 5), lambda a, b: int(a < 5)),
+]
+BRANCHES = [
+    ("beq", lambda a, b: a == b), ("bne", lambda a, b: a != b),
+    ("blt", lambda a, b: s64(a) < s64(b)), ("bge", lambda a, b: s64(a) >= s64(b)),
+    ("bltu", lambda a, b: a < b), ("bgeu", lambda a, b: a >= b),
+]
+
+
+@pytest.mark.parametrize("name,word,model", CMP_OPS, ids=[f"{o[0]}{i}" for i, o in enumerate(CMP_OPS)])
+def test_compare_forms(oracle_mod, name, word, model):
+    assert oracle_mod.mnemonic(word).replace(".", "_") == name
+    for a, b in vectors():
+        regs = [0] * 32
+        regs[11], regs[12] = a, b
+        p = oracle_mod.probe(word, 0x10000, regs)
+        assert p.rd_value == model(a, b), (name, hex(a), hex(b))
+
+
+def test_jalr_clears_bit0_and_links(oracle_mod):
+    for base, imm in ((0x20001, 0), (0x20000, 3), (0x20000, -1), (M64, 2)):
+        word = enc_i(0x67, 0, 1, 11, imm)             # jalr ra, imm(a1)
+        regs = [0] * 32
+        regs[11] = base
+        p = oracle_mod.probe(word, 0x10000, regs)
+        assert p.fault == 0 and p.rd == 1 and p.rd_value == 0x10004
+        assert p.npc == ((base + imm) & M64) & ~1
+
+
+def cmp_program_source() -> str:
+    pairs = program_pairs()
+    body = []
+    k = 0
+    for _, word, _ in CMP_OPS:
+        body += [f"    .word {word:#010x}", f"    sd    a0, {8 * k}(s2)"]
+        k += 1
+    for j, (br, _) in enumerate(BRANCHES):
+        body += ["    li    a0, 0", f"    {br:<5} a1, a2, br_{j}", "    li    a0, 1", f"br_{j}:",
+                 f"    sd    a0, {8 * k}(s2)"]
+        k += 1
+    n_out = 8 * k * len(pairs)
+    data = "\n".join(f"    .dword {a:#x}, {b:#x}" for a, b in pairs)
+    return f"""    .text
+_start:
+    la    s0, vec
+    li    s1, {len(pairs)}
+    la    s2, out
+loop:
+    ld    a1, 0(s0)
+    ld    a2, 8(s0)
+{chr(10).join(body)}
+    addi  s0, s0, 16
+    addi  s2, s2, {8 * k}
+    addi  s1, s1, -1
+    bnez  s1, loop
+    li    a0, 1
+    la    a1, out
+    li    a2, {n_out}
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 94
+    ecall
+    .data
+    .balign 8
+vec:
+{data}
+    .bss
+    .balign 8
+out:
+    .zero {n_out}
+"""
+
+
+def cmp_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(cmp_program_source())
+
+
+def cmp_program_expected() -> bytes:
+    out = bytearray()
+    for a, b in program_pairs():
+        for _, _, m in CMP_OPS:
+            out += m(a, b).to_bytes(8, "little")
+        for _, c in BRANCHES:
+            out += (0 if c(a, b) else 1).to_bytes(8, "little")
+    return bytes(out)
+
+
+def test_cmp_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(cmp_program_elf(), "cmp")
+    g = o.run_golden()
+    assert g.exit_code == 0
+    assert o.golden_stdout() == cmp_program_expected()
