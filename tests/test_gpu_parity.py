@@ -248,7 +248,7 @@ def test_native_driver_matches_engine(engine_factory, tmp_path):
     assert hist["counts"].tobytes() == rh["counts"].tobytes()
 
 
-@pytest.mark.parametrize("prog", ["alu", "mem", "cmp"])
+@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc"])
 def test_known_answer_programs(oracle_mod, prog):
     """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
@@ -256,7 +256,8 @@ def test_known_answer_programs(oracle_mod, prog):
     mem: sb/sh/sw/sd then all seven loads at misaligned, 64-byte-line-crossing
     and page-crossing offsets.
     cmp: slt/sltu/slti/sltiu and the six branches (data-dependent, so the
-    translated code diverges and merges).  The device golden run (general interpreter)
+    translated code diverges and merges).
+    rvc: the compressed (RVC + Zcb) register forms.  The device golden run (general interpreter)
     must print exactly the reference-derived models; no-fault trials
     (pre-decoded and translated paths, from snapshots) must end masked with
     the oracle's records; faulted trials must match the oracle bit for bit."""
@@ -264,7 +265,8 @@ def test_known_answer_programs(oracle_mod, prog):
     import test_isa_vectors as kat
     elf, expected = {"alu": (kat.program_elf, kat.program_expected),
                      "mem": (kat.mem_program_elf, kat.mem_program_expected),
-                     "cmp": (kat.cmp_program_elf, kat.cmp_program_expected)}[prog]
+                     "cmp": (kat.cmp_program_elf, kat.cmp_program_expected),
+                     "rvc": (kat.rvc_program_elf, kat.rvc_program_expected)}[prog]
     elf, expected = elf(), expected()
     e = Engine(private_pages=64)
     e.load_elf(elf, [prog])

@@ -516,3 +516,117 @@ def test_cmp_program_on_oracle(oracle_mod):
     g = o.run_golden()
     assert g.exit_code == 0
     assert o.golden_stdout() == cmp_program_expected()
+
+
+# ---- compressed (RVC + Zcb) register forms, single-instruction probes ----
+# `decoder.isa:43-536`.  rd = rd' = a0 (x10, also the first source), rs2' = a1.
+def _c(f3, b12, b11_7, b6_2, op):
+    return (f3 << 13) | (b12 << 12) | (b11_7 << 7) | (b6_2 << 2) | op
+
+
+def _ca(f6, rdp, f2, rs2p):
+    return (f6 << 10) | (rdp << 7) | (f2 << 5) | (rs2p << 2) | 1
+
+
+def _cb(f2, sh):   # c.srli / c.srai / c.andi on a0 (rd' = 2)
+    return (0b100 << 13) | (((sh >> 5) & 1) << 12) | (f2 << 10) | (2 << 7) | ((sh & 31) << 2) | 1
+
+
+COMPRESSED = [
+    ("c_addi", _c(0, 1, 10, 0b11001, 1), lambda a, b: a - 7),
+    ("c_addiw", _c(1, 1, 10, 0b11001, 1), lambda a, b: sx(a - 7, 32)),
+    ("c_li", _c(2, 1, 10, 0b11001, 1), lambda a, b: -7),
+    ("c_lui", _c(3, 1, 10, 0b00001, 1), lambda a, b: sx(0x21 << 12, 18)),
+    ("c_srli", _cb(0, 33), lambda a, b: a >> 33),
+    ("c_srai", _cb(1, 33), lambda a, b: s64(a) >> 33),
+    ("c_andi", _cb(2, 0x39), lambda a, b: a & -7),
+    ("c_sub", _ca(0b100011, 2, 0, 3), lambda a, b: a - b),
+    ("c_xor", _ca(0b100011, 2, 1, 3), lambda a, b: a ^ b),
+    ("c_or", _ca(0b100011, 2, 2, 3), lambda a, b: a | b),
+    ("c_and", _ca(0b100011, 2, 3, 3), lambda a, b: a & b),
+    ("c_subw", _ca(0b100111, 2, 0, 3), lambda a, b: sx(a - b, 32)),
+    ("c_addw", _ca(0b100111, 2, 1, 3), lambda a, b: sx(a + b, 32)),
+    ("c_mul", _ca(0b100111, 2, 2, 3), lambda a, b: a * b),
+    ("c_zext_b", _ca(0b100111, 2, 3, 0), lambda a, b: a & 0xFF),
+    ("c_sext_b", _ca(0b100111, 2, 3, 1), lambda a, b: sx(a, 8)),
+    ("c_zext_h", _ca(0b100111, 2, 3, 2), lambda a, b: a & 0xFFFF),
+    ("c_sext_h", _ca(0b100111, 2, 3, 3), lambda a, b: sx(a, 16)),
+    ("c_zext_w", _ca(0b100111, 2, 3, 4), lambda a, b: a & M32),
+    ("c_not", _ca(0b100111, 2, 3, 5), lambda a, b: ~a),
+    ("c_slli", _c(0, 1, 10, 1, 2), lambda a, b: a << 33),
+    ("c_mv", _c(4, 0, 10, 11, 2), lambda a, b: b),
+    ("c_add", _c(4, 1, 10, 11, 2), lambda a, b: a + b),
+]
+
+
+@pytest.mark.parametrize("name,word,model", COMPRESSED, ids=[o[0] for o in COMPRESSED])
+def test_compressed_forms(oracle_mod, name, word, model):
+    assert oracle_mod.mnemonic(word).replace(".", "_") == name
+    bad = []
+    for a, b in vectors():
+        regs = [0] * 32
+        regs[10], regs[11] = a, b
+        p = oracle_mod.probe(word, 0x10000, regs)
+        assert p.fault == 0 and p.rd == 10 and p.len == 2 and p.npc == 0x10002
+        want = model(a, b) & M64
+        if p.rd_value != want:
+            bad.append((hex(a), hex(b), hex(p.rd_value), hex(want)))
+    assert not bad, f"{name}: {len(bad)} mismatches, first {bad[:3]}"
+
+
+def rvc_program_source() -> str:
+    pairs = program_pairs()
+    body = []
+    for k, (_, word, _) in enumerate(COMPRESSED):
+        body += ["    ld    a0, 0(s0)", f"    .half {word:#06x}", f"    sd    a0, {8 * k}(s2)"]
+    n_out = 8 * len(COMPRESSED) * len(pairs)
+    data = "\n".join(f"    .dword {a:#x}, {b:#x}" for a, b in pairs)
+    return f"""    .text
+_start:
+    la    s0, vec
+    li    s1, {len(pairs)}
+    la    s2, out
+loop:
+    ld    a1, 8(s0)
+{chr(10).join(body)}
+    addi  s0, s0, 16
+    addi  s2, s2, {8 * len(COMPRESSED)}
+    addi  s1, s1, -1
+    bnez  s1, loop
+    li    a0, 1
+    la    a1, out
+    li    a2, {n_out}
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 94
+    ecall
+    .data
+    .balign 8
+vec:
+{data}
+    .bss
+    .balign 8
+out:
+    .zero {n_out}
+"""
+
+
+def rvc_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(rvc_program_source())
+
+
+def rvc_program_expected() -> bytes:
+    out = bytearray()
+    for a, b in program_pairs():
+        for _, _, m in COMPRESSED:
+            out += (m(a, b) & M64).to_bytes(8, "little")
+    return bytes(out)
+
+
+def test_rvc_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(rvc_program_elf(), "rvc")
+    g = o.run_golden()
+    assert g.exit_code == 0
+    assert o.golden_stdout() == rvc_program_expected()
