@@ -248,7 +248,7 @@ def test_native_driver_matches_engine(engine_factory, tmp_path):
     assert hist["counts"].tobytes() == rh["counts"].tobytes()
 
 
-@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc"])
+@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys"])
 def test_known_answer_programs(oracle_mod, prog):
     """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
@@ -257,7 +257,9 @@ def test_known_answer_programs(oracle_mod, prog):
     and page-crossing offsets.
     cmp: slt/sltu/slti/sltiu and the six branches (data-dependent, so the
     translated code diverges and merges).
-    rvc: the compressed (RVC + Zcb) register forms.  The device golden run (general interpreter)
+    rvc: the compressed (RVC + Zcb) register forms.
+    sys: the modelled syscalls (get*id, write to stdout/stderr/bad fd,
+    an ignored call, exit status & 0xff).  The device golden run (general interpreter)
     must print exactly the reference-derived models; no-fault trials
     (pre-decoded and translated paths, from snapshots) must end masked with
     the oracle's records; faulted trials must match the oracle bit for bit."""
@@ -266,12 +268,14 @@ def test_known_answer_programs(oracle_mod, prog):
     elf, expected = {"alu": (kat.program_elf, kat.program_expected),
                      "mem": (kat.mem_program_elf, kat.mem_program_expected),
                      "cmp": (kat.cmp_program_elf, kat.cmp_program_expected),
-                     "rvc": (kat.rvc_program_elf, kat.rvc_program_expected)}[prog]
+                     "rvc": (kat.rvc_program_elf, kat.rvc_program_expected),
+                     "sys": (kat.sys_program_elf, kat.sys_program_expected)}[prog]
     elf, expected = elf(), expected()
     e = Engine(private_pages=64)
     e.load_elf(elf, [prog])
     g = e.golden_run()
-    assert g.exit_code == 0
+    assert g.exit_code == (300 & 0xFF if prog == "sys" else 0)
+    assert g.stderr_len == (len(kat.SYS_STDERR) if prog == "sys" else 0)
     assert e.golden_stdout() == expected
     o = oracle_mod.Oracle(elf, prog)
     o.run_golden()

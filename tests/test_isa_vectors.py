@@ -630,3 +630,78 @@ def test_rvc_program_on_oracle(oracle_mod):
     g = o.run_golden()
     assert g.exit_code == 0
     assert o.golden_stdout() == rvc_program_expected()
+
+
+# ---- modelled syscalls (guest program) ----
+# get*id return the Process params (`sim/Process.py:61-67`: pid 100, ppid 0,
+# uid/euid/gid/egid 100; gettid -> pid), write to fd > 2 returns -EBADF,
+# write of 0 bytes returns 0, write(2) goes to stderr, an ignoreFunc syscall
+# returns 0 (`syscall_emul.cc:84-104`), exit status is `& 0xff`
+# (`syscall_emul.cc:120-248`).
+SYS_STDERR = b"err!\n?"
+SYS_EXPECTED_VALUES = [100, 0, 100, 100, 100, 100, 100, -9, 0, len(SYS_STDERR), 0]
+
+
+def sys_program_source() -> str:
+    ids = "\n".join(f"    li    a7, {n}\n    ecall\n    sd    a0, {8 * k}(s2)" for k, n in enumerate(range(172, 179)))
+    n_out = 8 * len(SYS_EXPECTED_VALUES)
+    msg = ", ".join(str(c) for c in SYS_STDERR)
+    return f"""    .text
+_start:
+    la    s2, out
+{ids}
+    li    a0, 5
+    mv    a1, s2
+    li    a2, 8
+    li    a7, 64
+    ecall
+    sd    a0, 56(s2)
+    li    a0, 1
+    mv    a1, s2
+    li    a2, 0
+    li    a7, 64
+    ecall
+    sd    a0, 64(s2)
+    li    a0, 2
+    la    a1, msg
+    li    a2, {len(SYS_STDERR)}
+    li    a7, 64
+    ecall
+    sd    a0, 72(s2)
+    li    a0, 12345
+    li    a7, 99
+    ecall
+    sd    a0, 80(s2)
+    li    a0, 1
+    mv    a1, s2
+    li    a2, {n_out}
+    li    a7, 64
+    ecall
+    li    a0, 300
+    li    a7, 93
+    ecall
+    .data
+msg:
+    .byte {msg}
+    .bss
+    .balign 8
+out:
+    .zero {n_out}
+"""
+
+
+def sys_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(sys_program_source())
+
+
+def sys_program_expected() -> bytes:
+    return b"".join((v & M64).to_bytes(8, "little") for v in SYS_EXPECTED_VALUES)
+
+
+def test_sys_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(sys_program_elf(), "sys")
+    g = o.run_golden()
+    assert g.exit_code == 300 & 0xFF
+    assert g.stderr_len == len(SYS_STDERR)
+    assert o.golden_stdout() == sys_program_expected()
