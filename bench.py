@@ -6,9 +6,11 @@ inst/sec.  Workload (configs[1]): the RV64 MiBench-style CRC32 kernel,
 100k register-file + PC single-bit trials per GPU, seeded sites.
 
 One step = one campaign pass over a batch of `--trials` trials per GPU:
-device-side site sampling, sort by inject time, the interpreter kernel (all
-trials from process start to exit/crash/hang), outcome histogram, and the
-RCCL all-reduce of the histogram (the campaign's only exchange; N > 1).
+device-side site sampling, sort by inject time, the interpreter kernel (each
+trial starts from the golden snapshot at or before its inject time and ends
+at exit / crash / hang, or early as masked once its whole state equals a later
+golden snapshot -- exact), outcome histogram, and the RCCL
+all-reduce of the histogram (the campaign's only exchange; N > 1).
 Trials shard by id across ranks (weak scaling: per-GPU work fixed).
 
 Launch: python bench.py [--gpus 1] [--steps 5] [--warmup 1]
@@ -49,11 +51,36 @@ def parse():
     return ap.parse_args()
 
 
+def host_cores():
+    """Host CPUs this process may run on (the cgroup/affinity share, capped by
+    OMP_NUM_THREADS when the box sets it), the machine's total, and the CPU model."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        avail = min(avail, int(omp))
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return max(1, avail), os.cpu_count() or 1, model
+
+
 def cpu_baseline(elf: bytes, argv0: str, seed: int, budget_s: float):
     """The oracle (plain-C restatement of gem5 RV64 SE, test infrastructure)
-    on the host cores, same campaign, bounded sample."""
+    on every host core this process may use, same campaign, bounded sample.
+    Like a serial gem5 run, the oracle runs every trial from process start to
+    its end (no golden snapshots, no early exit).  Returns the baseline record
+    and the sampled trials' outcomes (kept for the parity check)."""
     from oracle.pyoracle import Oracle
-    threads = max(1, min(16, os.cpu_count() or 1))
+    threads, machine_cpus, model = host_cores()
     o = Oracle(elf, argv0)
     o.run_golden()
     calib = o.sample(seed, 0, 64 * threads, REGS_PC, 1)
@@ -67,10 +94,13 @@ def cpu_baseline(elf: bytes, argv0: str, seed: int, budget_s: float):
     dt = time.perf_counter() - t0
     insts = int(out["ninst"].sum())
     o.close()
-    return {"value": n / dt, "unit": "trials/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} trials of the same {argv0} campaign (seed {seed:#x}, regs+pc), "
-                      f"oracle/rv64se.c with {threads} pthreads, {dt:.1f}s wall",
-            "guest_inst_per_s": insts / dt}
+    rec = {"value": n / dt, "unit": "trials/s", "cores": threads, "kind": "port",
+           "sample": f"first {n} trials of the same {argv0} campaign (seed {seed:#x}, regs+pc), "
+                     f"oracle/rv64se.c with {threads} pthreads, each trial from process start to its end "
+                     f"(no snapshots, no early exit), {dt:.1f}s wall",
+           "host_cpus_total": machine_cpus, "cpu_model": model,
+           "guest_inst_per_s": insts / dt}
+    return rec, out
 
 
 def main():
@@ -146,6 +176,7 @@ def main():
         trials_total = world * T * a.steps
         value = trials_total / elapsed
         guest_ips = int(node_h["guest_insts"]) * a.steps / elapsed
+        device_ips = int(node_h["device_insts"]) * a.steps / elapsed
         # roofline of the dominant kernel (fi_trial_kernel), per launch:
         # algorithmic bytes = fetched instruction bytes + load/store bytes of all
         # executed guest instructions + 264 B initial state + 16 B outcome per
@@ -157,7 +188,7 @@ def main():
         per_launch_bytes = per_step_bytes * a.steps // max(launches, 1)
         avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
         achieved = per_launch_bytes / avg_kernel_s / 1e9
-        traffic = None
+        traffic, issue = None, None
         if os.path.exists(a.traffic_json):
             try:
                 with open(a.traffic_json) as f:
@@ -165,8 +196,9 @@ def main():
                 if (tj.get("workload") == a.workload and tj.get("trials") == T
                         and tj.get("lanes_per_wave", 64) == lanes):
                     traffic = tj.get("hbm_bytes_per_launch")
+                    issue = tj.get("issue")
             except (OSError, ValueError):
-                traffic = None
+                traffic, issue = None, None
         cls = node_h["counts"].sum(axis=(0, 1))
         res = {
             "metric": "fault-injection trials/sec (whole node)",
@@ -186,18 +218,33 @@ def main():
                        "trials_per_gpu": T, "seed": hex(a.seed), "structures": "x1-x31,pc", "burst": 1,
                        "lanes_per_wave": lanes,
                        "parallelism": f"trial-sharded x{world}, RCCL histogram all-reduce"},
-            "guest_inst_per_s": guest_ips,
+            # gem5-equivalent: each trial's numInst at its end, as a serial gem5
+            # run commits it (restored snapshot prefix and skipped golden suffix
+            # of early-masked trials included); device: instructions the GPU
+            # actually executed
+            "guest_inst_per_s_gem5_equiv": guest_ips,
+            "device_inst_per_s": device_ips,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "fi_trial_kernel", "avg_kernel_ms": avg_kernel_s * 1e3,
                          "dispatches_per_step": launches / a.steps,
-                         "algorithmic_bytes_per_launch": per_launch_bytes},
+                         "algorithmic_bytes_per_launch": per_launch_bytes,
+                         # the roof that binds: issue slots (SQ counters of the same
+                         # command, profiles/)
+                         "issue": issue},
             "outcomes": {n: int(cls[i]) for i, n in enumerate(["masked", "sdc", "crash", "hang", "detected",
                                                                  "escape"])},
             "golden_s": golden_s,
         }
+        res["parity"] = None
         if world == 1 and not a.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(elf, a.workload, a.seed, a.cpu_seconds)
+            res["cpu_baseline"], ref = cpu_baseline(elf, a.workload, a.seed, a.cpu_seconds)
+            # the same trial ids through the device (the timed campaign's first
+            # trials): every outcome must equal the oracle's, bit for bit
+            dev, _ = eng.run_trials(0, len(ref))
+            bad = int((dev != ref).sum())
+            res["parity"] = {"checked": int(len(ref)), "mismatches": bad,
+                             "against": "oracle/rv64se.c, trial ids [0, checked) of the benched campaign"}
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)

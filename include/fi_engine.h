@@ -150,10 +150,13 @@ typedef struct {
     uint64_t crash_sub[16];
     uint64_t escape_sub[8];
     uint64_t trials;
-    uint64_t guest_insts;   /* sum of committed instructions over trials */
+    uint64_t guest_insts;   /* sum of each trial's numInst at its end, as a serial gem5 run commits them
+                               (includes the snapshot-restored prefix and a masked trial's golden suffix) */
     uint64_t fetch_bytes;   /* algorithmic bytes: instruction fetch */
     uint64_t data_bytes;    /* algorithmic bytes: loads + stores */
     uint64_t cow_pages;     /* private pages materialised (copy-on-write / zero-fill) */
+    uint64_t device_insts;  /* guest instructions the device actually committed (no restored prefix, no
+                               skipped suffix): the executed-instruction count behind device inst/s */
 } fi_histogram;
 
 typedef struct fi_engine fi_engine;
@@ -169,6 +172,8 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
 fi_status fi_golden_run(fi_engine *e, fi_golden_info *out);
 /* copies up to cap bytes of golden stdout; returns the full length in *len */
 fi_status fi_golden_stdout(fi_engine *e, uint8_t *buf, uint64_t cap, uint64_t *len);
+/* same for the golden run's stderr (fd 2) stream */
+fi_status fi_golden_stderr(fi_engine *e, uint8_t *buf, uint64_t cap, uint64_t *len);
 
 /* Campaign definition: SplitMix64 sites keyed by (seed, trial id); structures
  * is a bitmask (bit r = x_r, bit 32 = pc, bit 33 = memory, bit 34 = instruction

@@ -51,6 +51,8 @@ def lib():
         L.or_golden.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(Golden)]
         L.or_golden_stdout.restype = C.c_uint64
         L.or_golden_stdout.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64]
+        L.or_golden_stderr.restype = C.c_uint64
+        L.or_golden_stderr.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64]
         L.or_sample.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]
         L.or_run_trials.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]
         L.or_run_one_capture.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
@@ -93,8 +95,15 @@ class Oracle:
         return g
 
     def golden_stdout(self) -> bytes:
-        buf = C.create_string_buffer(1 << 20)
-        n = self.L.or_golden_stdout(self.h, buf, 1 << 20)
+        n = self.L.or_golden_stdout(self.h, None, 0)
+        buf = C.create_string_buffer(max(n, 1))
+        self.L.or_golden_stdout(self.h, buf, n)
+        return buf.raw[:n]
+
+    def golden_stderr(self) -> bytes:
+        n = self.L.or_golden_stderr(self.h, None, 0)
+        buf = C.create_string_buffer(max(n, 1))
+        self.L.or_golden_stderr(self.h, buf, n)
         return buf.raw[:n]
 
     def sample(self, seed, first, n, structures, burst=1) -> np.ndarray:

@@ -1394,6 +1394,12 @@ uint64_t or_golden_stdout(or_campaign_t *c, uint8_t *buf, uint64_t cap) {
     return c->gout.len;
 }
 
+uint64_t or_golden_stderr(or_campaign_t *c, uint8_t *buf, uint64_t cap) {
+    u64 n = c->gerr.len < cap ? c->gerr.len : cap;
+    if (n) memcpy(buf, c->gerr.buf, n);
+    return c->gerr.len;
+}
+
 /* ------------------------------------------------------------- sampler */
 /* SplitMix64 (Steele et al. 2014); site = f(seed, trial) only, so it is
  * shard-invariant.  Same definition as shrewd_amd/csrc/hip/sampler. */

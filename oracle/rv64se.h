@@ -84,6 +84,8 @@ const char *or_error(or_campaign_t *c);
 int or_golden(or_campaign_t *c, uint64_t max_inst, or_golden_t *out);
 /* copies golden stdout into buf (up to cap bytes); returns length */
 uint64_t or_golden_stdout(or_campaign_t *c, uint8_t *buf, uint64_t cap);
+/* same for golden stderr */
+uint64_t or_golden_stderr(or_campaign_t *c, uint8_t *buf, uint64_t cap);
 
 /* Counter-based site sampler: SplitMix64 keyed by (seed, trial).  structures
  * is a bitmask over {bit r = x_r (1..31), bit 32 = pc, bit 33 = memory}. */

@@ -770,6 +770,13 @@ fi_status fi_golden_stdout(fi_engine *e, uint8_t *buf, uint64_t cap, uint64_t *l
     return FI_OK;
 }
 
+fi_status fi_golden_stderr(fi_engine *e, uint8_t *buf, uint64_t cap, uint64_t *len) {
+    if (!e || !e->have_golden) return fail(e, FI_E_STATE, "no golden run");
+    if (buf && cap) memcpy(buf, e->gerr.data(), std::min<uint64_t>(cap, e->gerr.size()));
+    if (len) *len = e->gerr.size();
+    return FI_OK;
+}
+
 fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint32_t burst) {
     if (!e) return FI_E_ARG;
     structures &= ~1ULL;

@@ -135,6 +135,7 @@ struct DevCtx {
                                      // [15] golden trace events [16] translated insts [17] translated entries
                                      // [18] slowest wave: iters<<32 | tx permille<<20 | entries [19] iters<<32 | slow
                                      // [20] wave-0 s_memtime delta [21] s_memrealtime delta
+                                     // [22] golden run wrote FP state [23] instructions executed on the device
 };
 
 struct SampleCtx {

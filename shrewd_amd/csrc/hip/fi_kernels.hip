@@ -108,19 +108,46 @@ __global__ void fi_debug_decode_kernel(const uint32_t *raws, uint64_t n, PreInst
 }
 
 // ------------------------------------------------------------------ histogram
-__global__ void fi_hist_kernel(const fi_site *sites, const fi_outcome *out, uint64_t n, fi_histogram *h) {
+// One trial per lane.  The [structure][bit][class] bins are scattered, so each
+// lane adds its own bin; everything else is reduced in the wave first: the
+// crash / escape sub-codes by ballot + popcount (one wave-uniform count per
+// code), the trial and instruction totals by a DPP/shuffle sum, then one
+// atomic per wave and counter.
+__global__ void __launch_bounds__(256) fi_hist_kernel(const fi_site *sites, const fi_outcome *out, uint64_t n,
+                                                      fi_histogram *h) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const fi_site s = sites[i];
-    const fi_outcome o = out[i];
-    const uint32_t t = s.target < FI_N_STRUCT ? s.target : 0;
-    const uint32_t bit = s.mask ? (uint32_t)__builtin_ctzll(s.mask) : 0;
-    const uint32_t cls = o.cls < FI_N_CLASS ? o.cls : FI_ESCAPE;
-    atomicAdd((unsigned long long *)&h->counts[t][bit][cls], 1ULL);
-    if (cls == FI_CRASH) atomicAdd((unsigned long long *)&h->crash_sub[o.sub & 15], 1ULL);
-    if (cls == FI_ESCAPE) atomicAdd((unsigned long long *)&h->escape_sub[o.sub & 7], 1ULL);
-    atomicAdd((unsigned long long *)&h->trials, 1ULL);
-    atomicAdd((unsigned long long *)&h->guest_insts, (unsigned long long)o.ninst);
+    const bool v = i < n;
+    uint32_t cls = FI_N_CLASS, sub = 0;
+    uint64_t ninst = 0;
+    if (v) {
+        const fi_site s = sites[i];
+        const fi_outcome o = out[i];
+        const uint32_t t = s.target < FI_N_STRUCT ? s.target : 0;
+        const uint32_t bit = s.mask ? (uint32_t)__builtin_ctzll(s.mask) : 0;
+        cls = o.cls < FI_N_CLASS ? o.cls : FI_ESCAPE;
+        sub = o.sub;
+        ninst = o.ninst;
+        atomicAdd((unsigned long long *)&h->counts[t][bit][cls], 1ULL);
+    }
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t crash = __ballot(cls == FI_CRASH), esc = __ballot(cls == FI_ESCAPE);
+    if (crash) {
+        for (uint32_t k = 0; k < 16; k++) {
+            const uint32_t c = (uint32_t)__popcll(crash & __ballot((sub & 15) == k));
+            if (c && lane == 0) atomicAdd((unsigned long long *)&h->crash_sub[k], (unsigned long long)c);
+        }
+    }
+    if (esc) {
+        for (uint32_t k = 0; k < 8; k++) {
+            const uint32_t c = (uint32_t)__popcll(esc & __ballot((sub & 7) == k));
+            if (c && lane == 0) atomicAdd((unsigned long long *)&h->escape_sub[k], (unsigned long long)c);
+        }
+    }
+    const uint64_t nt = (uint64_t)__popcll(__ballot(v)), ni = wave_sum64(ninst);
+    if (lane == 0 && nt) {
+        atomicAdd((unsigned long long *)&h->trials, (unsigned long long)nt);
+        atomicAdd((unsigned long long *)&h->guest_insts, (unsigned long long)ni);
+    }
 }
 
 // Epochs: sort keys of the suspended lanes (their pc: lanes of one loop end
@@ -165,6 +192,7 @@ __global__ void fi_hist_stats_kernel(const unsigned long long *stats, fi_histogr
         h->fetch_bytes += stats[0];
         h->data_bytes += stats[1];
         h->cow_pages += stats[2];
+        h->device_insts += stats[23];
     }
 }
 

@@ -680,6 +680,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
     }
     bool suspended = false;
     const uint64_t start_inst = (live && !resume) ? L.ninst : 0;
+    const uint64_t launch_inst = live ? L.ninst : 0;   // executed instructions = L.ninst - this at the end
     uint64_t pages_made = 0;
     uint64_t next_snap = (CX->record && CX->rec_interval) ? 0 : kNone;   // record mode: capture points
     uint32_t snaps_taken = 0;
@@ -1593,7 +1594,9 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
     }
     const uint64_t fb = wave_sum64(L.fetch_b), db = wave_sum64(L.data_b), pm = wave_sum64(pages_made);
     const uint64_t si = wave_sum64(start_inst);
+    const uint64_t xi = wave_sum64(live ? L.ninst - launch_inst : 0);
     if (lane == 0) {
+        atomicAdd(&CX->stats[23], (unsigned long long)xi);
         atomicAdd(&CX->stats[0], (unsigned long long)fb);
         atomicAdd(&CX->stats[1], (unsigned long long)db);
         atomicAdd(&CX->stats[2], (unsigned long long)pm);

@@ -30,7 +30,7 @@ OUTCOME_DT = np.dtype([("cls", "u1"), ("sub", "u1"), ("exit_code", "u1"), ("flag
 SITE_DT = np.dtype([("inst", "<u8"), ("mask", "<u8"), ("addr", "<u8"), ("target", "<u4"), ("trial", "<u4")])
 HIST_DT = np.dtype([("counts", "<u8", (N_STRUCT, 64, 6)), ("crash_sub", "<u8", (16,)), ("escape_sub", "<u8", (8,)),
                     ("trials", "<u8"), ("guest_insts", "<u8"), ("fetch_bytes", "<u8"), ("data_bytes", "<u8"),
-                    ("cow_pages", "<u8")])
+                    ("cow_pages", "<u8"), ("device_insts", "<u8")])
 
 ABI_NAMES = {"zero": 0, "ra": 1, "sp": 2, "gp": 3, "tp": 4, "t0": 5, "t1": 6, "t2": 7, "s0": 8, "fp": 8, "s1": 9,
              **{f"a{i}": 10 + i for i in range(8)}, **{f"s{i}": 16 + i for i in range(2, 12)},
@@ -136,6 +136,7 @@ def lib():
         L.fi_load_elf.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]
         L.fi_golden_run.argtypes = [vp, C.POINTER(GoldenInfo)]
         L.fi_golden_stdout.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.fi_golden_stderr.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.fi_set_campaign.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32]
         L.fi_set_protect.argtypes = [vp, C.c_uint64]
         L.fi_set_protect_opclasses.argtypes = [vp, C.c_uint64]
@@ -214,11 +215,18 @@ class Engine:
         self.golden = g
         return g
 
-    def golden_stdout(self) -> bytes:
+    def _golden_stream(self, fn, what) -> bytes:
         n = C.c_uint64()
-        buf = C.create_string_buffer(1 << 20)
-        self._chk(self.L.fi_golden_stdout(self.h, buf, 1 << 20, C.byref(n)), "fi_golden_stdout")
+        self._chk(fn(self.h, None, 0, C.byref(n)), what)        # length first: no silent truncation
+        buf = C.create_string_buffer(max(n.value, 1))
+        self._chk(fn(self.h, buf, n.value, C.byref(n)), what)
         return buf.raw[:n.value]
+
+    def golden_stdout(self) -> bytes:
+        return self._golden_stream(self.L.fi_golden_stdout, "fi_golden_stdout")
+
+    def golden_stderr(self) -> bytes:
+        return self._golden_stream(self.L.fi_golden_stderr, "fi_golden_stderr")
 
     def set_campaign(self, seed: int, structures, burst: int = 1):
         self._chk(self.L.fi_set_campaign(self.h, seed & (2**64 - 1), structures_mask(structures), burst),

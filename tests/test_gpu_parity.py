@@ -101,7 +101,7 @@ def test_sampler_matches_oracle(engine_factory, oracle_mod, name):
     ("crc32", MEM, 1, 3000),              # C4 memory words
     ("qsort", MEM, 4, 3000),              # C4 bursts
     ("qsort", REGS | PC | MEM, 8, 2000),
-    ("intmix", REGS | PC, 1, 600),        # C3 kernel (sampled)
+    ("intmix", REGS | PC, 1, 5000),       # C3 kernel (sampled)
     ("fpamo", REGS | PC | MEM, 1, 4000),  # F/D data movement + AMOs (the golden run has FP state)
     ("fpamo", REGS | PC, 3, 2000),
 ])
@@ -133,8 +133,13 @@ def test_rewritten_code_bit_exact(engine_factory, oracle_mod):
     compare(dev, ref, sites)
 
 
+S_REGS = (1 << 8) | (1 << 9) | sum(1 << r for r in range(18, 28))     # s0-s11
+T_REGS = (1 << 5) | (1 << 6) | (1 << 7) | sum(1 << r for r in range(28, 32))   # t0-t6
+
+
 @pytest.mark.parametrize("mask", [0, (1 << 1) | (1 << 2) | (1 << 3) | (1 << 4),
-                                  sum(1 << r for r in range(10, 18)), (1 << 32) - 2 | (1 << 32)])
+                                  sum(1 << r for r in range(10, 18)), S_REGS, T_REGS,
+                                  (1 << 32) - 2 | (1 << 32)])
 def test_protect_mask_bit_exact(engine_factory, oracle_mod, mask):
     """C5: selective-replication sweep -- detected-by-replica classification."""
     e = engine_factory("crc32")
@@ -174,6 +179,55 @@ def test_result_faults_bit_exact(engine_factory, oracle_mod, name, opc, n):
     compare(dev, ref, sites)
     if opc and name != "hello":
         assert (dev["cls"] == 4).sum() > 0
+
+
+@pytest.mark.parametrize("name", ["crc32", "qsort", "intmix", "hello"])
+def test_translated_path_active(engine_factory, name):
+    """The load-time translated kernel (fi_trial_kernel_tx) is built and runs:
+    a hipRTC failure would otherwise fall back to the static kernel silently."""
+    e = engine_factory(name)
+    assert e.translate_status() == "", e.translate_status()
+    assert e.golden.translated_blocks > 0 and e.golden.translated_insts > 0
+    e.set_campaign(0x7A11, REGS | PC, 1)
+    e.run_trials(0, 2000)
+    st = e.debug_stats()
+    assert int(st[16]) > 0 and int(st[17]) > 0   # translated instructions, block entries
+
+
+PATH_FLAGS = {
+    "default": 0,
+    "no_translate": 4,                      # FI_CFG_NO_TRANSLATE: interpreter only
+    "from_start": 1 | 2,                    # FI_CFG_NO_SNAPSHOT_START | FI_CFG_NO_EARLY_EXIT
+    "no_epochs": 8,                         # FI_CFG_NO_EPOCHS
+    "pack_runs": 16,                        # FI_CFG_PACK_RUNS
+    "fixed_resume": 32,                     # FI_CFG_FIXED_RESUME
+}
+_PATH_REF = {}
+
+
+@pytest.mark.parametrize("name", ["crc32", "qsort", "intmix"])
+@pytest.mark.parametrize("path", list(PATH_FLAGS))
+def test_execution_paths_bit_exact(engine_factory, oracle_mod, name, path):
+    """Every execution path of the engine (translated blocks, pre-decoded and
+    general interpreter, snapshot start + early exit, epochs and the resume
+    packings) gives the oracle's outcomes on the same sites."""
+    n = 3000
+    e = engine_factory(name, flags=PATH_FLAGS[path], max_trials_per_launch=n)
+    if PATH_FLAGS[path] & 4:
+        assert e.translate_status().startswith("disabled")
+    e.set_campaign(0x5EED0BAD, REGS | PC | MEM, 1)
+    e.set_protect(0)
+    sites = e.sample(0, n)
+    if name not in _PATH_REF:
+        o = oracle_for(oracle_mod, name)
+        _PATH_REF[name] = (sites, o.run_trials(sites, protect_mask=0))
+    rsites, ref = _PATH_REF[name]
+    assert np.array_equal(sites, rsites)
+    dev, hist = e.run_sites(sites)
+    compare(dev, ref, sites)
+    assert int(hist["device_insts"]) <= int(hist["guest_insts"])
+    if PATH_FLAGS[path] & 1:   # from process start with no early exit: the device runs every instruction
+        assert int(hist["device_insts"]) == int(hist["guest_insts"])
 
 
 def test_run_trials_equals_run_sites(engine_factory):
@@ -277,8 +331,10 @@ def test_known_answer_programs(oracle_mod, prog):
     assert g.exit_code == (300 & 0xFF if prog == "sys" else 0)
     assert g.stderr_len == (len(kat.SYS_STDERR) if prog == "sys" else 0)
     assert e.golden_stdout() == expected
+    assert e.golden_stderr() == (kat.SYS_STDERR if prog == "sys" else b"")
     o = oracle_mod.Oracle(elf, prog)
     o.run_golden()
+    assert o.golden_stderr() == e.golden_stderr()
     e.set_campaign(0x5EED00A1, REGS | PC, 1)
     e.set_protect(0)
     sites = e.sample(0, 3000)

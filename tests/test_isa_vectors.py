@@ -705,3 +705,4 @@ def test_sys_program_on_oracle(oracle_mod):
     assert g.exit_code == 300 & 0xFF
     assert g.stderr_len == len(SYS_STDERR)
     assert o.golden_stdout() == sys_program_expected()
+    assert o.golden_stderr() == SYS_STDERR

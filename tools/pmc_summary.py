@@ -55,18 +55,30 @@ def main():
     durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in trace
             if KERNEL in r["Kernel_Name"] and int(r["Grid_Size_X"]) > 64]
     hbm = (2 * fetch + write) * 1024 if fetch is not None and write is not None else None
+    # issue roof: instructions issued per SIMD-cycle (MI355X: 256 CUs x 4
+    # SIMDs; GRBM_GUI_ACTIVE sums the 8 XCDs, SQ_WAVE_CYCLES counts quad-cycles)
+    issue = None
+    if sq.get("GRBM_GUI_ACTIVE") and sq.get("SQ_INSTS_VALU") is not None:
+        cyc = sq["GRBM_GUI_ACTIVE"] / 8
+        simds = 1024
+        issue = {"valu_frac": sq["SQ_INSTS_VALU"] / (simds * cyc),
+                 "salu_frac": sq["SQ_INSTS_SALU"] / (simds * cyc),
+                 "waves_per_simd": sq["SQ_WAVE_CYCLES"] * 4 / cyc / simds,
+                 "clock_ghz": cyc / (sum(durs) / len(durs)) if durs else None,
+                 "source": f"profiles/{tag}_pmc.json"}
     wl = bench["config"]["workload"].split()[0]
     pmc = {"tag": tag, "kernel": KERNEL, "launches_fetch": nf, "launches_write": nw,
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write, "hbm_bytes_per_launch": hbm,
            "trace_avg_ms": sum(durs) / len(durs) / 1e6 if durs else None, "trace_launches": len(durs),
            "bench_avg_kernel_ms": bench["roofline"]["avg_kernel_ms"],
-           "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"], "sq": sq}
+           "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"], "sq": sq,
+           "issue": issue}
     with open(os.path.join(p, f"{tag}_pmc.json"), "w") as f:
         json.dump(pmc, f, indent=1)
     with open(os.path.join(p, "pmc_traffic.json"), "w") as f:
         json.dump({"tag": tag, "workload": wl, "trials": bench["config"]["trials_per_gpu"],
                    "lanes_per_wave": bench["config"].get("lanes_per_wave", 64),
-                   "hbm_bytes_per_launch": hbm, "source": f"profiles/{tag}_pmc.json"}, f, indent=1)
+                   "hbm_bytes_per_launch": hbm, "issue": issue, "source": f"profiles/{tag}_pmc.json"}, f, indent=1)
     print(json.dumps(pmc, indent=1))
 
 
