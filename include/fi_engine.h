@@ -132,6 +132,12 @@ typedef struct {
  * resumed epoch with few survivors spreads them down to one per wave, so that
  * no two diverged survivors share a wave while SIMDs idle) */
 #define FI_CFG_FIXED_RESUME 32u
+/* resumed epochs run on the 64-lane kernel (by default they run on the solo
+ * kernel: one survivor per single-lane wave, trial state in SGPRs, low VGPR use
+ * so that many waves share a SIMD) */
+#define FI_CFG_NO_SOLO 64u
+/* every epoch, the first included, on the solo kernel (A/B and parity checks) */
+#define FI_CFG_SOLO_ALL 128u
 
 typedef struct {
     uint64_t ninst, ncycles;

@@ -13,6 +13,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -28,6 +29,7 @@ hipError_t launch_predecode(const uint8_t *text, uint64_t code_off, uint64_t cod
                            hipStream_t st);
 hipError_t launch_debug_decode(const uint32_t *raws, uint64_t n, PreInst *out, hipStream_t st);
 hipError_t launch_trials(const DevCtx &c, hipStream_t st);
+hipError_t launch_trials_solo(const DevCtx &c, hipStream_t st);
 hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, fi_histogram *h,
                        const unsigned long long *stats, hipStream_t st);
 hipError_t sort_pairs_bytes(uint64_t n, size_t &bytes);
@@ -84,7 +86,7 @@ struct fi_engine {
     bool pre_ok = true;
     // load-time build of the trial kernel with the translated golden blocks
     hipModule_t tx_mod = nullptr;
-    hipFunction_t tx_fn = nullptr;
+    hipFunction_t tx_fn = nullptr, tx_fn_solo = nullptr;
     std::string tx_status = "no golden run";
     std::string tx_body;   // last generated translation (diagnostics)
     std::vector<PreInst> tx_pre;     // its inputs: the pre-decoded text and the golden trace
@@ -148,6 +150,20 @@ static void dfree(T *&p) {
     if (p) { (void)hipFree((void *)p); p = nullptr; }
 }
 
+// Diagnostics (SHREWD_FI_TRACE): a native backtrace on SIGSEGV.
+#include <execinfo.h>
+#include <csignal>
+#include <unistd.h>
+static void segv_trace(int sig) {
+    void *bt[64];
+    const int n = backtrace(bt, 64);
+    const char msg[] = "[fi] fatal signal, native backtrace:\n";
+    (void)!write(2, msg, sizeof msg - 1);
+    backtrace_symbols_fd(bt, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
 extern "C" {
 
 // errors of calls that have no engine yet (fi_create), per host thread
@@ -161,6 +177,7 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
         g_create_err = "fi_create: no HIP device visible (the engine has no CPU fallback)";
         return FI_E_NODEVICE;
     }
+    if (getenv("SHREWD_FI_TRACE")) signal(SIGSEGV, segv_trace);
     fi_engine *e = new fi_engine();
     if (cfg) e->cfg = *cfg;
     if (e->cfg.private_pages == 0) e->cfg.private_pages = 16;
@@ -202,7 +219,7 @@ static void free_snaps(fi_engine *e) { dfree(e->d_snaps); dfree(e->d_tab); dfree
 static void free_tx(fi_engine *e) {
     if (e->tx_mod) (void)hipModuleUnload(e->tx_mod);
     e->tx_mod = nullptr;
-    e->tx_fn = nullptr;
+    e->tx_fn = e->tx_fn_solo = nullptr;
 }
 static void free_image(fi_engine *e) {
     dfree(e->d_pre); dfree(e->d_zero); dfree(e->d_sink);
@@ -735,16 +752,26 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         e->tx_trace = trace;
         hipDeviceProp_t prop;
         HIPCHK(hipGetDeviceProperties(&prop, e->dev));
+        if (const char *dump = getenv("SHREWD_FI_DUMP_TX")) {   // diagnostics: the generated blocks
+            if (FILE *f = fopen(dump, "w")) { fputs(body.c_str(), f); fclose(f); }
+        }
+        const bool trace_jit = getenv("SHREWD_FI_TRACE") != nullptr;
+#define JTRACE(...) do { if (trace_jit) { fprintf(stderr, "[fi jit] " __VA_ARGS__); fflush(stderr); } } while (0)
+        JTRACE("compile (%zu bytes of blocks)\n", body.size());
         std::vector<char> code;
         bool cached = false;
         const std::string err = jit_compile(body, prop.gcnArchName, code, cached);
+        JTRACE("load module (err=%s, %zu bytes)\n", err.c_str(), code.size());
         if (!err.empty()) {
             e->tx_status = err;
         } else if (hipModuleLoadData(&e->tx_mod, code.data()) != hipSuccess ||
-                   hipModuleGetFunction(&e->tx_fn, e->tx_mod, "fi_trial_kernel_tx") != hipSuccess) {
+                   hipModuleGetFunction(&e->tx_fn, e->tx_mod, "fi_trial_kernel_tx") != hipSuccess ||
+                   hipModuleGetFunction(&e->tx_fn_solo, e->tx_mod, "fi_trial_kernel_tx_solo") != hipSuccess) {
             free_tx(e);
             e->tx_status = "code object did not load";
         } else {
+            JTRACE("loaded\n");
+#undef JTRACE
             for (uint32_t h : leaders) pre[h].flags |= kPreLeader;
             HIPCHK(hipMemcpy(e->d_pre, pre.data(), pre.size() * sizeof(PreInst), hipMemcpyHostToDevice));
             e->tx_status = "";
@@ -833,9 +860,14 @@ fi_status fi_sample_sites(fi_engine *e, uint64_t first, uint64_t n, fi_site *out
 
 // The trial kernel: the load-time build with translated blocks when there is
 // one, else the static (interpreter-only) kernel.
-static hipError_t launch_trial_kernel(fi_engine *e, DevCtx &c, hipStream_t st) {
-    if (!e->tx_fn) return launch_trials(c, st);
+// solo: the one-trial-per-wave build, one single-lane workgroup per slot.
+static hipError_t launch_trial_kernel(fi_engine *e, DevCtx &c, hipStream_t st, bool solo) {
     void *args[] = {&c};
+    if (solo) {
+        if (!e->tx_fn_solo) return launch_trials_solo(c, st);
+        return hipModuleLaunchKernel(e->tx_fn_solo, (unsigned)c.n, 1, 1, 1, 1, 1, 0, st, args, nullptr);
+    }
+    if (!e->tx_fn) return launch_trials(c, st);
     const uint32_t gl = (c.resume && c.resume_waves) ? 1u : c.lanes;   // grid for the fewest lanes per wave
     return hipModuleLaunchKernel(e->tx_fn, (unsigned)((c.n + gl - 1) / gl), 1, 1, 64, 1, 1, 0, st, args,
                                  nullptr);
@@ -874,6 +906,7 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     }
     HIPCHK(hipEventRecord(e->ev0, st));
     for (size_t ep = 0; ep < budgets.size(); ep++) {
+        const bool solo = (e->cfg.flags & FI_CFG_SOLO_ALL) || (ep > 0 && !(e->cfg.flags & FI_CFG_NO_SOLO));
         c.wave_budget = budgets[ep];
         c.surv = e->d_surv[ep & 1];
         c.surv_n = e->d_cnt + ep;
@@ -890,7 +923,7 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
             HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_skeys, e->d_skeys2, e->d_svals, e->d_svals2, k, 64, st));
             c.resume = e->d_svals2;
             c.resume_n = e->d_cnt + ep - 1;
-            if (pack) {
+            if (pack && !solo) {
                 // one wave per same-pc run of survivors (<= 64 lanes); the grid
                 // covers the worst case (every survivor alone), surplus waves exit
                 HIPCHK(launch_pack_runs(e->d_skeys2, c.resume_n, k, e->d_wrange + 0, e->d_nwaves + ep, st));
@@ -910,7 +943,8 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
         }
         auto &tp = e->tpool[e->tused++];
         HIPCHK(hipEventRecord(tp.first, st));
-        HIPCHK(launch_trial_kernel(e, c, st));
+        if (solo) { c.lanes = 1; c.resume_waves = 0; c.wrange = nullptr; c.n_waves = nullptr; }
+        HIPCHK(launch_trial_kernel(e, c, st, solo));
         HIPCHK(hipEventRecord(tp.second, st));
     }
     HIPCHK(hipEventRecord(e->ev1, st));

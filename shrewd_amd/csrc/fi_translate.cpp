@@ -447,7 +447,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 g.put("  { const uint64_t t_ = (%s + (uint64_t)(int64_t)%lldLL) & ~1ULL;\n", A.c_str(), (long long)im);
                 if (rd) g.put("    TXSET(%u, %s);\n", rd, ftb);
                 g.put("    %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
-                g.put("    const uint64_t t0_ = readlane64(t_, __ffsll((unsigned long long)gmr) - 1);\n");
+                g.put("    const uint64_t t0_ = rdl64<kNL>(t_, __ffsll((unsigned long long)gmr) - 1);\n");
                 g.put("    if (TXB(mine && t_ != t0_)) { dpc = t_; jdiv = mine; goto tx_out; }\n");
                 g.put("    spc = uni64(t0_); goto tx_dispatch; }\n");
                 break;

@@ -28,6 +28,32 @@
 
 namespace fi {
 
+// Lanes per wave.  Every kernel below is instantiated twice from the same
+// source: the campaign kernel runs 64 trials per wave (kNL = 64); the solo
+// kernel runs one trial per single-lane wave (kNL = 1), for the diverged
+// survivors of resumed epochs.  In the solo instantiation the lane index is
+// the constant 0, so every per-trial value is wave-uniform: the compiler keeps
+// the trial state in SGPRs, VGPR use drops, and many more waves share a SIMD
+// to hide the memory latency of serial trials.  Same semantics, same code.
+template <uint32_t kNL> __device__ __forceinline__ uint32_t lane_id() {
+    return kNL == 1 ? 0u : (uint32_t)threadIdx.x;
+}
+template <uint32_t kNL> __device__ __forceinline__ uint64_t wmin64(uint64_t v) {
+    return kNL == 1 ? v : wave_min64(v);
+}
+template <uint32_t kNL> __device__ __forceinline__ uint64_t wsum64(uint64_t v) {
+    return kNL == 1 ? v : wave_sum64(v);
+}
+template <uint32_t kNL> __device__ __forceinline__ uint64_t rdl64(uint64_t v, int l) {
+    return kNL == 1 ? v : readlane64(v, l);
+}
+template <uint32_t kNL> __device__ __forceinline__ uint32_t rdl32(uint32_t v, int l) {
+    return kNL == 1 ? v : (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+template <uint32_t kNL> __device__ __forceinline__ uint64_t wballot(bool x) {
+    return kNL == 1 ? (uint64_t)x : (uint64_t)__ballot(x);
+}
+
 constexpr uint64_t kNone = ~0ULL;
 constexpr uint32_t kSinkRow = 32;
 constexpr uint32_t kRows = 33;
@@ -398,10 +424,11 @@ __device__ __forceinline__ void finish(Lane &L, int cls, int sub, int code, uint
     L.res.ninst = L.ninst;
 }
 
-#define RREG(r) R[(uint32_t)(r) * 64u + lane]
+#define RREG(r) R[(uint32_t)(r) * kNL + lane]
 
 // The syscall path of one lane: EmuLinux::syscall (se_workload.cc:95-106)
 // with the golden-output comparator folded into write().
+template <uint32_t kNL>
 __device__ __forceinline__ void do_syscall(KCtx *c, const WaveMem &w, Lane &L, LaneMem &m, uint64_t slot,
                                            uint64_t *R, uint32_t lane) {
     const int num = (int)(uint32_t)RREG(17);
@@ -467,16 +494,23 @@ __device__ __forceinline__ void do_syscall(KCtx *c, const WaveMem &w, Lane &L, L
 // ------------------------------------------------------------------ snapshots
 // Wave-cooperative 4 KiB comparison (all 64 lanes active): each lane compares
 // 64 bytes.
+template <uint32_t kNL>
 __device__ __forceinline__ bool page_eq(const uint8_t *a, const uint8_t *b, uint32_t lane) {
     if (a == b) return true;
     const uint4 *x = (const uint4 *)a, *y = (const uint4 *)b;
     bool eq = true;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint4 u = x[lane + 64 * k], v = y[lane + 64 * k];
+#pragma unroll 4
+    for (uint32_t k = lane; k < 256; k += kNL) {
+        const uint4 u = x[k], v = y[k];
         eq = eq && u.x == v.x && u.y == v.y && u.z == v.z && u.w == v.w;
     }
-    return __ballot(!eq) == 0;
+    return wballot<kNL>(!eq) == 0;
+}
+// Copy one 4 KiB page, the wave cooperating.
+template <uint32_t kNL>
+__device__ __forceinline__ void page_copy(uint4 *dst, const uint4 *src, uint32_t lane) {
+#pragma unroll 4
+    for (uint32_t k = lane; k < 256; k += kNL) dst[k] = src[k];
 }
 
 // Is lane l's memory equal to the golden memory of snapshot S?  (wave-uniform
@@ -484,6 +518,7 @@ __device__ __forceinline__ bool page_eq(const uint8_t *a, const uint8_t *b, uint
 // over the start snapshot's table over zero stack pages; the golden one is
 // S's table over zero stack pages.  Called only once pc, registers, output
 // positions and stack limit already match, so the stack ranges agree.
+template <uint32_t kNL>
 __device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32_t np, const SnapState *S,
                                uint32_t lane) {
     const PageEnt *tk = c->snap_tab + S->tab_off;
@@ -495,7 +530,7 @@ __device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32
         const uint8_t *g = f >= 0 ? c->pool + ((uint64_t)f << 12)
                                   : ((v >= smin && v <= kStackTopVpn) ? c->zero_page : nullptr);
         if (!g) return false;
-        if (!page_eq(priv_frame(c, lslot, i), g, lane)) return false;
+        if (!page_eq<kNL>(priv_frame(c, lslot, i), g, lane)) return false;
     }
     for (uint32_t e = 0; e < nk; e++) {   // golden pages the lane still sees through its start snapshot
         const uint64_t v = uni64(tk[e].vpn);
@@ -507,7 +542,7 @@ __device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32
         const uint8_t *lv = fj >= 0 ? c->pool + ((uint64_t)fj << 12)
                                     : ((v >= smin && v <= kStackTopVpn) ? c->zero_page : nullptr);
         if (!lv) return false;
-        if (!page_eq(lv, c->pool + ((uint64_t)f << 12), lane)) return false;
+        if (!page_eq<kNL>(lv, c->pool + ((uint64_t)f << 12), lane)) return false;
     }
     return true;
 }
@@ -521,12 +556,12 @@ typedef __attribute__((address_space(1))) uint64_t g_u64;
 // a value pinned in a VGPR so that `mine ? v : X` stays a select (a select on
 // a load's result is otherwise turned into a divergent branch around the load,
 // which makes the whole region divergent).
-#define TXB(x) __builtin_amdgcn_ballot_w64(x)
-#define TXSET(r, e)                         \
-    do {                                    \
-        uint64_t t_ = (uint64_t)(e);        \
-        __asm__ volatile("" : "+v"(t_));    \
-        X##r = mine ? t_ : X##r;            \
+#define TXB(x) (kNL == 1 ? (uint64_t)(bool)(x) : (uint64_t)__builtin_amdgcn_ballot_w64(x))
+#define TXSET(r, e)                                         \
+    do {                                                    \
+        uint64_t t_ = (uint64_t)(e);                        \
+        if (kNL > 1) __asm__ volatile("" : "+v"(t_));       \
+        X##r = mine ? t_ : X##r;                            \
     } while (0)
 
 // The pre-decoded text (uniform): table, text range, exact code range.
@@ -597,22 +632,18 @@ __device__ __forceinline__ bool ult64(uint64_t a, uint64_t b) {
 #ifndef FI_WAVES_PER_EU
 #define FI_WAVES_PER_EU 1
 #endif
-#ifdef __HIPCC_RTC__
-extern "C" __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel_tx(DevCtx ctx_arg) {
-#else
-__global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ctx_arg) {
-#endif
-    (void)ctx_arg;
+template <uint32_t kNL>
+__device__ __forceinline__ void trial_body() {
     KCtx *const kc = (KCtx *)__builtin_amdgcn_kernarg_segment_ptr();
 #define CX (opq(kc))
-    __shared__ uint64_t R[kRows * 64];
+    __shared__ uint64_t R[kRows * kNL];
     const uint64_t t_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = lane_id<kNL>();
     // ---- the lane's slot: a fresh launch takes slot = global lane index, a
     // resume launch (epochs) the slots of suspended lanes, sorted by pc
     const bool resume = CX->resume != nullptr;
-    uint32_t nlw = CX->lanes;
-    if (resume && CX->resume_waves) {   // few survivors: fewer per wave (the grid allows one per wave)
+    uint32_t nlw = kNL == 1 ? 1u : CX->lanes;
+    if (kNL > 1 && resume && CX->resume_waves) {   // few survivors: fewer per wave (the grid allows one per wave)
         const uint32_t ns = *CX->resume_n, per = (ns + CX->resume_waves - 1) / CX->resume_waves;
         uint32_t l = 1;
         while (l < per && l < nlw) l <<= 1;
@@ -727,19 +758,17 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
             break;
         }
         // ---- A. materialise requested pages, whole wave cooperating
-        const uint64_t want = __ballot(!L.done && m.req_vpn != kNone);
+        const uint64_t want = wballot<kNL>(!L.done && m.req_vpn != kNone);
         if (want) {
             uint64_t wl = want;
             while (wl) {
                 const int l = __ffsll((unsigned long long)wl) - 1;
                 wl &= wl - 1;
-                const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)m.n_priv, l);
+                const uint32_t np = (uint32_t)rdl32<kNL>((uint32_t)m.n_priv, l);
                 if (np >= CX->priv_pages) continue;
-                const uint64_t lslot = readlane64(slot, l);
-                const uint4 *src = (const uint4 *)readlane64((uint64_t)m.req_src, l);
-                uint4 *dst = (uint4 *)priv_frame(CX, lslot, np);
-#pragma unroll
-                for (int k = 0; k < 4; k++) dst[lane + 64 * k] = src[lane + 64 * k];
+                const uint64_t lslot = rdl64<kNL>(slot, l);
+                const uint4 *src = (const uint4 *)rdl64<kNL>((uint64_t)m.req_src, l);
+                page_copy<kNL>((uint4 *)priv_frame(CX, lslot, np), src, lane);
             }
             __syncthreads();
             if (!L.done && m.req_vpn != kNone) {
@@ -792,33 +821,33 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
 
         // ---- B'. golden comparator at snapshot boundaries (exact early exit)
         if (CX->early_exit) {
-            uint64_t pend = __ballot(!L.done && m.req_vpn == kNone && L.ninst == L.next_chk);
+            uint64_t pend = wballot<kNL>(!L.done && m.req_vpn == kNone && L.ninst == L.next_chk);
             if (pend) __syncthreads();   // the lanes' own stores are complete before others read them
             while (pend) {
                 const int ld = __ffsll((unsigned long long)pend) - 1;
-                const uint64_t kn = uni64(readlane64(L.ninst, ld));
+                const uint64_t kn = uni64(rdl64<kNL>(L.ninst, ld));
                 const bool grp = !L.done && m.req_vpn == kNone && L.ninst == L.next_chk && L.ninst == kn;
-                pend &= ~__ballot(grp);
+                pend &= ~wballot<kNL>(grp);
                 const SnapState *S = CX->snaps + (uint32_t)(kn / CX->snap_interval);
                 bool eq = grp && L.pc == S->pc && L.out_pos == S->out_pos && L.err_pos == S->err_pos && !L.out_bad &&
                           m.stack_min == S->stack_min && !L.fp && L.injected != 3;
-                if (__ballot(eq)) {
+                if (wballot<kNL>(eq)) {
                     // a register the golden future writes before reading it cannot
                     // influence the outcome (liveness from the golden trace)
                     const uint32_t lv = S->live;
 #pragma unroll
                     for (int r = 1; r < 32; r++) eq = eq && (RREG(r) == S->regs[r] || !((lv >> r) & 1));
                 }
-                n_chk += (uint32_t)__popcll(__ballot(grp));
-                uint64_t mm = __ballot(eq);
+                n_chk += (uint32_t)__popcll(wballot<kNL>(grp));
+                uint64_t mm = wballot<kNL>(eq);
                 while (mm) {
                     const int l = __ffsll((unsigned long long)mm) - 1;
                     mm &= mm - 1;
                     WaveMem wl;
-                    wl.tab = (const PageEnt *)readlane64((uint64_t)w.tab, l);
-                    wl.tab_n = (uint32_t)__builtin_amdgcn_readlane((int)w.tab_n, l);
-                    const bool same = lane_mem_equal(CX, wl, readlane64(slot, l),
-                                                     (uint32_t)__builtin_amdgcn_readlane((int)m.n_priv, l), S, lane);
+                    wl.tab = (const PageEnt *)rdl64<kNL>((uint64_t)w.tab, l);
+                    wl.tab_n = (uint32_t)rdl32<kNL>((uint32_t)w.tab_n, l);
+                    const bool same = lane_mem_equal<kNL>(CX, wl, rdl64<kNL>(slot, l),
+                                                     (uint32_t)rdl32<kNL>((uint32_t)m.n_priv, l), S, lane);
                     if ((int)lane == l) eq = same;
                 }
                 if (grp) {
@@ -833,15 +862,15 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                         L.next_chk = nx / CX->snap_interval < CX->n_snap ? nx : kNone;
                     }
                 }
-                n_early += (uint32_t)__popcll(__ballot(grp && eq));
+                n_early += (uint32_t)__popcll(wballot<kNL>(grp && eq));
             }
         }
 
         // ---- B''. record mode: capture a golden snapshot (one live lane)
-        if (CX->record && uni64(readlane64(L.ninst, 0)) == next_snap && !__builtin_amdgcn_readlane((int)L.done, 0)) {
+        if (CX->record && uni64(rdl64<kNL>(L.ninst, 0)) == next_snap && !rdl32<kNL>((uint32_t)L.done, 0)) {
             if (snaps_taken < CX->rec_max_snaps) {
                 SnapState *S = CX->rec_snaps + snaps_taken;
-                const uint32_t np = (uint32_t)__builtin_amdgcn_readlane((int)m.n_priv, 0);
+                const uint32_t np = (uint32_t)rdl32<kNL>((uint32_t)m.n_priv, 0);
                 if (lane == 0) {
 #pragma unroll
                     for (int r = 0; r < 32; r++) S->regs[r] = RREG(r);
@@ -852,9 +881,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                 for (uint32_t i = 0; i < np; i++) {
                     if (lane == 0) CX->rec_vpns[(uint64_t)snaps_taken * CX->priv_pages + i] = CX->priv_vpn[i * CX->n_slots];
                     const uint4 *src = (const uint4 *)priv_frame(CX, 0, i);
-                    uint4 *dst = (uint4 *)(CX->rec_pages + (((uint64_t)snaps_taken * CX->priv_pages + i) << 12));
-#pragma unroll
-                    for (int k = 0; k < 4; k++) dst[lane + 64 * k] = src[lane + 64 * k];
+                    page_copy<kNL>((uint4 *)(CX->rec_pages + (((uint64_t)snaps_taken * CX->priv_pages + i) << 12)), src, lane);
                 }
             }
             snaps_taken++;
@@ -862,21 +889,21 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
         }
 
         const bool ready = !L.done && m.req_vpn == kNone;
-        const uint64_t act = __ballot(ready);
+        const uint64_t act = wballot<kNL>(ready);
         if (act == 0) {
-            if (__ballot(!L.done) == 0) break;
+            if (wballot<kNL>(!L.done) == 0) break;
             continue;
         }
         // ---- C. leader PC: first ready lane, or min-PC if the lanes diverged
         const int leader = __ffsll((unsigned long long)act) - 1;
-        uint64_t lpc = readlane64(L.pc, leader);
+        uint64_t lpc = rdl64<kNL>(L.pc, leader);
         n_iter++;
-        if (__ballot(ready && L.pc == lpc) != act) { lpc = wave_min64(ready ? L.pc : kNone); n_min++; }
+        if (wballot<kNL>(ready && L.pc == lpc) != act) { lpc = wmin64<kNL>(ready ? L.pc : kNone); n_min++; }
         lpc = uni64(lpc);   // wave-uniform: keeps fetch/decode/dispatch on the scalar unit
         bool mine = ready && L.pc == lpc;
         // lanes of other groups wait; the group keeps the wave only while its PC
         // stays below theirs (min-PC order, so groups merge when they meet)
-        const uint64_t wait_min = (__ballot(mine) != act) ? uni64(wave_min64((ready && !mine) ? L.pc : kNone)) : kNone;
+        const uint64_t wait_min = (wballot<kNL>(mine) != act) ? uni64(wmin64<kNL>((ready && !mine) ? L.pc : kNone)) : kNone;
         // next instruction-count event of this lane: injection, snapshot
         // comparison, hang cap, or (record mode) snapshot capture
         uint64_t next_ev = CX->hang_cap;
@@ -905,14 +932,14 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
             tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
             const PreRef E0 = pre_entry(tx, lpc);
             if (!(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader) &&
-                __ballot(mine && (dirty_near(m, lpc) || L.injected == 3)) == 0) {
+                wballot<kNL>(mine && (dirty_near(m, lpc) || L.injected == 3)) == 0) {
                 // lanes that rewrote code: every block checks its bytes against their range
-                const bool wdirty = uni32(__ballot(m.code_dirty) != 0);
+                const bool wdirty = uni32(wballot<kNL>(m.code_dirty) != 0);
                 const uint64_t ldlo = m.code_dirty ? m.dlo : kNone, ldhi = m.code_dirty ? m.dhi : 0;
                 // lanes watching a protected flipped register: blocks that touch it exit first
-                const bool wwatch = uni32(__ballot(L.watch > 0) != 0);
+                const bool wwatch = uni32(wballot<kNL>(L.watch > 0) != 0);
                 const uint32_t lwm = L.watch > 0 ? (1u << L.watch) : 0u;
-                const uint64_t gm = __ballot(mine);      // the entry group
+                const uint64_t gm = wballot<kNL>(mine);      // the entry group
                 uint64_t gmr = gm;                        // the running group
                 uint64_t pend = 0, pmin = kNone;          // parked lanes, their lowest pc
                 const uint64_t owm = wait_min;            // lanes outside the entry group
@@ -924,7 +951,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                 // branch of the translated code divergent
                 const uint32_t wbud = uni32(CX->wave_budget ? CX->wave_budget - n_iter : (1u << 30));
                 // scalar lower bound of the budget checks (translated blocks)
-                const uint32_t urem = (uint32_t)uni64(wave_min64(mine ? (uint64_t)rem : kNone));
+                const uint32_t urem = (uint32_t)uni64(wmin64<kNL>(mine ? (uint64_t)rem : kNone));
                 const uint32_t ubud = urem < wbud ? urem : wbud;
                 const uint8_t *const zp = CX->zero_page;
                 uint8_t *const sink = CX->tx_sink + 8 * lane;
@@ -963,7 +990,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                     pend = uni64(pend & ~gmr);
                     spc = pmin;
                 }
-                pmin = uni64(pend ? wave_min64(((pend >> lane) & 1) ? lp : kNone) : kNone);
+                pmin = uni64(pend ? wmin64<kNL>(((pend >> lane) & 1) ? lp : kNone) : kNone);
                 wmin = uni64(ult64(pmin, owm) ? pmin : owm);
                 goto tx_dispatch;
             tx_out:
@@ -991,15 +1018,15 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
         // (K_SLOW op, fault, page request, syscall).  Nothing commits unless the
         // whole instruction commits for every group lane.
         if (CX->pre_ok && lpc >= CX->text_lo && lpc < CX->text_hi &&
-            __ballot(mine && L.injected == 3) == 0) {   // an armed result fault commits in the general path
+            wballot<kNL>(mine && L.injected == 3) == 0) {   // an armed result fault commits in the general path
             // lanes that rewrote code run here too, until they reach a rewritten
             // instruction; lanes watching a protected flipped register, until an
             // instruction reads it (the general path classifies the detection)
-            const bool any_dirty = __ballot(mine && m.code_dirty) != 0;
-            const bool any_watch = __ballot(mine && L.watch > 0) != 0;
-            const uint64_t gm = __ballot(mine);
+            const bool any_dirty = wballot<kNL>(mine && m.code_dirty) != 0;
+            const bool any_watch = wballot<kNL>(mine && L.watch > 0) != 0;
+            const uint64_t gm = wballot<kNL>(mine);
             const int glane = __ffsll((unsigned long long)gm) - 1;
-            uint64_t budget64 = uni64(wave_min64(mine ? next_ev - L.ninst : kNone));
+            uint64_t budget64 = uni64(wmin64<kNL>(mine ? next_ev - L.ninst : kNone));
             if (CX->wave_budget && budget64 > CX->wave_budget - n_iter) budget64 = CX->wave_budget - n_iter;
             const uint32_t budget = budget64 > (1u << 30) ? (1u << 30) : (uint32_t)budget64;
             uint64_t spc = lpc;
@@ -1012,7 +1039,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
             while (budget) {
                 PSTAMP(3);
                 spc = uni64(spc);
-                if (any_dirty && __ballot(mine && dirty_at(m, spc)) != 0) {
+                if (any_dirty && wballot<kNL>(mine && dirty_at(m, spc)) != 0) {
                     // the group rewrote this instruction: decode the bytes the
                     // lanes hold now (Decoder::moreBytes on their own pages) when
                     // they all hold the same; otherwise the general path
@@ -1020,9 +1047,9 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                     uint64_t fva = 0;
                     int fr = 0;
                     if (mine) fr = fetch_lane(CX, w, m, slot, spc, raw, t, fva);
-                    const uint32_t raw0 = (uint32_t)__builtin_amdgcn_readlane((int)raw, glane);
-                    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)t, glane);
-                    if (__ballot(mine && (fr != 0 || raw != raw0)) != 0) break;
+                    const uint32_t raw0 = (uint32_t)rdl32<kNL>((uint32_t)raw, glane);
+                    const uint32_t t0 = (uint32_t)rdl32<kNL>((uint32_t)t, glane);
+                    if (wballot<kNL>(mine && (fr != 0 || raw != raw0)) != 0) break;
                     Dec dd = rv_decode(uni32(raw0));
                     const uint32_t u = uop_of(dd);
                     E.in = true;
@@ -1038,7 +1065,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                 if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
 #ifdef FI_TX
                 if (steps && ((q3 >> 8) & kPreLeader) &&   // translated blocks take over here
-                    !(any_dirty && __ballot(mine && dirty_near(m, spc)) != 0))
+                    !(any_dirty && wballot<kNL>(mine && dirty_near(m, spc)) != 0))
                     break;
 #endif
                 const uint32_t rd = q1 >> 8 & 0xFF, rs1 = q1 >> 16 & 0xFF, rs2 = q1 >> 24;
@@ -1046,7 +1073,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                     const uint32_t fl = q3 >> 8;
                     const bool rw = L.watch > 0 && (((fl & kPreRs1) && rs1 == (uint32_t)L.watch) ||
                                                     ((fl & kPreRs2) && rs2 == (uint32_t)L.watch));
-                    if (__ballot(mine && rw) != 0) break;
+                    if (wballot<kNL>(mine && rw) != 0) break;
                 }
                 const int64_t imm = (int32_t)q2;
                 const uint32_t len = q3 & 0xFF, straddle = ((q3 >> 8) & kPreStraddle) ? 1 : 0;
@@ -1083,8 +1110,8 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                 case K_JALR: {
                     v = ft;
                     const uint64_t t = (a0 + imm) & ~1ULL;
-                    const uint64_t t0 = readlane64(t, glane);
-                    if (__ballot(mine && t != t0) == 0) { npc = uni64(t0); ind = true; }
+                    const uint64_t t0 = rdl64<kNL>(t, glane);
+                    if (wballot<kNL>(mine && t != t0) == 0) { npc = uni64(t0); ind = true; }
                     else { div = true; if (mine) L.pc = t; }
                     break;
                 }
@@ -1099,7 +1126,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                     case K_BLTU: cnd = a0 < b0; break;
                     default: cnd = a0 >= b0; break;
                     }
-                    const uint64_t tk = __ballot(mine && cnd);
+                    const uint64_t tk = wballot<kNL>(mine && cnd);
                     if (tk == gm) { npc = spc + imm; took = true; }
                     else if (tk != 0) { div = true; if (mine) L.pc = cnd ? spc + imm : ft; }
                     break;
@@ -1115,7 +1142,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                         if (!p) p = lookup_full(CX, w, m, slot, ea >> 12);
                     }
                     const bool ok = p && (!st || ((p & 1) && (ea >= tx.chi || ea + msz <= tx.clo))) && off + msz <= 4096;
-                    if (__ballot(mine && !ok) != 0) { msz = 0xFFFFFFFFu; break; }   // bail: general path
+                    if (wballot<kNL>(mine && !ok) != 0) { msz = 0xFFFFFFFFu; break; }   // bail: general path
                     if (mine) {
                         uint8_t *pg = const_cast<uint8_t *>(page_of(p));
                         const bool al = (off & (msz - 1)) == 0;
@@ -1189,7 +1216,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
         uint32_t ticks = 1;
         bool fast = false;
         const uint64_t key = (lpc & 3) ? ((lpc & ~3ULL) | 2) : lpc;
-        if (CX->pre_ok && key >= CX->text_lo && key < CX->text_hi && __ballot(mine && dirty_at(m, lpc)) == 0) {
+        if (CX->pre_ok && key >= CX->text_lo && key < CX->text_hi && wballot<kNL>(mine && dirty_at(m, lpc)) == 0) {
             const Pre4 q = pre_load(CX->pre + ((key - CX->text_lo) >> 1));
             const uint32_t pflags = (q.w >> 8) & 0xFF;
             if (pflags & kPreValid) {
@@ -1221,11 +1248,11 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
                     }
                 }
             }
-            const uint64_t okm = __ballot(mine);
+            const uint64_t okm = wballot<kNL>(mine);
             if (okm == 0) break;
             const int ld = __ffsll((unsigned long long)okm) - 1;
-            const uint32_t lraw = (uint32_t)__builtin_amdgcn_readlane((int)raw, ld);
-            const uint32_t lt = (uint32_t)__builtin_amdgcn_readlane((int)t, ld);
+            const uint32_t lraw = (uint32_t)rdl32<kNL>((uint32_t)raw, ld);
+            const uint32_t lt = (uint32_t)rdl32<kNL>((uint32_t)t, ld);
             mine = mine && raw == lraw;
             PSTAMP(5);
             d = rv_decode(lraw);
@@ -1241,7 +1268,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
         d.rs2 = (uint8_t)uni32(d.rs2); d.len = (uint8_t)uni32(d.len); d.flags = (uint8_t)uni32(d.flags);
         d.imm = (int32_t)uni32((uint32_t)d.imm); d.aux = (uint16_t)uni32(d.aux); d.raw = uni32(d.raw);
         ticks = uni32(ticks);
-        const uint64_t gmask = __ballot(mine);
+        const uint64_t gmask = wballot<kNL>(mine);
         n_exec += (uint32_t)__popcll(gmask);
         int f = F_NONE;
         {   // every lane evaluates the (uniform) op: the switch stays a scalar
@@ -1518,7 +1545,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
         switch (f) {
         case F_SYSCALL:   // SyscallFault::invokeSE advances the PC first (arch/riscv/faults.cc:325-333)
             L.pc = pc + d.len;
-            do_syscall(CX, w, L, m, slot, R, lane);
+            do_syscall<kNL>(CX, w, L, m, slot, R, lane);
             break;
         case F_BREAK: finish(L, FI_CRASH, FI_CRASH_SIGTRAP, 133, (uint32_t)pc); break;
         case F_ILLEGAL: finish(L, FI_CRASH, FI_CRASH_ILLEGAL_INST, 134, (uint32_t)pc); break;
@@ -1548,10 +1575,10 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
         // ---- stay in the inner loop? every group lane committed, none reached
         // its next event, all at one PC that is still the wave's minimum
         const bool cont = mine && f == F_NONE && !L.done && L.ninst < next_ev;
-        const uint64_t cm = __ballot(cont);
+        const uint64_t cm = wballot<kNL>(cont);
         if (cm != gmask) break;
-        const uint64_t npc0 = uni64(readlane64(L.pc, __ffsll((unsigned long long)cm) - 1));
-        if (__ballot(cont && L.pc == npc0) != cm || npc0 >= wait_min) break;
+        const uint64_t npc0 = uni64(rdl64<kNL>(L.pc, __ffsll((unsigned long long)cm) - 1));
+        if (wballot<kNL>(cont && L.pc == npc0) != cm || npc0 >= wait_min) break;
         if (CX->wave_budget && n_iter + 1 >= CX->wave_budget) break;
         if (CX->pre_ok) {   // back to the fast path (or translated blocks) when they can take the next one
             TextRef tn;
@@ -1560,7 +1587,7 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
             const PreRef En = pre_entry(tn, npc0);
             const uint32_t wn = uni32(En.e.w);
             if (En.in && ((wn >> 8) & kPreValid) && ((wn >> 16) & 63) != K_SLOW &&
-                __ballot(cont && dirty_at(m, npc0)) == 0)
+                wballot<kNL>(cont && dirty_at(m, npc0)) == 0)
                 break;
         }
         lpc = npc0;
@@ -1592,9 +1619,9 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
         CX->stats[20] = __builtin_amdgcn_s_memtime() - t_start;
         CX->stats[21] = __builtin_amdgcn_s_memrealtime() - rt_start;
     }
-    const uint64_t fb = wave_sum64(L.fetch_b), db = wave_sum64(L.data_b), pm = wave_sum64(pages_made);
-    const uint64_t si = wave_sum64(start_inst);
-    const uint64_t xi = wave_sum64(live ? L.ninst - launch_inst : 0);
+    const uint64_t fb = wsum64<kNL>(L.fetch_b), db = wsum64<kNL>(L.data_b), pm = wsum64<kNL>(pages_made);
+    const uint64_t si = wsum64<kNL>(start_inst);
+    const uint64_t xi = wsum64<kNL>(live ? L.ninst - launch_inst : 0);
     if (lane == 0) {
         atomicAdd(&CX->stats[23], (unsigned long long)xi);
         atomicAdd(&CX->stats[0], (unsigned long long)fb);
@@ -1625,10 +1652,22 @@ __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx ct
     }
 }
 
-#ifndef __HIPCC_RTC__
+// The two instantiations (load-time build: with the translated blocks).
+#ifdef __HIPCC_RTC__
+extern "C" __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel_tx(DevCtx) { trial_body<64>(); }
+extern "C" __global__ void __launch_bounds__(1) fi_trial_kernel_tx_solo(DevCtx) { trial_body<1>(); }
+#else
+__global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx) { trial_body<64>(); }
+__global__ void __launch_bounds__(1) fi_trial_kernel_solo(DevCtx) { trial_body<1>(); }
+
 hipError_t launch_trials(const DevCtx &c, hipStream_t st) {
     const uint32_t gl = (c.resume && c.resume_waves) ? 1u : c.lanes;   // grid for the fewest lanes per wave
     hipLaunchKernelGGL(fi_trial_kernel, dim3((unsigned)((c.n + gl - 1) / gl)), dim3(64), 0, st, c);
+    return hipGetLastError();
+}
+// one trial per single-lane workgroup (surplus workgroups of a resume grid exit at once)
+hipError_t launch_trials_solo(const DevCtx &c, hipStream_t st) {
+    hipLaunchKernelGGL(fi_trial_kernel_solo, dim3((unsigned)c.n), dim3(1), 0, st, c);
     return hipGetLastError();
 }
 #endif

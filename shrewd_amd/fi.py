@@ -100,6 +100,8 @@ CFG_NO_TRANSLATE = 4
 CFG_NO_EPOCHS = 8
 CFG_PACK_RUNS = 16
 CFG_FIXED_RESUME = 32
+CFG_NO_SOLO = 64
+CFG_SOLO_ALL = 128
 
 
 class GoldenInfo(C.Structure):

@@ -201,6 +201,9 @@ PATH_FLAGS = {
     "no_epochs": 8,                         # FI_CFG_NO_EPOCHS
     "pack_runs": 16,                        # FI_CFG_PACK_RUNS
     "fixed_resume": 32,                     # FI_CFG_FIXED_RESUME
+    "no_solo": 64,                          # FI_CFG_NO_SOLO: resumed epochs on the 64-lane kernel
+    "solo_all": 128,                        # FI_CFG_SOLO_ALL: every epoch on the one-trial-per-wave kernel
+    "solo_all_interp": 128 | 4,             # the solo build without translated blocks
 }
 _PATH_REF = {}
 
