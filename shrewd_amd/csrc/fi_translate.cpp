@@ -19,7 +19,9 @@
 #include <cctype>
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
+#include <map>
 #include <set>
 #include <string>
 #include <vector>
@@ -48,23 +50,6 @@ struct Gen {
     }
     static std::string R(uint32_t r) { return r ? "X" + std::to_string(r) : std::string("0ULL"); }
     uint64_t pc_of(uint32_t h) const { return text_lo + 2ULL * h; }
-    // Jump from the block at `from` to the block at pc, or leave at pc if it
-    // is not translated.  Only forward edges and self-loops are direct: every
-    // cycle then passes through tx_dispatch, the single header, and the CFG
-    // stays reducible (with direct backward edges every block of a loop would
-    // be one of its entries, and the compiler's irreducible-control-flow fix
-    // routes every transition through a linear guard chain).
-    std::string go(uint64_t pc, uint32_t from) const {
-        char buf[96];
-        const uint64_t off = pc - text_lo;
-        if (pc >= text_lo && !(off & 1) && off / 2 < pre.size() && leaders.count((uint32_t)(off / 2))) {
-            if ((uint32_t)(off / 2) >= from) snprintf(buf, sizeof buf, "goto B_%u;", (uint32_t)(off / 2));
-            else snprintf(buf, sizeof buf, "{ spc = 0x%llxULL; goto tx_dispatch; }", (unsigned long long)pc);
-        } else {
-            snprintf(buf, sizeof buf, "{ spc = 0x%llxULL; goto tx_out; }", (unsigned long long)pc);
-        }
-        return buf;
-    }
 };
 
 enum Cls { C_STOP, C_ALU, C_NOP, C_LOAD, C_STORE, C_BR, C_JAL, C_JALR };
@@ -237,10 +222,131 @@ const char *ltype(uint32_t size) {
 
 }  // namespace
 
+namespace {
+
+// Reducible entries.  Every cycle of blocks must have a single
+// entry (its header), or the compiler's irreducible-flow fix routes every
+// transition through a guard chain -- and then all loops run slowly.  The
+// headers are found the classic way: strongly connected components, one
+// header each (its lowest-address entry block), recursively inside each
+// component with the back edges to its header removed.  Every block stays an
+// entry point of the translated code, but the dispatch switch jumps only to
+// top-level blocks and headers: a block inside cycles is reached through the
+// outermost cycle's header, each header's prologue routing the wanted block
+// (etgt) one nesting level further.  Loop back edges are direct gotos; an edge
+// that enters a cycle from the side goes through the dispatch switch.
+struct Structurer {
+    const std::map<uint32_t, std::vector<uint32_t>> &succ;   // block -> successor blocks (direct candidates)
+    std::set<uint32_t> entries;                            // top-level entries: reached from dispatch directly
+    std::set<std::pair<uint32_t, uint32_t>> exits;         // side entries into a cycle: routed through dispatch
+    std::map<uint32_t, std::vector<uint32_t>> chain;       // block -> headers of the cycles around it, outermost first
+    std::set<uint32_t> headers;
+
+    void run(const std::vector<uint32_t> &nodes, bool top, std::set<std::pair<uint32_t, uint32_t>> removed) {
+        const std::set<uint32_t> in(nodes.begin(), nodes.end());
+        // Tarjan's SCC over the induced subgraph (iterative)
+        std::map<uint32_t, int> idx, low;
+        std::set<uint32_t> onst;
+        std::vector<uint32_t> st;
+        std::vector<std::vector<uint32_t>> sccs;
+        int counter = 0;
+        auto edges = [&](uint32_t v) {
+            std::vector<uint32_t> r;
+            auto it = succ.find(v);
+            if (it == succ.end()) return r;
+            for (uint32_t w : it->second)
+                if (in.count(w) && !removed.count({v, w})) r.push_back(w);
+            return r;
+        };
+        for (uint32_t root : nodes) {
+            if (idx.count(root)) continue;
+            std::vector<std::pair<uint32_t, size_t>> stack{{root, 0}};
+            idx[root] = low[root] = counter++;
+            st.push_back(root);
+            onst.insert(root);
+            while (!stack.empty()) {
+                auto &[v, i] = stack.back();
+                const std::vector<uint32_t> es = edges(v);
+                if (i < es.size()) {
+                    const uint32_t w = es[i++];
+                    if (!idx.count(w)) {
+                        idx[w] = low[w] = counter++;
+                        st.push_back(w);
+                        onst.insert(w);
+                        stack.push_back({w, 0});
+                    } else if (onst.count(w)) {
+                        low[v] = std::min(low[v], idx[w]);
+                    }
+                    continue;
+                }
+                if (low[v] == idx[v]) {
+                    std::vector<uint32_t> comp;
+                    uint32_t w;
+                    do {
+                        w = st.back();
+                        st.pop_back();
+                        onst.erase(w);
+                        comp.push_back(w);
+                    } while (w != v);
+                    sccs.push_back(comp);
+                }
+                const uint32_t done = v;
+                stack.pop_back();
+                if (!stack.empty()) low[stack.back().first] = std::min(low[stack.back().first], low[done]);
+            }
+        }
+        for (auto &comp : sccs) {
+            std::sort(comp.begin(), comp.end());
+            const std::set<uint32_t> cs(comp.begin(), comp.end());
+            bool cyclic = comp.size() > 1;
+            if (!cyclic)
+                for (uint32_t w : edges(comp[0]))
+                    if (w == comp[0]) cyclic = true;
+            if (!cyclic) {
+                if (top) entries.insert(comp[0]);
+                continue;
+            }
+            uint32_t header = comp[0];
+            bool have = false;
+            for (uint32_t v : nodes) {   // lowest-address block entered from outside the component
+                if (cs.count(v)) continue;
+                for (uint32_t w : edges(v))
+                    if (cs.count(w) && (!have || w < header)) { header = w; have = true; }
+            }
+            for (uint32_t v : nodes) {
+                if (cs.count(v)) continue;
+                for (uint32_t w : edges(v))
+                    if (cs.count(w) && w != header) exits.insert({v, w});
+            }
+            if (top) entries.insert(header);
+            headers.insert(header);
+            for (uint32_t v : comp) chain[v].push_back(header);
+            auto inner = removed;
+            for (uint32_t v : comp) inner.insert({v, header});
+            run(comp, false, inner);
+        }
+    }
+};
+
+struct Block {
+    uint32_t h0;
+    std::vector<uint32_t> insts;
+    bool term;
+};
+
+}  // namespace
+
 // Leaders: the first executed instruction, every instruction the golden run
 // reached other than by falling through, the successor of every executed
-// control transfer or ecall, the extra pcs (snapshot pcs: where waves start),
-// and the same for the code statically reachable from the executed code.  trace = halfword index per golden event (bit 31: ecall).
+// control transfer or ecall, the extra pcs, and the same for the code
+// statically reachable from the executed code.  trace = halfword index per
+// golden event (bit 31: ecall).
+//
+// Two bodies are generated (joined by the marker FI_TX_SPLIT): the 64-lane one
+// (blocks B_*, guest registers X1..X31 in VGPRs, register writes as selects on
+// the running group, divergence parked and merged by the min-PC rule) and the
+// solo one for the one-trial-per-wave kernel (blocks S_*, every value
+// uniform, no groups).
 std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
                              const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
                              uint32_t &n_insts) {
@@ -310,19 +416,19 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         else ++it;
     }
 
-    Gen g{pre, text_lo, leaders, executed, {}};
-    n_insts = 0;
-    g.put("tx_dispatch: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", (unsigned long long)text_lo);
-    g.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto tx_out;\n  switch ((uint32_t)off_ >> 1) {\n");
-    for (uint32_t h : leaders) g.put("  case %u: goto B_%u;\n", h, h);
-    g.put("  default: goto tx_out;\n  }\n}\n");
-
+    // ---- the blocks: from a leader until a control transfer (inclusive), an
+    // untranslatable or unexecuted instruction, or the next leader
+    std::vector<Block> blocks;
+    std::map<uint32_t, std::vector<uint32_t>> succ;
+    auto hof = [&](uint64_t pc, uint32_t &h) {
+        const uint64_t off = pc - text_lo;
+        if (pc < text_lo || (off & 1) || off / 2 >= pre.size() || !leaders.count((uint32_t)(off / 2))) return false;
+        h = (uint32_t)(off / 2);
+        return true;
+    };
     for (uint32_t h0 : leaders) {
-        // the block: instructions from h0 until a control transfer (inclusive),
-        // an untranslatable or unexecuted instruction, or the next leader
-        std::vector<uint32_t> insts;
+        Block b{h0, {}, false};
         uint32_t h = h0;
-        bool term = false;
         for (;;) {
             if (!valid(h) || !executed.count(h)) break;
             if (h != h0 && leaders.count(h)) break;
@@ -332,37 +438,131 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             const char *cond;
             const Cls k = classify(pre[h], e, sz, sx, cond);
             if (k == C_STOP) break;
-            insts.push_back(h);
-            if (k == C_BR || k == C_JAL || k == C_JALR) { term = true; break; }
+            b.insts.push_back(h);
+            if (k == C_BR || k == C_JAL || k == C_JALR) { b.term = true; break; }
             h += pre[h].len / 2u;
         }
+        auto &sv = succ[h0];
+        const uint64_t pc_last = b.insts.empty() ? text_lo + 2ULL * h0 : text_lo + 2ULL * b.insts.back();
+        const PreInst &pl = pre[b.insts.empty() ? h0 : b.insts.back()];
+        uint32_t t;
+        if (b.term) {
+            std::string e;
+            uint32_t sz;
+            int sx;
+            const char *cond;
+            const Cls k = classify(pl, e, sz, sx, cond);
+            if (k == C_BR || k == C_JAL) {
+                if (hof(pc_last + (int64_t)pl.imm, t)) sv.push_back(t);
+            }
+            if (k == C_BR && hof(pc_last + pl.len, t)) sv.push_back(t);
+        } else if (!b.insts.empty() && hof(pc_last + pl.len, t)) {
+            sv.push_back(t);
+        }
+        blocks.push_back(b);
+    }
+    Structurer S{succ, {}, {}};
+    S.run(std::vector<uint32_t>(leaders.begin(), leaders.end()), true, {});
+
+    enum Edge { E_DIRECT, E_DISPATCH, E_OUT };
+    auto edge = [&](uint32_t from, uint64_t pc) {
+        uint32_t t;
+        if (!hof(pc, t)) return E_OUT;
+        return S.exits.count({from, t}) ? E_DISPATCH : E_DIRECT;
+    };
+
+    Gen g{pre, text_lo, leaders, executed, {}};
+    Gen so{pre, text_lo, leaders, executed, {}};
+    n_insts = 0;
+    auto hex = [](uint64_t v) {
+        char b[32];
+        snprintf(b, sizeof b, "0x%llxULL", (unsigned long long)v);
+        return std::string(b);
+    };
+    // wave: where to go from block `from` to pc (lanes of the running group)
+    auto wgo = [&](uint32_t from, uint64_t pc) {
+        const Edge k = edge(from, pc);
+        uint32_t t = 0;
+        hof(pc, t);
+        if (k == E_DIRECT) return "goto B_" + std::to_string(t) + ";";
+        return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto tx_dispatch; }" : "; goto tx_out; }");
+    };
+    auto sgo = [&](uint32_t from, uint64_t pc) {
+        const Edge k = edge(from, pc);
+        uint32_t t = 0;
+        hof(pc, t);
+        if (k == E_DIRECT) return "goto S_" + std::to_string(t) + ";";
+        return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto S_dispatch; }" : "; goto S_out; }");
+    };
+    g.put("tx_dispatch: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", (unsigned long long)text_lo);
+    g.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto tx_out;\n  switch ((uint32_t)off_ >> 1) {\n");
+    so.put("S_dispatch: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", (unsigned long long)text_lo);
+    so.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto S_out;\n  switch ((uint32_t)off_ >> 1) {\n");
+    for (uint32_t h : leaders) {
+        auto it = S.chain.find(h);
+        if (it == S.chain.end() || (it->second.size() == 1 && it->second[0] == h)) {
+            g.put("  case %u: goto B_%u;\n", h, h);
+            so.put("  case %u: goto S_%u;\n", h, h);
+        } else {
+            g.put("  case %u: etgt = %uu; goto B_%u;\n", h, h, it->second[0]);
+            so.put("  case %u: etgt = %uu; goto S_%u;\n", h, h, it->second[0]);
+        }
+    }
+    g.put("  default: goto tx_out;\n  }\n}\n");
+    so.put("  default: goto S_out;\n  }\n}\n");
+
+    static const bool tx_watch = !getenv("SHREWD_FI_TX_NOWATCH");   // A/B switch (diagnostics)
+    for (const Block &b : blocks) {
+        const uint32_t h0 = b.h0;
+        const std::vector<uint32_t> &insts = b.insts;
         const uint32_t n = (uint32_t)insts.size();
         n_insts += n;
         const uint64_t pc0 = g.pc_of(h0);
+        const std::string P0 = hex(pc0);
+        uint32_t rw = 0;   // registers the block reads or writes (watch check)
+        for (uint32_t hh : insts) {
+            const PreInst &p = pre[hh];
+            if ((p.flags & kPreRs1) && p.rs1) rw |= 1u << p.rs1;
+            if ((p.flags & kPreRs2) && p.rs2) rw |= 1u << p.rs2;
+            if ((p.flags & kPreRd) && p.rd) rw |= 1u << p.rd;
+        }
+        if (!tx_watch) rw = 0;
+        const uint64_t blo = pc0 & ~3ULL, bhi = g.pc_of(insts.empty() ? h0 : insts.back()) + 6;
         g.put("B_%u: { // pc 0x%llx, %u insts\n", h0, (unsigned long long)pc0, n);
-        g.put("  if (!ult64(0x%llxULL, wmin)) { spc = 0x%llxULL; goto tx_sched; }\n", (unsigned long long)pc0,
-              (unsigned long long)pc0);
-        // ubud = min(wbud, every entry-group lane's rem) and lst <= wst, so the
-        // exact per-lane check only runs when the scalar bound is reached
-        g.put("  if (wst + %uu > ubud && (wst + %uu > wbud || TXB(mine && rem - lst < %uu))) { spc = 0x%llxULL; "
-              "goto tx_out; }\n", n, n, n, (unsigned long long)pc0);
-        {   // a lane watching a protected flipped register this block reads or writes leaves before it
-            uint32_t rw = 0;
-            for (uint32_t hh : insts) {
-                const PreInst &p = pre[hh];
-                if ((p.flags & kPreRs1) && p.rs1) rw |= 1u << p.rs1;
-                if ((p.flags & kPreRs2) && p.rs2) rw |= 1u << p.rs2;
-                if ((p.flags & kPreRd) && p.rd) rw |= 1u << p.rd;
+        so.put("S_%u: { // pc 0x%llx, %u insts\n", h0, (unsigned long long)pc0, n);
+        if (S.headers.count(h0)) {   // a cycle header routes an entry into its cycle one level on (etgt)
+            std::string rw_, rs_;
+            for (uint32_t x : leaders) {
+                auto it = S.chain.find(x);
+                if (it == S.chain.end() || x == h0) continue;
+                const auto &ch = it->second;
+                const auto pos = std::find(ch.begin(), ch.end(), h0);
+                if (pos == ch.end()) continue;
+                const uint32_t next = (pos + 1 != ch.end()) ? *(pos + 1) : x;
+                // a nested header routes further, and clears etgt when it is the target
+                const std::string clr = S.headers.count(next) ? "" : "etgt = 0xFFFFFFFFu; ";
+                rw_ += "case " + std::to_string(x) + ": " + clr + "goto B_" + std::to_string(next) + "; ";
+                rs_ += "case " + std::to_string(x) + ": " + clr + "goto S_" + std::to_string(next) + "; ";
             }
-            static const bool tx_watch = !getenv("SHREWD_FI_TX_NOWATCH");   // A/B switch (diagnostics)
-            if (rw && tx_watch) g.put("  if (wwatch && TXB(mine && (lwm & 0x%xu) != 0)) { spc = 0x%llxULL; goto tx_out; }\n", rw,
-                          (unsigned long long)pc0);
+            const char *fmt = "  if (etgt != 0xFFFFFFFFu) { if (etgt == %uu) etgt = 0xFFFFFFFFu; "
+                              "else switch (etgt) { %sdefault: break; } }\n";
+            g.put(fmt, h0, rw_.c_str());
+            so.put(fmt, h0, rs_.c_str());
         }
-        {   // a lane that rewrote one of this block's instruction bytes leaves before it
-            const uint64_t blo = pc0 & ~3ULL, bhi = g.pc_of(insts.empty() ? h0 : insts.back()) + 6;
-            g.put("  if (wdirty && TXB(mine && ldlo < 0x%llxULL && ldhi > 0x%llxULL)) { spc = 0x%llxULL; goto tx_out; }\n",
-                  (unsigned long long)bhi, (unsigned long long)blo, (unsigned long long)pc0);
-        }
+        // ---- wave block prologue: merge a parked group waiting here, leave or
+        // switch groups when lanes outside run first, then one combined check
+        // (budget, watched registers, rewritten bytes)
+        g.put("  if (!ult64(%s, wmin)) {\n    if (%s == pmin && ult64(pmin, owm)) TXMERGE(%s);\n"
+              "    else { spc = %s; goto tx_sched; }\n  }\n", P0.c_str(), P0.c_str(), P0.c_str(), P0.c_str());
+        g.put("  if (((wst + %uu > ubud) & ((wst + %uu > wbud) | (TXB(mine && rem - lst < %uu) != 0)))", n, n, n);
+        if (rw) g.put(" |\n      (wwatch & (TXB(mine && (lwm & 0x%xu) != 0) != 0))", rw);
+        g.put(" |\n      (wdirty & (TXB(mine && ldlo < %s && ldhi > %s) != 0))) { spc = %s; goto tx_out; }\n",
+              hex(bhi).c_str(), hex(blo).c_str(), P0.c_str());
+        // ---- solo block prologue: one uniform check
+        so.put("  if ((st + %uu > bud)", n);
+        if (rw) so.put(" | ((lwm & 0x%xu) != 0)", rw);
+        so.put(" | ((sdlo < %uu) & (sdhi > %uu))) { spc = %s; goto S_out; }\n", (uint32_t)(bhi - text_lo),
+               (uint32_t)(blo - text_lo), P0.c_str());
         uint32_t k_st = 0, k_xt = 0, k_fb = 0, k_db = 0;   // committed so far in this block
         auto commit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
             // per-lane counters of the running lanes (zero terms omitted), wave iterations
@@ -372,6 +572,14 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             if (fb) r += "lfb += " + std::to_string(fb) + "u & mm_; ";
             if (db) r += "ldb += " + std::to_string(db) + "u & mm_; ";
             return r + "wst = uni32(wst + " + std::to_string(st) + "u); } ";
+        };
+        auto scommit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
+            if (!st) return std::string();
+            std::string r = "st += " + std::to_string(st) + "u; ";
+            if (xt) r += "xt += " + std::to_string(xt) + "u; ";
+            if (fb) r += "fb += " + std::to_string(fb) + "u; ";
+            if (db) r += "db += " + std::to_string(db) + "u; ";
+            return r;
         };
         for (uint32_t i = 0; i < n; i++) {
             const PreInst &p = pre[insts[i]];
@@ -383,73 +591,97 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             const char *cond;
             const Cls k = classify(p, e, sz, sx, cond);
             const std::string A = Gen::R(p.rs1), B = Gen::R(p.rs2);
-            char immb[48], pcb[32], ftb[32];
+            char immb[48];
             snprintf(immb, sizeof immb, "((uint64_t)(int64_t)%dLL)", p.imm);
-            snprintf(pcb, sizeof pcb, "0x%llxULL", (unsigned long long)pc);
-            snprintf(ftb, sizeof ftb, "0x%llxULL", (unsigned long long)ft);
+            const std::string pcb = hex(pc), ftb = hex(ft);
             const uint32_t xt = (p.flags & kPreStraddle) ? 1 : 0;
             const std::string leave_here = "{ " + commit(k_st, k_xt, k_fb, k_db) + "spc = " + pcb + "; goto tx_out; }";
+            const std::string sleave_here = "{ " + scommit(k_st, k_xt, k_fb, k_db) + "spc = " + pcb + "; goto S_out; }";
             switch (k) {
-            case C_ALU:
-                if (p.rd) g.put("  TXSET(%u, %s);\n", p.rd, subst(e, A, B, immb, pcb).c_str());
+            case C_ALU: {
+                const std::string v = subst(e, A, B, immb, pcb);
+                if (p.rd) {
+                    g.put("  TXSET(%u, %s);\n", p.rd, v.c_str());
+                    so.put("  X%u = %s;\n", p.rd, v.c_str());
+                }
                 break;
+            }
             case C_NOP:
                 break;
             case C_LOAD:
                 g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, false, p_, tx);\n", A.c_str(), immb, sz);
                 g.put("    if (TXB(mine && !ok_)) %s\n", leave_here.c_str());
+                so.put("  { uint8_t *p_; if (!tx_probe(m, %s + %s, %uu, false, p_, tx)) %s\n", A.c_str(), immb, sz,
+                       sleave_here.c_str());
                 if (p.rd) {
                     g.put("    p_ = ok_ ? p_ : const_cast<uint8_t *>(zp);\n");
-                    if (sx) g.put("    TXSET(%u, (int64_t)(int%d_t)*(const g_%s *)p_); }\n", p.rd, sx, gtype(sz));
-                    else g.put("    TXSET(%u, *(const g_%s *)p_); }\n", p.rd, gtype(sz));
+                    if (sx) {
+                        g.put("    TXSET(%u, (int64_t)(int%d_t)*(const g_%s *)p_); }\n", p.rd, sx, gtype(sz));
+                        so.put("    X%u = (uint64_t)(int64_t)(int%d_t)*(const g_%s *)p_; }\n", p.rd, sx, gtype(sz));
+                    } else {
+                        g.put("    TXSET(%u, *(const g_%s *)p_); }\n", p.rd, gtype(sz));
+                        so.put("    X%u = *(const g_%s *)p_; }\n", p.rd, gtype(sz));
+                    }
                 } else {
                     g.put("  }\n");
+                    so.put("  }\n");
                 }
                 break;
             case C_STORE:
                 g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, true, p_, tx);\n", A.c_str(), immb, sz);
                 g.put("    if (TXB(mine && !ok_)) %s\n", leave_here.c_str());
                 g.put("    p_ = (mine && ok_) ? p_ : sink; *(g_%s *)p_ = (%s)%s; }\n", gtype(sz), ltype(sz), B.c_str());
+                so.put("  { uint8_t *p_; if (!tx_probe(m, %s + %s, %uu, true, p_, tx)) %s\n", A.c_str(), immb, sz,
+                       sleave_here.c_str());
+                so.put("    *(g_%s *)p_ = (%s)%s; }\n", gtype(sz), ltype(sz), B.c_str());
                 break;
             case C_BR: {
                 const std::string c = subst(cond, A, B, immb, pcb);
                 const uint64_t tgt = pc + (int64_t)p.imm;
                 g.put("  { const bool c_ = %s; const uint64_t tk_ = uni64(TXB(mine && c_));\n", c.c_str());
                 g.put("    %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
-                g.put("    if (tk_ == gmr) %s\n", g.go(tgt, h0).c_str());
-                g.put("    if (tk_ == 0) %s\n", g.go(ft, h0).c_str());
+                g.put("    if (tk_ == gmr) %s\n", wgo(h0, tgt).c_str());
+                g.put("    if (tk_ == 0) %s\n", wgo(h0, ft).c_str());
                 // divergent: the lanes bound for the higher pc park, the others run on
                 if (tgt > ft) {
-                    g.put("    lp = (mine && c_) ? 0x%llxULL : lp; pend = uni64(pend | tk_); mine = mine && !c_;"
-                          " gmr = uni64(gmr & ~tk_);\n", (unsigned long long)tgt);
-                    g.put("    pmin = uni64(ult64(0x%llxULL, pmin) ? 0x%llxULL : pmin);"
-                          " wmin = uni64(ult64(pmin, owm) ? pmin : owm);\n",
-                          (unsigned long long)tgt, (unsigned long long)tgt);
-                    g.put("    %s }\n", g.go(ft, h0).c_str());
+                    g.put("    lp = (mine && c_) ? %s : lp; pend = uni64(pend | tk_); mine = mine && !c_;"
+                          " gmr = uni64(gmr & ~tk_);\n", hex(tgt).c_str());
+                    g.put("    pmin = uni64(ult64(%s, pmin) ? %s : pmin);"
+                          " wmin = uni64(ult64(pmin, owm) ? pmin : owm);\n", hex(tgt).c_str(), hex(tgt).c_str());
+                    g.put("    %s }\n", wgo(h0, ft).c_str());
                 } else {
                     g.put("    lp = (mine && !c_) ? %s : lp; pend = uni64(pend | (gmr & ~tk_)); mine = mine && c_;"
-                          " gmr = uni64(tk_);\n", ftb);
+                          " gmr = uni64(tk_);\n", ftb.c_str());
                     g.put("    pmin = uni64(ult64(%s, pmin) ? %s : pmin); wmin = uni64(ult64(pmin, owm) ? pmin : owm);\n",
-                          ftb, ftb);
-                    g.put("    %s }\n", g.go(tgt, h0).c_str());
+                          ftb.c_str(), ftb.c_str());
+                    g.put("    %s }\n", wgo(h0, tgt).c_str());
                 }
+                so.put("  %s\n  if (%s) %s\n  %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), c.c_str(),
+                       sgo(h0, tgt).c_str(), sgo(h0, ft).c_str());
                 break;
             }
             case C_JAL: {
                 const uint64_t tgt = pc + (int64_t)p.imm;
-                if (p.rd) g.put("  TXSET(%u, %s);\n", p.rd, ftb);
-                g.put("  %s %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), g.go(tgt, h0).c_str());
+                if (p.rd) {
+                    g.put("  TXSET(%u, %s);\n", p.rd, ftb.c_str());
+                    so.put("  X%u = %s;\n", p.rd, ftb.c_str());
+                }
+                g.put("  %s %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), wgo(h0, tgt).c_str());
+                so.put("  %s %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), sgo(h0, tgt).c_str());
                 break;
             }
             case C_JALR: {
                 const int64_t im = (p.op == OP_jalr) ? p.imm : 0;
                 const uint32_t rd = (p.op == OP_c_jalr) ? 1 : (p.op == OP_c_jr ? 0 : p.rd);
                 g.put("  { const uint64_t t_ = (%s + (uint64_t)(int64_t)%lldLL) & ~1ULL;\n", A.c_str(), (long long)im);
-                if (rd) g.put("    TXSET(%u, %s);\n", rd, ftb);
+                if (rd) g.put("    TXSET(%u, %s);\n", rd, ftb.c_str());
                 g.put("    %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
                 g.put("    const uint64_t t0_ = rdl64<kNL>(t_, __ffsll((unsigned long long)gmr) - 1);\n");
                 g.put("    if (TXB(mine && t_ != t0_)) { dpc = t_; jdiv = mine; goto tx_out; }\n");
                 g.put("    spc = uni64(t0_); goto tx_dispatch; }\n");
+                so.put("  { const uint64_t t_ = (%s + (uint64_t)(int64_t)%lldLL) & ~1ULL;\n", A.c_str(), (long long)im);
+                if (rd) so.put("    X%u = %s;\n", rd, ftb.c_str());
+                so.put("    %s spc = t_; goto S_dispatch; }\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
                 break;
             }
             default:
@@ -457,14 +689,16 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             }
             k_st += 1; k_xt += xt; k_fb += p.len; k_db += (k == C_LOAD || k == C_STORE) ? sz : 0;
         }
-        if (!term) {   // fell into the next leader, or stops before an instruction it does not cover
+        if (!b.term) {   // fell into the next leader, or stops before an instruction it does not cover
             const uint64_t nxt = n ? g.pc_of(insts[n - 1]) + pre[insts[n - 1]].len : pc0;
-            g.put("  %s %s\n", commit(k_st, k_xt, k_fb, k_db).c_str(), g.go(nxt, h0).c_str());
+            g.put("  %s %s\n", commit(k_st, k_xt, k_fb, k_db).c_str(), wgo(h0, nxt).c_str());
+            so.put("  %s %s\n", scommit(k_st, k_xt, k_fb, k_db).c_str(), sgo(h0, nxt).c_str());
         }
         g.put("}\n");
+        so.put("}\n");
     }
     leaders_out.assign(leaders.begin(), leaders.end());
-    return g.out;
+    return g.out + FI_TX_SPLIT + so.out;
 }
 
 }  // namespace fi

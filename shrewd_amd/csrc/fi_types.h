@@ -27,7 +27,10 @@ struct PreInst {
 };
 static_assert(sizeof(PreInst) == 16, "PreInst must stay 16 bytes (one s_load_dwordx4)");
 constexpr uint8_t kPreValid = 1, kPreStraddle = 2, kPreRs1 = 4, kPreRs2 = 8, kPreRd = 16;
-constexpr uint8_t kPreLeader = 32;   // a translated golden basic block starts here (load-time build)
+constexpr uint8_t kPreLeader = 32;   // translated code may be entered here (load-time build)
+// Separates the 64-lane and the solo translated bodies in the generated text
+// (fi_translate.cpp -> fi_jit.cpp splices them at /*@TX_BODY@*/ and /*@TX_SOLO@*/).
+#define FI_TX_SPLIT "\n/*@TX_SPLIT@*/\n"
 
 // Golden snapshot: the architectural state at the top of the first tick with
 // numInst == k * snap_interval, plus the page table of the whole guest address

@@ -931,8 +931,43 @@ __device__ __forceinline__ void trial_body() {
             tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
             tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
             const PreRef E0 = pre_entry(tx, lpc);
-            if (!(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader) &&
-                wballot<kNL>(mine && (dirty_near(m, lpc) || L.injected == 3)) == 0) {
+            const bool tx_entry = !(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader);
+            if constexpr (kNL == 1) {
+                // ---- solo: one trial, every value uniform -- no groups, no
+                // parking, plain register writes; the same exits and counters
+                if (tx_entry && mine && !dirty_near(m, lpc) && L.injected != 3) {
+                    const uint64_t rem64 = next_ev - L.ninst;
+                    const uint32_t rem = rem64 > (1u << 30) ? (1u << 30) : (uint32_t)rem64;
+                    const uint32_t wbud = CX->wave_budget ? CX->wave_budget - n_iter : (1u << 30);
+                    const uint32_t bud = rem < wbud ? rem : wbud;
+                    // rewritten code bytes as offsets from the text base (empty range if none)
+                    const uint64_t tlo = CX->text_lo;
+                    const uint32_t sdlo = m.code_dirty ? (uint32_t)((m.dlo > tlo ? m.dlo : tlo) - tlo) : 0xFFFFFFFFu;
+                    const uint32_t sdhi = m.code_dirty ? (uint32_t)((m.dhi > tlo ? m.dhi : tlo) - tlo) : 0u;
+                    const uint32_t lwm = L.watch > 0 ? (1u << L.watch) : 0u;
+                    uint32_t st = 0, xt = 0, fb = 0, db = 0;   // instructions, straddles, fetch/data bytes
+                    uint64_t spc = lpc;
+                    uint32_t etgt = 0xFFFFFFFFu;   // block an entry is routed to through its cycle headers
+#define TXR(r) uint64_t X##r = RREG(r);
+                    TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
+                    TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
+                    TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
+#undef TXR
+                    goto S_dispatch;
+                    /*@TX_SOLO@*/
+                S_out:
+#define TXW(r) RREG(r) = X##r;
+                    TXW(1) TXW(2) TXW(3) TXW(4) TXW(5) TXW(6) TXW(7) TXW(8) TXW(9) TXW(10) TXW(11) TXW(12) TXW(13)
+                    TXW(14) TXW(15) TXW(16) TXW(17) TXW(18) TXW(19) TXW(20) TXW(21) TXW(22) TXW(23) TXW(24) TXW(25)
+                    TXW(26) TXW(27) TXW(28) TXW(29) TXW(30) TXW(31)
+#undef TXW
+                    L.ninst += st; L.ncyc += st + xt; L.fetch_b += fb; L.data_b += db; L.pc = spc;
+                    n_iter += st;
+                    n_tx += st;
+                    n_txin++;
+                    if (st) continue;
+                }
+            } else if (tx_entry && wballot<kNL>(mine && (dirty_near(m, lpc) || L.injected == 3)) == 0) {
                 // lanes that rewrote code: every block checks its bytes against their range
                 const bool wdirty = uni32(wballot<kNL>(m.code_dirty) != 0);
                 const uint64_t ldlo = m.code_dirty ? m.dlo : kNone, ldhi = m.code_dirty ? m.dhi : 0;
@@ -958,21 +993,28 @@ __device__ __forceinline__ void trial_body() {
                 uint32_t lst = 0, lxt = 0, lfb = 0, ldb = 0;   // per lane: insts, straddles, fetch/data bytes
                 uint32_t wst = 0;                              // wave iterations
                 uint64_t spc = lpc, lp = 0, dpc = 0;
+                uint32_t etgt = 0xFFFFFFFFu;   // block an entry is routed to through its cycle headers
                 bool jdiv = false;
 #define TXR(r) uint64_t X##r = RREG(r);
                 TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
                 TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
                 TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
 #undef TXR
-#define TXC(st, xt, fb, db)                                                               \
-    do {                                                                                  \
-        const uint32_t mm_ = mine ? 0xFFFFFFFFu : 0u;                                     \
-        lst += (st) & mm_; lxt += (xt) & mm_; lfb += (fb) & mm_; ldb += (db) & mm_;       \
-        wst += (st);                                                                      \
+// a group parked at pc joins the running group (pc == pmin, lanes outside the
+// entry group all wait at higher pcs)
+#define TXMERGE(pc)                                                                          \
+    do {                                                                                     \
+        const bool jn_ = ((pend >> lane) & 1) && lp == (pc);                                 \
+        const uint64_t b_ = TXB(jn_);                                                        \
+        mine = mine || jn_;                                                                  \
+        gmr = uni64(gmr | b_);                                                               \
+        pend = uni64(pend & ~b_);                                                            \
+        pmin = uni64(pend ? wmin64<kNL>(((pend >> lane) & 1) ? lp : kNone) : kNone);         \
+        wmin = uni64(ult64(pmin, owm) ? pmin : owm);                                         \
     } while (0)
                 goto tx_dispatch;
                 /*@TX_BODY@*/
-#undef TXC
+#undef TXMERGE
             tx_sched:   // spc >= wmin: merge with the parked group, switch to it, or leave
                 if (!ult64(pmin, owm)) goto tx_out;   // lanes outside run first (or no parked lanes)
                 if (spc == pmin) {
