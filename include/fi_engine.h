@@ -73,6 +73,7 @@ typedef int32_t fi_status;
 #define FI_CRASH_SIGTRAP 8        /* ebreak -> SIGTRAP            arch/riscv/faults.cc:317-322 */
 #define FI_CRASH_STACK_LIMIT 9    /* fatal  max stack exceeded    sim/mem_state.cc:440 */
 #define FI_CRASH_AMO_LINE 10      /* panic  AMO across a cache line cpu/simple/atomic.cc:569-570 */
+#define FI_CRASH_SC_LINE 11       /* abort  SC across a cache line  cpu/simple/atomic.cc:482 assert(curr_frag_id == 0) */
 /* FI_ESCAPE sub-codes */
 #define FI_ESC_INST 1
 #define FI_ESC_SYSCALL 2
@@ -114,7 +115,7 @@ typedef struct {
     uint32_t lanes_per_wave;        /* trials per 64-lane wave in the first epoch: 1, 2, 4, ..., 64 (0 -> 64) */
     uint32_t resume_lanes;          /* trials per wave in resumed epochs (0 -> default): survivors have diverged, and
                                        a wave serialises its lanes' distinct control flows, so fewer per wave */
-    uint32_t epochs;                /* epochs per chunk (0 -> 4): budgets b, 4b, 16b, 16b, ..., unbounded */
+    uint32_t epochs;                /* epochs per chunk (0 -> 2): budgets b, 4b, 16b, 16b, ..., unbounded */
 } fi_config;
 /* fi_config.flags: trials start from process start / run to their natural end
  * (the plain serial semantics, for A/B checks; outcomes are identical) */

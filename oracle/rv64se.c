@@ -19,6 +19,7 @@
 #include <string.h>
 
 #define PAGE 4096ULL
+#define OR_NONE (~0ULL)
 #define PAGE_MASK (~(PAGE - 1))
 /* RiscvProcess64 ctor, arch/riscv/process.cc:71-82 */
 #define STACK_BASE 0x7FFFFFFFFFFFFFFFULL
@@ -125,6 +126,10 @@ typedef struct {
     /* fault injection */
     const or_site_t *site; int injected; int watch; /* watch = protected flipped reg, -1 none */
     int rarm, wrote;      /* result fault armed (OR_T_RESULT); the executing instruction wrote x[rd] */
+    /* LR/SC: the ISA's load reservation (isa.cc:1006-1064) and this context's
+     * lock record in memory (abstract_mem.cc:258-345), as virtual addresses
+     * (the SE page mapping is a per-page bijection); OR_NONE = none */
+    u64 resv, lock;
     u64 protect_mask;
     /* termination */
     int done; or_outcome_t res;
@@ -133,7 +138,8 @@ typedef struct {
     const or_campaign_t *c;
 } mach_t;
 
-enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_ESCAPE = 5, F_PGFAULT = 6, F_AMOLINE = 7 };
+enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_ESCAPE = 5, F_PGFAULT = 6, F_AMOLINE = 7,
+       F_SCLINE = 8 };
 
 /* -------------------------------------------------------------- decode */
 /* Op ids.  Names follow gem5's mnemonics (arch/riscv/isa/decoder.isa). */
@@ -166,7 +172,8 @@ enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_E
     X(fsgnj_s) X(fsgnjn_s) X(fsgnjx_s) X(fsgnj_d) X(fsgnjn_d) X(fsgnjx_d) X(fsgnj_h) X(fsgnjn_h) X(fsgnjx_h) \
     X(fclass_s) X(fclass_d) X(fclass_h) \
     X(amoadd_w) X(amoswap_w) X(amoxor_w) X(amoor_w) X(amoand_w) X(amomin_w) X(amomax_w) X(amominu_w) X(amomaxu_w) \
-    X(amoadd_d) X(amoswap_d) X(amoxor_d) X(amoor_d) X(amoand_d) X(amomin_d) X(amomax_d) X(amominu_d) X(amomaxu_d)
+    X(amoadd_d) X(amoswap_d) X(amoxor_d) X(amoor_d) X(amoand_d) X(amomin_d) X(amomax_d) X(amominu_d) X(amomaxu_d) \
+    X(lr_w) X(sc_w) X(lr_d) X(sc_d)
 
 enum {
 #define X(n) OP_##n,
@@ -243,8 +250,15 @@ static void refine_fp_amo(u32 raw, dec_t *d) {
         static const int w[32] = {[0x00] = OP_amoadd_w, [0x01] = OP_amoswap_w, [0x04] = OP_amoxor_w,
                                   [0x08] = OP_amoor_w, [0x0c] = OP_amoand_w, [0x10] = OP_amomin_w,
                                   [0x14] = OP_amomax_w, [0x18] = OP_amominu_w, [0x1c] = OP_amomaxu_w};
-        int o = w[bits(raw, 31, 27)];
-        if (!o) return;   /* lr / sc: escape */
+        u32 f5 = bits(raw, 31, 27);
+        if (f5 == 0x02 || f5 == 0x03) {   /* lr / sc (decoder.isa:2069-2075, 2175-2181) */
+            d->op = f5 == 0x02 ? (f3 == 2 ? OP_lr_w : OP_lr_d) : (f3 == 2 ? OP_sc_w : OP_sc_d);
+            d->rd = rd; d->rs1 = rs1; d->rs2 = f5 == 0x03 ? rs2 : -1; d->imm = 0;
+            d->funct3 = bits(raw, 26, 25);   /* aq << 1 | rl */
+            return;
+        }
+        int o = w[f5];
+        if (!o) return;
         d->op = f3 == 2 ? o : o + (OP_amoadd_d - OP_amoadd_w);
         d->rd = rd; d->rs1 = rs1; d->rs2 = rs2; d->imm = 0;
         d->funct3 = bits(raw, 26, 25);   /* aq << 1 | rl: the macro-op's fence micro-ops */
@@ -672,6 +686,9 @@ static int mem_write(mach_t *m, u64 addr, unsigned size, u64 val, u64 *fault_va)
         uint8_t *pg = translate_w(m, a);
         if (!pg) { *fault_va = a; return F_PGFAULT; }
         for (unsigned i = 0; i < frag; i++) pg[(a + i) & (PAGE - 1)] = (uint8_t)(val >> (8 * (done + i)));
+        /* AbstractMemory::checkLockedAddrList: a store erases the lock records
+         * of its fragment's 16-byte granule (abstract_mem.cc:290-345) */
+        if (m->lock == (a & ~0xFULL)) m->lock = OR_NONE;
         done += frag; a += frag;
     }
     m->data_bytes += size;
@@ -834,6 +851,59 @@ static int csr_u_accessible(u32 csr) {
     if (csr >= 0xC00 && csr <= 0xC1F) return 1;
     if (csr >= 0xC20 && csr <= 0xC22) return 1;
     return 0;                              /* absent from CSRData, or RV32-only *H */
+}
+
+/* LR: AtomicSimpleCPU::readMem with an LLSC request (atomic.cc:331-434): each
+ * fragment that is read sets the ISA reservation to its address
+ * (ISA::handleLockedRead, isa.cc:1006-1013) and makes it this context's lock
+ * record (AbstractMemory::trackLoadLocked, abstract_mem.cc:258-283). */
+static int lr_read(mach_t *m, u64 addr, unsigned size, u64 *val, u64 *fault_va) {
+    u64 v = 0;
+    unsigned done = 0;
+    u64 a = addr;
+    while (done < size) {
+        unsigned frag = 64 - (unsigned)(a & 63);
+        if (frag > size - done) frag = size - done;
+        if (a + frag - 1 < a) { *fault_va = a; return F_PGFAULT; }
+        uint8_t *pg = translate(m, a);
+        if (!pg) { *fault_va = a; return F_PGFAULT; }
+        for (unsigned i = 0; i < frag; i++) v |= (u64)pg[(a + i) & (PAGE - 1)] << (8 * (done + i));
+        m->resv = a;
+        m->lock = a & ~0xFULL;
+        done += frag; a += frag;
+    }
+    *val = v;
+    m->data_bytes += size;
+    return F_NONE;
+}
+/* SC: AtomicSimpleCPU::writeMem with an LLSC request (atomic.cc:437-544).
+ * Per fragment, after translation: the ISA check (ISA::handleLockedWrite,
+ * isa.cc:1015-1060) fails when the reservation is empty or in another 64-byte
+ * line, and clears it either way; a passing store reaches memory, which
+ * performs it only if this context's lock record is the fragment's granule
+ * (abstract_mem.cc:290-345) and then erases the record.  A second fragment
+ * trips assert(curr_frag_id == 0) after its translation.  *ok = success. */
+static int sc_write(mach_t *m, u64 addr, unsigned size, u64 val, int *ok, u64 *fault_va) {
+    unsigned frag = 64 - (unsigned)(addr & 63);
+    if (frag > size) frag = size;
+    if (addr + frag - 1 < addr) { *fault_va = addr; return F_PGFAULT; }
+    uint8_t *pg = translate_w(m, addr);
+    if (!pg) { *fault_va = addr; return F_PGFAULT; }
+    int pass = m->resv != OR_NONE && (m->resv & ~63ULL) == (addr & ~63ULL);
+    m->resv = OR_NONE;
+    *ok = 0;
+    if (pass && m->lock == (addr & ~0xFULL)) {
+        for (unsigned i = 0; i < frag; i++) pg[(addr + i) & (PAGE - 1)] = (uint8_t)(val >> (8 * i));
+        m->lock = OR_NONE;
+        *ok = 1;
+    }
+    if (frag < size) {
+        u64 a2 = addr + frag;
+        if (a2 + (size - frag) - 1 < a2 || !translate(m, a2)) { *fault_va = a2; return F_PGFAULT; }
+        return F_SCLINE;
+    }
+    if (*ok) m->data_bytes += size;
+    return F_NONE;
 }
 
 /* Execute one decoded instruction (the generated StaticInst::execute bodies of
@@ -1053,6 +1123,23 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
         v = w ? sx32(old) : old;
         break;
     }
+    /* ---- LR / SC (formats/amo.isa LoadReserved / StoreCond; rl/aq fence
+     * micro-ops are one tick each, like the AMOs) */
+    case OP_lr_w: case OP_lr_d: {
+        unsigned sz = d->op == OP_lr_w ? 4 : 8;
+        r = lr_read(m, a, sz, &t, fault_va); if (r) return r;
+        m->num_cycles += (d->funct3 & 1) + (d->funct3 >> 1);
+        v = sz == 4 ? sx32(t) : t;
+        break;
+    }
+    case OP_sc_w: case OP_sc_d: {
+        unsigned sz = d->op == OP_sc_w ? 4 : 8;
+        int ok = 0;
+        r = sc_write(m, a, sz, b, &ok, fault_va); if (r) return r;
+        m->num_cycles += (d->funct3 & 1) + (d->funct3 >> 1);
+        v = ok ? 0 : 1;   /* result = !success (amo.isa StoreCondExecute) */
+        break;
+    }
     default: return F_UNKNOWN;
     }
     wrreg(m, d->rd, v);
@@ -1102,6 +1189,7 @@ static void invoke_fault(mach_t *m, int f, u64 fault_va, const dec_t *d) {
     case F_ESCAPE: finish(m, OR_ESCAPE, OR_ESC_INST, 0); m->res.detail = d->raw; return;
     case F_ESCAPE + 100: finish(m, OR_ESCAPE, OR_ESC_CSR, 0); m->res.detail = d->raw; return;
     case F_AMOLINE: finish(m, OR_CRASH, OR_CRASH_AMO_LINE, 134); return;
+    case F_SCLINE: finish(m, OR_CRASH, OR_CRASH_SC_LINE, 134); return;
     case 100: finish(m, OR_DETECTED, 0, 0); return;
     case F_PGFAULT: {
         int h = fixup_fault(m, fault_va);
@@ -1360,6 +1448,7 @@ static void mach_init(mach_t *m, const or_campaign_t *c) {
     m->pc = c->entry;
     m->stack_min = c->stack_min0;
     m->watch = -1;
+    m->resv = m->lock = OR_NONE;
 }
 static void mach_free(mach_t *m) { pm_free(&m->mem); free(m->out.buf); free(m->err.buf); }
 
@@ -1510,7 +1599,7 @@ int or_probe(u32 inst, u64 pc, const u64 regs[32], or_probe_t *o) {
     pm_init(&m.mem, 64);
     for (int i = 0; i < 32; i++) m.x[i] = regs[i];
     m.x[0] = 0;
-    m.pc = pc; m.watch = -1; m.stack_min = STACK_BASE;
+    m.pc = pc; m.watch = -1; m.stack_min = STACK_BASE; m.resv = m.lock = OR_NONE;
     dec_t d; decode(inst, &d);
     m.npc = pc + d.len;
     /* memory: every page the access touches is mapped zero (probe semantics) */

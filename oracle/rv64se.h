@@ -37,7 +37,8 @@ enum {
     OR_CRASH_FD_ASSERT = 7,     /* abort: FDArray assert          fd_array.cc:320-323 */
     OR_CRASH_SIGTRAP = 8,       /* ebreak -> kill(SIGTRAP)        faults.cc:317-322, debug.cc:64-70 */
     OR_CRASH_STACK_LIMIT = 9,   /* fatal: Maximum stack size      mem_state.cc:440 */
-    OR_CRASH_AMO_LINE = 10      /* panic: AMO across a cache line atomic.cc:569-570 */
+    OR_CRASH_AMO_LINE = 10,     /* panic: AMO across a cache line atomic.cc:569-570 */
+    OR_CRASH_SC_LINE = 11       /* abort: SC across a cache line  atomic.cc:482 assert(curr_frag_id == 0) */
 };
 enum {
     OR_ESC_INST = 1,            /* instruction gem5 decodes but the engine does not model */

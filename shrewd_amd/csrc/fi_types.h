@@ -64,6 +64,7 @@ struct LaneSave {
     uint32_t flags;                  // bit 0 out_bad, bits 1-2 injected, bit 3 code_dirty, bit 4 FP state
     uint32_t dlo, dhi;               // rewritten code bytes [code_lo + dlo, code_lo + dhi) (if code_dirty)
     uint32_t pad;
+    uint64_t resv, lock;             // LR/SC: load reservation and lock record (~0 = none)
 };
 
 // Everything one launch of the trial kernel needs.  Passed by value as the

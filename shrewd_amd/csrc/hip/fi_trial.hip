@@ -133,6 +133,11 @@ struct LaneMem {
     const uint8_t *req_src;
     bool code_dirty;
     uint64_t dlo, dhi;             // bounding range of the code bytes the lane rewrote (valid if code_dirty)
+    // LR/SC: the ISA's load reservation (isa.cc:1006-1064) and this context's
+    // lock record in memory (abstract_mem.cc:258-345), as virtual addresses
+    // (the SE mapping is a per-page bijection); kNone = none.  A lane holding a
+    // lock record stays on the general path, whose stores erase it.
+    uint64_t resv, lock;
 };
 
 // The golden pre-decode of the instruction at pc is stale for this lane only if
@@ -222,27 +227,54 @@ __device__ __forceinline__ uint64_t lookup(KCtx *c, const WaveMem &w, LaneMem &m
 __device__ __forceinline__ const uint8_t *page_of(uint64_t p) { return (const uint8_t *)(p & ~1ULL); }
 
 enum { F_NONE = 0, F_SYSCALL, F_BREAK, F_ILLEGAL, F_UNKNOWN, F_ESCAPE, F_ESCCSR, F_PGFAULT, F_NEEDPAGE, F_DETECT,
-       F_AMOLINE };
+       F_AMOLINE, F_SCLINE };
 
 // AtomicSimpleCPU::readMem/writeMem (atomic.cc:331-544): the access is split
 // at 64-byte line boundaries, each fragment translated on its own; faults are
 // raised in fragment order.  Writes to a shared page request a copy-on-write
-// page first (not a gem5 event: the tick is retried).
+// page first (not a gem5 event: the tick is retried).  llsc: 1 = LR (each
+// fragment read sets the reservation and the lock record), 2 = SC (val in:
+// data, out: 1 if the store was performed), 3 = AMO.  Plain stores erase the
+// lock record of their fragment's 16-byte granule (abstract_mem.cc:290-345);
+// AMOs do not.
 __device__ int mem_access(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t ea,
-                          uint32_t size, bool wr, uint64_t &val, uint64_t &fva) {
+                          uint32_t size, bool wr, uint64_t &val, uint64_t &fva, int llsc) {
     uint32_t n1 = 64 - (uint32_t)(ea & 63);
     if (n1 > size) n1 = size;
     if (ea + n1 - 1 < ea) { fva = ea; return F_PGFAULT; }
     const uint64_t p1 = lookup(c, w, m, slot, ea >> 12);
     if (!p1) { fva = ea; return F_PGFAULT; }
     const uint64_t ea2 = ea + n1;
+    const uint32_t off = (uint32_t)(ea & 4095);
+    if (llsc == 2) {
+        // SC (atomic.cc:437-544, ISA::handleLockedWrite isa.cc:1015-1060):
+        // the ISA check after translation clears the reservation either way;
+        // memory performs a passing store only if this context's lock record
+        // is the fragment's granule, then erases it.  A second fragment trips
+        // assert(curr_frag_id == 0) after its translation.
+        if (!(p1 & 1)) { m.req_vpn = ea >> 12; m.req_src = page_of(p1); return F_NEEDPAGE; }
+        const bool pass = m.resv != kNone && (m.resv & ~63ULL) == (ea & ~63ULL);
+        m.resv = kNone;
+        const bool ok = pass && m.lock == (ea & ~0xFULL);
+        if (ok) {
+            uint8_t *w1 = const_cast<uint8_t *>(page_of(p1));
+            for (uint32_t i = 0; i < n1; i++) w1[off + i] = (uint8_t)(val >> (8 * i));
+            if (ea < c->code_hi && ea + n1 > c->code_lo) mark_dirty(m, ea, ea + n1);
+            m.lock = kNone;
+        }
+        val = ok ? 1 : 0;
+        if (n1 < size) {
+            if (ea2 + (size - n1) - 1 < ea2 || !lookup(c, w, m, slot, ea2 >> 12)) { fva = ea2; return F_PGFAULT; }
+            return F_SCLINE;
+        }
+        return F_NONE;
+    }
     uint64_t p2 = p1;
     if (n1 < size) {
-        if (ea2 + (size - n1) - 1 < ea2) { fva = ea2; return F_PGFAULT; }
+        if (ea2 + (size - n1) - 1 < ea2) { fva = ea2; if (llsc) { m.resv = ea; m.lock = ea & ~0xFULL; } return F_PGFAULT; }
         p2 = lookup(c, w, m, slot, ea2 >> 12);
-        if (!p2) { fva = ea2; return F_PGFAULT; }
+        if (!p2) { fva = ea2; if (llsc) { m.resv = ea; m.lock = ea & ~0xFULL; } return F_PGFAULT; }
     }
-    const uint32_t off = (uint32_t)(ea & 4095);
     if (wr) {
         if (!(p1 & 1)) { m.req_vpn = ea >> 12; m.req_src = page_of(p1); return F_NEEDPAGE; }
         if (!(p2 & 1)) { m.req_vpn = ea2 >> 12; m.req_src = page_of(p2); return F_NEEDPAGE; }
@@ -259,6 +291,8 @@ __device__ int mem_access(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, 
             uint8_t *w2 = const_cast<uint8_t *>(page_of(p2));
             for (uint32_t i = 0; i < size; i++) (i < n1 ? w1 : w2)[(ea + i) & 4095] = (uint8_t)(val >> (8 * i));
         }
+        // (an AMO's write, llsc == 3, leaves the lock records alone: atomic.cc:546-608)
+        if (llsc != 3 && (m.lock == (ea & ~0xFULL) || (n1 < size && m.lock == (ea2 & ~0xFULL)))) m.lock = kNone;
     } else {
         const uint8_t *r1 = page_of(p1);
         uint64_t v = 0;
@@ -274,6 +308,10 @@ __device__ int mem_access(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, 
             for (uint32_t i = 0; i < size; i++) v |= (uint64_t)(i < n1 ? r1 : r2)[(ea + i) & 4095] << (8 * i);
         }
         val = v;
+        if (llsc) {   // LR: the last fragment read holds the reservation (ISA::handleLockedRead, trackLoadLocked)
+            m.resv = n1 < size ? ea2 : ea;
+            m.lock = m.resv & ~0xFULL;
+        }
     }
     return F_NONE;
 }
@@ -702,12 +740,14 @@ __device__ __forceinline__ void trial_body() {
     m.tp0 = m.tp1 = m.tp2 = m.tp3 = 0;
     m.tnext = 0; m.n_priv = 0; m.req_vpn = kNone; m.req_src = nullptr; m.code_dirty = false;
     m.dlo = m.dhi = 0;
+    m.resv = m.lock = kNone;
     if (resume && live) {
         L.pc = SV->pc; L.ninst = SV->ninst; L.ncyc = SV->ncyc; L.out_pos = SV->out_pos; L.err_pos = SV->err_pos;
         L.next_chk = SV->next_chk; L.nfail = SV->nfail; L.watch = SV->watch;
         L.out_bad = SV->flags & 1; L.injected = (uint8_t)((SV->flags >> 1) & 3); L.fp = (SV->flags >> 4) & 1;
         m.stack_min = SV->stack_min; m.n_priv = SV->n_priv; m.code_dirty = (SV->flags >> 3) & 1;
         m.dlo = CX->code_lo + SV->dlo; m.dhi = CX->code_lo + SV->dhi;
+        m.resv = SV->resv; m.lock = SV->lock;
     }
     bool suspended = false;
     const uint64_t start_inst = (live && !resume) ? L.ninst : 0;
@@ -728,6 +768,28 @@ __device__ __forceinline__ void trial_body() {
     __shared__ uint32_t WS[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) WS[k] = 0;
+    // solo only: decode cache of the lane's rewritten code (code range, keyed by
+    // exact pc).  Every store into the code range goes through mem_access (the
+    // pre-decoded and translated paths refuse them), which drops the entries
+    // it overlaps, so a hit equals a fresh fetch + decode.
+    constexpr uint32_t kDC = kNL == 1 ? 64u : 1u;
+    __shared__ uint32_t DCT[kDC];   // tag: pc - text_lo (0xFFFFFFFF empty)
+    __shared__ Pre4 DCE[kDC];
+    if constexpr (kNL == 1) {
+#pragma unroll 8
+        for (uint32_t k = 0; k < kDC; k++) DCT[k] = 0xFFFFFFFFu;
+    }
+#define DC_INVAL(lo_, sz_)                                                                          \
+    do {                                                                                            \
+        if constexpr (kNL == 1) {                                                                   \
+            const uint64_t a_ = (lo_), e_ = a_ + (sz_);                                             \
+            if (a_ < CX->code_hi && e_ > CX->code_lo)                                               \
+                for (uint64_t q_ = (a_ > 3 ? a_ - 3 : 0); q_ < e_; q_++) {                          \
+                    const uint32_t i_ = (uint32_t)(q_ >> 1) & (kDC - 1);                            \
+                    if (DCT[i_] == (uint32_t)(q_ - CX->text_lo)) DCT[i_] = 0xFFFFFFFFu;             \
+                }                                                                                   \
+        }                                                                                           \
+    } while (0)
 #define n_slow WS[0]
 #define n_min WS[1]
 #define n_exec WS[2]
@@ -751,6 +813,7 @@ __device__ __forceinline__ void trial_body() {
                 sv->dhi = m.code_dirty ? (uint32_t)((m.dhi < CX->code_hi ? m.dhi : CX->code_hi) - CX->code_lo) : 0;
                 sv->flags = (L.out_bad ? 1u : 0u) | ((uint32_t)L.injected << 1) | (m.code_dirty ? 8u : 0u) |
                             (L.fp ? 16u : 0u);
+                sv->resv = m.resv; sv->lock = m.lock;
                 CX->surv[atomicAdd(CX->surv_n, 1u)] = (uint32_t)slot;
                 suspended = true;
                 L.done = true;
@@ -807,6 +870,7 @@ __device__ __forceinline__ void trial_body() {
                     uint64_t *wp = (uint64_t *)(const_cast<uint8_t *>(page_of(p)) + (s.addr & 4095));
                     *wp ^= s.mask;
                     if (s.addr < CX->code_hi && s.addr + 8 > CX->code_lo) mark_dirty(m, s.addr, s.addr + 8);
+                    DC_INVAL(s.addr, 8);
                     L.injected = 1;
                 }
             } else {
@@ -830,7 +894,8 @@ __device__ __forceinline__ void trial_body() {
                 pend &= ~wballot<kNL>(grp);
                 const SnapState *S = CX->snaps + (uint32_t)(kn / CX->snap_interval);
                 bool eq = grp && L.pc == S->pc && L.out_pos == S->out_pos && L.err_pos == S->err_pos && !L.out_bad &&
-                          m.stack_min == S->stack_min && !L.fp && L.injected != 3;
+                          m.stack_min == S->stack_min && !L.fp && L.injected != 3 && m.resv == kNone &&
+                          m.lock == kNone;
                 if (wballot<kNL>(eq)) {
                     // a register the golden future writes before reading it cannot
                     // influence the outcome (liveness from the golden trace)
@@ -935,7 +1000,7 @@ __device__ __forceinline__ void trial_body() {
             if constexpr (kNL == 1) {
                 // ---- solo: one trial, every value uniform -- no groups, no
                 // parking, plain register writes; the same exits and counters
-                if (tx_entry && mine && !dirty_near(m, lpc) && L.injected != 3) {
+                if (tx_entry && mine && !dirty_near(m, lpc) && L.injected != 3 && m.lock == kNone) {
                     const uint64_t rem64 = next_ev - L.ninst;
                     const uint32_t rem = rem64 > (1u << 30) ? (1u << 30) : (uint32_t)rem64;
                     const uint32_t wbud = CX->wave_budget ? CX->wave_budget - n_iter : (1u << 30);
@@ -967,7 +1032,8 @@ __device__ __forceinline__ void trial_body() {
                     n_txin++;
                     if (st) continue;
                 }
-            } else if (tx_entry && wballot<kNL>(mine && (dirty_near(m, lpc) || L.injected == 3)) == 0) {
+            } else if (tx_entry &&
+                       wballot<kNL>(mine && (dirty_near(m, lpc) || L.injected == 3 || m.lock != kNone)) == 0) {
                 // lanes that rewrote code: every block checks its bytes against their range
                 const bool wdirty = uni32(wballot<kNL>(m.code_dirty) != 0);
                 const uint64_t ldlo = m.code_dirty ? m.dlo : kNone, ldhi = m.code_dirty ? m.dhi : 0;
@@ -1059,12 +1125,14 @@ __device__ __forceinline__ void trial_body() {
         // diverges, meets another group, or hits something the general path owns
         // (K_SLOW op, fault, page request, syscall).  Nothing commits unless the
         // whole instruction commits for every group lane.
+        // (an armed result fault commits in the general path, and a lane holding
+        // an LR/SC lock record stays there: only its stores erase the record)
         if (CX->pre_ok && lpc >= CX->text_lo && lpc < CX->text_hi &&
-            wballot<kNL>(mine && L.injected == 3) == 0) {   // an armed result fault commits in the general path
+            wballot<kNL>(mine && (L.injected == 3 || m.lock != kNone)) == 0) {
             // lanes that rewrote code run here too, until they reach a rewritten
             // instruction; lanes watching a protected flipped register, until an
             // instruction reads it (the general path classifies the detection)
-            const bool any_dirty = wballot<kNL>(mine && m.code_dirty) != 0;
+            bool any_dirty = wballot<kNL>(mine && m.code_dirty) != 0;
             const bool any_watch = wballot<kNL>(mine && L.watch > 0) != 0;
             const uint64_t gm = wballot<kNL>(mine);
             const int glane = __ffsll((unsigned long long)gm) - 1;
@@ -1085,6 +1153,13 @@ __device__ __forceinline__ void trial_body() {
                     // the group rewrote this instruction: decode the bytes the
                     // lanes hold now (Decoder::moreBytes on their own pages) when
                     // they all hold the same; otherwise the general path
+                    bool hit = false;
+                    const bool in_code = spc >= CX->code_lo && spc < CX->code_hi;
+                    if constexpr (kNL == 1) {
+                        const uint32_t ci = (uint32_t)(spc >> 1) & (kDC - 1);
+                        if (in_code && DCT[ci] == (uint32_t)(spc - CX->text_lo)) { E.e = DCE[ci]; E.in = true; hit = true; }
+                    }
+                    if (!hit) {
                     uint32_t raw = 0, t = 1;
                     uint64_t fva = 0;
                     int fr = 0;
@@ -1100,6 +1175,14 @@ __device__ __forceinline__ void trial_body() {
                     E.e.z = (uint32_t)dd.imm;
                     E.e.w = (uint32_t)dd.len |
                             ((uint32_t)(kPreValid | (uni32(t0) == 2 ? kPreStraddle : 0) | dd.flags) << 8) | (u << 16);
+                    if constexpr (kNL == 1) {
+                        if (in_code) {
+                            const uint32_t ci = (uint32_t)(spc >> 1) & (kDC - 1);
+                            DCT[ci] = (uint32_t)(spc - CX->text_lo);
+                            DCE[ci] = E.e;
+                        }
+                    }
+                    }
                     PSTAMP(5);
                 }
                 const uint32_t q1 = uni32(E.e.y), q2 = uni32(E.e.z), q3 = uni32(E.e.w);
@@ -1147,6 +1230,18 @@ __device__ __forceinline__ void trial_body() {
                 case K_SRL: v = (w32 ? (av & 0xFFFFFFFFULL) : av) >> (bv & shm); break;
                 case K_SRA: v = (uint64_t)((w32 ? (int64_t)(int32_t)av : (int64_t)av) >> (bv & shm)); break;
                 case K_MUL: v = av * bv; break;
+                // M-extension high products and division (utility.hh:171-231)
+                case K_MULH: v = (uint64_t)__mul64hi((int64_t)av, (int64_t)bv); break;
+                case K_MULHU: v = __umul64hi(av, bv); break;
+                case K_MULHSU: v = __umul64hi(av, bv) - (((int64_t)av < 0) ? bv : 0); break;
+                case K_DIV: v = w32 ? divw(av, bv) : div64(av, bv); break;
+                case K_DIVU:
+                    v = w32 ? ((uint32_t)bv == 0 ? ~0ULL : sx32((uint32_t)av / (uint32_t)bv)) : (bv == 0 ? ~0ULL : av / bv);
+                    break;
+                case K_REM: v = w32 ? remw(av, bv) : rem64(av, bv); break;
+                case K_REMU:
+                    v = w32 ? ((uint32_t)bv == 0 ? sx32(av) : sx32((uint32_t)av % (uint32_t)bv)) : (bv == 0 ? av : av % bv);
+                    break;
                 case K_NOP: wr = false; break;
                 case K_JAL: v = ft; npc = spc + imm; took = true; break;
                 case K_JALR: {
@@ -1183,8 +1278,19 @@ __device__ __forceinline__ void trial_body() {
                         p = tlb_find(m, ea >> 12);
                         if (!p) p = lookup_full(CX, w, m, slot, ea >> 12);
                     }
-                    const bool ok = p && (!st || ((p & 1) && (ea >= tx.chi || ea + msz <= tx.clo))) && off + msz <= 4096;
+                    // a store into the code range rewrites the lane's code: the
+                    // general path's business, except in the solo kernel, which
+                    // marks it here (dirty range, decode cache, any_dirty)
+                    const bool code_st = st && !(ea >= tx.chi || ea + msz <= tx.clo);
+                    const bool ok = p && (!st || ((p & 1) && (kNL == 1 || !code_st))) && off + msz <= 4096;
                     if (wballot<kNL>(mine && !ok) != 0) { msz = 0xFFFFFFFFu; break; }   // bail: general path
+                    if constexpr (kNL == 1) {
+                        if (code_st) {
+                            mark_dirty(m, ea, ea + msz);
+                            DC_INVAL(ea, msz);
+                            any_dirty = true;
+                        }
+                    }
                     if (mine) {
                         uint8_t *pg = const_cast<uint8_t *>(page_of(p));
                         const bool al = (off & (msz - 1)) == 0;
@@ -1269,6 +1375,20 @@ __device__ __forceinline__ void trial_body() {
                 ticks = (pflags & kPreStraddle) ? 2 : 1;
             }
         }
+        if constexpr (kNL == 1) {   // solo: rewritten code decoded before (DCT/DCE)
+            if (!fast && L.pc >= CX->code_lo && L.pc < CX->code_hi) {
+                const uint32_t ci = (uint32_t)(L.pc >> 1) & (kDC - 1);
+                if (DCT[ci] == (uint32_t)(L.pc - CX->text_lo)) {
+                    const Pre4 q = DCE[ci];
+                    const uint32_t pflags = (q.w >> 8) & 0xFF;
+                    fast = true;
+                    d.raw = q.x; d.op = (uint8_t)q.y; d.rd = (uint8_t)(q.y >> 8); d.rs1 = (uint8_t)(q.y >> 16);
+                    d.rs2 = (uint8_t)(q.y >> 24); d.imm = (int32_t)q.z; d.len = (uint8_t)q.w;
+                    d.flags = (uint8_t)pflags; d.aux = (uint16_t)(q.w >> 16);
+                    ticks = (pflags & kPreStraddle) ? 2 : 1;
+                }
+            }
+        }
         if (!fast) {
             PSTAMP(4);
             n_slow++;
@@ -1299,6 +1419,20 @@ __device__ __forceinline__ void trial_body() {
             PSTAMP(5);
             d = rv_decode(lraw);
             ticks = lt;
+            if constexpr (kNL == 1) {
+                if (L.pc >= CX->code_lo && L.pc < CX->code_hi) {
+                    Dec dd = d;
+                    const uint32_t u = uop_of(dd);   // uop_of may normalise dd.imm (the fast path's form)
+                    const uint32_t ci = (uint32_t)(L.pc >> 1) & (kDC - 1);
+                    DCT[ci] = (uint32_t)(L.pc - CX->text_lo);
+                    DCE[ci].x = dd.raw;
+                    DCE[ci].y = (uint32_t)dd.op | ((uint32_t)dd.rd << 8) | ((uint32_t)dd.rs1 << 16) |
+                                ((uint32_t)dd.rs2 << 24);
+                    DCE[ci].z = (uint32_t)dd.imm;
+                    DCE[ci].w = (uint32_t)dd.len | ((uint32_t)(kPreValid | (lt == 2 ? kPreStraddle : 0) | dd.flags) << 8) |
+                                (u << 16);
+                }
+            }
 #ifdef FI_PROF
             asm volatile("" :: "s"((uint32_t)d.op), "s"((uint32_t)d.imm));
 #endif
@@ -1330,6 +1464,7 @@ __device__ __forceinline__ void trial_body() {
         uint32_t fbox = 0;            // FP destination: 0 none, 1 fval, 16/32/64 loaded (NaN-boxed) width
         uint32_t xticks = 0;          // extra micro-op ticks (AMO fences)
         int amo = -1;                 // AMO read-modify-write op (amo_apply), -1 none
+        int llsc = 0;                 // 1 LR, 2 SC
 #define FREG_RD(r) (L.fp ? CX->fregs[(uint64_t)(r) * CX->n_slots + slot] : 0ULL)
         // detected-by-replica: the flipped protected register is read before
         // being overwritten (build-defined SHREWD semantics)
@@ -1524,6 +1659,18 @@ __device__ __forceinline__ void trial_body() {
                 xticks = ((d.raw >> 25) & 1) + ((d.raw >> 26) & 1);   // rl, aq (pre-decoded aux holds the micro-op)
                 break;
             }
+            // ---- LR / SC (formats/amo.isa LoadReserved / StoreCond; the rl / aq
+            // fence micro-ops are one tick each, like the AMOs')
+            case OP_lr_w: case OP_lr_d:
+                msz = d.op == OP_lr_w ? 4 : 8; mext = msz == 4 ? 32 : 0; llsc = 1;
+                xticks = ((d.raw >> 25) & 1) + ((d.raw >> 26) & 1);
+                if (CX->record) CX->stats[22] = 1;   // golden LR/SC state is not in the snapshots
+                break;
+            case OP_sc_w: case OP_sc_d:
+                msz = d.op == OP_sc_w ? 4 : 8; llsc = 2;
+                xticks = ((d.raw >> 25) & 1) + ((d.raw >> 26) & 1);
+                if (CX->record) CX->stats[22] = 1;
+                break;
             default: f = F_UNKNOWN; break;
             }
         }
@@ -1532,18 +1679,20 @@ __device__ __forceinline__ void trial_body() {
         if (msz && f == F_NONE) {
             // one call site (an AMO reads, then writes, in a second pass): a
             // second inlined copy of mem_access puts the lane state in scratch
-            const uint64_t ea = amo >= 0 ? a : a + imm;
+            const uint64_t ea = (amo >= 0 || llsc) ? a : a + imm;
             uint64_t old = 0;
 #pragma unroll 1
             for (int pass = 0; pass < (amo >= 0 ? 2 : 1); pass++) {
-                t = pass ? amo_apply(amo, old, b, msz == 4) : (amo >= 0 ? 0 : sval);
-                f = mem_access(CX, w, m, slot, ea, msz, pass ? true : mst, t, fva);
+                t = pass ? amo_apply(amo, old, b, msz == 4) : (amo >= 0 ? 0 : (llsc == 2 ? b : sval));
+                f = mem_access(CX, w, m, slot, ea, msz, pass ? true : mst, t, fva, amo >= 0 ? 3 : llsc);
                 if (f != F_NONE) break;
                 if (!pass) old = t;
             }
             if (f == F_NONE) {
-                L.data_b += amo >= 0 ? 2 * msz : msz;
+                if (mst || amo >= 0 || (llsc == 2 && t)) DC_INVAL(ea, msz);   // rewritten code: drop its cached decodes
+                if (llsc != 2 || t) L.data_b += amo >= 0 ? 2 * msz : msz;
                 if (amo >= 0) v = msz == 4 ? sx32(old) : old;
+                else if (llsc == 2) v = t ? 0 : 1;   // rd = !success (amo.isa StoreCondExecute)
                 else if (!mst) {
                     if (fbox) fval = fbox == 16 ? (0xFFFFFFFFFFFF0000ULL | t) : fbox == 32 ? (0xFFFFFFFF00000000ULL | t) : t;
                     else v = mext ? (uint64_t)sext64(t, mext) : t;
@@ -1596,6 +1745,7 @@ __device__ __forceinline__ void trial_body() {
         case F_ESCCSR: finish(L, FI_ESCAPE, FI_ESC_CSR, 0, d.raw); break;
         case F_DETECT: finish(L, FI_DETECTED, 0, 0, (uint32_t)pc); break;
         case F_AMOLINE: finish(L, FI_CRASH, FI_CRASH_AMO_LINE, 134, (uint32_t)pc); break;
+        case F_SCLINE: finish(L, FI_CRASH, FI_CRASH_SC_LINE, 134, (uint32_t)pc); break;
         case F_PGFAULT:
             if (fva < m.stack_min && fva >= kStackBase - kMaxStack) {
                 const uint64_t nm = fva & ~4095ULL;
@@ -1628,8 +1778,12 @@ __device__ __forceinline__ void trial_body() {
             tn.bytes = CX->text_bytes; tn.clo = CX->code_lo; tn.chi = CX->code_hi;
             const PreRef En = pre_entry(tn, npc0);
             const uint32_t wn = uni32(En.e.w);
-            if (En.in && ((wn >> 8) & kPreValid) && ((wn >> 16) & 63) != K_SLOW &&
-                wballot<kNL>(cont && dirty_at(m, npc0)) == 0)
+            // (solo: a lane in rewritten code goes back too; the pre-decoded
+            // path decodes its own bytes through the decode cache)
+            const bool dty = wballot<kNL>(cont && dirty_at(m, npc0)) != 0;
+            const bool lck = wballot<kNL>(cont && m.lock != kNone) != 0;
+            if (!lck && En.in && ((wn >> 8) & kPreValid) &&
+                ((kNL == 1 && dty) || (((wn >> 16) & 63) != K_SLOW && !dty)))
                 break;
         }
         lpc = npc0;

@@ -41,7 +41,8 @@
     X(fsgnj_s) X(fsgnjn_s) X(fsgnjx_s) X(fsgnj_d) X(fsgnjn_d) X(fsgnjx_d) X(fsgnj_h) X(fsgnjn_h) X(fsgnjx_h) \
     X(fclass_s) X(fclass_d) X(fclass_h) \
     X(amoadd_w) X(amoswap_w) X(amoxor_w) X(amoor_w) X(amoand_w) X(amomin_w) X(amomax_w) X(amominu_w) X(amomaxu_w) \
-    X(amoadd_d) X(amoswap_d) X(amoxor_d) X(amoor_d) X(amoand_d) X(amomin_d) X(amomax_d) X(amominu_d) X(amomaxu_d)
+    X(amoadd_d) X(amoswap_d) X(amoxor_d) X(amoor_d) X(amoand_d) X(amomin_d) X(amomax_d) X(amominu_d) X(amomaxu_d) \
+    X(lr_w) X(sc_w) X(lr_d) X(sc_d)
 
 namespace fi {
 
@@ -397,7 +398,13 @@ __device__ inline void rv_refine_fp_amo(uint32_t raw, Dec &d) {
         case 0x00: o = OP_amoadd_w; break;  case 0x01: o = OP_amoswap_w; break; case 0x04: o = OP_amoxor_w; break;
         case 0x08: o = OP_amoor_w; break;   case 0x0c: o = OP_amoand_w; break;  case 0x10: o = OP_amomin_w; break;
         case 0x14: o = OP_amomax_w; break;  case 0x18: o = OP_amominu_w; break; case 0x1c: o = OP_amomaxu_w; break;
-        default: return;   // lr / sc stay escapes
+        case 0x02: case 0x03:   // lr / sc (decoder.isa:2069-2075, 2175-2181)
+            d.op = (uint8_t)(fbits(raw, 31, 27) == 0x02 ? (f3 == 2 ? OP_lr_w : OP_lr_d) : (f3 == 2 ? OP_sc_w : OP_sc_d));
+            D_RD(rd); D_RS1(rs1);
+            if (fbits(raw, 31, 27) == 0x03) D_RS2(rs2);
+            d.imm = 0;
+            return;
+        default: return;
         }
         d.op = (uint8_t)(f3 == 2 ? o : o + (OP_amoadd_d - OP_amoadd_w));
         D_RD(rd); D_RS1(rs1); D_RS2(rs2); d.imm = 0;
@@ -438,7 +445,8 @@ __device__ inline Dec rv_decode(uint32_t raw) {
 // K_SLOW and goes through the full per-op switch of the general path.
 enum Kind : uint8_t {
     K_SLOW = 0, K_ADD, K_SUB, K_AND, K_OR, K_XOR, K_SLT, K_SLTU, K_SLL, K_SRL, K_SRA, K_MUL,
-    K_LOAD, K_STORE, K_BEQ, K_BNE, K_BLT, K_BGE, K_BLTU, K_BGEU, K_JAL, K_JALR, K_NOP
+    K_LOAD, K_STORE, K_BEQ, K_BNE, K_BLT, K_BGE, K_BLTU, K_BGEU, K_JAL, K_JALR, K_NOP,
+    K_MULH, K_MULHU, K_MULHSU, K_DIV, K_DIVU, K_REM, K_REMU
 };
 constexpr uint16_t U_BIMM = 1u << 8, U_APC = 1u << 9, U_W32 = 1u << 10, U_SEXT = 1u << 11;
 
@@ -480,6 +488,17 @@ __host__ __device__ inline uint16_t uop_of(Dec &d) {
     case OP_c_subw: case OP_subw: return K_SUB | U_W32;
     case OP_c_addw: case OP_addw: return K_ADD | U_W32;
     case OP_c_mul: case OP_mul: return K_MUL;
+    case OP_mulh: return K_MULH;
+    case OP_mulhu: return K_MULHU;
+    case OP_mulhsu: return K_MULHSU;
+    case OP_div_: return K_DIV;
+    case OP_divu: return K_DIVU;
+    case OP_rem: return K_REM;
+    case OP_remu: return K_REMU;
+    case OP_divw: return K_DIV | U_W32;
+    case OP_divuw: return K_DIVU | U_W32;
+    case OP_remw: return K_REM | U_W32;
+    case OP_remuw: return K_REMU | U_W32;
     case OP_mulw: return K_MUL | U_W32;
     case OP_c_zext_b: d.imm = 0xFF; return K_AND | U_BIMM;
     case OP_c_zext_h: d.imm = 0xFFFF; return K_AND | U_BIMM;

@@ -305,7 +305,7 @@ def test_native_driver_matches_engine(engine_factory, tmp_path):
     assert hist["counts"].tobytes() == rh["counts"].tobytes()
 
 
-@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys"])
+@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc"])
 def test_known_answer_programs(oracle_mod, prog):
     """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
@@ -326,7 +326,8 @@ def test_known_answer_programs(oracle_mod, prog):
                      "mem": (kat.mem_program_elf, kat.mem_program_expected),
                      "cmp": (kat.cmp_program_elf, kat.cmp_program_expected),
                      "rvc": (kat.rvc_program_elf, kat.rvc_program_expected),
-                     "sys": (kat.sys_program_elf, kat.sys_program_expected)}[prog]
+                     "sys": (kat.sys_program_elf, kat.sys_program_expected),
+                     "lrsc": (kat.lrsc_program_elf, kat.lrsc_program_expected)}[prog]
     elf, expected = elf(), expected()
     e = Engine(private_pages=64)
     e.load_elf(elf, [prog])

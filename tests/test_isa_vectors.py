@@ -706,3 +706,134 @@ def test_sys_program_on_oracle(oracle_mod):
     assert g.stderr_len == len(SYS_STDERR)
     assert o.golden_stdout() == sys_program_expected()
     assert o.golden_stderr() == SYS_STDERR
+
+
+# ---------------------------------------------------------------- LR / SC
+# Known answers for LR/SC as gem5's atomic CPU with the reference's SE memory
+# (NoCache: the data port reaches AbstractMemory) gives them: the ISA
+# reservation (src/arch/riscv/isa.cc:1006-1064: set by each LR fragment,
+# cleared by every SC, SC fails when it is empty or in another 64-byte line),
+# and this context's lock record in memory (src/mem/abstract_mem.cc:258-345:
+# granule = paddr & ~0xf, replaced by each LR, erased by any store to its
+# granule -- the SC's own included -- kept by a failed SC; AMOs and proxy
+# writes leave it).  rd = 0 on success, 1 on failure (formats/amo.isa).
+LRSC_EXPECTED = [
+    0x1111,      # 1. lr.d A
+    0,           #    sc.d A succeeds (A = 0x2222)
+    1,           # 2. sc.d with no reservation fails
+    1,           # 3. lr.d A; sd to A's granule erases the lock; sc.d fails
+    0,           # 4. lr.d A; sd to another granule of the line; sc.d succeeds (A = 0x3333)
+    1,           # 5. lr.d A; sc.d to the next line fails (ISA) and clears the reservation
+    1,           #    sc.d A fails: reservation empty
+    1,           # 6. lr.d A; lr.d B (same line): record -> B; sc.d A passes the ISA, memory refuses
+    0,           #    lr.w B; sc.w B succeeds
+    (-5) & M64,  #    lw B: -5
+    0,           # 7. lr.d A; amoadd.d A leaves the record; sc.d.aqrl A succeeds
+    0x5555,      #    ld A
+    (-2**31) & M64,   # 8. lr.w sign-extends
+    0,           # 9. lr.d across a line (last fragment holds the reservation); sc.d there succeeds
+    0x6666,      #    ld at the second fragment
+]
+
+
+def lrsc_program_source() -> str:
+    return f"""    .text
+_start:
+    la    s0, buf
+    la    s2, out
+    li    t0, 0x1111
+    sd    t0, 0(s0)
+    sd    t0, 16(s0)
+    sd    t0, 64(s0)
+    lr.d  t1, (s0)
+    li    t2, 0x2222
+    sc.d  t3, t2, (s0)
+    sd    t1, 0(s2)
+    sd    t3, 8(s2)
+    li    t2, 0x3333
+    sc.d  t3, t2, (s0)
+    sd    t3, 16(s2)
+    lr.d  t1, (s0)
+    sd    zero, 8(s0)
+    sc.d  t3, t2, (s0)
+    sd    t3, 24(s2)
+    lr.d  t1, (s0)
+    sd    zero, 16(s0)
+    sc.d  t3, t2, (s0)
+    sd    t3, 32(s2)
+    lr.d  t1, (s0)
+    addi  t4, s0, 64
+    sc.d  t3, t2, (t4)
+    sd    t3, 40(s2)
+    sc.d  t3, t2, (s0)
+    sd    t3, 48(s2)
+    lr.d  t1, (s0)
+    addi  t4, s0, 16
+    lr.d  t1, (t4)
+    li    t2, 0x4444
+    sc.d  t3, t2, (s0)
+    sd    t3, 56(s2)
+    lr.w  t1, (t4)
+    li    t2, -5
+    sc.w  t3, t2, (t4)
+    sd    t3, 64(s2)
+    lw    t5, 0(t4)
+    sd    t5, 72(s2)
+    lr.d  t1, (s0)
+    li    t2, 1
+    amoadd.d t6, t2, (s0)
+    li    t2, 0x5555
+    sc.d.aqrl t3, t2, (s0)
+    sd    t3, 80(s2)
+    ld    t5, 0(s0)
+    sd    t5, 88(s2)
+    addi  t4, s0, 128
+    li    t2, 0x80000000
+    sw    t2, 0(t4)
+    lr.w.aq t5, (t4)
+    sd    t5, 96(s2)
+    addi  t4, s0, 188
+    lr.d  t1, (t4)
+    addi  t4, s0, 192
+    li    t2, 0x6666
+    sc.d.rl t3, t2, (t4)
+    sd    t3, 104(s2)
+    ld    t5, 0(t4)
+    sd    t5, 112(s2)
+    li    a0, 1
+    la    a1, out
+    li    a2, {8 * len(LRSC_EXPECTED)}
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 94
+    ecall
+    .bss
+    .balign 4096
+buf:
+    .zero 4096
+out:
+    .zero {8 * len(LRSC_EXPECTED)}
+"""
+
+
+def lrsc_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(lrsc_program_source())
+
+
+def lrsc_program_expected() -> bytes:
+    return b"".join((v & M64).to_bytes(8, "little") for v in LRSC_EXPECTED)
+
+
+def test_lrsc_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(lrsc_program_elf(), "lrsc")
+    g = o.run_golden()
+    assert g.exit_code == 0
+    assert o.golden_stdout() == lrsc_program_expected()
+
+
+def test_lrsc_decode(oracle_mod):
+    # lr.w / sc.d / lr.d.aqrl decode to the executed ops (no longer escapes)
+    for raw, name in ((0x1005272F, "lr_w"), (0x18B5362F, "sc_d"), (0x1605352F, "lr_d")):
+        assert oracle_mod.mnemonic(raw) == name, hex(raw)
