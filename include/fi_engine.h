@@ -74,6 +74,7 @@ typedef int32_t fi_status;
 #define FI_CRASH_STACK_LIMIT 9    /* fatal  max stack exceeded    sim/mem_state.cc:440 */
 #define FI_CRASH_AMO_LINE 10      /* panic  AMO across a cache line cpu/simple/atomic.cc:569-570 */
 #define FI_CRASH_SC_LINE 11       /* abort  SC across a cache line  cpu/simple/atomic.cc:482 assert(curr_frag_id == 0) */
+#define FI_CRASH_SE_PANIC 12      /* panic  in an SE syscall handler (null ProxyPtr, MemState::isUnmapped) */
 /* FI_ESCAPE sub-codes */
 #define FI_ESC_INST 1
 #define FI_ESC_SYSCALL 2

@@ -130,6 +130,14 @@ typedef struct {
      * lock record in memory (abstract_mem.cc:258-345), as virtual addresses
      * (the SE page mapping is a per-page bijection); OR_NONE = none */
     u64 resv, lock;
+    /* SE memory map (MemState, sim/mem_state.cc): the VMA list as disjoint
+     * [lo, hi) page ranges (only their union matters: names and file backing
+     * are not modelled), the break point and the mmap end; plus the fd table
+     * entries 0..2 closed (fdc bit fd) and set_tid_address's childClearTID */
+    struct { u64 lo, hi; } vma[64];
+    int nvma;
+    u64 brk, mmap_end, ctid;
+    u32 fdc;
     u64 protect_mask;
     /* termination */
     int done; or_outcome_t res;
@@ -636,7 +644,9 @@ static void alloc_page(mach_t *m, u64 vaddr) {
  * handled (panic), -1 fatal("Maximum stack size exceeded"). */
 static int fixup_fault(mach_t *m, u64 vaddr) {
     const or_campaign_t *c = m->c;
-    if (vaddr >= c->stack_vma_lo && vaddr < c->stack_vma_hi) { alloc_page(m, vaddr & PAGE_MASK); return 1; }
+    for (int i = 0; i < m->nvma; i++)
+        if (vaddr >= m->vma[i].lo && vaddr < m->vma[i].hi) { alloc_page(m, vaddr & PAGE_MASK); return 1; }
+    (void)c;
     if (vaddr >= m->stack_min && vaddr < STACK_BASE) { alloc_page(m, vaddr & PAGE_MASK); return 1; }
     if (vaddr < m->stack_min && vaddr >= STACK_BASE - MAX_STACK) {
         while (vaddr < m->stack_min) {
@@ -704,6 +714,99 @@ static void finish(mach_t *m, int cls, int sub, int exit_code) {
     m->res.ninst = m->num_inst;
 }
 
+/* ------------------------------------------------------------- memory map */
+static int vma_intersects(const mach_t *m, u64 lo, u64 hi) {
+    for (int i = 0; i < m->nvma; i++)
+        if (m->vma[i].lo < hi && lo < m->vma[i].hi) return 1;
+    return 0;
+}
+/* the page-table half of MemState::isUnmapped (mem_state.cc:84-106) */
+static int pt_intersects(const mach_t *m, u64 lo, u64 hi) {
+    for (u64 i = 0; i < m->mem.cap; i++) {
+        const u64 v = m->mem.tab[i].vpn;
+        if (v != UINT64_MAX && (v << 12) >= lo && (v << 12) < hi) return 1;
+    }
+    return 0;
+}
+/* MemState::isUnmapped: 1 unmapped, 0 a VMA intersects, -1 panic ("Someone
+ * allocated physical memory at VA %p without creating a VMA!") */
+static int is_unmapped(const mach_t *m, u64 s, u64 len) {
+    if (vma_intersects(m, s, s + len)) return 0;
+    if (pt_intersects(m, s, s + len)) return -1;
+    return 1;
+}
+/* MemState::mapRegion (mem_state.cc:172-189): 0 if the list is full (the
+ * engine's capacity, not gem5's: the trial escapes) */
+static int vma_add(mach_t *m, u64 lo, u64 hi) {
+    if (lo >= hi) return 1;
+    if (m->nvma == (int)(sizeof(m->vma) / sizeof(m->vma[0]))) return 0;
+    m->vma[m->nvma].lo = lo; m->vma[m->nvma].hi = hi; m->nvma++;
+    return 1;
+}
+/* MemState::unmapRegion (mem_state.cc:191-266): VMAs lose [lo, hi), then
+ * Process::deallocateMem (process.cc:348-382) unmaps the pages that are
+ * mapped (zeroed on deallocation: zeroPages=True, Process.py:55-58). */
+static int vma_unmap(mach_t *m, u64 lo, u64 hi) {
+    int n = m->nvma;
+    for (int i = 0; i < n; i++) {
+        u64 a = m->vma[i].lo, b = m->vma[i].hi;
+        if (!(a < hi && lo < b)) continue;
+        if (a < lo && b > hi) {            /* strict superset: split */
+            m->vma[i].hi = lo;
+            if (!vma_add(m, hi, b)) return 0;
+        } else if (a >= lo && b <= hi) {   /* subset: gone */
+            m->vma[i].lo = m->vma[i].hi = 0;
+        } else if (a < lo) {
+            m->vma[i].hi = lo;
+        } else {
+            m->vma[i].lo = hi;
+        }
+    }
+    int k = 0;
+    for (int i = 0; i < m->nvma; i++)
+        if (m->vma[i].lo < m->vma[i].hi) m->vma[k++] = m->vma[i];
+    m->nvma = k;
+    pmap_t n2;
+    pm_init(&n2, m->mem.cap);
+    for (u64 i = 0; i < m->mem.cap; i++) {
+        pte_t *e = &m->mem.tab[i];
+        if (e->vpn == UINT64_MAX) continue;
+        if ((e->vpn << 12) >= lo && (e->vpn << 12) < hi) { if (e->owned) free(e->data); continue; }
+        pm_insert(&n2, e->vpn, e->data, e->owned);
+    }
+    free(m->mem.tab);
+    m->mem = n2;
+    return 1;
+}
+/* Are all bytes [a, a + n) mapped (a read through SETranslatingPortProxy:
+ * no fixups on reads, mem/se_translating_port_proxy.cc:50-70)? */
+static int proxy_readable(mach_t *m, u64 a, u64 n) {
+    if (!n) return 1;
+    if (a + n - 1 < a) return 0;
+    for (u64 v = a >> 12; v <= ((a + n - 1) >> 12); v++)
+        if (!pm_find(&m->mem, v)) return 0;
+    return 1;
+}
+/* A write through the proxy (NextPage: fixupFault for each missing page);
+ * 0 = fatal, -1 = "Maximum stack size exceeded". */
+static int fixup_fault(mach_t *m, u64 vaddr);
+static int proxy_writable(mach_t *m, u64 a, u64 n) {
+    if (!n) return 1;
+    if (a + n - 1 < a) return 0;
+    for (u64 v = a >> 12; v <= ((a + n - 1) >> 12); v++) {
+        if (pm_find(&m->mem, v)) continue;
+        const int h = fixup_fault(m, v << 12 > a ? v << 12 : a);
+        if (h != 1) return h;
+    }
+    return 1;
+}
+static void proxy_write(mach_t *m, u64 a, const uint8_t *src, u64 n) {
+    for (u64 i = 0; i < n; i++) {
+        uint8_t *pg = translate_w(m, a + i);
+        pg[(a + i) & (PAGE - 1)] = src[i];
+    }
+}
+
 /* ------------------------------------------------------------- syscalls */
 /* Classification of the RV64 Linux syscall table (arch/riscv/linux/
  * se_workload.cc:529-895; pinned by tests/golden/syscalls_rv64.json):
@@ -718,8 +821,18 @@ static const uint16_t sys_impl_escape[] = {
     201, 202, 203, 204, 205, 206, 207, 208, 209, 210, 211, 212, 214, 215, 216, 220, 221, 222, 258, 260, 261,
     278, 435, 1024, 1025, 1026, 1027, 1028, 1029, 1030, 1031, 1033, 1034, 1035, 1036, 1037, 1038, 1039, 1040,
     1041, 1044, 1047, 1048, 1049, 1050, 1051, 1052, 1054, 1055, 1056, 1057, 1058, 1060, 1062, 1065, 1067, 1068};
+/* modelled: the deterministic handlers (syscall_emul.{cc,hh}, se_workload.cc) */
+static int sys_modelled(int num) {
+    switch (num) {
+    case 29: case 57: case 64: case 66: case 93: case 94: case 96: case 160: case 163: case 214: case 215:
+    case 222: case 261: case 1058:
+        return 1;
+    default:
+        return num >= 172 && num <= 178;
+    }
+}
 int or_sys_class(int num) {
-    if (num == 64 || num == 93 || num == 94 || (num >= 172 && num <= 178)) return 4;
+    if (sys_modelled(num)) return 4;
     int present = (num >= 0 && num <= 64) || (num >= 66 && num <= 243) || num == 258 ||
                   (num >= 260 && num <= 287) || (num >= 424 && num <= 450) || (num >= 1024 && num <= 1079) ||
                   num == 2011;
@@ -730,6 +843,105 @@ int or_sys_class(int num) {
     for (size_t i = 0; i < sizeof(sys_impl_escape) / sizeof(sys_impl_escape[0]); i++)
         if (sys_impl_escape[i] == num) return 3;
     return 1;
+}
+
+#define EBADF_ 9
+#define EINVAL_ 22
+#define ENOTTY_ 25
+#define EPERM_ 1
+static u64 round_up(u64 v) { return (v + PAGE - 1) & ~(PAGE - 1); }   /* base/intmath.hh roundUp (wraps) */
+/* Ranges the VM handlers walk page by page (MemState::isUnmapped, Process::
+ * deallocateMem, whose page count is an int) are bounded here: a longer one
+ * is a host-side hazard the engine does not model (escape). */
+#define VM_MAX_LEN (1ULL << 43)
+static void vm_escape(mach_t *m, int num) { finish(m, OR_ESCAPE, OR_ESC_SYSCALL, 0); m->res.detail = (u32)num; }
+/* an SE handler panics (e.g. "Accessing null ProxyPtr", MemState::isUnmapped) */
+static void se_panic(mach_t *m) { finish(m, OR_CRASH, OR_CRASH_SE_PANIC, 134); }
+
+/* writevFunc<RiscvLinux64> (syscall_emul.hh:1964-1996): the iovecs and their
+ * buffers are read through the proxy in order (fatal on an unmapped byte),
+ * then host writev() on the target fd */
+static void sys_writev(mach_t *m) {
+    const int fd = (int)(s32)(u32)m->x[10];
+    const u64 iov = m->x[11], cnt = m->x[12];
+    if (fd < 0 || fd >= 1024) { finish(m, OR_CRASH, OR_CRASH_FD_ASSERT, 134); return; }   /* fd_array.cc:322 */
+    if (fd > 2 || ((m->fdc >> fd) & 1)) { m->x[10] = (u64)(s64)-EBADF_; return; }
+    if (fd == 0) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }             /* host stdin */
+    if (cnt > (1u << 20)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }    /* host allocation */
+    u64 total = 0;
+    for (u64 i = 0; i < cnt; i++) {
+        const u64 e = iov + 16 * i;
+        if (e < iov || !proxy_readable(m, e, 16)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        u64 base = 0, len = 0;
+        for (int k = 0; k < 8; k++) {
+            base |= (u64)translate(m, e + k)[(e + k) & (PAGE - 1)] << (8 * k);
+            len |= (u64)translate(m, e + 8 + k)[(e + 8 + k) & (PAGE - 1)] << (8 * k);
+        }
+        if (len > (1ULL << 31)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }
+        if (!proxy_readable(m, base, len)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        total += len;
+    }
+    if (cnt > 1024) { m->x[10] = (u64)(s64)-EINVAL_; return; }   /* host writev: IOV_MAX */
+    if (total > (1ULL << 31)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }
+    bytes_t *dst = fd == 1 ? &m->out : &m->err;
+    for (u64 i = 0; i < cnt; i++) {
+        const u64 e = iov + 16 * i;
+        u64 base = 0, len = 0;
+        for (int k = 0; k < 8; k++) {
+            base |= (u64)translate(m, e + k)[(e + k) & (PAGE - 1)] << (8 * k);
+            len |= (u64)translate(m, e + 8 + k)[(e + 8 + k) & (PAGE - 1)] << (8 * k);
+        }
+        for (u64 j = 0; j < len; j++) {
+            const uint8_t ch = translate(m, base + j)[(base + j) & (PAGE - 1)];
+            by_push(dst, &ch, 1);
+        }
+    }
+    m->x[10] = total;
+}
+
+/* mmapFunc<RiscvLinux64> (syscall_emul.hh:2002-2126) for anonymous mappings,
+ * MemState::extendMmap (mem_state.cc:450-477: the region grows down from
+ * mmap_end, RiscvProcess64 mmap_end = 0x4000000000000000, process.cc:79). */
+static void sys_mmap(mach_t *m) {
+    u64 start = m->x[10], len = m->x[11];
+    const int flags = (int)(s32)(u32)m->x[13], fd = (int)(s32)(u32)m->x[14];
+    const u64 off = m->x[15];
+    if ((start & (PAGE - 1)) || (off & (PAGE - 1)) || ((flags & 2) && (flags & 1)) || (!(flags & 2) && !(flags & 1)) ||
+        !len) { m->x[10] = (u64)(s64)-EINVAL_; return; }
+    if (len > VM_MAX_LEN) { vm_escape(m, 222); return; }
+    len = round_up(len);
+    if (!(flags & 0x20)) {   /* file-backed: the fd table entry */
+        if (fd < 0 || fd >= 1024) { finish(m, OR_CRASH, OR_CRASH_FD_ASSERT, 134); return; }
+        if (fd > 2 || ((m->fdc >> fd) & 1)) { m->x[10] = (u64)(s64)-EBADF_; return; }
+        finish(m, OR_ESCAPE, OR_ESC_HOST, 0);   /* a host file mapping */
+        return;
+    }
+    if (start + len < start) { vm_escape(m, 222); return; }
+    if (!(flags & 0x10)) {
+        int u = 0;
+        if (start) {
+            u = is_unmapped(m, start, len);
+            if (u < 0) { se_panic(m); return; }
+        }
+        if (!u) {
+            u64 s2 = m->mmap_end - len;
+            for (;;) {
+                if (s2 > m->mmap_end) { vm_escape(m, 222); return; }   /* wrapped below 0 */
+                int hit = -1;
+                for (int i = 0; i < m->nvma; i++)
+                    if (m->vma[i].lo < s2 + len && s2 < m->vma[i].hi) { hit = i; break; }
+                if (hit < 0) break;
+                s2 = m->vma[hit].lo - len;   /* the page-by-page scan lands right below it */
+            }
+            if (pt_intersects(m, s2, s2 + len)) { se_panic(m); return; }
+            m->mmap_end = s2;
+            start = s2;
+        }
+    } else if (!vma_unmap(m, start, start + len)) {
+        finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return;
+    }
+    if (!vma_add(m, start, start + len)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return; }
+    m->x[10] = start;
 }
 
 static void do_syscall(mach_t *m) {
@@ -743,6 +955,11 @@ static void do_syscall(mach_t *m) {
     switch (num) {
     case 93: case 94: {   /* exitImpl -> exitSimLoop(status & 0xff) (syscall_emul.cc:120-248) */
         int status = (int)(s32)(u32)m->x[10];
+        if (m->ctid) {   /* exitFutexWake: clear *childClearTID through the proxy (syscall_emul.cc:106-117) */
+            const int h = proxy_writable(m, m->ctid, 8);
+            if (h == 0) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+            if (h < 0) { finish(m, OR_CRASH, OR_CRASH_STACK_LIMIT, 1); return; }
+        }
         int code = status & 0xff;
         const or_campaign_t *c = m->c;
         int same = c->have_golden && code == (int)c->golden.exit_code &&
@@ -757,12 +974,89 @@ static void do_syscall(mach_t *m) {
     case 174: case 175: m->x[10] = UID; return;
     case 176: case 177: m->x[10] = GID; return;
     case 178: m->x[10] = PID; return;     /* gettid -> pid */
+    case 96: m->ctid = m->x[10]; m->x[10] = PID; return;   /* setTidAddressFunc (syscall_emul.cc:292-299) */
+    case 57: {   /* closeFunc -> FDArray::closeFDEntry (fd_array.cc:334-352): 0 for any fd in range */
+        const int fd = (int)(s32)(u32)m->x[10];
+        if (fd < 0 || fd >= 1024) { m->x[10] = (u64)(s64)-EBADF_; return; }
+        if (fd <= 2) m->fdc |= 1u << fd;
+        m->x[10] = 0;
+        return;
+    }
+    case 29: {   /* ioctlFunc (syscall_emul.hh:743-813): tty requests first, then the fd entry */
+        const int fd = (int)(s32)(u32)m->x[10];
+        const u32 req = (u32)m->x[11];
+        if (req == 0x5401 || req == 0x5405 || req == 0x5407 || req == 0x541B) { m->x[10] = (u64)(s64)-ENOTTY_; return; }
+        if (fd < 0 || fd >= 1024) { finish(m, OR_CRASH, OR_CRASH_FD_ASSERT, 134); return; }
+        m->x[10] = (u64)(s64)-ENOTTY_;   /* not a device or socket entry */
+        return;
+    }
+    case 66: sys_writev(m); return;
+    case 222: case 1058: sys_mmap(m); return;
+    case 215: {   /* munmapFunc (syscall_emul.hh:3140-3156) */
+        const u64 st = m->x[10];
+        u64 len = m->x[11];
+        if (st & (PAGE - 1)) { m->x[10] = (u64)(s64)-EINVAL_; return; }
+        if (len > VM_MAX_LEN) { vm_escape(m, 215); return; }
+        len = round_up(len);
+        if (st + len < st) { vm_escape(m, 215); return; }
+        if (!vma_unmap(m, st, st + len)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return; }
+        m->x[10] = 0;
+        return;
+    }
+    case 214: {   /* brkFunc (syscall_emul.cc:268-289), MemState::updateBrkRegion (mem_state.cc:107-170) */
+        const u64 nb = m->x[10], ob = m->brk;
+        if (nb == 0 || nb == ob) { m->x[10] = ob; return; }
+        const u64 na = round_up(nb), oa = round_up(ob);
+        if ((na > oa ? na - oa : oa - na) > VM_MAX_LEN) { vm_escape(m, 214); return; }
+        if (nb < ob) {
+            if (oa - na > 0 && !vma_unmap(m, na, oa)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return; }
+            m->brk = nb;
+            m->x[10] = nb;
+            return;
+        }
+        if (na > oa) {
+            const int u = is_unmapped(m, oa, na - oa);
+            if (u < 0) { se_panic(m); return; }
+            if (!u) { m->x[10] = ob; return; }   /* existing mappings impede the heap */
+            if (!vma_add(m, oa, na)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return; }
+        }
+        m->brk = nb;
+        m->x[10] = nb;
+        return;
+    }
+    case 163: case 261: {   /* getrlimitFunc / prlimitFunc (syscall_emul.hh:2197-2265) */
+        const u64 rlp = num == 163 ? m->x[11] : m->x[13];
+        if (rlp && !proxy_readable(m, rlp, 16)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }   /* VPtr load */
+        if (num == 261 && (int)(s32)(u32)m->x[10] != 0) { m->x[10] = (u64)(s64)-EPERM_; return; }
+        if (num == 261 && !rlp) { m->x[10] = 0; return; }
+        const s64 res = num == 163 ? (s64)(u32)m->x[10] : (s64)(s32)(u32)m->x[11];
+        u64 lim;
+        if (res == 3) lim = 8ULL << 20;                     /* RLIMIT_STACK */
+        else if (res == 2) lim = 256ULL << 20;              /* RLIMIT_DATA */
+        else if (res == 6 && num == 163) lim = 1;           /* RLIMIT_NPROC: system thread contexts (1) */
+        else { m->x[10] = (u64)(s64)-EINVAL_; return; }
+        if (!rlp) { se_panic(m); return; }                  /* null ProxyPtr */
+        uint8_t b[16];
+        for (int k = 0; k < 8; k++) b[k] = b[8 + k] = (uint8_t)(lim >> (8 * k));
+        proxy_write(m, rlp, b, 16);
+        m->x[10] = 0;
+        return;
+    }
+    case 160: {   /* unameFunc64 (arch/riscv/linux/se_workload.cc:109-122), Linux::utsname = 5 x 65 chars */
+        const u64 p = m->x[10];
+        if (!p) { se_panic(m); return; }
+        if (!proxy_readable(m, p, 325)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        static const char *f[5] = {"Linux", "sim.gem5.org", "5.1.0", "#1 Mon Aug 18 11:32:15 EDT 2003", "riscv64"};
+        for (int k = 0; k < 5; k++) proxy_write(m, p + 65 * k, (const uint8_t *)f[k], strlen(f[k]) + 1);
+        m->x[10] = 0;
+        return;
+    }
     case 64: {  /* writeFunc<RiscvLinux64>(int fd, VPtr buf, size_t n) syscall_emul.hh:2826-2860 */
         int fd = (int)(s32)(u32)m->x[10];
         u64 buf = m->x[11], n = m->x[12];
         if (fd < 0 || fd >= 1024) { finish(m, OR_CRASH, OR_CRASH_FD_ASSERT, 134); return; }  /* fd_array.cc:322 */
+        if (fd > 2 || ((m->fdc >> fd) & 1)) { m->x[10] = (u64)(s64)-9; return; }   /* no entry: -EBADF */
         if (fd == 0) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* host stdin poll/write */
-        if (fd > 2) { m->x[10] = (u64)(s64)-9; return; }                  /* -EBADF */
         if (n > (1ULL << 31)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; } /* host allocation */
         /* BufferArg::copyIn -> readBlob: fatal if any byte is unmapped (no fixup on reads) */
         if (n) {
@@ -1449,6 +1743,9 @@ static void mach_init(mach_t *m, const or_campaign_t *c) {
     m->stack_min = c->stack_min0;
     m->watch = -1;
     m->resv = m->lock = OR_NONE;
+    m->vma[0].lo = c->stack_vma_lo; m->vma[0].hi = c->stack_vma_hi; m->nvma = 1;   /* argsInit's "stack" VMA */
+    m->brk = c->brk0;
+    m->mmap_end = 0x4000000000000000ULL;
 }
 static void mach_free(mach_t *m) { pm_free(&m->mem); free(m->out.buf); free(m->err.buf); }
 

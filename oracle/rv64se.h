@@ -38,7 +38,8 @@ enum {
     OR_CRASH_SIGTRAP = 8,       /* ebreak -> kill(SIGTRAP)        faults.cc:317-322, debug.cc:64-70 */
     OR_CRASH_STACK_LIMIT = 9,   /* fatal: Maximum stack size      mem_state.cc:440 */
     OR_CRASH_AMO_LINE = 10,     /* panic: AMO across a cache line atomic.cc:569-570 */
-    OR_CRASH_SC_LINE = 11       /* abort: SC across a cache line  atomic.cc:482 assert(curr_frag_id == 0) */
+    OR_CRASH_SC_LINE = 11,      /* abort: SC across a cache line  atomic.cc:482 assert(curr_frag_id == 0) */
+    OR_CRASH_SE_PANIC = 12      /* panic in an SE handler (null ProxyPtr, MemState::isUnmapped) */
 };
 enum {
     OR_ESC_INST = 1,            /* instruction gem5 decodes but the engine does not model */

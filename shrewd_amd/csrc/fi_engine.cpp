@@ -120,6 +120,8 @@ struct fi_engine {
     bool golden_fp = false;          // the golden run wrote FP state: no snapshot start / early exit
     uint8_t *d_priv = nullptr;
     uint64_t *d_priv_vpn = nullptr;
+    VmState *d_vm = nullptr;         // [cap] per-slot SE memory map (trials that made a VM syscall)
+    uint64_t brk0 = 0;               // roundUp(maxAddr, page): the process-start brk point
     // epochs: suspended lanes, survivor lists, counts, sort buffers
     LaneSave *d_save = nullptr;
     uint32_t *d_surv[2] = {nullptr, nullptr};
@@ -212,7 +214,7 @@ static void free_work(fi_engine *e) {
     dfree(e->d_sites); dfree(e->d_keys); dfree(e->d_keys2); dfree(e->d_perm); dfree(e->d_perm2);
     dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg); dfree(e->d_fregs);
     dfree(e->d_save); dfree(e->d_surv[0]); dfree(e->d_surv[1]); dfree(e->d_cnt);
-    dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_wrange); dfree(e->d_nwaves); dfree(e->d_priv); dfree(e->d_priv_vpn);
+    dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_wrange); dfree(e->d_nwaves); dfree(e->d_priv); dfree(e->d_priv_vpn); dfree(e->d_vm);
     e->cap = 0;
 }
 static void free_snaps(fi_engine *e) { dfree(e->d_snaps); dfree(e->d_tab); dfree(e->d_pool); }
@@ -399,7 +401,7 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
     std::sort(wpages.begin(), wpages.end());
     wpages.erase(std::unique(wpages.begin(), wpages.end()), wpages.end());
     e->mem_pages = wpages;
-    (void)max_addr;   // brk = roundUp(maxAddr) is not needed: brk() is an escape
+    e->brk0 = (max_addr + kPage - 1) & ~(kPage - 1);   // Process brk point (process.cc: roundUp(maxAddr))
 
     // ---- snapshot 0: the process-start image (frames sorted by vpn) and the
     // initial architectural state (RiscvProcess::argsInit leaves every
@@ -468,6 +470,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_priv, c * e->cfg.private_pages * kPage));
     HIPCHK(hipMalloc(&e->d_priv_vpn, c * e->cfg.private_pages * 8));
     HIPCHK(hipMalloc(&e->d_save, c * sizeof(LaneSave)));
+    HIPCHK(hipMalloc(&e->d_vm, c * sizeof(VmState)));
     HIPCHK(hipMalloc(&e->d_fregs, c * 32 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&e->d_surv[0], c * 4));
     HIPCHK(hipMalloc(&e->d_surv[1], c * 4));
@@ -506,6 +509,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.fregs = e->d_fregs;
     c.wave_dbg = e->d_wave_dbg;
     c.stats = e->d_stats;
+    c.brk0 = e->brk0; c.svma_lo = e->svma_lo; c.svma_hi = e->svma_hi; c.vm = e->d_vm;
     c.lanes = e->cfg.lanes_per_wave;
     return c;
 }

@@ -61,10 +61,23 @@ struct LaneSave {
     uint64_t pc, ninst, ncyc, out_pos, err_pos, stack_min, next_chk;
     int32_t watch;
     uint32_t nfail, n_priv, snap_j;
-    uint32_t flags;                  // bit 0 out_bad, bits 1-2 injected, bit 3 code_dirty, bit 4 FP state
+    uint32_t flags;                  // bit 0 out_bad, bits 1-2 injected, bit 3 code_dirty, bit 4 FP state,
+                                     // bit 5 VM state (VmState of the slot is live)
     uint32_t dlo, dhi;               // rewritten code bytes [code_lo + dlo, code_lo + dhi) (if code_dirty)
     uint32_t pad;
     uint64_t resv, lock;             // LR/SC: load reservation and lock record (~0 = none)
+};
+
+// A trial's SE memory-map state once it made a VM syscall (brk, mmap, munmap,
+// close, set_tid_address): gem5's MemState VMA list, brk point and mmap end
+// (src/sim/mem_state.hh), the fd entries 0-2 it closed and childClearTID.
+// Until then the state is the process-start one (DevCtx brk0 / svma_*).
+constexpr uint32_t kMaxVma = 64;    // == oracle/rv64se.c mach_t.vma (overflow: resource escape)
+constexpr uint64_t kTomb = 1ULL << 63;   // priv_vpn entry: the page is unmapped for this trial
+struct VmState {
+    uint64_t brk, mmap_end, ctid;
+    uint32_t nvma, fdc;
+    uint64_t vma[kMaxVma][2];
 };
 
 // Everything one launch of the trial kernel needs.  Passed by value as the
@@ -133,13 +146,17 @@ struct DevCtx {
     fi_outcome *out;
     uint64_t n;                      // trials in this launch
     uint64_t *wave_dbg;              // per wave: {s_memtime cycles, loop iterations, translated insts, slow fetches}
+    // SE memory map: process-start brk and "stack" VMA; per-slot VM state
+    uint64_t brk0, svma_lo, svma_hi;
+    VmState *vm;                     // [n_slots]
     unsigned long long *stats;       // [0] fetch B [1] data B [2] pages [3..5] golden ncycles/out/err
                                      // [6] loop iterations [7] lane-insts [8] slow fetches [9] min-PC [10] max iter/wave
                                      // [11] early-exit checks [12] early exits [13] snapshots captured [14] start-inst sum
                                      // [15] golden trace events [16] translated insts [17] translated entries
                                      // [18] slowest wave: iters<<32 | tx permille<<20 | entries [19] iters<<32 | slow
                                      // [20] wave-0 s_memtime delta [21] s_memrealtime delta
-                                     // [22] golden run wrote FP state [23] instructions executed on the device
+                                     // [22] golden run holds state outside the snapshots (FP, LR/SC, VM)
+                                     // [23] instructions executed on the device
 };
 
 struct SampleCtx {

@@ -138,6 +138,7 @@ struct LaneMem {
     // (the SE mapping is a per-page bijection); kNone = none.  A lane holding a
     // lock record stays on the general path, whose stores erase it.
     uint64_t resv, lock;
+    bool vm;                       // VmState of the slot is live (the trial made a VM syscall)
 };
 
 // The golden pre-decode of the instruction at pc is stale for this lane only if
@@ -205,13 +206,17 @@ __device__ __forceinline__ int64_t tab_find(const PageEnt *t, uint32_t n, uint64
 // over the lane's page set: its private pages, then the start snapshot's
 // pages, then the stack pages [stack_min, top] that MemState::fixupFault
 // (src/sim/mem_state.cc:387-447) has mapped and nobody has written (zero).
+// The newest private entry of a vpn decides it; a tombstone entry (vpn |
+// kTomb, left by munmap / brk shrink) means unmapped.
 // Returns the page address | 1 for a private (writable) page, 0 if unmapped.
 __device__ uint64_t lookup_full(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t vpn) {
     uint64_t p = 0;
-    for (uint32_t i = 0; i < m.n_priv; i++) {
-        if (c->priv_vpn[(uint64_t)i * c->n_slots + slot] == vpn) { p = (uint64_t)priv_frame(c, slot, i) | 1; break; }
+    bool dec = false;
+    for (uint32_t i = m.n_priv; i-- > 0;) {
+        const uint64_t e = c->priv_vpn[(uint64_t)i * c->n_slots + slot];
+        if ((e & ~kTomb) == vpn) { dec = true; if (!(e & kTomb)) p = (uint64_t)priv_frame(c, slot, i) | 1; break; }
     }
-    if (!p) {
+    if (!dec) {
         const int64_t f = tab_find(w.tab, w.tab_n, vpn);
         if (f >= 0) p = (uint64_t)(c->pool + ((uint64_t)f << 12));
         else if (vpn >= (m.stack_min >> 12) && vpn <= kStackTopVpn) p = (uint64_t)c->zero_page;
@@ -225,6 +230,181 @@ __device__ __forceinline__ uint64_t lookup(KCtx *c, const WaveMem &w, LaneMem &m
     return p ? p : lookup_full(c, w, m, slot, vpn);
 }
 __device__ __forceinline__ const uint8_t *page_of(uint64_t p) { return (const uint8_t *)(p & ~1ULL); }
+
+// ------------------------------------------------------------------ SE memory map
+// (syscall and fault paths only: one lane at a time, serial)
+// The private entry that decides vpn (newest first), or -1.
+__device__ int priv_decider(KCtx *c, const LaneMem &m, uint64_t slot, uint64_t vpn) {
+    for (uint32_t i = m.n_priv; i-- > 0;)
+        if ((c->priv_vpn[(uint64_t)i * c->n_slots + slot] & ~kTomb) == vpn) return (int)i;
+    return -1;
+}
+// Process::allocateMem of one page for this trial: a new private entry filled
+// from src (the zero page, or the current page for a proxy write).  nullptr if
+// the trial has no free private page (resource escape).
+__device__ uint8_t *priv_new(KCtx *c, LaneMem &m, uint64_t slot, uint64_t vpn, const uint8_t *src) {
+    if (m.n_priv >= c->priv_pages) return nullptr;
+    uint4 *d = (uint4 *)priv_frame(c, slot, m.n_priv);
+    const uint4 *q = (const uint4 *)src;
+    for (int k = 0; k < 256; k++) d[k] = q[k];
+    c->priv_vpn[(uint64_t)m.n_priv * c->n_slots + slot] = vpn;
+    m.n_priv++;
+    tlb_flush(m);
+    return (uint8_t *)d;
+}
+// The trial's VM state, materialised from the process-start one on first use.
+__device__ VmState *vm_of(KCtx *c, LaneMem &m, uint64_t slot) {
+    VmState *v = c->vm + slot;
+    if (!m.vm) {
+        v->brk = c->brk0; v->mmap_end = 0x4000000000000000ULL; v->ctid = 0;   // RiscvProcess64 (process.cc:79)
+        v->nvma = 1; v->fdc = 0;
+        v->vma[0][0] = c->svma_lo; v->vma[0][1] = c->svma_hi;                 // argsInit's "stack" VMA
+        m.vm = true;
+        if (c->record) c->stats[22] = 1;   // the golden VM state is not in the snapshots
+    }
+    return v;
+}
+__device__ bool in_vma(KCtx *c, const LaneMem &m, uint64_t slot, uint64_t a) {
+    if (!m.vm) return a >= c->svma_lo && a < c->svma_hi;
+    const VmState *v = c->vm + slot;
+    for (uint32_t i = 0; i < v->nvma; i++)
+        if (a >= v->vma[i][0] && a < v->vma[i][1]) return true;
+    return false;
+}
+// MemState::fixupFault (mem_state.cc:387-447): 1 handled, 0 not (panic),
+// -1 fatal "Maximum stack size exceeded", -2 no free private page.
+__device__ int fixup_fault(KCtx *c, LaneMem &m, uint64_t slot, uint64_t fva) {
+    if (in_vma(c, m, slot, fva) || (fva >= m.stack_min && fva < kStackBase))
+        return priv_new(c, m, slot, fva >> 12, c->zero_page) ? 1 : -2;
+    if (fva < m.stack_min && fva >= kStackBase - kMaxStack) {
+        const uint64_t nm = fva & ~4095ULL;
+        if (kStackBase - nm > kMaxStack) return -1;
+        m.stack_min = nm;   // [nm, old stack_min) are zero pages of the trial's set
+        return 1;
+    }
+    return 0;
+}
+// Calls f(vpn, decider) for every page of the trial's set in vpns [lo, hi)
+// until f returns false.
+template <typename F>
+__device__ __forceinline__ void for_mapped(KCtx *c, const WaveMem &w, const LaneMem &m, uint64_t slot, uint64_t lo,
+                                           uint64_t hi, F f) {
+    for (uint32_t i = m.n_priv; i-- > 0;) {
+        const uint64_t e = c->priv_vpn[(uint64_t)i * c->n_slots + slot];
+        if ((e & kTomb) || e < lo || e >= hi || priv_decider(c, m, slot, e) != (int)i) continue;
+        if (!f(e, (int)i)) return;
+    }
+    uint32_t a = 0, b = w.tab_n;
+    while (a < b) {
+        const uint32_t mid = (a + b) >> 1;
+        if (w.tab[mid].vpn < lo) a = mid + 1; else b = mid;
+    }
+    for (; a < w.tab_n && w.tab[a].vpn < hi; a++)
+        if (priv_decider(c, m, slot, w.tab[a].vpn) < 0 && !f(w.tab[a].vpn, -1)) return;
+    for (uint64_t v = lo > (m.stack_min >> 12) ? lo : (m.stack_min >> 12); v < hi && v <= kStackTopVpn; v++)
+        if (tab_find(w.tab, w.tab_n, v) < 0 && priv_decider(c, m, slot, v) < 0 && !f(v, -1)) return;
+}
+// MemState::isUnmapped (mem_state.cc:82-104): 1 unmapped, 0 a VMA intersects,
+// -1 panic (a page is mapped without a VMA)
+__device__ int vm_is_unmapped(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t lo, uint64_t len) {
+    const VmState *v = c->vm + slot;
+    const uint64_t hi = lo + len;
+    for (uint32_t i = 0; i < v->nvma; i++)
+        if (v->vma[i][0] < hi && lo < v->vma[i][1]) return 0;
+    bool any = false;
+    for_mapped(c, w, m, slot, lo >> 12, (hi + 4095) >> 12, [&](uint64_t, int) { any = true; return false; });
+    return any ? -1 : 1;
+}
+// MemState::mapRegion (mem_state.cc:172-189); false = the list is full
+__device__ bool vm_add(VmState *v, uint64_t lo, uint64_t hi) {
+    if (lo >= hi) return true;
+    if (v->nvma == kMaxVma) return false;
+    v->vma[v->nvma][0] = lo; v->vma[v->nvma][1] = hi; v->nvma++;
+    return true;
+}
+// MemState::unmapRegion (mem_state.cc:191-276) + Process::deallocateMem
+// (process.cc:348-382): the VMAs lose [lo, hi), the mapped pages in it leave
+// the trial's set (a private entry turns into a tombstone, a snapshot or zero
+// stack page gets one).  0 ok, 1 no room (resource escape).
+__device__ int vm_unmap(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, VmState *v, uint64_t lo, uint64_t hi) {
+    const uint32_t n = v->nvma;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint64_t a = v->vma[i][0], b = v->vma[i][1];
+        if (!(a < hi && lo < b)) continue;
+        if (a < lo && b > hi) {
+            v->vma[i][1] = lo;
+            if (!vm_add(v, hi, b)) return 1;
+        } else if (a >= lo && b <= hi) {
+            v->vma[i][0] = v->vma[i][1] = 0;
+        } else if (a < lo) {
+            v->vma[i][1] = lo;
+        } else {
+            v->vma[i][0] = hi;
+        }
+    }
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < v->nvma; i++)
+        if (v->vma[i][0] < v->vma[i][1]) { v->vma[k][0] = v->vma[i][0]; v->vma[k][1] = v->vma[i][1]; k++; }
+    v->nvma = k;
+    bool full = false;
+    for_mapped(c, w, m, slot, lo >> 12, hi >> 12, [&](uint64_t vpn, int d) {
+        if (d >= 0) {
+            c->priv_vpn[(uint64_t)d * c->n_slots + slot] = vpn | kTomb;
+        } else if (m.n_priv < c->priv_pages) {
+            c->priv_vpn[(uint64_t)m.n_priv * c->n_slots + slot] = vpn | kTomb;
+            m.n_priv++;
+        } else {
+            full = true;
+            return false;
+        }
+        return true;
+    });
+    tlb_flush(m);
+    if (lo < c->code_hi && hi > c->code_lo) mark_dirty(m, lo, hi);   // the pre-decoded text no longer applies
+    return full ? 1 : 0;
+}
+// Readable through SETranslatingPortProxy (no fixups on reads)
+__device__ bool proxy_readable(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t a, uint64_t n) {
+    if (!n) return true;
+    const uint64_t last = a + n - 1;
+    if (last < a) return false;
+    for (uint64_t v = a >> 12; v <= (last >> 12); v++)
+        if (!lookup(c, w, m, slot, v)) return false;
+    return true;
+}
+__device__ uint8_t proxy_byte(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t a) {
+    return page_of(lookup(c, w, m, slot, a >> 12))[a & 4095];
+}
+// A write through the proxy (NextPage: fixupFault for each missing page):
+// 1 ok, 0 fatal, -1 stack limit, -2 no free private page
+__device__ int proxy_writable(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t a, uint64_t n) {
+    if (!n) return 1;
+    const uint64_t last = a + n - 1;
+    if (last < a) return 0;
+    for (uint64_t v = a >> 12; v <= (last >> 12); v++) {
+        if (lookup(c, w, m, slot, v)) continue;
+        const int h = fixup_fault(c, m, slot, (v << 12) > a ? (v << 12) : a);
+        if (h != 1) return h;
+    }
+    return 1;
+}
+// Store bytes through the proxy (every page mapped): copy-on-write as needed.
+// false = no free private page.
+__device__ bool proxy_write(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t a, const char *src,
+                            uint64_t n) {
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t x = a + i;
+        uint64_t p = lookup(c, w, m, slot, x >> 12);
+        if (!(p & 1)) {
+            uint8_t *q = priv_new(c, m, slot, x >> 12, page_of(p));
+            if (!q) return false;
+            p = (uint64_t)q | 1;
+        }
+        const_cast<uint8_t *>(page_of(p))[x & 4095] = (uint8_t)src[i];
+    }
+    if (a < c->code_hi && a + n > c->code_lo) mark_dirty(m, a, a + n);
+    return true;
+}
 
 enum { F_NONE = 0, F_SYSCALL, F_BREAK, F_ILLEGAL, F_UNKNOWN, F_ESCAPE, F_ESCCSR, F_PGFAULT, F_NEEDPAGE, F_DETECT,
        F_AMOLINE, F_SCLINE };
@@ -347,7 +527,13 @@ __device__ int fetch_lane(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, 
 // se_workload.cc:529-895); 0 absent, 1 unimplemented, 2 ignore, 3 escape,
 // 4 modelled.
 __device__ int sys_class(int num) {
-    if (num == 64 || num == 93 || num == 94 || (num >= 172 && num <= 178)) return 4;
+    switch (num) {   // modelled (oracle/rv64se.c:sys_modelled)
+    case 29: case 57: case 64: case 66: case 93: case 94: case 96: case 160: case 163: case 214: case 215:
+    case 222: case 261: case 1058:
+        return 4;
+    default:
+        if (num >= 172 && num <= 178) return 4;
+    }
     const bool present = (num >= 0 && num <= 64) || (num >= 66 && num <= 243) || num == 258 ||
                          (num >= 260 && num <= 287) || (num >= 424 && num <= 450) ||
                          (num >= 1024 && num <= 1079) || num == 2011;
@@ -465,48 +651,24 @@ __device__ __forceinline__ void finish(Lane &L, int cls, int sub, int code, uint
 #define RREG(r) R[(uint32_t)(r) * kNL + lane]
 
 // The syscall path of one lane: EmuLinux::syscall (se_workload.cc:95-106)
-// with the golden-output comparator folded into write().
+// with the golden-output comparator folded into write()/writev().  Returns
+// true if the trial's code mapping or bytes may have changed (the solo
+// kernel's decode cache is dropped).
+constexpr uint64_t kVmMaxLen = 1ULL << 43;   // == oracle/rv64se.c VM_MAX_LEN
 template <uint32_t kNL>
-__device__ __forceinline__ void do_syscall(KCtx *c, const WaveMem &w, Lane &L, LaneMem &m, uint64_t slot,
-                                           uint64_t *R, uint32_t lane) {
+__device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m, uint64_t slot, uint64_t *R,
+                                        uint32_t lane) {
     const int num = (int)(uint32_t)RREG(17);
     const int cls = sys_class(num);
-    if (cls == 0) { finish(L, FI_CRASH, FI_CRASH_SYSCALL_RANGE, 1, (uint32_t)num); return; }
-    if (cls == 1) { finish(L, FI_CRASH, FI_CRASH_SYSCALL_UNIMPL, 1, (uint32_t)num); return; }
-    if (cls == 3) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, (uint32_t)num); return; }
-    if (cls == 2) { RREG(10) = 0; return; }
-    switch (num) {
-    case 93: case 94: {  // exitImpl -> exitSimLoop(status & 0xff), sim/syscall_emul.cc:120-248
-        const int code = (int)(uint32_t)RREG(10) & 0xff;
-        if (c->record) {
-            finish(L, FI_MASKED, 0, code, (uint32_t)L.pc);
-            return;
-        }
-        const bool same = !L.out_bad && L.out_pos == c->gout_len && L.err_pos == c->gerr_len && code == (int)c->gexit;
-        finish(L, same ? FI_MASKED : FI_SDC, 0, code, (uint32_t)L.pc);
-        return;
-    }
-    case 172: case 178: RREG(10) = kPid; return;
-    case 173: RREG(10) = kPpid; return;
-    case 174: case 175: RREG(10) = kUid; return;
-    case 176: case 177: RREG(10) = kGid; return;
-    default: break;   // 64: write
-    }
-    // writeFunc (src/sim/syscall_emul.hh:2826-2860): int fd, buffer copied in
-    // through a non-allocating proxy (fatal on an unmapped byte), then compared
-    // with the golden stream at the current position.
-    const int fd = (int)(uint32_t)RREG(10);
-    const uint64_t buf = RREG(11), n = RREG(12);
-    if (fd < 0 || fd >= 1024) { finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, (uint32_t)L.pc); return; }
-    if (fd == 0) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, (uint32_t)L.pc); return; }
-    if (fd > 2) { RREG(10) = (uint64_t)(int64_t)-9; return; }
-    if (n > (1ULL << 31)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, (uint32_t)L.pc); return; }
-    if (n) {
-        const uint64_t last = buf + n - 1;
-        if (last < buf) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, (uint32_t)L.pc); return; }
-        for (uint64_t v = buf >> 12; v <= (last >> 12); v++) {
-            if (!lookup(c, w, m, slot, v)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, (uint32_t)L.pc); return; }
-        }
+    const uint32_t pc32 = (uint32_t)L.pc;
+    if (cls == 0) { finish(L, FI_CRASH, FI_CRASH_SYSCALL_RANGE, 1, (uint32_t)num); return false; }
+    if (cls == 1) { finish(L, FI_CRASH, FI_CRASH_SYSCALL_UNIMPL, 1, (uint32_t)num); return false; }
+    if (cls == 3) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, (uint32_t)num); return false; }
+    if (cls == 2) { RREG(10) = 0; return false; }
+    const uint64_t a0 = RREG(10), a1 = RREG(11), a2 = RREG(12), a3 = RREG(13), a4 = RREG(14), a5 = RREG(15);
+    const uint32_t fdc = m.vm ? c->vm[slot].fdc : 0u;
+    // the bytes [buf, buf + n) (all mapped) appended to stream fd (1 or 2)
+    auto emit = [&](int fd, uint64_t buf, uint64_t n) {
         uint64_t &pos = fd == 1 ? L.out_pos : L.err_pos;
         const uint8_t *gold = fd == 1 ? c->gout : c->gerr;
         const uint64_t glen = fd == 1 ? c->gout_len : c->gerr_len;
@@ -525,8 +687,204 @@ __device__ __forceinline__ void do_syscall(KCtx *c, const WaveMem &w, Lane &L, L
             }
         }
         pos += n;
+    };
+    auto rd64 = [&](uint64_t a) {
+        uint64_t v = 0;
+        for (int k = 0; k < 8; k++) v |= (uint64_t)proxy_byte(c, w, m, slot, a + k) << (8 * k);
+        return v;
+    };
+    auto set_ret = [&](int64_t v) { RREG(10) = (uint64_t)v; };
+    switch (num) {
+    case 93: case 94: {  // exitImpl -> exitSimLoop(status & 0xff), sim/syscall_emul.cc:120-248
+        const int code = (int)(uint32_t)a0 & 0xff;
+        if (m.vm && c->vm[slot].ctid) {   // exitFutexWake: *childClearTID = 0 through the proxy (:106-117)
+            const int h = proxy_writable(c, w, m, slot, c->vm[slot].ctid, 8);
+            if (h == 0) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+            if (h == -1) { finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, pc32); return false; }
+            if (h == -2) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        }
+        if (c->record) {
+            finish(L, FI_MASKED, 0, code, pc32);
+            return false;
+        }
+        const bool same = !L.out_bad && L.out_pos == c->gout_len && L.err_pos == c->gerr_len && code == (int)c->gexit;
+        finish(L, same ? FI_MASKED : FI_SDC, 0, code, pc32);
+        return false;
+    }
+    case 172: case 178: set_ret(kPid); return false;
+    case 173: set_ret(kPpid); return false;
+    case 174: case 175: set_ret(kUid); return false;
+    case 176: case 177: set_ret(kGid); return false;
+    case 96:   // setTidAddressFunc (syscall_emul.cc:292-299)
+        vm_of(c, m, slot)->ctid = a0;
+        set_ret(kPid);
+        return false;
+    case 57: {   // closeFunc -> FDArray::closeFDEntry (fd_array.cc:334-352)
+        const int fd = (int)(uint32_t)a0;
+        if (fd < 0 || fd >= 1024) { set_ret(-9); return false; }
+        if (fd <= 2) vm_of(c, m, slot)->fdc |= 1u << fd;
+        set_ret(0);
+        return false;
+    }
+    case 29: {   // ioctlFunc (syscall_emul.hh:743-813)
+        const int fd = (int)(uint32_t)a0;
+        const uint32_t req = (uint32_t)a1;
+        if (!(req == 0x5401 || req == 0x5405 || req == 0x5407 || req == 0x541B) && (fd < 0 || fd >= 1024)) {
+            finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, pc32);
+            return false;
+        }
+        set_ret(-25);   // -ENOTTY
+        return false;
+    }
+    case 214: {   // brkFunc (syscall_emul.cc:268-289), MemState::updateBrkRegion (mem_state.cc:107-170)
+        VmState *v = vm_of(c, m, slot);
+        const uint64_t nb = a0, ob = v->brk;
+        if (nb == 0 || nb == ob) { set_ret((int64_t)ob); return false; }
+        const uint64_t na = (nb + 4095) & ~4095ULL, oa = (ob + 4095) & ~4095ULL;
+        if ((na > oa ? na - oa : oa - na) > kVmMaxLen) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, 214u); return false; }
+        if (nb < ob) {
+            if (oa != na && vm_unmap(c, w, m, slot, v, na, oa)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            v->brk = nb;
+            set_ret((int64_t)nb);
+            return true;
+        }
+        if (na > oa) {
+            const int u = vm_is_unmapped(c, w, m, slot, oa, na - oa);
+            if (u < 0) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }
+            if (!u) { set_ret((int64_t)ob); return false; }
+            if (!vm_add(v, oa, na)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        }
+        v->brk = nb;
+        set_ret((int64_t)nb);
+        return false;
+    }
+    case 222: case 1058: {   // mmapFunc (syscall_emul.hh:2002-2126), anonymous mappings; MemState::extendMmap
+        uint64_t start = a0, len = a1;
+        const int flags = (int)(uint32_t)a3, fd = (int)(uint32_t)a4;
+        if ((start & 4095) || (a5 & 4095) || ((flags & 2) && (flags & 1)) || (!(flags & 2) && !(flags & 1)) || !len) {
+            set_ret(-22);
+            return false;
+        }
+        if (len > kVmMaxLen) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, 222u); return false; }
+        len = (len + 4095) & ~4095ULL;
+        if (!(flags & 0x20)) {
+            if (fd < 0 || fd >= 1024) { finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, pc32); return false; }
+            if (fd > 2 || ((fdc >> fd) & 1)) { set_ret(-9); return false; }
+            finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32);   // a host file mapping
+            return false;
+        }
+        if (start + len < start) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, 222u); return false; }
+        VmState *v = vm_of(c, m, slot);
+        bool changed = false;
+        if (!(flags & 0x10)) {
+            int u = 0;
+            if (start) {
+                u = vm_is_unmapped(c, w, m, slot, start, len);
+                if (u < 0) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }
+            }
+            if (!u) {
+                uint64_t s2 = v->mmap_end - len;
+                for (;;) {
+                    if (s2 > v->mmap_end) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, 222u); return false; }
+                    int hit = -1;
+                    for (uint32_t i = 0; i < v->nvma && hit < 0; i++)
+                        if (v->vma[i][0] < s2 + len && s2 < v->vma[i][1]) hit = (int)i;
+                    if (hit < 0) break;
+                    s2 = v->vma[hit][0] - len;   // the page-by-page scan lands right below it
+                }
+                if (vm_is_unmapped(c, w, m, slot, s2, len) < 0) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }
+                v->mmap_end = s2;
+                start = s2;
+            }
+        } else {
+            if (vm_unmap(c, w, m, slot, v, start, start + len)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            changed = true;
+        }
+        if (!vm_add(v, start, start + len)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        set_ret((int64_t)start);
+        return changed;
+    }
+    case 215: {   // munmapFunc (syscall_emul.hh:3140-3156)
+        if (a0 & 4095) { set_ret(-22); return false; }
+        if (a1 > kVmMaxLen) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, 215u); return false; }
+        const uint64_t len = (a1 + 4095) & ~4095ULL;
+        if (a0 + len < a0) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, 215u); return false; }
+        if (vm_unmap(c, w, m, slot, vm_of(c, m, slot), a0, a0 + len)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        set_ret(0);
+        return true;
+    }
+    case 163: case 261: {   // getrlimitFunc / prlimitFunc (syscall_emul.hh:2197-2264)
+        const uint64_t rlp = num == 163 ? a1 : a3;
+        if (rlp && !proxy_readable(c, w, m, slot, rlp, 16)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+        if (num == 261 && (int)(uint32_t)a0 != 0) { set_ret(-1); return false; }   // -EPERM
+        if (num == 261 && !rlp) { set_ret(0); return false; }
+        const int64_t res = num == 163 ? (int64_t)(uint32_t)a0 : (int64_t)(int32_t)(uint32_t)a1;
+        uint64_t lim;
+        if (res == 3) lim = 8ULL << 20;
+        else if (res == 2) lim = 256ULL << 20;
+        else if (res == 6 && num == 163) lim = 1;   // RLIMIT_NPROC: the system's thread contexts
+        else { set_ret(-22); return false; }
+        if (!rlp) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }   // null ProxyPtr
+        char b[16];
+        for (int k = 0; k < 8; k++) b[k] = b[8 + k] = (char)(lim >> (8 * k));
+        if (!proxy_write(c, w, m, slot, rlp, b, 16)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        set_ret(0);
+        return rlp < c->code_hi && rlp + 16 > c->code_lo;
+    }
+    case 160: {   // unameFunc64 (arch/riscv/linux/se_workload.cc:109-122): 5 fields of 65 chars
+        if (!a0) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }
+        if (!proxy_readable(c, w, m, slot, a0, 325)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+        const char *f0 = "Linux", *f1 = "sim.gem5.org", *f2 = "5.1.0", *f3 = "#1 Mon Aug 18 11:32:15 EDT 2003",
+                   *f4 = "riscv64";
+        const char *f[5] = {f0, f1, f2, f3, f4};
+        for (int k = 0; k < 5; k++) {
+            uint64_t n = 0;
+            while (f[k][n]) n++;
+            if (!proxy_write(c, w, m, slot, a0 + 65 * k, f[k], n + 1)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        }
+        set_ret(0);
+        return a0 < c->code_hi && a0 + 325 > c->code_lo;
+    }
+    case 66: {   // writevFunc (syscall_emul.hh:1964-1996)
+        const int fd = (int)(uint32_t)a0;
+        if (fd < 0 || fd >= 1024) { finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, pc32); return false; }
+        if (fd > 2 || ((fdc >> fd) & 1)) { set_ret(-9); return false; }
+        if (fd == 0 || a2 > (1u << 20)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+        uint64_t total = 0;
+        for (uint64_t i = 0; i < a2; i++) {
+            const uint64_t e = a1 + 16 * i;
+            if (e < a1 || !proxy_readable(c, w, m, slot, e, 16)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+            const uint64_t base = rd64(e), n = rd64(e + 8);
+            if (n > (1ULL << 31)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+            if (!proxy_readable(c, w, m, slot, base, n)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+            total += n;
+        }
+        if (a2 > 1024) { set_ret(-22); return false; }   // host writev: IOV_MAX
+        if (total > (1ULL << 31)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+        for (uint64_t i = 0; i < a2; i++) {
+            const uint64_t e = a1 + 16 * i;
+            emit(fd, rd64(e), rd64(e + 8));
+        }
+        set_ret((int64_t)total);
+        return false;
+    }
+    default: break;   // 64: write
+    }
+    // writeFunc (src/sim/syscall_emul.hh:2826-2860): int fd, buffer copied in
+    // through a non-allocating proxy (fatal on an unmapped byte), then compared
+    // with the golden stream at the current position.
+    const int fd = (int)(uint32_t)a0;
+    const uint64_t buf = a1, n = a2;
+    if (fd < 0 || fd >= 1024) { finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, pc32); return false; }
+    if (fd > 2 || ((fdc >> fd) & 1)) { set_ret(-9); return false; }   // no fd entry: -EBADF
+    if (fd == 0) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+    if (n > (1ULL << 31)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+    if (n) {
+        if (!proxy_readable(c, w, m, slot, buf, n)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+        emit(fd, buf, n);
     }
     RREG(10) = n;
+    return false;
 }
 
 // ------------------------------------------------------------------ snapshots
@@ -741,6 +1099,7 @@ __device__ __forceinline__ void trial_body() {
     m.tnext = 0; m.n_priv = 0; m.req_vpn = kNone; m.req_src = nullptr; m.code_dirty = false;
     m.dlo = m.dhi = 0;
     m.resv = m.lock = kNone;
+    m.vm = false;
     if (resume && live) {
         L.pc = SV->pc; L.ninst = SV->ninst; L.ncyc = SV->ncyc; L.out_pos = SV->out_pos; L.err_pos = SV->err_pos;
         L.next_chk = SV->next_chk; L.nfail = SV->nfail; L.watch = SV->watch;
@@ -748,6 +1107,7 @@ __device__ __forceinline__ void trial_body() {
         m.stack_min = SV->stack_min; m.n_priv = SV->n_priv; m.code_dirty = (SV->flags >> 3) & 1;
         m.dlo = CX->code_lo + SV->dlo; m.dhi = CX->code_lo + SV->dhi;
         m.resv = SV->resv; m.lock = SV->lock;
+        m.vm = (SV->flags >> 5) & 1;
     }
     bool suspended = false;
     const uint64_t start_inst = (live && !resume) ? L.ninst : 0;
@@ -812,7 +1172,7 @@ __device__ __forceinline__ void trial_body() {
                 sv->dlo = m.code_dirty ? (uint32_t)(m.dlo > CX->code_lo ? m.dlo - CX->code_lo : 0) : 0;
                 sv->dhi = m.code_dirty ? (uint32_t)((m.dhi < CX->code_hi ? m.dhi : CX->code_hi) - CX->code_lo) : 0;
                 sv->flags = (L.out_bad ? 1u : 0u) | ((uint32_t)L.injected << 1) | (m.code_dirty ? 8u : 0u) |
-                            (L.fp ? 16u : 0u);
+                            (L.fp ? 16u : 0u) | (m.vm ? 32u : 0u);
                 sv->resv = m.resv; sv->lock = m.lock;
                 CX->surv[atomicAdd(CX->surv_n, 1u)] = (uint32_t)slot;
                 suspended = true;
@@ -895,7 +1255,7 @@ __device__ __forceinline__ void trial_body() {
                 const SnapState *S = CX->snaps + (uint32_t)(kn / CX->snap_interval);
                 bool eq = grp && L.pc == S->pc && L.out_pos == S->out_pos && L.err_pos == S->err_pos && !L.out_bad &&
                           m.stack_min == S->stack_min && !L.fp && L.injected != 3 && m.resv == kNone &&
-                          m.lock == kNone;
+                          m.lock == kNone && !m.vm;
                 if (wballot<kNL>(eq)) {
                     // a register the golden future writes before reading it cannot
                     // influence the outcome (liveness from the golden trace)
@@ -1401,13 +1761,10 @@ __device__ __forceinline__ void trial_body() {
                     // GenericPageTableFault::invoke -> fixupFault (sim/faults.cc:95-105)
                     L.ncyc += t;
                     mine = false;
-                    if (fva < m.stack_min && fva >= kStackBase - kMaxStack) {
-                        const uint64_t nm = fva & ~4095ULL;
-                        if (kStackBase - nm > kMaxStack) finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, (uint32_t)L.pc);
-                        else m.stack_min = nm;
-                    } else {
-                        finish(L, FI_CRASH, FI_CRASH_PAGE_FAULT, 134, (uint32_t)fva);
-                    }
+                    const int h = fixup_fault(CX, m, slot, fva);
+                    if (h == 0) finish(L, FI_CRASH, FI_CRASH_PAGE_FAULT, 134, (uint32_t)fva);
+                    else if (h == -1) finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, (uint32_t)L.pc);
+                    else if (h == -2) finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, (uint32_t)L.pc);
                 }
             }
             const uint64_t okm = wballot<kNL>(mine);
@@ -1734,10 +2091,21 @@ __device__ __forceinline__ void trial_body() {
             else L.pc = npc;
         } else {
         switch (f) {
-        case F_SYSCALL:   // SyscallFault::invokeSE advances the PC first (arch/riscv/faults.cc:325-333)
+        case F_SYSCALL: {   // SyscallFault::invokeSE advances the PC first (arch/riscv/faults.cc:325-333)
             L.pc = pc + d.len;
-            do_syscall<kNL>(CX, w, L, m, slot, R, lane);
+            // (out of line on copies: the interpreter's state stays in registers)
+            Lane Ls = L;
+            LaneMem ms = m;
+            const bool chg = do_syscall<kNL>(CX, w, Ls, ms, slot, R, lane);
+            L = Ls;
+            m = ms;
+            if (chg) {
+                if constexpr (kNL == 1) {
+                    for (uint32_t k = 0; k < kDC; k++) DCT[k] = 0xFFFFFFFFu;   // the code mapping changed
+                }
+            }
             break;
+        }
         case F_BREAK: finish(L, FI_CRASH, FI_CRASH_SIGTRAP, 133, (uint32_t)pc); break;
         case F_ILLEGAL: finish(L, FI_CRASH, FI_CRASH_ILLEGAL_INST, 134, (uint32_t)pc); break;
         case F_UNKNOWN: finish(L, FI_CRASH, FI_CRASH_UNKNOWN_INST, 134, (uint32_t)pc); break;
@@ -1746,15 +2114,13 @@ __device__ __forceinline__ void trial_body() {
         case F_DETECT: finish(L, FI_DETECTED, 0, 0, (uint32_t)pc); break;
         case F_AMOLINE: finish(L, FI_CRASH, FI_CRASH_AMO_LINE, 134, (uint32_t)pc); break;
         case F_SCLINE: finish(L, FI_CRASH, FI_CRASH_SC_LINE, 134, (uint32_t)pc); break;
-        case F_PGFAULT:
-            if (fva < m.stack_min && fva >= kStackBase - kMaxStack) {
-                const uint64_t nm = fva & ~4095ULL;
-                if (kStackBase - nm > kMaxStack) finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, (uint32_t)pc);
-                else m.stack_min = nm;
-            } else {
-                finish(L, FI_CRASH, FI_CRASH_PAGE_FAULT, 134, (uint32_t)fva);
-            }
+        case F_PGFAULT: {   // GenericPageTableFault::invoke -> fixupFault (sim/faults.cc:95-105)
+            const int h = fixup_fault(CX, m, slot, fva);
+            if (h == 0) finish(L, FI_CRASH, FI_CRASH_PAGE_FAULT, 134, (uint32_t)fva);
+            else if (h == -1) finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, (uint32_t)pc);
+            else if (h == -2) finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, (uint32_t)pc);
             break;
+        }
         default: break;
         }
         }   // fault disposition
@@ -1815,6 +2181,7 @@ __device__ __forceinline__ void trial_body() {
         CX->stats[20] = __builtin_amdgcn_s_memtime() - t_start;
         CX->stats[21] = __builtin_amdgcn_s_memrealtime() - rt_start;
     }
+    if (CX->record) pages_made = m.n_priv;   // golden: every private entry (pages, tombstones)
     const uint64_t fb = wsum64<kNL>(L.fetch_b), db = wsum64<kNL>(L.data_b), pm = wsum64<kNL>(pages_made);
     const uint64_t si = wsum64<kNL>(start_inst);
     const uint64_t xi = wsum64<kNL>(live ? L.ninst - launch_inst : 0);

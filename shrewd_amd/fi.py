@@ -21,7 +21,7 @@ FI_OK, FI_E_ARG, FI_E_NODEVICE, FI_E_HIP, FI_E_ELF, FI_E_STATE, FI_E_GOLDEN = 0,
 CLASS_NAMES = ["masked", "sdc", "crash", "hang", "detected", "escape"]
 CRASH_NAMES = {1: "panic_unknown_inst", 2: "panic_illegal_inst", 3: "panic_page_fault",
                4: "fatal_syscall_range", 5: "fatal_syscall_unimpl", 6: "fatal_proxy", 7: "abort_fd_assert",
-               8: "sigtrap", 9: "fatal_stack_limit", 10: "panic_amo_line", 11: "abort_sc_line"}
+               8: "sigtrap", 9: "fatal_stack_limit", 10: "panic_amo_line", 11: "abort_sc_line", 12: "panic_se_handler"}
 ESCAPE_NAMES = {1: "inst", 2: "syscall", 3: "csr", 4: "host", 5: "resource"}
 T_PC, T_MEM, T_RESULT, N_STRUCT = 32, 33, 34, 35
 

@@ -305,7 +305,7 @@ def test_native_driver_matches_engine(engine_factory, tmp_path):
     assert hist["counts"].tobytes() == rh["counts"].tobytes()
 
 
-@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc"])
+@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm"])
 def test_known_answer_programs(oracle_mod, prog):
     """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
@@ -316,7 +316,10 @@ def test_known_answer_programs(oracle_mod, prog):
     translated code diverges and merges).
     rvc: the compressed (RVC + Zcb) register forms.
     sys: the modelled syscalls (get*id, write to stdout/stderr/bad fd,
-    an ignored call, exit status & 0xff).  The device golden run (general interpreter)
+    an ignored call, exit status & 0xff).
+    lrsc: LR/SC reservations and lock records.
+    vm: brk / mmap / munmap / set_tid_address / ioctl / getrlimit / prlimit64 /
+    uname / writev / close (the SE memory map).  The device golden run (general interpreter)
     must print exactly the reference-derived models; no-fault trials
     (pre-decoded and translated paths, from snapshots) must end masked with
     the oracle's records; faulted trials must match the oracle bit for bit."""
@@ -327,15 +330,17 @@ def test_known_answer_programs(oracle_mod, prog):
                      "cmp": (kat.cmp_program_elf, kat.cmp_program_expected),
                      "rvc": (kat.rvc_program_elf, kat.rvc_program_expected),
                      "sys": (kat.sys_program_elf, kat.sys_program_expected),
-                     "lrsc": (kat.lrsc_program_elf, kat.lrsc_program_expected)}[prog]
+                     "lrsc": (kat.lrsc_program_elf, kat.lrsc_program_expected),
+                     "vm": (kat.vm_program_elf, kat.vm_program_expected)}[prog]
+    stderr = {"sys": kat.SYS_STDERR, "vm": kat.VM_STDERR}.get(prog, b"")
     elf, expected = elf(), expected()
     e = Engine(private_pages=64)
     e.load_elf(elf, [prog])
     g = e.golden_run()
     assert g.exit_code == (300 & 0xFF if prog == "sys" else 0)
-    assert g.stderr_len == (len(kat.SYS_STDERR) if prog == "sys" else 0)
+    assert g.stderr_len == len(stderr)
     assert e.golden_stdout() == expected
-    assert e.golden_stderr() == (kat.SYS_STDERR if prog == "sys" else b"")
+    assert e.golden_stderr() == stderr
     o = oracle_mod.Oracle(elf, prog)
     o.run_golden()
     assert o.golden_stderr() == e.golden_stderr()

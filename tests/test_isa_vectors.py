@@ -837,3 +837,262 @@ def test_lrsc_decode(oracle_mod):
     # lr.w / sc.d / lr.d.aqrl decode to the executed ops (no longer escapes)
     for raw, name in ((0x1005272F, "lr_w"), (0x18B5362F, "sc_d"), (0x1605352F, "lr_d")):
         assert oracle_mod.mnemonic(raw) == name, hex(raw)
+
+
+# SE memory map and the remaining deterministic handlers (oracle/rv64se.c
+# do_syscall; gem5 MemState, src/sim/mem_state.cc): brk grows, shrinks (the
+# pages leave the map and come back zero) and regrows; anonymous mmap grows
+# down from mmap_end = 0x4000000000000000 (RiscvProcess64, process.cc:79), a
+# free hint is honoured, MAP_FIXED replaces; munmap; set_tid_address; ioctl;
+# getrlimit / prlimit64; uname; writev; close of stderr then write(2) ->
+# -EBADF; exit clears *childClearTID.
+VM_MMAP0 = 0x4000000000000000 - 0x2000
+VM_EXPECTED_TAIL = [0x2800, 0x1234, 8, 0x2000, 0, VM_MMAP0, 0x77, 0, 0x1000, 0, 0x1000, 0, 0, -22, -9, -22, 100,
+                    -25, -25, 0, 8 << 20, 0, 256 << 20, -1, -22, 0, 1, 0, 13, 5, 0, -9, -9, -9, 0, 0x2000]
+VM_STDOUT_HEAD = b"Linuxriscv64\n"
+VM_STDERR = b"Linux"
+
+
+def vm_program_source() -> str:
+    n_out = 8 * (1 + len(VM_EXPECTED_TAIL))
+    def mmap(a0, a1, a3, a4=-1, a2=3):
+        return (f"    {a0}\n    li    a1, {a1}\n    li    a2, {a2}\n    li    a3, {a3}\n    li    a4, {a4}\n"
+                f"    li    a5, 0\n    li    a7, 222\n    ecall\n")
+    return f"""    .text
+_start:
+    la    s2, out
+    li    a0, 0
+    li    a7, 214
+    ecall
+    mv    s0, a0
+    sd    a0, 0(s2)
+    li    t0, 0x2800
+    add   a0, s0, t0
+    li    a7, 214
+    ecall
+    sub   t1, a0, s0
+    sd    t1, 8(s2)
+    li    t0, 0x1000
+    add   t3, s0, t0
+    li    t1, 0x1234
+    sd    t1, 0(t3)
+    ld    t1, 0(t3)
+    sd    t1, 16(s2)
+    addi  a0, s0, 8
+    li    a7, 214
+    ecall
+    sub   t1, a0, s0
+    sd    t1, 24(s2)
+    li    t0, 0x2000
+    add   a0, s0, t0
+    li    a7, 214
+    ecall
+    sub   t1, a0, s0
+    sd    t1, 32(s2)
+    ld    t1, 0(t3)
+    sd    t1, 40(s2)
+{mmap("li    a0, 0", 0x2000, 0x22)}    mv    s1, a0
+    sd    a0, 48(s2)
+    li    t0, 0x1008
+    add   t3, s1, t0
+    li    t1, 0x77
+    sd    t1, 0(t3)
+    ld    t1, 0(t3)
+    sd    t1, 56(s2)
+    li    t0, 0x1000
+    add   a0, s1, t0
+    li    a1, 0x1000
+    li    a7, 215
+    ecall
+    sd    a0, 64(s2)
+    li    t0, 0x1000
+{mmap("add   a0, s1, t0", 0x1000, 0x22)}    sub   t1, a0, s1
+    sd    t1, 72(s2)
+    ld    t1, 0(t3)
+    sd    t1, 80(s2)
+{mmap("li    a0, 0", 0x1000, 0x22)}    sub   t1, s1, a0
+    sd    t1, 88(s2)
+    li    t1, 0x55
+    sd    t1, 0(s1)
+{mmap("mv    a0, s1", 0x1000, 0x32)}    sub   t1, a0, s1
+    sd    t1, 96(s2)
+    ld    t1, 0(s1)
+    sd    t1, 104(s2)
+{mmap("li    a0, 0", 0x1000, 0x20)}    sd    a0, 112(s2)
+{mmap("li    a0, 0", 0x1000, 0x2, a4=3, a2=1)}    sd    a0, 120(s2)
+    addi  a0, s1, 1
+    li    a1, 0x1000
+    li    a7, 215
+    ecall
+    sd    a0, 128(s2)
+    la    a0, tid
+    li    a7, 96
+    ecall
+    sd    a0, 136(s2)
+    li    a0, 1
+    li    a1, 0x5401
+    li    a2, 0
+    li    a7, 29
+    ecall
+    sd    a0, 144(s2)
+    li    a0, 7
+    li    a1, 0x1234
+    li    a2, 0
+    li    a7, 29
+    ecall
+    sd    a0, 152(s2)
+    la    s3, rl
+    li    a0, 3
+    mv    a1, s3
+    li    a7, 163
+    ecall
+    sd    a0, 160(s2)
+    ld    t1, 0(s3)
+    sd    t1, 168(s2)
+    li    a0, 0
+    li    a1, 2
+    li    a2, 0
+    mv    a3, s3
+    li    a7, 261
+    ecall
+    sd    a0, 176(s2)
+    ld    t1, 8(s3)
+    sd    t1, 184(s2)
+    li    a0, 1
+    li    a1, 2
+    li    a2, 0
+    mv    a3, s3
+    li    a7, 261
+    ecall
+    sd    a0, 192(s2)
+    li    a0, 7
+    mv    a1, s3
+    li    a7, 163
+    ecall
+    sd    a0, 200(s2)
+    li    a0, 6
+    mv    a1, s3
+    li    a7, 163
+    ecall
+    sd    a0, 208(s2)
+    ld    t1, 0(s3)
+    sd    t1, 216(s2)
+    la    a0, uts
+    li    a7, 160
+    ecall
+    sd    a0, 224(s2)
+    la    t0, iov
+    la    t1, uts
+    sd    t1, 0(t0)
+    li    t2, 5
+    sd    t2, 8(t0)
+    addi  t1, t1, 260
+    sd    t1, 16(t0)
+    li    t2, 7
+    sd    t2, 24(t0)
+    la    t1, nl
+    sd    t1, 32(t0)
+    li    t2, 1
+    sd    t2, 40(t0)
+    li    a0, 1
+    la    a1, iov
+    li    a2, 3
+    li    a7, 66
+    ecall
+    sd    a0, 232(s2)
+    li    a0, 2
+    la    a1, iov
+    li    a2, 1
+    li    a7, 66
+    ecall
+    sd    a0, 240(s2)
+    li    a0, 2
+    li    a7, 57
+    ecall
+    sd    a0, 248(s2)
+    li    a0, 2
+    la    a1, nl
+    li    a2, 1
+    li    a7, 64
+    ecall
+    sd    a0, 256(s2)
+    li    a0, 2
+    la    a1, iov
+    li    a2, 1
+    li    a7, 66
+    ecall
+    sd    a0, 264(s2)
+    li    a0, -1
+    li    a7, 57
+    ecall
+    sd    a0, 272(s2)
+    li    a0, 9
+    li    a7, 57
+    ecall
+    sd    a0, 280(s2)
+    li    a0, 0
+    li    a7, 214
+    ecall
+    sub   t1, a0, s0
+    sd    t1, 288(s2)
+    li    a0, 1
+    mv    a1, s2
+    li    a2, {n_out}
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 93
+    ecall
+    .data
+nl:
+    .byte 10
+    .bss
+    .balign 8
+out:
+    .zero {n_out}
+rl:
+    .zero 16
+iov:
+    .zero 48
+tid:
+    .zero 8
+uts:
+    .zero 328
+"""
+
+
+def vm_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(vm_program_source())
+
+
+def elf_brk0(elf: bytes) -> int:
+    """roundUp(max p_vaddr + p_memsz of the PT_LOAD segments, page)."""
+    import struct
+    phoff, = struct.unpack_from("<Q", elf, 0x20)
+    phentsize, phnum = struct.unpack_from("<HH", elf, 0x36)
+    top = 0
+    for i in range(phnum):
+        p_type, _, _, vaddr, paddr, _, memsz = struct.unpack_from("<IIQQQQQ", elf, phoff + i * phentsize)
+        if p_type == 1:
+            top = max(top, paddr + memsz)
+    return (top + 4095) & ~4095
+
+
+def vm_program_expected() -> bytes:
+    vals = [elf_brk0(vm_program_elf())] + VM_EXPECTED_TAIL
+    return VM_STDOUT_HEAD + b"".join((v & M64).to_bytes(8, "little") for v in vals)
+
+
+def test_vm_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(vm_program_elf(), "vm")
+    g = o.run_golden()
+    assert g.exit_code == 0
+    got = o.golden_stdout()
+    exp = vm_program_expected()
+    assert len(got) == len(exp)
+    vals = [int.from_bytes(got[13 + 8 * k:21 + 8 * k], "little") for k in range((len(got) - 13) // 8)]
+    evals = [int.from_bytes(exp[13 + 8 * k:21 + 8 * k], "little") for k in range((len(exp) - 13) // 8)]
+    assert [hex(v) for v in vals] == [hex(v) for v in evals]
+    assert got == exp
+    assert o.golden_stderr() == VM_STDERR

@@ -39,11 +39,19 @@ L.fi_debug_jit_compile(body, b"gfx950", buf, n.value, C.byref(n), err, 8192)
 co = "/tmp/fi_jit_inspect.co"
 open(co, "wb").write(buf.raw[:n.value])
 notes = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "--notes", co], capture_output=True, text=True).stdout
-for key in (".vgpr_count", ".sgpr_count", ".vgpr_spill_count", ".sgpr_spill_count", ".private_segment_fixed_size"):
-    for line in notes.splitlines():
-        if key + ":" in line:
-            print(line.strip())
-            break
+# per kernel (each kernel's metadata block is sorted by key; .wavefront_size closes it)
+keys = (".vgpr_count", ".sgpr_count", ".vgpr_spill_count", ".sgpr_spill_count", ".private_segment_fixed_size")
+cur = {}
+for line in notes.splitlines():
+    t = line.strip().lstrip("- ")
+    for key in keys:
+        if t.startswith(key + ":"):
+            cur[key] = t.split(":", 1)[1].strip()
+    if t.startswith(".name:"):
+        cur["name"] = t.split(":", 1)[1].strip()
+    if t.startswith(".wavefront_size:"):   # the last key of a kernel's block
+        print(cur.get("name"), " ".join(f"{k[1:]}={cur.get(k)}" for k in keys))
+        cur = {}
 if len(sys.argv) > 2:
     dis = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "-d", co], capture_output=True, text=True).stdout
     open(sys.argv[2], "w").write(dis)
