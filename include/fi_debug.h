@@ -16,7 +16,7 @@ fi_status fi_debug_decode(fi_engine *e, const uint32_t *raws, uint64_t n, void *
  * cycles/output, loop iterations, lane-instructions, slow fetches, min-PC
  * reductions, snapshot comparisons and early exits, translated instructions
  * and entries, the slowest wave, wave-0 clock; [24..27] -DFI_PROF builds only. */
-fi_status fi_debug_stats(fi_engine *e, uint64_t *out32);
+fi_status fi_debug_stats(fi_engine *e, uint64_t *out40);
 /* Per wave of the last launch: {s_memtime cycles, loop iterations,
  * translated instructions, slow fetches} (4 x u64 each). */
 fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves);

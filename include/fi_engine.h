@@ -140,6 +140,11 @@ typedef struct {
 #define FI_CFG_NO_SOLO 64u
 /* every epoch, the first included, on the solo kernel (A/B and parity checks) */
 #define FI_CFG_SOLO_ALL 128u
+/* diverged-lanes step loop in the 64-lane kernel: lanes at
+ * different pcs each execute their own pre-decoded micro-op per step.  Off by
+ * default: it trades per-trial latency for throughput, and the campaign tail
+ * is latency-bound (profiles/r02d_simt_sweep.jsonl) */
+#define FI_CFG_SIMT 256u
 
 typedef struct {
     uint64_t ninst, ncycles;

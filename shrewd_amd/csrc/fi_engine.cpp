@@ -465,7 +465,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_tmp, std::max<size_t>(e->tmp_bytes, 16)));
     HIPCHK(hipMalloc(&e->d_out, c * sizeof(fi_outcome)));
     HIPCHK(hipMalloc(&e->d_hist, sizeof(fi_histogram)));
-    HIPCHK(hipMalloc(&e->d_stats, 32 * sizeof(unsigned long long)));
+    HIPCHK(hipMalloc(&e->d_stats, kNStats * sizeof(unsigned long long)));
     HIPCHK(hipMalloc(&e->d_wave_dbg, c * 4 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&e->d_priv, c * e->cfg.private_pages * kPage));
     HIPCHK(hipMalloc(&e->d_priv_vpn, c * e->cfg.private_pages * 8));
@@ -510,6 +510,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.wave_dbg = e->d_wave_dbg;
     c.stats = e->d_stats;
     c.brk0 = e->brk0; c.svma_lo = e->svma_lo; c.svma_hi = e->svma_hi; c.vm = e->d_vm;
+    c.simt_min = (e->cfg.flags & FI_CFG_SIMT) ? 8u : 0u;
     c.lanes = e->cfg.lanes_per_wave;
     return c;
 }
@@ -539,7 +540,7 @@ static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_
     c.n = 1;
     c.n_slots = 1;
     c.sites = nullptr; c.perm = nullptr;
-    hipError_t err = hipMemsetAsync(e->d_stats, 0, 32 * sizeof(unsigned long long), e->stream);
+    hipError_t err = hipMemsetAsync(e->d_stats, 0, kNStats * sizeof(unsigned long long), e->stream);
     if (err == hipSuccess) err = hipEventRecord(e->ev0, e->stream);
     if (err == hipSuccess) err = launch_trials(c, e->stream);
     if (err == hipSuccess) err = hipEventRecord(e->ev1, e->stream);
@@ -547,7 +548,7 @@ static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_
     float ms = 0;
     if (err == hipSuccess) err = hipEventElapsedTime(&ms, e->ev0, e->ev1);
     if (err == hipSuccess) err = hipMemcpy(&o, e->d_out, sizeof o, hipMemcpyDeviceToHost);
-    if (err == hipSuccess) err = hipMemcpy(stats, e->d_stats, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(stats, e->d_stats, kNStats * sizeof(unsigned long long), hipMemcpyDeviceToHost);
     (void)hipFree(d_gpriv);
     (void)hipFree(d_gfregs);
     (void)hipFree(d_gvpn);
@@ -582,7 +583,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     HIPCHK(hipMalloc(&d_rec_out, rec_cap));
     HIPCHK(hipMalloc(&d_rec_err, rec_cap));
     fi_outcome o;
-    unsigned long long stats[32];
+    unsigned long long stats[kNStats];
     st = golden_launch(e, kGoldenPages, 0, 0, nullptr, nullptr, nullptr, nullptr, 0, d_rec_out, d_rec_err, rec_cap, o,
                        stats);
     if (st) { (void)hipFree(d_rec_out); (void)hipFree(d_rec_err); return st; }
@@ -888,7 +889,7 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     c.n = k;
     c.n_slots = (uint32_t)k;
     c.save = e->d_save;
-    HIPCHK(hipMemsetAsync(e->d_stats, 0, 32 * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(e->d_stats, 0, kNStats * sizeof(unsigned long long), st));
     HIPCHK(hipMemsetAsync(e->d_cnt, 0, 16 * 4, st));
     const bool pack = (e->cfg.flags & FI_CFG_PACK_RUNS) != 0;
     int n_cu = 0;
@@ -1120,10 +1121,10 @@ fi_status fi_debug_translation(fi_engine *e, char *buf, uint64_t cap, uint64_t *
     return FI_OK;
 }
 
-fi_status fi_debug_stats(fi_engine *e, uint64_t *out16) {
-    if (!e || !out16) return FI_E_ARG;
+fi_status fi_debug_stats(fi_engine *e, uint64_t *out40) {
+    if (!e || !out40) return FI_E_ARG;
     HIPCHK(hipStreamSynchronize(e->stream));
-    HIPCHK(hipMemcpy(out16, e->d_stats, 32 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out40, e->d_stats, kNStats * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return FI_OK;
 }
 

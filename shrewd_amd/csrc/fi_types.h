@@ -82,6 +82,8 @@ struct VmState {
 
 // Everything one launch of the trial kernel needs.  Passed by value as the
 // kernel argument (lives in the kernarg segment -> scalar loads).
+constexpr int kNStats = 40;          // DevCtx::stats entries
+
 struct DevCtx {
     // golden text, pre-decoded (pre_ok = 0 if the golden run rewrote its text)
     const PreInst *pre;
@@ -149,6 +151,7 @@ struct DevCtx {
     // SE memory map: process-start brk and "stack" VMA; per-slot VM state
     uint64_t brk0, svma_lo, svma_hi;
     VmState *vm;                     // [n_slots]
+    uint32_t simt_min;               // diverged-lanes step loop: least lanes to enter it (0 = off)
     unsigned long long *stats;       // [0] fetch B [1] data B [2] pages [3..5] golden ncycles/out/err
                                      // [6] loop iterations [7] lane-insts [8] slow fetches [9] min-PC [10] max iter/wave
                                      // [11] early-exit checks [12] early exits [13] snapshots captured [14] start-inst sum
@@ -157,6 +160,8 @@ struct DevCtx {
                                      // [20] wave-0 s_memtime delta [21] s_memrealtime delta
                                      // [22] golden run holds state outside the snapshots (FP, LR/SC, VM)
                                      // [23] instructions executed on the device
+                                     // [24] lane-instructions of the diverged-lanes step loop
+                                     // [32..39] FI_PROF phase cycles
 };
 
 struct SampleCtx {

@@ -1157,6 +1157,7 @@ __device__ __forceinline__ void trial_body() {
 #define n_early WS[4]
 #define n_tx WS[5]
 #define n_txin WS[6]
+#define n_simt WS[7]
 
     for (;;) {
         // ---- epochs: after wave_budget iterations the wave suspends its live
@@ -1335,6 +1336,147 @@ __device__ __forceinline__ void trial_body() {
         if (!L.injected) next_ev = s.inst < next_ev ? s.inst : next_ev;
         if (L.next_chk < next_ev) next_ev = L.next_chk;
         if (next_snap < next_ev) next_ev = next_snap;
+
+        // ---- DIVERGED LANES (64-lane kernel): when the ready
+        // lanes sit at different pcs, every one of them on unmodified golden
+        // text executes its own pre-decoded micro-op -- per-lane entry,
+        // registers, TLB and pages, a divergent switch over the ~30 kinds --
+        // instead of one pc group at a time.  A lane stops at anything else
+        // (K_SLOW ops, faults, misses lookup_full cannot resolve, copy-on-write,
+        // stores into the code range, page-crossing accesses, odd pcs, its next
+        // instruction-count event, a watched register or an armed result fault,
+        // an LR/SC lock record) and the group machinery below serves it.  The
+        // step loop runs while at least half of the lanes it started with
+        // commit.  Same counters as the fast path, per lane.
+        if constexpr (kNL > 1) {
+            if (CX->simt_min && !CX->record && CX->pre_ok && wait_min != kNone) {
+                const uint64_t lim = (ready && L.watch <= 0 && L.injected != 3 && m.lock == kNone && next_ev > L.ninst)
+                                         ? next_ev - L.ninst : 0;
+                bool run = lim != 0;
+                const uint32_t n0 = (uint32_t)__popcll(wballot<kNL>(run));
+                if (n0 >= CX->simt_min) {
+                    uint64_t pc = L.pc;
+                    uint32_t lst = 0, lxt = 0, lfb = 0, ldb = 0;   // per lane: insts, straddles, fetch/data bytes
+                    uint32_t wst = 0, nex = 0;                     // wave steps, lane-instructions
+                    const uint32_t wbud = uni32(CX->wave_budget ? CX->wave_budget - n_iter : (1u << 30));
+                    const uint64_t tlo = CX->text_lo, clo = CX->code_lo, chi = CX->code_hi;
+                    const uint32_t tby = CX->text_bytes;
+                    const uint4 *const pre4 = (const uint4 *)CX->pre;
+                    for (;;) {
+                        const uint64_t toff = pc - tlo;
+                        bool go = run && toff < tby && !(pc & 1) && !dirty_at(m, pc);
+                        uint4 e = make_uint4(0u, 0u, 0u, 0u);
+                        if (go) e = pre4[toff >> 1];
+                        const uint32_t aux = e.w >> 16, kind = aux & 63, pf = (e.w >> 8) & 0xFF;
+                        go = go && (pf & kPreValid) && kind != K_SLOW;
+                        const uint32_t rd = (e.y >> 8) & 0xFF, rs1 = (e.y >> 16) & 0xFF, rs2 = e.y >> 24;
+                        const int64_t imm = (int32_t)e.z;
+                        const uint32_t len = e.w & 0xFF;
+                        const uint64_t ft = pc + len;
+                        uint64_t v = 0, npc = ft;
+                        uint32_t msz = 0;
+                        bool wr = true;
+                        if (go) {
+                            const uint64_t a0 = RREG(rs1), b0 = RREG(rs2);
+                            const uint64_t av = (aux & U_APC) ? pc : a0;
+                            const uint64_t bv = (aux & U_BIMM) ? (uint64_t)imm : b0;
+                            const bool w32 = aux & U_W32;
+                            const uint32_t shm = w32 ? 31 : 63;
+                            switch (kind) {
+                            case K_ADD: v = av + bv; break;
+                            case K_SUB: v = av - bv; break;
+                            case K_AND: v = av & bv; break;
+                            case K_OR: v = av | bv; break;
+                            case K_XOR: v = av ^ bv; break;
+                            case K_SLT: v = (int64_t)av < (int64_t)bv ? 1 : 0; break;
+                            case K_SLTU: v = av < bv ? 1 : 0; break;
+                            case K_SLL: v = av << (bv & shm); break;
+                            case K_SRL: v = (w32 ? (av & 0xFFFFFFFFULL) : av) >> (bv & shm); break;
+                            case K_SRA: v = (uint64_t)((w32 ? (int64_t)(int32_t)av : (int64_t)av) >> (bv & shm)); break;
+                            case K_MUL: v = av * bv; break;
+                            case K_MULH: v = (uint64_t)__mul64hi((int64_t)av, (int64_t)bv); break;
+                            case K_MULHU: v = __umul64hi(av, bv); break;
+                            case K_MULHSU: v = __umul64hi(av, bv) - (((int64_t)av < 0) ? bv : 0); break;
+                            case K_DIV: v = w32 ? divw(av, bv) : div64(av, bv); break;
+                            case K_DIVU:
+                                v = w32 ? ((uint32_t)bv == 0 ? ~0ULL : sx32((uint32_t)av / (uint32_t)bv))
+                                        : (bv == 0 ? ~0ULL : av / bv);
+                                break;
+                            case K_REM: v = w32 ? remw(av, bv) : rem64(av, bv); break;
+                            case K_REMU:
+                                v = w32 ? ((uint32_t)bv == 0 ? sx32(av) : sx32((uint32_t)av % (uint32_t)bv))
+                                        : (bv == 0 ? av : av % bv);
+                                break;
+                            case K_NOP: wr = false; break;
+                            case K_JAL: v = ft; npc = pc + imm; break;
+                            case K_JALR: v = ft; npc = (a0 + imm) & ~1ULL; break;
+                            case K_BEQ: wr = false; npc = a0 == b0 ? pc + imm : ft; break;
+                            case K_BNE: wr = false; npc = a0 != b0 ? pc + imm : ft; break;
+                            case K_BLT: wr = false; npc = (int64_t)a0 < (int64_t)b0 ? pc + imm : ft; break;
+                            case K_BGE: wr = false; npc = (int64_t)a0 >= (int64_t)b0 ? pc + imm : ft; break;
+                            case K_BLTU: wr = false; npc = a0 < b0 ? pc + imm : ft; break;
+                            case K_BGEU: wr = false; npc = a0 >= b0 ? pc + imm : ft; break;
+                            default: {   // K_LOAD / K_STORE inside one mapped page
+                                const bool st = kind == K_STORE;
+                                msz = 1u << ((aux >> 12) & 3);
+                                const uint64_t ea = a0 + imm;
+                                const uint32_t off = (uint32_t)(ea & 4095);
+                                uint64_t p = tlb_find(m, ea >> 12);
+                                if (!p) p = lookup_full(CX, w, m, slot, ea >> 12);
+                                const bool code_st = st && !(ea >= chi || ea + msz <= clo);
+                                if (!(p && (!st || ((p & 1) && !code_st)) && off + msz <= 4096)) { go = false; break; }
+                                uint8_t *pg = const_cast<uint8_t *>(page_of(p));
+                                const bool al = (off & (msz - 1)) == 0;
+                                if (st) {
+                                    wr = false;
+                                    if (al) {
+                                        switch (msz) {
+                                        case 1: pg[off] = (uint8_t)b0; break;
+                                        case 2: *(uint16_t *)(pg + off) = (uint16_t)b0; break;
+                                        case 4: *(uint32_t *)(pg + off) = (uint32_t)b0; break;
+                                        default: *(uint64_t *)(pg + off) = b0; break;
+                                        }
+                                    } else {
+                                        for (uint32_t i = 0; i < msz; i++) pg[off + i] = (uint8_t)(b0 >> (8 * i));
+                                    }
+                                } else {
+                                    uint64_t t = 0;
+                                    if (al) {
+                                        switch (msz) {
+                                        case 1: t = pg[off]; break;
+                                        case 2: t = *(const uint16_t *)(pg + off); break;
+                                        case 4: t = *(const uint32_t *)(pg + off); break;
+                                        default: t = *(const uint64_t *)(pg + off); break;
+                                        }
+                                    } else {
+                                        for (uint32_t i = 0; i < msz; i++) t |= (uint64_t)pg[off + i] << (8 * i);
+                                    }
+                                    v = (aux & U_SEXT) ? (uint64_t)sext64(t, 8 * msz) : t;
+                                }
+                                break;
+                            }
+                            }
+                            if (go) {
+                                if (w32) v = sx32(v);
+                                RREG((wr && rd) ? rd : kSinkRow) = v;
+                                pc = npc;
+                                lst++; lxt += (pf & kPreStraddle) ? 1 : 0; lfb += len; ldb += msz;
+                            }
+                        }
+                        run = go && lst < lim;   // a lane that stopped stays stopped in this loop
+                        const uint32_t na = (uint32_t)__popcll(wballot<kNL>(go));
+                        wst++;
+                        nex += na;
+                        if (2 * na < n0 || wballot<kNL>(run) == 0 || wst >= wbud) break;
+                    }
+                    if (lst) { L.pc = pc; L.ninst += lst; L.ncyc += lst + lxt; L.fetch_b += lfb; L.data_b += ldb; }
+                    n_iter += wst;
+                    n_exec += nex;
+                    n_simt += nex;
+                    if (nex) continue;
+                }
+            }
+        }
 
 #ifdef FI_TX
         // ---- TRANSLATED PATH (load-time build only): the golden run's basic
@@ -2168,7 +2310,7 @@ __device__ __forceinline__ void trial_body() {
     }
 #ifdef FI_PROF
     if (lane == 0)
-        for (int k = 0; k < 8; k++) atomicAdd(&CX->stats[24 + k], (unsigned long long)pacc[k]);
+        for (int k = 0; k < 8; k++) atomicAdd(&CX->stats[32 + k], (unsigned long long)pacc[k]);
 #endif
     if (lane == 0 && CX->wave_dbg) {
         uint64_t *wd = CX->wave_dbg + 4 * (uint64_t)blockIdx.x;
@@ -2200,6 +2342,7 @@ __device__ __forceinline__ void trial_body() {
         atomicAdd(&CX->stats[14], (unsigned long long)si);
         atomicAdd(&CX->stats[16], (unsigned long long)n_tx);
         atomicAdd(&CX->stats[17], (unsigned long long)n_txin);
+        atomicAdd(&CX->stats[24], (unsigned long long)n_simt);
         // the slowest wave: iterations, translated permille, entries (packed)
         atomicMax(&CX->stats[18], ((unsigned long long)n_iter << 32) |
                                       ((unsigned long long)(n_iter ? (uint64_t)n_tx * 1000 / n_iter : 0) << 20) |
@@ -2212,6 +2355,7 @@ __device__ __forceinline__ void trial_body() {
 #undef n_early
 #undef n_tx
 #undef n_txin
+#undef n_simt
     }
 }
 

@@ -102,6 +102,7 @@ CFG_PACK_RUNS = 16
 CFG_FIXED_RESUME = 32
 CFG_NO_SOLO = 64
 CFG_SOLO_ALL = 128
+CFG_SIMT = 256
 
 
 class GoldenInfo(C.Structure):
@@ -307,7 +308,7 @@ class Engine:
         return self.L.fi_last_kernel_ms(self.h)
 
     def debug_stats(self) -> np.ndarray:
-        out = np.zeros(32, np.uint64)
+        out = np.zeros(40, np.uint64)
         self._chk(self.L.fi_debug_stats(self.h, out.ctypes.data), "fi_debug_stats")
         return out
 

@@ -204,6 +204,8 @@ PATH_FLAGS = {
     "no_solo": 64,                          # FI_CFG_NO_SOLO: resumed epochs on the 64-lane kernel
     "solo_all": 128,                        # FI_CFG_SOLO_ALL: every epoch on the one-trial-per-wave kernel
     "solo_all_interp": 128 | 4,             # the solo build without translated blocks
+    "simt": 256,                            # FI_CFG_SIMT: diverged lanes step together, per lane
+    "simt_no_solo_interp": 256 | 64 | 4,    # the step loop for every epoch, no translated blocks
 }
 _PATH_REF = {}
 

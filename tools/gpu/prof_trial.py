@@ -26,4 +26,4 @@ for i in ids:
     it = max(1, int(st[6]))
     print(json.dumps({"trial": i, "cls": int(out["cls"][0]), "kernel_ms": round(ms, 3), "iters": it,
                       "slow": int(st[8]), "ns_per_iter": round(ms * 1e6 / it, 1),
-                      "cycles_per_iter_by_stamp": [round(int(st[24 + k]) / it, 1) for k in range(8)]}), flush=True)
+                      "cycles_per_iter_by_stamp": [round(int(st[32 + k]) / it, 1) for k in range(8)]}), flush=True)
