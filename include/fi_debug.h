@@ -17,6 +17,11 @@ fi_status fi_debug_decode(fi_engine *e, const uint32_t *raws, uint64_t n, void *
  * reductions, snapshot comparisons and early exits, translated instructions
  * and entries, the slowest wave, wave-0 clock; [24..27] -DFI_PROF builds only. */
 fi_status fi_debug_stats(fi_engine *e, uint64_t *out40);
+/* The engine's IEEE arithmetic port (shrewd_amd/csrc/hip/fi_softfp.h) over
+ * operand vectors, on the host (on_device = 0) or the device: op / fmt codes of
+ * fi::sf::op; out = result bits, fl = fflags raised. */
+fi_status fi_debug_softfp(int op, int fmt, int rm, const uint64_t *a, const uint64_t *b, const uint64_t *c,
+                          uint64_t n, uint64_t *out, uint32_t *fl, int on_device);
 /* Per wave of the last launch: {s_memtime cycles, loop iterations,
  * translated instructions, slow fetches} (4 x u64 each). */
 fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves);

@@ -62,6 +62,8 @@ def lib():
         L.or_mnemonic.argtypes = [C.c_uint32]
         L.or_sys_class.argtypes = [C.c_int]
         L.or_set_protect_opclasses.argtypes = [C.c_void_p, C.c_uint64]
+        L.or_sf_ref.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -146,3 +148,19 @@ def mnemonic(inst: int) -> str:
 
 def sys_class(num: int) -> int:
     return lib().or_sys_class(num)
+
+
+def has_softfloat() -> bool:
+    """The reference SoftFloat (oracle/_ref) is linked: F/D/Zfh arithmetic executes."""
+    return bool(lib().or_has_softfloat())
+
+
+def sf_ref(op: int, fmt: int, rm: int, a, b=None, c=None):
+    """The reference SoftFloat over operand vectors -> (result bits, flags)."""
+    a = np.ascontiguousarray(a, np.uint64)
+    b = np.ascontiguousarray(a if b is None else b, np.uint64)
+    c = np.ascontiguousarray(a if c is None else c, np.uint64)
+    out = np.zeros(len(a), np.uint64)
+    fl = np.zeros(len(a), np.uint32)
+    lib().or_sf_ref(op, fmt, rm, a.ctypes.data, b.ctypes.data, c.ctypes.data, len(a), out.ctypes.data, fl.ctypes.data)
+    return out, fl

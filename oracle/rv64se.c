@@ -14,9 +14,84 @@
 #include "../shrewd_amd/csrc/gem5_opclass_table.h"
 
 #include <pthread.h>
+#include <stdbool.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+/* ------------------------------------------------------------- SoftFloat */
+/* F/D/Zfh arithmetic is the reference's own SoftFloat (gem5 ext/softfloat,
+ * RISC-V specialization), compiled from its sources into oracle/_ref by
+ * oracle/softfloat_ref.mk and linked when present (OR_SOFTFLOAT).  The
+ * prototypes below restate its C interface (ext/softfloat/softfloat.h): each
+ * floatN_t is a struct of one uintN_t, the rounding mode and the exception
+ * flags are per-thread globals. */
+#ifdef OR_SOFTFLOAT
+typedef struct { uint16_t v; } sf16_t;
+typedef struct { uint32_t v; } sf32_t;
+typedef struct { uint64_t v; } sf64_t;
+extern __thread uint_fast8_t softfloat_roundingMode, softfloat_exceptionFlags;
+#define SF_DECL(T, p)                                                                                         \
+    T p##_add(T, T); T p##_sub(T, T); T p##_mul(T, T); T p##_div(T, T); T p##_sqrt(T); T p##_mulAdd(T, T, T); \
+    bool p##_eq(T, T); bool p##_lt(T, T); bool p##_le(T, T); bool p##_lt_quiet(T, T); bool p##_le_quiet(T, T); \
+    int_fast32_t p##_to_i32(T, uint_fast8_t, bool); uint_fast32_t p##_to_ui32(T, uint_fast8_t, bool);        \
+    int_fast64_t p##_to_i64(T, uint_fast8_t, bool); uint_fast64_t p##_to_ui64(T, uint_fast8_t, bool);        \
+    T i32_to_##p(int32_t); T ui32_to_##p(uint32_t); T i64_to_##p(int64_t); T ui64_to_##p(uint64_t);
+SF_DECL(sf16_t, f16)
+SF_DECL(sf32_t, f32)
+SF_DECL(sf64_t, f64)
+sf32_t f16_to_f32(sf16_t); sf64_t f16_to_f64(sf16_t); sf16_t f32_to_f16(sf32_t); sf64_t f32_to_f64(sf32_t);
+sf16_t f64_to_f16(sf64_t); sf32_t f64_to_f32(sf64_t);
+
+/* one operation by code (the op / fmt codes of shrewd_amd/csrc/hip/fi_softfp.h) */
+#define SF_OPS(T, p, W)                                                                                        \
+    static u64 sf_##p(int op, int rm, u64 a, u64 b, u64 c) {                                                   \
+        T x = {(W)a}, y = {(W)b}, z = {(W)c};                                                                   \
+        switch (op) {                                                                                          \
+        case 0: return p##_add(x, y).v; case 1: return p##_sub(x, y).v; case 2: return p##_mul(x, y).v;        \
+        case 3: return p##_div(x, y).v; case 4: return p##_sqrt(x).v; case 5: return p##_mulAdd(x, y, z).v;    \
+        case 6: return p##_eq(x, y); case 7: return p##_lt(x, y); case 8: return p##_le(x, y);                 \
+        case 9: return p##_lt_quiet(x, y); case 10: return p##_le_quiet(x, y);                                  \
+        case 11: return (u64)(s64)p##_to_i32(x, rm, true); case 12: return (u64)p##_to_ui32(x, rm, true);      \
+        case 13: return (u64)p##_to_i64(x, rm, true); case 14: return (u64)p##_to_ui64(x, rm, true);           \
+        case 15: return i32_to_##p((int32_t)a).v; case 16: return ui32_to_##p((uint32_t)a).v;                  \
+        case 17: return i64_to_##p((int64_t)a).v; case 18: return ui64_to_##p(a).v;                           \
+        default: return 0;                                                                                     \
+        }                                                                                                      \
+    }
+typedef uint64_t u64;
+typedef int64_t s64;
+SF_OPS(sf16_t, f16, uint16_t)
+SF_OPS(sf32_t, f32, uint32_t)
+SF_OPS(sf64_t, f64, uint64_t)
+static u64 sf_ref(int op, int fmt, int rm, u64 a, u64 b, u64 c, uint32_t *fl) {
+    softfloat_roundingMode = (uint_fast8_t)rm;
+    softfloat_exceptionFlags = 0;
+    u64 r;
+    if (op >= 19) {   /* conversions between formats */
+        const int to = op - 19;
+        if (fmt == to) r = a;
+        else if (fmt == 0) r = to == 1 ? f16_to_f32((sf16_t){(uint16_t)a}).v : f16_to_f64((sf16_t){(uint16_t)a}).v;
+        else if (fmt == 1) r = to == 0 ? f32_to_f16((sf32_t){(uint32_t)a}).v : f32_to_f64((sf32_t){(uint32_t)a}).v;
+        else r = to == 0 ? f64_to_f16((sf64_t){a}).v : f64_to_f32((sf64_t){a}).v;
+    } else {
+        r = fmt == 0 ? sf_f16(op, rm, a, b, c) : fmt == 1 ? sf_f32(op, rm, a, b, c) : sf_f64(op, rm, a, b, c);
+    }
+    *fl = softfloat_exceptionFlags;
+    return r;
+}
+int or_has_softfloat(void) { return 1; }
+void or_sf_ref(int op, int fmt, int rm, const uint64_t *a, const uint64_t *b, const uint64_t *c, uint64_t n,
+               uint64_t *out, uint32_t *fl) {
+    for (uint64_t i = 0; i < n; i++) out[i] = sf_ref(op, fmt, rm, a[i], b[i], c[i], &fl[i]);
+}
+#else
+int or_has_softfloat(void) { return 0; }
+void or_sf_ref(int op, int fmt, int rm, const uint64_t *a, const uint64_t *b, const uint64_t *c, uint64_t n,
+               uint64_t *out, uint32_t *fl) {
+    (void)op; (void)fmt; (void)rm; (void)a; (void)b; (void)c; (void)n; (void)out; (void)fl;
+}
+#endif
 
 #define PAGE 4096ULL
 #define OR_NONE (~0ULL)

@@ -127,6 +127,12 @@ int or_probe(uint32_t inst, uint64_t pc, const uint64_t regs[32], or_probe_t *ou
 const char *or_mnemonic(uint32_t inst);
 /* syscall classification (0 absent,1 unimpl,2 ignore,3 escape,4 modelled) */
 int or_sys_class(int num);
+/* SoftFloat (oracle/_ref) present: F/D/Zfh arithmetic executes */
+int or_has_softfloat(void);
+/* the reference SoftFloat over operand vectors (op / fmt codes of
+ * shrewd_amd/csrc/hip/fi_softfp.h): the pinning tests' expected values */
+void or_sf_ref(int op, int fmt, int rm, const uint64_t *a, const uint64_t *b, const uint64_t *c, uint64_t n,
+               uint64_t *out, uint32_t *fl);
 
 #ifdef __cplusplus
 }

@@ -13,6 +13,7 @@
 #include "fi_types.h"
 #include "fi_device.h"
 #include "rv64_isa.h"
+#include "fi_softfp.h"
 
 namespace fi {
 
@@ -246,3 +247,50 @@ hipError_t sort_pairs(void *tmp, size_t bytes, const uint64_t *kin, uint64_t *ko
 }
 
 }  // namespace fi
+
+// ------------------------------------------------------------------ FP port
+// The engine's IEEE arithmetic (fi_softfp.h) run on vectors of operands, on
+// the host or on the device, for the pinning tests against the reference's
+// SoftFloat (tests/test_softfp.py).
+namespace fi {
+__global__ void softfp_kernel(int op, int fmt, int rm, const uint64_t *a, const uint64_t *b, const uint64_t *c,
+                              uint64_t n, uint64_t *out, uint32_t *fl) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t f = 0;
+    out[i] = sf::op(op, fmt, rm, a[i], b[i], c[i], f);
+    fl[i] = f;
+}
+}  // namespace fi
+
+extern "C" fi_status fi_debug_softfp(int op, int fmt, int rm, const uint64_t *a, const uint64_t *b,
+                                     const uint64_t *c, uint64_t n, uint64_t *out, uint32_t *fl, int on_device) {
+    if (op < 0 || op >= fi::sf::OP_COUNT || fmt < 0 || fmt > 2 || rm < 0 || rm > 4 || !a || !b || !c || !out || !fl)
+        return FI_E_ARG;
+    if (!on_device) {
+        for (uint64_t i = 0; i < n; i++) {
+            uint32_t f = 0;
+            out[i] = fi::sf::op(op, fmt, rm, a[i], b[i], c[i], f);
+            fl[i] = f;
+        }
+        return FI_OK;
+    }
+    if (!n) return FI_OK;
+    uint64_t *d = nullptr;
+    if (hipMalloc(&d, n * 8 * 4 + n * 4) != hipSuccess) return FI_E_HIP;
+    uint64_t *da = d, *db = d + n, *dc = d + 2 * n, *dout = d + 3 * n;
+    uint32_t *dfl = (uint32_t *)(d + 4 * n);
+    hipError_t err = hipMemcpy(da, a, n * 8, hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(db, b, n * 8, hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(dc, c, n * 8, hipMemcpyHostToDevice);
+    if (err == hipSuccess) {
+        hipLaunchKernelGGL(fi::softfp_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, op, fmt, rm, da, db,
+                           dc, n, dout, dfl);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess) err = hipDeviceSynchronize();
+    if (err == hipSuccess) err = hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(fl, dfl, n * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return err == hipSuccess ? FI_OK : FI_E_HIP;
+}

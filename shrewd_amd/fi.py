@@ -154,6 +154,7 @@ def lib():
         L.fi_kernel_timer_reset.argtypes = [vp]
         L.fi_get_config.argtypes = [vp, C.POINTER(_Config)]
         L.fi_debug_stats.argtypes = [vp, vp]
+        L.fi_debug_softfp.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, vp, C.c_uint64, vp, vp, C.c_int]
         L.fi_kernel_timer_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
         L.fi_debug_waves.argtypes = [vp, vp, C.c_uint64]
         L.fi_debug_epochs.argtypes = [vp, vp]
@@ -428,3 +429,18 @@ class FaultCampaign:
                 "escape_sub": {ESCAPE_NAMES.get(i, str(i)): int(h["escape_sub"][i]) for i in range(8)
                                if h["escape_sub"][i]},
                 "guest_insts": int(h["guest_insts"])}
+
+
+def softfp(op: int, fmt: int, rm: int, a, b=None, c=None, device: bool = False):
+    """The engine's IEEE arithmetic port (csrc/hip/fi_softfp.h) over operand
+    vectors, run on the host or on the device -> (result bits, flags)."""
+    a = np.ascontiguousarray(a, np.uint64)
+    b = np.ascontiguousarray(a if b is None else b, np.uint64)
+    c = np.ascontiguousarray(a if c is None else c, np.uint64)
+    out = np.zeros(len(a), np.uint64)
+    fl = np.zeros(len(a), np.uint32)
+    st = lib().fi_debug_softfp(op, fmt, rm, a.ctypes.data, b.ctypes.data, c.ctypes.data, len(a), out.ctypes.data,
+                               fl.ctypes.data, 1 if device else 0)
+    if st != FI_OK:
+        raise EngineError(f"fi_debug_softfp failed ({st})")
+    return out, fl

@@ -1,0 +1,47 @@
+"""The north-star campaign on one GPU: >= 1M seeded single-bit register/PC
+trials of the intmix (C3) workload, timed end to end, with a seeded sample of
+10k trials re-run on the CPU oracle and compared bit for bit.
+
+python tools/gpu/north_star.py [N] [SEED] [CHECK]  -> one JSON line"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+from shrewd_amd import Engine  # noqa: E402
+
+REGS_PC = ((1 << 32) - 2) | (1 << 32)
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+SEED = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0x5EED0003
+CHECK = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000
+name = "intmix"
+elf = open(os.path.join(ROOT, "workloads", f"{name}.elf"), "rb").read()
+e = Engine(max_trials_per_launch=100_000)
+e.load_elf(elf, [name])
+g = e.golden_run()
+e.set_campaign(SEED, REGS_PC, 1)
+e.run_trials(0, 100_000, want_outcomes=False)   # warm-up (load-time translation, buffers)
+t0 = time.perf_counter()
+out, h = e.run_trials(0, N)
+wall = time.perf_counter() - t0
+cls = np.bincount(out["cls"], minlength=6).tolist()
+rec = {"workload": name, "trials": N, "seed": hex(SEED), "golden_ninst": int(g.ninst), "wall_s": round(wall, 3),
+       "trials_per_s": round(N / wall), "classes": cls, "device_insts": int(h["device_insts"]),
+       "guest_insts_gem5_equiv": int(out["ninst"].astype(np.uint64).sum())}
+print(json.dumps(rec), flush=True)
+# oracle check on a seeded sample (checker only)
+from oracle.pyoracle import Oracle  # noqa: E402
+rng = np.random.default_rng(SEED)
+idx = np.sort(rng.choice(N, size=min(CHECK, N), replace=False))
+sites = e.sample(0, N)[idx]
+o = Oracle(elf, name)
+o.run_golden()
+t1 = time.perf_counter()
+ref = o.run_trials(sites, threads=16)
+rec["oracle_check"] = {"checked": int(len(idx)), "mismatches": int((ref != out[idx]).sum()),
+                       "oracle_s": round(time.perf_counter() - t1, 2), "threads": 16}
+print(json.dumps(rec), flush=True)
+sys.exit(0 if rec["oracle_check"]["mismatches"] == 0 else 1)
