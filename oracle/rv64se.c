@@ -190,6 +190,7 @@ const char *or_error(or_campaign_t *c) { return c ? c->err : "null campaign"; }
 typedef struct {
     u64 x[32];
     u64 f[32];            /* FP registers (raw bits; zero at process start) */
+    u32 fflags, frm;      /* MISCREG_FFLAGS / MISCREG_FRM (zero at process start) */
     u64 pc, npc;
     u64 num_inst, num_cycles;
     /* decoder state machine, arch/riscv/decoder.cc:54-116 */
@@ -256,7 +257,9 @@ enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_E
     X(fclass_s) X(fclass_d) X(fclass_h) \
     X(amoadd_w) X(amoswap_w) X(amoxor_w) X(amoor_w) X(amoand_w) X(amomin_w) X(amomax_w) X(amominu_w) X(amomaxu_w) \
     X(amoadd_d) X(amoswap_d) X(amoxor_d) X(amoor_d) X(amoand_d) X(amomin_d) X(amomax_d) X(amominu_d) X(amomaxu_d) \
-    X(lr_w) X(sc_w) X(lr_d) X(sc_d)
+    X(lr_w) X(sc_w) X(lr_d) X(sc_d) \
+    X(fadd) X(fsub) X(fmul) X(fdiv) X(fsqrt) X(fmin) X(fmax) X(fmadd) X(fmsub) X(fnmsub) X(fnmadd) \
+    X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f)
 
 enum {
 #define X(n) OP_##n,
@@ -319,6 +322,76 @@ static void decode(u32 raw, dec_t *d) {
  * :1741-1763 fsh/fsw/fsd, :2067-2283 AMOs, :2896-2942 fsgnj*, :3500-3544
  * fmv.x.* / fclass.*, :3545-3548 fmv.w.x, :3593-3598 fmv.d.x, :3648-3652
  * fmv.h.x).  Everything else in those groups stays an escape. */
+#ifdef OR_SOFTFLOAT
+/* F/D/Zfh arithmetic (decoder.isa:2694-2810 FMADD group, 2811-3440 OP-FP):
+ * one op per operation, the format and operand details packed into imm as
+ * rm | fmt << 3 | sub << 5 | rs3 << 8 (fmt 0 binary16, 1 binary32, 2 binary64;
+ * sub: fmin/fmax 1 = the Zfa minimumNumber variant, flt/fle 1 = quiet (Zfa),
+ * fcvt to/from integer the kind w/wu/l/lu, fcvt between formats the source
+ * format).  Zfa's fli / fround / froundnx / fcvtmod stay escapes. */
+static int fp_fmt(u32 f) { return f == 0 ? 1 : f == 1 ? 2 : f == 2 ? 0 : -1; }
+static int refine_fp_arith(u32 raw, dec_t *d) {
+    u32 opc = bits(raw, 6, 2), f3 = bits(raw, 14, 12), f7 = bits(raw, 31, 25);
+    int rd = (int)bits(raw, 11, 7), rs1 = (int)bits(raw, 19, 15), rs2 = (int)bits(raw, 24, 20);
+    int fmt = fp_fmt(f7 & 3), op = -1, sub = 0;
+#define FP_SET(o, s_) do { op = (o); sub = (s_); } while (0)
+    if (opc >= 0x10 && opc <= 0x13) {
+        fmt = fp_fmt(bits(raw, 26, 25));
+        if (fmt < 0) return 0;
+        d->op = OP_fmadd + (int)(opc - 0x10);
+        d->frd = rd; d->frs1 = rs1; d->frs2 = rs2;
+        d->imm = f3 | ((u32)fmt << 3) | (bits(raw, 31, 27) << 8);
+        return 1;
+    }
+    if (opc != 0x14 || fmt < 0) return 0;
+    switch (f7 >> 2) {
+    case 0x00: op = OP_fadd; break;
+    case 0x01: op = OP_fsub; break;
+    case 0x02: op = OP_fmul; break;
+    case 0x03: op = OP_fdiv; break;
+    case 0x0b: op = OP_fsqrt; break;
+    case 0x05:   /* fmin / fmax / fminm / fmaxm (binary16: fminm at 3, fmaxm at 4) */
+        if (f3 == 0) FP_SET(OP_fmin, 0);
+        else if (f3 == 1) FP_SET(OP_fmax, 0);
+        else if (f3 == (fmt == 0 ? 3u : 2u)) FP_SET(OP_fmin, 1);
+        else if (f3 == (fmt == 0 ? 4u : 3u)) FP_SET(OP_fmax, 1);
+        else return 0;
+        break;
+    case 0x14:
+        if (f3 == 0) FP_SET(OP_fle, 0);
+        else if (f3 == 1) FP_SET(OP_flt, 0);
+        else if (f3 == 2) FP_SET(OP_feq, 0);
+        else if (f3 == 4) FP_SET(OP_fle, 1);
+        else if (f3 == 5) FP_SET(OP_flt, 1);
+        else return 0;
+        d->op = op; d->rd = rd; d->frs1 = rs1; d->frs2 = rs2;
+        d->imm = f3 | ((u32)fmt << 3) | ((u32)sub << 5);
+        return 1;
+    case 0x18:
+        if (rs2 > 3) return 0;
+        d->op = OP_fcvt_f2i; d->rd = rd; d->frs1 = rs1;
+        d->imm = f3 | ((u32)fmt << 3) | ((u32)rs2 << 5);
+        return 1;
+    case 0x1a:
+        if (rs2 > 3) return 0;
+        d->op = OP_fcvt_i2f; d->frd = rd; d->rs1 = rs1;
+        d->imm = f3 | ((u32)fmt << 3) | ((u32)rs2 << 5);
+        return 1;
+    case 0x08: {
+        const int src = fp_fmt((u32)rs2);
+        if (rs2 > 2 || src < 0 || src == fmt) return 0;
+        d->op = OP_fcvt_f2f; d->frd = rd; d->frs1 = rs1;
+        d->imm = f3 | ((u32)fmt << 3) | ((u32)src << 5);
+        return 1;
+    }
+    default: return 0;
+    }
+#undef FP_SET
+    d->op = op; d->frd = rd; d->frs1 = rs1; d->frs2 = rs2;
+    d->imm = f3 | ((u32)fmt << 3) | ((u32)sub << 5);
+    return 1;
+}
+#endif
 static void refine_fp_amo(u32 raw, dec_t *d) {
     u32 opc = bits(raw, 6, 2), f3 = bits(raw, 14, 12), f7 = bits(raw, 31, 25);
     int rd = (int)bits(raw, 11, 7), rs1 = (int)bits(raw, 19, 15), rs2 = (int)bits(raw, 24, 20);
@@ -347,6 +420,9 @@ static void refine_fp_amo(u32 raw, dec_t *d) {
         d->funct3 = bits(raw, 26, 25);   /* aq << 1 | rl: the macro-op's fence micro-ops */
         return;
     }
+#ifdef OR_SOFTFLOAT
+    if (refine_fp_arith(raw, d)) return;
+#endif
     if (opc != 0x14) return;
     if ((f7 == 0x10 || f7 == 0x11 || f7 == 0x12) && f3 <= 2) {
         d->op = (f7 == 0x10 ? OP_fsgnj_s : f7 == 0x11 ? OP_fsgnj_d : OP_fsgnj_h) + (int)f3;
@@ -683,6 +759,18 @@ const char *or_mnemonic(u32 inst) {
         static const char *cn[8] = {"?", "csrrw", "csrrs", "csrrc", "?", "csrrwi", "csrrsi", "csrrci"};
         return cn[d.funct3];
     }
+#ifdef OR_SOFTFLOAT
+    if (d.op >= OP_fadd && d.op <= OP_fcvt_f2f) {   /* gem5's per-format mnemonic */
+        static const char *fs[3] = {"h", "s", "d"}, *is[4] = {"w", "wu", "l", "lu"};
+        const int fmt = (int)((d.imm >> 3) & 3), sub = (int)((d.imm >> 5) & 7);
+        if (d.op == OP_fcvt_f2i) snprintf(buf, sizeof buf, "fcvt_%s_%s", is[sub], fs[fmt]);
+        else if (d.op == OP_fcvt_i2f) snprintf(buf, sizeof buf, "fcvt_%s_%s", fs[fmt], is[sub]);
+        else if (d.op == OP_fcvt_f2f) snprintf(buf, sizeof buf, "fcvt_%s_%s", fs[fmt], fs[sub]);
+        else snprintf(buf, sizeof buf, "%s%s_%s", op_names[d.op],
+                      !sub ? "" : (d.op == OP_fmin || d.op == OP_fmax) ? "m" : "q", fs[fmt]);
+        return buf;
+    }
+#endif
     const char *n = op_names[d.op];
     size_t l = strlen(n);
     if (l && n[l - 1] == '_') { snprintf(buf, sizeof buf, "%.*s", (int)(l - 1), n); return buf; }
@@ -1426,7 +1514,27 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
     case OP_jalr: v = m->npc; m->npc = (a + imm) & ~1ULL; break;
     case OP_jal: v = m->npc; m->npc = pc + imm; break;
     case OP_ecall: return F_SYSCALL;
-    case OP_csr: return csr_u_accessible(d->csr) ? F_ESCAPE + 100 : F_ILLEGAL;
+    case OP_csr:
+        if (d->csr >= 1 && d->csr <= 3) {
+            /* fflags / frm / fcsr (CSRExecute, formats/standard.isa:325-447; ISA::readCSR /
+             * writeCSR, isa.cc:1141-1300): csrrw(i) reads only if rd != 0, csrrs/c(i) write
+             * only if rs1 / uimm != 0; masks FFLAGS 0x1f, FRM 0x7 (regs/misc.hh) */
+            const u32 f3 = d->funct3;
+            const u64 src = f3 >= 5 ? (u64)d->imm : rdreg(m, d->rs1);
+            const int rdc = (f3 == 1 || f3 == 5) ? d->rd != 0 : 1;
+            const int wrc = (f3 == 1 || f3 == 5) ? 1 : (d->imm != 0);
+            u64 data = 0;
+            if (rdc) data = d->csr == 1 ? m->fflags : d->csr == 2 ? m->frm : (m->fflags | (m->frm << 5));
+            v = data;
+            const u64 nd = (f3 & 3) == 1 ? src : (f3 & 3) == 2 ? (data | src) : (data & ~src);
+            if (wrc) {
+                if (d->csr == 1) m->fflags = (u32)(nd & 0x1F);
+                else if (d->csr == 2) m->frm = (u32)(nd & 7);
+                else { m->fflags = (u32)(nd & 0x1F); m->frm = (u32)((nd >> 5) & 7); }
+            }
+            break;
+        }
+        return csr_u_accessible(d->csr) ? F_ESCAPE + 100 : F_ILLEGAL;
     /* ---- F/D/Zfh loads and stores (Load/Store formats, formats/mem.isa:123-207):
      * the access first, then the FPU-status update (never off in SE: fs is
      * INITIAL from ISA::resetThread, isa.cc:390); loads NaN-box (float.hh:104-107) */
@@ -1469,6 +1577,76 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
     case OP_fclass_s: v = fclassify(unbox32(m->f[d->frs1]), 8, 23); break;
     case OP_fclass_d: v = fclassify(m->f[d->frs1], 11, 52); break;
     case OP_fclass_h: v = fclassify(unbox16(m->f[d->frs1]), 5, 10); break;
+#ifdef OR_SOFTFLOAT
+    /* ---- F/D/Zfh arithmetic through the reference SoftFloat: FloatExecute
+     * (formats/fp.isa:34-56) ORs the raised flags into FFLAGS; RM_REQUIRED
+     * (fp_inst.hh:37-44) takes frm for the dynamic mode and faults on 5-7 */
+    case OP_fadd: case OP_fsub: case OP_fmul: case OP_fdiv: case OP_fsqrt: case OP_fmadd: case OP_fmsub:
+    case OP_fnmsub: case OP_fnmadd: case OP_fmin: case OP_fmax: case OP_feq: case OP_flt: case OP_fle:
+    case OP_fcvt_f2i: case OP_fcvt_i2f: case OP_fcvt_f2f: {
+        const int fmt = (int)((imm >> 3) & 3), sub = (int)((imm >> 5) & 7);
+        const u64 sgn = fmt == 0 ? 0x8000ULL : fmt == 1 ? 0x80000000ULL : 0x8000000000000000ULL;
+        const u64 qnan = fmt == 0 ? 0x7E00ULL : fmt == 1 ? 0x7FC00000ULL : 0x7FF8000000000000ULL;
+        const int rounds = !(d->op == OP_fmin || d->op == OP_fmax || d->op == OP_feq || d->op == OP_flt ||
+                             d->op == OP_fle);
+        if (d->op == OP_fsqrt && d->frs2 != 0) return F_ILLEGAL;   /* "source reg x1" */
+        int rm = (int)(imm & 7);
+        if (rounds) {
+            if (rm == 7) rm = (int)m->frm;
+            if (rm > 4) return F_ILLEGAL;                           /* "RM fault" */
+        }
+#define UNBOX(f_, x_) ((f_) == 0 ? unbox16(x_) : (f_) == 1 ? unbox32(x_) : (x_))
+#define BOX(f_, x_) ((f_) == 0 ? box16(x_) : (f_) == 1 ? box32(x_) : (x_))
+        uint32_t fl = 0, fl2 = 0;
+        const u64 x = d->frs1 >= 0 ? UNBOX(d->op == OP_fcvt_f2f ? sub : fmt, m->f[d->frs1]) : 0;
+        const u64 y = d->frs2 >= 0 ? UNBOX(fmt, m->f[d->frs2]) : 0;
+        const u64 z = UNBOX(fmt, m->f[(imm >> 8) & 31]);
+        int to_f = 1;
+        u64 r = 0;
+        switch (d->op) {
+        case OP_fadd: r = sf_ref(0, fmt, rm, x, y, 0, &fl); break;
+        case OP_fsub: r = sf_ref(1, fmt, rm, x, y, 0, &fl); break;
+        case OP_fmul: r = sf_ref(2, fmt, rm, x, y, 0, &fl); break;
+        case OP_fdiv: r = sf_ref(3, fmt, rm, x, y, 0, &fl); break;
+        case OP_fsqrt: r = sf_ref(4, fmt, rm, x, 0, 0, &fl); break;
+        case OP_fmadd: r = sf_ref(5, fmt, rm, x, y, z, &fl); break;                 /* decoder.isa:2694-2719 */
+        case OP_fmsub: r = sf_ref(5, fmt, rm, x, y, z ^ sgn, &fl); break;
+        case OP_fnmsub: r = sf_ref(5, fmt, rm, x ^ sgn, y, z, &fl); break;
+        case OP_fnmadd: r = sf_ref(5, fmt, rm, x ^ sgn, y, z ^ sgn, &fl); break;
+        case OP_fmin: case OP_fmax: {   /* decoder.isa:2944-3120: lt_quiet, then eq */
+            const int mx = d->op == OP_fmax;
+            const u64 p = mx ? y : x, q = mx ? x : y;   /* fmax compares (fs2, fs1) */
+            int pick = (int)sf_ref(9, fmt, rm, p, q, 0, &fl);
+            if (!pick) pick = (int)sf_ref(6, fmt, rm, p, q, 0, &fl2) && (p & sgn);
+            fl |= fl2;
+            const u64 inf = fmt == 0 ? 0x7C00ULL : fmt == 1 ? 0x7F800000ULL : 0x7FF0000000000000ULL;
+            const int nx = (x & ~sgn) > inf, ny = (y & ~sgn) > inf;
+            if (sub) {   /* fminm / fmaxm: a non-NaN result is written unboxed (Fd_bits = fs.v) */
+                if (!(nx || ny)) { m->fflags |= (fl | fl2) & 0x1F; m->f[d->frd] = pick ? x : y; goto no_rd; }
+                r = qnan;
+            } else {
+                r = (nx && ny) ? qnan : ((pick || ny) ? x : y);
+            }
+            break;
+        }
+        case OP_feq: v = sf_ref(6, fmt, rm, x, y, 0, &fl); to_f = 0; break;
+        case OP_flt: v = sf_ref(sub ? 9 : 7, fmt, rm, x, y, 0, &fl); to_f = 0; break;
+        case OP_fle: v = sf_ref(sub ? 10 : 8, fmt, rm, x, y, 0, &fl); to_f = 0; break;
+        case OP_fcvt_f2i:   /* decoder.isa:3273-3420: w/wu results sign-extended from 32 bits */
+            v = sf_ref(11 + sub, fmt, rm, x, 0, 0, &fl);
+            if (sub <= 1) v = sx32(v);
+            to_f = 0;
+            break;
+        case OP_fcvt_i2f: r = sf_ref(15 + sub, fmt, rm, a, 0, 0, &fl); break;
+        default: r = sf_ref(19 + fmt, sub, rm, x, 0, 0, &fl); break;   /* fcvt between formats */
+        }
+        m->fflags |= fl & 0x1F;
+        if (to_f) { m->f[d->frd] = BOX(fmt, r); goto no_rd; }
+#undef UNBOX
+#undef BOX
+        break;
+    }
+#endif
     /* ---- AMOs: AtomicSimpleCPU::amoMem (atomic.cc:546-608) panics on an
      * access that crosses a 64-byte line before translating; no alignment
      * check in SE (tlb.cc:573-604).  Rd = the old value (sign-extended .w). */
@@ -1818,6 +1996,7 @@ static void mach_init(mach_t *m, const or_campaign_t *c) {
     m->stack_min = c->stack_min0;
     m->watch = -1;
     m->resv = m->lock = OR_NONE;
+    m->fflags = m->frm = 0;
     m->vma[0].lo = c->stack_vma_lo; m->vma[0].hi = c->stack_vma_hi; m->nvma = 1;   /* argsInit's "stack" VMA */
     m->brk = c->brk0;
     m->mmap_end = 0x4000000000000000ULL;

@@ -466,7 +466,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_out, c * sizeof(fi_outcome)));
     HIPCHK(hipMalloc(&e->d_hist, sizeof(fi_histogram)));
     HIPCHK(hipMalloc(&e->d_stats, kNStats * sizeof(unsigned long long)));
-    HIPCHK(hipMalloc(&e->d_wave_dbg, c * 4 * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&e->d_wave_dbg, c * 10 * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&e->d_priv, c * e->cfg.private_pages * kPage));
     HIPCHK(hipMalloc(&e->d_priv_vpn, c * e->cfg.private_pages * 8));
     HIPCHK(hipMalloc(&e->d_save, c * sizeof(LaneSave)));
@@ -891,6 +891,7 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     c.save = e->d_save;
     HIPCHK(hipMemsetAsync(e->d_stats, 0, kNStats * sizeof(unsigned long long), st));
     HIPCHK(hipMemsetAsync(e->d_cnt, 0, 16 * 4, st));
+    HIPCHK(hipMemsetAsync(e->d_wave_dbg, 0, k * 10 * sizeof(uint64_t), st));
     const bool pack = (e->cfg.flags & FI_CFG_PACK_RUNS) != 0;
     int n_cu = 0;
     HIPCHK(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, e->dev));
@@ -1071,7 +1072,7 @@ fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves) {
     if (!e || !out) return FI_E_ARG;
     if (n_waves > e->cap) return fail(e, FI_E_ARG, "more waves than the work buffers hold");
     HIPCHK(hipStreamSynchronize(e->stream));
-    HIPCHK(hipMemcpy(out, e->d_wave_dbg, n_waves * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out, e->d_wave_dbg, n_waves * 10 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return FI_OK;
 }
 

@@ -64,7 +64,7 @@ struct LaneSave {
     uint32_t flags;                  // bit 0 out_bad, bits 1-2 injected, bit 3 code_dirty, bit 4 FP state,
                                      // bit 5 VM state (VmState of the slot is live)
     uint32_t dlo, dhi;               // rewritten code bytes [code_lo + dlo, code_lo + dhi) (if code_dirty)
-    uint32_t pad;
+    uint32_t pad;                    // fflags | frm << 5
     uint64_t resv, lock;             // LR/SC: load reservation and lock record (~0 = none)
 };
 
@@ -147,7 +147,9 @@ struct DevCtx {
     const uint32_t *perm;            // launch slot -> index into sites/out (sorted by site.inst)
     fi_outcome *out;
     uint64_t n;                      // trials in this launch
-    uint64_t *wave_dbg;              // per wave: {s_memtime cycles, loop iterations, translated insts, slow fetches}
+    uint64_t *wave_dbg;              // per wave: {s_memtime cycles, loop iterations, translated insts, slow fetches,
+                                     //            s_memrealtime at start, at end, lane 0's trial, its instructions,
+                                     //            translated entries, lane 0's full page lookups}
     // SE memory map: process-start brk and "stack" VMA; per-slot VM state
     uint64_t brk0, svma_lo, svma_hi;
     VmState *vm;                     // [n_slots]

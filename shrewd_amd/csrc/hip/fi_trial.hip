@@ -25,6 +25,7 @@
 #include "fi_device.h"
 #include "rv64_isa.h"
 #include "gem5_opclass_table.h"
+#include "fi_softfp.h"
 
 namespace fi {
 
@@ -139,6 +140,7 @@ struct LaneMem {
     // lock record stays on the general path, whose stores erase it.
     uint64_t resv, lock;
     bool vm;                       // VmState of the slot is live (the trial made a VM syscall)
+    uint32_t nmiss;                // diagnostics: full page-table lookups (TLB misses)
 };
 
 // The golden pre-decode of the instruction at pc is stale for this lane only if
@@ -210,6 +212,7 @@ __device__ __forceinline__ int64_t tab_find(const PageEnt *t, uint32_t n, uint64
 // kTomb, left by munmap / brk shrink) means unmapped.
 // Returns the page address | 1 for a private (writable) page, 0 if unmapped.
 __device__ uint64_t lookup_full(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, uint64_t vpn) {
+    m.nmiss++;
     uint64_t p = 0;
     bool dec = false;
     for (uint32_t i = m.n_priv; i-- > 0;) {
@@ -576,6 +579,7 @@ struct Lane {
     int watch;
     bool out_bad, done;
     bool fp;                      // FP registers materialised (else all zero, as at process start)
+    uint8_t fflags, frm;          // MISCREG_FFLAGS / MISCREG_FRM (zero at process start)
     uint8_t injected;             // 0 pending, 1 applied, 2 nothing to flip, 3 result fault armed
     fi_outcome res;
 };
@@ -638,6 +642,74 @@ __device__ __forceinline__ uint64_t amo_apply(int op, uint64_t mem, uint64_t src
     case 7: return src < mem ? src : mem;
     default: return src > mem ? src : mem;
     }
+}
+
+// F/D/Zfh arithmetic of one instruction (oracle/rv64se.c execute, FP cases):
+// FloatExecute (formats/fp.isa:34-56) with RM_REQUIRED (fp_inst.hh:37-44),
+// operands unboxed per format (float.hh), results boxed, except fminm/fmaxm's
+// non-NaN result, which gem5 writes unboxed.  Out of line: rare, and big.
+struct FpRes { uint64_t v; uint32_t fl, kind; };   // kind: 0 FP rd, 1 integer rd, 2 IllegalInst
+__device__ __noinline__ FpRes fp_exec(uint32_t op, uint32_t imm, uint32_t rs2, uint64_t r1, uint64_t r2, uint64_t r3,
+                                      uint64_t ia, uint32_t frm) {
+    namespace sf = fi::sf;
+    FpRes o;
+    o.v = 0; o.fl = 0; o.kind = 0;
+    const int fmt = (int)((imm >> 3) & 3), sub = (int)((imm >> 5) & 7);
+    const uint64_t sgn = fmt == 0 ? 0x8000ULL : fmt == 1 ? 0x80000000ULL : 0x8000000000000000ULL;
+    const uint64_t qnan = fmt == 0 ? 0x7E00ULL : fmt == 1 ? 0x7FC00000ULL : 0x7FF8000000000000ULL;
+    const uint64_t inf = fmt == 0 ? 0x7C00ULL : fmt == 1 ? 0x7F800000ULL : 0x7FF0000000000000ULL;
+    auto unbox = [](int f, uint64_t x) { return f == 0 ? fp_unbox16(x) : f == 1 ? fp_unbox32(x) : x; };
+    auto box = [](int f, uint64_t x) {
+        return f == 0 ? (0xFFFFFFFFFFFF0000ULL | x) : f == 1 ? (0xFFFFFFFF00000000ULL | x) : x;
+    };
+    const bool rounds = !(op == OP_fmin || op == OP_fmax || op == OP_feq || op == OP_flt || op == OP_fle);
+    if (op == OP_fsqrt && rs2 != 0) { o.kind = 2; return o; }   // "source reg x1"
+    int rm = (int)(imm & 7);
+    if (rounds) {
+        if (rm == 7) rm = (int)frm;
+        if (rm > 4) { o.kind = 2; return o; }                   // "RM fault"
+    }
+    const uint64_t x = unbox(op == OP_fcvt_f2f ? sub : fmt, r1), y = unbox(fmt, r2), z = unbox(fmt, r3);
+    uint32_t fl = 0;
+    uint64_t r = 0;
+    switch (op) {
+    case OP_fadd: r = sf::op(sf::OP_ADD, fmt, rm, x, y, 0, fl); break;
+    case OP_fsub: r = sf::op(sf::OP_SUB, fmt, rm, x, y, 0, fl); break;
+    case OP_fmul: r = sf::op(sf::OP_MUL, fmt, rm, x, y, 0, fl); break;
+    case OP_fdiv: r = sf::op(sf::OP_DIV, fmt, rm, x, y, 0, fl); break;
+    case OP_fsqrt: r = sf::op(sf::OP_SQRT, fmt, rm, x, 0, 0, fl); break;
+    case OP_fmadd: r = sf::op(sf::OP_FMA, fmt, rm, x, y, z, fl); break;
+    case OP_fmsub: r = sf::op(sf::OP_FMA, fmt, rm, x, y, z ^ sgn, fl); break;
+    case OP_fnmsub: r = sf::op(sf::OP_FMA, fmt, rm, x ^ sgn, y, z, fl); break;
+    case OP_fnmadd: r = sf::op(sf::OP_FMA, fmt, rm, x ^ sgn, y, z ^ sgn, fl); break;
+    case OP_fmin: case OP_fmax: {   // lt_quiet, then eq (decoder.isa:2944-3120)
+        const bool mx = op == OP_fmax;
+        const uint64_t p = mx ? y : x, q = mx ? x : y;
+        bool pick = sf::op(sf::OP_LTQ, fmt, rm, p, q, 0, fl) != 0;
+        if (!pick) pick = sf::op(sf::OP_EQ, fmt, rm, p, q, 0, fl) != 0 && (p & sgn);
+        const bool nx = (x & ~sgn) > inf, ny = (y & ~sgn) > inf;
+        if (sub) {
+            o.fl = fl;
+            o.v = (nx || ny) ? box(fmt, qnan) : (pick ? x : y);   // unboxed (Fd_bits = fs.v)
+            return o;
+        }
+        r = (nx && ny) ? qnan : ((pick || ny) ? x : y);
+        break;
+    }
+    case OP_feq: o.v = sf::op(sf::OP_EQ, fmt, rm, x, y, 0, fl); o.kind = 1; break;
+    case OP_flt: o.v = sf::op(sub ? sf::OP_LTQ : sf::OP_LT, fmt, rm, x, y, 0, fl); o.kind = 1; break;
+    case OP_fle: o.v = sf::op(sub ? sf::OP_LEQ : sf::OP_LE, fmt, rm, x, y, 0, fl); o.kind = 1; break;
+    case OP_fcvt_f2i:   // w / wu sign-extended from 32 bits (decoder.isa:3273-3420)
+        o.v = sf::op(sf::OP_TO_I32 + sub, fmt, rm, x, 0, 0, fl);
+        if (sub <= 1) o.v = sx32(o.v);
+        o.kind = 1;
+        break;
+    case OP_fcvt_i2f: r = sf::op(sf::OP_FROM_I32 + sub, fmt, rm, ia, 0, 0, fl); break;
+    default: r = sf::op(sf::OP_TO_H + fmt, sub, rm, x, 0, 0, fl); break;   // between formats
+    }
+    o.fl = fl;
+    if (o.kind == 0) o.v = box(fmt, r);
+    return o;
 }
 
 __device__ __forceinline__ void finish(Lane &L, int cls, int sub, int code, uint32_t detail) {
@@ -1091,6 +1163,7 @@ __device__ __forceinline__ void trial_body() {
     L.next_chk = kNone;
     L.nfail = 0;
     L.watch = -1; L.out_bad = false; L.fp = false; L.done = !live; L.injected = (CX->record || !live) ? 1 : 0;
+    L.fflags = L.frm = 0;
     L.res.cls = 0; L.res.sub = 0; L.res.exit_code = 0; L.res.flags = 0; L.res.detail = 0; L.res.ninst = 0;
     LaneMem m;
     m.stack_min = S0->stack_min;
@@ -1100,10 +1173,12 @@ __device__ __forceinline__ void trial_body() {
     m.dlo = m.dhi = 0;
     m.resv = m.lock = kNone;
     m.vm = false;
+    m.nmiss = 0;
     if (resume && live) {
         L.pc = SV->pc; L.ninst = SV->ninst; L.ncyc = SV->ncyc; L.out_pos = SV->out_pos; L.err_pos = SV->err_pos;
         L.next_chk = SV->next_chk; L.nfail = SV->nfail; L.watch = SV->watch;
         L.out_bad = SV->flags & 1; L.injected = (uint8_t)((SV->flags >> 1) & 3); L.fp = (SV->flags >> 4) & 1;
+        L.fflags = (uint8_t)(SV->pad & 0x1F); L.frm = (uint8_t)((SV->pad >> 5) & 7);
         m.stack_min = SV->stack_min; m.n_priv = SV->n_priv; m.code_dirty = (SV->flags >> 3) & 1;
         m.dlo = CX->code_lo + SV->dlo; m.dhi = CX->code_lo + SV->dhi;
         m.resv = SV->resv; m.lock = SV->lock;
@@ -1175,6 +1250,7 @@ __device__ __forceinline__ void trial_body() {
                 sv->flags = (L.out_bad ? 1u : 0u) | ((uint32_t)L.injected << 1) | (m.code_dirty ? 8u : 0u) |
                             (L.fp ? 16u : 0u) | (m.vm ? 32u : 0u);
                 sv->resv = m.resv; sv->lock = m.lock;
+                sv->pad = (uint32_t)L.fflags | ((uint32_t)L.frm << 5);
                 CX->surv[atomicAdd(CX->surv_n, 1u)] = (uint32_t)slot;
                 suspended = true;
                 L.done = true;
@@ -1961,6 +2037,7 @@ __device__ __forceinline__ void trial_body() {
         uint64_t sval = b;            // store data (an FP register for FP stores)
         uint64_t fval = 0;            // FP destination value
         uint32_t fbox = 0;            // FP destination: 0 none, 1 fval, 16/32/64 loaded (NaN-boxed) width
+        uint32_t fpst = 0;            // FP status update: 0x100 | flags raised, 0x200 | fflags | frm << 5 written
         uint32_t xticks = 0;          // extra micro-op ticks (AMO fences)
         int amo = -1;                 // AMO read-modify-write op (amo_apply), -1 none
         int llsc = 0;                 // 1 LR, 2 SC
@@ -2106,7 +2183,31 @@ __device__ __forceinline__ void trial_body() {
             case OP_jalr: v = npc; npc = (a + imm) & ~1ULL; break;
             case OP_jal: v = npc; npc = pc + imm; break;
             case OP_ecall: f = F_SYSCALL; break;
-            case OP_csr: f = csr_u_accessible(d.raw >> 20) ? F_ESCCSR : F_ILLEGAL; break;
+            case OP_csr: {
+                const uint32_t csr = d.raw >> 20;
+                if (csr >= 1 && csr <= 3) {
+                    // fflags / frm / fcsr (oracle/rv64se.c OP_csr; CSRExecute, formats/standard.isa:
+                    // 325-447; ISA::readCSR / writeCSR, isa.cc:1141-1300)
+                    const uint32_t f3 = (d.raw >> 12) & 7, idx = (uint32_t)d.imm;   // rs1 field / uimm
+                    const uint64_t src = f3 >= 5 ? (uint64_t)idx : a;
+                    const bool rdc = (f3 == 1 || f3 == 5) ? d.rd != 0 : true;
+                    const bool wrc = (f3 == 1 || f3 == 5) ? true : idx != 0;
+                    const uint64_t data = !rdc ? 0 : csr == 1 ? L.fflags : csr == 2 ? L.frm
+                                                                 : (uint64_t)(L.fflags | (L.frm << 5));
+                    v = data;
+                    const uint64_t nd = (f3 & 3) == 1 ? src : (f3 & 3) == 2 ? (data | src) : (data & ~src);
+                    if (wrc) {
+                        uint32_t nf = L.fflags, nr = L.frm;
+                        if (csr == 1) nf = (uint32_t)(nd & 0x1F);
+                        else if (csr == 2) nr = (uint32_t)(nd & 7);
+                        else { nf = (uint32_t)(nd & 0x1F); nr = (uint32_t)((nd >> 5) & 7); }
+                        fpst = 0x200u | nf | (nr << 5);
+                    }
+                    break;
+                }
+                f = csr_u_accessible(csr) ? F_ESCCSR : F_ILLEGAL;
+                break;
+            }
             // ---- F/D/Zfh data movement: loads/stores through the single access
             // site below (access first, then the FPU-status update, which never
             // faults in SE: fs = INITIAL, isa.cc:390)
@@ -2143,6 +2244,18 @@ __device__ __forceinline__ void trial_body() {
             case OP_fclass_s: v = fp_classify(fp_unbox32(FREG_RD(d.rs1)), 8, 23); break;
             case OP_fclass_d: v = fp_classify(FREG_RD(d.rs1), 11, 52); break;
             case OP_fclass_h: v = fp_classify(fp_unbox16(FREG_RD(d.rs1)), 5, 10); break;
+            case OP_fadd: case OP_fsub: case OP_fmul: case OP_fdiv: case OP_fsqrt: case OP_fmadd: case OP_fmsub:
+            case OP_fnmsub: case OP_fnmadd: case OP_fmin: case OP_fmax: case OP_feq: case OP_flt: case OP_fle:
+            case OP_fcvt_f2i: case OP_fcvt_i2f: case OP_fcvt_f2f: {
+                const uint32_t ui = (uint32_t)d.imm;
+                const FpRes fr = fp_exec(d.op, ui, d.rs2, FREG_RD(d.rs1), FREG_RD(d.rs2), FREG_RD((ui >> 8) & 31), a,
+                                         L.frm);
+                if (fr.kind == 2) { f = F_ILLEGAL; break; }
+                fpst = 0x100u | fr.fl;
+                if (fr.kind == 1) v = fr.v;
+                else { fval = fr.v; fbox = 1; wrd = false; }
+                break;
+            }
             // ---- A-extension RMW: AtomicSimpleCPU::amoMem (atomic.cc:546-608)
             // panics on a 64-byte-line crossing before translating; one
             // translation, then read-modify-write; rl/aq fences are extra
@@ -2211,13 +2324,15 @@ __device__ __forceinline__ void trial_body() {
             tpos++;
         }
         if (f == F_NONE) {
-            if (fbox) {   // FP destination: materialise the lane's FP file on its first write
+            if (fbox || fpst) {   // FP state written: materialise the lane's FP file on its first write
                 if (!L.fp) {
                     for (int r = 0; r < 32; r++) CX->fregs[(uint64_t)r * CX->n_slots + slot] = 0;
                     L.fp = true;
                     if (CX->record) CX->stats[22] = 1;   // the golden run uses FP state (host disables snapshots)
                 }
-                CX->fregs[(uint64_t)d.rd * CX->n_slots + slot] = fval;
+                if (fbox) CX->fregs[(uint64_t)d.rd * CX->n_slots + slot] = fval;
+                if (fpst & 0x100u) L.fflags |= (uint8_t)(fpst & 0x1F);       // FFLAGS_EXE: accumulate
+                if (fpst & 0x200u) { L.fflags = (uint8_t)(fpst & 0x1F); L.frm = (uint8_t)((fpst >> 5) & 7); }
             }
             L.ncyc += xticks;
             bool rdet = false;
@@ -2313,11 +2428,17 @@ __device__ __forceinline__ void trial_body() {
         for (int k = 0; k < 8; k++) atomicAdd(&CX->stats[32 + k], (unsigned long long)pacc[k]);
 #endif
     if (lane == 0 && CX->wave_dbg) {
-        uint64_t *wd = CX->wave_dbg + 4 * (uint64_t)blockIdx.x;
+        uint64_t *wd = CX->wave_dbg + 10 * (uint64_t)blockIdx.x;
         wd[0] = __builtin_amdgcn_s_memtime() - t_start;
         wd[1] = n_iter;
         wd[2] = n_tx;
         wd[3] = n_slow;
+        wd[4] = rt_start;                                // s_memrealtime (100 MHz) at the wave's start / end
+        wd[5] = __builtin_amdgcn_s_memrealtime();
+        wd[6] = live ? (uint64_t)sidx : ~0ULL;           // lane 0's trial (index into the sites)
+        wd[7] = live ? L.ninst - launch_inst : 0;        // lane 0's instructions in this dispatch
+        wd[8] = n_txin;                                  // translated-code entries
+        wd[9] = m.nmiss;                                 // lane 0's full page-table lookups
     }
     if (blockIdx.x == 0 && lane == 0) {
         CX->stats[20] = __builtin_amdgcn_s_memtime() - t_start;

@@ -42,7 +42,9 @@
     X(fclass_s) X(fclass_d) X(fclass_h) \
     X(amoadd_w) X(amoswap_w) X(amoxor_w) X(amoor_w) X(amoand_w) X(amomin_w) X(amomax_w) X(amominu_w) X(amomaxu_w) \
     X(amoadd_d) X(amoswap_d) X(amoxor_d) X(amoor_d) X(amoand_d) X(amomin_d) X(amomax_d) X(amominu_d) X(amomaxu_d) \
-    X(lr_w) X(sc_w) X(lr_d) X(sc_d)
+    X(lr_w) X(sc_w) X(lr_d) X(sc_d) \
+    X(fadd) X(fsub) X(fmul) X(fdiv) X(fsqrt) X(fmin) X(fmax) X(fmadd) X(fmsub) X(fnmsub) X(fnmadd) \
+    X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f)
 
 namespace fi {
 
@@ -375,6 +377,74 @@ __device__ inline bool gem5_known(uint32_t raw) {
     return false;
 }
 
+// F/D/Zfh arithmetic (decoder.isa:2694-2810, 2811-3440), as in
+// oracle/rv64se.c:refine_fp_arith: one op per operation, imm = rm | fmt << 3 |
+// sub << 5 | rs3 << 8 (fmt 0 binary16, 1 binary32, 2 binary64).  FP register
+// fields plain, integer ones with their flags.  Returns false if the encoding
+// is not one of them (fli / fround / froundnx / fcvtmod stay escapes).
+__device__ inline int fp_fmt_code(uint32_t f) { return f == 0 ? 1 : f == 1 ? 2 : f == 2 ? 0 : -1; }
+__device__ inline bool rv_refine_fp_arith(uint32_t raw, Dec &d) {
+    const uint32_t opc = fbits(raw, 6, 2), f3 = fbits(raw, 14, 12), f7 = fbits(raw, 31, 25);
+    const uint32_t rd = fbits(raw, 11, 7), rs1 = fbits(raw, 19, 15), rs2 = fbits(raw, 24, 20);
+    if (opc >= 0x10 && opc <= 0x13) {
+        const int fmt = fp_fmt_code(fbits(raw, 26, 25));
+        if (fmt < 0) return false;
+        d.op = (uint8_t)(OP_fmadd + (opc - 0x10));
+        d.rd = (uint8_t)rd; d.rs1 = (uint8_t)rs1; d.rs2 = (uint8_t)rs2;
+        d.imm = (int32_t)(f3 | ((uint32_t)fmt << 3) | (fbits(raw, 31, 27) << 8));
+        return true;
+    }
+    const int fmt = fp_fmt_code(f7 & 3);
+    if (opc != 0x14 || fmt < 0) return false;
+    int op = -1;
+    uint32_t sub = 0;
+    switch (f7 >> 2) {
+    case 0x00: op = OP_fadd; break;
+    case 0x01: op = OP_fsub; break;
+    case 0x02: op = OP_fmul; break;
+    case 0x03: op = OP_fdiv; break;
+    case 0x0b: op = OP_fsqrt; break;
+    case 0x05:   // fmin / fmax / fminm / fmaxm (binary16: fminm at 3, fmaxm at 4)
+        if (f3 == 0) op = OP_fmin;
+        else if (f3 == 1) op = OP_fmax;
+        else if (f3 == (fmt == 0 ? 3u : 2u)) { op = OP_fmin; sub = 1; }
+        else if (f3 == (fmt == 0 ? 4u : 3u)) { op = OP_fmax; sub = 1; }
+        else return false;
+        break;
+    case 0x14:
+        if (f3 == 0) op = OP_fle;
+        else if (f3 == 1) op = OP_flt;
+        else if (f3 == 2) op = OP_feq;
+        else if (f3 == 4) { op = OP_fle; sub = 1; }
+        else if (f3 == 5) { op = OP_flt; sub = 1; }
+        else return false;
+        d.op = (uint8_t)op; D_RD(rd); d.rs1 = (uint8_t)rs1; d.rs2 = (uint8_t)rs2;
+        d.imm = (int32_t)(f3 | ((uint32_t)fmt << 3) | (sub << 5));
+        return true;
+    case 0x18:
+        if (rs2 > 3) return false;
+        d.op = OP_fcvt_f2i; D_RD(rd); d.rs1 = (uint8_t)rs1;
+        d.imm = (int32_t)(f3 | ((uint32_t)fmt << 3) | (rs2 << 5));
+        return true;
+    case 0x1a:
+        if (rs2 > 3) return false;
+        d.op = OP_fcvt_i2f; d.rd = (uint8_t)rd; D_RS1(rs1);
+        d.imm = (int32_t)(f3 | ((uint32_t)fmt << 3) | (rs2 << 5));
+        return true;
+    case 0x08: {
+        const int src = fp_fmt_code(rs2);
+        if (rs2 > 2 || src < 0 || src == fmt) return false;
+        d.op = OP_fcvt_f2f; d.rd = (uint8_t)rd; d.rs1 = (uint8_t)rs1;
+        d.imm = (int32_t)(f3 | ((uint32_t)fmt << 3) | ((uint32_t)src << 5));
+        return true;
+    }
+    default: return false;
+    }
+    d.op = (uint8_t)op; d.rd = (uint8_t)rd; d.rs1 = (uint8_t)rs1; d.rs2 = (uint8_t)rs2;
+    d.imm = (int32_t)(f3 | ((uint32_t)fmt << 3) | (sub << 5));
+    return true;
+}
+
 // The executed members of the LOAD-FP / STORE-FP / OP-FP / AMO groups among
 // the encodings gem5 knows (decoder.isa:567-591, :1741-1763, :2067-2283,
 // :2896-2942, :3500-3548, :3593-3598, :3648-3652).  FP register indices sit in
@@ -410,6 +480,7 @@ __device__ inline void rv_refine_fp_amo(uint32_t raw, Dec &d) {
         D_RD(rd); D_RS1(rs1); D_RS2(rs2); d.imm = 0;
         return;
     }
+    if (rv_refine_fp_arith(raw, d)) return;
     if (opc != 0x14) return;
     if ((f7 == 0x10 || f7 == 0x11 || f7 == 0x12) && f3 <= 2) {
         d.op = (uint8_t)((f7 == 0x10 ? OP_fsgnj_s : f7 == 0x11 ? OP_fsgnj_d : OP_fsgnj_h) + f3);

@@ -273,7 +273,7 @@ class Engine:
         return self.L.fi_translate_status(self.h).decode()
 
     def debug_waves(self, n_waves: int) -> np.ndarray:
-        out = np.zeros((n_waves, 4), np.uint64)
+        out = np.zeros((n_waves, 10), np.uint64)
         self._chk(self.L.fi_debug_waves(self.h, out.ctypes.data, n_waves), "fi_debug_waves")
         return out
 

@@ -1096,3 +1096,190 @@ def test_vm_program_on_oracle(oracle_mod):
     assert [hex(v) for v in vals] == [hex(v) for v in evals]
     assert got == exp
     assert o.golden_stderr() == VM_STDERR
+
+
+# F/D/Zfh arithmetic known answers.  Each case loads NaN-boxed operand bits
+# into f1..f3, runs one instruction with an explicit rounding mode (or the
+# dynamic one after csrrwi frm), stores the destination's raw 64 bits and the
+# fflags it raised (read-and-clear through csrrw fflags).  The expected values
+# come from the reference's own SoftFloat (oracle/_ref) through the same
+# operation codes the engine's port uses, with gem5's instruction-level rules
+# (NaN-boxing, sign injection of fmsub/fnmadd, w/wu sign extension).
+FP_BOX = {"h": 0xFFFFFFFFFFFF0000, "s": 0xFFFFFFFF00000000, "d": 0}
+FP_SIGN = {"h": 0x8000, "s": 0x80000000, "d": 1 << 63}
+FP_FMTC = {"h": 0, "s": 1, "d": 2}
+RMS = {"rne": 0, "rtz": 1, "rdn": 2, "rup": 3, "rmm": 4}
+
+
+def fp_cases():
+    one = {"h": 0x3C00, "s": 0x3F800000, "d": 0x3FF0000000000000}
+    three = {"h": 0x4200, "s": 0x40400000, "d": 0x4008000000000000}
+    tenth = {"h": 0x2E66, "s": 0x3DCCCCCD, "d": 0x3FB999999999999A}
+    big = {"h": 0x7BFF, "s": 0x7F7FFFFF, "d": 0x7FEFFFFFFFFFFFFF}
+    tiny = {"h": 0x0001, "s": 0x00000001, "d": 0x0000000000000001}
+    qnan = {"h": 0x7E00, "s": 0x7FC00000, "d": 0x7FF8000000000000}
+    snan = {"h": 0x7C01, "s": 0x7F800001, "d": 0x7FF0000000000001}
+    inf = {"h": 0x7C00, "s": 0x7F800000, "d": 0x7FF0000000000000}
+    c = []
+    for f in ("d", "s", "h"):
+        n = lambda k: k[f] | FP_SIGN[f]   # noqa: E731
+        for rm in ("rne", "rtz", "rdn", "rup", "rmm"):
+            c.append(("fdiv", f, rm, one[f], three[f], 0))
+            c.append(("fadd", f, rm, tenth[f], three[f], 0))
+        c += [("fadd", f, "rne", big[f], big[f], 0), ("fsub", f, "rdn", three[f], three[f], 0),
+              ("fmul", f, "rne", tiny[f], tenth[f], 0), ("fmul", f, "rup", tiny[f], tenth[f], 0),
+              ("fmul", f, "rne", inf[f], 0, 0), ("fdiv", f, "rne", one[f], 0, 0), ("fdiv", f, "rne", 0, 0, 0),
+              ("fsqrt", f, "rne", three[f], 0, 0), ("fsqrt", f, "rne", n(one), 0, 0),
+              ("fsqrt", f, "rtz", tenth[f], 0, 0), ("fadd", f, "rne", snan[f], one[f], 0),
+              ("fmadd", f, "rne", three[f], tenth[f], one[f]), ("fmsub", f, "rtz", three[f], tenth[f], one[f]),
+              ("fnmsub", f, "rdn", three[f], tenth[f], one[f]), ("fnmadd", f, "rup", three[f], tenth[f], one[f]),
+              ("fmadd", f, "rne", inf[f], 0, qnan[f]),
+              ("fmin", f, None, 0, n({f: 0}), 0), ("fmax", f, None, 0, n({f: 0}), 0),
+              ("fmin", f, None, qnan[f], one[f], 0), ("fmax", f, None, snan[f], one[f], 0),
+              ("fminm", f, None, qnan[f], one[f], 0), ("fmaxm", f, None, three[f], one[f], 0),
+              ("feq", f, None, qnan[f], one[f], 0), ("feq", f, None, snan[f], one[f], 0),
+              ("flt", f, None, qnan[f], one[f], 0), ("fltq", f, None, qnan[f], one[f], 0),
+              ("fle", f, None, one[f], one[f], 0), ("fleq", f, None, n(one), one[f], 0),
+              ("fcvt.w", f, "rtz", n(three), 0, 0), ("fcvt.wu", f, "rne", n(three), 0, 0),
+              ("fcvt.wu", f, "rne", three[f], 0, 0), ("fcvt.l", f, "rmm", tenth[f], 0, 0),
+              ("fcvt.lu", f, "rup", tenth[f], 0, 0), ("fcvt.w", f, "rne", big[f], 0, 0),
+              ("fcvt.w", f, "rne", qnan[f], 0, 0),
+              ("fcvt.from.w", f, "rne", 0xFFFFFFFF80000001, 0, 0), ("fcvt.from.wu", f, "rtz", 0xFFFFFFFF, 0, 0),
+              ("fcvt.from.l", f, "rdn", 0x7FFFFFFFFFFFFFFF, 0, 0), ("fcvt.from.lu", f, "rup", 0x1FFFFFFFFFFFFF, 0, 0)]
+        for g in ("d", "s", "h"):
+            if g != f:
+                c += [(f"fcvt.to.{g}", f, "rne", tenth[f], 0, 0), (f"fcvt.to.{g}", f, "rtz", big[f], 0, 0),
+                      (f"fcvt.to.{g}", f, "rne", snan[f], 0, 0)]
+    return c
+
+
+def fp_expected(case):
+    """(destination register bits, fflags) per the reference SoftFloat."""
+    from oracle.pyoracle import sf_ref
+    op, f, rm, a, b, cc = case
+    fc, r = FP_FMTC[f], RMS.get(rm, 0)
+
+    def ref(code, x, y=0, z=0, fmt=fc, rmode=r):
+        v, fl = sf_ref(code, fmt, rmode, [x], [y], [z])
+        return int(v[0]), int(fl[0])
+    box = lambda v: (v | FP_BOX[f]) & 0xFFFFFFFFFFFFFFFF   # noqa: E731
+    s = FP_SIGN[f]
+    ex = {"h": 0x7C00, "s": 0x7F800000, "d": 0x7FF0000000000000}[f]
+    isnan = lambda v: (v & ~s) > ex   # noqa: E731
+    codes = {"fadd": 0, "fsub": 1, "fmul": 2, "fdiv": 3, "fsqrt": 4}
+    if op in codes:
+        v, fl = ref(codes[op], a, b)
+        return box(v), fl
+    if op in ("fmadd", "fmsub", "fnmsub", "fnmadd"):
+        x = a ^ (s if op in ("fnmsub", "fnmadd") else 0)
+        z = cc ^ (s if op in ("fmsub", "fnmadd") else 0)
+        v, fl = ref(5, x, b, z)
+        return box(v), fl
+    if op in ("fmin", "fmax", "fminm", "fmaxm"):
+        p, q = (b, a) if op.startswith("fmax") else (a, b)
+        pick, fl = ref(9, p, q)
+        if not pick:
+            e, fl2 = ref(6, p, q)
+            pick = e and bool(p & s)
+            fl |= fl2
+        qn = {"h": 0x7E00, "s": 0x7FC00000, "d": 0x7FF8000000000000}[f]
+        if op.endswith("m"):
+            return (box(qn) if isnan(a) or isnan(b) else (a if pick else b)), fl
+        return box(qn if isnan(a) and isnan(b) else (a if pick or isnan(b) else b)), fl
+    if op in ("feq", "flt", "fltq", "fle", "fleq"):
+        return ref({"feq": 6, "flt": 7, "fle": 8, "fltq": 9, "fleq": 10}[op], a, b)
+    if op.startswith("fcvt.from."):
+        k = {"w": 15, "wu": 16, "l": 17, "lu": 18}[op.split(".")[2]]
+        v, fl = ref(k, a)
+        return box(v), fl
+    if op.startswith("fcvt.to."):
+        g = op.split(".")[2]
+        v, fl = ref(19 + FP_FMTC[g], a)
+        return (v | FP_BOX[g]) & 0xFFFFFFFFFFFFFFFF, fl
+    k = {"fcvt.w": 11, "fcvt.wu": 12, "fcvt.l": 13, "fcvt.lu": 14}[op]
+    v, fl = ref(k, a)
+    if k <= 12:
+        v = (v & 0xFFFFFFFF) | (0xFFFFFFFF00000000 if v & 0x80000000 else 0)
+    return v & 0xFFFFFFFFFFFFFFFF, fl
+
+
+def fp_program_source():
+    lines = ["    .text", "_start:", "    la    s2, out", "    mv    s3, s2"]
+    for k, (op, f, rm, a, b, cc) in enumerate(fp_cases()):
+        for reg_, val in (("f1", a), ("f2", b), ("f3", cc)):
+            lines += [f"    li    t0, {(val | FP_BOX[f]) & 0xFFFFFFFFFFFFFFFF if not op.startswith('fcvt.from') else 0}",
+                      f"    fmv.d.x {reg_}, t0"]
+        rms = f", {rm}" if rm else ""
+        if op.startswith("fcvt.from."):
+            lines += [f"    li    t1, {a}", f"    fcvt.{f}.{op.split('.')[2]} f0, t1{rms}", "    fmv.x.d t1, f0"]
+        elif op.startswith("fcvt.to."):
+            lines += [f"    fcvt.{op.split('.')[2]}.{f} f0, f1{rms}", "    fmv.x.d t1, f0"]
+        elif op.startswith("fcvt."):
+            lines += [f"    {op}.{f} t1, f1{rms}"]
+        elif op in ("feq", "flt", "fltq", "fle", "fleq"):
+            lines += [f"    {op}.{f} t1, f1, f2"]
+        elif op in ("fmadd", "fmsub", "fnmsub", "fnmadd"):
+            lines += [f"    {op}.{f} f0, f1, f2, f3{rms}", "    fmv.x.d t1, f0"]
+        elif op == "fsqrt":
+            lines += [f"    fsqrt.{f} f0, f1{rms}", "    fmv.x.d t1, f0"]
+        else:
+            lines += [f"    {op}.{f} f0, f1, f2{rms}", "    fmv.x.d t1, f0"]
+        lines += ["    sd    t1, 0(s2)", "    csrrw t2, 1, zero", "    sd    t2, 8(s2)", "    addi  s2, s2, 16"]
+    n = len(fp_cases())
+    # the dynamic rounding mode: frm = rtz, 1/3 in binary64, then fcsr read back
+    lines += ["    csrrwi zero, 2, 1", "    li    t0, 4607182418800017408", "    fmv.d.x f1, t0",
+              "    li    t0, 4613937818241073152", "    fmv.d.x f2, t0", "    fdiv.d f0, f1, f2",
+              "    fmv.x.d t1, f0", "    sd    t1, 0(s2)", "    csrrs t2, 3, zero",
+              "    sd    t2, 8(s2)",
+              "    li    a0, 1", "    mv    a1, s3", f"    li    a2, {16 * (n + 1)}", "    li    a7, 64", "    ecall",
+              "    li    a0, 0", "    li    a7, 93", "    ecall", "    .bss", "    .balign 8", "out:",
+              f"    .zero {16 * (n + 1)}"]
+    return "\n".join(lines) + "\n"
+
+
+def fp_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(fp_program_source())
+
+
+def fp_program_expected() -> bytes:
+    from oracle.pyoracle import sf_ref
+    vals = []
+    for case in fp_cases():
+        vals += list(fp_expected(case))
+    v, fl = sf_ref(3, 2, 1, [0x3FF0000000000000], [0x4008000000000000])   # 1/3 rounded toward zero
+    vals += [int(v[0]), int(fl[0]) | (1 << 5)]                               # fcsr = fflags | rtz << 5
+    return b"".join((x & M64).to_bytes(8, "little") for x in vals)
+
+
+def test_fp_program_on_oracle(oracle_mod):
+    from oracle.pyoracle import has_softfloat
+    if not has_softfloat():
+        pytest.skip("oracle without the reference SoftFloat")
+    o = oracle_mod.Oracle(fp_program_elf(), "fp")
+    g = o.run_golden()
+    assert g.exit_code == 0, g
+    got, exp = o.golden_stdout(), fp_program_expected()
+    assert len(got) == len(exp)
+    cases = fp_cases() + [("dyn", "d", "frm", 0, 0, 0)]
+    for k, case in enumerate(cases):
+        gv, gf = (int.from_bytes(got[16 * k + 8 * j:16 * k + 8 * j + 8], "little") for j in (0, 1))
+        ev, ef = (int.from_bytes(exp[16 * k + 8 * j:16 * k + 8 * j + 8], "little") for j in (0, 1))
+        assert (gv, gf) == (ev, ef), (k, case, hex(gv), gf, hex(ev), ef)
+
+
+def test_fp_known_values():
+    """A few binary64 answers that need no SoftFloat: numpy's IEEE RNE arithmetic."""
+    import numpy as np
+    from oracle.pyoracle import has_softfloat, sf_ref
+    if not has_softfloat():
+        pytest.skip("oracle without the reference SoftFloat")
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal(1000) * 10.0 ** rng.integers(-30, 30, 1000)
+    y = rng.standard_normal(1000) * 10.0 ** rng.integers(-30, 30, 1000)
+    xb, yb = x.view(np.uint64), y.view(np.uint64)
+    for code, npop in ((0, np.add), (1, np.subtract), (2, np.multiply), (3, np.divide)):
+        v, _ = sf_ref(code, 2, 0, xb, yb)
+        assert (v == npop(x, y).view(np.uint64)).all()
+    v, _ = sf_ref(4, 2, 0, np.abs(x).view(np.uint64))
+    assert (v == np.sqrt(np.abs(x)).view(np.uint64)).all()

@@ -153,6 +153,29 @@ F_RR = {  # name: (funct7, funct3) -- fd, fs1, fs2
 F_TO_X = {"fmv.x.w": (0x70, 0), "fclass.s": (0x70, 1), "fmv.x.d": (0x71, 0), "fclass.d": (0x71, 1),
           "fmv.x.h": (0x72, 0), "fclass.h": (0x72, 1)}   # rd, fs1
 X_TO_F = {"fmv.w.x": 0x78, "fmv.d.x": 0x79, "fmv.h.x": 0x7A}   # fd, rs1
+# F/D/Zfh arithmetic: name -> (funct5, rs2 or None, operand kinds, rounding mode or fixed funct3)
+#   kinds: "ff" fd,fs1,fs2  "f" fd,fs1  "xff" rd,fs1,fs2  "xf" rd,fs1  "fx" fd,rs1; rm None = optional
+#   rounding-mode operand (default dyn), an int = fixed funct3
+FP_FMT = {"s": 0, "d": 1, "h": 2}
+FP_RM = {"rne": 0, "rtz": 1, "rdn": 2, "rup": 3, "rmm": 4, "dyn": 7}
+F_ARITH = {}
+for _f in FP_FMT:
+    F_ARITH.update({f"fadd.{_f}": (0x00, None, "ff", None), f"fsub.{_f}": (0x01, None, "ff", None),
+                    f"fmul.{_f}": (0x02, None, "ff", None), f"fdiv.{_f}": (0x03, None, "ff", None),
+                    f"fsqrt.{_f}": (0x0B, 0, "f", None), f"fmin.{_f}": (0x05, None, "ff", 0),
+                    f"fmax.{_f}": (0x05, None, "ff", 1),
+                    f"fminm.{_f}": (0x05, None, "ff", 3 if _f == "h" else 2),
+                    f"fmaxm.{_f}": (0x05, None, "ff", 4 if _f == "h" else 3),
+                    f"fle.{_f}": (0x14, None, "xff", 0), f"flt.{_f}": (0x14, None, "xff", 1),
+                    f"feq.{_f}": (0x14, None, "xff", 2), f"fleq.{_f}": (0x14, None, "xff", 4),
+                    f"fltq.{_f}": (0x14, None, "xff", 5)})
+    for _k, _n in (("w", 0), ("wu", 1), ("l", 2), ("lu", 3)):
+        F_ARITH[f"fcvt.{_k}.{_f}"] = (0x18, _n, "xf", None)
+        F_ARITH[f"fcvt.{_f}.{_k}"] = (0x1A, _n, "fx", None)
+    for _g in FP_FMT:
+        if _g != _f:
+            F_ARITH[f"fcvt.{_f}.{_g}"] = (0x08, FP_FMT[_g], "f", None)
+F_FMA = {"fmadd": 0x43, "fmsub": 0x47, "fnmsub": 0x4B, "fnmadd": 0x4F}
 AMO_F5 = {"amoadd": 0x00, "amoswap": 0x01, "lr": 0x02, "sc": 0x03, "amoxor": 0x04, "amoor": 0x08, "amoand": 0x0C,
           "amomin": 0x10, "amomax": 0x14, "amominu": 0x18, "amomaxu": 0x1C}
 
@@ -466,6 +489,21 @@ class Assembler:
             return [("csrrs", (reg(a[0]), parse_int(a[1]), 0))]
         if n in ("csrrw", "csrrs", "csrrc"):
             return [(n, (reg(a[0]), parse_int(a[1]), reg(a[2])))]
+        if n in ("csrrwi", "csrrsi", "csrrci"):
+            return [(n, (reg(a[0]), parse_int(a[1]), parse_int(a[2]) & 31))]
+        if n in F_ARITH:
+            f5, rs2, kinds, rmf = F_ARITH[n]
+            rd = reg(a[0]) if kinds[0] == "x" else freg(a[0])
+            rs1 = reg(a[1]) if kinds == "fx" else freg(a[1])
+            if kinds in ("ff", "xff"):
+                rs2v, rest = freg(a[2]), a[3:]
+            else:
+                rs2v, rest = rs2, a[2:]
+            f3 = rmf if isinstance(rmf, int) else FP_RM[rest[0]] if rest else 7
+            return [(n, (rd, rs1, rs2v, f3))]
+        if n.rsplit(".", 1)[0] in F_FMA and n.rsplit(".", 1)[-1] in FP_FMT:
+            f3 = FP_RM[a[4]] if len(a) > 4 else 7
+            return [(n, (freg(a[0]), freg(a[1]), freg(a[2]), freg(a[3]), f3))]
         if n == ".insn16" or n == ".insn32":
             return [(n, (parse_int(a[0]),))]
         if n in FLOADS or n in FSTORES:
@@ -644,9 +682,20 @@ class Assembler:
             f5, f3, aq, rl = amo_parse(name)
             rd, rs2, base = ops
             w = enc_r(0x2F, f3, (f5 << 2) | (aq << 1) | rl, rd, base, rs2)
-        elif name in ("csrrw", "csrrs", "csrrc"):
+        elif name in ("csrrw", "csrrs", "csrrc", "csrrwi", "csrrsi", "csrrci"):
             rd, csr, rs1 = ops
-            w = (csr << 20) | (rs1 << 15) | ({"csrrw": 1, "csrrs": 2, "csrrc": 3}[name] << 12) | (rd << 7) | 0x73
+            f3 = {"csrrw": 1, "csrrs": 2, "csrrc": 3, "csrrwi": 5, "csrrsi": 6, "csrrci": 7}[name]
+            w = (csr << 20) | (rs1 << 15) | (f3 << 12) | (rd << 7) | 0x73
+        elif name in F_ARITH:
+            f5 = F_ARITH[name][0]
+            rd, rs1, rs2, f3 = ops
+            # the format field: the destination's for fcvt.X.{w,..} and fcvt.X.Y, else the last suffix
+            fmt = name.split(".")[1] if f5 in (0x08, 0x1A) else name.rsplit(".", 1)[1]
+            w = enc_r(0x53, f3, (f5 << 2) | FP_FMT[fmt], rd, rs1, rs2)
+        elif name.rsplit(".", 1)[0] in F_FMA:
+            fd, fs1, fs2, fs3, f3 = ops
+            w = (fs3 << 27) | (FP_FMT[name.rsplit(".", 1)[1]] << 25) | (fs2 << 20) | (fs1 << 15) | (f3 << 12) | \
+                (fd << 7) | F_FMA[name.rsplit(".", 1)[0]]
         else:
             raise AsmError(f"cannot encode {name}")
         return struct.pack("<I", w)
