@@ -28,6 +28,7 @@ def parse(argv=None):
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0001)
     ap.add_argument("--structures", default="int_reg", help="comma list: int_reg,pc,mem,xN,<abi name>")
     ap.add_argument("--burst", type=int, default=1)
+    ap.add_argument("--bits", default="", help="eligible lowest flipped bit positions: mask or ranges, e.g. 0-31,63")
     ap.add_argument("--protect-mask", type=lambda s: int(s, 0), default=0)
     ap.add_argument("--protect-opclasses", default="", help="comma list of gem5 OpClass names (IntAlu,IntMult,...)")
     ap.add_argument("--num-gpus", type=int, default=1)
@@ -46,13 +47,16 @@ def run_gem5(a):
     from m5.objects import FaultCampaign, Root
     camp = FaultCampaign(workload=a.workload, cmd=_split(a.cmd) or [a.workload], env=_split(a.env),
                          trials=a.trials, first_trial=a.first_trial, seed=a.seed,
-                         structures=_split(a.structures), burst=a.burst, protect_mask=a.protect_mask,
+                         structures=_split(a.structures), bits=a.bits or "0-63", burst=a.burst,
+                         protect_mask=a.protect_mask,
                          protect_opclasses=_split(a.protect_opclasses), num_gpus=a.num_gpus, max_insts_factor=a.max_insts_factor,
                          private_pages=a.private_pages, output=a.output)
     root = Root(full_system=False, campaign=camp)
     m5.instantiate()
     root.campaign.run()
     print(root.campaign.summaryJson(), flush=True)
+    # histogram(): the fi_histogram counters, flattened (include/fi_engine.h)
+    print(len(root.campaign.histogram()), "histogram counters", flush=True)
 
 
 def run_ctypes(a):
@@ -72,7 +76,7 @@ def run_ctypes(a):
                       seed=a.seed, structures=_split(a.structures), burst=a.burst, protect_mask=a.protect_mask,
                       num_gpus=max(a.num_gpus, world), max_insts_factor=a.max_insts_factor, output=a.output,
                       device=local, private_pages=a.private_pages,
-                      protect_opclasses=_split(a.protect_opclasses))
+                      protect_opclasses=_split(a.protect_opclasses), bits=a.bits or None)
     t0 = time.perf_counter()
     c.run(first_trial=a.first_trial)
     dt = time.perf_counter() - t0

@@ -193,6 +193,10 @@ fi_status fi_golden_stderr(fi_engine *e, uint8_t *buf, uint64_t cap, uint64_t *l
  * result); burst = adjacent
  * bits flipped (1..64). */
 fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint32_t burst);
+/* Eligible bit positions (SURVEY §8b `bits`): bit b set = a fault's lowest
+ * flipped bit may be b (for a burst of k bits, b <= 64 - k).  Default (and
+ * ~0): every position, sampled as before.  Set after fi_set_campaign. */
+fi_status fi_set_bits(fi_engine *e, uint64_t bits_mask);
 /* selective-replication mask over x0..x31 (bits 0..31) and pc (bit 32) */
 fi_status fi_set_protect(fi_engine *e, uint64_t protect_mask);
 /* SHREWD selective replication by instruction class (the reference's

@@ -53,7 +53,8 @@ def lib():
         L.or_golden_stdout.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64]
         L.or_golden_stderr.restype = C.c_uint64
         L.or_golden_stderr.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64]
-        L.or_sample.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]
+        L.or_sample.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64,
+                                C.c_void_p]
         L.or_run_trials.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_int]
         L.or_run_one_capture.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p,
                                          C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
@@ -108,9 +109,9 @@ class Oracle:
         self.L.or_golden_stderr(self.h, buf, n)
         return buf.raw[:n]
 
-    def sample(self, seed, first, n, structures, burst=1) -> np.ndarray:
+    def sample(self, seed, first, n, structures, burst=1, bits=2**64 - 1) -> np.ndarray:
         sites = np.zeros(n, SITE_DT)
-        if self.L.or_sample(self.h, seed, first, n, structures, burst, sites.ctypes.data) != 0:
+        if self.L.or_sample(self.h, seed, first, n, structures, burst, bits & (2**64 - 1), sites.ctypes.data) != 0:
             raise RuntimeError(self.L.or_error(self.h).decode())
         return sites
 

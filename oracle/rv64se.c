@@ -2051,7 +2051,8 @@ static u64 splitmix(u64 *s) {
 }
 static u64 mulhi(u64 a, u64 b) { return (u64)(((unsigned __int128)a * b) >> 64); }
 
-int or_sample(or_campaign_t *c, u64 seed, u64 first, u64 n, u64 structures, u32 burst, or_site_t *sites) {
+int or_sample(or_campaign_t *c, u64 seed, u64 first, u64 n, u64 structures, u32 burst, u64 bits,
+              or_site_t *sites) {
     if (!c->have_golden) { snprintf(c->err, sizeof c->err, "golden run required before sampling"); return -1; }
     if (burst < 1 || burst > 64) burst = 1;
     structures &= ~1ULL;                        /* x0 is not a fault site */
@@ -2068,7 +2069,17 @@ int or_sample(or_campaign_t *c, u64 seed, u64 first, u64 n, u64 structures, u32 
         u64 m = structures;
         for (u64 j = 0; j < k; j++) m &= m - 1;
         s->target = (u32)__builtin_ctzll(m);
-        u64 b = mulhi(r2, 65 - burst);
+        /* bits: eligible lowest-bit positions (fi_set_bits); all of them = the plain draw */
+        const u64 valid = burst == 1 ? ~0ULL : ((2ULL << (64 - burst)) - 1);
+        u64 b;
+        if ((bits & valid) == valid) {
+            b = mulhi(r2, 65 - burst);
+        } else {
+            u64 mm = bits & valid;
+            const u64 kk = mulhi(r2, (u64)__builtin_popcountll(mm));
+            for (u64 j = 0; j < kk; j++) mm &= mm - 1;
+            b = (u64)__builtin_ctzll(mm);
+        }
         s->mask = (burst == 64 ? ~0ULL : ((1ULL << burst) - 1)) << b;
         s->addr = 0;
         if (s->target == OR_T_MEM) {

@@ -90,9 +90,10 @@ uint64_t or_golden_stdout(or_campaign_t *c, uint8_t *buf, uint64_t cap);
 uint64_t or_golden_stderr(or_campaign_t *c, uint8_t *buf, uint64_t cap);
 
 /* Counter-based site sampler: SplitMix64 keyed by (seed, trial).  structures
- * is a bitmask over {bit r = x_r (1..31), bit 32 = pc, bit 33 = memory}. */
+ * is a bitmask over {bit r = x_r (1..31), bit 32 = pc, bit 33 = memory}; bits
+ * the eligible lowest flipped bit positions (~0: all). */
 int or_sample(or_campaign_t *c, uint64_t seed, uint64_t first_trial, uint64_t n,
-              uint64_t structures, uint32_t burst, or_site_t *sites);
+              uint64_t structures, uint32_t burst, uint64_t bits, or_site_t *sites);
 
 /* SHREWD selective replication by instruction class: bit k = gem5 OpClass
  * enum value k (src/cpu/FuncUnit.py).  A result fault on a replicated

@@ -102,6 +102,7 @@ struct fi_engine {
     // campaign
     uint64_t seed = 0x5EED0001ULL, structures = 0;
     uint32_t burst = 1;
+    uint64_t bits = ~0ULL;      // eligible lowest-bit positions (fi_set_bits)
     uint64_t protect = 0;
     uint64_t protect_opc = 0;   // SHREWD replication by OpClass (fi_set_protect_opclasses)
 
@@ -765,7 +766,11 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         JTRACE("compile (%zu bytes of blocks)\n", body.size());
         std::vector<char> code;
         bool cached = false;
-        const std::string err = jit_compile(body, prop.gcnArchName, code, cached);
+        // nothing hot, or more than the load-time compiler handles in reasonable time:
+        // the static kernels (pre-decoded + general interpreter) run everything
+        const std::string err = leaders.empty() ? std::string("nothing to translate (no code run twice)")
+                              : n_tx > 24000 ? std::string("translation too large")
+                                             : jit_compile(body, prop.gcnArchName, code, cached);
         JTRACE("load module (err=%s, %zu bytes)\n", err.c_str(), code.size());
         if (!err.empty()) {
             e->tx_status = err;
@@ -816,6 +821,16 @@ fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint
     if (!structures) return fail(e, FI_E_ARG, "no fault structures selected");
     if (burst < 1 || burst > 64) return fail(e, FI_E_ARG, "burst must be 1..64");
     e->seed = seed; e->structures = structures; e->burst = burst;
+    e->bits = ~0ULL;
+    return FI_OK;
+}
+
+fi_status fi_set_bits(fi_engine *e, uint64_t bits_mask) {
+    if (!e) return FI_E_ARG;
+    if (!e->structures) return fail(e, FI_E_STATE, "fi_set_campaign first");
+    const uint64_t valid = e->burst == 1 ? ~0ULL : ((2ULL << (64 - e->burst)) - 1);
+    if (!(bits_mask & valid)) return fail(e, FI_E_ARG, "no eligible bit position for a %u-bit burst", e->burst);
+    e->bits = bits_mask;
     return FI_OK;
 }
 
@@ -835,6 +850,7 @@ static SampleCtx sample_ctx(fi_engine *e, uint64_t first) {
     SampleCtx s{};
     s.seed = e->seed;
     s.structures = e->structures;
+    s.bits = e->bits & (e->burst == 1 ? ~0ULL : ((2ULL << (64 - e->burst)) - 1));
     if (e->mem_pages.empty()) s.structures &= ~(1ULL << FI_T_MEM);
     s.golden_ninst = e->golden.ninst;
     s.first = first;

@@ -23,6 +23,7 @@
 #include <cstring>
 #include <map>
 #include <set>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -352,9 +353,17 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                              uint32_t &n_insts) {
     std::set<uint32_t> executed, leaders;
     auto valid = [&](uint32_t h) { return h < pre.size() && (pre[h].flags & kPreValid); };
+    // only code the golden run executed more than once is translated: straight-
+    // line code run once gains nothing from it, and a long run of it makes one
+    // huge block that takes the load-time compiler minutes
+    std::unordered_map<uint32_t, uint32_t> runs;
     for (size_t i = 0; i < trace.size(); i++) {
         const uint32_t h = trace[i] & 0x7FFFFFFFu;
-        if (!valid(h)) continue;
+        if (valid(h)) runs[h]++;
+    }
+    for (size_t i = 0; i < trace.size(); i++) {
+        const uint32_t h = trace[i] & 0x7FFFFFFFu;
+        if (!valid(h) || runs[h] < 2) continue;
         executed.insert(h);
         const bool is_ecall = trace[i] & 0x80000000u;
         if (i == 0) leaders.insert(h);
@@ -362,6 +371,10 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             const uint32_t nh = trace[i + 1] & 0x7FFFFFFFu;
             if (is_ecall || nh != h + pre[h].len / 2u) leaders.insert(nh);
         }
+    }
+    for (auto it = leaders.begin(); it != leaders.end();) {   // (a transition into code run once)
+        if (!executed.count(*it)) it = leaders.erase(it);
+        else ++it;
     }
     for (uint32_t h : executed) {   // successors of control transfers
         std::string e;

@@ -169,6 +169,7 @@ struct DevCtx {
 struct SampleCtx {
     uint64_t seed, structures, golden_ninst, first;
     uint32_t burst, n_struct;
+    uint64_t bits;                   // eligible lowest-bit positions (already limited to 0..64-burst)
     const uint64_t *mem_pages;
     uint64_t n_mem_pages;
 };

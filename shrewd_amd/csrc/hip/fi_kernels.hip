@@ -38,7 +38,15 @@ __global__ void fi_sample_kernel(SampleCtx c, uint64_t n, fi_site *sites, uint64
     uint64_t m = c.structures;
     for (uint64_t j = 0; j < k; j++) m &= m - 1;
     s.target = (uint32_t)__builtin_ctzll(m);
-    const uint64_t b = __umul64hi(r2, (uint64_t)(65 - c.burst));
+    uint64_t b;
+    if (c.bits == (c.burst == 1 ? ~0ULL : ((2ULL << (64 - c.burst)) - 1))) {
+        b = __umul64hi(r2, (uint64_t)(65 - c.burst));   // every position
+    } else {                                             // the k-th eligible position
+        uint64_t mm = c.bits;
+        const uint64_t kk = __umul64hi(r2, (uint64_t)__popcll(mm));
+        for (uint64_t j = 0; j < kk; j++) mm &= mm - 1;
+        b = (uint64_t)__builtin_ctzll(mm);
+    }
     s.mask = (c.burst == 64 ? ~0ULL : ((1ULL << c.burst) - 1)) << b;
     s.addr = 0;
     if (s.target == FI_T_MEM) {

@@ -1015,11 +1015,14 @@ __device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32
     return true;
 }
 
-// Guest memory through the global address space (global_load/store, not flat).
+// Guest memory through the global address space (global_load/store, not flat),
+// byte-aligned: a misaligned access inside one page is one unaligned memory
+// instruction (the HSA runtime runs the GPU in unaligned-access mode; the
+// compiler still emits global_load_dword[x2] for these types).
 typedef __attribute__((address_space(1))) uint8_t g_u8;
-typedef __attribute__((address_space(1))) uint16_t g_u16;
-typedef __attribute__((address_space(1))) uint32_t g_u32;
-typedef __attribute__((address_space(1))) uint64_t g_u64;
+typedef __attribute__((address_space(1), aligned(1))) uint16_t g_u16;
+typedef __attribute__((address_space(1), aligned(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1), aligned(1))) uint64_t g_u64;
 // Translated code: the wave mask of a lane predicate (no int round trip), and
 // a value pinned in a VGPR so that `mine ? v : X` stays a select (a select on
 // a load's result is otherwise turned into a divergent branch around the load,
@@ -1036,16 +1039,16 @@ typedef __attribute__((address_space(1))) uint64_t g_u64;
 struct TextRef { const PreInst *pre; uint32_t lo, hi, bytes; uint64_t clo, chi; };
 
 // Translated-code memory access: the page must be in the lane's TLB (and be
-// its private copy for a store) and the access naturally aligned; anything
-// else leaves the translated code before the instruction (the interpreter
-// handles misses, copy-on-write, faults and misaligned accesses).
+// its private copy for a store) and the access inside that page (misaligned
+// is fine); anything else leaves the translated code before the instruction
+// (the interpreter handles misses, copy-on-write, faults and page-crossing).
 __device__ __forceinline__ bool tx_probe(const LaneMem &m, uint64_t ea, uint32_t size, bool st, uint8_t *&p,
                                          const TextRef &t) {
     const uint64_t e = tlb_find(m, ea >> 12);
     p = const_cast<uint8_t *>(page_of(e)) + (ea & 4095);
     // bitwise, not short-circuit: a && here becomes a divergent branch
     const bool code_ok = (ea >= t.chi) | (ea + size <= t.clo);
-    return (e != 0) & (!st | (((e & 1) != 0) & code_ok)) & ((ea & (size - 1)) == 0);
+    return (e != 0) & (!st | (((e & 1) != 0) & code_ok)) & ((uint32_t)(ea & 4095) + size <= 4096u);
 }
 
 // ------------------------------------------------------------------ trial kernel

@@ -141,6 +141,7 @@ def lib():
         L.fi_golden_stdout.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.fi_golden_stderr.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.fi_set_campaign.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32]
+        L.fi_set_bits.argtypes = [vp, C.c_uint64]
         L.fi_set_protect.argtypes = [vp, C.c_uint64]
         L.fi_set_protect_opclasses.argtypes = [vp, C.c_uint64]
         L.fi_sample_sites.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
@@ -231,6 +232,10 @@ class Engine:
 
     def golden_stderr(self) -> bytes:
         return self._golden_stream(self.L.fi_golden_stderr, "fi_golden_stderr")
+
+    def set_bits(self, bits: int):
+        """Eligible lowest flipped bit positions (mask; ~0 = all): fi_set_bits."""
+        self._chk(self.L.fi_set_bits(self.h, bits & (2**64 - 1)), "fi_set_bits")
 
     def set_campaign(self, seed: int, structures, burst: int = 1):
         self._chk(self.L.fi_set_campaign(self.h, seed & (2**64 - 1), structures_mask(structures), burst),
@@ -358,18 +363,39 @@ def allreduce_histogram(hist, device=None, group=None):
     return np.frombuffer(t.cpu().numpy().tobytes(), HIST_DT)[0].copy()
 
 
+def bits_mask(spec) -> int:
+    """`bits` parameter -> mask of eligible lowest flipped bit positions: an int
+    mask, or a string of positions and ranges ("0-31,63"); None / "" = all."""
+    if spec is None or spec == "":
+        return 2**64 - 1
+    if isinstance(spec, int):
+        return spec & (2**64 - 1)
+    m = 0
+    for part in str(spec).split(","):
+        part = part.strip()
+        if not part:
+            continue
+        lo, _, hi = part.partition("-")
+        lo, hi = int(lo, 0), int(hi or lo, 0)
+        if not 0 <= lo <= hi <= 63:
+            raise ValueError(f"bad bit range {part!r}")
+        for b in range(lo, hi + 1):
+            m |= 1 << b
+    return m
+
+
 class FaultCampaign:
     """Mirror of the gem5 `FaultCampaign` SimObject (src/gem5ext/FaultCampaign.py).
 
     Params (same names/meaning as the SimObject): workload (binary path), cmd
-    (argv, cmd[0] defaults to workload), env, trials, seed, structures,
+    (argv, cmd[0] defaults to workload), env, trials, seed, structures, bits,
     burst, protect_mask, protect_opclasses, num_gpus, max_insts_factor, output.
     """
 
     def __init__(self, workload: str, cmd: Sequence[str] | None = None, env: Sequence[str] | None = None,
                  trials: int = 1000, seed: int = 0x5EED0001, structures=("int_reg",), burst: int = 1,
                  protect_mask: int = 0, num_gpus: int = 1, max_insts_factor: float = 2.0, output: str = "",
-                 device: int = 0, private_pages: int = 16, protect_opclasses=()):
+                 device: int = 0, private_pages: int = 16, protect_opclasses=(), bits=None):
         self.workload, self.cmd, self.env = workload, list(cmd or [workload]), list(env or [])
         self.trials, self.seed, self.structures, self.burst = trials, seed, structures, burst
         self.protect_mask, self.num_gpus, self.output = protect_mask, num_gpus, output
@@ -380,6 +406,8 @@ class FaultCampaign:
             self.engine.load_elf(f.read(), self.cmd, self.env)
         self.golden = self.engine.golden_run()
         self.engine.set_campaign(seed, structures, burst)
+        self.bits = bits_mask(bits)
+        self.engine.set_bits(self.bits)
         self.engine.set_protect(protect_mask)
         self.protect_opclasses = opclass_mask(protect_opclasses)
         self.engine.set_protect_opclasses(self.protect_opclasses)

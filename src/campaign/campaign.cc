@@ -72,6 +72,25 @@ uint64_t structures_mask(const std::vector<std::string> &names) {
     return m & ~1ULL;
 }
 
+uint64_t bits_mask(const std::string &spec) {
+    if (spec.empty()) return ~0ULL;
+    if (spec.find_first_of(",-") == std::string::npos) return std::stoull(spec, nullptr, 0);
+    uint64_t m = 0;
+    size_t pos = 0;
+    while (pos <= spec.size()) {
+        const size_t end = std::min(spec.find(',', pos), spec.size());
+        const std::string part = spec.substr(pos, end - pos);
+        pos = end + 1;
+        if (part.empty()) continue;
+        const size_t dash = part.find('-');
+        const unsigned long lo = std::stoul(part.substr(0, dash), nullptr, 0);
+        const unsigned long hi = dash == std::string::npos ? lo : std::stoul(part.substr(dash + 1), nullptr, 0);
+        if (lo > hi || hi > 63) throw std::runtime_error("bad bit range '" + part + "'");
+        for (unsigned long b = lo; b <= hi; b++) m |= 1ULL << b;
+    }
+    return m;
+}
+
 // gem5 OpClass names (src/cpu/FuncUnit.py:43) -> mask of enum values; a bare
 // number is taken as the enum value
 uint64_t opclass_mask(const std::vector<std::string> &names) {
@@ -117,6 +136,7 @@ Campaign::Campaign(const CampaignParams &p) : p_(p) {
         fi_golden_info gi{};
         check(e, fi_golden_run(e, &gi), "fi_golden_run");
         check(e, fi_set_campaign(e, p_.seed, smask, p_.burst), "fi_set_campaign");
+        check(e, fi_set_bits(e, bits_mask(p_.bits)), "fi_set_bits");
         check(e, fi_set_protect(e, p_.protect_mask), "fi_set_protect");
         check(e, fi_set_protect_opclasses(e, opclass_mask(p_.protect_opclasses)), "fi_set_protect_opclasses");
         if (g == 0) {

@@ -30,6 +30,7 @@ struct CampaignParams {
     uint64_t seed = 0x5EED0001ULL;
     std::vector<std::string> structures{"int_reg"};
     uint32_t burst = 1;
+    std::string bits;                     // eligible lowest flipped bits: "0-63" (all), "0-31,63", or a number
     uint64_t protect_mask = 0;
     std::vector<std::string> protect_opclasses;   // SHREWD replication set (gem5 OpClass names)
     uint32_t num_gpus = 1;
@@ -42,6 +43,8 @@ struct CampaignParams {
 // 'int_reg' (x1..x31), 'pc', 'mem', 'xN' or ABI register names -> bitmask
 // (bit r = x_r, bit 32 = pc, bit 33 = memory word).  Throws on unknown names.
 uint64_t structures_mask(const std::vector<std::string> &names);
+// `bits` spec ("", "0-63", "0-31,63", "0xffff") -> mask of eligible positions
+uint64_t bits_mask(const std::string &spec);
 // gem5 OpClass names ("IntAlu", "IntMultOp", ...) or enum values -> bitmask
 uint64_t opclass_mask(const std::vector<std::string> &names);
 

@@ -3,7 +3,7 @@
 //
 //   fi_campaign --workload crc32.elf [--cmd crc32[,arg...]] [--env K=V,...]
 //               [--trials N] [--first-trial F] [--seed S] [--structures int_reg,pc,mem]
-//               [--burst K] [--protect-mask M] [--protect-opclasses IntAlu,IntMult] [--num-gpus G] [--device D]
+//               [--burst K] [--bits 0-31,63] [--protect-mask M] [--protect-opclasses IntAlu,IntMult] [--num-gpus G] [--device D]
 //               [--max-insts-factor F] [--private-pages P] [--output PREFIX]
 //
 // Prints one JSON summary line; with --output also writes PREFIX.outcomes.bin
@@ -43,6 +43,7 @@ int main(int argc, char **argv) {
         else if (k == "--seed") p.seed = strtoull(v.c_str(), nullptr, 0);
         else if (k == "--structures") p.structures = split(v);
         else if (k == "--burst") p.burst = (uint32_t)strtoul(v.c_str(), nullptr, 0);
+        else if (k == "--bits") p.bits = v;
         else if (k == "--protect-mask") p.protect_mask = strtoull(v.c_str(), nullptr, 0);
         else if (k == "--protect-opclasses") p.protect_opclasses = split(v);
         else if (k == "--num-gpus") p.num_gpus = (uint32_t)strtoul(v.c_str(), nullptr, 0);

@@ -21,6 +21,7 @@ class FaultCampaign(SimObject):
         PyBindMethod("setProtectMask"),
         PyBindMethod("setProtectOpClasses"),
         PyBindMethod("trialsRun"),
+        PyBindMethod("histogram"),
     ]
 
     workload = Param.String("RV64 static ELF run in SE mode")
@@ -31,6 +32,8 @@ class FaultCampaign(SimObject):
     seed = Param.UInt64(0x5EED0001, "campaign seed")
     structures = VectorParam.String(
         ["int_reg"], "fault targets: int_reg, pc, mem, result, xN or ABI register names")
+    bits = Param.String(
+        "0-63", "eligible lowest flipped bit positions: ranges / positions ('0-31,63') or a mask")
     burst = Param.UInt32(1, "adjacent bits flipped per fault (1..64)")
     protect_mask = Param.UInt64(
         0, "selective replication: protected x0..x31 (bits 0-31) and pc (bit 32)")

@@ -24,6 +24,7 @@ FaultCampaign::init()
     cp.seed = params().seed;
     cp.structures = params().structures;
     cp.burst = params().burst;
+    cp.bits = params().bits;
     cp.protect_mask = params().protect_mask;
     cp.protect_opclasses = params().protect_opclasses;
     cp.num_gpus = params().num_gpus;
@@ -71,6 +72,15 @@ uint64_t
 FaultCampaign::trialsRun() const
 {
     return campaign->histogram().trials;
+}
+
+std::vector<uint64_t>
+FaultCampaign::histogram() const
+{
+    // the fi_histogram counters in declaration order (include/fi_engine.h)
+    const fi_histogram &h = campaign->histogram();
+    const uint64_t *p = reinterpret_cast<const uint64_t *>(&h);
+    return std::vector<uint64_t>(p, p + sizeof(h) / sizeof(uint64_t));
 }
 
 } // namespace gem5

@@ -4,8 +4,10 @@
 #ifndef __GEM5EXT_FAULT_CAMPAIGN_HH__
 #define __GEM5EXT_FAULT_CAMPAIGN_HH__
 
+#include <cstdint>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "params/FaultCampaign.hh"
 #include "sim/sim_object.hh"
@@ -33,6 +35,9 @@ class FaultCampaign : public SimObject
     void setProtectMask(uint64_t mask);
     void setProtectOpClasses(std::vector<std::string> opclasses);
     uint64_t trialsRun() const;
+    // the outcome histogram: the fi_histogram counters, flattened in
+    // declaration order (include/fi_engine.h)
+    std::vector<uint64_t> histogram() const;
 
   private:
     std::unique_ptr<shrewd::Campaign> campaign;

@@ -92,6 +92,14 @@ def test_sampler_matches_oracle(engine_factory, oracle_mod, name):
         dev = e.sample(1000, 3000)
         ref = o.sample(0xABCDEF, 1000, 3000, structs, burst)
         assert np.array_equal(dev, ref)
+    # the `bits` parameter (eligible lowest flipped bits)
+    from shrewd_amd.fi import bits_mask
+    for spec, burst in (("0-7,40,63", 1), ("10-20", 2), (0x8000000000000001, 1)):
+        e.set_campaign(0xABCDEF, REGS | PC | MEM, burst)
+        e.set_bits(bits_mask(spec))
+        dev = e.sample(0, 3000)
+        ref = o.sample(0xABCDEF, 0, 3000, REGS | PC | MEM, burst, bits_mask(spec))
+        assert np.array_equal(dev, ref), spec
 
 
 @pytest.mark.parametrize("name,structs,burst,n", [
@@ -181,7 +189,15 @@ def test_result_faults_bit_exact(engine_factory, oracle_mod, name, opc, n):
         assert (dev["cls"] == 4).sum() > 0
 
 
-@pytest.mark.parametrize("name", ["crc32", "qsort", "intmix", "hello"])
+def test_translation_skipped_without_hot_code(engine_factory):
+    """Straight-line code run once (hello) is not translated: the static
+    kernels run it, and the engine says why."""
+    e = engine_factory("hello")
+    assert e.translate_status().startswith("nothing to translate")
+    assert e.golden.translated_blocks == 0
+
+
+@pytest.mark.parametrize("name", ["crc32", "qsort", "intmix"])
 def test_translated_path_active(engine_factory, name):
     """The load-time translated kernel (fi_trial_kernel_tx) is built and runs:
     a hipRTC failure would otherwise fall back to the static kernel silently."""

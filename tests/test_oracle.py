@@ -330,3 +330,23 @@ def test_result_fault_replication_properties(oracle_mod):
     same = prot == base
     assert ((prot["cls"] == 4) | same).all() and (prot["cls"] == 4).sum() > 0
     assert (base["cls"][prot["cls"] == 4] != 4).all()
+
+
+def test_sampler_bits_mask(oracle_mod):
+    """`bits` restricts the lowest flipped bit to the eligible positions; the
+    full mask is the plain draw (same sites as without it)."""
+    from shrewd_amd.fi import bits_mask
+    o = oracle_mod.Oracle(workload_elf("crc32"), "crc32")
+    o.run_golden()
+    regs = ((1 << 32) - 2)
+    plain = o.sample(7, 0, 4000, regs, 1)
+    assert plain.tobytes() == o.sample(7, 0, 4000, regs, 1, bits_mask("0-63")).tobytes()
+    m = bits_mask("0-7,40,63")
+    s = o.sample(7, 0, 4000, regs, 1, m)
+    low = np.array([int(x).bit_length() - 1 for x in s["mask"]])
+    assert set(low.tolist()) == {0, 1, 2, 3, 4, 5, 6, 7, 40, 63}
+    assert (s["inst"] == plain["inst"]).all() and (s["target"] == plain["target"]).all()
+    s4 = o.sample(7, 0, 4000, regs, 4, bits_mask("58-63"))   # a 4-bit burst starts at 58..60
+    lows = {int(x & -x).bit_length() - 1 for x in s4["mask"]}
+    assert lows == {58, 59, 60}
+    assert bits_mask(0xF0) == 0xF0 and bits_mask(None) == 2**64 - 1

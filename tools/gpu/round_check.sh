@@ -6,7 +6,7 @@ set -o pipefail
 TAG=${1:-r02}
 mkdir -p gpurun_out
 export SHREWD_FI_JIT_CACHE=$PWD/gpurun_out/jitcache
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
     > gpurun_out/pytest_$TAG.log 2>&1 &&
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err &&
 timeout -k 10 300 python -u tools/gpu/tail_profile.py crc32 0x5EED0002 100000 > gpurun_out/tail_crc32_$TAG.log 2>&1 &&
