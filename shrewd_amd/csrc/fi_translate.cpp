@@ -644,9 +644,14 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, true, p_, tx);\n", A.c_str(), immb, sz);
                 g.put("    if (TXB(mine && !ok_)) %s\n", leave_here.c_str());
                 g.put("    p_ = (mine && ok_) ? p_ : sink; *(g_%s *)p_ = (%s)%s; }\n", gtype(sz), ltype(sz), B.c_str());
-                so.put("  { uint8_t *p_; if (!tx_probe(m, %s + %s, %uu, true, p_, tx)) %s\n", A.c_str(), immb, sz,
-                       sleave_here.c_str());
-                so.put("    *(g_%s *)p_ = (%s)%s; }\n", gtype(sz), ltype(sz), B.c_str());
+                // solo: a store into the code range is performed too; it marks the
+                // bytes rewritten and leaves after itself if they lie ahead in this block
+                so.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s; const uint32_t cs_ = tx_probe_st(m, ea_, %uu, "
+                       "p_, tx); if (!cs_) %s\n", A.c_str(), immb, sz, sleave_here.c_str());
+                so.put("    *(g_%s *)p_ = (%s)%s;\n", gtype(sz), ltype(sz), B.c_str());
+                so.put("    if (cs_ & 2u) { TXCODE(ea_, %uu); if (ea_ < %s && ea_ + %uu > %s) { %sspc = %s; "
+                       "goto S_out; } } }\n", sz, hex(bhi).c_str(), sz, ftb.c_str(),
+                       scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db + sz).c_str(), ftb.c_str());
                 break;
             case C_BR: {
                 const std::string c = subst(cond, A, B, immb, pcb);

@@ -1042,6 +1042,17 @@ struct TextRef { const PreInst *pre; uint32_t lo, hi, bytes; uint64_t clo, chi; 
 // its private copy for a store) and the access inside that page (misaligned
 // is fine); anything else leaves the translated code before the instruction
 // (the interpreter handles misses, copy-on-write, faults and page-crossing).
+// Solo translated stores: as tx_probe, but a store into the code range is
+// taken too (1 = ok, 3 = ok and it rewrites code: the block marks the bytes
+// dirty and leaves if they are still ahead of it; 0 = leave before it).
+__device__ __forceinline__ uint32_t tx_probe_st(const LaneMem &m, uint64_t ea, uint32_t size, uint8_t *&p,
+                                               const TextRef &t) {
+    const uint64_t e = tlb_find(m, ea >> 12);
+    p = const_cast<uint8_t *>(page_of(e)) + (ea & 4095);
+    const bool ok = (e & 1) != 0 && (uint32_t)(ea & 4095) + size <= 4096u;
+    const bool code = !((ea >= t.chi) | (ea + size <= t.clo));
+    return ok ? (code ? 3u : 1u) : 0u;
+}
 __device__ __forceinline__ bool tx_probe(const LaneMem &m, uint64_t ea, uint32_t size, bool st, uint8_t *&p,
                                          const TextRef &t) {
     const uint64_t e = tlb_find(m, ea >> 12);
@@ -1588,8 +1599,21 @@ __device__ __forceinline__ void trial_body() {
                     const uint32_t bud = rem < wbud ? rem : wbud;
                     // rewritten code bytes as offsets from the text base (empty range if none)
                     const uint64_t tlo = CX->text_lo;
-                    const uint32_t sdlo = m.code_dirty ? (uint32_t)((m.dlo > tlo ? m.dlo : tlo) - tlo) : 0xFFFFFFFFu;
-                    const uint32_t sdhi = m.code_dirty ? (uint32_t)((m.dhi > tlo ? m.dhi : tlo) - tlo) : 0u;
+                    uint32_t sdlo = m.code_dirty ? (uint32_t)((m.dlo > tlo ? m.dlo : tlo) - tlo) : 0xFFFFFFFFu;
+                    uint32_t sdhi = m.code_dirty ? (uint32_t)((m.dhi > tlo ? m.dhi : tlo) - tlo) : 0u;
+                    bool schg = false;                             // the blocks rewrote code
+                    uint32_t cslo = 0xFFFFFFFFu, cshi = 0u;        // ... these bytes (offsets)
+// a translated store rewrote code bytes [ea_, ea_ + sz_): later blocks see the
+// grown range; the decode cache forgets them when the blocks are left
+#define TXCODE(ea_, sz_)                                                                        \
+    do {                                                                                        \
+        const uint32_t o_ = (uint32_t)((ea_) - tlo);                                            \
+        sdlo = o_ < sdlo ? o_ : sdlo;                                                           \
+        sdhi = o_ + (sz_) > sdhi ? o_ + (sz_) : sdhi;                                           \
+        cslo = o_ < cslo ? o_ : cslo;                                                           \
+        cshi = o_ + (sz_) > cshi ? o_ + (sz_) : cshi;                                           \
+        schg = true;                                                                            \
+    } while (0)
                     const uint32_t lwm = L.watch > 0 ? (1u << L.watch) : 0u;
                     uint32_t st = 0, xt = 0, fb = 0, db = 0;   // instructions, straddles, fetch/data bytes
                     uint64_t spc = lpc;
@@ -1607,6 +1631,15 @@ __device__ __forceinline__ void trial_body() {
                     TXW(14) TXW(15) TXW(16) TXW(17) TXW(18) TXW(19) TXW(20) TXW(21) TXW(22) TXW(23) TXW(24) TXW(25)
                     TXW(26) TXW(27) TXW(28) TXW(29) TXW(30) TXW(31)
 #undef TXW
+#undef TXCODE
+                    if (schg) {
+                        m.code_dirty = true; m.dlo = tlo + sdlo; m.dhi = tlo + sdhi;
+#pragma unroll 8
+                        for (uint32_t k = 0; k < kDC; k++) {   // decode-cache entries whose bytes were rewritten
+                            const uint32_t tg = DCT[k];
+                            if (tg != 0xFFFFFFFFu && tg + 4 > cslo && tg < cshi) DCT[k] = 0xFFFFFFFFu;
+                        }
+                    }
                     L.ninst += st; L.ncyc += st + xt; L.fetch_b += fb; L.data_b += db; L.pc = spc;
                     n_iter += st;
                     n_tx += st;

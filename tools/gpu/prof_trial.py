@@ -1,6 +1,7 @@
 """FI_PROF phase cycles of chosen trials run alone through the interpreter
 (no translation): python tools/gpu/prof_trial.py WORKLOAD SEED ID [ID ...]
-(run with SHREWD_FI_LIB pointing at a -DFI_PROF build)."""
+(run with SHREWD_FI_LIB pointing at a -DFI_PROF build; PROF_FLAGS adds engine
+flags, e.g. 128 for the solo kernel)."""
 import json
 import os
 import sys
@@ -13,7 +14,7 @@ from shrewd_amd.fi import CFG_NO_TRANSLATE  # noqa: E402
 
 REGS_PC = ((1 << 32) - 2) | (1 << 32)
 name, seed, ids = sys.argv[1], int(sys.argv[2], 0), [int(x) for x in sys.argv[3:]]
-e = Engine(max_trials_per_launch=131072, flags=CFG_NO_TRANSLATE)
+e = Engine(max_trials_per_launch=131072, flags=CFG_NO_TRANSLATE | 8 | int(os.environ.get("PROF_FLAGS", "0"), 0))
 e.load_elf(open(os.path.join(ROOT, "workloads", f"{name}.elf"), "rb").read(), [name])
 e.golden_run()
 e.set_campaign(seed, REGS_PC, 1)
