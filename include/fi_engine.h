@@ -197,6 +197,10 @@ fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint
  * flipped bit may be b (for a burst of k bits, b <= 64 - k).  Default (and
  * ~0): every position, sampled as before.  Set after fi_set_campaign. */
 fi_status fi_set_bits(fi_engine *e, uint64_t bits_mask);
+/* SE time and randomness model: ticks (1 ps) per CPU cycle for clock_gettime
+ * (curTick at a tick = (cycles so far - 1) x period; default 500 = 2 GHz) and
+ * gem5's Random global seed for getrandom (default 5489, base/random.cc:79). */
+fi_status fi_set_clock(fi_engine *e, uint64_t period_ticks, uint64_t random_seed);
 /* selective-replication mask over x0..x31 (bits 0..31) and pc (bit 32) */
 fi_status fi_set_protect(fi_engine *e, uint64_t protect_mask);
 /* SHREWD selective replication by instruction class (the reference's

@@ -63,6 +63,7 @@ def lib():
         L.or_mnemonic.argtypes = [C.c_uint32]
         L.or_sys_class.argtypes = [C.c_int]
         L.or_set_protect_opclasses.argtypes = [C.c_void_p, C.c_uint64]
+        L.or_set_clock.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
         L.or_sf_ref.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                 C.c_void_p, C.c_void_p]
         _lib = L
@@ -123,6 +124,9 @@ class Oracle:
                                 out.ctypes.data, threads) != 0:
             raise RuntimeError(self.L.or_error(self.h).decode())
         return out
+
+    def set_clock(self, period_ticks=500, random_seed=5489):
+        self.L.or_set_clock(self.h, period_ticks, random_seed)
 
     def run_one(self, site=None, protect_mask=0, hang_x16=0):
         out = np.zeros(1, OUTCOME_DT)

@@ -174,6 +174,8 @@ struct or_campaign {
     u64 entry, sp0, stack_min0;
     u64 stack_vma_lo, stack_vma_hi;  /* the "stack" VMA created by argsInit */
     u64 brk0;
+    u64 clk_period;        /* ticks per CPU cycle (1 ps ticks; 500 = 2 GHz) */
+    u64 rnd_seed;          /* gem5 Random::globalSeed (base/random.cc:79) */
     u64 *mem_pages;        /* writable pages at process start (memory fault candidates) */
     u64 n_mem_pages;
     u64 protect_opc;       /* SHREWD replication: OpClass mask (bit = FuncUnit.py enum value) */
@@ -214,6 +216,10 @@ typedef struct {
     int nvma;
     u64 brk, mmap_end, ctid;
     u32 fdc;
+    /* getrandom's generator (syscall_emul.hh:3222-3236: one mt19937_64 per
+     * process, created at the first call from the global seed) */
+    u64 *mt; int mt_i;
+    u64 rnd_pos;          /* bytes drawn (the engine's table holds OR_RND_CAP) */
     u64 protect_mask;
     /* termination */
     int done; or_outcome_t res;
@@ -987,8 +993,8 @@ static const uint16_t sys_impl_escape[] = {
 /* modelled: the deterministic handlers (syscall_emul.{cc,hh}, se_workload.cc) */
 static int sys_modelled(int num) {
     switch (num) {
-    case 29: case 57: case 64: case 66: case 93: case 94: case 96: case 160: case 163: case 214: case 215:
-    case 222: case 261: case 1058:
+    case 29: case 57: case 64: case 66: case 93: case 94: case 96: case 113: case 160: case 163: case 214:
+    case 215: case 222: case 261: case 278: case 1058:
         return 1;
     default:
         return num >= 172 && num <= 178;
@@ -1024,6 +1030,31 @@ static void se_panic(mach_t *m) { finish(m, OR_CRASH, OR_CRASH_SE_PANIC, 134); }
 /* writevFunc<RiscvLinux64> (syscall_emul.hh:1964-1996): the iovecs and their
  * buffers are read through the proxy in order (fatal on an unmapped byte),
  * then host writev() on the target fd */
+/* std::mt19937_64 (Matsumoto & Nishimura; the C++ standard's parameters),
+ * seeded as gem5's Random(globalSeed) does (gen.seed(uint32 seed)) */
+static u64 mt64_next(mach_t *m) {
+    enum { N = 312, M = 156 };
+    if (!m->mt) {
+        m->mt = (u64 *)malloc(N * sizeof(u64));
+        m->mt[0] = (u64)(uint32_t)m->c->rnd_seed;
+        for (int i = 1; i < N; i++) m->mt[i] = 6364136223846793005ULL * (m->mt[i - 1] ^ (m->mt[i - 1] >> 62)) + (u64)i;
+        m->mt_i = N;
+    }
+    if (m->mt_i >= N) {
+        for (int i = 0; i < N; i++) {
+            const u64 x = (m->mt[i] & 0xFFFFFFFF80000000ULL) | (m->mt[(i + 1) % N] & 0x7FFFFFFFULL);
+            m->mt[i] = m->mt[(i + M) % N] ^ (x >> 1) ^ ((x & 1) ? 0xB5026F5AA96619E9ULL : 0);
+        }
+        m->mt_i = 0;
+    }
+    u64 y = m->mt[m->mt_i++];
+    y ^= (y >> 29) & 0x5555555555555555ULL;
+    y ^= (y << 17) & 0x71D67FFFEDA60000ULL;
+    y ^= (y << 37) & 0xFFF7EEE000000000ULL;
+    y ^= y >> 43;
+    return y;
+}
+
 static void sys_writev(mach_t *m) {
     const int fd = (int)(s32)(u32)m->x[10];
     const u64 iov = m->x[11], cnt = m->x[12];
@@ -1202,6 +1233,36 @@ static void do_syscall(mach_t *m) {
         uint8_t b[16];
         for (int k = 0; k < 8; k++) b[k] = b[8 + k] = (uint8_t)(lim >> (8 * k));
         proxy_write(m, rlp, b, 16);
+        m->x[10] = 0;
+        return;
+    }
+    case 278: {   /* getrandomFunc (syscall_emul.hh:3222-3236): count bytes of gen() % 255 */
+        const u64 buf = m->x[10], cnt = m->x[11];
+        if (cnt > (1ULL << 31)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* host buffer */
+        /* the engine precomputes the first 1 MiB of the stream: beyond it, a
+         * resource escape on both sides */
+        if (m->rnd_pos + cnt > (1ULL << 20)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return; }
+        m->rnd_pos += cnt;
+        uint8_t *tmp = (uint8_t *)malloc(cnt ? cnt : 1);
+        for (u64 i = 0; i < cnt; i++) tmp[i] = (uint8_t)(mt64_next(m) % 255);
+        const int h = proxy_writable(m, buf, cnt);
+        if (h == 0) { free(tmp); finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        if (h < 0) { free(tmp); finish(m, OR_CRASH, OR_CRASH_STACK_LIMIT, 1); return; }
+        proxy_write(m, buf, tmp, cnt);
+        free(tmp);
+        m->x[10] = cnt;
+        return;
+    }
+    case 113: {   /* clock_gettimeFunc (syscall_emul.hh:2266-2278): curTick() / 1000 ns since the
+                   * first tick (tick = (cycles so far - 1) x period) + seconds_since_epoch (1e9) */
+        const u64 tp = m->x[11];
+        if (!tp) { se_panic(m); return; }
+        if (!proxy_readable(m, tp, 16)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        const u64 ns = (m->num_cycles - 1) * m->c->clk_period / 1000;
+        const u64 sec = ns / 1000000000ULL + 1000000000ULL, nsec = ns % 1000000000ULL;
+        uint8_t b[16];
+        for (int k = 0; k < 8; k++) { b[k] = (uint8_t)(sec >> (8 * k)); b[8 + k] = (uint8_t)(nsec >> (8 * k)); }
+        proxy_write(m, tp, b, 16);
         m->x[10] = 0;
         return;
     }
@@ -1926,6 +1987,8 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
     }
     /* RiscvProcess64 ctor: brk = roundUp(image.maxAddr(), 4096) (process.cc:76) */
     c->brk0 = (max_addr + PAGE - 1) & PAGE_MASK;
+    c->clk_period = 500;
+    c->rnd_seed = 5489;
 
     /* RiscvProcess::argsInit<uint64_t> (process.cc:134-261), argv = {argv0}, envp = {} */
     const size_t alen = strlen(argv0);
@@ -2001,7 +2064,7 @@ static void mach_init(mach_t *m, const or_campaign_t *c) {
     m->brk = c->brk0;
     m->mmap_end = 0x4000000000000000ULL;
 }
-static void mach_free(mach_t *m) { pm_free(&m->mem); free(m->out.buf); free(m->err.buf); }
+static void mach_free(mach_t *m) { pm_free(&m->mem); free(m->out.buf); free(m->err.buf); free(m->mt); }
 
 static void run(mach_t *m, u64 cap) {
     while (!m->done) tick(m, cap);
@@ -2120,6 +2183,10 @@ static void *worker(void *arg) {
 }
 
 void or_set_protect_opclasses(or_campaign_t *c, u64 mask) { c->protect_opc = mask; }
+void or_set_clock(or_campaign_t *c, u64 period_ticks, u64 random_seed) {
+    c->clk_period = period_ticks;
+    c->rnd_seed = random_seed;
+}
 
 int or_run_trials(or_campaign_t *c, const or_site_t *sites, u64 n, u64 protect, u64 f16, or_outcome_t *out,
                   int nth) {

@@ -99,6 +99,9 @@ int or_sample(or_campaign_t *c, uint64_t seed, uint64_t first_trial, uint64_t n,
  * enum value k (src/cpu/FuncUnit.py).  A result fault on a replicated
  * instruction is detected (see rv64se.c:result_fault). */
 void or_set_protect_opclasses(or_campaign_t *c, uint64_t mask);
+/* SE time and randomness: ticks per CPU cycle (clock_gettime; default 500 =
+ * 2 GHz) and gem5's Random global seed (getrandom; default 5489) */
+void or_set_clock(or_campaign_t *c, uint64_t period_ticks, uint64_t random_seed);
 
 /* Run trials from scratch (no golden snapshots, no early exit): the plain
  * serial semantics the GPU engine must reproduce bit for bit. */

@@ -16,10 +16,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <random>
 #include <string>
 #include <vector>
 
 #include "fi_types.h"
+
+constexpr uint64_t kRndLen = 1ULL << 20;   // getrandom bytes precomputed per engine
 
 namespace fi {
 hipError_t launch_sample(const SampleCtx &c, uint64_t n, fi_site *sites, uint64_t *keys, uint32_t *perm,
@@ -103,6 +106,8 @@ struct fi_engine {
     uint64_t seed = 0x5EED0001ULL, structures = 0;
     uint32_t burst = 1;
     uint64_t bits = ~0ULL;      // eligible lowest-bit positions (fi_set_bits)
+    uint64_t clk_period = 500, rnd_seed = 5489;   // fi_set_clock
+    uint8_t *d_rnd = nullptr;   // getrandom's byte stream (kRndLen bytes)
     uint64_t protect = 0;
     uint64_t protect_opc = 0;   // SHREWD replication by OpClass (fi_set_protect_opclasses)
 
@@ -172,6 +177,17 @@ extern "C" {
 // errors of calls that have no engine yet (fi_create), per host thread
 static thread_local std::string g_create_err;
 
+// getrandom's bytes: gem5's Random(globalSeed) generator (std::mt19937_64,
+// base/random.hh:125) drawn once per byte, % 255 (Random::random<uint8_t>)
+static fi_status upload_rnd(fi_engine *e) {
+    std::vector<uint8_t> tab(kRndLen);
+    std::mt19937_64 gen((uint32_t)e->rnd_seed);
+    for (auto &b : tab) b = (uint8_t)(gen() % 255);
+    if (!e->d_rnd) HIPCHK(hipMalloc(&e->d_rnd, kRndLen));
+    HIPCHK(hipMemcpy(e->d_rnd, tab.data(), kRndLen, hipMemcpyHostToDevice));
+    return FI_OK;
+}
+
 fi_status fi_create(const fi_config *cfg, fi_engine **out) {
     if (!out) { g_create_err = "fi_create: out is NULL"; return FI_E_ARG; }
     *out = nullptr;
@@ -207,6 +223,11 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
         delete e;
         return FI_E_HIP;
     }
+    if (upload_rnd(e) != FI_OK) {
+        g_create_err = "fi_create: " + e->err;
+        delete e;
+        return FI_E_HIP;
+    }
     *out = e;
     return FI_OK;
 }
@@ -238,6 +259,7 @@ void fi_destroy(fi_engine *e) {
     (void)hipSetDevice(e->dev);
     free_work(e);
     free_image(e);
+    dfree(e->d_rnd);
     for (auto &tp : e->tpool) { (void)hipEventDestroy(tp.first); (void)hipEventDestroy(tp.second); }
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -512,6 +534,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.stats = e->d_stats;
     c.brk0 = e->brk0; c.svma_lo = e->svma_lo; c.svma_hi = e->svma_hi; c.vm = e->d_vm;
     c.simt_min = (e->cfg.flags & FI_CFG_SIMT) ? 8u : 0u;
+    c.rnd_tab = e->d_rnd; c.rnd_len = e->d_rnd ? kRndLen : 0; c.clk_period = e->clk_period;
     c.lanes = e->cfg.lanes_per_wave;
     return c;
 }
@@ -823,6 +846,14 @@ fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint
     e->seed = seed; e->structures = structures; e->burst = burst;
     e->bits = ~0ULL;
     return FI_OK;
+}
+
+fi_status fi_set_clock(fi_engine *e, uint64_t period_ticks, uint64_t random_seed) {
+    if (!e || !period_ticks) return FI_E_ARG;
+    HIPCHK(hipSetDevice(e->dev));
+    e->clk_period = period_ticks;
+    e->rnd_seed = random_seed;
+    return upload_rnd(e);
 }
 
 fi_status fi_set_bits(fi_engine *e, uint64_t bits_mask) {

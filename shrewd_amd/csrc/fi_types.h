@@ -76,6 +76,7 @@ constexpr uint32_t kMaxVma = 64;    // == oracle/rv64se.c mach_t.vma (overflow: 
 constexpr uint64_t kTomb = 1ULL << 63;   // priv_vpn entry: the page is unmapped for this trial
 struct VmState {
     uint64_t brk, mmap_end, ctid;
+    uint64_t rnd_pos;                // getrandom bytes drawn so far (index into DevCtx::rnd_tab)
     uint32_t nvma, fdc;
     uint64_t vma[kMaxVma][2];
 };
@@ -153,6 +154,9 @@ struct DevCtx {
     // SE memory map: process-start brk and "stack" VMA; per-slot VM state
     uint64_t brk0, svma_lo, svma_hi;
     VmState *vm;                     // [n_slots]
+    const uint8_t *rnd_tab;          // getrandom's byte stream: mt19937_64(seed)() % 255, rnd_len bytes
+    uint64_t rnd_len;
+    uint64_t clk_period;             // ticks per CPU cycle (clock_gettime)
     uint32_t simt_min;               // diverged-lanes step loop: least lanes to enter it (0 = off)
     unsigned long long *stats;       // [0] fetch B [1] data B [2] pages [3..5] golden ncycles/out/err
                                      // [6] loop iterations [7] lane-insts [8] slow fetches [9] min-PC [10] max iter/wave

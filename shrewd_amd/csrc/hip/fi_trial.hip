@@ -260,6 +260,7 @@ __device__ VmState *vm_of(KCtx *c, LaneMem &m, uint64_t slot) {
     VmState *v = c->vm + slot;
     if (!m.vm) {
         v->brk = c->brk0; v->mmap_end = 0x4000000000000000ULL; v->ctid = 0;   // RiscvProcess64 (process.cc:79)
+        v->rnd_pos = 0;
         v->nvma = 1; v->fdc = 0;
         v->vma[0][0] = c->svma_lo; v->vma[0][1] = c->svma_hi;                 // argsInit's "stack" VMA
         m.vm = true;
@@ -531,8 +532,8 @@ __device__ int fetch_lane(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, 
 // 4 modelled.
 __device__ int sys_class(int num) {
     switch (num) {   // modelled (oracle/rv64se.c:sys_modelled)
-    case 29: case 57: case 64: case 66: case 93: case 94: case 96: case 160: case 163: case 214: case 215:
-    case 222: case 261: case 1058:
+    case 29: case 57: case 64: case 66: case 93: case 94: case 96: case 113: case 160: case 163: case 214:
+    case 215: case 222: case 261: case 278: case 1058:
         return 4;
     default:
         if (num >= 172 && num <= 178) return 4;
@@ -902,6 +903,33 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         if (!proxy_write(c, w, m, slot, rlp, b, 16)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
         set_ret(0);
         return rlp < c->code_hi && rlp + 16 > c->code_lo;
+    }
+    case 278: {   // getrandomFunc (syscall_emul.hh:3222-3236): count bytes of mt19937_64() % 255
+        VmState *v = vm_of(c, m, slot);
+        if (a1 > (1ULL << 31)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+        if (v->rnd_pos + a1 > c->rnd_len) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        const int h = proxy_writable(c, w, m, slot, a0, a1);
+        if (h == 0) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+        if (h == -1) { finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, pc32); return false; }
+        if (h == -2) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        if (!proxy_write(c, w, m, slot, a0, (const char *)(c->rnd_tab + v->rnd_pos), a1)) {
+            finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32);
+            return false;
+        }
+        v->rnd_pos += a1;
+        set_ret((int64_t)a1);
+        return a0 < c->code_hi && a0 + a1 > c->code_lo;
+    }
+    case 113: {   // clock_gettimeFunc (syscall_emul.hh:2266-2278): curTick() in ns + 1e9 s
+        if (!a1) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }
+        if (!proxy_readable(c, w, m, slot, a1, 16)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+        const uint64_t ns = (L.ncyc - 1) * c->clk_period / 1000;
+        const uint64_t sec = ns / 1000000000ULL + 1000000000ULL, nsec = ns % 1000000000ULL;
+        char b[16];
+        for (int k = 0; k < 8; k++) { b[k] = (char)(sec >> (8 * k)); b[8 + k] = (char)(nsec >> (8 * k)); }
+        if (!proxy_write(c, w, m, slot, a1, b, 16)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        set_ret(0);
+        return a1 < c->code_hi && a1 + 16 > c->code_lo;
     }
     case 160: {   // unameFunc64 (arch/riscv/linux/se_workload.cc:109-122): 5 fields of 65 chars
         if (!a0) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }

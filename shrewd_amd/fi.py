@@ -142,6 +142,7 @@ def lib():
         L.fi_golden_stderr.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.fi_set_campaign.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32]
         L.fi_set_bits.argtypes = [vp, C.c_uint64]
+        L.fi_set_clock.argtypes = [vp, C.c_uint64, C.c_uint64]
         L.fi_set_protect.argtypes = [vp, C.c_uint64]
         L.fi_set_protect_opclasses.argtypes = [vp, C.c_uint64]
         L.fi_sample_sites.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
@@ -236,6 +237,10 @@ class Engine:
     def set_bits(self, bits: int):
         """Eligible lowest flipped bit positions (mask; ~0 = all): fi_set_bits."""
         self._chk(self.L.fi_set_bits(self.h, bits & (2**64 - 1)), "fi_set_bits")
+
+    def set_clock(self, period_ticks: int = 500, random_seed: int = 5489):
+        """clock_gettime's ticks per CPU cycle and getrandom's gem5 Random seed."""
+        self._chk(self.L.fi_set_clock(self.h, period_ticks, random_seed), "fi_set_clock")
 
     def set_campaign(self, seed: int, structures, burst: int = 1):
         self._chk(self.L.fi_set_campaign(self.h, seed & (2**64 - 1), structures_mask(structures), burst),

@@ -323,7 +323,7 @@ def test_native_driver_matches_engine(engine_factory, tmp_path):
     assert hist["counts"].tobytes() == rh["counts"].tobytes()
 
 
-@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp"])
+@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp", "rnd"])
 def test_known_answer_programs(oracle_mod, prog):
     """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
@@ -339,7 +339,8 @@ def test_known_answer_programs(oracle_mod, prog):
     vm: brk / mmap / munmap / set_tid_address / ioctl / getrlimit / prlimit64 /
     uname / writev / close (the SE memory map).
     fp: F/D/Zfh arithmetic in every rounding mode with fflags, the dynamic
-    rounding mode and fcsr (answers from the reference SoftFloat).  The device golden run (general interpreter)
+    rounding mode and fcsr (answers from the reference SoftFloat).
+    rnd: getrandom (gem5's mt19937_64 stream) and clock_gettime (curTick).  The device golden run (general interpreter)
     must print exactly the reference-derived models; no-fault trials
     (pre-decoded and translated paths, from snapshots) must end masked with
     the oracle's records; faulted trials must match the oracle bit for bit."""
@@ -352,7 +353,8 @@ def test_known_answer_programs(oracle_mod, prog):
                      "sys": (kat.sys_program_elf, kat.sys_program_expected),
                      "lrsc": (kat.lrsc_program_elf, kat.lrsc_program_expected),
                      "vm": (kat.vm_program_elf, kat.vm_program_expected),
-                     "fp": (kat.fp_program_elf, kat.fp_program_expected)}[prog]
+                     "fp": (kat.fp_program_elf, kat.fp_program_expected),
+                     "rnd": (kat.rnd_program_elf, kat.rnd_program_expected)}[prog]
     if prog == "fp" and not oracle_mod.has_softfloat():
         pytest.skip("oracle without the reference SoftFloat")
     stderr = {"sys": kat.SYS_STDERR, "vm": kat.VM_STDERR}.get(prog, b"")

@@ -1283,3 +1283,76 @@ def test_fp_known_values():
         assert (v == npop(x, y).view(np.uint64)).all()
     v, _ = sf_ref(4, 2, 0, np.abs(x).view(np.uint64))
     assert (v == np.sqrt(np.abs(x)).view(np.uint64)).all()
+
+
+# getrandom and clock_gettime (oracle/rv64se.c; syscall_emul.hh:3222-3236 and
+# 2266-2278): the bytes are gem5's Random(5489) stream (std::mt19937_64)
+# % 255 -- the first 12 draws below from the C++ standard library's
+# std::mt19937_64(5489u); clock_gettime reports curTick in ns + 1e9 s, so two
+# calls K uncompressed instructions (K ticks) apart differ by K x 500 / 1000 ns
+# at the default 2 GHz.
+RND_BYTES = bytes([175, 33, 200, 247, 86])
+CLK_GAP = 40
+
+
+def rnd_program_source() -> str:
+    gap = "\n".join(["    addi  t3, t3, 1"] * (CLK_GAP - 2))
+    return f"""    .text
+_start:
+    la    s2, out
+    mv    a0, s2
+    li    a1, 5
+    li    a2, 0
+    li    a7, 278
+    ecall
+    sd    a0, 8(s2)
+    li    a0, 0
+    addi  a1, s2, 16
+    li    a7, 113
+    ecall
+{gap}
+    addi  a1, s2, 32
+    ecall
+    li    a0, 1
+    mv    a1, s2
+    li    a2, 48
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 93
+    ecall
+    .bss
+    .balign 8
+out:
+    .zero 48
+"""
+
+
+def rnd_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(rnd_program_source(), compress=False)
+
+
+def rnd_check(out: bytes):
+    assert out[:5] == RND_BYTES and out[5:8] == bytes(3)
+    assert int.from_bytes(out[8:16], "little") == 5
+    s1, n1, s2, n2 = (int.from_bytes(out[k:k + 8], "little") for k in (16, 24, 32, 40))
+    assert s1 == s2 == 10**9
+    assert n2 - n1 == CLK_GAP * 500 // 1000
+
+
+def test_rnd_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(rnd_program_elf(), "rnd")
+    g = o.run_golden()
+    assert g.exit_code == 0
+    rnd_check(o.golden_stdout())
+
+
+def rnd_program_expected() -> bytes:
+    """The oracle's output for the rnd program, itself checked by rnd_check."""
+    from oracle import pyoracle
+    o = pyoracle.Oracle(rnd_program_elf(), "rnd")
+    o.run_golden()
+    out = o.golden_stdout()
+    rnd_check(out)
+    return out
