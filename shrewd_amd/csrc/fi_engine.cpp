@@ -86,6 +86,11 @@ struct fi_engine {
     PageEnt *d_tab = nullptr;
     uint8_t *d_pool = nullptr;
     uint64_t snap_I = 1ULL << 62;
+    // memory liveness index of the golden run (build_mem_index)
+    bool mem_live = false;
+    uint32_t mw_n = 0;
+    uint64_t *d_mw_addr = nullptr, *d_mw_ev = nullptr;
+    uint32_t *d_mw_off = nullptr;
     bool pre_ok = true;
     // load-time build of the trial kernel with the translated golden blocks
     hipModule_t tx_mod = nullptr;
@@ -240,6 +245,11 @@ static void free_work(fi_engine *e) {
     e->cap = 0;
 }
 static void free_snaps(fi_engine *e) { dfree(e->d_snaps); dfree(e->d_tab); dfree(e->d_pool); }
+static void free_mem_index(fi_engine *e) {
+    dfree(e->d_mw_addr); dfree(e->d_mw_off); dfree(e->d_mw_ev);
+    e->mw_n = 0;
+    e->mem_live = false;
+}
 static void free_tx(fi_engine *e) {
     if (e->tx_mod) (void)hipModuleUnload(e->tx_mod);
     e->tx_mod = nullptr;
@@ -249,6 +259,7 @@ static void free_image(fi_engine *e) {
     dfree(e->d_pre); dfree(e->d_zero); dfree(e->d_sink);
     dfree(e->d_text); dfree(e->d_mem_pages); dfree(e->d_gout); dfree(e->d_gerr);
     free_snaps(e);
+    free_mem_index(e);
     free_tx(e);
     e->have_golden = false;
     e->loaded = false;
@@ -536,6 +547,8 @@ static DevCtx base_ctx(fi_engine *e) {
     c.simt_min = (e->cfg.flags & FI_CFG_SIMT) ? 8u : 0u;
     c.rnd_tab = e->d_rnd; c.rnd_len = e->d_rnd ? kRndLen : 0; c.clk_period = e->clk_period;
     c.lanes = e->cfg.lanes_per_wave;
+    c.mem_live = (e->mem_live && !(e->cfg.flags & FI_CFG_NO_EARLY_EXIT)) ? 1 : 0;
+    c.mw_n = e->mw_n; c.mw_addr = e->d_mw_addr; c.mw_off = e->d_mw_off; c.mw_ev = e->d_mw_ev;
     return c;
 }
 
@@ -543,7 +556,8 @@ static DevCtx base_ctx(fi_engine *e) {
 // P private pages; rec_* capture snapshots every rec_I instructions (0 = off).
 static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_t rec_max, SnapState *d_rs,
                                uint8_t *d_rp, uint64_t *d_rv, uint32_t *d_trace, uint32_t trace_cap, uint8_t *d_ro,
-                               uint8_t *d_re, uint64_t rec_cap, fi_outcome &o, unsigned long long *stats) {
+                               uint8_t *d_re, uint64_t rec_cap, fi_outcome &o, unsigned long long *stats,
+                               MemEv *d_mem = nullptr, uint32_t mem_cap = 0) {
     uint8_t *d_gpriv = nullptr;
     uint64_t *d_gvpn = nullptr;
     HIPCHK(hipMalloc(&d_gpriv, (uint64_t)P * kPage));
@@ -560,6 +574,8 @@ static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_
     c.priv_pages = P; c.priv_frames = d_gpriv; c.priv_vpn = d_gvpn;
     c.rec_snaps = d_rs; c.rec_pages = d_rp; c.rec_vpns = d_rv; c.rec_interval = rec_I; c.rec_max_snaps = rec_max;
     c.rec_trace = d_trace; c.rec_trace_cap = d_trace ? trace_cap : 0;
+    c.rec_mem = d_mem; c.rec_mem_cap = d_mem ? mem_cap : 0;
+    c.mem_live = 0;
     c.out = e->d_out;
     c.n = 1;
     c.n_slots = 1;
@@ -581,6 +597,52 @@ static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_
     if (o.cls != FI_MASKED)
         return fail(e, FI_E_GOLDEN, "golden run did not exit normally (class %u sub %u detail %#x after %llu insts)",
                     o.cls, o.sub, o.detail, (unsigned long long)o.ninst);
+    return FI_OK;
+}
+
+// Memory liveness index (DevCtx::mw_*): the golden run's data accesses split
+// into 8-byte words, per word in time order as numInst << 16 | bytes read << 8
+// | bytes written.  A trial's memory fault looks its word up at injection
+// (fi_trial.hip:mem_dead).  complete = the access trace did not overflow and
+// every golden instruction came from the pre-decoded text.
+static fi_status build_mem_index(fi_engine *e, const std::vector<MemEv> &mev, bool complete) {
+    free_mem_index(e);
+    if (!complete) return FI_OK;
+    std::vector<std::pair<uint64_t, uint64_t>> ent;   // (word, event)
+    const uint64_t kMaxEnt = 1ULL << 26;
+    for (const MemEv &ev : mev) {
+        const uint64_t len = ev.len_kind & ((1u << 30) - 1), kind = ev.len_kind >> 30;
+        const uint64_t end = ev.addr + len;
+        if (end < ev.addr) return FI_OK;
+        for (uint64_t a = ev.addr; a < end;) {
+            const uint64_t wd = a & ~7ULL, we = std::min(end, wd + 8);
+            uint64_t bm = 0;
+            for (uint64_t b = a; b < we; b++) bm |= 1ULL << (b - wd);
+            ent.emplace_back(wd, ((uint64_t)ev.t << 16) | ((kind & 1) ? bm << 8 : 0) | ((kind & 2) ? bm : 0));
+            if (ent.size() > kMaxEnt) return FI_OK;
+            a = we;
+        }
+    }
+    std::stable_sort(ent.begin(), ent.end(), [](const auto &x, const auto &y) { return x.first < y.first; });
+    std::vector<uint64_t> addr, evs;
+    std::vector<uint32_t> off;
+    evs.reserve(ent.size());
+    for (size_t i = 0; i < ent.size(); i++) {
+        if (i == 0 || ent[i].first != ent[i - 1].first) {
+            addr.push_back(ent[i].first);
+            off.push_back((uint32_t)i);
+        }
+        evs.push_back(ent[i].second);
+    }
+    off.push_back((uint32_t)ent.size());
+    HIPCHK(hipMalloc(&e->d_mw_addr, std::max<size_t>(addr.size(), 1) * 8));
+    HIPCHK(hipMalloc(&e->d_mw_off, off.size() * 4));
+    HIPCHK(hipMalloc(&e->d_mw_ev, std::max<size_t>(evs.size(), 1) * 8));
+    if (!addr.empty()) HIPCHK(hipMemcpy(e->d_mw_addr, addr.data(), addr.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(e->d_mw_off, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+    if (!evs.empty()) HIPCHK(hipMemcpy(e->d_mw_ev, evs.data(), evs.size() * 8, hipMemcpyHostToDevice));
+    e->mw_n = (uint32_t)addr.size();
+    e->mem_live = true;
     return FI_OK;
 }
 
@@ -659,9 +721,13 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     const uint32_t trace_cap = (uint32_t)std::min<uint64_t>(o.ninst + 4096, 1ULL << 26);
     uint32_t *d_trace = nullptr;
     HIPCHK(hipMalloc(&d_trace, (uint64_t)trace_cap * 4));
+    // and its data accesses for the memory liveness index
+    const uint32_t mem_cap = (uint32_t)std::min<uint64_t>(2 * o.ninst + 4096, 1ULL << 24);
+    MemEv *d_mem = nullptr;
+    HIPCHK(hipMalloc(&d_mem, (uint64_t)mem_cap * sizeof(MemEv)));
     fi_outcome o2;
     st = golden_launch(e, P, I, rec_max, d_rs, d_rp, d_rv, d_trace, trace_cap, d_rec_out, d_rec_err, rec_cap, o2,
-                       stats);
+                       stats, d_mem, mem_cap);
     (void)hipFree(d_rec_out);
     (void)hipFree(d_rec_err);
     std::vector<SnapState> rs;
@@ -680,6 +746,14 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         if (err != hipSuccess) st = fail(e, FI_E_HIP, "trace download: %s", hipGetErrorString(err));
     }
     (void)hipFree(d_trace);
+    const uint64_t n_mem = stats[25];
+    std::vector<MemEv> mev;
+    if (!st && n_mem <= mem_cap) {
+        mev.resize(n_mem);
+        hipError_t err = n_mem ? hipMemcpy(mev.data(), d_mem, n_mem * sizeof(MemEv), hipMemcpyDeviceToHost) : hipSuccess;
+        if (err != hipSuccess) st = fail(e, FI_E_HIP, "access trace download: %s", hipGetErrorString(err));
+    }
+    (void)hipFree(d_mem);
     if (!st) {
         ns = (uint32_t)std::min<unsigned long long>(stats[13], rec_max);
         rs.resize(ns);
@@ -759,6 +833,8 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     e->tab = tab;
     e->snap_I = I;
     st = upload_snaps(e);
+    if (st) return st;
+    st = build_mem_index(e, mev, live_ok && n_mem <= mem_cap);
     if (st) return st;
 
     // ---- translate the golden basic blocks and build the trial kernel with

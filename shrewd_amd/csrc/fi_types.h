@@ -81,6 +81,15 @@ struct VmState {
     uint64_t vma[kMaxVma][2];
 };
 
+// One data access of the golden run (record mode): bytes [addr, addr + len)
+// read (kind 1), written (2) or read then written (3, an AMO) by the
+// instruction (or syscall) at numInst == t.
+struct MemEv {
+    uint64_t addr;
+    uint32_t t;
+    uint32_t len_kind;               // len (< 2^30) | kind << 30
+};
+
 // Everything one launch of the trial kernel needs.  Passed by value as the
 // kernel argument (lives in the kernarg segment -> scalar loads).
 constexpr int kNStats = 40;          // DevCtx::stats entries
@@ -158,7 +167,17 @@ struct DevCtx {
     uint64_t rnd_len;
     uint64_t clk_period;             // ticks per CPU cycle (clock_gettime)
     uint32_t simt_min;               // diverged-lanes step loop: least lanes to enter it (0 = off)
-    unsigned long long *stats;       // [0] fetch B [1] data B [2] pages [3..5] golden ncycles/out/err
+    // memory liveness: record mode appends the golden run's data accesses to
+    // rec_mem; trials look a memory fault's word up in the per-word index built
+    // from them (fi_engine.cpp:build_mem_index)
+    MemEv *rec_mem;
+    uint32_t rec_mem_cap;
+    uint32_t mem_live;               // 1 = the index below is complete: dead memory faults end at injection
+    uint32_t mw_n;                   // words in the index
+    const uint64_t *mw_addr;         // [mw_n] sorted 8-byte-aligned addresses the golden run accesses
+    const uint32_t *mw_off;          // [mw_n + 1] each word's events in mw_ev
+    const uint64_t *mw_ev;           // per word in time order: numInst << 16 | bytes read << 8 | bytes written
+    unsigned long long *stats;     // [0] fetch B [1] data B [2] pages [3..5] golden ncycles/out/err
                                      // [6] loop iterations [7] lane-insts [8] slow fetches [9] min-PC [10] max iter/wave
                                      // [11] early-exit checks [12] early exits [13] snapshots captured [14] start-inst sum
                                      // [15] golden trace events [16] translated insts [17] translated entries
@@ -167,6 +186,7 @@ struct DevCtx {
                                      // [22] golden run holds state outside the snapshots (FP, LR/SC, VM)
                                      // [23] instructions executed on the device
                                      // [24] lane-instructions of the diverged-lanes step loop
+                                     // [25] golden data-access events [26] memory faults ended at injection
                                      // [32..39] FI_PROF phase cycles
 };
 

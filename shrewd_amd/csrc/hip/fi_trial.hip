@@ -721,6 +721,54 @@ __device__ __forceinline__ void finish(Lane &L, int cls, int sub, int code, uint
     L.res.ninst = L.ninst;
 }
 
+// Record mode: one data access of the golden run (the host builds the memory
+// liveness index from them).  Not in the load-time build: the golden run is
+// over before it exists.
+__device__ __forceinline__ void rec_mem(KCtx *c, uint64_t a, uint64_t n, uint64_t t, uint32_t kind) {
+#ifndef FI_TX
+    while (n && kind) {
+        const uint64_t k = n < (1u << 29) ? n : (1u << 29);
+        const unsigned long long i = atomicAdd(&c->stats[25], 1ull);
+        if (i < c->rec_mem_cap) {
+            MemEv ev;
+            ev.addr = a; ev.t = (uint32_t)t; ev.len_kind = (uint32_t)k | (kind << 30);
+            c->rec_mem[i] = ev;
+        }
+        a += k; n -= k;
+    }
+#endif
+}
+
+// A memory fault (8-byte word at addr, xor mask, at numInst t) is dead when
+// the golden run from t on never reads a flipped byte before writing it: the
+// trial then executes exactly the golden run (a machine that differs only in
+// bytes no instruction or syscall reads behaves identically), so its outcome
+// is the golden one.  Instruction bytes are never dead (fetches are not in the
+// index).
+__device__ __noinline__ bool mem_dead(const KCtx *c, uint64_t addr, uint64_t mask, uint64_t t) {
+    if (addr < c->text_hi && addr + 8 > c->text_lo) return false;
+    uint32_t fb = 0;
+    for (int b = 0; b < 8; b++) fb |= ((mask >> (8 * b)) & 0xFF) ? (1u << b) : 0u;
+    uint32_t lo = 0, hi = c->mw_n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (c->mw_addr[mid] < addr) lo = mid + 1; else hi = mid;
+    }
+    if (lo == c->mw_n || c->mw_addr[lo] != addr) return true;   // never accessed again... or at all
+    uint32_t a = c->mw_off[lo], b = c->mw_off[lo + 1];
+    while (a < b) {   // first event at numInst >= t
+        const uint32_t mid = (a + b) >> 1;
+        if ((c->mw_ev[mid] >> 16) < t) a = mid + 1; else b = mid;
+    }
+    for (const uint32_t e = c->mw_off[lo + 1]; a < e; a++) {
+        const uint64_t ev = c->mw_ev[a];
+        if ((ev >> 8) & fb & 0xFF) return false;   // read while flipped
+        fb &= ~(uint32_t)ev & 0xFF;                // overwritten: the golden value again
+        if (!fb) return true;
+    }
+    return true;
+}
+
 #define RREG(r) R[(uint32_t)(r) * kNL + lane]
 
 // The syscall path of one lane: EmuLinux::syscall (se_workload.cc:95-106)
@@ -748,6 +796,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         uint8_t *rec = fd == 1 ? c->rec_out : c->rec_err;
         uint64_t cur_vpn = kNone;
         const uint8_t *pg = nullptr;
+        if (c->record) rec_mem(c, buf, n, L.ninst, 1u);
         for (uint64_t i = 0; i < n; i++) {
             const uint64_t a = buf + i;
             if ((a >> 12) != cur_vpn) { cur_vpn = a >> 12; pg = page_of(lookup(c, w, m, slot, cur_vpn)); }
@@ -762,11 +811,16 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         pos += n;
     };
     auto rd64 = [&](uint64_t a) {
+        if (c->record) rec_mem(c, a, 8, L.ninst, 1u);
         uint64_t v = 0;
         for (int k = 0; k < 8; k++) v |= (uint64_t)proxy_byte(c, w, m, slot, a + k) << (8 * k);
         return v;
     };
     auto set_ret = [&](int64_t v) { RREG(10) = (uint64_t)v; };
+    auto pwrite = [&](uint64_t a, const char *src, uint64_t n) {
+        if (c->record) rec_mem(c, a, n, L.ninst, 2u);
+        return proxy_write(c, w, m, slot, a, src, n);
+    };
     switch (num) {
     case 93: case 94: {  // exitImpl -> exitSimLoop(status & 0xff), sim/syscall_emul.cc:120-248
         const int code = (int)(uint32_t)a0 & 0xff;
@@ -900,7 +954,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         if (!rlp) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }   // null ProxyPtr
         char b[16];
         for (int k = 0; k < 8; k++) b[k] = b[8 + k] = (char)(lim >> (8 * k));
-        if (!proxy_write(c, w, m, slot, rlp, b, 16)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        if (!pwrite(rlp, b, 16)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
         set_ret(0);
         return rlp < c->code_hi && rlp + 16 > c->code_lo;
     }
@@ -912,7 +966,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         if (h == 0) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
         if (h == -1) { finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, pc32); return false; }
         if (h == -2) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
-        if (!proxy_write(c, w, m, slot, a0, (const char *)(c->rnd_tab + v->rnd_pos), a1)) {
+        if (!pwrite(a0, (const char *)(c->rnd_tab + v->rnd_pos), a1)) {
             finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32);
             return false;
         }
@@ -927,7 +981,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         const uint64_t sec = ns / 1000000000ULL + 1000000000ULL, nsec = ns % 1000000000ULL;
         char b[16];
         for (int k = 0; k < 8; k++) { b[k] = (char)(sec >> (8 * k)); b[8 + k] = (char)(nsec >> (8 * k)); }
-        if (!proxy_write(c, w, m, slot, a1, b, 16)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        if (!pwrite(a1, b, 16)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
         set_ret(0);
         return a1 < c->code_hi && a1 + 16 > c->code_lo;
     }
@@ -940,7 +994,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         for (int k = 0; k < 5; k++) {
             uint64_t n = 0;
             while (f[k][n]) n++;
-            if (!proxy_write(c, w, m, slot, a0 + 65 * k, f[k], n + 1)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            if (!pwrite(a0 + 65 * k, f[k], n + 1)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
         }
         set_ret(0);
         return a0 < c->code_hi && a0 + 325 > c->code_lo;
@@ -1343,6 +1397,16 @@ __device__ __forceinline__ void trial_body() {
                 const uint64_t p = lookup(CX, w, m, slot, s.addr >> 12);
                 if (!p) {
                     L.injected = 2;    // page not mapped at t: nothing to flip
+                    if (CX->mem_live) {   // ... so the trial is the golden run
+                        finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
+                        L.res.ninst = CX->gninst;
+                        atomicAdd(&CX->stats[26], 1ull);
+                    }
+                } else if (CX->mem_live && mem_dead(CX, s.addr, s.mask, L.ninst)) {
+                    L.injected = 1;
+                    finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
+                    L.res.ninst = CX->gninst;
+                    atomicAdd(&CX->stats[26], 1ull);
                 } else if (!(p & 1)) {
                     m.req_vpn = s.addr >> 12; m.req_src = page_of(p);   // copy-on-write first, flip next iteration
                 } else {
@@ -1926,6 +1990,7 @@ __device__ __forceinline__ void trial_body() {
                     const bool code_st = st && !(ea >= tx.chi || ea + msz <= tx.clo);
                     const bool ok = p && (!st || ((p & 1) && (kNL == 1 || !code_st))) && off + msz <= 4096;
                     if (wballot<kNL>(mine && !ok) != 0) { msz = 0xFFFFFFFFu; break; }   // bail: general path
+                    if (CX->record && mine) rec_mem(CX, ea, msz, L.ninst + steps, st ? 2u : 1u);
                     if constexpr (kNL == 1) {
                         if (code_st) {
                             mark_dirty(m, ea, ea + msz);
@@ -2365,6 +2430,8 @@ __device__ __forceinline__ void trial_body() {
                 if (!pass) old = t;
             }
             if (f == F_NONE) {
+                if (CX->record)   // an AMO reads, then writes; a failed SC touches nothing
+                    rec_mem(CX, ea, msz, L.ninst, amo >= 0 ? 3u : llsc == 2 ? (t ? 2u : 0u) : (mst ? 2u : 1u));
                 if (mst || amo >= 0 || (llsc == 2 && t)) DC_INVAL(ea, msz);   // rewritten code: drop its cached decodes
                 if (llsc != 2 || t) L.data_b += amo >= 0 ? 2 * msz : msz;
                 if (amo >= 0) v = msz == 4 ? sx32(old) : old;

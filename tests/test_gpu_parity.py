@@ -210,6 +210,20 @@ def test_translated_path_active(engine_factory, name):
     assert int(st[16]) > 0 and int(st[17]) > 0   # translated instructions, block entries
 
 
+def test_dead_memory_faults_end_at_injection(engine_factory, oracle_mod):
+    """A memory fault on bytes the golden run never reads again before writing
+    them ends at injection as the golden run (the golden run's access index,
+    fi_trial.hip:mem_dead); the outcomes still equal the oracle's full runs,
+    and the shortcut is really taken."""
+    e = engine_factory("crc32")
+    o = oracle_for(oracle_mod, "crc32")
+    e.set_campaign(0x5EED0D0D, MEM, 2)
+    sites = e.sample(0, 4000)
+    dev, _ = e.run_sites(sites)
+    assert int(e.debug_stats()[26]) > 1000
+    compare(dev, o.run_trials(sites), sites)
+
+
 PATH_FLAGS = {
     "default": 0,
     "no_translate": 4,                      # FI_CFG_NO_TRANSLATE: interpreter only

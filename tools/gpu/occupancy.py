@@ -1,6 +1,6 @@
 """Residency timeline of the last dispatch of a campaign (the solo epoch by
 default): per-wave start/end s_memrealtime stamps -> waves resident over time.
-python tools/gpu/occupancy.py [WORKLOAD] [SEED] [N] [FLAGS]"""
+python tools/gpu/occupancy.py [WORKLOAD] [SEED] [N] [FLAGS] [STRUCTURES] [BURST]"""
 import json
 import os
 import sys
@@ -15,10 +15,12 @@ name = sys.argv[1] if len(sys.argv) > 1 else "qsort"
 seed = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0x5EED0003
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 100000
 flags = int(sys.argv[4], 0) if len(sys.argv) > 4 else 0
+structures = int(sys.argv[5], 0) if len(sys.argv) > 5 else REGS_PC
+burst = int(sys.argv[6]) if len(sys.argv) > 6 else 1
 e = Engine(max_trials_per_launch=n, flags=flags)
 e.load_elf(open(os.path.join(ROOT, "workloads", f"{name}.elf"), "rb").read(), [name])
 e.golden_run()
-e.set_campaign(seed, REGS_PC, 1)
+e.set_campaign(seed, structures, burst)
 sites = e.sample(0, n)
 for rep in range(2):
     e.kernel_timer_reset()
@@ -37,7 +39,7 @@ span = tt[-1] - tt[0]
 avg = float((conc * dur).sum() / span) if span else 0.0
 q = {f"t_conc_below_{k}_us": float(tt[np.nonzero(conc >= k)[0][-1]]) if (conc >= k).any() else 0.0
      for k in (3000, 1000, 300, 100, 30, 10, 1)}
-print(json.dumps({"workload": name, "flags": flags, "dispatch_ms": e.debug_dispatch_ms(), "waves": int(live.sum()),
+print(json.dumps({"workload": name, "flags": flags, "structures": hex(structures), "burst": burst, "dispatch_ms": e.debug_dispatch_ms(), "waves": int(live.sum()),
                   "span_us": round(float(span), 1), "max_resident": int(conc.max()), "avg_resident": round(avg, 1),
                   "last_start_us": round(float(st.max()), 1),
                   "start_quantiles_us": {p: round(float(np.quantile(st, p)), 1) for p in (0.1, 0.5, 0.9, 0.99)},
