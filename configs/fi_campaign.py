@@ -31,6 +31,11 @@ def parse(argv=None):
     ap.add_argument("--bits", default="", help="eligible lowest flipped bit positions: mask or ranges, e.g. 0-31,63")
     ap.add_argument("--protect-mask", type=lambda s: int(s, 0), default=0)
     ap.add_argument("--protect-opclasses", default="", help="comma list of gem5 OpClass names (IntAlu,IntMult,...)")
+    ap.add_argument("--shadow-fu-model", action="store_true",
+                    help="SHREWD FU contention: replicate only where the shadow finds a free unit")
+    ap.add_argument("--priority-to-shadow", action="store_true", help="BaseO3CPU.priorityToShadow")
+    ap.add_argument("--issue-width", type=int, default=8)
+    ap.add_argument("--load-latency", type=int, default=2)
     ap.add_argument("--num-gpus", type=int, default=1)
     ap.add_argument("--max-insts-factor", type=float, default=2.0)
     ap.add_argument("--private-pages", type=int, default=16)
@@ -49,7 +54,9 @@ def run_gem5(a):
                          trials=a.trials, first_trial=a.first_trial, seed=a.seed,
                          structures=_split(a.structures), bits=a.bits or "0-63", burst=a.burst,
                          protect_mask=a.protect_mask,
-                         protect_opclasses=_split(a.protect_opclasses), num_gpus=a.num_gpus, max_insts_factor=a.max_insts_factor,
+                         protect_opclasses=_split(a.protect_opclasses), shadow_fu_model=a.shadow_fu_model,
+                         priority_to_shadow=a.priority_to_shadow, issue_width=a.issue_width,
+                         load_latency=a.load_latency, num_gpus=a.num_gpus, max_insts_factor=a.max_insts_factor,
                          private_pages=a.private_pages, output=a.output)
     root = Root(full_system=False, campaign=camp)
     m5.instantiate()
@@ -76,7 +83,9 @@ def run_ctypes(a):
                       seed=a.seed, structures=_split(a.structures), burst=a.burst, protect_mask=a.protect_mask,
                       num_gpus=max(a.num_gpus, world), max_insts_factor=a.max_insts_factor, output=a.output,
                       device=local, private_pages=a.private_pages,
-                      protect_opclasses=_split(a.protect_opclasses), bits=a.bits or None)
+                      protect_opclasses=_split(a.protect_opclasses), bits=a.bits or None,
+                      shadow_fu_model=a.shadow_fu_model, priority_to_shadow=a.priority_to_shadow,
+                      issue_params={"issue_width": a.issue_width, "load_latency": a.load_latency})
     t0 = time.perf_counter()
     c.run(first_trial=a.first_trial)
     dt = time.perf_counter() - t0

@@ -211,6 +211,88 @@ fi_status fi_set_protect(fi_engine *e, uint64_t protect_mask);
  * are replicated; a result fault (FI_T_RESULT) on one is detected. */
 fi_status fi_set_protect_opclasses(fi_engine *e, uint64_t opclass_mask);
 
+/* ---- SHREWD functional-unit contention.
+ *
+ * In the reference a shadow copy is issued only when FUPool::getUnit(cap,
+ * is_shadow=true) finds a free unit in the issue cycle
+ * (src/cpu/o3/inst_queue.cc:835-1066 scheduleReadyInsts, :1082-1181
+ * requestShadow; src/cpu/o3/fu_pool.cc:155-301 findFreeUnit/getUnit), either
+ * before the next instruction takes its unit (BaseO3CPU.priorityToShadow) or
+ * after the whole issue group (the default, "deferred").  The issue model
+ * replays the golden run's committed instructions through an O3 issue stage
+ * with the reference's FU pool and widths and records, per dynamic
+ * instruction, whether its shadow got a unit.  With the model on, a result
+ * fault (FI_T_RESULT) on a protected instruction is detected only if that
+ * instruction's shadow was issued.
+ *
+ * What is the reference's code, restated exactly: the pool (DefaultFUPool,
+ * src/cpu/o3/FUPool.py:52-66; counts, latencies and pipelining of
+ * src/cpu/o3/FuncUnitConfig.py:45-198), the per-capability round-robin unit
+ * queues, the shadow substitutions (IntAlu -> FloatAdd -> FloatCmp, IntMult
+ * -> FloatMult, IntDiv -> FloatDiv, FloatAdd/Mult/Div/Sqrt -> IntAlu; no
+ * shadow unit for memory and other classes), the unit release rules (next
+ * cycle, or after op_latency for unpipelined classes; priority mode raises the
+ * primary's latency to the shadow's), the age-ordered issue over ready
+ * instructions with a class skipped for the rest of the cycle once it finds no
+ * free unit, and issueWidth.  What is a model (no O3 pipeline runs here): the
+ * schedule of ready instructions.  Cycle c: (1) units released at c are
+ * freed; (2) up to commit_width oldest ops with done <= c commit; (3) issue
+ * walks the IQ oldest first: an op is ready when it was dispatched before c,
+ * every source register's latest older writer has done <= c, and (for a
+ * serialising op) every older op has committed; done = issue + latency
+ * (loads: issue + load_latency); (4) up to dispatch_width ops enter the IQ
+ * and ROB in program order while both have room and no older serialising op
+ * is uncommitted.  Non-memory ops leave the IQ at issue, memory ops at done.
+ * Perfect branch prediction, no wrong-path work, no memory dependences. */
+typedef struct {
+    uint32_t issue_width;        /* BaseO3CPU.issueWidth (src/cpu/o3/BaseO3CPU.py:128): 8 */
+    uint32_t dispatch_width;     /* dispatchWidth (:127): 8 */
+    uint32_t commit_width;       /* commitWidth (:136): 8 */
+    uint32_t iq_entries;         /* numIQEntries (:193): 64 */
+    uint32_t rob_entries;        /* numROBEntries (:194): 192 */
+    uint32_t load_latency;       /* model: cycles from a load's issue to its value: 2 */
+    uint32_t priority_to_shadow; /* BaseO3CPU.priorityToShadow (:227): 0 */
+    uint32_t fu_count[6];        /* IntALU, IntMultDiv, FP_ALU, FP_MultDiv, RdWrPort, IprPort
+                                    (FuncUnitConfig.py): 6, 2, 4, 2, 4, 1 */
+} fi_issue_params;
+
+/* One dynamic instruction of the replayed trace. */
+typedef struct {
+    uint64_t src;      /* bit r (1..31): reads x_r; bit 32: reads the FP state */
+    uint64_t dst;      /* bit r: writes x_r; bit 32: writes the FP state */
+    uint8_t opclass;   /* gem5 OpClass enum value (src/cpu/FuncUnit.py:43) */
+    uint8_t kind;      /* FI_ISSUE_* */
+    uint8_t pad[6];
+} fi_issue_op;
+#define FI_ISSUE_PLAIN 0
+#define FI_ISSUE_LOAD 1     /* value at issue + load_latency; holds its IQ entry until then */
+#define FI_ISSUE_STORE 2    /* holds its IQ entry until done */
+#define FI_ISSUE_SERIAL 3   /* ecall: issues only as the oldest op; younger ops dispatch after it commits */
+
+/* Counters named after the reference's iqIOStats (inst_queue.cc:1082-1181). */
+typedef struct {
+    uint64_t ops, cycles;                  /* ops replayed; cycle at which the last one committed */
+    uint64_t shadow_available, shadow_not_available;
+    uint64_t shadow_same_fu, shadow_not_same_fu;
+    uint64_t class_available[12];          /* per OpClass 0..11 (IntAlu..FloatSqrt at 1..11) */
+    uint64_t class_not_available[12];
+} fi_issue_stats;
+
+/* Defaults listed above. */
+void fi_issue_default_params(fi_issue_params *p);
+/* Pure host function (no device, no engine): replay ops[0..n) and write
+ * shadow[i] = 1 if op i's shadow was issued (the reference's has_shadow). */
+fi_status fi_issue_model_run(const fi_issue_op *ops, uint64_t n, const fi_issue_params *p, uint8_t *shadow,
+                             fi_issue_stats *stats);
+/* Turn the model on for this engine's result faults (p = NULL: off, every
+ * protected shadow-capable instruction is replicated, as without O3 timing).
+ * Needs a golden run; computed at once from the golden trace. */
+fi_status fi_set_issue_model(fi_engine *e, const fi_issue_params *p);
+/* The engine's map: shadow[k] for the k-th committed golden instruction
+ * (numInst index; ecalls, which numInst does not count, are left out).
+ * *n = golden ninst; stats may be NULL. */
+fi_status fi_shadow_map(fi_engine *e, uint8_t *shadow, uint64_t cap, uint64_t *n, fi_issue_stats *stats);
+
 fi_status fi_sample_sites(fi_engine *e, uint64_t first_trial, uint64_t n, fi_site *out);
 /* out (n entries, trial order) and hist may be NULL. hist is accumulated into (+=). */
 fi_status fi_run_trials(fi_engine *e, uint64_t first_trial, uint64_t n, fi_outcome *out, fi_histogram *hist);

@@ -30,6 +30,51 @@ class Probe(C.Structure):
                 ("len", C.c_uint32), ("op", C.c_uint32)]
 
 
+class IssueParams(C.Structure):
+    _fields_ = [("issue_width", C.c_uint32), ("dispatch_width", C.c_uint32), ("commit_width", C.c_uint32),
+                ("iq_entries", C.c_uint32), ("rob_entries", C.c_uint32), ("load_latency", C.c_uint32),
+                ("priority_to_shadow", C.c_uint32), ("fu_count", C.c_uint32 * 6)]
+
+
+class IssueStats(C.Structure):
+    _fields_ = [("ops", C.c_uint64), ("cycles", C.c_uint64), ("shadow_available", C.c_uint64),
+                ("shadow_not_available", C.c_uint64), ("shadow_same_fu", C.c_uint64),
+                ("shadow_not_same_fu", C.c_uint64), ("class_available", C.c_uint64 * 12),
+                ("class_not_available", C.c_uint64 * 12)]
+
+
+ISSUE_OP_DT = np.dtype([("src", "<u8"), ("dst", "<u8"), ("opclass", "u1"), ("kind", "u1"), ("pad", "u1", (6,))])
+FU_NAMES = ("IntALU", "IntMultDiv", "FP_ALU", "FP_MultDiv", "RdWrPort", "IprPort")
+
+
+def issue_params(**kw) -> IssueParams:
+    """The reference's O3 defaults (o3/BaseO3CPU.py:127-194, FuncUnitConfig.py)
+    plus a 2-cycle load; overrides by field name or FU name."""
+    p = IssueParams(8, 8, 8, 64, 192, 2, 0)
+    for i, c in enumerate((6, 2, 4, 2, 4, 1)):
+        p.fu_count[i] = c
+    for k, v in kw.items():
+        if k in FU_NAMES:
+            p.fu_count[FU_NAMES.index(k)] = int(v)
+        elif k == "fu_count":
+            for i, c in enumerate(v):
+                p.fu_count[i] = int(c)
+        else:
+            setattr(p, k, int(v))
+    return p
+
+
+def issue_model(ops: np.ndarray, params: IssueParams | None = None):
+    """or_issue_model -> (shadow uint8[n], IssueStats)"""
+    ops = np.ascontiguousarray(ops, ISSUE_OP_DT)
+    out = np.zeros(len(ops), np.uint8)
+    st = IssueStats()
+    if lib().or_issue_model(ops.ctypes.data, len(ops), C.byref(params or issue_params()), out.ctypes.data,
+                            C.byref(st)) != 0:
+        raise RuntimeError("or_issue_model: bad parameters")
+    return out, st
+
+
 def build():
     subprocess.run(["make", "-s", "-C", HERE], check=True)
 
@@ -64,6 +109,11 @@ def lib():
         L.or_sys_class.argtypes = [C.c_int]
         L.or_set_protect_opclasses.argtypes = [C.c_void_p, C.c_uint64]
         L.or_set_clock.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+        L.or_issue_model.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(IssueParams), C.c_void_p,
+                                     C.POINTER(IssueStats)]
+        L.or_set_issue_model.argtypes = [C.c_void_p, C.POINTER(IssueParams)]
+        L.or_shadow_map.restype = C.c_uint64
+        L.or_shadow_map.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(IssueStats)]
         L.or_sf_ref.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                 C.c_void_p, C.c_void_p]
         _lib = L
@@ -90,6 +140,22 @@ class Oracle:
     def set_protect_opclasses(self, mask: int):
         """SHREWD replication set: bit k = gem5 OpClass enum value k."""
         self.L.or_set_protect_opclasses(self.h, mask)
+
+    def set_issue_model(self, params: IssueParams | dict | None = None, **kw):
+        """SHREWD FU contention for result faults; None and no keywords: off."""
+        if params is None and not kw:
+            self.L.or_set_issue_model(self.h, None)
+            return
+        p = params if isinstance(params, IssueParams) else issue_params(**{**(params or {}), **kw})
+        if self.L.or_set_issue_model(self.h, C.byref(p)) != 0:
+            raise RuntimeError(self.L.or_error(self.h).decode())
+
+    def shadow_map(self):
+        n = self.L.or_shadow_map(self.h, None, 0, None)
+        out = np.zeros(n, np.uint8)
+        st = IssueStats()
+        self.L.or_shadow_map(self.h, out.ctypes.data, n, C.byref(st))
+        return out, st
 
     def run_golden(self, max_inst=1 << 32) -> Golden:
         g = Golden()

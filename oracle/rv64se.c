@@ -179,6 +179,9 @@ struct or_campaign {
     u64 *mem_pages;        /* writable pages at process start (memory fault candidates) */
     u64 n_mem_pages;
     u64 protect_opc;       /* SHREWD replication: OpClass mask (bit = FuncUnit.py enum value) */
+    uint8_t *shadow;       /* issue model on: shadow issued per golden numInst index (NULL: off) */
+    u64 n_shadow;
+    or_issue_stats_t issue_stats;
     /* golden */
     int have_golden;
     or_golden_t golden;
@@ -204,6 +207,8 @@ typedef struct {
     /* fault injection */
     const or_site_t *site; int injected; int watch; /* watch = protected flipped reg, -1 none */
     int rarm, wrote;      /* result fault armed (OR_T_RESULT); the executing instruction wrote x[rd] */
+    /* golden trace recording for the issue model (or_set_issue_model) */
+    or_issue_op_t *rec; u64 rec_n, rec_cap;
     /* LR/SC: the ISA's load reservation (isa.cc:1006-1064) and this context's
      * lock record in memory (abstract_mem.cc:258-345), as virtual addresses
      * (the SE page mapping is a per-page bijection); OR_NONE = none */
@@ -1821,13 +1826,271 @@ static int op_class(int op) {
     }
 }
 
+/* ------------------------------------------------ SHREWD FU contention */
+/* The O3 issue stage replayed over the golden run (include/fi_engine.h,
+ * "SHREWD functional-unit contention": what is restated from the reference
+ * and what is a model).  Written from the reference, independently of
+ * shrewd_amd/csrc/fi_issue.cpp: a plain cycle loop over arrays. */
+enum { OC_NONE = 0, OC_INTALU = 1, OC_INTMULT = 2, OC_INTDIV = 3, OC_FADD = 4, OC_FCMP = 5, OC_FCVT = 6,
+       OC_FMULT = 7, OC_FMULTACC = 8, OC_FDIV = 9, OC_FMISC = 10, OC_FSQRT = 11, OC_MEMREAD = 52,
+       OC_MEMWRITE = 53, OC_FMEMREAD = 54, OC_FMEMWRITE = 55, OC_IPR = 56, OC_N = 77 };
+/* fu_pool.hh:148-167 */
+enum { FU_NOSHADOW = -7, FU_NONEED = -3, FU_NOCAPABLE = -2, FU_NOFREE = -1 };
+
+typedef struct {
+    int nunits;
+    u64 busy_until[64];           /* unitBusy: busy while busy_until > now */
+    int cap_n[OC_N], cap_units[OC_N][16], cap_rr[OC_N];   /* fuPerCapList: FUIdxQueue */
+    int capable[OC_N], lat[OC_N], piped[OC_N];           /* capabilityList, maxOpLatencies, pipelined */
+} fupool_t;
+
+/* FUPool::FUPool over DefaultFUPool (o3/FUPool.py:52-66) with the counts of
+ * FuncUnitConfig.py (IntALU 6, IntMultDiv 2, FP_ALU 4, FP_MultDiv 2,
+ * RdWrPort 4, IprPort 1; SIMD/matrix/predicate units serve no scalar class). */
+static void fupool_init(fupool_t *P, const or_issue_params_t *p) {
+    static const struct { int desc, cls, lat, piped; } opdesc[] = {
+        {0, OC_INTALU, 1, 1},                                                    /* IntALU      :45-47 */
+        {1, OC_INTMULT, 3, 1}, {1, OC_INTDIV, 20, 0},                            /* IntMultDiv  :50-56 */
+        {2, OC_FADD, 2, 1}, {2, OC_FCMP, 2, 1}, {2, OC_FCVT, 2, 1},              /* FP_ALU      :59-65 */
+        {3, OC_FMULT, 4, 1}, {3, OC_FMULTACC, 5, 1}, {3, OC_FMISC, 3, 1},
+        {3, OC_FDIV, 12, 0}, {3, OC_FSQRT, 24, 0},                               /* FP_MultDiv  :68-76 */
+        {4, OC_MEMREAD, 1, 1}, {4, OC_MEMWRITE, 1, 1}, {4, OC_FMEMREAD, 1, 1}, {4, OC_FMEMWRITE, 1, 1},  /* RdWrPort */
+        {5, OC_IPR, 3, 0},                                                       /* IprPort     :196-198 */
+    };
+    memset(P, 0, sizeof *P);
+    for (int k = 0; k < OC_N; k++) P->piped[k] = 1;
+    for (int d = 0; d < 6; d++) {
+        int n = (int)p->fu_count[d];
+        if (n <= 0) continue;
+        if (n > 8) n = 8;
+        for (unsigned j = 0; j < sizeof opdesc / sizeof opdesc[0]; j++) {
+            if (opdesc[j].desc != d) continue;
+            int c = opdesc[j].cls;
+            P->capable[c] = 1;
+            for (int k = 0; k < n; k++) P->cap_units[c][P->cap_n[c]++] = P->nunits + k;
+            if (opdesc[j].lat > P->lat[c]) P->lat[c] = opdesc[j].lat;
+            if (!opdesc[j].piped) P->piped[c] = 0;
+        }
+        P->nunits += n;
+    }
+}
+
+/* FUPool::findFreeUnit (fu_pool.cc:155-173) */
+static int fu_find(fupool_t *P, int cls, u64 now) {
+    if (!P->cap_n[cls]) return FU_NOFREE;
+    int *rr = &P->cap_rr[cls];
+#define GETFU() (u = P->cap_units[cls][*rr], *rr = (*rr + 1 == P->cap_n[cls]) ? 0 : *rr + 1)
+    int u, start;
+    GETFU();
+    start = u;
+    while (P->busy_until[u] > now) {
+        GETFU();
+        if (u == start) return FU_NOFREE;
+    }
+#undef GETFU
+    return u;
+}
+
+/* FUPool::getUnit(capability, is_shadow, approx_capability) (fu_pool.cc:175-301) */
+static int fu_get(fupool_t *P, int cap, int is_shadow, int *approx, u64 now) {
+    if (!P->capable[cap]) return FU_NOCAPABLE;
+    int fu = FU_NOFREE, aux = FU_NOFREE, aux2 = FU_NOFREE;
+    *approx = cap;
+    if (is_shadow) {
+        switch (cap) {
+        case OC_INTALU:
+            fu = fu_find(P, cap, now); aux = fu_find(P, OC_FADD, now); aux2 = fu_find(P, OC_FCMP, now);
+            if (fu == FU_NOFREE) {
+                fu = aux; *approx = OC_FADD;
+                if (aux == FU_NOFREE) { *approx = OC_FCMP; fu = aux2; }
+            }
+            break;
+        case OC_INTMULT:
+            fu = fu_find(P, cap, now); aux = fu_find(P, OC_FMULT, now);
+            if (fu == FU_NOFREE) { *approx = OC_FMULT; fu = aux; }
+            break;
+        case OC_INTDIV:
+            fu = fu_find(P, cap, now); aux = fu_find(P, OC_FDIV, now);
+            if (fu == FU_NOFREE) { *approx = OC_FDIV; fu = aux; }
+            break;
+        case OC_FADD: case OC_FMULT: case OC_FDIV: case OC_FSQRT:
+            fu = fu_find(P, cap, now); aux = fu_find(P, OC_INTALU, now);
+            if (fu == FU_NOFREE) { *approx = OC_INTALU; fu = aux; }
+            break;
+        case OC_FMULTACC: case OC_FCVT: case OC_FCMP: case OC_FMISC:
+            fu = fu_find(P, cap, now);
+            break;
+        default:
+            fu = FU_NOSHADOW;
+            break;
+        }
+    } else {
+        fu = fu_find(P, cap, now);
+    }
+    if (fu == FU_NOSHADOW) return FU_NOSHADOW;
+    if (fu == FU_NOFREE) return FU_NOFREE;
+    P->busy_until[fu] = ~0ULL;
+    return fu;
+}
+
+/* InstructionQueue::requestShadow (inst_queue.cc:1082-1181) */
+static void request_shadow(fupool_t *P, int idx, int *idx_shadow, int op_class, int *shadow_class, int *has_shadow,
+                           u64 *op_latency, u64 now, or_issue_stats_t *st) {
+    if (idx != FU_NOFREE && idx != FU_NOCAPABLE) {
+        *idx_shadow = fu_get(P, op_class, 1, shadow_class, now);
+        if (*idx_shadow != FU_NOSHADOW && idx != FU_NOCAPABLE) {
+            if (*idx_shadow != FU_NOFREE) {
+                *has_shadow = 1;
+                st->shadow_available++;
+                if ((u64)P->lat[*shadow_class] > *op_latency) *op_latency = (u64)P->lat[*shadow_class];
+                if (op_class == *shadow_class) st->shadow_same_fu++; else st->shadow_not_same_fu++;
+            } else {
+                st->shadow_not_available++;
+            }
+            if (op_class >= OC_INTALU && op_class <= OC_FSQRT) {
+                if (*has_shadow) st->class_available[op_class]++; else st->class_not_available[op_class]++;
+            }
+        }
+    }
+}
+
+int or_issue_model(const or_issue_op_t *ops, uint64_t n, const or_issue_params_t *p, uint8_t *shadow,
+                   or_issue_stats_t *stats) {
+    if (!p || !p->issue_width || !p->dispatch_width || !p->commit_width || !p->iq_entries || !p->rob_entries ||
+        !p->load_latency)
+        return -1;
+    or_issue_stats_t st; memset(&st, 0, sizeof st);
+    st.ops = n;
+    fupool_t *P = (fupool_t *)calloc(1, sizeof *P);
+    fupool_init(P, p);
+    u64 *done = (u64 *)malloc((n + 1) * sizeof(u64));   /* value ready; ~0 = not issued */
+    u64 *dcyc = (u64 *)malloc((n + 1) * sizeof(u64));   /* dispatch cycle */
+    int32_t (*prod)[8] = (int32_t (*)[8])malloc((n + 1) * sizeof *prod);   /* latest older writer of each source */
+    int *in_iq = (int *)calloc(n + 1, sizeof(int));
+    for (u64 i = 0; i < n; i++) done[i] = ~0ULL;
+    s64 writer[33];
+    for (int r = 0; r < 33; r++) writer[r] = -1;
+    u64 committed = 0, dispatched = 0, iq_count = 0, cyc = 0, serial_open = 0;
+    u64 *grp = (u64 *)malloc((p->issue_width + 1) * sizeof(u64));
+    int *grp_idx = (int *)malloc((p->issue_width + 1) * sizeof(int));
+    u64 *grp_lat = (u64 *)malloc((p->issue_width + 1) * sizeof(u64));
+    while (committed < n) {
+        /* memory ops leave the IQ once done */
+        for (u64 i = committed; i < dispatched; i++)
+            if (in_iq[i] && done[i] <= cyc) { in_iq[i] = 0; iq_count--; }
+        /* in-order commit of up to commitWidth completed ops */
+        for (u32 k = 0; k < p->commit_width; k++) {
+            if (committed >= dispatched || done[committed] > cyc) break;
+            if (ops[committed].kind == OR_ISSUE_SERIAL) serial_open--;
+            committed++;
+        }
+        if (committed == n) break;
+        /* scheduleReadyInsts: oldest ready first; a class that finds no free
+         * unit is passed over for the rest of the cycle */
+        int skip[OC_N]; memset(skip, 0, sizeof skip);
+        u32 issued = 0, ng = 0;
+        for (u64 i = committed; i < dispatched && issued < p->issue_width; i++) {
+            if (!in_iq[i] || done[i] != ~0ULL || dcyc[i] >= cyc) continue;
+            int oc = ops[i].opclass;
+            if (skip[oc]) continue;
+            int ok = 1;
+            if (ops[i].kind == OR_ISSUE_SERIAL && committed != i) ok = 0;
+            for (int r = 0; ok && r < 8; r++)
+                if (prod[i][r] >= 0 && done[prod[i][r]] > cyc) ok = 0;
+            if (!ok) continue;
+            int idx = FU_NONEED, approx = oc;
+            u64 op_latency = 1;
+            if (oc != OC_NONE) {
+                idx = fu_get(P, oc, 0, &approx, cyc);
+                if (idx > FU_NOFREE) op_latency = (u64)P->lat[oc];
+            }
+            int idx_shadow = FU_NONEED, has_shadow = 0, shadow_oc = oc;
+            if (p->priority_to_shadow)
+                request_shadow(P, idx, &idx_shadow, oc, &shadow_oc, &has_shadow, &op_latency, cyc, &st);
+            if (idx > FU_NOFREE || idx == FU_NONEED || idx == FU_NOCAPABLE) {
+                if (op_latency == 1) {
+                    if (idx >= 0) {
+                        P->busy_until[idx] = cyc + 1;                  /* freeUnitNextCycle */
+                        if (has_shadow) P->busy_until[idx_shadow] = cyc + 1;
+                    }
+                } else {
+                    P->busy_until[idx] = P->piped[oc] ? cyc + 1 : cyc + op_latency;   /* FUCompletion setFreeFU */
+                    if (has_shadow) P->busy_until[idx_shadow] = P->piped[shadow_oc] ? cyc + 1 : cyc + op_latency;
+                }
+                if (!p->priority_to_shadow) { grp[ng] = i; grp_idx[ng] = idx; grp_lat[ng] = op_latency; ng++; }
+                shadow[i] = (uint8_t)has_shadow;
+                done[i] = cyc + (ops[i].kind == OR_ISSUE_LOAD ? (u64)p->load_latency : op_latency);
+                if (ops[i].kind != OR_ISSUE_LOAD && ops[i].kind != OR_ISSUE_STORE) { in_iq[i] = 0; iq_count--; }
+                issued++;
+            } else {
+                skip[oc] = 1;
+            }
+        }
+        /* !priorityToShadow: shadows for the issued group, in issue order */
+        for (u32 g = 0; g < ng; g++) {
+            u64 i = grp[g];
+            int idx_shadow = FU_NONEED, has_shadow = 0, oc = ops[i].opclass, shadow_oc = oc;
+            u64 lat = grp_lat[g];
+            request_shadow(P, grp_idx[g], &idx_shadow, oc, &shadow_oc, &has_shadow, &lat, cyc, &st);
+            shadow[i] = (uint8_t)has_shadow;
+            if (has_shadow) {
+                if (lat == 1) { if (idx_shadow >= 0) P->busy_until[idx_shadow] = cyc + 1; }
+                else P->busy_until[idx_shadow] = P->piped[shadow_oc] ? cyc + 1 : cyc + lat;
+            }
+        }
+        /* dispatch in program order into IQ + ROB; nothing passes an
+         * uncommitted serialising op */
+        for (u32 k = 0; k < p->dispatch_width && dispatched < n; k++) {
+            if (iq_count >= p->iq_entries || dispatched - committed >= p->rob_entries) break;
+            if (serial_open) break;
+            u64 i = dispatched++;
+            dcyc[i] = cyc;
+            int np = 0;
+            for (int r = 0; r < 8; r++) prod[i][r] = -1;
+            for (int r = 1; r < 33 && np < 8; r++)
+                if (((ops[i].src >> r) & 1) && writer[r] >= 0) prod[i][np++] = (int32_t)writer[r];
+            if (ops[i].kind == OR_ISSUE_SERIAL) serial_open++;
+            for (int r = 1; r < 33; r++) if ((ops[i].dst >> r) & 1) writer[r] = (s64)i;
+            in_iq[i] = 1; iq_count++;
+        }
+        cyc++;
+    }
+    st.cycles = cyc;
+    if (stats) *stats = st;
+    free(P); free(done); free(dcyc); free(prod); free(in_iq); free(grp); free(grp_idx); free(grp_lat);
+    return 0;
+}
+
+/* One trace event of the golden run as a replayed op (restates
+ * shrewd_amd/csrc/fi_issue.cpp:issue_ops_from_trace's rule from the oracle's
+ * own decode): integer operands x1..x31; ecall reads a0..a7, writes a0 and
+ * serialises; FP ops chain through one FP-state register (bit 32). */
+static or_issue_op_t issue_op(const dec_t *d, int is_ecall) {
+    or_issue_op_t o; memset(&o, 0, sizeof o);
+    int oc = op_class(d->op);
+    o.opclass = (uint8_t)oc;
+    if (is_ecall) { o.src = 0x3FC00ULL; o.dst = 1ULL << 10; o.kind = OR_ISSUE_SERIAL; return o; }
+    if (d->rs1 > 0) o.src |= 1ULL << d->rs1;
+    if (d->rs2 > 0) o.src |= 1ULL << d->rs2;
+    if (d->rd > 0) o.dst |= 1ULL << d->rd;
+    if (oc >= OC_FADD && oc <= OC_FSQRT) { o.src |= 1ULL << 32; o.dst |= 1ULL << 32; }
+    if (oc == OC_FMEMREAD) o.dst |= 1ULL << 32;
+    if (oc == OC_FMEMWRITE) o.src |= 1ULL << 32;
+    o.kind = (oc == OC_MEMREAD || oc == OC_FMEMREAD) ? OR_ISSUE_LOAD
+           : (oc == OC_MEMWRITE || oc == OC_FMEMWRITE) ? OR_ISSUE_STORE : OR_ISSUE_PLAIN;
+    return o;
+}
+
 /* SHREWD shadow execution: FUPool::getUnit(cap, is_shadow=true) (cpu/o3/
  * fu_pool.cc:177-301) finds a shadow unit only for IntAlu, IntMult, IntDiv and
  * the scalar Float classes (FloatAdd..FloatSqrt, enum 1..11); every other
- * class returns NoShadowFU.  The atomic model has no FU contention, so a
- * shadow-capable class in the protected set is always replicated. */
-static int replicated(u64 protect_opc, int cls) {
-    return cls >= FI_OPC_INTALU && cls <= FI_OPC_FLOATSQRT && ((protect_opc >> cls) & 1);
+ * class returns NoShadowFU.  Without the issue model the shadow is always
+ * available; with it (or_set_issue_model), only if the k-th committed golden
+ * instruction's shadow found a unit (the target of a result fault at numInst
+ * k is that golden instruction: the trial equals the golden run until then). */
+static int replicated(const or_campaign_t *c, int cls, u64 k) {
+    if (!(cls >= FI_OPC_INTALU && cls <= FI_OPC_FLOATSQRT && ((c->protect_opc >> cls) & 1))) return 0;
+    return !c->shadow || k >= c->n_shadow || c->shadow[k];
 }
 
 /* Result fault (OR_T_RESULT): applied to the first instruction that commits
@@ -1838,7 +2101,7 @@ static int replicated(u64 protect_opc, int cls) {
 static int result_fault(mach_t *m, const dec_t *d) {
     m->rarm = 0;
     if (!m->wrote) { m->injected = 2; return 0; }
-    if (replicated(m->c->protect_opc, op_class(d->op))) { finish(m, OR_DETECTED, 0, 0); return 1; }
+    if (replicated(m->c, op_class(d->op), m->num_inst - 1)) { finish(m, OR_DETECTED, 0, 0); return 1; }
     m->x[d->rd] ^= m->site->mask;
     return 0;
 }
@@ -1893,6 +2156,13 @@ static void tick(mach_t *m, u64 cap) {
         if (have_inst) {
             m->wrote = 0;
             f = execute(m, &d, &fva);
+            if (m->rec && (f == F_NONE || f == F_SYSCALL)) {
+                if (m->rec_n == m->rec_cap) {
+                    m->rec_cap = m->rec_cap ? 2 * m->rec_cap : 4096;
+                    m->rec = (or_issue_op_t *)realloc(m->rec, m->rec_cap * sizeof *m->rec);
+                }
+                m->rec[m->rec_n++] = issue_op(&d, f == F_SYSCALL);
+            }
             if (f == F_NONE) {
                 m->num_inst++;   /* countInst only on NoFault (atomic.cc:687-689) */
                 if (m->rarm && result_fault(m, &d)) return;
@@ -2044,7 +2314,7 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
 void or_destroy(or_campaign_t *c) {
     if (!c) return;
     pm_free(&c->image);
-    free(c->mem_pages); free(c->gout.buf); free(c->gerr.buf);
+    free(c->mem_pages); free(c->gout.buf); free(c->gerr.buf); free(c->shadow);
     free(c);
 }
 
@@ -2089,6 +2359,40 @@ int or_golden(or_campaign_t *c, u64 max_inst, or_golden_t *out) {
     mach_free(&m);
     if (out) *out = c->golden;
     return 0;
+}
+
+int or_set_issue_model(or_campaign_t *c, const or_issue_params_t *p) {
+    if (!p) { free(c->shadow); c->shadow = NULL; c->n_shadow = 0; return 0; }
+    if (!c->have_golden) { snprintf(c->err, sizeof c->err, "or_set_issue_model: no golden run"); return -1; }
+    mach_t m; mach_init(&m, c);
+    m.rec_cap = 4096;
+    m.rec = (or_issue_op_t *)malloc(m.rec_cap * sizeof *m.rec);
+    run(&m, c->golden.ninst + 1);
+    uint8_t *all = (uint8_t *)calloc(m.rec_n + 1, 1);
+    or_issue_stats_t st;
+    int rc = or_issue_model(m.rec, m.rec_n, p, all, &st);
+    if (rc == 0) {
+        free(c->shadow);
+        c->shadow = (uint8_t *)calloc(c->golden.ninst + 1, 1);
+        u64 k = 0;
+        for (u64 i = 0; i < m.rec_n; i++)
+            if (m.rec[i].kind != OR_ISSUE_SERIAL && k < c->golden.ninst) c->shadow[k++] = all[i];
+        c->n_shadow = k;
+        c->issue_stats = st;
+        if (k != c->golden.ninst) { snprintf(c->err, sizeof c->err, "issue model: trace length"); rc = -1; }
+    } else {
+        snprintf(c->err, sizeof c->err, "issue model: invalid parameters");
+    }
+    free(all); free(m.rec); m.rec = NULL;
+    mach_free(&m);
+    return rc;
+}
+
+uint64_t or_shadow_map(or_campaign_t *c, uint8_t *buf, uint64_t cap, or_issue_stats_t *stats) {
+    if (!c->shadow) return 0;
+    if (buf && cap) memcpy(buf, c->shadow, cap < c->n_shadow ? cap : c->n_shadow);
+    if (stats) *stats = c->issue_stats;
+    return c->n_shadow;
 }
 
 uint64_t or_golden_stdout(or_campaign_t *c, uint8_t *buf, uint64_t cap) {

@@ -99,6 +99,33 @@ int or_sample(or_campaign_t *c, uint64_t seed, uint64_t first_trial, uint64_t n,
  * enum value k (src/cpu/FuncUnit.py).  A result fault on a replicated
  * instruction is detected (see rv64se.c:result_fault). */
 void or_set_protect_opclasses(or_campaign_t *c, uint64_t mask);
+/* SHREWD functional-unit contention (include/fi_engine.h, fi_issue_*): the
+ * same parameter, op and counter layouts as fi_issue_params / fi_issue_op /
+ * fi_issue_stats. */
+typedef struct {
+    uint32_t issue_width, dispatch_width, commit_width, iq_entries, rob_entries, load_latency;
+    uint32_t priority_to_shadow;
+    uint32_t fu_count[6];   /* IntALU, IntMultDiv, FP_ALU, FP_MultDiv, RdWrPort, IprPort */
+} or_issue_params_t;
+typedef struct {
+    uint64_t src, dst;      /* bit r = x_r (1..31), bit 32 = FP state */
+    uint8_t opclass, kind, pad[6];
+} or_issue_op_t;
+enum { OR_ISSUE_PLAIN = 0, OR_ISSUE_LOAD = 1, OR_ISSUE_STORE = 2, OR_ISSUE_SERIAL = 3 };
+typedef struct {
+    uint64_t ops, cycles, shadow_available, shadow_not_available, shadow_same_fu, shadow_not_same_fu;
+    uint64_t class_available[12], class_not_available[12];
+} or_issue_stats_t;
+/* Replay ops[0..n) through the O3 issue model; shadow[i] = 1 if op i's shadow
+ * was issued.  Returns 0, or -1 on bad parameters. */
+int or_issue_model(const or_issue_op_t *ops, uint64_t n, const or_issue_params_t *p, uint8_t *shadow,
+                   or_issue_stats_t *stats);
+/* Turn the model on for result faults (p = NULL: off).  Runs the golden
+ * program once more to record its trace.  Returns 0 or -1. */
+int or_set_issue_model(or_campaign_t *c, const or_issue_params_t *p);
+/* shadow per golden numInst index; returns the count (golden ninst) */
+uint64_t or_shadow_map(or_campaign_t *c, uint8_t *buf, uint64_t cap, or_issue_stats_t *stats);
+
 /* SE time and randomness: ticks per CPU cycle (clock_gettime; default 500 =
  * 2 GHz) and gem5's Random global seed (getrandom; default 5489) */
 void or_set_clock(or_campaign_t *c, uint64_t period_ticks, uint64_t random_seed);

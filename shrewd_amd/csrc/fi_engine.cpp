@@ -44,6 +44,7 @@ hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const ui
 std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
                              const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
                              uint32_t &n_insts);
+std::vector<fi_issue_op> issue_ops_from_trace(const std::vector<PreInst> &pre, const std::vector<uint32_t> &trace);
 std::string jit_compile(const std::string &body, const char *arch, std::vector<char> &code, bool &cached);
 hipError_t sort_pairs(void *tmp, size_t bytes, const uint64_t *kin, uint64_t *kout, const uint32_t *vin,
                       uint32_t *vout, uint64_t n, int end_bit, hipStream_t st);
@@ -115,6 +116,14 @@ struct fi_engine {
     uint8_t *d_rnd = nullptr;   // getrandom's byte stream (kRndLen bytes)
     uint64_t protect = 0;
     uint64_t protect_opc = 0;   // SHREWD replication by OpClass (fi_set_protect_opclasses)
+    // SHREWD FU contention (fi_set_issue_model): shadow issued per golden numInst index
+    bool issue_on = false;
+    fi_issue_params issue_p{};
+    fi_issue_stats issue_stats{};
+    std::vector<uint8_t> shadow;
+    uint32_t *d_shadow = nullptr;    // the same as a bitmap, [ninst / 32 + 1]
+    std::vector<PreInst> g_pre;      // golden pre-decoded text and trace (empty: unavailable)
+    std::vector<uint32_t> g_trace;
 
     // work buffers, sized for `cap` trials per launch
     uint64_t cap = 0;
@@ -261,6 +270,8 @@ static void free_image(fi_engine *e) {
     free_snaps(e);
     free_mem_index(e);
     free_tx(e);
+    dfree(e->d_shadow);
+    e->g_pre.clear(); e->g_trace.clear(); e->shadow.clear();
     e->have_golden = false;
     e->loaded = false;
 }
@@ -333,6 +344,34 @@ struct Mt64 {
         return y;
     }
 };
+
+// The issue model over the golden trace (fi_issue.cpp), indexed by numInst
+// (ecall events are replayed but numInst does not count them), uploaded as a
+// bitmap for the result-fault commit (fi_trial.hip:replicated).
+static fi_status compute_shadow(fi_engine *e) {
+    if (e->g_trace.empty() && e->golden.ninst)
+        return fail(e, FI_E_STATE, "issue model: the golden trace is unavailable (trace overflow or rewritten text)");
+    const std::vector<fi_issue_op> ops = issue_ops_from_trace(e->g_pre, e->g_trace);
+    std::vector<uint8_t> all(ops.size());
+    fi_issue_stats st{};
+    const fi_status s = fi_issue_model_run(ops.data(), ops.size(), &e->issue_p, all.data(), &st);
+    if (s) return fail(e, s, "issue model: invalid parameters");
+    e->shadow.clear();
+    e->shadow.reserve(e->golden.ninst);
+    for (size_t i = 0; i < ops.size(); i++)
+        if (!(e->g_trace[i] & 0x80000000u)) e->shadow.push_back(all[i]);
+    if (e->shadow.size() != e->golden.ninst)
+        return fail(e, FI_E_STATE, "issue model: trace holds %zu instructions, golden run %llu", e->shadow.size(),
+                    (unsigned long long)e->golden.ninst);
+    std::vector<uint32_t> bits(e->shadow.size() / 32 + 1, 0);
+    for (size_t k = 0; k < e->shadow.size(); k++)
+        if (e->shadow[k]) bits[k >> 5] |= 1u << (k & 31);
+    dfree(e->d_shadow);
+    HIPCHK(hipMalloc(&e->d_shadow, bits.size() * 4));
+    HIPCHK(hipMemcpy(e->d_shadow, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
+    e->issue_stats = st;
+    return FI_OK;
+}
 
 static fi_status upload_snaps(fi_engine *e) {
     free_snaps(e);
@@ -538,6 +577,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.hang_cap = e->golden.ninst * e->cfg.hang_factor_x16 / 16 + 1000;
     c.protect_mask = e->protect;
     c.protect_opc = e->protect_opc;
+    c.shadow_bits = e->issue_on ? e->d_shadow : nullptr;
     c.priv_frames = e->d_priv; c.priv_vpn = e->d_priv_vpn;
     c.tx_sink = e->d_sink;
     c.fregs = e->d_fregs;
@@ -832,6 +872,8 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     e->snaps = snaps;
     e->tab = tab;
     e->snap_I = I;
+    e->g_pre.clear(); e->g_trace.clear();
+    if (live_ok && !trace.empty()) { e->g_pre = pre; e->g_trace = trace; }
     st = upload_snaps(e);
     if (st) return st;
     st = build_mem_index(e, mev, live_ok && n_mem <= mem_cap);
@@ -895,6 +937,10 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     e->golden.snapshot_interval = I;
     e->golden.snapshot_frames = e->pool.size() / kPage;
     e->have_golden = true;
+    if (e->issue_on) {   // the model follows the new golden run
+        st = compute_shadow(e);
+        if (st) return st;
+    }
     if (out) *out = e->golden;
     return FI_OK;
 }
@@ -950,6 +996,30 @@ fi_status fi_set_protect(fi_engine *e, uint64_t protect_mask) {
 fi_status fi_set_protect_opclasses(fi_engine *e, uint64_t opclass_mask) {
     if (!e) return FI_E_ARG;
     e->protect_opc = opclass_mask;
+    return FI_OK;
+}
+
+fi_status fi_set_issue_model(fi_engine *e, const fi_issue_params *p) {
+    if (!e) return FI_E_ARG;
+    if (!p) {
+        e->issue_on = false;
+        return FI_OK;
+    }
+    if (!e->have_golden) return fail(e, FI_E_STATE, "fi_set_issue_model: no golden run");
+    const fi_issue_params keep = e->issue_p;
+    e->issue_p = *p;
+    const fi_status st = compute_shadow(e);
+    if (st) { e->issue_p = keep; return st; }
+    e->issue_on = true;
+    return FI_OK;
+}
+
+fi_status fi_shadow_map(fi_engine *e, uint8_t *shadow, uint64_t cap, uint64_t *n, fi_issue_stats *stats) {
+    if (!e) return FI_E_ARG;
+    if (!e->issue_on) return fail(e, FI_E_STATE, "fi_shadow_map: the issue model is off");
+    if (shadow && cap) memcpy(shadow, e->shadow.data(), std::min<uint64_t>(cap, e->shadow.size()));
+    if (n) *n = e->shadow.size();
+    if (stats) *stats = e->issue_stats;
     return FI_OK;
 }
 

@@ -123,6 +123,8 @@ struct DevCtx {
     uint64_t hang_cap;
     uint64_t protect_mask;
     uint64_t protect_opc;            // SHREWD replication: protected gem5 OpClass values (bit mask)
+    const uint32_t *shadow_bits;     // FU contention model: bit k = the k-th golden instruction's shadow issued
+                                     // (nullptr: every shadow-capable instruction has one)
     // per-trial private (copy-on-write) pages: frames [slot][P][4096], vpns [P][n]
     uint8_t *priv_frames;
     uint64_t *priv_vpn;

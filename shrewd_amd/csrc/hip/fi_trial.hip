@@ -597,10 +597,15 @@ __device__ __forceinline__ uint32_t op_class(uint32_t op) {
 }
 // SHREWD shadow execution: FUPool::getUnit(cap, is_shadow) (src/cpu/o3/
 // fu_pool.cc:177-301) has a shadow unit only for IntAlu, IntMult, IntDiv and
-// FloatAdd..FloatSqrt; the atomic model has no FU contention, so a protected
-// class among them is always replicated (oracle/rv64se.c:replicated)
-__device__ __forceinline__ bool replicated(uint64_t protect_opc, uint32_t cls) {
-    return cls >= FI_OPC_INTALU && cls <= FI_OPC_FLOATSQRT && ((protect_opc >> cls) & 1);
+// FloatAdd..FloatSqrt.  Without the issue model a protected class among them
+// is always replicated; with it (fi_set_issue_model) only if the k-th golden
+// instruction's shadow found a free unit (oracle/rv64se.c:replicated).  The
+// target of a result fault is the golden instruction numInst = k: the trial
+// equals the golden run up to its commit.
+__device__ __forceinline__ bool replicated(KCtx *CX, uint32_t cls, uint64_t k) {
+    if (!(cls >= FI_OPC_INTALU && cls <= FI_OPC_FLOATSQRT && ((CX->protect_opc >> cls) & 1))) return false;
+    const uint32_t *sb = CX->shadow_bits;
+    return !sb || k >= CX->gninst || ((sb[k >> 5] >> (k & 31)) & 1u);
 }
 
 // ------------------------------------------------------------------ F/D/Zfh + A
@@ -2469,7 +2474,7 @@ __device__ __forceinline__ void trial_body() {
             bool rdet = false;
             if (L.injected == 3) {   // result fault (oracle/rv64se.c:result_fault)
                 if (!(wrd && d.rd)) L.injected = 2;
-                else if (replicated(CX->protect_opc, op_class(d.op))) rdet = true;
+                else if (replicated(CX, op_class(d.op), L.ninst)) rdet = true;
                 else { v ^= s.mask; L.injected = 1; }
             }
             if (wrd && d.rd) RREG(d.rd) = v;

@@ -113,6 +113,60 @@ class GoldenInfo(C.Structure):
                 ("translated_insts", C.c_uint64), ("translate_us", C.c_uint64)]
 
 
+class IssueParams(C.Structure):
+    """fi_issue_params: the O3 issue model of SHREWD's FU contention."""
+    _fields_ = [("issue_width", C.c_uint32), ("dispatch_width", C.c_uint32), ("commit_width", C.c_uint32),
+                ("iq_entries", C.c_uint32), ("rob_entries", C.c_uint32), ("load_latency", C.c_uint32),
+                ("priority_to_shadow", C.c_uint32), ("fu_count", C.c_uint32 * 6)]
+
+
+class IssueStats(C.Structure):
+    _fields_ = [("ops", C.c_uint64), ("cycles", C.c_uint64), ("shadow_available", C.c_uint64),
+                ("shadow_not_available", C.c_uint64), ("shadow_same_fu", C.c_uint64),
+                ("shadow_not_same_fu", C.c_uint64), ("class_available", C.c_uint64 * 12),
+                ("class_not_available", C.c_uint64 * 12)]
+
+    def as_dict(self) -> dict:
+        d = {n: getattr(self, n) for n in ("ops", "cycles", "shadow_available", "shadow_not_available",
+                                              "shadow_same_fu", "shadow_not_same_fu")}
+        for n in ("class_available", "class_not_available"):
+            d[n] = {OPCLASS_NAMES[k]: int(getattr(self, n)[k]) for k in range(1, 12) if getattr(self, n)[k]}
+        return d
+
+
+ISSUE_OP_DT = np.dtype([("src", "<u8"), ("dst", "<u8"), ("opclass", "u1"), ("kind", "u1"), ("pad", "u1", (6,))])
+ISSUE_PLAIN, ISSUE_LOAD, ISSUE_STORE, ISSUE_SERIAL = 0, 1, 2, 3
+FU_NAMES = ("IntALU", "IntMultDiv", "FP_ALU", "FP_MultDiv", "RdWrPort", "IprPort")
+
+
+def issue_params(**kw) -> IssueParams:
+    """The reference's O3 defaults (BaseO3CPU.py, FuncUnitConfig.py) with
+    overrides by field name; fu_count also by FU name (IntALU=4, ...)."""
+    p = IssueParams()
+    lib().fi_issue_default_params(C.byref(p))
+    for k, v in kw.items():
+        if k in FU_NAMES:
+            p.fu_count[FU_NAMES.index(k)] = int(v)
+        elif k == "fu_count":
+            for i, c in enumerate(v):
+                p.fu_count[i] = int(c)
+        else:
+            setattr(p, k, int(v))
+    return p
+
+
+def issue_model_run(ops: np.ndarray, params: IssueParams | None = None):
+    """fi_issue_model_run (pure host code): -> (shadow uint8[n], IssueStats)."""
+    ops = np.ascontiguousarray(ops, ISSUE_OP_DT)
+    p = params if params is not None else issue_params()
+    out = np.zeros(len(ops), np.uint8)
+    st = IssueStats()
+    rc = lib().fi_issue_model_run(ops.ctypes.data, len(ops), C.byref(p), out.ctypes.data, C.byref(st))
+    if rc != FI_OK:
+        raise EngineError(f"fi_issue_model_run: {rc}")
+    return out, st
+
+
 _lib = None
 
 
@@ -166,6 +220,10 @@ def lib():
         L.fi_debug_translate.argtypes = [vp, C.c_uint64, C.c_uint64, vp, C.c_uint64, C.c_char_p, C.c_uint64,
                                          C.POINTER(C.c_uint64)]
         L.fi_debug_translation.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.fi_issue_default_params.argtypes = [C.POINTER(IssueParams)]
+        L.fi_issue_model_run.argtypes = [vp, C.c_uint64, C.POINTER(IssueParams), vp, C.POINTER(IssueStats)]
+        L.fi_set_issue_model.argtypes = [vp, C.POINTER(IssueParams)]
+        L.fi_shadow_map.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(IssueStats)]
         L.fi_translate_status.restype = C.c_char_p
         L.fi_translate_status.argtypes = [vp]
         _lib = L
@@ -251,6 +309,23 @@ class Engine:
 
     def set_protect_opclasses(self, opclasses):
         self._chk(self.L.fi_set_protect_opclasses(self.h, opclass_mask(opclasses)), "fi_set_protect_opclasses")
+
+    def set_issue_model(self, params: IssueParams | dict | None = None, **kw):
+        """SHREWD FU contention for result faults (fi_set_issue_model): None and
+        no keywords -> off; a dict / keywords override the O3 defaults."""
+        if params is None and not kw:
+            self._chk(self.L.fi_set_issue_model(self.h, None), "fi_set_issue_model")
+            return
+        p = params if isinstance(params, IssueParams) else issue_params(**{**(params or {}), **kw})
+        self._chk(self.L.fi_set_issue_model(self.h, C.byref(p)), "fi_set_issue_model")
+
+    def shadow_map(self):
+        """(uint8 per golden numInst index: shadow issued, IssueStats)"""
+        n, st = C.c_uint64(), IssueStats()
+        self._chk(self.L.fi_shadow_map(self.h, None, 0, C.byref(n), None), "fi_shadow_map")
+        out = np.zeros(n.value, np.uint8)
+        self._chk(self.L.fi_shadow_map(self.h, out.ctypes.data, n.value, C.byref(n), C.byref(st)), "fi_shadow_map")
+        return out, st
 
     def sample(self, first: int, n: int) -> np.ndarray:
         out = np.zeros(n, SITE_DT)
@@ -394,13 +469,16 @@ class FaultCampaign:
 
     Params (same names/meaning as the SimObject): workload (binary path), cmd
     (argv, cmd[0] defaults to workload), env, trials, seed, structures, bits,
-    burst, protect_mask, protect_opclasses, num_gpus, max_insts_factor, output.
+    burst, protect_mask, protect_opclasses, num_gpus, max_insts_factor, output;
+    shadow_fu_model (SHREWD FU contention for result faults, off by default),
+    priority_to_shadow and issue_params (the O3 issue model's parameters).
     """
 
     def __init__(self, workload: str, cmd: Sequence[str] | None = None, env: Sequence[str] | None = None,
                  trials: int = 1000, seed: int = 0x5EED0001, structures=("int_reg",), burst: int = 1,
                  protect_mask: int = 0, num_gpus: int = 1, max_insts_factor: float = 2.0, output: str = "",
-                 device: int = 0, private_pages: int = 16, protect_opclasses=(), bits=None):
+                 device: int = 0, private_pages: int = 16, protect_opclasses=(), bits=None,
+                 shadow_fu_model: bool = False, priority_to_shadow: bool = False, issue_params: dict | None = None):
         self.workload, self.cmd, self.env = workload, list(cmd or [workload]), list(env or [])
         self.trials, self.seed, self.structures, self.burst = trials, seed, structures, burst
         self.protect_mask, self.num_gpus, self.output = protect_mask, num_gpus, output
@@ -416,6 +494,9 @@ class FaultCampaign:
         self.engine.set_protect(protect_mask)
         self.protect_opclasses = opclass_mask(protect_opclasses)
         self.engine.set_protect_opclasses(self.protect_opclasses)
+        self.shadow_fu_model = shadow_fu_model
+        if shadow_fu_model:
+            self.engine.set_issue_model({**(issue_params or {}), "priority_to_shadow": int(priority_to_shadow)})
         self._hist = None
         self.outcomes = None
 

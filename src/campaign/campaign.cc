@@ -139,6 +139,14 @@ Campaign::Campaign(const CampaignParams &p) : p_(p) {
         check(e, fi_set_bits(e, bits_mask(p_.bits)), "fi_set_bits");
         check(e, fi_set_protect(e, p_.protect_mask), "fi_set_protect");
         check(e, fi_set_protect_opclasses(e, opclass_mask(p_.protect_opclasses)), "fi_set_protect_opclasses");
+        if (p_.shadow_fu_model) {
+            fi_issue_params ip;
+            fi_issue_default_params(&ip);
+            ip.priority_to_shadow = p_.priority_to_shadow ? 1 : 0;
+            ip.issue_width = p_.issue_width;
+            ip.load_latency = p_.load_latency;
+            check(e, fi_set_issue_model(e, &ip), "fi_set_issue_model");
+        }
         if (g == 0) {
             golden_.ninst = gi.ninst;
             golden_.ncycles = gi.ncycles;

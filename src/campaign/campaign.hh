@@ -33,6 +33,10 @@ struct CampaignParams {
     std::string bits;                     // eligible lowest flipped bits: "0-63" (all), "0-31,63", or a number
     uint64_t protect_mask = 0;
     std::vector<std::string> protect_opclasses;   // SHREWD replication set (gem5 OpClass names)
+    bool shadow_fu_model = false;         // SHREWD FU contention for result faults (fi_set_issue_model)
+    bool priority_to_shadow = false;      // BaseO3CPU.priorityToShadow (src/cpu/o3/BaseO3CPU.py:227)
+    uint32_t issue_width = 8;             // BaseO3CPU.issueWidth
+    uint32_t load_latency = 2;            // issue model: cycles from a load's issue to its value
     uint32_t num_gpus = 1;
     uint32_t first_device = 0;
     double max_insts_factor = 2.0;        // hang cap = golden * f + 1000

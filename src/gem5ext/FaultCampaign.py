@@ -40,6 +40,14 @@ class FaultCampaign(SimObject):
     protect_opclasses = VectorParam.String(
         [], "SHREWD replication: gem5 OpClass names whose instructions get a shadow "
         "execution (IntAlu, IntMult, IntDiv, Float*); a result fault on one is detected")
+    shadow_fu_model = Param.Bool(
+        False, "SHREWD FU contention: a protected instruction is replicated only if its "
+        "shadow finds a free functional unit in an O3 issue model of the golden run "
+        "(FUPool::getUnit / InstructionQueue::requestShadow)")
+    priority_to_shadow = Param.Bool(
+        False, "shadows claim units before younger primaries (BaseO3CPU.priorityToShadow)")
+    issue_width = Param.UInt32(8, "issue model: instructions issued per cycle (BaseO3CPU.issueWidth)")
+    load_latency = Param.UInt32(2, "issue model: cycles from a load's issue to its value")
     num_gpus = Param.UInt32(1, "MI355X devices used by this process")
     first_gpu = Param.UInt32(0, "first HIP device ordinal")
     max_insts_factor = Param.Float(

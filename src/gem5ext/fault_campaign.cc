@@ -27,6 +27,10 @@ FaultCampaign::init()
     cp.bits = params().bits;
     cp.protect_mask = params().protect_mask;
     cp.protect_opclasses = params().protect_opclasses;
+    cp.shadow_fu_model = params().shadow_fu_model;
+    cp.priority_to_shadow = params().priority_to_shadow;
+    cp.issue_width = params().issue_width;
+    cp.load_latency = params().load_latency;
     cp.num_gpus = params().num_gpus;
     cp.first_device = params().first_gpu;
     cp.max_insts_factor = params().max_insts_factor;

@@ -189,6 +189,50 @@ def test_result_faults_bit_exact(engine_factory, oracle_mod, name, opc, n):
         assert (dev["cls"] == 4).sum() > 0
 
 
+@pytest.mark.parametrize("name", ["crc32", "qsort", "intmix", "fpamo"])
+@pytest.mark.parametrize("prio", [0, 1])
+def test_shadow_map_matches_oracle(engine_factory, oracle_mod, name, prio):
+    """SHREWD FU contention: the engine's issue model over the device-recorded
+    golden trace equals the oracle's over its own golden run, per committed
+    instruction and in every counter."""
+    e = engine_factory(name)
+    o = oracle_for(oracle_mod, name)
+    e.set_issue_model(priority_to_shadow=prio)
+    o.set_issue_model(priority_to_shadow=prio)
+    a, sa = e.shadow_map()
+    b, sb = o.shadow_map()
+    e.set_issue_model(None)
+    assert len(a) == e.golden.ninst
+    bad = np.flatnonzero(a != b)
+    assert not len(bad), f"{len(bad)} instructions differ, first {bad[:5].tolist()}"
+    for f, _ in oracle_mod.IssueStats._fields_:
+        va, vb = getattr(sa, f), getattr(sb, f)
+        assert (list(va) if not isinstance(va, int) else va) == (list(vb) if not isinstance(vb, int) else vb), f
+
+
+@pytest.mark.parametrize("name,opc,n", [("crc32", OPC_INT, 6000), ("qsort", 1 << 1, 4000),
+                                        ("intmix", OPC_INT, 3000)])
+def test_result_faults_under_contention_bit_exact(engine_factory, oracle_mod, name, opc, n):
+    """Result faults with the FU-contention model on (deferred shadows): a
+    protected instruction is detected only if its shadow found a unit."""
+    e = engine_factory(name)
+    o = oracle_for(oracle_mod, name)
+    e.set_campaign(0xC0DE + n, RESULT, 1)
+    e.set_protect_opclasses(opc)
+    o.set_protect_opclasses(opc)
+    e.set_issue_model({})
+    o.set_issue_model({})
+    sites = e.sample(0, n)
+    dev, _ = e.run_sites(sites)
+    ref = o.run_trials(sites)
+    sh, _ = e.shadow_map()
+    e.set_issue_model(None)
+    e.set_protect_opclasses(0)
+    compare(dev, ref, sites)
+    det = dev["cls"] == 4
+    assert det.any() and not (det & (sh[sites["inst"]] == 0)).any()
+
+
 def test_translation_skipped_without_hot_code(engine_factory):
     """Straight-line code run once (hello) is not translated: the static
     kernels run it, and the engine says why."""
