@@ -14,7 +14,11 @@ trials/s, outcome classes, crash/escape sub-codes.
   C5b SHREWD replication by instruction class: result faults (the value an
      instruction writes) on crc32 and qsort with protected gem5 OpClass sets
      (a replicated instruction's shadow execution detects the fault)
-python tools/campaigns.py [TAG]
+  C5c the same with SHREWD FU contention (fi_set_issue_model): a protected
+     instruction is replicated only if its shadow found a free unit in the O3
+     issue model of the golden run; deferred and priority shadows, the default
+     pool and a pool with fewer ALUs
+python tools/campaigns.py [TAG] [--only C5c]
 """
 import json
 import os
@@ -51,8 +55,14 @@ def engine(name):
     return _engines[name]
 
 
-def run(cfg, name, n, structs, burst=1, protect=0, seed=0x5EED0003, opc=0):
+FU_MODELS = {"off": None, "deferred": {}, "priority": {"priority_to_shadow": 1},
+             "deferred, 4 IntALU 2 FP_ALU": {"IntALU": 4, "FP_ALU": 2},
+             "priority, 4 IntALU 2 FP_ALU": {"IntALU": 4, "FP_ALU": 2, "priority_to_shadow": 1}}
+
+
+def run(cfg, name, n, structs, burst=1, protect=0, seed=0x5EED0003, opc=0, fu=None):
     e = engine(name)
+    e.set_issue_model(fu)
     e.set_campaign(seed, structs, burst)
     e.set_protect(protect)
     e.set_protect_opclasses(opc)
@@ -62,6 +72,11 @@ def run(cfg, name, n, structs, burst=1, protect=0, seed=0x5EED0003, opc=0):
     dt = time.perf_counter() - t0
     e.set_protect(0)
     e.set_protect_opclasses(0)
+    extra = {}
+    if fu is not None:
+        _, st = e.shadow_map()
+        extra = {"issue_model": fu, "issue_stats": st.as_dict()}
+    e.set_issue_model(None)
     cls = h["counts"].sum(axis=(0, 1))
     rec = {"config": cfg, "workload": name, "golden_ninst": int(e.golden.ninst), "trials": n,
            "structures": hex(structs), "burst": burst, "protect_mask": hex(protect), "protect_opclasses": hex(opc),
@@ -70,14 +85,18 @@ def run(cfg, name, n, structs, burst=1, protect=0, seed=0x5EED0003, opc=0):
            "crash_sub": {CRASH_NAMES.get(i, str(i)): int(h["crash_sub"][i]) for i in range(16) if h["crash_sub"][i]},
            "escape_sub": {ESCAPE_NAMES.get(i, str(i)): int(h["escape_sub"][i]) for i in range(8)
                           if h["escape_sub"][i]},
-           "sdc_rate": int(cls[1]) / n}
+           "sdc_rate": int(cls[1]) / n, **extra}
     print(json.dumps(rec), flush=True)
     return rec, out
 
 
 def main():
-    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    tag = sys.argv[1] if len(sys.argv) > 1 and not sys.argv[1].startswith("-") else "r01"
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     recs = []
+    if only == "C5c":
+        c5c(recs)
+        return dump(recs, tag)
     # C1 (its bit-exactness against the oracle: tests/test_gpu_parity.py)
     recs.append(run("C1", "hello", 1000, REGS, seed=0x5EED0001)[0])
     for w in ("crc32", "qsort"):
@@ -95,6 +114,19 @@ def main():
             r = run("C5b", w, 100_000, RESULT, opc=m)[0]
             r["opclass_name"] = label
             recs.append(r)
+    c5c(recs)
+    dump(recs, tag)
+
+
+def c5c(recs):
+    for w in ("crc32", "qsort"):
+        for label, fu in FU_MODELS.items():
+            r = run("C5c", w, 100_000, RESULT, opc=OPC["IntAlu+IntMult+IntDiv"], fu=fu)[0]
+            r["opclass_name"], r["fu_model"] = "IntAlu+IntMult+IntDiv", label
+            recs.append(r)
+
+
+def dump(recs, tag):
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"{tag}_campaigns.json"), "w") as f:
         json.dump(recs, f, indent=1)
