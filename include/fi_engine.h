@@ -145,6 +145,11 @@ typedef struct {
  * default: it trades per-trial latency for throughput, and the campaign tail
  * is latency-bound (profiles/r02d_simt_sweep.jsonl) */
 #define FI_CFG_SIMT 256u
+/* no first-access forwarding: a register or memory fault is
+ * injected at its sampled time instead of at the golden run's next access of
+ * the flipped register or bytes (A/B and parity checks; outcomes are
+ * identical).  FI_CFG_NO_EARLY_EXIT implies it. */
+#define FI_CFG_NO_FORWARD 512u
 
 typedef struct {
     uint64_t ninst, ncycles;

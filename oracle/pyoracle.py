@@ -112,6 +112,8 @@ def lib():
         L.or_issue_model.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(IssueParams), C.c_void_p,
                                      C.POINTER(IssueStats)]
         L.or_set_issue_model.argtypes = [C.c_void_p, C.POINTER(IssueParams)]
+        L.or_golden_ops.restype = C.c_uint64
+        L.or_golden_ops.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.or_shadow_map.restype = C.c_uint64
         L.or_shadow_map.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(IssueStats)]
         L.or_sf_ref.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
@@ -149,6 +151,13 @@ class Oracle:
         p = params if isinstance(params, IssueParams) else issue_params(**{**(params or {}), **kw})
         if self.L.or_set_issue_model(self.h, C.byref(p)) != 0:
             raise RuntimeError(self.L.or_error(self.h).decode())
+
+    def golden_ops(self) -> np.ndarray:
+        """The golden trace as ISSUE_OP_DT records (register reads / writes)."""
+        n = self.L.or_golden_ops(self.h, None, 0)
+        out = np.zeros(n, ISSUE_OP_DT)
+        self.L.or_golden_ops(self.h, out.ctypes.data, n)
+        return out
 
     def shadow_map(self):
         n = self.L.or_shadow_map(self.h, None, 0, None)

@@ -2361,6 +2361,19 @@ int or_golden(or_campaign_t *c, u64 max_inst, or_golden_t *out) {
     return 0;
 }
 
+uint64_t or_golden_ops(or_campaign_t *c, or_issue_op_t *out, uint64_t cap) {
+    if (!c->have_golden) return 0;
+    mach_t m; mach_init(&m, c);
+    m.rec_cap = 4096;
+    m.rec = (or_issue_op_t *)malloc(m.rec_cap * sizeof *m.rec);
+    run(&m, c->golden.ninst + 1);
+    const u64 n = m.rec_n;
+    if (out) memcpy(out, m.rec, (cap < n ? cap : n) * sizeof *out);
+    free(m.rec); m.rec = NULL;
+    mach_free(&m);
+    return n;
+}
+
 int or_set_issue_model(or_campaign_t *c, const or_issue_params_t *p) {
     if (!p) { free(c->shadow); c->shadow = NULL; c->n_shadow = 0; return 0; }
     if (!c->have_golden) { snprintf(c->err, sizeof c->err, "or_set_issue_model: no golden run"); return -1; }

@@ -123,6 +123,9 @@ int or_issue_model(const or_issue_op_t *ops, uint64_t n, const or_issue_params_t
 /* Turn the model on for result faults (p = NULL: off).  Runs the golden
  * program once more to record its trace.  Returns 0 or -1. */
 int or_set_issue_model(or_campaign_t *c, const or_issue_params_t *p);
+/* The golden run's trace as replayed ops (one per committed instruction and
+ * ecall): copies up to cap, returns the count (needs or_golden first). */
+uint64_t or_golden_ops(or_campaign_t *c, or_issue_op_t *out, uint64_t cap);
 /* shadow per golden numInst index; returns the count (golden ninst) */
 uint64_t or_shadow_map(or_campaign_t *c, uint8_t *buf, uint64_t cap, or_issue_stats_t *stats);
 

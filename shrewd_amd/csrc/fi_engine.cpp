@@ -28,6 +28,8 @@ namespace fi {
 hipError_t launch_sample(const SampleCtx &c, uint64_t n, fi_site *sites, uint64_t *keys, uint32_t *perm,
                          hipStream_t st);
 hipError_t launch_keys(const fi_site *sites, uint64_t n, uint64_t *keys, uint32_t *perm, hipStream_t st);
+hipError_t launch_forward(const fi_site *sites, uint64_t n, const FwdCtx &c, uint64_t *keys, uint64_t *eff,
+                          hipStream_t st);
 hipError_t launch_predecode(const uint8_t *text, uint64_t code_off, uint64_t code_end, uint64_t nhalf, PreInst *pre,
                            hipStream_t st);
 hipError_t launch_debug_decode(const uint32_t *raws, uint64_t n, PreInst *out, hipStream_t st);
@@ -91,6 +93,11 @@ struct fi_engine {
     bool mem_live = false;
     uint32_t mw_n = 0;
     uint64_t *d_mw_addr = nullptr, *d_mw_ev = nullptr;
+    // first-access forwarding: per register x1..x31, the golden trace's
+    // accesses in order, entry = (2 * numInst + !ecall) << 1 | reads
+    uint32_t *d_fw_off = nullptr, *d_fw_ev = nullptr;
+    bool fw_ok = false;
+    uint64_t *d_eff = nullptr;       // [cap] effective inject time per trial (kFwDead: dead at injection)
     uint32_t *d_mw_off = nullptr;
     bool pre_ok = true;
     // load-time build of the trial kernel with the translated golden blocks
@@ -98,8 +105,6 @@ struct fi_engine {
     hipFunction_t tx_fn = nullptr, tx_fn_solo = nullptr;
     std::string tx_status = "no golden run";
     std::string tx_body;   // last generated translation (diagnostics)
-    std::vector<PreInst> tx_pre;     // its inputs: the pre-decoded text and the golden trace
-    std::vector<uint32_t> tx_trace;
 
     // golden
     bool have_golden = false;
@@ -250,6 +255,7 @@ static void free_work(fi_engine *e) {
     dfree(e->d_sites); dfree(e->d_keys); dfree(e->d_keys2); dfree(e->d_perm); dfree(e->d_perm2);
     dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg); dfree(e->d_fregs);
     dfree(e->d_save); dfree(e->d_surv[0]); dfree(e->d_surv[1]); dfree(e->d_cnt);
+    dfree(e->d_eff);
     dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_wrange); dfree(e->d_nwaves); dfree(e->d_priv); dfree(e->d_priv_vpn); dfree(e->d_vm);
     e->cap = 0;
 }
@@ -258,6 +264,10 @@ static void free_mem_index(fi_engine *e) {
     dfree(e->d_mw_addr); dfree(e->d_mw_off); dfree(e->d_mw_ev);
     e->mw_n = 0;
     e->mem_live = false;
+}
+static void free_fw(fi_engine *e) {
+    dfree(e->d_fw_off); dfree(e->d_fw_ev);
+    e->fw_ok = false;
 }
 static void free_tx(fi_engine *e) {
     if (e->tx_mod) (void)hipModuleUnload(e->tx_mod);
@@ -269,6 +279,7 @@ static void free_image(fi_engine *e) {
     dfree(e->d_text); dfree(e->d_mem_pages); dfree(e->d_gout); dfree(e->d_gerr);
     free_snaps(e);
     free_mem_index(e);
+    free_fw(e);
     free_tx(e);
     dfree(e->d_shadow);
     e->g_pre.clear(); e->g_trace.clear(); e->shadow.clear();
@@ -537,6 +548,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(sort_pairs_bytes(c, e->tmp_bytes));
     HIPCHK(hipMalloc(&e->d_tmp, std::max<size_t>(e->tmp_bytes, 16)));
     HIPCHK(hipMalloc(&e->d_out, c * sizeof(fi_outcome)));
+    HIPCHK(hipMalloc(&e->d_eff, c * 8));
     HIPCHK(hipMalloc(&e->d_hist, sizeof(fi_histogram)));
     HIPCHK(hipMalloc(&e->d_stats, kNStats * sizeof(unsigned long long)));
     HIPCHK(hipMalloc(&e->d_wave_dbg, c * 10 * sizeof(uint64_t)));
@@ -874,6 +886,37 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     e->snap_I = I;
     e->g_pre.clear(); e->g_trace.clear();
     if (live_ok && !trace.empty()) { e->g_pre = pre; e->g_trace = trace; }
+    // ---- first-access index (DESIGN.md §4 "first-access forwarding"): a
+    // register flipped at numInst t is neither read nor written by the golden
+    // run before its next access, so flipping it at that access instead gives
+    // the same machine; written first (or never touched again) it is dead.
+    free_fw(e);
+    {
+        const bool ok = live_ok && !trace.empty() && o.ninst < (1ULL << 29);
+        std::vector<uint32_t> off(33, 0), ev;
+        if (ok) {
+            for (size_t i = 0; i < trace.size(); i++)
+                for (uint32_t m = (rmask[i] | wmask[i]) & ~1u; m; m &= m - 1) off[__builtin_ctz(m) + 1]++;
+            for (int r = 0; r < 32; r++) off[r + 1] += off[r];
+            ev.resize(off[32]);
+            std::vector<uint32_t> at(off.begin(), off.end() - 1);
+            uint64_t t = 0;
+            for (size_t i = 0; i < trace.size(); i++) {
+                const bool ecall = (trace[i] & 0x80000000u) != 0;
+                const uint32_t key = (uint32_t)(2 * t + (ecall ? 0 : 1));
+                for (uint32_t m = (rmask[i] | wmask[i]) & ~1u; m; m &= m - 1) {
+                    const int r = __builtin_ctz(m);
+                    ev[at[r]++] = (key << 1) | ((rmask[i] >> r) & 1u);
+                }
+                if (!ecall) t++;
+            }
+            HIPCHK(hipMalloc(&e->d_fw_off, 33 * 4));
+            HIPCHK(hipMalloc(&e->d_fw_ev, std::max<size_t>(ev.size(), 1) * 4));
+            HIPCHK(hipMemcpy(e->d_fw_off, off.data(), 33 * 4, hipMemcpyHostToDevice));
+            if (!ev.empty()) HIPCHK(hipMemcpy(e->d_fw_ev, ev.data(), ev.size() * 4, hipMemcpyHostToDevice));
+            e->fw_ok = true;
+        }
+    }
     st = upload_snaps(e);
     if (st) return st;
     st = build_mem_index(e, mev, live_ok && n_mem <= mem_cap);
@@ -895,8 +938,6 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         uint32_t n_tx = 0;
         const std::string body = translate_blocks(pre, e->text_lo, trace, pcs, leaders, n_tx);
         e->tx_body = body;
-        e->tx_pre = pre;
-        e->tx_trace = trace;
         hipDeviceProp_t prop;
         HIPCHK(hipGetDeviceProperties(&prop, e->dev));
         if (const char *dump = getenv("SHREWD_FI_DUMP_TX")) {   // diagnostics: the generated blocks
@@ -1074,10 +1115,25 @@ static hipError_t launch_trial_kernel(fi_engine *e, DevCtx &c, hipStream_t st, b
 // One launch: d_sites[0..k) holds the sites in trial order, keys/perm set.
 static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histogram *d_hist, hipStream_t st) {
     int end_bit = 64 - __builtin_clzll(std::max<uint64_t>(e->golden.ninst, 1));
+    // (a dead site ends at injection: an early exit, so not with FI_CFG_NO_EARLY_EXIT)
+    const bool fwd = e->fw_ok && !(e->cfg.flags & (FI_CFG_NO_FORWARD | FI_CFG_NO_EARLY_EXIT));
+    if (fwd) {
+        FwdCtx fc{};
+        fc.reg_off = e->d_fw_off; fc.reg_ev = e->d_fw_ev;
+        // memory sites only when the golden run's mappings are static (no VM
+        // syscalls: golden_fp covers them) and its access index is complete
+        const bool memf = e->mem_live && !e->golden_fp && e->snaps.size() > 1;
+        fc.mw_n = memf ? e->mw_n : 0;
+        fc.mw_addr = e->d_mw_addr; fc.mw_off = e->d_mw_off; fc.mw_ev = e->d_mw_ev;
+        fc.snaps = e->d_snaps; fc.snap_tab = e->d_tab; fc.n_snap = (uint32_t)e->snaps.size();
+        fc.snap_interval = e->snap_I; fc.text_lo = e->text_lo; fc.text_hi = e->text_hi;
+        HIPCHK(launch_forward(e->d_sites, k, fc, e->d_keys, e->d_eff, st));
+    }
     HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_keys, e->d_keys2, e->d_perm, e->d_perm2, k, end_bit, st));
     DevCtx c = base_ctx(e);
     c.sites = e->d_sites;
     c.perm = e->d_perm2;
+    c.eff = fwd ? e->d_eff : nullptr;
     c.out = d_out;
     c.n = k;
     c.n_slots = (uint32_t)k;
@@ -1279,10 +1335,10 @@ fi_status fi_debug_epochs(fi_engine *e, uint32_t *out16) {
 fi_status fi_debug_golden_trace(fi_engine *e, void *pre_out, uint64_t pre_cap, uint64_t *n_pre, uint32_t *trace_out,
                                 uint64_t trace_cap, uint64_t *n_trace, uint64_t *text_lo) {
     if (!e) return FI_E_ARG;
-    if (pre_out) memcpy(pre_out, e->tx_pre.data(), std::min<uint64_t>(pre_cap, e->tx_pre.size()) * sizeof(PreInst));
-    if (trace_out) memcpy(trace_out, e->tx_trace.data(), std::min<uint64_t>(trace_cap, e->tx_trace.size()) * 4);
-    if (n_pre) *n_pre = e->tx_pre.size();
-    if (n_trace) *n_trace = e->tx_trace.size();
+    if (pre_out) memcpy(pre_out, e->g_pre.data(), std::min<uint64_t>(pre_cap, e->g_pre.size()) * sizeof(PreInst));
+    if (trace_out) memcpy(trace_out, e->g_trace.data(), std::min<uint64_t>(trace_cap, e->g_trace.size()) * 4);
+    if (n_pre) *n_pre = e->g_pre.size();
+    if (n_trace) *n_trace = e->g_trace.size();
     if (text_lo) *text_lo = e->text_lo;
     return FI_OK;
 }

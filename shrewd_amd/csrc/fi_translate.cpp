@@ -615,7 +615,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 const std::string v = subst(e, A, B, immb, pcb);
                 if (p.rd) {
                     g.put("  TXSET(%u, %s);\n", p.rd, v.c_str());
-                    so.put("  X%u = %s;\n", p.rd, v.c_str());
+                    so.put("  SX(%u, %s);\n", p.rd, v.c_str());
                 }
                 break;
             }
@@ -624,7 +624,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             case C_LOAD:
                 g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, false, p_, tx);\n", A.c_str(), immb, sz);
                 g.put("    if (TXB(mine && !ok_)) %s\n", leave_here.c_str());
-                so.put("  { uint8_t *p_; if (!tx_probe(m, %s + %s, %uu, false, p_, tx)) %s\n", A.c_str(), immb, sz,
+                so.put("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, false, p_, tx))) %s\n", A.c_str(), immb, sz,
                        sleave_here.c_str());
                 if (p.rd) {
                     g.put("    p_ = ok_ ? p_ : const_cast<uint8_t *>(zp);\n");
@@ -647,9 +647,9 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 // solo: a store into the code range is performed too; it marks the
                 // bytes rewritten and leaves after itself if they lie ahead in this block
                 so.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s; const uint32_t cs_ = tx_probe_st(m, ea_, %uu, "
-                       "p_, tx); if (!cs_) %s\n", A.c_str(), immb, sz, sleave_here.c_str());
+                       "p_, tx); if (SCOND(!cs_)) %s\n", A.c_str(), immb, sz, sleave_here.c_str());
                 so.put("    *(g_%s *)p_ = (%s)%s;\n", gtype(sz), ltype(sz), B.c_str());
-                so.put("    if (cs_ & 2u) { TXCODE(ea_, %uu); if (ea_ < %s && ea_ + %uu > %s) { %sspc = %s; "
+                so.put("    if (SCOND(cs_ & 2u)) { TXCODE(ea_, %uu); if (SCOND(ea_ < %s && ea_ + %uu > %s)) { %sspc = %s; "
                        "goto S_out; } } }\n", sz, hex(bhi).c_str(), sz, ftb.c_str(),
                        scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db + sz).c_str(), ftb.c_str());
                 break;
@@ -674,7 +674,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                           ftb.c_str(), ftb.c_str());
                     g.put("    %s }\n", wgo(h0, tgt).c_str());
                 }
-                so.put("  %s\n  if (%s) %s\n  %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), c.c_str(),
+                so.put("  %s\n  if (SCOND(%s)) %s\n  %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), c.c_str(),
                        sgo(h0, tgt).c_str(), sgo(h0, ft).c_str());
                 break;
             }
@@ -682,7 +682,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 const uint64_t tgt = pc + (int64_t)p.imm;
                 if (p.rd) {
                     g.put("  TXSET(%u, %s);\n", p.rd, ftb.c_str());
-                    so.put("  X%u = %s;\n", p.rd, ftb.c_str());
+                    so.put("  SX(%u, %s);\n", p.rd, ftb.c_str());
                 }
                 g.put("  %s %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), wgo(h0, tgt).c_str());
                 so.put("  %s %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), sgo(h0, tgt).c_str());
@@ -698,8 +698,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 g.put("    if (TXB(mine && t_ != t0_)) { dpc = t_; jdiv = mine; goto tx_out; }\n");
                 g.put("    spc = uni64(t0_); goto tx_dispatch; }\n");
                 so.put("  { const uint64_t t_ = (%s + (uint64_t)(int64_t)%lldLL) & ~1ULL;\n", A.c_str(), (long long)im);
-                if (rd) so.put("    X%u = %s;\n", rd, ftb.c_str());
-                so.put("    %s spc = t_; goto S_dispatch; }\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
+                if (rd) so.put("    SX(%u, %s);\n", rd, ftb.c_str());
+                so.put("    %s spc = SUNI(t_); goto S_dispatch; }\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
                 break;
             }
             default:

@@ -8,6 +8,7 @@
 namespace fi {
 
 constexpr uint64_t kPage = 4096;
+constexpr uint64_t kFwDead = ~0ULL;  // DevCtx::eff: the flipped register is dead at injection
 // RiscvProcess64 constants, src/arch/riscv/process.cc:73-80
 constexpr uint64_t kStackBase = 0x7FFFFFFFFFFFFFFFULL;
 constexpr uint64_t kMaxStack = 8ULL * 1024 * 1024;
@@ -90,6 +91,23 @@ struct MemEv {
     uint32_t len_kind;               // len (< 2^30) | kind << 30
 };
 
+// First-access forwarding (fi_forward_kernel): the golden run's register
+// accesses (always) and its memory accesses (when complete and the golden
+// run's mappings never change: no VM syscalls), with the snapshot page tables
+// to check that a memory site is mapped at its sampled time.
+struct FwdCtx {
+    const uint32_t *reg_off, *reg_ev;    // per register x1..x31: (2 * numInst + !ecall) << 1 | reads
+    uint32_t mw_n;                       // 0: no memory forwarding
+    const uint64_t *mw_addr;
+    const uint32_t *mw_off;
+    const uint64_t *mw_ev;
+    const SnapState *snaps;
+    const PageEnt *snap_tab;
+    uint32_t n_snap;
+    uint64_t snap_interval;
+    uint64_t text_lo, text_hi;
+};
+
 // Everything one launch of the trial kernel needs.  Passed by value as the
 // kernel argument (lives in the kernarg segment -> scalar loads).
 constexpr int kNStats = 40;          // DevCtx::stats entries
@@ -123,6 +141,8 @@ struct DevCtx {
     uint64_t hang_cap;
     uint64_t protect_mask;
     uint64_t protect_opc;            // SHREWD replication: protected gem5 OpClass values (bit mask)
+    const uint64_t *eff;             // first-access forwarding: effective inject time per trial (in site order;
+                                     // kFwDead = dead at injection), nullptr = the sampled times
     const uint32_t *shadow_bits;     // FU contention model: bit k = the k-th golden instruction's shadow issued
                                      // (nullptr: every shadow-capable instruction has one)
     // per-trial private (copy-on-write) pages: frames [slot][P][4096], vpns [P][n]

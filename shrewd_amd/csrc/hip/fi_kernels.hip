@@ -66,6 +66,65 @@ __global__ void fi_keys_kernel(const fi_site *sites, uint64_t n, uint64_t *keys,
     perm[i] = (uint32_t)i;
 }
 
+// First-access forwarding.  A register site (x1..x31) at
+// time t is injected at the golden run's next access of that register
+// instead: the golden run neither reads nor writes it in between, so the
+// trial's machine is the same.  Next access a write (or none): dead, the
+// trial is the golden run.  A memory site likewise moves to the next golden
+// access of any of its flipped bytes, if its page is mapped at t (present
+// in the page table of the snapshot at or before t; the golden run maps and
+// unmaps nothing) and it lies outside the text (fetches are not accesses);
+// its dead case stays with the kernel (mem_dead).  Sort key = the effective
+// time (dead: 0, they end at once).
+__device__ __forceinline__ bool fw_mapped(const FwdCtx &c, uint64_t vpn, uint64_t t) {
+    const uint64_t k = t / c.snap_interval;
+    const SnapState &S = c.snaps[k < c.n_snap ? k : c.n_snap - 1];
+    uint32_t lo = S.tab_off, hi = S.tab_off + S.tab_n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (c.snap_tab[mid].vpn < vpn) lo = mid + 1; else hi = mid;
+    }
+    return lo < S.tab_off + S.tab_n && c.snap_tab[lo].vpn == vpn;
+}
+__global__ void fi_forward_kernel(const fi_site *sites, uint64_t n, FwdCtx c, uint64_t *keys, uint64_t *eff) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const fi_site s = sites[i];
+    uint64_t f = s.inst;
+    if (s.target >= 1 && s.target <= 31 && s.inst < (1ULL << 29)) {
+        const uint32_t key = (uint32_t)(4 * s.inst);   // (2t) << 1: before both events of numInst t
+        uint32_t lo = c.reg_off[s.target], hi = c.reg_off[s.target + 1];
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (c.reg_ev[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        f = (lo == c.reg_off[s.target + 1] || !(c.reg_ev[lo] & 1u)) ? kFwDead : (uint64_t)(c.reg_ev[lo] >> 2);
+    } else if (s.target == FI_T_MEM && c.mw_n && !(s.addr < c.text_hi && s.addr + 8 > c.text_lo) &&
+               fw_mapped(c, s.addr >> 12, s.inst)) {
+        uint32_t fb = 0;
+        for (int b = 0; b < 8; b++) fb |= ((s.mask >> (8 * b)) & 0xFF) ? (1u << b) : 0u;
+        uint32_t lo = 0, hi = c.mw_n;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (c.mw_addr[mid] < s.addr) lo = mid + 1; else hi = mid;
+        }
+        if (lo < c.mw_n && c.mw_addr[lo] == s.addr) {
+            uint32_t a = c.mw_off[lo], b = c.mw_off[lo + 1];
+            const uint32_t e = b;
+            while (a < b) {   // first event at numInst >= t
+                const uint32_t mid = (a + b) >> 1;
+                if ((c.mw_ev[mid] >> 16) < s.inst) a = mid + 1; else b = mid;
+            }
+            for (; a < e; a++) {
+                const uint64_t ev = c.mw_ev[a];
+                if (((ev >> 8) | ev) & fb & 0xFF) { f = ev >> 16; break; }
+            }
+        }
+    }
+    eff[i] = f;
+    keys[i] = f == kFwDead ? 0 : f;
+}
+
 // ------------------------------------------------------------------ predecode
 // One entry per halfword of [text_lo, text_hi).  Fetch follows
 // Decoder::moreBytes (src/arch/riscv/decoder.cc:63-116): a 4-byte word at
@@ -211,6 +270,11 @@ static inline unsigned nblk(uint64_t n, unsigned b) { return (unsigned)((n + b -
 hipError_t launch_sample(const SampleCtx &c, uint64_t n, fi_site *sites, uint64_t *keys, uint32_t *perm,
                          hipStream_t st) {
     hipLaunchKernelGGL(fi_sample_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, c, n, sites, keys, perm);
+    return hipGetLastError();
+}
+hipError_t launch_forward(const fi_site *sites, uint64_t n, const FwdCtx &c, uint64_t *keys, uint64_t *eff,
+                          hipStream_t st) {
+    hipLaunchKernelGGL(fi_forward_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, sites, n, c, keys, eff);
     return hipGetLastError();
 }
 hipError_t launch_keys(const fi_site *sites, uint64_t n, uint64_t *keys, uint32_t *perm, hipStream_t st) {

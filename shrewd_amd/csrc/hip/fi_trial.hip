@@ -1122,6 +1122,29 @@ typedef __attribute__((address_space(1), aligned(1))) uint64_t g_u64;
         X##r = mine ? t_ : X##r;                            \
     } while (0)
 
+// Solo translated code: where the trial's guest registers live.  By default
+// the compiler keeps them (uniform in a one-lane wave) in SGPRs; with
+// FI_SOLO_VREG they are pinned in VGPRs (an asm barrier on every write) and
+// only branch conditions and jump targets are made uniform again, which
+// trades SGPR spills for VALU work (A/B knob SHREWD_FI_SOLO_VREG).
+#ifdef FI_SOLO_VREG
+#define SVREG(v) __asm__ volatile("" : "+v"(v))
+#define SCOND(x) (__builtin_amdgcn_readfirstlane((int)(bool)(x)) != 0)
+#define SUNI(x) uni64(x)
+#define SUNI32(x) ((uint32_t)__builtin_amdgcn_readfirstlane((int)(x)))
+#else
+#define SVREG(v) ((void)0)
+#define SCOND(x) (x)
+#define SUNI(x) (x)
+#define SUNI32(x) (x)
+#endif
+#define SX(r, e)                         \
+    do {                                 \
+        uint64_t s_ = (uint64_t)(e);     \
+        SVREG(s_);                       \
+        X##r = s_;                       \
+    } while (0)
+
 // The pre-decoded text (uniform): table, text range, exact code range.
 struct TextRef { const PreInst *pre; uint32_t lo, hi, bytes; uint64_t clo, chi; };
 
@@ -1198,6 +1221,13 @@ __device__ __forceinline__ bool ult64(uint64_t a, uint64_t b) {
 
 // Waves per SIMD the register allocation must allow (the translated build
 // sets it per engine; see fi_jit.cpp).
+// solo kernel register budget: 4 waves per SIMD (<= 128 VGPRs).  A/B on
+// crc32 (tools/gpu/solo_ab.sh, profiles/r02j_solo_ab.txt): 1 (no bound, 136-140
+// VGPRs, 3 waves) 6.44M, 4: 7.06M trials/s; VGPR-pinned guest registers
+// (FI_SOLO_VREG) 3.2-3.7M.
+#ifndef FI_SOLO_WAVES_PER_EU
+#define FI_SOLO_WAVES_PER_EU 4
+#endif
 #ifndef FI_WAVES_PER_EU
 #define FI_WAVES_PER_EU 1
 #endif
@@ -1233,13 +1263,23 @@ __device__ __forceinline__ void trial_body() {
     fi_site s;
     s.inst = kNone; s.mask = 0; s.addr = 0; s.target = 0; s.trial = 0;
     uint32_t sidx = 0;
-    if (live && !CX->record) { sidx = CX->perm[slot]; s = CX->sites[sidx]; }
+    bool fw_dead = false;
+    if (live && !CX->record) {
+        sidx = CX->perm[slot]; s = CX->sites[sidx];
+        if (CX->eff) {   // first-access forwarding (fi_forward_kernel)
+            const uint64_t f = CX->eff[sidx];
+            fw_dead = f == kFwDead;
+            s.inst = fw_dead ? s.inst : f;
+        }
+    }
 
     // ---- start snapshot: the last one at or before the wave's earliest
     // inject time (lane 0 holds it: slots are sorted by inject time)
     uint32_t j = 0;
     if (!resume && !CX->record && CX->snap_start && CX->n_snap > 1) {
-        const uint64_t t0 = uni64(CX->sites[CX->perm[(uint64_t)blockIdx.x * nlw]].inst);
+        const uint32_t i0 = CX->perm[(uint64_t)blockIdx.x * nlw];
+        const uint64_t e0 = CX->eff ? CX->eff[i0] : CX->sites[i0].inst;
+        const uint64_t t0 = uni64(e0 == kFwDead ? 0 : e0);
         const uint64_t k = t0 / CX->snap_interval;
         j = (uint32_t)(k < CX->n_snap ? k : CX->n_snap - 1);
     }
@@ -1284,6 +1324,12 @@ __device__ __forceinline__ void trial_body() {
         m.dlo = CX->code_lo + SV->dlo; m.dhi = CX->code_lo + SV->dhi;
         m.resv = SV->resv; m.lock = SV->lock;
         m.vm = (SV->flags >> 5) & 1;
+    }
+    if (fw_dead && !resume) {   // dead at injection: the trial is the golden run
+        L.injected = 1;
+        finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
+        L.res.ninst = CX->gninst;
+        atomicAdd(&CX->stats[27], 1ull);
     }
     bool suspended = false;
     const uint64_t start_inst = (live && !resume) ? L.ninst : 0;
@@ -1704,7 +1750,7 @@ __device__ __forceinline__ void trial_body() {
 // grown range; the decode cache forgets them when the blocks are left
 #define TXCODE(ea_, sz_)                                                                        \
     do {                                                                                        \
-        const uint32_t o_ = (uint32_t)((ea_) - tlo);                                            \
+        const uint32_t o_ = SUNI32((uint32_t)((ea_) - tlo));                                    \
         sdlo = o_ < sdlo ? o_ : sdlo;                                                           \
         sdhi = o_ + (sz_) > sdhi ? o_ + (sz_) : sdhi;                                           \
         cslo = o_ < cslo ? o_ : cslo;                                                           \
@@ -1715,7 +1761,7 @@ __device__ __forceinline__ void trial_body() {
                     uint32_t st = 0, xt = 0, fb = 0, db = 0;   // instructions, straddles, fetch/data bytes
                     uint64_t spc = lpc;
                     uint32_t etgt = 0xFFFFFFFFu;   // block an entry is routed to through its cycle headers
-#define TXR(r) uint64_t X##r = RREG(r);
+#define TXR(r) uint64_t X##r = RREG(r); SVREG(X##r);
                     TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
                     TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
                     TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
@@ -2619,7 +2665,7 @@ __device__ __forceinline__ void trial_body() {
 // The two instantiations (load-time build: with the translated blocks).
 #ifdef __HIPCC_RTC__
 extern "C" __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel_tx(DevCtx) { trial_body<64>(); }
-extern "C" __global__ void __launch_bounds__(1) fi_trial_kernel_tx_solo(DevCtx) { trial_body<1>(); }
+extern "C" __global__ void __launch_bounds__(1, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_tx_solo(DevCtx) { trial_body<1>(); }
 #else
 __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx) { trial_body<64>(); }
 __global__ void __launch_bounds__(1) fi_trial_kernel_solo(DevCtx) { trial_body<1>(); }

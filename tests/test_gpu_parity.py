@@ -233,6 +233,47 @@ def test_result_faults_under_contention_bit_exact(engine_factory, oracle_mod, na
     assert det.any() and not (det & (sh[sites["inst"]] == 0)).any()
 
 
+@pytest.mark.parametrize("name", ["hello", "crc32", "qsort", "intmix", "fpamo"])
+def test_golden_register_accesses_match_oracle(engine_factory, oracle_mod, name):
+    """The integer registers every golden instruction and ecall reads and
+    writes -- the inputs of register liveness, first-access forwarding and the
+    issue model -- equal the oracle's, event by event."""
+    e = engine_factory(name)
+    o = oracle_for(oracle_mod, name)
+    pre, tr, _ = e.debug_golden_trace()
+    ops = o.golden_ops()
+    assert len(tr) == len(ops) > 0
+    rec = pre[tr & 0x7FFFFFFF]
+    rd, rs1, rs2, fl = (rec[:, k].astype(np.uint64) for k in (5, 6, 7, 13))
+    one = np.uint64(1)
+    src = (np.where((fl & 4) != 0, one << rs1, 0) | np.where((fl & 8) != 0, one << rs2, 0)).astype(np.uint64)
+    dst = np.where((fl & 16) != 0, one << rd, 0).astype(np.uint64)
+    ecall = (tr & 0x80000000) != 0
+    src[ecall], dst[ecall] = 0x3FC00, 1 << 10
+    m = np.uint64(0xFFFFFFFE)
+    bad = np.flatnonzero(((src & m) != (ops["src"] & m)) | ((dst & m) != (ops["dst"] & m)))
+    assert not len(bad), f"{len(bad)} events differ, first {bad[:5].tolist()}"
+
+
+@pytest.mark.parametrize("name", ["crc32", "qsort", "intmix"])
+def test_first_access_forwarding(engine_factory, oracle_mod, name):
+    """Register sites are injected at the golden run's next access of the
+    register (dead ones end at injection): outcomes equal the oracle's and
+    the unforwarded engine's."""
+    e = engine_factory(name)
+    f = engine_factory(name, flags=512)
+    o = oracle_for(oracle_mod, name)
+    for x in (e, f):
+        x.set_campaign(0xF0A0, REGS, 1)
+    sites = e.sample(0, 3000)
+    dev, _ = e.run_sites(sites)
+    dead = int(e.debug_stats()[27])
+    ref, _ = f.run_sites(sites)
+    assert int(f.debug_stats()[27]) == 0 and dead > 0
+    compare(dev, ref, sites)
+    compare(dev, o.run_trials(sites), sites)
+
+
 def test_translation_skipped_without_hot_code(engine_factory):
     """Straight-line code run once (hello) is not translated: the static
     kernels run it, and the engine says why."""
@@ -279,6 +320,7 @@ PATH_FLAGS = {
     "solo_all": 128,                        # FI_CFG_SOLO_ALL: every epoch on the one-trial-per-wave kernel
     "solo_all_interp": 128 | 4,             # the solo build without translated blocks
     "simt": 256,                            # FI_CFG_SIMT: diverged lanes step together, per lane
+    "no_forward": 512,                      # FI_CFG_NO_FORWARD: inject at the sampled time
     "simt_no_solo_interp": 256 | 64 | 4,    # the step loop for every epoch, no translated blocks
 }
 _PATH_REF = {}
