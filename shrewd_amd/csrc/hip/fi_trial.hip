@@ -1231,10 +1231,41 @@ __device__ __forceinline__ bool ult64(uint64_t a, uint64_t b) {
 #ifndef FI_WAVES_PER_EU
 #define FI_WAVES_PER_EU 1
 #endif
+// Solo kernel: the launch context through a plain pointer, so that the
+// compiler can keep loop-invariant fields in registers (a one-lane wave has
+// VGPR lanes to spill them to) instead of a scalar load + wait at each use
+// (A/B knob SHREWD_FI_SOLO_CX=0).
+#ifndef FI_SOLO_CX_DIRECT
+#define FI_SOLO_CX_DIRECT 1
+#endif
 template <uint32_t kNL>
 __device__ __forceinline__ void trial_body() {
     KCtx *const kc = (KCtx *)__builtin_amdgcn_kernarg_segment_ptr();
-#define CX (opq(kc))
+#define CX ((kNL == 1 && FI_SOLO_CX_DIRECT) ? kc : opq(kc))
+// An out-of-line helper that takes the lane's memory state (or the wave's
+// page table) by reference runs on copies: a reference to the interpreter's
+// own LaneMem would pin it in scratch memory for the whole kernel, and every
+// TLB probe of the hot loops would become a scratch load.
+// (A/B knob SHREWD_FI_SOLO_OOL=1, solo kernel only: with the copies the
+// interpreter-bound tail trials ran 10-20 % faster, but the crc32 bench lost
+// 12 %, 10.0M -> 8.8M trials/s, profiles/r02l_ab.txt)
+#ifndef FI_SOLO_OOL_COPY
+#define FI_SOLO_OOL_COPY 0
+#endif
+#define OOL(stmt)                                 \
+    do {                                          \
+        if constexpr (kNL == 1 && FI_SOLO_OOL_COPY) { \
+            LaneMem mc_ = m;                      \
+            WaveMem wc_ = w;                      \
+            stmt;                                 \
+            m = mc_;                              \
+            (void)wc_;                            \
+        } else {                                  \
+            LaneMem &mc_ = m;                     \
+            const WaveMem &wc_ = w;               \
+            stmt;                                 \
+        }                                         \
+    } while (0)
     __shared__ uint64_t R[kRows * kNL];
     const uint64_t t_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
     const uint32_t lane = lane_id<kNL>();
@@ -1343,6 +1374,10 @@ __device__ __forceinline__ void trial_body() {
     uint64_t plast = __builtin_amdgcn_s_memtime();
 #endif
     uint32_t n_iter = 0;   // per-wave loop iterations (uniform)
+    // solo: a lane whose translated runs keep ending after a few instructions
+    // (its loop holds rewritten code, so every block exit writes back and
+    // reloads the register file) stays in the pre-decoded path for a while
+    uint32_t tx_short = 0, tx_skip_until = 0;
     // per-wave diagnostic counters live in LDS, not SGPRs (the loop's scalar
     // registers are scarce): slow fetches, min-PC reductions, lane-instructions,
     // snapshot checks, early exits, translated instructions and entries.  Every
@@ -1445,7 +1480,8 @@ __device__ __forceinline__ void trial_body() {
             } else if (s.target == FI_T_RESULT) {
                 L.injected = 3;   // armed: the next instruction that commits (general path) is the target
             } else if (s.target == FI_T_MEM) {
-                const uint64_t p = lookup(CX, w, m, slot, s.addr >> 12);
+                uint64_t p;
+                OOL(p = lookup(CX, wc_, mc_, slot, s.addr >> 12));
                 if (!p) {
                     L.injected = 2;    // page not mapped at t: nothing to flip
                     if (CX->mem_live) {   // ... so the trial is the golden run
@@ -1655,7 +1691,7 @@ __device__ __forceinline__ void trial_body() {
                                 const uint64_t ea = a0 + imm;
                                 const uint32_t off = (uint32_t)(ea & 4095);
                                 uint64_t p = tlb_find(m, ea >> 12);
-                                if (!p) p = lookup_full(CX, w, m, slot, ea >> 12);
+                                if (!p) OOL(p = lookup_full(CX, wc_, mc_, slot, ea >> 12));
                                 const bool code_st = st && !(ea >= chi || ea + msz <= clo);
                                 if (!(p && (!st || ((p & 1) && !code_st)) && off + msz <= 4096)) { go = false; break; }
                                 uint8_t *pg = const_cast<uint8_t *>(page_of(p));
@@ -1735,7 +1771,8 @@ __device__ __forceinline__ void trial_body() {
             if constexpr (kNL == 1) {
                 // ---- solo: one trial, every value uniform -- no groups, no
                 // parking, plain register writes; the same exits and counters
-                if (tx_entry && mine && !dirty_near(m, lpc) && L.injected != 3 && m.lock == kNone) {
+                if (tx_entry && mine && n_iter >= tx_skip_until && !dirty_near(m, lpc) && L.injected != 3 &&
+                    m.lock == kNone) {
                     const uint64_t rem64 = next_ev - L.ninst;
                     const uint32_t rem = rem64 > (1u << 30) ? (1u << 30) : (uint32_t)rem64;
                     const uint32_t wbud = CX->wave_budget ? CX->wave_budget - n_iter : (1u << 30);
@@ -1787,6 +1824,11 @@ __device__ __forceinline__ void trial_body() {
                     n_iter += st;
                     n_tx += st;
                     n_txin++;
+                    if (m.code_dirty && st < 8) {
+                        if (++tx_short >= 4) { tx_short = 0; tx_skip_until = n_iter + 4096; }
+                    } else {
+                        tx_short = 0;
+                    }
                     if (st) continue;
                 }
             } else if (tx_entry &&
@@ -1920,7 +1962,7 @@ __device__ __forceinline__ void trial_body() {
                     uint32_t raw = 0, t = 1;
                     uint64_t fva = 0;
                     int fr = 0;
-                    if (mine) fr = fetch_lane(CX, w, m, slot, spc, raw, t, fva);
+                    if (mine) OOL(fr = fetch_lane(CX, wc_, mc_, slot, spc, raw, t, fva));
                     const uint32_t raw0 = (uint32_t)rdl32<kNL>((uint32_t)raw, glane);
                     const uint32_t t0 = (uint32_t)rdl32<kNL>((uint32_t)t, glane);
                     if (wballot<kNL>(mine && (fr != 0 || raw != raw0)) != 0) break;
@@ -1947,7 +1989,7 @@ __device__ __forceinline__ void trial_body() {
                 if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
 #ifdef FI_TX
                 if (steps && ((q3 >> 8) & kPreLeader) &&   // translated blocks take over here
-                    !(any_dirty && wballot<kNL>(mine && dirty_near(m, spc)) != 0))
+                    !(any_dirty && wballot<kNL>(mine && dirty_near(m, spc)) != 0) && n_iter + steps >= tx_skip_until)
                     break;
 #endif
                 const uint32_t rd = q1 >> 8 & 0xFF, rs1 = q1 >> 16 & 0xFF, rs2 = q1 >> 24;
@@ -2033,7 +2075,7 @@ __device__ __forceinline__ void trial_body() {
                     uint64_t p = 0;
                     if (mine) {
                         p = tlb_find(m, ea >> 12);
-                        if (!p) p = lookup_full(CX, w, m, slot, ea >> 12);
+                        if (!p) OOL(p = lookup_full(CX, wc_, mc_, slot, ea >> 12));
                     }
                     // a store into the code range rewrites the lane's code: the
                     // general path's business, except in the solo kernel, which
@@ -2153,13 +2195,15 @@ __device__ __forceinline__ void trial_body() {
             uint32_t raw = 0, t = 1;
             uint64_t fva = 0;
             if (mine) {
-                const int fr = fetch_lane(CX, w, m, slot, L.pc, raw, t, fva);
+                int fr;
+                OOL(fr = fetch_lane(CX, wc_, mc_, slot, L.pc, raw, t, fva));
                 if (fr) {
                     // the faulting tick(s) count, nothing commits; decoder reset;
                     // GenericPageTableFault::invoke -> fixupFault (sim/faults.cc:95-105)
                     L.ncyc += t;
                     mine = false;
-                    const int h = fixup_fault(CX, m, slot, fva);
+                    int h;
+                    OOL(h = fixup_fault(CX, mc_, slot, fva));
                     if (h == 0) finish(L, FI_CRASH, FI_CRASH_PAGE_FAULT, 134, (uint32_t)fva);
                     else if (h == -1) finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, (uint32_t)L.pc);
                     else if (h == -2) finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, (uint32_t)L.pc);
@@ -2476,7 +2520,7 @@ __device__ __forceinline__ void trial_body() {
 #pragma unroll 1
             for (int pass = 0; pass < (amo >= 0 ? 2 : 1); pass++) {
                 t = pass ? amo_apply(amo, old, b, msz == 4) : (amo >= 0 ? 0 : (llsc == 2 ? b : sval));
-                f = mem_access(CX, w, m, slot, ea, msz, pass ? true : mst, t, fva, amo >= 0 ? 3 : llsc);
+                OOL(f = mem_access(CX, wc_, mc_, slot, ea, msz, pass ? true : mst, t, fva, amo >= 0 ? 3 : llsc));
                 if (f != F_NONE) break;
                 if (!pass) old = t;
             }
@@ -2554,7 +2598,8 @@ __device__ __forceinline__ void trial_body() {
         case F_AMOLINE: finish(L, FI_CRASH, FI_CRASH_AMO_LINE, 134, (uint32_t)pc); break;
         case F_SCLINE: finish(L, FI_CRASH, FI_CRASH_SC_LINE, 134, (uint32_t)pc); break;
         case F_PGFAULT: {   // GenericPageTableFault::invoke -> fixupFault (sim/faults.cc:95-105)
-            const int h = fixup_fault(CX, m, slot, fva);
+            int h;
+            OOL(h = fixup_fault(CX, mc_, slot, fva));
             if (h == 0) finish(L, FI_CRASH, FI_CRASH_PAGE_FAULT, 134, (uint32_t)fva);
             else if (h == -1) finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, (uint32_t)pc);
             else if (h == -2) finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, (uint32_t)pc);
@@ -2668,7 +2713,7 @@ extern "C" __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kerne
 extern "C" __global__ void __launch_bounds__(1, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_tx_solo(DevCtx) { trial_body<1>(); }
 #else
 __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx) { trial_body<64>(); }
-__global__ void __launch_bounds__(1) fi_trial_kernel_solo(DevCtx) { trial_body<1>(); }
+__global__ void __launch_bounds__(1, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_solo(DevCtx) { trial_body<1>(); }
 
 hipError_t launch_trials(const DevCtx &c, hipStream_t st) {
     const uint32_t gl = (c.resume && c.resume_waves) ? 1u : c.lanes;   // grid for the fewest lanes per wave
