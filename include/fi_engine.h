@@ -109,7 +109,7 @@ typedef struct {
     int32_t device;                 /* HIP device ordinal */
     uint32_t private_pages;         /* copy-on-write pages per trial (0 -> 16) */
     uint32_t hang_factor_x16;       /* hang cap = golden_ninst * f / 16 + 1000 (0 -> 32) */
-    uint32_t max_trials_per_launch; /* 0 -> 65536 */
+    uint32_t max_trials_per_launch; /* 0 -> auto: as many as half the free device memory holds (65536 .. 2M) */
     uint32_t snapshot_interval;     /* golden snapshot every N committed insts (0 -> auto, >= 256) */
     uint32_t flags;                 /* FI_CFG_* */
     uint32_t epoch_iters;           /* first epoch's loop iterations per wave (0 -> 4096; then x4, x16, unbounded) */

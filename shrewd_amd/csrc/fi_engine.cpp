@@ -220,7 +220,6 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
     if (cfg) e->cfg = *cfg;
     if (e->cfg.private_pages == 0) e->cfg.private_pages = 16;
     if (e->cfg.hang_factor_x16 == 0) e->cfg.hang_factor_x16 = 32;
-    if (e->cfg.max_trials_per_launch == 0) e->cfg.max_trials_per_launch = 65536;
     if (e->cfg.lanes_per_wave == 0) e->cfg.lanes_per_wave = kDefaultLanes;
     if (e->cfg.resume_lanes == 0) e->cfg.resume_lanes = kDefaultResumeLanes;
     for (uint32_t l : {e->cfg.lanes_per_wave, e->cfg.resume_lanes}) {
@@ -246,6 +245,16 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
         g_create_err = "fi_create: " + e->err;
         delete e;
         return FI_E_HIP;
+    }
+    if (e->cfg.max_trials_per_launch == 0) {
+        // auto: a campaign's trials in as few launches as half the free HBM
+        // holds (each launch ends in its own serial tail of long trials), at
+        // ~(4 KiB + 8 B) per private page + ~2.5 KiB of per-trial state
+        size_t free_b = 0, total_b = 0;
+        const uint64_t per = (uint64_t)e->cfg.private_pages * (kPage + 8) + 2560;
+        uint64_t cap = 65536;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = (uint64_t)free_b / 2 / per;
+        e->cfg.max_trials_per_launch = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(cap, 65536), 1u << 21);
     }
     *out = e;
     return FI_OK;

@@ -243,7 +243,7 @@ class Engine:
     """Thin RAII wrapper of one fi_engine (one HIP device)."""
 
     def __init__(self, device: int = 0, private_pages: int = 16, hang_factor_x16: int = 32,
-                 max_trials_per_launch: int = 65536, snapshot_interval: int = 0, flags: int = 0,
+                 max_trials_per_launch: int = 0, snapshot_interval: int = 0, flags: int = 0,
                  epoch_iters: int = 0, lanes_per_wave: int = 0, resume_lanes: int = 0,
                  epochs: int = 0):
         self.L = lib()

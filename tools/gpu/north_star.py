@@ -17,18 +17,23 @@ REGS_PC = ((1 << 32) - 2) | (1 << 32)
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 SEED = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0x5EED0003
 CHECK = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000
+# trials per launch: the whole campaign in one launch by default (1M trials x
+# 16 private pages = 65 GiB of copy-on-write frames, well inside 288 GB of
+# HBM): one campaign tail instead of one per chunk
+PER_LAUNCH = int(sys.argv[4]) if len(sys.argv) > 4 else N
 name = "intmix"
 elf = open(os.path.join(ROOT, "workloads", f"{name}.elf"), "rb").read()
-e = Engine(max_trials_per_launch=100_000)
+e = Engine(max_trials_per_launch=PER_LAUNCH)
 e.load_elf(elf, [name])
 g = e.golden_run()
 e.set_campaign(SEED, REGS_PC, 1)
-e.run_trials(0, 100_000, want_outcomes=False)   # warm-up (load-time translation, buffers)
+e.run_trials(0, min(PER_LAUNCH, N), want_outcomes=False)   # warm-up (load-time translation, buffers)
 t0 = time.perf_counter()
 out, h = e.run_trials(0, N)
 wall = time.perf_counter() - t0
 cls = np.bincount(out["cls"], minlength=6).tolist()
-rec = {"workload": name, "trials": N, "seed": hex(SEED), "golden_ninst": int(g.ninst), "wall_s": round(wall, 3),
+rec = {"workload": name, "trials": N, "trials_per_launch": PER_LAUNCH, "seed": hex(SEED), "golden_ninst": int(g.ninst),
+       "wall_s": round(wall, 3),
        "trials_per_s": round(N / wall), "classes": cls, "device_insts": int(h["device_insts"]),
        "guest_insts_gem5_equiv": int(out["ninst"].astype(np.uint64).sum())}
 print(json.dumps(rec), flush=True)
