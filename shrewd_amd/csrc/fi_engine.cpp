@@ -1163,9 +1163,11 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
     if (e->cfg.flags & FI_CFG_NO_EPOCHS) {
         budgets = {0};
     } else {
-        const uint32_t b = e->cfg.epoch_iters ? e->cfg.epoch_iters : 4096;
+        const uint32_t b = e->cfg.epoch_iters ? e->cfg.epoch_iters : 1024;
         // default: one 64-lane epoch, then every survivor to completion on the
-        // solo kernel (profiles/r02c epoch_sweep: 2 epochs at 4096 beat 3 and 4)
+        // solo kernel (profiles/r02c epoch_sweep: 2 epochs beat 3 and 4; with
+        // first-access forwarding a 1024-iteration first epoch beats 4096:
+        // crc32 12.7M vs 9.8M, qsort +3 %, intmix even, profiles/r02l_ab.txt)
         const uint32_t n_ep = e->cfg.epochs ? std::max(2u, std::min(e->cfg.epochs, 14u)) : 2u;
         for (uint32_t i = 0; i + 1 < n_ep; i++) budgets.push_back(b << (2 * std::min(i, 2u)));
         budgets.push_back(0);
