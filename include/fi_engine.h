@@ -187,6 +187,16 @@ const char *fi_last_error(fi_engine *e);
  * (it shapes the initial stack exactly as in RiscvProcess64::argsInit). */
 fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *const *argv,
                       const char *const *envp);
+/* Start the campaign from a gem5 SE-mode checkpoint instead of process start
+ * (Process::unserialize src/sim/process.cc:427-441,
+ * m5.instantiate(ckpt_dir) src/python/m5/simulate.py:338): registers, pc,
+ * memory (page table + physical memory store), brk point and stack VMA come
+ * from cpt_dir/m5.cpt; the workload ELF gives the executable range for
+ * pre-decode and translation.  numInst counts from the restore point (gem5
+ * does not checkpoint statistics).  Supported: one CPU thread, no FP state,
+ * the stack as the only VMA, the default mmap end; anything else is
+ * FI_E_ARG with the reason in fi_last_error. */
+fi_status fi_load_checkpoint(fi_engine *e, const char *cpt_dir, const uint8_t *elf, size_t len);
 fi_status fi_golden_run(fi_engine *e, fi_golden_info *out);
 /* copies up to cap bytes of golden stdout; returns the full length in *len */
 fi_status fi_golden_stdout(fi_engine *e, uint8_t *buf, uint64_t cap, uint64_t *len);

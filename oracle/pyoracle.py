@@ -88,6 +88,9 @@ def lib():
         if not os.path.exists(LIB):
             build()
         L = C.CDLL(LIB)
+        L.or_create_checkpoint.restype = C.c_void_p
+        L.or_create_checkpoint.argtypes = [C.c_char_p, C.c_char_p, C.c_size_t]
+        L.or_write_checkpoint.argtypes = [C.c_void_p, C.c_uint64, C.c_char_p]
         L.or_create.restype = C.c_void_p
         L.or_create.argtypes = [C.c_char_p, C.c_size_t, C.c_char_p]
         L.or_destroy.argtypes = [C.c_void_p]
@@ -123,9 +126,14 @@ def lib():
 
 
 class Oracle:
-    def __init__(self, elf: bytes, argv0: str):
+    def __init__(self, elf: bytes, argv0: str, checkpoint: str | None = None):
+        """A campaign from process start (cmd = [argv0]) or, with checkpoint,
+        from a gem5 SE checkpoint directory."""
         self.L = lib()
-        self.h = self.L.or_create(elf, len(elf), argv0.encode())
+        if checkpoint is not None:
+            self.h = self.L.or_create_checkpoint(checkpoint.encode(), elf, len(elf))
+        else:
+            self.h = self.L.or_create(elf, len(elf), argv0.encode())
         err = self.L.or_error(self.h).decode()
         if err:
             raise RuntimeError(err)
@@ -138,6 +146,11 @@ class Oracle:
 
     def __del__(self):
         self.close()
+
+    def write_checkpoint(self, ninst: int, directory: str):
+        """The golden run's state at numInst == ninst as a gem5 SE checkpoint."""
+        if self.L.or_write_checkpoint(self.h, ninst, directory.encode()) != 0:
+            raise RuntimeError(self.L.or_error(self.h).decode())
 
     def set_protect_opclasses(self, mask: int):
         """SHREWD replication set: bit k = gem5 OpClass enum value k."""

@@ -13,7 +13,10 @@
 #include "../shrewd_amd/csrc/gem5_decode_table.h"
 #include "../shrewd_amd/csrc/gem5_opclass_table.h"
 
+#include <errno.h>
 #include <pthread.h>
+#include <sys/stat.h>
+#include <zlib.h>
 #include <stdbool.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -172,6 +175,8 @@ static void by_push(bytes_t *b, const uint8_t *p, u64 n) {
 struct or_campaign {
     pmap_t image;          /* initial process image pages (shared, read-only) */
     u64 entry, sp0, stack_min0;
+    u64 regs0[32], pc0;    /* initial architectural state (process start or a checkpoint) */
+    u64 text_lo, text_hi;  /* page-aligned executable range (PT_LOAD with PF_X) */
     u64 stack_vma_lo, stack_vma_hi;  /* the "stack" VMA created by argsInit */
     u64 brk0;
     u64 clk_period;        /* ticks per CPU cycle (1 ps ticks; 500 = 2 GHz) */
@@ -2254,6 +2259,11 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
         if (off <= phoff && off + filesz > phoff) phdr_vaddr = vaddr + (phoff - off);   /* :396-402 */
         if (flags & 2)
             for (u64 pg = paddr & PAGE_MASK; pg < paddr + memsz && nw < 4096; pg += PAGE) wpages[nw++] = pg;
+        if (flags & 1) {
+            u64 lo = paddr & PAGE_MASK, hi = (paddr + memsz + PAGE - 1) & PAGE_MASK;
+            if (!c->text_hi || lo < c->text_lo) c->text_lo = lo;
+            if (hi > c->text_hi) c->text_hi = hi;
+        }
     }
     /* RiscvProcess64 ctor: brk = roundUp(image.maxAddr(), 4096) (process.cc:76) */
     c->brk0 = (max_addr + PAGE - 1) & PAGE_MASK;
@@ -2308,6 +2318,9 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
     c->n_mem_pages = nw;
     c->mem_pages = (u64 *)malloc(sizeof(u64) * (nw ? nw : 1));
     memcpy(c->mem_pages, wpages, sizeof(u64) * nw);
+    memset(c->regs0, 0, sizeof c->regs0);
+    c->regs0[2] = c->sp0;   /* argsInit: every register 0 but sp, pc = e_entry */
+    c->pc0 = c->entry;
     return c;
 }
 
@@ -2324,8 +2337,9 @@ static void mach_init(mach_t *m, const or_campaign_t *c) {
     pm_init(&m->mem, 64);
     for (u64 i = 0; i < c->image.cap; i++)
         if (c->image.tab[i].vpn != UINT64_MAX) pm_insert(&m->mem, c->image.tab[i].vpn, c->image.tab[i].data, 0);
-    m->x[2] = c->sp0;
-    m->pc = c->entry;
+    memcpy(m->x, c->regs0, sizeof m->x);
+    m->x[0] = 0;
+    m->pc = c->pc0;
     m->stack_min = c->stack_min0;
     m->watch = -1;
     m->resv = m->lock = OR_NONE;
@@ -2565,4 +2579,225 @@ int or_probe(u32 inst, u64 pc, const u64 regs[32], or_probe_t *o) {
     o->op = (u32)d.op;
     pm_free(&m.mem);
     return 0;
+}
+
+/* ------------------------------------------------------------ checkpoints */
+/* gem5 SE checkpoints (test infrastructure).  The writer produces what
+ * gem5's serialization writes for this machine (m5.cpt INI sections and a
+ * gzip-compressed physical memory store; formats cited in
+ * shrewd_amd/csrc/fi_checkpoint.cpp): thread context [system.cpu.xc.0]
+ * (serialize(tc), cpu/thread_context.cc:194-218; 33 integer registers,
+ * int.hh:62-80), process [system.cpu.workload] (MemState::serialize,
+ * sim/mem_state.hh:189-210), its page table (page_table.cc:186-201) and
+ * [system.physmem] (physical.cc:340-405), frames assigned in vpn order.  The
+ * reader is the oracle's own restatement of the restore
+ * (Process::unserialize, sim/process.cc:427-441). */
+static void cpt_bytes(FILE *f, const char *name, const uint8_t *b, int n) {
+    fprintf(f, "%s=", name);
+    for (int i = 0; i < n; i++) fprintf(f, i ? " %u" : "%u", b[i]);
+    fprintf(f, "\n");
+}
+
+int or_write_checkpoint(or_campaign_t *c, uint64_t ninst, const char *dir) {
+    if (!c->have_golden || ninst >= c->golden.ninst) {
+        snprintf(c->err, sizeof c->err, "or_write_checkpoint: need a golden run longer than %llu",
+                 (unsigned long long)ninst);
+        return -1;
+    }
+    mach_t m; mach_init(&m, c);
+    while (!m.done && m.num_inst < ninst) tick(&m, UINT64_MAX);
+    if (m.done || m.stay_at_pc || m.fetch_offset) { mach_free(&m); snprintf(c->err, sizeof c->err, "not at a boundary"); return -1; }
+    if (mkdir(dir, 0755) && errno != EEXIST) { mach_free(&m); snprintf(c->err, sizeof c->err, "mkdir %s", dir); return -1; }
+    char path[4096];
+    /* pages in vpn order -> frames 0, 1, ... */
+    u64 n = 0;
+    for (u64 i = 0; i < m.mem.cap; i++) if (m.mem.tab[i].vpn != UINT64_MAX) n++;
+    u64 *vpns = (u64 *)malloc(sizeof(u64) * (n ? n : 1));
+    uint8_t **data = (uint8_t **)malloc(sizeof(uint8_t *) * (n ? n : 1));
+    u64 k = 0;
+    for (u64 i = 0; i < m.mem.cap; i++) if (m.mem.tab[i].vpn != UINT64_MAX) { vpns[k] = m.mem.tab[i].vpn; k++; }
+    for (u64 i = 1; i < n; i++)
+        for (u64 j = i; j > 0 && vpns[j - 1] > vpns[j]; j--) { u64 t = vpns[j]; vpns[j] = vpns[j - 1]; vpns[j - 1] = t; }
+    for (u64 i = 0; i < n; i++) data[i] = pm_find(&m.mem, vpns[i])->data;
+    snprintf(path, sizeof path, "%s/system.physmem.store0.pmem", dir);
+    gzFile gz = gzopen(path, "wb");
+    for (u64 i = 0; gz && i < n; i++) gzwrite(gz, data[i], (unsigned)PAGE);
+    if (gz) gzclose(gz);
+    snprintf(path, sizeof path, "%s/m5.cpt", dir);
+    FILE *f = fopen(path, "w");
+    if (!gz || !f) { free(vpns); free(data); mach_free(&m); if (f) fclose(f); snprintf(c->err, sizeof c->err, "write %s", dir); return -1; }
+    fprintf(f, "## checkpoint generated by oracle/rv64se.c:or_write_checkpoint at numInst %llu\n\n",
+            (unsigned long long)ninst);
+    fprintf(f, "[Globals]\ncurTick=%llu\n\n", (unsigned long long)(m.num_cycles * c->clk_period));
+    fprintf(f, "[system.cpu.xc.0]\n_status=1\n");
+    uint8_t ib[33 * 8], fb[32 * 8];
+    memset(ib, 0, sizeof ib);
+    for (int r = 1; r < 32; r++) for (int b = 0; b < 8; b++) ib[r * 8 + b] = (uint8_t)(m.x[r] >> (8 * b));
+    for (int r = 0; r < 32; r++) for (int b = 0; b < 8; b++) fb[r * 8 + b] = (uint8_t)(m.f[r] >> (8 * b));
+    cpt_bytes(f, "regs.integer", ib, 33 * 8);
+    cpt_bytes(f, "regs.floating_point", fb, 32 * 8);
+    fprintf(f, "_pc=%llu\n_upc=0\n_npc=%llu\n_nupc=1\n_rvType=1\n_compressed=false\n\n", (unsigned long long)m.pc,
+            (unsigned long long)(m.pc + 4));
+    fprintf(f, "[system.cpu.workload]\nbrkPoint=%llu\nstackBase=%llu\nstackSize=%llu\nmaxStackSize=%llu\n"
+               "stackMin=%llu\nnextThreadStackBase=%llu\nmmapEnd=%llu\n\n",
+            (unsigned long long)m.brk, (unsigned long long)STACK_BASE, (unsigned long long)(STACK_BASE - m.stack_min),
+            (unsigned long long)MAX_STACK, (unsigned long long)m.stack_min,
+            (unsigned long long)(STACK_BASE - MAX_STACK), (unsigned long long)m.mmap_end);
+    fprintf(f, "[system.cpu.workload.vmalist]\nsize=%d\n\n", m.nvma);
+    for (int i = 0; i < m.nvma; i++)
+        fprintf(f, "[system.cpu.workload.vmalist.Vma%d]\nname=%s\naddrRangeStart=%llu\naddrRangeEnd=%llu\n\n", i,
+                (m.vma[i].lo == c->stack_vma_lo && m.vma[i].hi == c->stack_vma_hi) ? "stack" : "anon",
+                (unsigned long long)m.vma[i].lo, (unsigned long long)m.vma[i].hi);
+    fprintf(f, "[system.cpu.workload.ptable]\nsize=%llu\n\n", (unsigned long long)n);
+    for (u64 i = 0; i < n; i++)
+        fprintf(f, "[system.cpu.workload.ptable.Entry%llu]\nvaddr=%llu\npaddr=%llu\nflags=0\n\n", (unsigned long long)i,
+                (unsigned long long)(vpns[i] << 12), (unsigned long long)(i << 12));
+    fprintf(f, "[system.physmem]\nlal_addr=\nlal_cid=\nnbr_of_stores=1\n\n");
+    fprintf(f, "[system.physmem.store0]\nstore_id=0\nfilename=system.physmem.store0.pmem\nrange_size=%llu\n",
+            (unsigned long long)(n << 12));
+    fclose(f);
+    free(vpns); free(data);
+    mach_free(&m);
+    return 0;
+}
+
+/* m5.cpt reader: section/key lookup by a linear scan of the file's lines */
+typedef struct { char **lines; int n; } cpt_t;
+static int cpt_load(cpt_t *t, const char *path) {
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    t->lines = NULL; t->n = 0;
+    char *line = NULL; size_t cap = 0; ssize_t len;
+    int capn = 0;
+    while ((len = getline(&line, &cap, f)) >= 0) {
+        while (len > 0 && (line[len - 1] == '\n' || line[len - 1] == '\r')) line[--len] = 0;
+        if (t->n == capn) { capn = capn ? 2 * capn : 1024; t->lines = (char **)realloc(t->lines, sizeof(char *) * capn); }
+        t->lines[t->n++] = strdup(line);
+    }
+    free(line);
+    fclose(f);
+    return 0;
+}
+static void cpt_free(cpt_t *t) { for (int i = 0; i < t->n; i++) free(t->lines[i]); free(t->lines); }
+/* value of key in section sec (NULL if absent) */
+static const char *cpt_get(const cpt_t *t, const char *sec, const char *key) {
+    int in = 0;
+    size_t kl = strlen(key);
+    for (int i = 0; i < t->n; i++) {
+        const char *l = t->lines[i];
+        if (l[0] == '[') { in = strlen(l) == strlen(sec) + 2 && !strncmp(l + 1, sec, strlen(sec)); continue; }
+        if (in && !strncmp(l, key, kl) && l[kl] == '=') return l + kl + 1;
+    }
+    return NULL;
+}
+/* the first section holding key (copied into out) */
+static int cpt_find(const cpt_t *t, const char *key, char *out, size_t cap) {
+    const char *sec = NULL;
+    size_t kl = strlen(key);
+    for (int i = 0; i < t->n; i++) {
+        const char *l = t->lines[i];
+        if (l[0] == '[') { sec = l; continue; }
+        if (sec && !strncmp(l, key, kl) && l[kl] == '=') {
+            size_t n = strlen(sec) - 2;
+            if (n >= cap) return -1;
+            memcpy(out, sec + 1, n); out[n] = 0;
+            return 0;
+        }
+    }
+    return -1;
+}
+static u64 cpt_u64(const cpt_t *t, const char *sec, const char *key, int *ok) {
+    const char *v = cpt_get(t, sec, key);
+    if (!v) { *ok = 0; return 0; }
+    return strtoull(v, NULL, 0);
+}
+
+or_campaign_t *or_create_checkpoint(const char *dir, const uint8_t *elf, size_t len) {
+    or_campaign_t *c = or_create(elf, len, "checkpoint");
+    if (c->err[0]) return c;
+    char path[4096], xc[512], ps[512], pm[512], sec[1024];
+    snprintf(path, sizeof path, "%s/m5.cpt", dir);
+    cpt_t t;
+    if (cpt_load(&t, path)) { snprintf(c->err, sizeof c->err, "cannot read %.200s", path); return c; }
+    int ok = 1;
+    if (cpt_find(&t, "regs.integer", xc, sizeof xc) || cpt_find(&t, "brkPoint", ps, sizeof ps) ||
+        cpt_find(&t, "nbr_of_stores", pm, sizeof pm)) {
+        snprintf(c->err, sizeof c->err, "m5.cpt lacks a thread context, process or memory"); cpt_free(&t); return c;
+    }
+    /* registers: 8 bytes each, little-endian, x0 first */
+    const char *v = cpt_get(&t, xc, "regs.integer");
+    memset(c->regs0, 0, sizeof c->regs0);
+    for (int i = 0; i < 32 * 8 && v && *v; i++) {
+        char *e;
+        unsigned long b = strtoul(v, &e, 10);
+        if (e == v) break;
+        if (i >= 8) c->regs0[i / 8] |= (u64)(b & 0xFF) << (8 * (i % 8));
+        v = e;
+    }
+    const char *fv = cpt_get(&t, xc, "regs.floating_point");
+    while (fv && *fv) {
+        char *e;
+        unsigned long b = strtoul(fv, &e, 10);
+        if (e == fv) break;
+        if (b) { snprintf(c->err, sizeof c->err, "FP registers hold state (not supported)"); cpt_free(&t); return c; }
+        fv = e;
+    }
+    c->pc0 = cpt_u64(&t, xc, "_pc", &ok);
+    c->brk0 = cpt_u64(&t, ps, "brkPoint", &ok);
+    u64 sbase = cpt_u64(&t, ps, "stackBase", &ok), smax = cpt_u64(&t, ps, "maxStackSize", &ok);
+    u64 smin = cpt_u64(&t, ps, "stackMin", &ok), mend = cpt_u64(&t, ps, "mmapEnd", &ok);
+    snprintf(sec, sizeof sec, "%s.vmalist", ps);
+    u64 nv = cpt_u64(&t, sec, "size", &ok);
+    snprintf(sec, sizeof sec, "%s.vmalist.Vma0", ps);
+    const char *vn = cpt_get(&t, sec, "name");
+    if (!ok || sbase != STACK_BASE || smax != MAX_STACK || mend != 0x4000000000000000ULL || nv != 1 || !vn ||
+        strcmp(vn, "stack")) {
+        snprintf(c->err, sizeof c->err, "unsupported checkpoint (process state beyond RiscvProcess64's stack VMA)");
+        cpt_free(&t); return c;
+    }
+    c->stack_vma_lo = cpt_u64(&t, sec, "addrRangeStart", &ok);
+    c->stack_vma_hi = cpt_u64(&t, sec, "addrRangeEnd", &ok);
+    c->stack_min0 = smin & PAGE_MASK;
+    c->sp0 = c->regs0[2];
+    /* page table + memory store (frames read in paddr order) */
+    snprintf(sec, sizeof sec, "%s.ptable", ps);
+    u64 np = cpt_u64(&t, sec, "size", &ok);
+    u64 *va = (u64 *)malloc(sizeof(u64) * (np ? np : 1)), *pa = (u64 *)malloc(sizeof(u64) * (np ? np : 1));
+    for (u64 i = 0; i < np; i++) {
+        snprintf(sec, sizeof sec, "%s.ptable.Entry%llu", ps, (unsigned long long)i);
+        va[i] = cpt_u64(&t, sec, "vaddr", &ok);
+        pa[i] = cpt_u64(&t, sec, "paddr", &ok);
+    }
+    for (u64 i = 1; i < np; i++)
+        for (u64 j = i; j > 0 && pa[j - 1] > pa[j]; j--) {
+            u64 x = pa[j]; pa[j] = pa[j - 1]; pa[j - 1] = x;
+            x = va[j]; va[j] = va[j - 1]; va[j - 1] = x;
+        }
+    snprintf(sec, sizeof sec, "%s.store0", pm);
+    const char *fn = cpt_get(&t, sec, "filename");
+    snprintf(path, sizeof path, "%s/%s", dir, fn ? fn : "");
+    gzFile gz = fn ? gzopen(path, "rb") : NULL;
+    if (!ok || !gz) { snprintf(c->err, sizeof c->err, "bad page table or memory store"); free(va); free(pa); cpt_free(&t); return c; }
+    pm_free(&c->image);
+    pm_init(&c->image, 64);
+    u64 at = 0;
+    uint8_t skip[4096];
+    u64 nmem = 0;
+    u64 *mp = (u64 *)malloc(sizeof(u64) * (np ? np : 1));
+    for (u64 i = 0; i < np && ok; i++) {
+        while (at < pa[i]) { if (gzread(gz, skip, (unsigned)PAGE) != (int)PAGE) { ok = 0; break; } at += PAGE; }
+        uint8_t *pg = (uint8_t *)malloc(PAGE);
+        if (!ok || at != pa[i] || gzread(gz, pg, (unsigned)PAGE) != (int)PAGE) { free(pg); ok = 0; break; }
+        at += PAGE;
+        pm_insert(&c->image, va[i] >> 12, pg, 1);
+        if (va[i] >= c->text_hi || va[i] + PAGE <= c->text_lo) mp[nmem++] = va[i];
+    }
+    gzclose(gz);
+    for (u64 i = 1; i < nmem; i++)
+        for (u64 j = i; j > 0 && mp[j - 1] > mp[j]; j--) { u64 x = mp[j]; mp[j] = mp[j - 1]; mp[j - 1] = x; }
+    free(c->mem_pages);
+    c->mem_pages = mp; c->n_mem_pages = nmem;
+    if (!ok) snprintf(c->err, sizeof c->err, "memory store truncated");
+    free(va); free(pa); cpt_free(&t);
+    return c;
 }

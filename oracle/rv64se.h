@@ -82,6 +82,13 @@ or_campaign_t *or_create(const uint8_t *elf, size_t elf_len, const char *argv0);
 void or_destroy(or_campaign_t *c);
 const char *or_error(or_campaign_t *c);
 
+/* Campaign from a gem5 SE checkpoint directory (m5.cpt + memory store); the
+ * ELF gives the executable range.  or_error() is non-empty on failure. */
+or_campaign_t *or_create_checkpoint(const char *dir, const uint8_t *elf, size_t elf_len);
+/* Write the golden run's state at the top of the first tick with numInst ==
+ * ninst as a gem5 SE checkpoint into dir (test fixtures).  Returns 0 / -1. */
+int or_write_checkpoint(or_campaign_t *c, uint64_t ninst, const char *dir);
+
 /* Fault-free run; records golden stdout/stderr/exit code/instruction count. */
 int or_golden(or_campaign_t *c, uint64_t max_inst, or_golden_t *out);
 /* copies golden stdout into buf (up to cap bytes); returns length */

@@ -20,6 +20,7 @@
 #include <string>
 #include <vector>
 
+#include "fi_checkpoint.h"
 #include "fi_types.h"
 
 constexpr uint64_t kRndLen = 1ULL << 20;   // getrandom bytes precomputed per engine
@@ -405,6 +406,8 @@ static fi_status upload_snaps(fi_engine *e) {
     return FI_OK;
 }
 
+static fi_status finish_load(fi_engine *e, const uint64_t regs[32], uint64_t pc);
+
 fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *const *argv, const char *const *envp) {
     if (!e || !elf || !argv || !argv[0]) return fail(e, FI_E_ARG, "fi_load_elf: elf and argv[0] required");
     HIPCHK(hipSetDevice(e->dev));
@@ -495,10 +498,17 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
     wpages.erase(std::unique(wpages.begin(), wpages.end()), wpages.end());
     e->mem_pages = wpages;
     e->brk0 = (max_addr + kPage - 1) & ~(kPage - 1);   // Process brk point (process.cc: roundUp(maxAddr))
+    // RiscvProcess::argsInit leaves every register 0 but sp; pc = e_entry
+    uint64_t regs[32] = {};
+    regs[2] = e->sp0;
+    return finish_load(e, regs, e->entry);
+}
 
-    // ---- snapshot 0: the process-start image (frames sorted by vpn) and the
-    // initial architectural state (RiscvProcess::argsInit leaves every
-    // register 0 but sp; pc = e_entry)
+// ---- snapshot 0: the start image in e->pages (frames sorted by vpn) and the
+// initial architectural state; the text pre-decoded on the device.  The
+// common tail of fi_load_elf and fi_load_checkpoint.
+static fi_status finish_load(fi_engine *e, const uint64_t regs[32], uint64_t pc) {
+    const std::vector<uint64_t> &wpages = e->mem_pages;
     e->pool.clear();
     e->tab.clear();
     e->snaps.clear();
@@ -511,8 +521,8 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
     }
     e->n_start_frames = (uint32_t)e->tab.size();
     SnapState s0{};
-    s0.regs[2] = e->sp0;
-    s0.pc = e->entry;
+    for (int r = 1; r < 32; r++) s0.regs[r] = regs[r];
+    s0.pc = pc;
     s0.stack_min = e->stack_min0;
     s0.tab_off = 0;
     s0.tab_n = (uint32_t)e->tab.size();
@@ -545,6 +555,37 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
 }
 
 // ------------------------------------------------------------------ work buffers
+fi_status fi_load_checkpoint(fi_engine *e, const char *cpt_dir, const uint8_t *elf, size_t len) {
+    if (!e || !cpt_dir || !elf) return fail(e, FI_E_ARG, "fi_load_checkpoint: checkpoint directory and ELF required");
+    const char *argv[] = {"checkpoint", nullptr};
+    fi_status st = fi_load_elf(e, elf, len, argv, nullptr);   // executable range, entry checks
+    if (st) return st;
+    CptImage img;
+    const std::string err = read_gem5_checkpoint(cpt_dir, img);
+    if (!err.empty()) return fail(e, FI_E_ARG, "fi_load_checkpoint: %s", err.c_str());
+    // what the engine's SE model starts from (RiscvProcess64, process.cc:71-82)
+    if (img.fp_state) return fail(e, FI_E_ARG, "fi_load_checkpoint: FP registers hold state (not supported)");
+    if (img.stack_base != kStackBase || img.max_stack != kMaxStack || img.mmap_end != 0x4000000000000000ULL)
+        return fail(e, FI_E_ARG, "fi_load_checkpoint: stack base / max stack / mmap end differ from RiscvProcess64's");
+    if (img.vmas.size() != 1 || img.vma_names[0] != "stack")
+        return fail(e, FI_E_ARG, "fi_load_checkpoint: %zu VMAs (only the stack VMA is supported)", img.vmas.size());
+    free_image(e);
+    e->pages.clear();
+    for (auto &kv : img.pages) e->pages[kv.first] = kv.second;
+    // memory-fault candidates: every mapped page outside the executable range
+    e->mem_pages.clear();
+    for (auto &kv : img.pages) {
+        const uint64_t a = kv.first << 12;
+        if (a >= e->text_hi || a + kPage <= e->text_lo) e->mem_pages.push_back(a);
+    }
+    e->brk0 = img.brk;
+    e->svma_lo = img.vmas[0].first;
+    e->svma_hi = img.vmas[0].second;
+    e->sp0 = img.regs[2];
+    e->stack_min0 = img.stack_min & ~(kPage - 1);
+    return finish_load(e, img.regs, img.pc);
+}
+
 static fi_status ensure_work(fi_engine *e, uint64_t n) {
     if (n <= e->cap) return FI_OK;
     free_work(e);

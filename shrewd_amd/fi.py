@@ -192,6 +192,7 @@ def lib():
         L.fi_last_error.argtypes = [vp]
         L.fi_load_elf.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]
         L.fi_golden_run.argtypes = [vp, C.POINTER(GoldenInfo)]
+        L.fi_load_checkpoint.argtypes = [vp, C.c_char_p, C.c_char_p, C.c_size_t]
         L.fi_golden_stdout.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.fi_golden_stderr.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.fi_set_campaign.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32]
@@ -272,6 +273,10 @@ class Engine:
 
     def load_elf(self, elf: bytes, argv: Sequence[str], envp: Sequence[str] | None = None):
         self._chk(self.L.fi_load_elf(self.h, elf, len(elf), _cstrs(argv), _cstrs(envp)), "fi_load_elf")
+
+    def load_checkpoint(self, directory: str, elf: bytes):
+        """Start from a gem5 SE checkpoint (fi_load_checkpoint); elf = the workload."""
+        self._chk(self.L.fi_load_checkpoint(self.h, directory.encode(), elf, len(elf)), "fi_load_checkpoint")
 
     def golden_run(self) -> GoldenInfo:
         g = GoldenInfo()
@@ -470,6 +475,7 @@ class FaultCampaign:
     Params (same names/meaning as the SimObject): workload (binary path), cmd
     (argv, cmd[0] defaults to workload), env, trials, seed, structures, bits,
     burst, protect_mask, protect_opclasses, num_gpus, max_insts_factor, output;
+    checkpoint (a gem5 SE checkpoint directory to start from),
     shadow_fu_model (SHREWD FU contention for result faults, off by default),
     priority_to_shadow and issue_params (the O3 issue model's parameters).
     """
@@ -478,15 +484,20 @@ class FaultCampaign:
                  trials: int = 1000, seed: int = 0x5EED0001, structures=("int_reg",), burst: int = 1,
                  protect_mask: int = 0, num_gpus: int = 1, max_insts_factor: float = 2.0, output: str = "",
                  device: int = 0, private_pages: int = 16, protect_opclasses=(), bits=None,
-                 shadow_fu_model: bool = False, priority_to_shadow: bool = False, issue_params: dict | None = None):
+                 shadow_fu_model: bool = False, priority_to_shadow: bool = False, issue_params: dict | None = None,
+                 checkpoint: str = ""):
         self.workload, self.cmd, self.env = workload, list(cmd or [workload]), list(env or [])
         self.trials, self.seed, self.structures, self.burst = trials, seed, structures, burst
         self.protect_mask, self.num_gpus, self.output = protect_mask, num_gpus, output
         self.max_insts_factor = max_insts_factor
         self.engine = Engine(device=device, private_pages=private_pages,
                              hang_factor_x16=max(1, int(round(max_insts_factor * 16))))
+        self.checkpoint = checkpoint
         with open(workload, "rb") as f:
-            self.engine.load_elf(f.read(), self.cmd, self.env)
+            if checkpoint:
+                self.engine.load_checkpoint(checkpoint, f.read())
+            else:
+                self.engine.load_elf(f.read(), self.cmd, self.env)
         self.golden = self.engine.golden_run()
         self.engine.set_campaign(seed, structures, burst)
         self.bits = bits_mask(bits)

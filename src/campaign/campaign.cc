@@ -132,7 +132,10 @@ Campaign::Campaign(const CampaignParams &p) : p_(p) {
             throw std::runtime_error("fi_create(device " + std::to_string(cfg.device) + "): " + msg);
         }
         engines_.push_back(e);
-        check(e, fi_load_elf(e, elf.data(), elf.size(), argv.data(), envp.data()), "fi_load_elf");
+        if (p_.checkpoint.empty())
+            check(e, fi_load_elf(e, elf.data(), elf.size(), argv.data(), envp.data()), "fi_load_elf");
+        else
+            check(e, fi_load_checkpoint(e, p_.checkpoint.c_str(), elf.data(), elf.size()), "fi_load_checkpoint");
         fi_golden_info gi{};
         check(e, fi_golden_run(e, &gi), "fi_golden_run");
         check(e, fi_set_campaign(e, p_.seed, smask, p_.burst), "fi_set_campaign");

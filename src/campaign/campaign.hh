@@ -23,6 +23,7 @@ namespace shrewd {
 
 struct CampaignParams {
     std::string workload;                 // RV64 static ELF path
+    std::string checkpoint;               // gem5 SE checkpoint directory to start from ("" = process start)
     std::vector<std::string> cmd;         // argv; empty -> {workload}
     std::vector<std::string> env;
     uint64_t trials = 1000;

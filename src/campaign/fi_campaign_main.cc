@@ -37,6 +37,7 @@ int main(int argc, char **argv) {
         std::string v = argv[++i];
         if (k == "--workload") p.workload = v;
         else if (k == "--cmd") p.cmd = split(v);
+        else if (k == "--checkpoint") p.checkpoint = v;
         else if (k == "--env") p.env = split(v);
         else if (k == "--trials") p.trials = strtoull(v.c_str(), nullptr, 0);
         else if (k == "--first-trial") p.first_trial = strtoull(v.c_str(), nullptr, 0);

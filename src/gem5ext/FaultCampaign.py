@@ -26,6 +26,9 @@ class FaultCampaign(SimObject):
 
     workload = Param.String("RV64 static ELF run in SE mode")
     cmd = VectorParam.String([], "argv of the workload (cmd[0] defaults to workload)")
+    checkpoint = Param.String(
+        "", "gem5 SE checkpoint directory the trials start from (m5.cpt + memory store); "
+        "empty: process start")
     env = VectorParam.String([], "environment of the workload")
     trials = Param.UInt64(1000, "number of fault-injection trials")
     first_trial = Param.UInt64(0, "first trial id (sites are keyed by (seed, trial id))")

@@ -17,6 +17,7 @@ FaultCampaign::init()
     SimObject::init();
     shrewd::CampaignParams cp;
     cp.workload = params().workload;
+    cp.checkpoint = params().checkpoint;
     cp.cmd = params().cmd;
     cp.env = params().env;
     cp.trials = params().trials;

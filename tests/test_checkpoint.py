@@ -1,0 +1,107 @@
+"""gem5 SE checkpoint ingestion: campaigns that start from a
+checkpoint instead of process start.
+
+The checkpoints are written by the oracle in gem5's serialization format
+(oracle/rv64se.c:or_write_checkpoint: m5.cpt INI sections + gzip memory
+store).  A real gem5 checkpoint cannot be produced here (no gem5 build), so
+the format is "parity unpinned" against gem5 itself; what is pinned is the
+round trip: a campaign restored at numInst K behaves exactly like the
+process-start campaign from K on.
+"""
+import numpy as np
+import pytest
+
+from conftest import workload_elf
+
+REGS_PC = ((1 << 32) - 2) | (1 << 32)
+MEM = 1 << 33
+
+
+@pytest.fixture(scope="module")
+def crc32_cpt(tmp_path_factory, oracle_mod):
+    elf = workload_elf("crc32")
+    o = oracle_mod.Oracle(elf, "crc32")
+    g = o.run_golden()
+    k = 20_000
+    d = str(tmp_path_factory.mktemp("cpt") / "crc32_20000")
+    o.write_checkpoint(k, d)
+    return elf, d, k, o, g
+
+
+def test_checkpoint_files(crc32_cpt):
+    import gzip
+    import os
+    _, d, k, _, _ = crc32_cpt
+    txt = open(os.path.join(d, "m5.cpt")).read()
+    for sec in ("[system.cpu.xc.0]", "[system.cpu.workload]", "[system.cpu.workload.ptable]",
+                "[system.cpu.workload.vmalist.Vma0]", "[system.physmem.store0]"):
+        assert sec in txt
+    regs = [l for l in txt.splitlines() if l.startswith("regs.integer=")][0]
+    assert len(regs.split("=")[1].split()) == 33 * 8
+    mem = gzip.open(os.path.join(d, "system.physmem.store0.pmem")).read()
+    assert len(mem) % 4096 == 0 and len(mem) > 0
+
+
+def test_restored_golden_is_the_suffix(crc32_cpt, oracle_mod):
+    elf, d, k, o, g = crc32_cpt
+    r = oracle_mod.Oracle(elf, "crc32", checkpoint=d)
+    rg = r.run_golden()
+    assert rg.ninst == g.ninst - k
+    assert rg.exit_code == g.exit_code
+    full = o.golden_stdout()
+    assert full.endswith(r.golden_stdout())
+
+
+def test_restored_trials_equal_shifted_process_start_trials(crc32_cpt, oracle_mod):
+    """A trial restored at K and injected at t is the process-start trial
+    injected at K + t: same class, sub-code, exit code, detail and flags;
+    numInst shifted by K.  (Hangs only agree in class: the cap, 2 x golden
+    numInst + 1000, follows each campaign's own golden run.)"""
+    elf, d, k, o, g = crc32_cpt
+    r = oracle_mod.Oracle(elf, "crc32", checkpoint=d)
+    r.run_golden()
+    sites = r.sample(0x5EED0C97, 0, 3000, REGS_PC)
+    got = r.run_trials(sites, threads=8)
+    shifted = sites.copy()
+    shifted["inst"] += k
+    ref = o.run_trials(shifted, threads=8)
+    assert np.array_equal(got["cls"], ref["cls"])
+    fin = got["cls"] != 3
+    assert fin.sum() > 2500
+    for f in ("sub", "exit_code", "flags", "detail"):
+        assert np.array_equal(got[f][fin], ref[f][fin]), f
+    assert np.array_equal(got["ninst"][fin] + k, ref["ninst"][fin])
+
+
+def test_unsupported_checkpoint_is_refused(tmp_path, oracle_mod):
+    elf = workload_elf("crc32")
+    r = oracle_mod.Oracle.__new__(oracle_mod.Oracle)
+    r.L = oracle_mod.lib()
+    r.h = r.L.or_create_checkpoint(str(tmp_path).encode(), elf, len(elf))
+    assert r.L.or_error(r.h).decode().startswith("cannot read")
+    r.close()
+
+
+@pytest.mark.gpu
+def test_engine_from_checkpoint_matches_oracle(crc32_cpt, oracle_mod):
+    """The engine restored from the same checkpoint: golden run and trials
+    (register, pc and memory sites) bit-exact against the restored oracle."""
+    from shrewd_amd import Engine
+    elf, d, k, o, g = crc32_cpt
+    r = oracle_mod.Oracle(elf, "crc32", checkpoint=d)
+    rg = r.run_golden()
+    e = Engine()
+    e.load_checkpoint(d, elf)
+    eg = e.golden_run()
+    assert (eg.ninst, eg.ncycles, eg.exit_code) == (rg.ninst, rg.ncycles, rg.exit_code)
+    assert e.golden_stdout() == r.golden_stdout()
+    assert e.translate_status() == ""
+    for structs, n in ((REGS_PC, 4000), (MEM, 2000)):
+        e.set_campaign(0x5EEDC0DE, structs, 1)
+        sites = e.sample(0, n)
+        assert np.array_equal(sites, r.sample(0x5EEDC0DE, 0, n, structs))
+        dev, _ = e.run_sites(sites)
+        ref = r.run_trials(sites)
+        bad = np.flatnonzero(dev != ref)
+        assert not len(bad), f"{len(bad)} differ, first {sites[bad[0]]} {dev[bad[0]]} {ref[bad[0]]}"
+    e.close()
