@@ -1337,7 +1337,16 @@ __device__ __forceinline__ void trial_body() {
     L.watch = -1; L.out_bad = false; L.fp = false; L.done = !live; L.injected = (CX->record || !live) ? 1 : 0;
     L.fflags = L.frm = 0;
     L.res.cls = 0; L.res.sub = 0; L.res.exit_code = 0; L.res.flags = 0; L.res.detail = 0; L.res.ninst = 0;
-    LaneMem m;
+    // the solo kernel's LaneMem lives in LDS: the out-of-line helpers take it
+    // by reference, which would otherwise pin it in scratch, and every TLB
+    // probe and dirty-range check of the hot loops would be a scratch load
+    // (FI_SOLO_M_LDS=0: the private copy, A/B)
+#ifndef FI_SOLO_M_LDS
+#define FI_SOLO_M_LDS 1
+#endif
+    __shared__ LaneMem m_lds[1];
+    LaneMem m_priv;
+    LaneMem &m = (kNL == 1 && FI_SOLO_M_LDS) ? m_lds[0] : m_priv;
     m.stack_min = S0->stack_min;
     tlb_flush(m);
     m.tp0 = m.tp1 = m.tp2 = m.tp3 = 0;
@@ -1988,7 +1997,9 @@ __device__ __forceinline__ void trial_body() {
                 const uint32_t aux = q3 >> 16, kind = aux & 63;
                 if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
 #ifdef FI_TX
-                if (steps && ((q3 >> 8) & kPreLeader) &&   // translated blocks take over here
+                // translated blocks take over here (not at odd pcs: their entries are
+                // their word's pc | 2 entries, and the translated path refuses them)
+                if (steps && ((q3 >> 8) & kPreLeader) && !((uint32_t)spc & 1) &&
                     !(any_dirty && wballot<kNL>(mine && dirty_near(m, spc)) != 0) && n_iter + steps >= tx_skip_until)
                     break;
 #endif
