@@ -105,3 +105,29 @@ def test_engine_from_checkpoint_matches_oracle(crc32_cpt, oracle_mod):
         bad = np.flatnonzero(dev != ref)
         assert not len(bad), f"{len(bad)} differ, first {sites[bad[0]]} {dev[bad[0]]} {ref[bad[0]]}"
     e.close()
+
+
+@pytest.mark.gpu
+def test_native_driver_from_checkpoint_matches_oracle(crc32_cpt, oracle_mod, tmp_path):
+    """The native driver (the FaultCampaign SimObject's core) with --checkpoint:
+    per-trial outcomes bit-exact against the oracle restored from the same
+    directory."""
+    import os
+    import subprocess
+    from conftest import ROOT
+    from shrewd_amd import OUTCOME_DT
+    from shrewd_amd import build as b
+    elf, d, k, o, g = crc32_cpt
+    exe = b.build_cli()
+    n, seed = 2000, 0x5EEDC0DF
+    prefix = str(tmp_path / "cpt_camp")
+    r = subprocess.run([exe, "--workload", os.path.join(ROOT, "workloads", "crc32.elf"), "--cmd", "crc32",
+                        "--trials", str(n), "--seed", hex(seed), "--structures", "int_reg,pc",
+                        "--checkpoint", d, "--output", prefix], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    out = np.fromfile(prefix + ".outcomes.bin", OUTCOME_DT)
+    ro = oracle_mod.Oracle(elf, "crc32", checkpoint=d)
+    ro.run_golden()
+    ref = ro.run_trials(ro.sample(seed, 0, n, REGS_PC))
+    bad = np.flatnonzero(out != ref)
+    assert not len(bad), f"{len(bad)} differ, first {bad[0]}: {out[bad[0]]} {ref[bad[0]]}"
