@@ -844,7 +844,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         pre.resize((e->text_hi - e->text_lo) / 2);
         hipError_t err = hipMemcpy(trace.data(), d_trace, n_events * 4, hipMemcpyDeviceToHost);
         if (err == hipSuccess) err = hipMemcpy(pre.data(), e->d_pre, pre.size() * sizeof(PreInst), hipMemcpyDeviceToHost);
-        for (auto &p : pre) p.flags &= (uint8_t)~kPreLeader;
+        for (auto &p : pre) p.flags &= (uint8_t)~(kPreLeader | kPreOddLeader);
         if (err != hipSuccess) st = fail(e, FI_E_HIP, "trace download: %s", hipGetErrorString(err));
     }
     (void)hipFree(d_trace);
@@ -1014,7 +1014,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         } else {
             JTRACE("loaded\n");
 #undef JTRACE
-            for (uint32_t h : leaders) pre[h].flags |= kPreLeader;
+            for (uint32_t h : leaders) pre[h & 0x7FFFFFFFu].flags |= (h >> 31) ? kPreOddLeader : kPreLeader;
             HIPCHK(hipMemcpy(e->d_pre, pre.data(), pre.size() * sizeof(PreInst), hipMemcpyHostToDevice));
             e->tx_status = "";
             e->golden.translated_blocks = leaders.size();

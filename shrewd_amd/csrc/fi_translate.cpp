@@ -333,6 +333,8 @@ struct Block {
     uint32_t h0;
     std::vector<uint32_t> insts;
     bool term;
+    uint64_t opc = 0;             // odd-pc block (solo body only): its first pc
+    std::vector<uint64_t> opcs;   // ... and the pc of each instruction (insts: their keys)
 };
 
 }  // namespace
@@ -385,6 +387,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         if ((k == C_BR || k == C_JAL || k == C_JALR) && executed.count(h + pre[h].len / 2u))
             leaders.insert(h + pre[h].len / 2u);
     }
+    const std::set<uint32_t> golden_exec = executed;
     // static closure: code the golden run never executed but that its direct
     // control flow reaches (the other side of a branch, a call's return site,
     // the code after an ecall) -- faulty trials go there, and translated code
@@ -427,6 +430,51 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         const char *cond;
         if (!valid(*it) || classify(pre[*it], e, sz, sx, cond) == C_STOP) it = leaders.erase(it);
         else ++it;
+    }
+
+    // ---- odd-pc streams (solo body only).  A pc bit-0 flip leaves the pc odd;
+    // an odd pc fetches its word's pc | 2 halfword (key (pc & ~3) | 2) and
+    // steps by the instruction length, so the stream stays odd until a jalr.
+    // The entries are the golden pcs | 1 (both odd pcs of a word, which share
+    // one pre-decoded entry and its flag), closed under the stream's direct
+    // control flow.  Blocks run from an odd leader (a branch or jal target, the
+    // pc after a control transfer, a pc no other odd instruction falls into)
+    // to a control transfer or the next leader; they are entered and left
+    // through the dispatch (no direct edges: the even blocks' cycle structure
+    // stays as the structurer made it).  Both odd pcs of a word lead together:
+    // they share the key's kPreOddLeader flag, at which the interpreter hands
+    // over.
+    // Off by default (SHREWD_FI_TX_ODD=1 turns it on): the odd blocks take a
+    // crc32 pc bit-0 tail trial from ~600 to ~128 ns per instruction and a
+    // qsort one from ~676 to ~275 ns, but they are ~2.7x the solo body's even
+    // code on crc32, and the larger solo kernel (SGPR spills 1.7k -> 8.3k)
+    // slows the whole solo epoch: crc32 bench 13.1M -> 11.7M trials/s,
+    // intmix 90k -> 83k, qsort 438k -> 444k (profiles/r02p_odd_ab.txt).
+    static const bool tx_odd = getenv("SHREWD_FI_TX_ODD") && atoi(getenv("SHREWD_FI_TX_ODD")) != 0;
+    std::set<uint64_t> odd;
+    if (tx_odd) {
+        const size_t cap = 2 * golden_exec.size() + 1024;
+        std::vector<uint64_t> work;
+        for (uint32_t h : golden_exec) work.push_back(text_lo + 2ULL * h + 1);
+        while (!work.empty() && odd.size() < cap) {
+            const uint64_t pc = work.back();
+            work.pop_back();
+            if (pc < text_lo || odd.count(pc)) continue;
+            const uint64_t hk = (((pc & ~3ULL) | 2) - text_lo) / 2;
+            if (hk >= pre.size() || !valid((uint32_t)hk)) continue;
+            std::string e;
+            uint32_t sz;
+            int sx;
+            const char *cond;
+            const Cls k = classify(pre[hk], e, sz, sx, cond);
+            if (k == C_STOP) continue;
+            odd.insert(pc);
+            work.push_back(pc ^ 2);
+            const uint64_t ft = pc + pre[hk].len, tg = pc + (int64_t)pre[hk].imm;
+            if (k == C_BR) { work.push_back(ft); work.push_back(tg); }
+            else if (k == C_JAL) work.push_back(tg);
+            else if (k != C_JALR) work.push_back(ft);
+        }
     }
 
     // ---- the blocks: from a leader until a control transfer (inclusive), an
@@ -476,6 +524,42 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     }
     Structurer S{succ, {}, {}};
     S.run(std::vector<uint32_t>(leaders.begin(), leaders.end()), true, {});
+    auto okey = [&](uint64_t pc) { return (uint32_t)((((pc & ~3ULL) | 2) - text_lo) / 2); };
+    auto ocls = [&](uint64_t pc) {
+        std::string e;
+        uint32_t sz;
+        int sx;
+        const char *cond;
+        return classify(pre[okey(pc)], e, sz, sx, cond);
+    };
+    std::set<uint64_t> olead, ofall;   // odd leaders; odd pcs some odd non-transfer falls into
+    for (uint64_t pc : odd) {
+        const Cls k = ocls(pc);
+        const uint64_t ft = pc + pre[okey(pc)].len;
+        if (k == C_BR || k == C_JAL) {
+            const uint64_t tg = pc + (int64_t)pre[okey(pc)].imm;
+            if (odd.count(tg)) olead.insert(tg);
+        }
+        if (k == C_BR || k == C_JAL || k == C_JALR) { if (odd.count(ft)) olead.insert(ft); }
+        else ofall.insert(ft);
+    }
+    for (uint64_t pc : odd)
+        if (!ofall.count(pc)) olead.insert(pc);
+    for (uint64_t pc : std::vector<uint64_t>(olead.begin(), olead.end()))
+        if (odd.count(pc ^ 2)) olead.insert(pc ^ 2);
+    for (uint64_t pc0 : olead) {
+        Block b{okey(pc0), {}, false};
+        b.opc = pc0;
+        for (uint64_t pc = pc0; odd.count(pc) && (pc == pc0 || !olead.count(pc));) {
+            b.insts.push_back(okey(pc));
+            b.opcs.push_back(pc);
+            const Cls k = ocls(pc);
+            if (k == C_BR || k == C_JAL || k == C_JALR) { b.term = true; break; }
+            pc += pre[okey(pc)].len;
+        }
+        blocks.push_back(b);
+    }
+    bool cur_odd = false;   // generating an odd-pc block: every edge goes through the dispatch
 
     enum Edge { E_DIRECT, E_DISPATCH, E_OUT };
     auto edge = [&](uint32_t from, uint64_t pc) {
@@ -501,6 +585,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto tx_dispatch; }" : "; goto tx_out; }");
     };
     auto sgo = [&](uint32_t from, uint64_t pc) {
+        if (cur_odd || (pc & 1))
+            return "{ spc = " + hex(pc) + ((!(pc & 1) || olead.count(pc)) ? "; goto S_dispatch; }" : "; goto S_out; }");
         const Edge k = edge(from, pc);
         uint32_t t = 0;
         hof(pc, t);
@@ -510,7 +596,16 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     g.put("tx_dispatch: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", (unsigned long long)text_lo);
     g.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto tx_out;\n  switch ((uint32_t)off_ >> 1) {\n");
     so.put("S_dispatch: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", (unsigned long long)text_lo);
-    so.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto S_out;\n  switch ((uint32_t)off_ >> 1) {\n");
+    if (odd.empty()) {
+        so.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto S_out;\n  switch ((uint32_t)off_ >> 1) {\n");
+    } else {
+        so.put("  if ((off_ >> 32) != 0) goto S_out;\n  if (off_ & 1) switch ((uint32_t)off_ >> 1) {\n");
+        for (uint64_t pc : olead) {
+            const uint32_t i = (uint32_t)((pc - text_lo) >> 1);
+            so.put("  case %u: goto SO_%u;\n", i, i);
+        }
+        so.put("  default: goto S_out;\n  }\n  switch ((uint32_t)off_ >> 1) {\n");
+    }
     for (uint32_t h : leaders) {
         auto it = S.chain.find(h);
         if (it == S.chain.end() || (it->second.size() == 1 && it->second[0] == h)) {
@@ -530,7 +625,10 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         const std::vector<uint32_t> &insts = b.insts;
         const uint32_t n = (uint32_t)insts.size();
         n_insts += n;
-        const uint64_t pc0 = g.pc_of(h0);
+        cur_odd = b.opc != 0;
+        std::string g_keep;   // an odd-pc block has no wave form: its wave text is dropped
+        if (cur_odd) g_keep.swap(g.out);
+        const uint64_t pc0 = cur_odd ? b.opc : g.pc_of(h0);
         const std::string P0 = hex(pc0);
         uint32_t rw = 0;   // registers the block reads or writes (watch check)
         for (uint32_t hh : insts) {
@@ -540,10 +638,20 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             if ((p.flags & kPreRd) && p.rd) rw |= 1u << p.rd;
         }
         if (!tx_watch) rw = 0;
-        const uint64_t blo = pc0 & ~3ULL, bhi = g.pc_of(insts.empty() ? h0 : insts.back()) + 6;
+        uint64_t blo = pc0 & ~3ULL, bhi = g.pc_of(insts.empty() ? h0 : insts.back()) + 6;
+        if (cur_odd) {   // the bytes the keys cover
+            blo = ~0ULL; bhi = 0;
+            for (uint32_t hh : insts) {
+                blo = std::min<uint64_t>(blo, g.pc_of(hh) & ~3ULL);
+                bhi = std::max<uint64_t>(bhi, g.pc_of(hh) + 7);
+            }
+        }
         g.put("B_%u: { // pc 0x%llx, %u insts\n", h0, (unsigned long long)pc0, n);
-        so.put("S_%u: { // pc 0x%llx, %u insts\n", h0, (unsigned long long)pc0, n);
-        if (S.headers.count(h0)) {   // a cycle header routes an entry into its cycle one level on (etgt)
+        if (cur_odd)
+            so.put("SO_%u: { // pc 0x%llx (odd)\n", (uint32_t)((pc0 - text_lo) >> 1), (unsigned long long)pc0);
+        else
+            so.put("S_%u: { // pc 0x%llx, %u insts\n", h0, (unsigned long long)pc0, n);
+        if (!cur_odd && S.headers.count(h0)) {   // a cycle header routes an entry into its cycle one level on (etgt)
             std::string rw_, rs_;
             for (uint32_t x : leaders) {
                 auto it = S.chain.find(x);
@@ -596,7 +704,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         };
         for (uint32_t i = 0; i < n; i++) {
             const PreInst &p = pre[insts[i]];
-            const uint64_t pc = g.pc_of(insts[i]);
+            const uint64_t pc = cur_odd ? b.opcs[i] : g.pc_of(insts[i]);
             const uint64_t ft = pc + p.len;
             std::string e;
             uint32_t sz;
@@ -708,14 +816,19 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             k_st += 1; k_xt += xt; k_fb += p.len; k_db += (k == C_LOAD || k == C_STORE) ? sz : 0;
         }
         if (!b.term) {   // fell into the next leader, or stops before an instruction it does not cover
-            const uint64_t nxt = n ? g.pc_of(insts[n - 1]) + pre[insts[n - 1]].len : pc0;
+            const uint64_t nxt = cur_odd ? (n ? b.opcs[n - 1] + pre[insts[n - 1]].len : pc0)
+                                         : n ? g.pc_of(insts[n - 1]) + pre[insts[n - 1]].len : pc0;
             g.put("  %s %s\n", commit(k_st, k_xt, k_fb, k_db).c_str(), wgo(h0, nxt).c_str());
             so.put("  %s %s\n", scommit(k_st, k_xt, k_fb, k_db).c_str(), sgo(h0, nxt).c_str());
         }
         g.put("}\n");
         so.put("}\n");
+        if (cur_odd) g.out.swap(g_keep);
     }
+    cur_odd = false;
     leaders_out.assign(leaders.begin(), leaders.end());
+    // odd-pc entries: bit 31 + the pre-decoded index of their key (kPreOddLeader)
+    for (uint64_t pc : olead) leaders_out.push_back(0x80000000u | okey(pc));
     return g.out + FI_TX_SPLIT + so.out;
 }
 

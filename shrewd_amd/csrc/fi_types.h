@@ -29,6 +29,7 @@ struct PreInst {
 static_assert(sizeof(PreInst) == 16, "PreInst must stay 16 bytes (one s_load_dwordx4)");
 constexpr uint8_t kPreValid = 1, kPreStraddle = 2, kPreRs1 = 4, kPreRs2 = 8, kPreRd = 16;
 constexpr uint8_t kPreLeader = 32;   // translated code may be entered here (load-time build)
+constexpr uint8_t kPreOddLeader = 64;   // ... and (solo kernel) at the odd pcs that fetch this halfword
 // Separates the 64-lane and the solo translated bodies in the generated text
 // (fi_translate.cpp -> fi_jit.cpp splices them at /*@TX_BODY@*/ and /*@TX_SOLO@*/).
 #define FI_TX_SPLIT "\n/*@TX_SPLIT@*/\n"

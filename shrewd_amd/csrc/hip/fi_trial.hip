@@ -1776,7 +1776,13 @@ __device__ __forceinline__ void trial_body() {
             tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
             tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
             const PreRef E0 = pre_entry(tx, lpc);
+#ifdef FI_TX_ODD
+            // (odd pcs: the solo body's odd-pc blocks, flagged on their key's entry)
+            const bool tx_entry = E0.in && ((lpc & 1) ? (kNL == 1 && ((uni32(E0.e.w) >> 8) & kPreOddLeader))
+                                                      : ((uni32(E0.e.w) >> 8) & kPreLeader));
+#else
             const bool tx_entry = !(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader);
+#endif
             if constexpr (kNL == 1) {
                 // ---- solo: one trial, every value uniform -- no groups, no
                 // parking, plain register writes; the same exits and counters
@@ -1997,9 +2003,14 @@ __device__ __forceinline__ void trial_body() {
                 const uint32_t aux = q3 >> 16, kind = aux & 63;
                 if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
 #ifdef FI_TX
-                // translated blocks take over here (not at odd pcs: their entries are
-                // their word's pc | 2 entries, and the translated path refuses them)
-                if (steps && ((q3 >> 8) & kPreLeader) && !((uint32_t)spc & 1) &&
+                // translated blocks take over here (odd pcs: only the solo kernel's
+                // odd-pc blocks, flagged on the entry of the halfword they fetch)
+#ifdef FI_TX_ODD
+                const bool lead = ((uint32_t)spc & 1) ? (kNL == 1 && ((q3 >> 8) & kPreOddLeader)) : ((q3 >> 8) & kPreLeader);
+#else
+                const bool lead = ((q3 >> 8) & kPreLeader) && !((uint32_t)spc & 1);
+#endif
+                if (steps && lead &&
                     !(any_dirty && wballot<kNL>(mine && dirty_near(m, spc)) != 0) && n_iter + steps >= tx_skip_until)
                     break;
 #endif
