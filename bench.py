@@ -118,7 +118,8 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from shrewd_amd import HIST_DT, Engine
+    from shrewd_amd import ESCAPE_NAMES, HIST_DT, Engine
+    from shrewd_amd.fi import escape_breakdown
     with open(os.path.join(ROOT, "workloads", f"{a.workload}.elf"), "rb") as f:
         elf = f.read()
     eng = Engine(device=local, max_trials_per_launch=max(a.trials, 1024), lanes_per_wave=a.lanes,
@@ -236,6 +237,8 @@ def main():
                                                                  "escape"])},
             "golden_s": golden_s,
         }
+        res["escape_sub"] = {ESCAPE_NAMES.get(i, str(i)): int(node_h["escape_sub"][i]) for i in range(8)
+                             if node_h["escape_sub"][i]}
         res["parity"] = None
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"], ref = cpu_baseline(elf, a.workload, a.seed, a.cpu_seconds)
@@ -243,6 +246,7 @@ def main():
             # trials): every outcome must equal the oracle's, bit for bit
             dev, _ = eng.run_trials(0, len(ref))
             bad = int((dev != ref).sum())
+            res["escapes_in_checked"] = escape_breakdown(dev)
             res["parity"] = {"checked": int(len(ref)), "mismatches": bad,
                              "against": "oracle/rv64se.c, trial ids [0, checked) of the benched campaign"}
         else:

@@ -75,6 +75,7 @@ typedef int32_t fi_status;
 #define FI_CRASH_AMO_LINE 10      /* panic  AMO across a cache line cpu/simple/atomic.cc:569-570 */
 #define FI_CRASH_SC_LINE 11       /* abort  SC across a cache line  cpu/simple/atomic.cc:482 assert(curr_frag_id == 0) */
 #define FI_CRASH_SE_PANIC 12      /* panic  in an SE syscall handler (null ProxyPtr, MemState::isUnmapped) */
+#define FI_CRASH_M5_PANIC 13      /* panic  in an M5 pseudo-op (m5_panic, unknown initparam key) sim/pseudo_inst.* */
 /* FI_ESCAPE sub-codes */
 #define FI_ESC_INST 1
 #define FI_ESC_SYSCALL 2

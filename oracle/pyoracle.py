@@ -119,6 +119,7 @@ def lib():
         L.or_golden_ops.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64]
         L.or_shadow_map.restype = C.c_uint64
         L.or_shadow_map.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(IssueStats)]
+        L.or_rvk.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
         L.or_sf_ref.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                 C.c_void_p, C.c_void_p]
         _lib = L
@@ -257,3 +258,17 @@ def sf_ref(op: int, fmt: int, rm: int, a, b=None, c=None):
     fl = np.zeros(len(a), np.uint32)
     lib().or_sf_ref(op, fmt, rm, a.ctypes.data, b.ctypes.data, c.ctypes.data, len(a), out.ctypes.data, fl.ctypes.data)
     return out, fl
+
+
+def has_rvk() -> bool:
+    """The reference's scalar-crypto helpers (oracle/_ref) are linked: Zkn/Zks execute."""
+    return bool(lib().or_has_rvk())
+
+
+def rvk_ref(fn: int, a, b=None):
+    """The reference's rvk.hh over operand vectors (fi_crypto.h function numbers)."""
+    a = np.ascontiguousarray(a, np.uint64)
+    b = np.ascontiguousarray(a if b is None else b, np.uint64)
+    out = np.zeros(len(a), np.uint64)
+    lib().or_rvk(fn, a.ctypes.data, b.ctypes.data, len(a), out.ctypes.data)
+    return out

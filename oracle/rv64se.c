@@ -22,6 +22,25 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* Zkn/Zks: the reference's scalar-crypto helpers (oracle/rvk_ref.cc over
+ * src/arch/riscv/rvk.hh, oracle/rvk_ref.mk), linked when present (OR_RVK). */
+#ifdef OR_RVK
+uint64_t or_rvk_ref(int fn, uint64_t a, uint64_t b);   /* oracle/rvk_ref.cc: the reference's rvk.hh */
+#endif
+
+#ifdef OR_RVK
+int or_has_rvk(void) { return 1; }
+void or_rvk(int fn, const uint64_t *a, const uint64_t *b, uint64_t n, uint64_t *out) {
+    for (uint64_t i = 0; i < n; i++) out[i] = or_rvk_ref(fn, a[i], b[i]);
+}
+#else
+int or_has_rvk(void) { return 0; }
+void or_rvk(int fn, const uint64_t *a, const uint64_t *b, uint64_t n, uint64_t *out) {
+    (void)fn; (void)a; (void)b;
+    memset(out, 0, n * sizeof *out);
+}
+#endif
+
 /* ------------------------------------------------------------- SoftFloat */
 /* F/D/Zfh arithmetic is the reference's own SoftFloat (gem5 ext/softfloat,
  * RISC-V specialization), compiled from its sources into oracle/_ref by
@@ -239,7 +258,7 @@ typedef struct {
 } mach_t;
 
 enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_ESCAPE = 5, F_PGFAULT = 6, F_AMOLINE = 7,
-       F_SCLINE = 8 };
+       F_SCLINE = 8, F_M5PANIC = 9 };
 
 /* -------------------------------------------------------------- decode */
 /* Op ids.  Names follow gem5's mnemonics (arch/riscv/isa/decoder.isa). */
@@ -275,7 +294,8 @@ enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_E
     X(amoadd_d) X(amoswap_d) X(amoxor_d) X(amoor_d) X(amoand_d) X(amomin_d) X(amomax_d) X(amominu_d) X(amomaxu_d) \
     X(lr_w) X(sc_w) X(lr_d) X(sc_d) \
     X(fadd) X(fsub) X(fmul) X(fdiv) X(fsqrt) X(fmin) X(fmax) X(fmadd) X(fmsub) X(fnmsub) X(fnmadd) \
-    X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f)
+    X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f) \
+    X(priv) X(cbo) X(m5op) X(crypto)
 
 enum {
 #define X(n) OP_##n,
@@ -325,6 +345,70 @@ static int gem5_known(u32 raw) {
 }
 /* Unknown and escape encodings read and write no registers. */
 static void refine_fp_amo(u32 raw, dec_t *d);
+/* The gem5-known members of the privileged SYSTEM, hypervisor load/store,
+ * cache-block, M5 pseudo-op and scalar-crypto groups, which the SE process
+ * executes deterministically (registers: the source operands the generated
+ * execute() reads first, exec-ns.cc.inc of the reference's ISA parser).
+ *   priv   imm 0: IllegalInstFault in PRV_U (SE runs the process in PRV_U,
+ *          arch/riscv/process.cc:105; privilege set MSU, no RVH, no Smrnmi,
+ *          RiscvISA.py:108,129): sret / wfi / sfence_vma / hfence_vvma / mret /
+ *          hfence_gvma / mnret (decoder.isa:5966-6233) and every hlv* / hsv*
+ *          (formats/mem.isa:364-376,461-473, after reading Rs1 [, Rs2]);
+ *          imm 1: warn-only no-ops sinval_vvma / sfence_w_inval /
+ *          sfence_inval_ir / hinval_vvma / hinval_gvma (:6070-6090,6112,6236).
+ *   cbo    imm = FUNCT12 (0 inval, 1 clean, 2 flush, 4 zero): a 64-byte
+ *          request at Rs1 & ~63 (CacheBlockBasedStoreExecute, formats/
+ *          mem.isa:244-268: the body's privilege checks are not part of
+ *          execute); zero writes 64 zero bytes (CACHE_BLOCK_ZERO ->
+ *          WriteReq), the others only translate (CleanShared / CleanInvalid /
+ *          InvalidateReq: AbstractMemory::access leaves memory alone).
+ *   m5op   imm = M5FUNC (bitfields.isa:135); a0 = result, a1 = 0.
+ *   crypto imm = function (see crypto_fn) | RNUM or BS << 8. */
+static const char *const crypto_names[22] = {
+    "sha256sum0", "sha256sum1", "sha256sig0", "sha256sig1", "sha512sum0", "sha512sum1", "sha512sig0", "sha512sig1",
+    "sm3p0", "sm3p1", "aes64im", "aes64ks1i", "brev8", "sm4ed", "sm4ks", "aes64es", "aes64esm", "aes64ds", "aes64dsm",
+    "aes64ks2", "xperm4", "xperm8"};
+static void refine_misc(u32 raw, dec_t *d) {
+    const u32 f3 = bits(raw, 14, 12), f7 = bits(raw, 31, 25);
+    const int rd = (int)bits(raw, 11, 7), rs1 = (int)bits(raw, 19, 15), rs2 = (int)bits(raw, 24, 20);
+    switch (d->op) {
+    case OP_ESC_SYS:
+        d->op = OP_priv;
+        d->imm = (f7 == 0x0b || f7 == 0x0c || f7 == 0x13 || f7 == 0x33) ? 1 : 0;
+        if (f7 == 0x09 || f7 == 0x11 || f7 == 0x31) { d->rs1 = rs1; d->rs2 = rs2; }   /* demapPage(Rs1, Rs2) */
+        return;
+    case OP_ESC_HYP:
+        d->op = OP_priv; d->imm = 0; d->rs1 = rs1;
+        if (f7 & 1) d->rs2 = rs2;   /* hsv_*: FUNCT7 0x31 / 0x33 / 0x35 / 0x37 */
+        return;
+    case OP_ESC_CBO: d->op = OP_cbo; d->rs1 = rs1; d->imm = bits(raw, 31, 20); return;
+    case OP_ESC_M5: d->op = OP_m5op; d->rd = 10; d->imm = f7; return;
+    case OP_ESC_CRYPTO: {
+        const u32 opc = bits(raw, 6, 2), kf5 = bits(raw, 29, 25), bs = bits(raw, 31, 30);
+        int fn = -1;
+        if (opc == 0x04 && f3 == 1) {
+            if (bits(raw, 31, 27) == 0x02) fn = rs2;                            /* sha256* sha512* sm3p*: 0..9 */
+            else fn = bits(raw, 24, 24) ? 11 | (int)(bits(raw, 23, 20) << 8) : 10;   /* aes64ks1i / aes64im */
+        } else if (opc == 0x04) {
+            fn = 12;                                                            /* brev8 */
+        } else if (opc == 0x0c && f3 == 0) {
+            switch (kf5) {
+            case 0x18: fn = 13 | (int)(bs << 8); break;                         /* sm4ed */
+            case 0x1a: fn = 14 | (int)(bs << 8); break;                         /* sm4ks */
+            case 0x19: fn = 15; break; case 0x1b: fn = 16; break; case 0x1d: fn = 17; break;
+            case 0x1f: fn = bs ? 19 : 18; break;                                /* aes64dsm / aes64ks2 */
+            }
+        } else if (opc == 0x0c) {
+            fn = f3 == 2 ? 20 : 21;                                             /* xperm4 / xperm8 */
+        }
+        if (fn < 0) return;
+        d->op = OP_crypto; d->imm = fn; d->rd = rd; d->rs1 = rs1;
+        if ((fn & 0xFF) >= 13) d->rs2 = rs2;
+        return;
+    }
+    default: return;
+    }
+}
 static void decode(u32 raw, dec_t *d) {
     decode_tree(raw, d);
     if ((raw & 3) == 3 && (d->op == OP_ESC_FP || d->op == OP_ESC_VEC || d->op == OP_ESC_AMO ||
@@ -332,6 +416,7 @@ static void decode(u32 raw, dec_t *d) {
         d->op = OP_UNKNOWN;
     if ((raw & 3) == 3 && (d->op == OP_ESC_FP || d->op == OP_ESC_AMO)) refine_fp_amo(raw, d);
     if (d->op < OP_c_addi4spn) d->rd = d->rs1 = d->rs2 = d->frd = d->frs1 = d->frs2 = -1;
+    if ((raw & 3) == 3) refine_misc(raw, d);
 }
 /* The executed members of the LOAD-FP / STORE-FP / OP-FP / AMO groups, among
  * the encodings gem5 decodes to a known class (decoder.isa:567-591 flh/flw/fld,
@@ -787,6 +872,37 @@ const char *or_mnemonic(u32 inst) {
         return buf;
     }
 #endif
+    if (d.op == OP_priv) {
+        const u32 f7 = bits(inst, 31, 25), rs2 = bits(inst, 24, 20);
+        if (bits(inst, 14, 12) == 4) {
+            static const char *hn[8][4] = {{"hlv_b", "hlv_bu"}, {"hsv_b", "hsv_b", "hsv_b", "hsv_b"},
+                                           {"hlv_h", "hlv_hu", 0, "hlvx_hu"}, {"hsv_h", "hsv_h", "hsv_h", "hsv_h"},
+                                           {"hlv_w", "hlv_wu", 0, "hlvx_wu"}, {"hsv_w", "hsv_w", "hsv_w", "hsv_w"},
+                                           {"hlv_d"}, {"hsv_d", "hsv_d", "hsv_d", "hsv_d"}};
+            /* hsv_* and hlv_d are decoded on FUNCT7 alone (decoder.isa:6240-6297) */
+            const char *n = ((f7 & 1) || f7 == 0x36) ? hn[f7 - 0x30][0] : rs2 < 4 ? hn[f7 - 0x30][rs2] : 0;
+            return n ? n : "?";
+        }
+        switch (f7) {
+        case 0x08: return rs2 == 2 ? "sret" : "wfi";
+        case 0x09: return "sfence_vma";
+        case 0x0b: return "sinval_vvma";
+        case 0x0c: return rs2 ? "sfence_inval_ir" : "sfence_w_inval";
+        case 0x11: return "hfence_vvma";
+        case 0x13: return "hinval_vvma";
+        case 0x18: return "mret";
+        case 0x31: return "hfence_gvma";
+        case 0x33: return "hinval_gvma";
+        case 0x38: return "mnret";
+        default: return "?";
+        }
+    }
+    if (d.op == OP_cbo) {
+        static const char *cn[5] = {"cbo_inval", "cbo_clean", "cbo_flush", "?", "cbo_zero"};
+        return d.imm <= 4 ? cn[d.imm] : "?";
+    }
+    if (d.op == OP_m5op) return "M5Op";
+    if (d.op == OP_crypto) return crypto_names[d.imm & 0xFF];
     const char *n = op_names[d.op];
     size_t l = strlen(n);
     if (l && n[l - 1] == '_') { snprintf(buf, sizeof buf, "%.*s", (int)(l - 1), n); return buf; }
@@ -881,6 +997,17 @@ static int mem_write(mach_t *m, u64 addr, unsigned size, u64 val, u64 *fault_va)
         done += frag; a += frag;
     }
     m->data_bytes += size;
+    return F_NONE;
+}
+
+/* cbo.zero: AtomicSimpleCPU::writeMem(nullptr data -> zero_array, 64 bytes at
+ * a 64-byte-aligned address: one fragment, atomic.cc:437-449) */
+static int mem_write_zero64(mach_t *m, u64 ea, u64 *fault_va) {
+    uint8_t *pg = translate_w(m, ea);
+    if (!pg) { *fault_va = ea; return F_PGFAULT; }
+    memset(pg + (ea & (PAGE - 1)), 0, 64);
+    if (m->lock == ea) m->lock = OR_NONE;
+    m->data_bytes += 64;
     return F_NONE;
 }
 
@@ -1758,6 +1885,67 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
         v = ok ? 0 : 1;   /* result = !success (amo.isa StoreCondExecute) */
         break;
     }
+    /* ---- privileged SYSTEM / hypervisor load-store from PRV_U (refine_misc) */
+    case OP_priv:
+        if (!imm) return F_ILLEGAL;
+        goto no_rd;
+    /* ---- cache-block operations: one 64-byte request at the line of Rs1 */
+    case OP_cbo: {
+        const u64 ea = a & ~63ULL;
+        if (imm == 4) { r = mem_write_zero64(m, ea, fault_va); if (r) return r; goto no_rd; }
+        if (!translate(m, ea)) { *fault_va = ea; return F_PGFAULT; }
+        goto no_rd;
+    }
+    /* ---- M5Op (formats/m5ops.isa:39-57): pseudoInstWork (sim/pseudo_inst.hh)
+     * with RegABI64 arguments a0.. (reg_abi.cc:37-40); the generated execute()
+     * then writes a0 = rvSext(result) and a1 = 0 (its RV32 branch's second
+     * destination, zero-initialised: exec-ns.cc.inc M5Op::execute).  Under the
+     * default System / BaseCPU params of an SE run (System.py:120-149,
+     * BaseCPU.py:124-129; one thread context, no dist-gem5). */
+    case OP_m5op: {
+        u64 res = 0;
+        switch (imm) {
+        case 0x07: res = (m->num_cycles - 1) * m->c->clk_period / 1000; break;   /* rpns: curTick() / ns */
+        case 0x23:   /* m5sum(a0..a5) */
+            if (m->watch >= 10 && m->watch <= 15) return 100;
+            for (int k = 10; k <= 15; k++) res += m->x[k];
+            break;
+        case 0x30: {   /* initParam: the key is the 16 bytes of a0, a1 as a C string */
+            if (m->watch == 10 || m->watch == 11) return 100;
+            char key[17];
+            for (int k = 0; k < 8; k++) { key[k] = (char)(m->x[10] >> (8 * k)); key[8 + k] = (char)(m->x[11] >> (8 * k)); }
+            key[16] = 0;
+            if (!key[0]) res = 0;                              /* DEFAULT "": System.init_param = 0 */
+            else if (!strcmp(key, "dist-rank")) res = 0;       /* DistIface::rankParam, no primary */
+            else if (!strcmp(key, "dist-size")) res = 1;       /* DistIface::sizeParam, no primary */
+            else return F_M5PANIC;                             /* "Unknown key for initparam" */
+            break;
+        }
+        case 0x51: return F_BREAK;      /* debugbreak: debug::breakpoint() -> SIGTRAP (base/debug.cc:64-70) */
+        case 0x54: return F_M5PANIC;    /* M5OP_PANIC */
+        /* simulator control or host files: quiesce*, exit, fail, checkpoint,
+         * writefile, switchcpu, addsymbol, workbegin / workend, togglesync,
+         * workload event, hypercall */
+        case 0x01: case 0x02: case 0x03: case 0x04: case 0x21: case 0x22: case 0x43: case 0x4f: case 0x52:
+        case 0x53: case 0x5a: case 0x5b: case 0x62: case 0x70: case 0x71:
+            return F_ESCAPE;
+        /* arm (Workload stats), wakeCPU (the only context is active), loadsymbol
+         * (symbolfile ""), reset/dump stats (a later stats event only),
+         * readfile (readfile ""), reserved and unhandled functions: result 0 */
+        default: break;
+        }
+        wrreg(m, 10, res);
+        wrreg(m, 11, 0);
+        m->wrote = 1;
+        if (m->watch == 10 || m->watch == 11) m->watch = -1;
+        return F_NONE;
+    }
+#ifdef OR_RVK
+    /* ---- Zkn / Zks through the reference's own helpers (rvk_ref.cc) */
+    case OP_crypto: v = or_rvk_ref((int)imm, a, b); break;
+#else
+    case OP_crypto: return F_ESCAPE;
+#endif
     default: return F_UNKNOWN;
     }
     wrreg(m, d->rd, v);
@@ -1808,6 +1996,7 @@ static void invoke_fault(mach_t *m, int f, u64 fault_va, const dec_t *d) {
     case F_ESCAPE + 100: finish(m, OR_ESCAPE, OR_ESC_CSR, 0); m->res.detail = d->raw; return;
     case F_AMOLINE: finish(m, OR_CRASH, OR_CRASH_AMO_LINE, 134); return;
     case F_SCLINE: finish(m, OR_CRASH, OR_CRASH_SC_LINE, 134); return;
+    case F_M5PANIC: finish(m, OR_CRASH, OR_CRASH_M5_PANIC, 134); return;
     case 100: finish(m, OR_DETECTED, 0, 0); return;
     case F_PGFAULT: {
         int h = fixup_fault(m, fault_va);

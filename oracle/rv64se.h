@@ -39,7 +39,8 @@ enum {
     OR_CRASH_STACK_LIMIT = 9,   /* fatal: Maximum stack size      mem_state.cc:440 */
     OR_CRASH_AMO_LINE = 10,     /* panic: AMO across a cache line atomic.cc:569-570 */
     OR_CRASH_SC_LINE = 11,      /* abort: SC across a cache line  atomic.cc:482 assert(curr_frag_id == 0) */
-    OR_CRASH_SE_PANIC = 12      /* panic in an SE handler (null ProxyPtr, MemState::isUnmapped) */
+    OR_CRASH_SE_PANIC = 12,     /* panic in an SE handler (null ProxyPtr, MemState::isUnmapped) */
+    OR_CRASH_M5_PANIC = 13      /* panic in an M5 pseudo-op (m5_panic, unknown initparam key) sim/pseudo_inst.* */
 };
 enum {
     OR_ESC_INST = 1,            /* instruction gem5 decodes but the engine does not model */
@@ -168,6 +169,10 @@ int or_probe(uint32_t inst, uint64_t pc, const uint64_t regs[32], or_probe_t *ou
 const char *or_mnemonic(uint32_t inst);
 /* syscall classification (0 absent,1 unimpl,2 ignore,3 escape,4 modelled) */
 int or_sys_class(int num);
+/* the reference's rvk.hh (oracle/_ref) present: Zkn/Zks execute; or_rvk runs
+ * function fn (shrewd_amd/csrc/hip/fi_crypto.h numbering) over vectors */
+int or_has_rvk(void);
+void or_rvk(int fn, const uint64_t *a, const uint64_t *b, uint64_t n, uint64_t *out);
 /* SoftFloat (oracle/_ref) present: F/D/Zfh arithmetic executes */
 int or_has_softfloat(void);
 /* the reference SoftFloat over operand vectors (op / fmt codes of

@@ -22,6 +22,7 @@
 
 #include "fi_checkpoint.h"
 #include "fi_types.h"
+#include "rv64_isa.h"
 
 constexpr uint64_t kRndLen = 1ULL << 20;   // getrandom bytes precomputed per engine
 
@@ -917,7 +918,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         uint32_t r = 0, w = 0;
         if ((p.flags & kPreRs1) && p.rs1) r |= 1u << p.rs1;
         if ((p.flags & kPreRs2) && p.rs2) r |= 1u << p.rs2;
-        if (trace[i] & 0x80000000u) r |= 0x3FC00u;   // x10..x17
+        if ((trace[i] & 0x80000000u) || p.op == OP_m5op) r |= 0x3FC00u;   // x10..x17 (an M5Op's ABI arguments)
         else if ((p.flags & kPreRd) && p.rd) w |= 1u << p.rd;
         rmask[i] = r;
         wmask[i] = w;

@@ -14,6 +14,7 @@
 #include "fi_device.h"
 #include "rv64_isa.h"
 #include "fi_softfp.h"
+#include "fi_crypto.h"
 
 namespace fi {
 
@@ -363,6 +364,40 @@ extern "C" fi_status fi_debug_softfp(int op, int fmt, int rm, const uint64_t *a,
     if (err == hipSuccess) err = hipDeviceSynchronize();
     if (err == hipSuccess) err = hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost);
     if (err == hipSuccess) err = hipMemcpy(fl, dfl, n * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return err == hipSuccess ? FI_OK : FI_E_HIP;
+}
+
+// ------------------------------------------------------------- crypto port
+// The engine's scalar-crypto port (fi_crypto.h) over operand vectors, on the
+// host or on the device, for the pinning test against the reference's rvk.hh
+// (tests/test_crypto.py).
+namespace fi {
+__global__ void crypto_kernel(int fn, const uint64_t *a, const uint64_t *b, uint64_t n, uint64_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = rvk::exec(fn, a[i], b[i]);
+}
+}  // namespace fi
+
+extern "C" fi_status fi_debug_crypto(int fn, const uint64_t *a, const uint64_t *b, uint64_t n, uint64_t *out,
+                                     int on_device) {
+    if ((fn & 0xFF) > 21 || !a || !b || !out) return FI_E_ARG;
+    if (!on_device) {
+        for (uint64_t i = 0; i < n; i++) out[i] = fi::rvk::exec(fn, a[i], b[i]);
+        return FI_OK;
+    }
+    if (!n) return FI_OK;
+    uint64_t *d = nullptr;
+    if (hipMalloc(&d, n * 8 * 3) != hipSuccess) return FI_E_HIP;
+    hipError_t err = hipMemcpy(d, a, n * 8, hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = hipMemcpy(d + n, b, n * 8, hipMemcpyHostToDevice);
+    if (err == hipSuccess) {
+        hipLaunchKernelGGL(fi::crypto_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, fn, d, d + n, n,
+                           d + 2 * n);
+        err = hipGetLastError();
+    }
+    if (err == hipSuccess) err = hipDeviceSynchronize();
+    if (err == hipSuccess) err = hipMemcpy(out, d + 2 * n, n * 8, hipMemcpyDeviceToHost);
     (void)hipFree(d);
     return err == hipSuccess ? FI_OK : FI_E_HIP;
 }

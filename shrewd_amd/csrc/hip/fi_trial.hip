@@ -26,6 +26,7 @@
 #include "rv64_isa.h"
 #include "gem5_opclass_table.h"
 #include "fi_softfp.h"
+#include "fi_crypto.h"
 
 namespace fi {
 
@@ -411,7 +412,7 @@ __device__ bool proxy_write(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot
 }
 
 enum { F_NONE = 0, F_SYSCALL, F_BREAK, F_ILLEGAL, F_UNKNOWN, F_ESCAPE, F_ESCCSR, F_PGFAULT, F_NEEDPAGE, F_DETECT,
-       F_AMOLINE, F_SCLINE };
+       F_AMOLINE, F_SCLINE, F_M5PANIC };
 
 // AtomicSimpleCPU::readMem/writeMem (atomic.cc:331-544): the access is split
 // at 64-byte line boundaries, each fragment translated on its own; faults are
@@ -469,6 +470,9 @@ __device__ int mem_access(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, 
             case 1: w1[off] = (uint8_t)val; break;
             case 2: *(uint16_t *)(w1 + off) = (uint16_t)val; break;
             case 4: *(uint32_t *)(w1 + off) = (uint32_t)val; break;
+            case 64:   // cbo.zero: the 64-byte line (val is 0)
+                for (int k = 0; k < 8; k++) *(uint64_t *)(w1 + off + 8 * k) = 0;
+                break;
             default: *(uint64_t *)(w1 + off) = val; break;
             }
         } else {
@@ -2287,6 +2291,9 @@ __device__ __forceinline__ void trial_body() {
         uint32_t xticks = 0;          // extra micro-op ticks (AMO fences)
         int amo = -1;                 // AMO read-modify-write op (amo_apply), -1 none
         int llsc = 0;                 // 1 LR, 2 SC
+        uint32_t cbo = 0;             // cache-block op: 1 translate only, 2 zero the line
+        bool m5 = false;              // M5Op: a1 = 0 at commit
+        bool xdet = false;            // a replica watch read through an M5Op's ABI arguments
 #define FREG_RD(r) (L.fp ? CX->fregs[(uint64_t)(r) * CX->n_slots + slot] : 0ULL)
         // detected-by-replica: the flipped protected register is read before
         // being overwritten (build-defined SHREWD semantics)
@@ -2529,15 +2536,46 @@ __device__ __forceinline__ void trial_body() {
                 xticks = ((d.raw >> 25) & 1) + ((d.raw >> 26) & 1);
                 if (CX->record) CX->stats[22] = 1;
                 break;
+            // ---- privileged SYSTEM / hypervisor load-store from PRV_U, cache-block
+            // ops, M5 pseudo-ops, scalar crypto (oracle/rv64se.c refine_misc, execute)
+            case OP_priv: if (!d.imm) f = F_ILLEGAL; wrd = false; break;
+            case OP_cbo: wrd = false; cbo = d.imm == 4 ? 2u : 1u; msz = d.imm == 4 ? 64u : 1u; mst = d.imm == 4; break;
+            case OP_m5op: {   // a0 = result, a1 = 0 (M5Op::execute); pseudoInstWork under SE defaults
+                m5 = true;
+                switch ((uint32_t)d.imm) {
+                case 0x07: v = (L.ncyc - 1) * CX->clk_period / 1000; break;   // rpns
+                case 0x23:   // m5sum(a0..a5)
+                    xdet = L.watch >= 10 && L.watch <= 15;
+                    v = RREG(10) + RREG(11) + RREG(12) + RREG(13) + RREG(14) + RREG(15);
+                    break;
+                case 0x30: {   // initParam: key = the C string in a0, a1 ("", dist-rank, dist-size)
+                    xdet = L.watch == 10 || L.watch == 11;
+                    const uint64_t k0 = RREG(10), k1 = RREG(11);
+                    if ((k0 & 0xFF) == 0) v = 0;
+                    else if (k0 == 0x6E61722D74736964ULL && (k1 & 0xFFFF) == 0x6B) v = 0;
+                    else if (k0 == 0x7A69732D74736964ULL && (k1 & 0xFFFF) == 0x65) v = 1;
+                    else f = F_M5PANIC;
+                    break;
+                }
+                case 0x51: f = F_BREAK; break;       // debugbreak -> SIGTRAP
+                case 0x54: f = F_M5PANIC; break;     // m5_panic
+                case 0x01: case 0x02: case 0x03: case 0x04: case 0x21: case 0x22: case 0x43: case 0x4f: case 0x52:
+                case 0x53: case 0x5a: case 0x5b: case 0x62: case 0x70: case 0x71:
+                    f = F_ESCAPE; break;             // simulator control / host files
+                default: v = 0; break;               // no architectural effect: result 0
+                }
+                break;
+            }
+            case OP_crypto: v = rvk::exec(d.imm, a, b); break;
             default: f = F_UNKNOWN; break;
             }
         }
-        if (detect) f = F_DETECT;   // the op does not execute
+        if (detect || xdet) f = F_DETECT;   // the op does not execute
         if (mine) {
         if (msz && f == F_NONE) {
             // one call site (an AMO reads, then writes, in a second pass): a
             // second inlined copy of mem_access puts the lane state in scratch
-            const uint64_t ea = (amo >= 0 || llsc) ? a : a + imm;
+            const uint64_t ea = cbo ? (a & ~63ULL) : (amo >= 0 || llsc) ? a : a + imm;
             uint64_t old = 0;
 #pragma unroll 1
             for (int pass = 0; pass < (amo >= 0 ? 2 : 1); pass++) {
@@ -2550,7 +2588,7 @@ __device__ __forceinline__ void trial_body() {
                 if (CX->record)   // an AMO reads, then writes; a failed SC touches nothing
                     rec_mem(CX, ea, msz, L.ninst, amo >= 0 ? 3u : llsc == 2 ? (t ? 2u : 0u) : (mst ? 2u : 1u));
                 if (mst || amo >= 0 || (llsc == 2 && t)) DC_INVAL(ea, msz);   // rewritten code: drop its cached decodes
-                if (llsc != 2 || t) L.data_b += amo >= 0 ? 2 * msz : msz;
+                if ((llsc != 2 || t) && cbo != 1) L.data_b += amo >= 0 ? 2 * msz : msz;
                 if (amo >= 0) v = msz == 4 ? sx32(old) : old;
                 else if (llsc == 2) v = t ? 0 : 1;   // rd = !success (amo.isa StoreCondExecute)
                 else if (!mst) {
@@ -2591,6 +2629,7 @@ __device__ __forceinline__ void trial_body() {
             }
             if (wrd && d.rd) RREG(d.rd) = v;
             if (wrd && L.watch > 0 && (d.flags & kPreRd) && d.rd == L.watch) L.watch = -1;
+            if (m5) { RREG(11) = 0; if (L.watch == 11) L.watch = -1; }
             L.ninst++;
             if (rdet) finish(L, FI_DETECTED, 0, 0, (uint32_t)pc);   // the shadow disagrees at commit
             else L.pc = npc;
@@ -2619,6 +2658,7 @@ __device__ __forceinline__ void trial_body() {
         case F_DETECT: finish(L, FI_DETECTED, 0, 0, (uint32_t)pc); break;
         case F_AMOLINE: finish(L, FI_CRASH, FI_CRASH_AMO_LINE, 134, (uint32_t)pc); break;
         case F_SCLINE: finish(L, FI_CRASH, FI_CRASH_SC_LINE, 134, (uint32_t)pc); break;
+        case F_M5PANIC: finish(L, FI_CRASH, FI_CRASH_M5_PANIC, 134, (uint32_t)pc); break;
         case F_PGFAULT: {   // GenericPageTableFault::invoke -> fixupFault (sim/faults.cc:95-105)
             int h;
             OOL(h = fixup_fault(CX, mc_, slot, fva));

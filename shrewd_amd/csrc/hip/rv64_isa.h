@@ -44,7 +44,8 @@
     X(amoadd_d) X(amoswap_d) X(amoxor_d) X(amoor_d) X(amoand_d) X(amomin_d) X(amomax_d) X(amominu_d) X(amomaxu_d) \
     X(lr_w) X(sc_w) X(lr_d) X(sc_d) \
     X(fadd) X(fsub) X(fmul) X(fdiv) X(fsqrt) X(fmin) X(fmax) X(fmadd) X(fmsub) X(fnmsub) X(fnmadd) \
-    X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f)
+    X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f) \
+    X(priv) X(cbo) X(m5op) X(crypto)
 
 namespace fi {
 
@@ -496,12 +497,60 @@ __device__ inline void rv_refine_fp_amo(uint32_t raw, Dec &d) {
     if (f7 == 0x7a && rs2 == 0) { d.op = OP_fmv_h_x; d.rd = (uint8_t)rd; D_RS1(rs1); return; }
 }
 
+// The gem5-known members of the privileged SYSTEM, hypervisor load/store,
+// cache-block, M5 pseudo-op and scalar-crypto groups (oracle/rv64se.c:
+// refine_misc, which cites the reference): priv imm 0 = IllegalInst in PRV_U,
+// 1 = warn-only no-op; cbo imm = FUNCT12; m5op imm = M5FUNC, rd = a0;
+// crypto imm = function | RNUM / BS << 8 (fi_crypto.h).
+__device__ inline void rv_refine_misc(uint32_t raw, Dec &d) {
+    const uint32_t f3 = fbits(raw, 14, 12), f7 = fbits(raw, 31, 25);
+    const uint32_t rd = fbits(raw, 11, 7), rs1 = fbits(raw, 19, 15), rs2 = fbits(raw, 24, 20);
+    switch (d.op) {
+    case OP_ESC_SYS:
+        d.op = OP_priv;
+        d.imm = (f7 == 0x0b || f7 == 0x0c || f7 == 0x13 || f7 == 0x33) ? 1 : 0;
+        if (f7 == 0x09 || f7 == 0x11 || f7 == 0x31) { D_RS1(rs1); D_RS2(rs2); }
+        return;
+    case OP_ESC_HYP:
+        d.op = OP_priv; d.imm = 0; D_RS1(rs1);
+        if (f7 & 1) D_RS2(rs2);
+        return;
+    case OP_ESC_CBO: d.op = OP_cbo; D_RS1(rs1); d.imm = (int32_t)fbits(raw, 31, 20); return;
+    case OP_ESC_M5: d.op = OP_m5op; D_RD(10); d.imm = (int32_t)f7; return;
+    case OP_ESC_CRYPTO: {
+        const uint32_t opc = fbits(raw, 6, 2), kf5 = fbits(raw, 29, 25), bs = fbits(raw, 31, 30);
+        int fn = -1;
+        if (opc == 0x04 && f3 == 1) {
+            if (fbits(raw, 31, 27) == 0x02) fn = (int)rs2;
+            else fn = fbits(raw, 24, 24) ? (int)(11 | (fbits(raw, 23, 20) << 8)) : 10;
+        } else if (opc == 0x04) {
+            fn = 12;
+        } else if (opc == 0x0c && f3 == 0) {
+            if (kf5 == 0x18) fn = (int)(13 | (bs << 8));
+            else if (kf5 == 0x1a) fn = (int)(14 | (bs << 8));
+            else if (kf5 == 0x19) fn = 15;
+            else if (kf5 == 0x1b) fn = 16;
+            else if (kf5 == 0x1d) fn = 17;
+            else if (kf5 == 0x1f) fn = bs ? 19 : 18;
+        } else if (opc == 0x0c) {
+            fn = f3 == 2 ? 20 : 21;
+        }
+        if (fn < 0) return;
+        d.op = OP_crypto; d.imm = fn; D_RD(rd); D_RS1(rs1);
+        if ((fn & 0xFF) >= 13) D_RS2(rs2);
+        return;
+    }
+    default: return;
+    }
+}
+
 __device__ inline Dec rv_decode(uint32_t raw) {
     Dec d = rv_decode_tree(raw);
     if ((raw & 3) == 3 && (d.op == OP_ESC_FP || d.op == OP_ESC_VEC || d.op == OP_ESC_AMO ||
                            d.op == OP_ESC_SYS || d.op == OP_ESC_HYP) && !gem5_known(raw))
         d.op = OP_UNKNOWN;
     if ((raw & 3) == 3 && (d.op == OP_ESC_FP || d.op == OP_ESC_AMO)) rv_refine_fp_amo(raw, d);
+    if ((raw & 3) == 3) rv_refine_misc(raw, d);
     return d;
 }
 #undef D_RD

@@ -21,7 +21,8 @@ FI_OK, FI_E_ARG, FI_E_NODEVICE, FI_E_HIP, FI_E_ELF, FI_E_STATE, FI_E_GOLDEN = 0,
 CLASS_NAMES = ["masked", "sdc", "crash", "hang", "detected", "escape"]
 CRASH_NAMES = {1: "panic_unknown_inst", 2: "panic_illegal_inst", 3: "panic_page_fault",
                4: "fatal_syscall_range", 5: "fatal_syscall_unimpl", 6: "fatal_proxy", 7: "abort_fd_assert",
-               8: "sigtrap", 9: "fatal_stack_limit", 10: "panic_amo_line", 11: "abort_sc_line", 12: "panic_se_handler"}
+               8: "sigtrap", 9: "fatal_stack_limit", 10: "panic_amo_line", 11: "abort_sc_line", 12: "panic_se_handler",
+               13: "panic_m5op"}
 ESCAPE_NAMES = {1: "inst", 2: "syscall", 3: "csr", 4: "host", 5: "resource"}
 T_PC, T_MEM, T_RESULT, N_STRUCT = 32, 33, 34, 35
 
@@ -212,6 +213,7 @@ def lib():
         L.fi_get_config.argtypes = [vp, C.POINTER(_Config)]
         L.fi_debug_stats.argtypes = [vp, vp]
         L.fi_debug_softfp.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, vp, C.c_uint64, vp, vp, C.c_int]
+        L.fi_debug_crypto.argtypes = [C.c_int, vp, vp, C.c_uint64, vp, C.c_int]
         L.fi_kernel_timer_read.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]
         L.fi_debug_waves.argtypes = [vp, vp, C.c_uint64]
         L.fi_debug_epochs.argtypes = [vp, vp]
@@ -425,6 +427,46 @@ class Engine:
         return out
 
 
+def inst_group(raw: int) -> str:
+    """gem5 instruction group of an `escape/inst` outcome's raw word (its
+    `detail`): the opcode groups of src/arch/riscv/isa/decoder.isa that the
+    engine decodes exactly but does not execute."""
+    raw &= 0xFFFFFFFF
+    if raw & 3 != 3:
+        return "compressed"
+    opc, f3 = (raw >> 2) & 31, (raw >> 12) & 7
+    if opc == 0x15 or (opc in (0x01, 0x09) and f3 in (0, 5, 6, 7)):
+        return "vector"                          # OP-V; LOAD-FP / STORE-FP vector widths
+    if opc in (0x01, 0x09, 0x10, 0x11, 0x12, 0x13, 0x14):
+        return "fp"
+    if opc == 0x1e:
+        return "m5op"
+    if opc == 0x0b:
+        return "amo"
+    if opc == 0x1c:
+        return "system" if f3 == 0 else "hypervisor" if f3 == 4 else "csr"
+    if opc == 0x03:
+        return "cbo"
+    if opc in (0x04, 0x0c):
+        return "crypto"
+    return "other"
+
+
+def escape_breakdown(out: np.ndarray) -> dict:
+    """Escape outcomes by sub-code and, for escape/inst, by gem5 instruction
+    group ("inst:vector", ...); escape/syscall by number ("syscall:78")."""
+    esc = out[out["cls"] == 5]
+    res: dict[str, int] = {}
+    for sub, det in zip(esc["sub"].tolist(), esc["detail"].tolist()):
+        name = ESCAPE_NAMES.get(sub, str(sub))
+        if sub == 1:
+            name += ":" + inst_group(det)
+        elif sub == 2:
+            name += f":{det}"
+        res[name] = res.get(name, 0) + 1
+    return dict(sorted(res.items()))
+
+
 def shard_range(trials: int, world: int, rank: int) -> tuple[int, int]:
     """Contiguous trial-id block of `rank`: [r*T/G, (r+1)*T/G).
     Sites are counter-based on (seed, trial id), so any sharding runs the same
@@ -569,3 +611,16 @@ def softfp(op: int, fmt: int, rm: int, a, b=None, c=None, device: bool = False):
     if st != FI_OK:
         raise EngineError(f"fi_debug_softfp failed ({st})")
     return out, fl
+
+
+def crypto(fn: int, a, b=None, device: bool = False):
+    """The engine's scalar-crypto port (csrc/hip/fi_crypto.h) over operand
+    vectors, on the host or on the device -> results (function numbers as in
+    fi_crypto.h, RNUM / BS in bits 8+)."""
+    a = np.ascontiguousarray(a, np.uint64)
+    b = np.ascontiguousarray(a if b is None else b, np.uint64)
+    out = np.zeros(len(a), np.uint64)
+    st = lib().fi_debug_crypto(fn, a.ctypes.data, b.ctypes.data, len(a), out.ctypes.data, 1 if device else 0)
+    if st != FI_OK:
+        raise EngineError(f"fi_debug_crypto failed ({st})")
+    return out

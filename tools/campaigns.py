@@ -28,7 +28,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from shrewd_amd import Engine  # noqa: E402
-from shrewd_amd.fi import CLASS_NAMES, CRASH_NAMES, ESCAPE_NAMES  # noqa: E402
+from shrewd_amd.fi import CLASS_NAMES, CRASH_NAMES, ESCAPE_NAMES, escape_breakdown  # noqa: E402
 
 REGS = (1 << 32) - 2
 PC = 1 << 32
@@ -85,6 +85,7 @@ def run(cfg, name, n, structs, burst=1, protect=0, seed=0x5EED0003, opc=0, fu=No
            "crash_sub": {CRASH_NAMES.get(i, str(i)): int(h["crash_sub"][i]) for i in range(16) if h["crash_sub"][i]},
            "escape_sub": {ESCAPE_NAMES.get(i, str(i)): int(h["escape_sub"][i]) for i in range(8)
                           if h["escape_sub"][i]},
+           "escapes": escape_breakdown(out),
            "sdc_rate": int(cls[1]) / n, **extra}
     print(json.dumps(rec), flush=True)
     return rec, out

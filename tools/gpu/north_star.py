@@ -1,6 +1,6 @@
 """The north-star campaign on one GPU: >= 1M seeded single-bit register/PC
 trials of the intmix (C3) workload, timed end to end, with a seeded sample of
-10k trials re-run on the CPU oracle and compared bit for bit.
+100k trials re-run on the CPU oracle and compared bit for bit.
 
 python tools/gpu/north_star.py [N] [SEED] [CHECK]  -> one JSON line"""
 import json
@@ -12,11 +12,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 from shrewd_amd import Engine  # noqa: E402
+from shrewd_amd.fi import escape_breakdown  # noqa: E402
 
 REGS_PC = ((1 << 32) - 2) | (1 << 32)
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 SEED = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0x5EED0003
-CHECK = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000
+CHECK = int(sys.argv[3]) if len(sys.argv) > 3 else 100_000
 # trials per launch: the whole campaign in one launch by default (1M trials x
 # 16 private pages = 65 GiB of copy-on-write frames, well inside 288 GB of
 # HBM): one campaign tail instead of one per chunk
@@ -34,7 +35,7 @@ wall = time.perf_counter() - t0
 cls = np.bincount(out["cls"], minlength=6).tolist()
 rec = {"workload": name, "trials": N, "trials_per_launch": PER_LAUNCH, "seed": hex(SEED), "golden_ninst": int(g.ninst),
        "wall_s": round(wall, 3),
-       "trials_per_s": round(N / wall), "classes": cls, "device_insts": int(h["device_insts"]),
+       "trials_per_s": round(N / wall), "classes": cls, "escapes": escape_breakdown(out), "device_insts": int(h["device_insts"]),
        "guest_insts_gem5_equiv": int(out["ninst"].astype(np.uint64).sum())}
 print(json.dumps(rec), flush=True)
 # oracle check on a seeded sample (checker only)

@@ -77,7 +77,16 @@ def main():
                    "fle": [f"fle{v}_{f}" for v in ("", "q") for f in fm],
                    "fcvt_f2i": [f"fcvt_{i}_{f}" for i in ik for f in fm],
                    "fcvt_i2f": [f"fcvt_{f}_{i}" for i in ik for f in fm],
-                   "fcvt_f2f": [f"fcvt_{a}_{b}" for a in fm for b in fm if a != b]})
+                   "fcvt_f2f": [f"fcvt_{a}_{b}" for a in fm for b in fm if a != b],
+                   # the privileged SYSTEM members that commit (the warn-only no-ops);
+                   # the others raise IllegalInst before committing anything
+                   "priv": ["sinval_vvma", "sfence_w_inval", "sfence_inval_ir", "hinval_vvma", "hinval_gvma"],
+                   "cbo": [f"cbo_{k}" for k in ("inval", "clean", "flush", "zero")],
+                   "m5op": ["M5Op"],
+                   "crypto": [f"sha256{k}" for k in ("sum0", "sum1", "sig0", "sig1")] +
+                             [f"sha512{k}" for k in ("sum0", "sum1", "sig0", "sig1")] +
+                             ["sm3p0", "sm3p1", "aes64im", "aes64ks1i", "brev8", "sm4ed", "sm4ks", "aes64es",
+                              "aes64esm", "aes64ds", "aes64dsm", "aes64ks2", "xperm4", "xperm8"]})
     for op in engine_ops():
         base = op.rstrip("_")
         if op in groups:
