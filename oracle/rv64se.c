@@ -58,7 +58,8 @@ extern __thread uint_fast8_t softfloat_roundingMode, softfloat_exceptionFlags;
     bool p##_eq(T, T); bool p##_lt(T, T); bool p##_le(T, T); bool p##_lt_quiet(T, T); bool p##_le_quiet(T, T); \
     int_fast32_t p##_to_i32(T, uint_fast8_t, bool); uint_fast32_t p##_to_ui32(T, uint_fast8_t, bool);        \
     int_fast64_t p##_to_i64(T, uint_fast8_t, bool); uint_fast64_t p##_to_ui64(T, uint_fast8_t, bool);        \
-    T i32_to_##p(int32_t); T ui32_to_##p(uint32_t); T i64_to_##p(int64_t); T ui64_to_##p(uint64_t);
+    T i32_to_##p(int32_t); T ui32_to_##p(uint32_t); T i64_to_##p(int64_t); T ui64_to_##p(uint64_t);          \
+    T p##_roundToInt(T, uint_fast8_t, bool);
 SF_DECL(sf16_t, f16)
 SF_DECL(sf32_t, f32)
 SF_DECL(sf64_t, f64)
@@ -78,6 +79,7 @@ sf16_t f64_to_f16(sf64_t); sf32_t f64_to_f32(sf64_t);
         case 13: return (u64)p##_to_i64(x, rm, true); case 14: return (u64)p##_to_ui64(x, rm, true);           \
         case 15: return i32_to_##p((int32_t)a).v; case 16: return ui32_to_##p((uint32_t)a).v;                  \
         case 17: return i64_to_##p((int64_t)a).v; case 18: return ui64_to_##p(a).v;                           \
+        case 22: return p##_roundToInt(x, rm, false).v; case 23: return p##_roundToInt(x, rm, true).v;         \
         default: return 0;                                                                                     \
         }                                                                                                      \
     }
@@ -90,7 +92,7 @@ static u64 sf_ref(int op, int fmt, int rm, u64 a, u64 b, u64 c, uint32_t *fl) {
     softfloat_roundingMode = (uint_fast8_t)rm;
     softfloat_exceptionFlags = 0;
     u64 r;
-    if (op >= 19) {   /* conversions between formats */
+    if (op >= 19 && op <= 21) {   /* conversions between formats */
         const int to = op - 19;
         if (fmt == to) r = a;
         else if (fmt == 0) r = to == 1 ? f16_to_f32((sf16_t){(uint16_t)a}).v : f16_to_f64((sf16_t){(uint16_t)a}).v;
@@ -295,7 +297,7 @@ enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_E
     X(lr_w) X(sc_w) X(lr_d) X(sc_d) \
     X(fadd) X(fsub) X(fmul) X(fdiv) X(fsqrt) X(fmin) X(fmax) X(fmadd) X(fmsub) X(fnmsub) X(fnmadd) \
     X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f) \
-    X(priv) X(cbo) X(m5op) X(crypto)
+    X(priv) X(cbo) X(m5op) X(crypto) X(fli) X(fround) X(fcvtmod)
 
 enum {
 #define X(n) OP_##n,
@@ -469,6 +471,10 @@ static int refine_fp_arith(u32 raw, dec_t *d) {
         d->imm = f3 | ((u32)fmt << 3) | ((u32)sub << 5);
         return 1;
     case 0x18:
+        if (rs2 == 8 && fmt == 2) {   /* Zfa fcvtmod.w.d (decoder.isa:3320) */
+            d->op = OP_fcvtmod; d->rd = rd; d->frs1 = rs1; d->imm = f3 | (2u << 3);
+            return 1;
+        }
         if (rs2 > 3) return 0;
         d->op = OP_fcvt_f2i; d->rd = rd; d->frs1 = rs1;
         d->imm = f3 | ((u32)fmt << 3) | ((u32)rs2 << 5);
@@ -479,6 +485,11 @@ static int refine_fp_arith(u32 raw, dec_t *d) {
         d->imm = f3 | ((u32)fmt << 3) | ((u32)rs2 << 5);
         return 1;
     case 0x08: {
+        if (rs2 == 4 || rs2 == 5) {   /* Zfa fround / froundnx (decoder.isa:3105-3170) */
+            d->op = OP_fround; d->frd = rd; d->frs1 = rs1;
+            d->imm = f3 | ((u32)fmt << 3) | ((u32)(rs2 == 5) << 5);
+            return 1;
+        }
         const int src = fp_fmt((u32)rs2);
         if (rs2 > 2 || src < 0 || src == fmt) return 0;
         d->op = OP_fcvt_f2f; d->frd = rd; d->frs1 = rs1;
@@ -534,6 +545,11 @@ static void refine_fp_amo(u32 raw, dec_t *d) {
     if (f7 == 0x71 && f3 == 0 && rs2 == 0) { d->op = OP_fmv_x_d; d->rd = rd; d->frs1 = rs1; return; }
     if (f7 == 0x72 && f3 <= 1) { d->op = f3 ? OP_fclass_h : OP_fmv_x_h; d->rd = rd; d->frs1 = rs1; return; }
     if (f7 == 0x78 && f3 == 0 && rs2 == 0) { d->op = OP_fmv_w_x; d->frd = rd; d->rs1 = rs1; return; }
+    /* Zfa fli.s / fli.d / fli.h (decoder.isa:3550,3600,3653): rs1 is the table index */
+    if ((f7 == 0x78 && f3 == 0 && rs2 == 1) || ((f7 == 0x79 || f7 == 0x7a) && rs2 == 1)) {
+        d->op = OP_fli; d->frd = rd; d->imm = ((u32)rs1 << 8) | ((u32)(f7 == 0x78 ? 1 : f7 == 0x79 ? 2 : 0) << 3);
+        return;
+    }
     if (f7 == 0x79 && rs2 == 0) { d->op = OP_fmv_d_x; d->frd = rd; d->rs1 = rs1; return; }
     if (f7 == 0x7a && rs2 == 0) { d->op = OP_fmv_h_x; d->frd = rd; d->rs1 = rs1; return; }
 }
@@ -902,6 +918,13 @@ const char *or_mnemonic(u32 inst) {
         return d.imm <= 4 ? cn[d.imm] : "?";
     }
     if (d.op == OP_m5op) return "M5Op";
+    if (d.op == OP_fli || d.op == OP_fround || d.op == OP_fcvtmod) {
+        static const char *fs[3] = {"h", "s", "d"};
+        const int fmt = (int)((d.imm >> 3) & 3);
+        if (d.op == OP_fcvtmod) return "fcvtmod_w_d";
+        snprintf(buf, sizeof buf, "%s_%s", d.op == OP_fli ? "fli" : (d.imm >> 5) & 1 ? "froundnx" : "fround", fs[fmt]);
+        return buf;
+    }
     if (d.op == OP_crypto) return crypto_names[d.imm & 0xFF];
     const char *n = op_names[d.op];
     size_t l = strlen(n);
@@ -1561,6 +1584,55 @@ static int sc_write(mach_t *m, u64 addr, unsigned size, u64 val, int *ok, u64 *f
     return F_NONE;
 }
 
+/* Zfa fli: table entry i of format fmt (0 binary16, 1 binary32, 2 binary64).
+ * The Zfa list: -1.0, the minimum positive normal, 2^-16, 2^-15, 2^-8, 2^-7,
+ * 2^-4, 2^-3, 0.25 .. 0.4375, 0.5 .. 0.875, 1.0 .. 1.75 (steps of 1/4 of the
+ * binade), 2.0, 2.5, 3, 4, 8, 16, 2^7, 2^8, 2^15, 2^16, +inf and the
+ * canonical NaN; a value beyond the format's range rounds to +inf (binary16
+ * 2^16) and one below its normal range is encoded subnormal. */
+static u64 fli_bits(int fmt, u32 i) {
+    const int mb = fmt == 0 ? 10 : fmt == 1 ? 23 : 52, eb = fmt == 0 ? 5 : fmt == 1 ? 8 : 11;
+    const int bias = (1 << (eb - 1)) - 1, emax = (1 << eb) - 1;
+    if (i == 30) return (u64)emax << mb;
+    if (i == 31) return ((u64)emax << mb) | (1ULL << (mb - 1));
+    if (i == 1) return 1ULL << mb;
+    static const signed char e2[8] = {-16, -15, -8, -7, -4, -3};
+    static const signed char big[8] = {0, 2, 3, 4, 7, 8, 15, 16};   /* i = 22..29: 3, then powers of two */
+    u64 num = 1; int e = 0, neg = 0;
+    if (i == 0) neg = 1;
+    else if (i < 8) e = e2[i - 2];
+    else if (i < 22) { num = 4 + (i - 8) % 4; e = (int)((i - 8) / 4) - 4; }
+    else if (i == 22) num = 3;
+    else e = big[i - 22];
+    const int t = num >= 4 ? 2 : num >= 2 ? 1 : 0;
+    const int be = e + t + bias;
+    u64 r;
+    if (be >= emax) r = (u64)emax << mb;
+    else if (be <= 0) r = num << (e + bias - 1 + mb);
+    else r = ((u64)be << mb) | ((num << (mb - t)) & ((1ULL << mb) - 1));
+    return neg ? r | (1ULL << (eb + mb)) : r;
+}
+/* Zfa fcvtmod.w.d, decoder.isa:3320-3384 */
+static u64 fcvtmod_w_d(u64 a, uint32_t *fl) {
+    const int sign = (int)(a >> 63), ex = (int)((a >> 52) & 0x7FF);
+    u64 frac = a & ((1ULL << 52) - 1);
+    int inexact = 0, invalid = 0;
+    if (ex == 0) { inexact = frac != 0; frac = 0; }
+    else if (ex == 0x7FF) { invalid = 1; frac = 0; }
+    else {
+        const int true_exp = ex - 1023, shift = true_exp - 52;
+        frac |= 1ULL << 52;
+        if (shift >= 64) frac = 0;
+        else if (shift >= 0) frac <<= shift;
+        else if (shift > -64) { inexact = (frac << (64 + shift)) != 0; frac >>= -shift; }
+        else { frac = 0; inexact = 1; }
+        if (true_exp > 31 || frac > (sign ? 0x80000000ULL : 0x7fffffffULL)) { invalid = 1; inexact = 0; }
+        if (sign) frac = -frac;
+    }
+    *fl = (inexact ? 1u : 0u) | (invalid ? 16u : 0u);
+    return (u64)(s64)(int32_t)(u32)frac;
+}
+
 /* Execute one decoded instruction (the generated StaticInst::execute bodies of
  * decoder.isa).  Returns a fault kind; on F_NONE the caller commits npc. */
 static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
@@ -1885,6 +1957,44 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
         v = ok ? 0 : 1;   /* result = !success (amo.isa StoreCondExecute) */
         break;
     }
+    /* ---- Zfa.  fli: the value the 5-bit rs1 field selects from the table the
+     * Zfa specification lists (decoder.isa:3550-3700; pinned by
+     * tests/golden/fli_rv64.json); no rounding mode, no flags. */
+    case OP_fli: {
+        const int fmt = (int)((imm >> 3) & 3);
+        const u64 x = fli_bits(fmt, (u32)(imm >> 8) & 31);
+        m->f[d->frd] = fmt == 0 ? box16(x) : fmt == 1 ? box32(x) : x;
+        goto no_rd;
+    }
+    /* fcvtmod.w.d: RM_REQUIRED (fp_inst.hh:34-41), then the modular
+     * truncation of decoder.isa:3320-3384 (flags through FFLAGS_EXE) */
+    case OP_fcvtmod: {
+        int rm = (int)(imm & 7);
+        if (rm == 7) rm = (int)m->frm;
+        if (rm > 4) return F_ILLEGAL;
+        uint32_t fl = 0;
+        v = fcvtmod_w_d(m->f[d->frs1], &fl);
+        m->fflags |= fl;
+        break;
+    }
+#ifdef OR_SOFTFLOAT
+    /* fround / froundnx: RM_REQUIRED, then f*_roundToInt(fs1, rm, exact) of
+     * the reference SoftFloat (decoder.isa:3105-3170) */
+    case OP_fround: {
+        const int fmt = (int)((imm >> 3) & 3);
+        int rm = (int)(imm & 7);
+        if (rm == 7) rm = (int)m->frm;
+        if (rm > 4) return F_ILLEGAL;
+        uint32_t fl = 0;
+        const u64 x = fmt == 0 ? unbox16(m->f[d->frs1]) : fmt == 1 ? unbox32(m->f[d->frs1]) : m->f[d->frs1];
+        const u64 r2 = sf_ref(22 + (int)((imm >> 5) & 1), fmt, rm, x, 0, 0, &fl);
+        m->fflags |= fl & 0x1F;
+        m->f[d->frd] = fmt == 0 ? box16(r2) : fmt == 1 ? box32(r2) : r2;
+        goto no_rd;
+    }
+#else
+    case OP_fround: return F_ESCAPE;
+#endif
     /* ---- privileged SYSTEM / hypervisor load-store from PRV_U (refine_misc) */
     case OP_priv:
         if (!imm) return F_ILLEGAL;
@@ -2763,6 +2873,7 @@ int or_probe(u32 inst, u64 pc, const u64 regs[32], or_probe_t *o) {
                f == F_UNKNOWN ? 4 : f == F_PGFAULT ? 6 : 5;
     o->rd = d.rd;
     o->rd_value = d.rd > 0 ? m.x[d.rd] : 0;
+    if (d.rd < 0 && d.frd >= 0) { o->rd = 32 + d.frd; o->rd_value = m.f[d.frd]; }   /* FP destination: 32 + f */
     o->npc = m.npc;
     o->len = d.len;
     o->op = (u32)d.op;

@@ -159,7 +159,7 @@ int or_run_one_capture(or_campaign_t *c, const or_site_t *site, uint64_t protect
 typedef struct {
     uint64_t rd_value, npc;
     int32_t fault;      /* 0 none, 1 syscall, 2 breakpoint, 3 illegal, 4 unknown, 5 escape, 6 pagefault */
-    int32_t rd;         /* destination register written, -1 none */
+    int32_t rd;         /* destination register written, -1 none (32 + f for an FP destination) */
     uint32_t len;
     uint32_t op;        /* oracle-internal op id */
 } or_probe_t;

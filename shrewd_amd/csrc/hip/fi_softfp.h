@@ -386,6 +386,86 @@ template <class FS, class FD> FI_SF_HD uint64_t convert(uint64_t a, int rm, uint
     return round_pack<FD>(neg, e, m, rm, fl);
 }
 
+// roundToInt (Zfa fround / froundnx): the integral value nearest to a in
+// rounding mode rm, in a's format; exact = raise inexact when it differs.
+// NaN -> canonical NaN (invalid if signalling); zeros, infinities and values
+// of magnitude >= 2^mb are returned as they are; a zero result keeps a's sign.
+template <class F> FI_SF_HD uint64_t rint(uint64_t a, int rm, bool exact, uint32_t &fl) {
+    if (is_nan<F>(a)) { if (is_snan<F>(a)) fl |= FL_NV; return F::qnan; }
+    if (is_inf<F>(a) || is_zero<F>(a)) return a;
+    const bool neg = (a & F::sign) != 0;
+    int e;
+    uint64_t m;
+    unpack<F>(a, e, m);
+    if (e >= F::mb) return a;
+    const int sh = 62 - e;   // > 62 - mb
+    uint64_t ip, fr;
+    if (sh >= 128) { ip = 0; fr = 1; }
+    else {
+        const u128 x = srj128((u128)m << 64, sh);
+        ip = (uint64_t)(x >> 64);
+        fr = (uint64_t)x;
+    }
+    if (round_up(rm, neg, ip, fr, 1ULL << 63)) ip++;
+    if (fr && exact) fl |= FL_NX;
+    const uint64_t sgn = neg ? F::sign : 0;
+    if (!ip) return sgn;
+    const int t = 63 - clz64(ip);   // <= mb: exactly representable
+    return sgn | ((uint64_t)(t + F::bias) << F::mb) | ((ip << (F::mb - t)) & F::frac);
+}
+
+// fli (Zfa; decoder.isa:3550-3700): entry i of the Zfa constant list in
+// format F: -1, the minimum positive normal, 2^-16, 2^-15, 2^-8, 2^-7, 2^-4,
+// 2^-3, then n/16, n/8, n/4 (n = 4..7), 2, 2.5, 3, 4, 8, 16, 2^7, 2^8, 2^15,
+// 2^16, +inf, NaN; out-of-range values are +inf, tiny ones subnormal.
+template <class F> FI_SF_HD uint64_t fli(uint32_t i) {
+    if (i == 30) return F::inf;
+    if (i == 31) return F::qnan;
+    if (i == 1) return 1ULL << F::mb;
+    uint64_t num = 1;
+    int e = 0;
+    if (i >= 2 && i < 8) { const int t = (int)(i - 2); e = t < 2 ? -16 + t : t < 4 ? -8 + (t - 2) : -4 + (t - 4); }
+    else if (i >= 8 && i < 22) { num = 4 + (i - 8) % 4; e = (int)((i - 8) / 4) - 4; }
+    else if (i == 22) num = 3;
+    else if (i > 22) { const int t = (int)(i - 23); e = t < 3 ? t + 2 : t < 5 ? t + 4 : t + 10; }
+    const int t = num >= 4 ? 2 : num >= 2 ? 1 : 0;
+    const int be = e + t + F::bias;
+    uint64_t r;
+    if (be >= F::emax_b) r = F::inf;
+    else if (be <= 0) r = num << (e + F::bias - 1 + F::mb);
+    else r = ((uint64_t)be << F::mb) | ((num << (F::mb - t)) & F::frac);
+    return i == 0 ? r | F::sign : r;
+}
+
+// fcvtmod.w.d (Zfa; decoder.isa:3320-3384): the binary64 value truncated to an
+// integer, taken modulo 2^32 and sign-extended from bit 31; inexact when bits
+// are dropped, invalid (instead of inexact) for NaN, infinity or a magnitude
+// outside the int32 range.
+FI_SF_HD uint64_t fcvtmod_w_d(uint64_t a, uint32_t &fl) {
+    const bool neg = (a >> 63) != 0;
+    const int ex = (int)((a >> 52) & 0x7FF);
+    uint64_t frac = a & D::frac;
+    bool inexact = false, invalid = false;
+    if (ex == 0) {
+        inexact = frac != 0;
+        frac = 0;
+    } else if (ex == 0x7FF) {
+        invalid = true;
+        frac = 0;
+    } else {
+        const int true_exp = ex - 1023, shift = true_exp - 52;
+        frac |= 1ULL << 52;
+        if (shift >= 64) frac = 0;
+        else if (shift >= 0) frac <<= shift;
+        else if (shift > -64) { inexact = (frac << (64 + shift)) != 0; frac >>= -shift; }
+        else { frac = 0; inexact = true; }
+        if (true_exp > 31 || frac > (neg ? 0x80000000ULL : 0x7FFFFFFFULL)) { invalid = true; inexact = false; }
+        if (neg) frac = 0 - frac;
+    }
+    fl |= (inexact ? FL_NX : 0) | (invalid ? FL_NV : 0);
+    return (uint64_t)(int64_t)(int32_t)(uint32_t)frac;
+}
+
 }  // namespace sf
 }  // namespace fi
 
@@ -396,10 +476,11 @@ namespace sf {
 // 7 lt, 8 le, 9 lt_quiet, 10 le_quiet, 11..14 to i32/u32/i64/u64 (result as
 // the reference returns it: i32 sign-extended, u32 zero-extended), 15..18
 // from i32/u32/i64/u64, 19..21 convert to binary16/32/64; fmt 0 binary16,
-// 1 binary32, 2 binary64 (the source format of a conversion).
+// 1 binary32, 2 binary64 (the source format of a conversion); 22, 23
+// roundToInt without / with the inexact flag (Zfa fround / froundnx).
 enum : int { OP_ADD = 0, OP_SUB, OP_MUL, OP_DIV, OP_SQRT, OP_FMA, OP_EQ, OP_LT, OP_LE, OP_LTQ, OP_LEQ,
              OP_TO_I32, OP_TO_U32, OP_TO_I64, OP_TO_U64, OP_FROM_I32, OP_FROM_U32, OP_FROM_I64, OP_FROM_U64,
-             OP_TO_H, OP_TO_S, OP_TO_D, OP_COUNT };
+             OP_TO_H, OP_TO_S, OP_TO_D, OP_RINT, OP_RINTX, OP_COUNT };
 
 template <class F> FI_SF_HD uint64_t op_fmt(int op, int rm, uint64_t a, uint64_t b, uint64_t c, uint32_t &fl) {
     switch (op) {
@@ -417,6 +498,7 @@ template <class F> FI_SF_HD uint64_t op_fmt(int op, int rm, uint64_t a, uint64_t
     case OP_TO_I32: case OP_TO_U32: case OP_TO_I64: case OP_TO_U64: return to_int<F>(a, op - OP_TO_I32, rm, fl);
     case OP_FROM_I32: case OP_FROM_U32: case OP_FROM_I64: case OP_FROM_U64:
         return from_int<F>(a, op - OP_FROM_I32, rm, fl);
+    case OP_RINT: case OP_RINTX: return rint<F>(a, rm, op == OP_RINTX, fl);
     default: return 0;
     }
 }
@@ -428,7 +510,7 @@ template <class F> FI_SF_HD uint64_t cvt_from(int op, int rm, uint64_t a, uint32
     }
 }
 FI_SF_HD uint64_t op(int op, int fmt, int rm, uint64_t a, uint64_t b, uint64_t c, uint32_t &fl) {
-    if (op >= OP_TO_H) return fmt == 0 ? cvt_from<H>(op, rm, a, fl) : fmt == 1 ? cvt_from<S>(op, rm, a, fl)
+    if (op >= OP_TO_H && op <= OP_TO_D) return fmt == 0 ? cvt_from<H>(op, rm, a, fl) : fmt == 1 ? cvt_from<S>(op, rm, a, fl)
                                                                     : cvt_from<D>(op, rm, a, fl);
     return fmt == 0 ? op_fmt<H>(op, rm, a, b, c, fl) : fmt == 1 ? op_fmt<S>(op, rm, a, b, c, fl)
                                                      : op_fmt<D>(op, rm, a, b, c, fl);

@@ -672,7 +672,8 @@ __device__ __noinline__ FpRes fp_exec(uint32_t op, uint32_t imm, uint32_t rs2, u
     auto box = [](int f, uint64_t x) {
         return f == 0 ? (0xFFFFFFFFFFFF0000ULL | x) : f == 1 ? (0xFFFFFFFF00000000ULL | x) : x;
     };
-    const bool rounds = !(op == OP_fmin || op == OP_fmax || op == OP_feq || op == OP_flt || op == OP_fle);
+    const bool rounds = !(op == OP_fmin || op == OP_fmax || op == OP_feq || op == OP_flt || op == OP_fle ||
+                          op == OP_fli);
     if (op == OP_fsqrt && rs2 != 0) { o.kind = 2; return o; }   // "source reg x1"
     int rm = (int)(imm & 7);
     if (rounds) {
@@ -715,6 +716,13 @@ __device__ __noinline__ FpRes fp_exec(uint32_t op, uint32_t imm, uint32_t rs2, u
         o.kind = 1;
         break;
     case OP_fcvt_i2f: r = sf::op(sf::OP_FROM_I32 + sub, fmt, rm, ia, 0, 0, fl); break;
+    case OP_fli: {   // Zfa fli: table index in imm >> 8, no flags
+        const uint32_t i = (imm >> 8) & 31;
+        r = fmt == 0 ? sf::fli<sf::H>(i) : fmt == 1 ? sf::fli<sf::S>(i) : sf::fli<sf::D>(i);
+        break;
+    }
+    case OP_fround: r = sf::op((sub & 1) ? sf::OP_RINTX : sf::OP_RINT, fmt, rm, x, 0, 0, fl); break;
+    case OP_fcvtmod: o.v = sf::fcvtmod_w_d(x, fl); o.kind = 1; break;
     default: r = sf::op(sf::OP_TO_H + fmt, sub, rm, x, 0, 0, fl); break;   // between formats
     }
     o.fl = fl;
@@ -2499,7 +2507,7 @@ __device__ __forceinline__ void trial_body() {
             case OP_fclass_h: v = fp_classify(fp_unbox16(FREG_RD(d.rs1)), 5, 10); break;
             case OP_fadd: case OP_fsub: case OP_fmul: case OP_fdiv: case OP_fsqrt: case OP_fmadd: case OP_fmsub:
             case OP_fnmsub: case OP_fnmadd: case OP_fmin: case OP_fmax: case OP_feq: case OP_flt: case OP_fle:
-            case OP_fcvt_f2i: case OP_fcvt_i2f: case OP_fcvt_f2f: {
+            case OP_fcvt_f2i: case OP_fcvt_i2f: case OP_fcvt_f2f: case OP_fli: case OP_fround: case OP_fcvtmod: {
                 const uint32_t ui = (uint32_t)d.imm;
                 const FpRes fr = fp_exec(d.op, ui, d.rs2, FREG_RD(d.rs1), FREG_RD(d.rs2), FREG_RD((ui >> 8) & 31), a,
                                          L.frm);

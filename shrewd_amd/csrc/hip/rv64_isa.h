@@ -45,7 +45,7 @@
     X(lr_w) X(sc_w) X(lr_d) X(sc_d) \
     X(fadd) X(fsub) X(fmul) X(fdiv) X(fsqrt) X(fmin) X(fmax) X(fmadd) X(fmsub) X(fnmsub) X(fnmadd) \
     X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f) \
-    X(priv) X(cbo) X(m5op) X(crypto)
+    X(priv) X(cbo) X(m5op) X(crypto) X(fli) X(fround) X(fcvtmod)
 
 namespace fi {
 
@@ -423,6 +423,10 @@ __device__ inline bool rv_refine_fp_arith(uint32_t raw, Dec &d) {
         d.imm = (int32_t)(f3 | ((uint32_t)fmt << 3) | (sub << 5));
         return true;
     case 0x18:
+        if (rs2 == 8 && fmt == 2) {   // Zfa fcvtmod.w.d
+            d.op = OP_fcvtmod; D_RD(rd); d.rs1 = (uint8_t)rs1; d.imm = (int32_t)(f3 | (2u << 3));
+            return true;
+        }
         if (rs2 > 3) return false;
         d.op = OP_fcvt_f2i; D_RD(rd); d.rs1 = (uint8_t)rs1;
         d.imm = (int32_t)(f3 | ((uint32_t)fmt << 3) | (rs2 << 5));
@@ -433,6 +437,11 @@ __device__ inline bool rv_refine_fp_arith(uint32_t raw, Dec &d) {
         d.imm = (int32_t)(f3 | ((uint32_t)fmt << 3) | (rs2 << 5));
         return true;
     case 0x08: {
+        if (rs2 == 4 || rs2 == 5) {   // Zfa fround / froundnx
+            d.op = OP_fround; d.rd = (uint8_t)rd; d.rs1 = (uint8_t)rs1;
+            d.imm = (int32_t)(f3 | ((uint32_t)fmt << 3) | ((uint32_t)(rs2 == 5) << 5));
+            return true;
+        }
         const int src = fp_fmt_code(rs2);
         if (rs2 > 2 || src < 0 || src == fmt) return false;
         d.op = OP_fcvt_f2f; d.rd = (uint8_t)rd; d.rs1 = (uint8_t)rs1;
@@ -493,6 +502,11 @@ __device__ inline void rv_refine_fp_amo(uint32_t raw, Dec &d) {
     if (f7 == 0x71 && f3 == 0 && rs2 == 0) { d.op = OP_fmv_x_d; D_RD(rd); d.rs1 = (uint8_t)rs1; return; }
     if (f7 == 0x72 && f3 <= 1) { d.op = f3 ? OP_fclass_h : OP_fmv_x_h; D_RD(rd); d.rs1 = (uint8_t)rs1; return; }
     if (f7 == 0x78 && f3 == 0 && rs2 == 0) { d.op = OP_fmv_w_x; d.rd = (uint8_t)rd; D_RS1(rs1); return; }
+    if ((f7 == 0x78 && f3 == 0 && rs2 == 1) || ((f7 == 0x79 || f7 == 0x7a) && rs2 == 1)) {   // Zfa fli: rs1 = index
+        d.op = OP_fli; d.rd = (uint8_t)rd;
+        d.imm = (int32_t)((rs1 << 8) | ((uint32_t)(f7 == 0x78 ? 1 : f7 == 0x79 ? 2 : 0) << 3));
+        return;
+    }
     if (f7 == 0x79 && rs2 == 0) { d.op = OP_fmv_d_x; d.rd = (uint8_t)rd; D_RS1(rs1); return; }
     if (f7 == 0x7a && rs2 == 0) { d.op = OP_fmv_h_x; d.rd = (uint8_t)rd; D_RS1(rs1); return; }
 }

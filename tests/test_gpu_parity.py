@@ -423,7 +423,7 @@ def test_native_driver_matches_engine(engine_factory, tmp_path):
     assert hist["counts"].tobytes() == rh["counts"].tobytes()
 
 
-@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp", "rnd"])
+@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp", "rnd", "xop"])
 def test_known_answer_programs(oracle_mod, prog):
     """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
@@ -440,7 +440,9 @@ def test_known_answer_programs(oracle_mod, prog):
     uname / writev / close (the SE memory map).
     fp: F/D/Zfh arithmetic in every rounding mode with fflags, the dynamic
     rounding mode and fcsr (answers from the reference SoftFloat).
-    rnd: getrandom (gem5's mt19937_64 stream) and clock_gettime (curTick).  The device golden run (general interpreter)
+    rnd: getrandom (gem5's mt19937_64 stream) and clock_gettime (curTick).
+    xop: scalar crypto, Zfa (fli / fround / fcvtmod.w.d), M5 pseudo-ops, the
+    warn-only privileged no-ops and the cache-block ops.  The device golden run (general interpreter)
     must print exactly the reference-derived models; no-fault trials
     (pre-decoded and translated paths, from snapshots) must end masked with
     the oracle's records; faulted trials must match the oracle bit for bit."""
@@ -454,9 +456,12 @@ def test_known_answer_programs(oracle_mod, prog):
                      "lrsc": (kat.lrsc_program_elf, kat.lrsc_program_expected),
                      "vm": (kat.vm_program_elf, kat.vm_program_expected),
                      "fp": (kat.fp_program_elf, kat.fp_program_expected),
-                     "rnd": (kat.rnd_program_elf, kat.rnd_program_expected)}[prog]
-    if prog == "fp" and not oracle_mod.has_softfloat():
+                     "rnd": (kat.rnd_program_elf, kat.rnd_program_expected),
+                     "xop": (kat.xop_program_elf, kat.xop_program_expected)}[prog]
+    if prog in ("fp", "xop") and not oracle_mod.has_softfloat():
         pytest.skip("oracle without the reference SoftFloat")
+    if prog == "xop" and not oracle_mod.has_rvk():
+        pytest.skip("oracle without the reference rvk.hh")
     stderr = {"sys": kat.SYS_STDERR, "vm": kat.VM_STDERR}.get(prog, b"")
     elf, expected = elf(), expected()
     e = Engine(private_pages=64)

@@ -13,6 +13,7 @@ Each instruction runs through `or_probe` (one instruction in a scratch
 machine), the same entry the GPU parity tests use.
 """
 import itertools
+import json
 import os
 import random
 import sys
@@ -1356,3 +1357,176 @@ def rnd_program_expected() -> bytes:
     out = o.golden_stdout()
     rnd_check(out)
     return out
+
+
+# ---------------------------------------------------------------- xop program
+# The instruction groups gem5 executes outside the base ISA (oracle/rv64se.c
+# refine_misc, the Zfa ops): scalar crypto on operand pairs (answers from the
+# reference's rvk.hh through oracle/_ref), Zfa fli (the reference decoder's
+# tables, tests/golden/fli_rv64.json), fround / froundnx (the reference
+# SoftFloat's roundToInt) and fcvtmod.w.d (a model of decoder.isa:3320-3384),
+# M5 pseudo-ops under SE defaults (rpns = curTick() in ns, m5sum, initparam
+# keys, functions without an architectural effect; a1 = 0 after each), the
+# warn-only privileged no-ops, and cbo.zero / cbo.clean / cbo.flush /
+# cbo.inval on a 64-byte line.
+XOP_PAIRS = [(0x0123456789ABCDEF, 0xFEDCBA9876543210), (0, 0xFFFFFFFFFFFFFFFF), (0x8000000080000000, 0x7F),
+             (0xDEADBEEFCAFEBABE, 0x0F1E2D3C4B5A6978)]
+XOP_CRYPTO = [*range(0, 11), 11 | (0 << 8), 11 | (9 << 8), 11 | (0xA << 8), 11 | (0xF << 8), 12,
+              *[13 | (bs << 8) for bs in range(4)], *[14 | (bs << 8) for bs in range(4)], *range(15, 22)]
+XOP_FROUND = [0x3FF8000000000000, 0xC004000000000000, 0x4330000000000001, 0x3FE0000000000000,
+              0xBFE8000000000000, 0x7FF0000000000000, 0x7FF4000000000000, 0x0000000000000001]
+XOP_FCVTMOD = [0x41E0000000000000, 0xC1E0000000200000, 0x4340000000000001, 0x4540000000000005,
+               0x3FF8000000000000, 0xBFF0000000000000, 0x7FF8000000000000, 0x0000000000000003,
+               0x45B0000000000000, 0xC3F0000000012345]
+XOP_M5_NOEFFECT = [0x00, 0x09, 0x0D, 0x10, 0x11, 0x20, 0x31, 0x40, 0x41, 0x42, 0x50, 0x55, 0x59, 0x7F]
+XOP_RPNS_GAP = 40
+XOP_PRIV_NOPS = [0x16000073, 0x18000073, 0x18100073, 0x26000073, 0x66000073]
+
+
+def _crypto_word(fn, rd=7, rs1=5, rs2=6):
+    f, sub = fn & 0xFF, fn >> 8
+    if f <= 9:
+        return (0x08 << 25) | (f << 20) | (rs1 << 15) | (1 << 12) | (rd << 7) | 0x13
+    if f == 10:
+        return (0x18 << 25) | (rs1 << 15) | (1 << 12) | (rd << 7) | 0x13
+    if f == 11:
+        return (0x18 << 25) | (1 << 24) | (sub << 20) | (rs1 << 15) | (1 << 12) | (rd << 7) | 0x13
+    if f == 12:
+        return (0x34 << 25) | (7 << 20) | (rs1 << 15) | (5 << 12) | (rd << 7) | 0x13
+    f7 = {13: (sub << 5) | 0x18, 14: (sub << 5) | 0x1A, 15: 0x19, 16: 0x1B, 17: 0x1D, 18: 0x1F, 19: 0x3F,
+          20: 0x14, 21: 0x14}[f]
+    f3 = {20: 2, 21: 4}.get(f, 0)
+    return (f7 << 25) | (rs2 << 20) | (rs1 << 15) | (f3 << 12) | (rd << 7) | 0x33
+
+
+def _fcvtmod_model(a):
+    sign, ex, frac = a >> 63, (a >> 52) & 0x7FF, a & ((1 << 52) - 1)
+    inexact = invalid = False
+    if ex == 0:
+        inexact, frac = frac != 0, 0
+    elif ex == 0x7FF:
+        invalid, frac = True, 0
+    else:
+        te = ex - 1023
+        m = frac | (1 << 52)
+        sh = te - 52
+        if sh >= 0:
+            v = (m << sh) if sh < 64 else 0
+            v &= (1 << 64) - 1
+        else:
+            inexact = (m & ((1 << -sh) - 1)) != 0 if -sh < 64 else True
+            v = m >> -sh if -sh < 64 else 0
+        if te > 31 or v > (0x80000000 if sign else 0x7FFFFFFF):
+            invalid, inexact = True, False
+        frac = (-v) & ((1 << 64) - 1) if sign else v
+    r = frac & 0xFFFFFFFF
+    r = r | 0xFFFFFFFF00000000 if r & 0x80000000 else r
+    return r, (1 if inexact else 0) | (16 if invalid else 0)
+
+
+def xop_program_source() -> str:
+    L = ["    .text", "_start:", "    .word 0x0E00007B", "    mv    s4, a0"]      # rpns at tick 0
+    L += ["    addi  t3, t3, 1"] * (XOP_RPNS_GAP - 2)
+    L += ["    .word 0x0E00007B", "    mv    s5, a0", "    la    s2, out", "    mv    s3, s2",
+          "    sd    s4, 0(s2)", "    sd    s5, 8(s2)", "    addi  s2, s2, 16"]
+    # m5sum, initparam keys, functions without an effect (a0 / a1 after each)
+    L += [f"    li    a{k}, {0x1111 * (k + 1) + (1 << (60 - k))}" for k in range(6)]
+    L += ["    .word 0x4600007B", "    sd    a0, 0(s2)", "    sd    a1, 8(s2)", "    addi  s2, s2, 16"]
+    for k0, k1 in ((0, 0x55), (int.from_bytes(b"dist-ran", "little"), ord("k")),
+                   (int.from_bytes(b"dist-siz", "little"), ord("e"))):
+        L += [f"    li    a0, {k0}", f"    li    a1, {k1}", "    .word 0x6000007B", "    sd    a0, 0(s2)",
+              "    sd    a1, 8(s2)", "    addi  s2, s2, 16"]
+    for fn in XOP_M5_NOEFFECT:
+        L += ["    li    a0, -1", "    li    a1, -2", f"    .word {(fn << 25) | 0x7B:#x}", "    sd    a0, 0(s2)",
+              "    sd    a1, 8(s2)", "    addi  s2, s2, 16"]
+    L += [f"    .word {w:#x}" for w in XOP_PRIV_NOPS]
+    # scalar crypto
+    for a, b in XOP_PAIRS:
+        L += [f"    li    t0, {a}", f"    li    t1, {b}"]
+        for fn in XOP_CRYPTO:
+            L += [f"    .word {_crypto_word(fn):#x}", "    sd    t2, 0(s2)", "    addi  s2, s2, 8"]
+    # Zfa: fli in all three formats
+    for f7 in (0x78, 0x79, 0x7A):
+        for i in range(32):
+            L += [f"    .word {(f7 << 25) | (1 << 20) | (i << 15) | (0 << 7) | 0x53:#x}", "    fmv.x.d t2, f0",
+                  "    sd    t2, 0(s2)", "    addi  s2, s2, 8"]
+    # fround / froundnx (binary64, every static rounding mode), flags read and cleared
+    for x in XOP_FROUND:
+        L += [f"    li    t0, {x}", "    fmv.d.x f1, t0"]
+        for nx in (0, 1):
+            for rm in range(5):
+                L += [f"    .word {(0x21 << 25) | ((4 + nx) << 20) | (1 << 15) | (rm << 12) | 0x53:#x}",
+                      "    fmv.x.d t2, f0", "    csrrw t3, 1, zero", "    sd    t2, 0(s2)", "    sd    t3, 8(s2)",
+                      "    addi  s2, s2, 16"]
+    for x in XOP_FCVTMOD:
+        L += [f"    li    t0, {x}", "    fmv.d.x f1, t0",
+              f"    .word {(0x61 << 25) | (8 << 20) | (1 << 15) | (1 << 12) | (7 << 7) | 0x53:#x}",
+              "    csrrw t3, 1, zero", "    sd    t2, 0(s2)", "    sd    t3, 8(s2)", "    addi  s2, s2, 16"]
+    # cache-block ops on two 0xFF lines: zero the first (through an unaligned
+    # pointer), clean / flush / inval the second; then print both lines
+    L += ["    la    t0, lines", "    li    t1, -1", "    li    t4, 16"]
+    L += ["fill:", "    sd    t1, 0(t0)", "    addi  t0, t0, 8", "    addi  t4, t4, -1", "    bnez  t4, fill"]
+    L += ["    la    t0, lines", "    addi  t0, t0, 37", f"    .word {(4 << 20) | (5 << 15) | (2 << 12) | 0x0F:#x}",
+          "    addi  t0, t0, 64"]
+    L += [f"    .word {(k << 20) | (5 << 15) | (2 << 12) | 0x0F:#x}" for k in (0, 1, 2)]
+    L += ["    la    t0, lines", "    li    t4, 16"]
+    L += ["dump:", "    ld    t1, 0(t0)", "    sd    t1, 0(s2)", "    addi  s2, s2, 8", "    addi  t0, t0, 8",
+          "    addi  t4, t4, -1", "    bnez  t4, dump"]
+    L += ["    li    a0, 1", "    mv    a1, s3", "    sub   a2, s2, s3", "    li    a7, 64", "    ecall",
+          "    li    a0, 0", "    li    a7, 93", "    ecall",
+          "    .data", "    .balign 64", "lines:", "    .zero 128",
+          "    .bss", "    .balign 8", "out:", "    .zero 8192"]
+    return "\n".join(L) + "\n"
+
+
+def xop_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(xop_program_source(), compress=False)
+
+
+def xop_program_expected() -> bytes:
+    from oracle.pyoracle import rvk_ref, sf_ref
+    M = (1 << 64) - 1
+    vals = [0, XOP_RPNS_GAP * 500 // 1000]
+    sargs = [0x1111 * (k + 1) + (1 << (60 - k)) for k in range(6)]
+    vals += [sum(sargs) & M, 0]
+    vals += [0, 0, 0, 0, 1, 0]
+    for _ in XOP_M5_NOEFFECT:
+        vals += [0, 0]
+    for a, b in XOP_PAIRS:
+        for fn in XOP_CRYPTO:
+            vals.append(int(rvk_ref(fn, [a], [b])[0]))
+    fli = json.load(open(os.path.join(ROOT, "tests", "golden", "fli_rv64.json")))
+    for f, box in (("s", 0xFFFFFFFF00000000), ("d", 0), ("h", 0xFFFFFFFFFFFF0000)):
+        vals += [v | box for v in fli[f]]
+    for x in XOP_FROUND:
+        for nx in (0, 1):
+            for rm in range(5):
+                v, fl = sf_ref(22 + nx, 2, rm, [x])
+                vals += [int(v[0]), int(fl[0])]
+    for x in XOP_FCVTMOD:
+        vals += list(_fcvtmod_model(x))
+    lines = [0] * 8 + [M] * 8
+    vals += lines
+    return b"".join((v & M).to_bytes(8, "little") for v in vals)
+
+
+def test_xop_program_on_oracle(oracle_mod):
+    from oracle.pyoracle import has_rvk, has_softfloat
+    if not (has_softfloat() and has_rvk()):
+        pytest.skip("oracle without the reference SoftFloat / rvk.hh")
+    o = oracle_mod.Oracle(xop_program_elf(), "xop")
+    g = o.run_golden()
+    assert g.exit_code == 0, g
+    got, exp = o.golden_stdout(), xop_program_expected()
+    assert len(got) == len(exp)
+    for k in range(0, len(exp), 8):
+        assert got[k:k + 8] == exp[k:k + 8], (k // 8, got[k:k + 8].hex(), exp[k:k + 8].hex())
+
+
+def test_fli_probe_matches_reference_table(oracle_mod):
+    fli = json.load(open(os.path.join(ROOT, "tests", "golden", "fli_rv64.json")))
+    for f7, f, box in ((0x78, "s", 0xFFFFFFFF00000000), (0x79, "d", 0), (0x7A, "h", 0xFFFFFFFFFFFF0000)):
+        for i in range(32):
+            p = oracle_mod.probe((f7 << 25) | (1 << 20) | (i << 15) | (3 << 7) | 0x53, 0x1000, [0] * 32)
+            assert p.fault == 0 and p.rd == 35 and p.rd_value == fli[f][i] | box, (f, i, hex(p.rd_value))

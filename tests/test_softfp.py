@@ -16,9 +16,9 @@ from oracle import pyoracle
 
 OPS = {"add": 0, "sub": 1, "mul": 2, "div": 3, "sqrt": 4, "fma": 5, "eq": 6, "lt": 7, "le": 8, "ltq": 9, "leq": 10,
        "to_i32": 11, "to_u32": 12, "to_i64": 13, "to_u64": 14, "from_i32": 15, "from_u32": 16, "from_i64": 17,
-       "from_u64": 18, "to_h": 19, "to_s": 20, "to_d": 21}
+       "from_u64": 18, "to_h": 19, "to_s": 20, "to_d": 21, "rint": 22, "rintx": 23}
 FMTS = {"h": (0, 5, 10), "s": (1, 8, 23), "d": (2, 11, 52)}
-ARITY = {"sqrt": 1, "fma": 3}
+ARITY = {"sqrt": 1, "fma": 3, "rint": 1, "rintx": 1}
 
 pytestmark = pytest.mark.skipif(not pyoracle.has_softfloat(),
                                 reason="oracle built without the reference SoftFloat (oracle/_ref)")
