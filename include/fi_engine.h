@@ -82,6 +82,7 @@ typedef int32_t fi_status;
 #define FI_ESC_CSR 3
 #define FI_ESC_HOST 4
 #define FI_ESC_RESOURCE 5
+#define FI_ESC_UNDEF 6      /* gem5's own behaviour is undefined (GEM5_UNREACHABLE: an RVV floating-point op at SEW = 8) */
 
 /* Fault-site structures: 1..31 = x1..x31, 32 = pc, 33 = 8-byte memory word,
  * 34 = the result of an instruction: the value the first instruction that

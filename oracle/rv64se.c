@@ -260,7 +260,7 @@ typedef struct {
 } mach_t;
 
 enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_ESCAPE = 5, F_PGFAULT = 6, F_AMOLINE = 7,
-       F_SCLINE = 8, F_M5PANIC = 9 };
+       F_SCLINE = 8, F_M5PANIC = 9, F_UNDEF = 10 };
 
 /* -------------------------------------------------------------- decode */
 /* Op ids.  Names follow gem5's mnemonics (arch/riscv/isa/decoder.isa). */
@@ -297,7 +297,7 @@ enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_E
     X(lr_w) X(sc_w) X(lr_d) X(sc_d) \
     X(fadd) X(fsub) X(fmul) X(fdiv) X(fsqrt) X(fmin) X(fmax) X(fmadd) X(fmsub) X(fnmsub) X(fnmadd) \
     X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f) \
-    X(priv) X(cbo) X(m5op) X(crypto) X(fli) X(fround) X(fcvtmod)
+    X(priv) X(cbo) X(m5op) X(crypto) X(fli) X(fround) X(fcvtmod) X(vec)
 
 enum {
 #define X(n) OP_##n,
@@ -345,6 +345,13 @@ static int gem5_known(u32 raw) {
 #undef IDX
     return 1;
 }
+/* RVV in a process that has not executed a vset* (vtype = vill, vl = 0:
+ * decoder.hh:68-69): the row's action (gem5_decode_table.h, generated by
+ * tools/oracle/gen_vector_actions.py from the reference's micro-op code)
+ * becomes op `vec`, imm = 2 no-op, 3 no-op of two ticks, 4 IllegalInst
+ * ("VILL is set", isa.cc:1400-1402), 5 undefined in gem5 (GEM5_UNREACHABLE
+ * at the SEW = 8 decode), 6 needs vector state (vset*, whole-register). */
+enum { VEC_NOP = 2, VEC_NOP2 = 3, VEC_ILLEGAL = 4, VEC_UNDEF = 5, VEC_STATE = 6 };
 /* Unknown and escape encodings read and write no registers. */
 static void refine_fp_amo(u32 raw, dec_t *d);
 /* The gem5-known members of the privileged SYSTEM, hypervisor load/store,
@@ -414,8 +421,11 @@ static void refine_misc(u32 raw, dec_t *d) {
 static void decode(u32 raw, dec_t *d) {
     decode_tree(raw, d);
     if ((raw & 3) == 3 && (d->op == OP_ESC_FP || d->op == OP_ESC_VEC || d->op == OP_ESC_AMO ||
-                           d->op == OP_ESC_SYS || d->op == OP_ESC_HYP) && !gem5_known(raw))
-        d->op = OP_UNKNOWN;
+                           d->op == OP_ESC_SYS || d->op == OP_ESC_HYP)) {
+        const int k = gem5_known(raw);
+        if (!k) d->op = OP_UNKNOWN;
+        else if (k >= VEC_NOP) { d->op = OP_vec; d->imm = k; }
+    }
     if ((raw & 3) == 3 && (d->op == OP_ESC_FP || d->op == OP_ESC_AMO)) refine_fp_amo(raw, d);
     if (d->op < OP_c_addi4spn) d->rd = d->rs1 = d->rs2 = d->frd = d->frs1 = d->frs2 = -1;
     if ((raw & 3) == 3) refine_misc(raw, d);
@@ -918,6 +928,7 @@ const char *or_mnemonic(u32 inst) {
         return d.imm <= 4 ? cn[d.imm] : "?";
     }
     if (d.op == OP_m5op) return "M5Op";
+    if (d.op == OP_vec) { snprintf(buf, sizeof buf, "vector:%d", (int)d.imm); return buf; }
     if (d.op == OP_fli || d.op == OP_fround || d.op == OP_fcvtmod) {
         static const char *fs[3] = {"h", "s", "d"};
         const int fmt = (int)((d.imm >> 3) & 3);
@@ -1995,6 +2006,15 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
 #else
     case OP_fround: return F_ESCAPE;
 #endif
+    /* ---- RVV before any vset* (decode: op vec) */
+    case OP_vec:
+        switch ((int)imm) {
+        case VEC_NOP: goto no_rd;
+        case VEC_NOP2: m->num_cycles += 1; goto no_rd;   /* the trailing micro-op's tick */
+        case VEC_ILLEGAL: return F_ILLEGAL;
+        case VEC_UNDEF: return F_UNDEF;
+        default: return F_ESCAPE;
+        }
     /* ---- privileged SYSTEM / hypervisor load-store from PRV_U (refine_misc) */
     case OP_priv:
         if (!imm) return F_ILLEGAL;
@@ -2107,6 +2127,7 @@ static void invoke_fault(mach_t *m, int f, u64 fault_va, const dec_t *d) {
     case F_AMOLINE: finish(m, OR_CRASH, OR_CRASH_AMO_LINE, 134); return;
     case F_SCLINE: finish(m, OR_CRASH, OR_CRASH_SC_LINE, 134); return;
     case F_M5PANIC: finish(m, OR_CRASH, OR_CRASH_M5_PANIC, 134); return;
+    case F_UNDEF: finish(m, OR_ESCAPE, OR_ESC_UNDEF, 0); m->res.detail = d->raw; return;
     case 100: finish(m, OR_DETECTED, 0, 0); return;
     case F_PGFAULT: {
         int h = fixup_fault(m, fault_va);

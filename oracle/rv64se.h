@@ -47,7 +47,8 @@ enum {
     OR_ESC_SYSCALL = 2,         /* syscall gem5 implements but the engine does not model */
     OR_ESC_CSR = 3,             /* U-mode-accessible CSR */
     OR_ESC_HOST = 4,            /* behaviour that depends on the host (fd 0, huge buffers) */
-    OR_ESC_RESOURCE = 5         /* engine resource limit (private pages) -- device only */
+    OR_ESC_RESOURCE = 5,        /* engine resource limit (private pages) -- device only */
+    OR_ESC_UNDEF = 6            /* gem5's own behaviour is undefined (GEM5_UNREACHABLE reached) */
 };
 enum { OR_HANG_INSTS = 1 };
 

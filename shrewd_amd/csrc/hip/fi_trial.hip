@@ -412,7 +412,7 @@ __device__ bool proxy_write(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot
 }
 
 enum { F_NONE = 0, F_SYSCALL, F_BREAK, F_ILLEGAL, F_UNKNOWN, F_ESCAPE, F_ESCCSR, F_PGFAULT, F_NEEDPAGE, F_DETECT,
-       F_AMOLINE, F_SCLINE, F_M5PANIC };
+       F_AMOLINE, F_SCLINE, F_M5PANIC, F_UNDEF };
 
 // AtomicSimpleCPU::readMem/writeMem (atomic.cc:331-544): the access is split
 // at 64-byte line boundaries, each fragment translated on its own; faults are
@@ -2575,6 +2575,15 @@ __device__ __forceinline__ void trial_body() {
                 break;
             }
             case OP_crypto: v = rvk::exec(d.imm, a, b); break;
+            // RVV before any vset* (oracle/rv64se.c VEC_*): no-op (one or two
+            // micro-op ticks), IllegalInst (vill), undefined in gem5, needs vector state
+            case OP_vec:
+                wrd = false;
+                if (d.imm == 3) xticks = 1;
+                else if (d.imm == 4) f = F_ILLEGAL;
+                else if (d.imm == 5) f = F_UNDEF;
+                else if (d.imm == 6) f = F_ESCAPE;
+                break;
             default: f = F_UNKNOWN; break;
             }
         }
@@ -2667,6 +2676,7 @@ __device__ __forceinline__ void trial_body() {
         case F_AMOLINE: finish(L, FI_CRASH, FI_CRASH_AMO_LINE, 134, (uint32_t)pc); break;
         case F_SCLINE: finish(L, FI_CRASH, FI_CRASH_SC_LINE, 134, (uint32_t)pc); break;
         case F_M5PANIC: finish(L, FI_CRASH, FI_CRASH_M5_PANIC, 134, (uint32_t)pc); break;
+        case F_UNDEF: finish(L, FI_ESCAPE, FI_ESC_UNDEF, 0, d.raw); break;
         case F_PGFAULT: {   // GenericPageTableFault::invoke -> fixupFault (sim/faults.cc:95-105)
             int h;
             OOL(h = fixup_fault(CX, mc_, slot, fva));

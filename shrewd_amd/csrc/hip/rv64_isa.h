@@ -45,7 +45,7 @@
     X(lr_w) X(sc_w) X(lr_d) X(sc_d) \
     X(fadd) X(fsub) X(fmul) X(fdiv) X(fsqrt) X(fmin) X(fmax) X(fmadd) X(fmsub) X(fnmsub) X(fnmadd) \
     X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f) \
-    X(priv) X(cbo) X(m5op) X(crypto) X(fli) X(fround) X(fcvtmod)
+    X(priv) X(cbo) X(m5op) X(crypto) X(fli) X(fround) X(fcvtmod) X(vec)
 
 namespace fi {
 
@@ -366,16 +366,19 @@ struct DecRow { uint32_t mask, match, known; };
 __constant__ const DecRow kGem5Rows[FI_GEM5_DEC_ROWS] = { FI_GEM5_DEC_TABLE(FI_ROW) };
 #undef FI_ROW
 
-__device__ inline bool gem5_known(uint32_t raw) {
+// 0 Unknown, 1 known; RVV classes: their action before any vset* (2 no-op,
+// 3 no-op of two ticks, 4 IllegalInst, 5 undefined in gem5, 6 needs vector
+// state; oracle/rv64se.c VEC_*)
+__device__ inline uint32_t gem5_known(uint32_t raw) {
     const uint32_t op5 = (raw >> 2) & 31;
     int first = -1, cnt = 0;
 #define FI_IDX(o, f, c) if (op5 == (o)) { first = (f); cnt = (c); }
     FI_GEM5_DEC_INDEX(FI_IDX)
 #undef FI_IDX
-    if (first < 0) return true;
+    if (first < 0) return 1;
     for (int i = first; i < first + cnt; i++)
-        if ((raw & kGem5Rows[i].mask) == kGem5Rows[i].match) return kGem5Rows[i].known != 0;
-    return false;
+        if ((raw & kGem5Rows[i].mask) == kGem5Rows[i].match) return kGem5Rows[i].known;
+    return 0;
 }
 
 // F/D/Zfh arithmetic (decoder.isa:2694-2810, 2811-3440), as in
@@ -561,8 +564,11 @@ __device__ inline void rv_refine_misc(uint32_t raw, Dec &d) {
 __device__ inline Dec rv_decode(uint32_t raw) {
     Dec d = rv_decode_tree(raw);
     if ((raw & 3) == 3 && (d.op == OP_ESC_FP || d.op == OP_ESC_VEC || d.op == OP_ESC_AMO ||
-                           d.op == OP_ESC_SYS || d.op == OP_ESC_HYP) && !gem5_known(raw))
-        d.op = OP_UNKNOWN;
+                           d.op == OP_ESC_SYS || d.op == OP_ESC_HYP)) {
+        const uint32_t k = gem5_known(raw);
+        if (!k) d.op = OP_UNKNOWN;
+        else if (k >= 2) { d.op = OP_vec; d.imm = (int32_t)k; }
+    }
     if ((raw & 3) == 3 && (d.op == OP_ESC_FP || d.op == OP_ESC_AMO)) rv_refine_fp_amo(raw, d);
     if ((raw & 3) == 3) rv_refine_misc(raw, d);
     return d;

@@ -23,7 +23,7 @@ CRASH_NAMES = {1: "panic_unknown_inst", 2: "panic_illegal_inst", 3: "panic_page_
                4: "fatal_syscall_range", 5: "fatal_syscall_unimpl", 6: "fatal_proxy", 7: "abort_fd_assert",
                8: "sigtrap", 9: "fatal_stack_limit", 10: "panic_amo_line", 11: "abort_sc_line", 12: "panic_se_handler",
                13: "panic_m5op"}
-ESCAPE_NAMES = {1: "inst", 2: "syscall", 3: "csr", 4: "host", 5: "resource"}
+ESCAPE_NAMES = {1: "inst", 2: "syscall", 3: "csr", 4: "host", 5: "resource", 6: "undefined"}
 T_PC, T_MEM, T_RESULT, N_STRUCT = 32, 33, 34, 35
 
 OUTCOME_DT = np.dtype([("cls", "u1"), ("sub", "u1"), ("exit_code", "u1"), ("flags", "u1"),
@@ -459,7 +459,7 @@ def escape_breakdown(out: np.ndarray) -> dict:
     res: dict[str, int] = {}
     for sub, det in zip(esc["sub"].tolist(), esc["detail"].tolist()):
         name = ESCAPE_NAMES.get(sub, str(sub))
-        if sub == 1:
+        if sub in (1, 6):
             name += ":" + inst_group(det)
         elif sub == 2:
             name += f":{det}"

@@ -1381,6 +1381,11 @@ XOP_FCVTMOD = [0x41E0000000000000, 0xC1E0000000200000, 0x4340000000000001, 0x454
 XOP_M5_NOEFFECT = [0x00, 0x09, 0x0D, 0x10, 0x11, 0x20, 0x31, 0x40, 0x41, 0x42, 0x50, 0x55, 0x59, 0x7F]
 XOP_RPNS_GAP = 40
 XOP_PRIV_NOPS = [0x16000073, 0x18000073, 0x18100073, 0x26000073, 0x66000073]
+# RVV before any vset* (vl = 0): no-ops of one micro-op tick (vadd.vv, vle8.v,
+# vse32.v, vmerge.vvm, vslideup.vx, vrgather.vv, vlse64.v, vluxei8.v,
+# vlseg2e8.v) and of two (vle8ff.v: + the vl trim; vsaddu.vv: + vxsat)
+XOP_VNOPS = [0x02218057, 0x02050087, 0x0205e0a7, 0x5c2180d7, 0x3a2540d7, 0x322180d7, 0x0a2570d7 & ~0x70 | 0x07,
+             0x06250087, 0x22050087, 0x03050087, 0x822180d7]
 
 
 def _crypto_word(fn, rd=7, rs1=5, rs2=6):
@@ -1427,8 +1432,10 @@ def _fcvtmod_model(a):
 def xop_program_source() -> str:
     L = ["    .text", "_start:", "    .word 0x0E00007B", "    mv    s4, a0"]      # rpns at tick 0
     L += ["    addi  t3, t3, 1"] * (XOP_RPNS_GAP - 2)
-    L += ["    .word 0x0E00007B", "    mv    s5, a0", "    la    s2, out", "    mv    s3, s2",
-          "    sd    s4, 0(s2)", "    sd    s5, 8(s2)", "    addi  s2, s2, 16"]
+    L += ["    .word 0x0E00007B", "    mv    s5, a0"]
+    L += [f"    .word {w:#x}" for w in XOP_VNOPS]
+    L += ["    .word 0x0E00007B", "    mv    s6, a0", "    la    s2, out", "    mv    s3, s2",
+          "    sd    s4, 0(s2)", "    sd    s5, 8(s2)", "    sd    s6, 16(s2)", "    addi  s2, s2, 24"]
     # m5sum, initparam keys, functions without an effect (a0 / a1 after each)
     L += [f"    li    a{k}, {0x1111 * (k + 1) + (1 << (60 - k))}" for k in range(6)]
     L += ["    .word 0x4600007B", "    sd    a0, 0(s2)", "    sd    a1, 8(s2)", "    addi  s2, s2, 16"]
@@ -1486,8 +1493,12 @@ def xop_program_elf() -> bytes:
 
 def xop_program_expected() -> bytes:
     from oracle.pyoracle import rvk_ref, sf_ref
+    from oracle.pyoracle import mnemonic
     M = (1 << 64) - 1
-    vals = [0, XOP_RPNS_GAP * 500 // 1000]
+    acts = [mnemonic(w) for w in XOP_VNOPS]
+    assert set(acts) == {"vector:2", "vector:3"}, acts
+    ticks = XOP_RPNS_GAP + 2 + sum(1 if a == "vector:2" else 2 for a in acts)
+    vals = [0, XOP_RPNS_GAP * 500 // 1000, ticks * 500 // 1000]
     sargs = [0x1111 * (k + 1) + (1 << (60 - k)) for k in range(6)]
     vals += [sum(sargs) & M, 0]
     vals += [0, 0, 0, 0, 1, 0]
@@ -1530,3 +1541,20 @@ def test_fli_probe_matches_reference_table(oracle_mod):
         for i in range(32):
             p = oracle_mod.probe((f7 << 25) | (1 << 20) | (i << 15) | (3 << 7) | 0x53, 0x1000, [0] * 32)
             assert p.fault == 0 and p.rd == 35 and p.rd_value == fli[f][i] | box, (f, i, hex(p.rd_value))
+
+
+def test_vector_actions_before_vset(oracle_mod):
+    """RVV before any vset* (gen_vector_actions.py): vill-checking classes raise
+    IllegalInst, floating-point classes reach GEM5_UNREACHABLE at SEW = 8
+    (escape), vset* and whole-register moves need vector state (escape)."""
+    P = oracle_mod.probe
+    regs = [0] * 32
+    cases = {0x622180d7: ("vector:4", 3),    # vmseq.vv: the first micro-op checks vill
+             0x422020d7: ("vector:4", 3),    # vmv.x.s x1, v2 (non-split)
+             0x02219057: ("vector:5", 5),    # vfadd.vv: no SEW = 8 instantiation
+             0x0c0071d7: ("vector:6", 5),    # vsetvli
+             0x02828087: ("vector:6", 5),    # vl1re8.v (whole register)
+             0x02218057: ("vector:2", 0)}    # vadd.vv: a no-op at vl = 0
+    for w, (name, fault) in cases.items():
+        assert oracle_mod.mnemonic(w) == name, (hex(w), oracle_mod.mnemonic(w))
+        assert P(w, 0x1000, regs).fault == fault, hex(w)

@@ -264,6 +264,15 @@ def test_decode_matches_gem5_decoder(oracle_mod):
         elif name.startswith("escape:"):
             # ... a class the engine does not execute ends the trial as an escape
             assert name != "escape:UNKNOWN"
+        elif name.startswith("vector:"):
+            # ... an RVV class carries its action before any vset*
+            # (gen_vector_actions.py): whole-register moves and vset* need vector state
+            act = int(name.split(":")[1])
+            assert 2 <= act <= 6
+            if str(fmt[lf]) in ("VConfOp", "VlWholeOp", "VsWholeOp", "VMvWholeFormat"):
+                assert act == 6, cls[lf]
+            if "Float" in str(fmt[lf]):   # no vill check before the SEW = 8 decode, no non-split float op at SEW 8
+                assert act in (2, 5), cls[lf]
         else:
             # ... and an executed class carries gem5's own mnemonic
             assert name == str(mnem[lf]), (cls[lf], name)

@@ -278,10 +278,15 @@ def flatten(node, fields, cons, out):
             m = ((1 << (hi - lo + 1)) - 1) << lo
             mask |= m
             match |= (val << lo) & m
-        out.append((mask, match, 0 if node[1] == "Unknown" else 1, node[1]))
+        out.append((mask, match, 0 if node[1] == "Unknown" else 1, node[1], node[2]))
         return
     _, name, cases, default = node
     if name.startswith("machInst."):
+        # the SEW switch of a vector class: without an SEW = 8 case (vsew 0)
+        # the decode of a process that has not run vset* is GEM5_UNREACHABLE
+        if name == "machInst.vtype8.vsew":
+            lf = first_leaf(node)
+            SEW0[lf[1]] = 0 in cases
         leaves = []
         def collect(n):
             if n is None:
@@ -303,9 +308,14 @@ def flatten(node, fields, cons, out):
     flatten(default, fields, cons, out)
 
 
-def emit_table(tree, fields, path):
+SEW0: dict[str, bool] = {}
+
+
+def emit_table(tree, fields, path, generated=None):
     """Known-vs-Unknown first-match table for the opcode groups the engine does
-    not execute (FP, vector, AMO, SYSTEM privileged / hypervisor)."""
+    not execute (FP, vector, AMO, SYSTEM privileged / hypervisor).  With the
+    ISA parser's output (generated), vector classes carry their action in a
+    process that has not run vset* (gen_vector_actions.py) instead of 1."""
     q3 = tree[2][3]
     assert q3[1] == "OPCODE5"
     rows = []
@@ -318,6 +328,11 @@ def emit_table(tree, fields, path):
             pats.pop()
         index.append((op, len(rows), len(pats)))
         rows += pats
+    if generated:
+        from gen_vector_actions import vector_actions
+        vec = {r[3]: r[4] for r in rows if r[2] and r[4].startswith("V")}
+        act = vector_actions(generated, vec, SEW0)
+        rows = [(m, v, act.get(c, k) if k else 0, c, f) for m, v, k, c, f in rows]
     with open(path, "w") as f:
         f.write("// GENERATED by tools/oracle/gen_decode_vectors.py --emit-table from the\n"
                 "// reference's ISA description (src/arch/riscv/isa/decoder.isa via its\n"
@@ -328,10 +343,14 @@ def emit_table(tree, fields, path):
                 "// encoding gem5 decodes to a real instruction (-> escape outcome) from one\n"
                 "// it decodes to Unknown (-> illegal-instruction crash).  Rows are\n"
                 "// first-match (mask, match, known) patterns grouped per opcode5.\n"
+                "// known: 0 Unknown, 1 known; vector classes: what they do before any\n"
+                "// vset* (tools/oracle/gen_vector_actions.py): 2 no-op (one tick), 3 no-op\n"
+                "// (two ticks), 4 IllegalInst (vill), 5 undefined in gem5 (escape), 6 needs\n"
+                "// vector state (escape).\n"
                 "#pragma once\n\n")
         f.write(f"#define FI_GEM5_DEC_ROWS {len(rows)}\n")
         f.write("// X(mask, match, known)\n#define FI_GEM5_DEC_TABLE(X) \\\n")
-        for mask, match, known, cls in rows:
+        for mask, match, known, cls, _ in rows:
             f.write(f"    X(0x{mask:08x}u, 0x{match:08x}u, {known}) /* {cls} */ \\\n")
         f.write("\n// X(opcode5, first row, row count)\n#define FI_GEM5_DEC_INDEX(X) \\\n")
         for op, first, cnt in index:
@@ -364,7 +383,7 @@ def main():
     tree = p.switch()
 
     if a.emit_table:
-        emit_table(tree, fields, a.emit_table)
+        emit_table(tree, fields, a.emit_table, os.path.dirname(path))
 
     rng = random.Random(a.seed)
     words = [w for w in range(1 << 16) if (w & 3) != 3]
