@@ -152,6 +152,12 @@ typedef struct {
  * the flipped register or bytes (A/B and parity checks; outcomes are
  * identical).  FI_CFG_NO_EARLY_EXIT implies it. */
 #define FI_CFG_NO_FORWARD 512u
+/* no early SDC exit: a trial whose output already differs from the golden
+ * output but whose machine state equals a golden snapshot (pc, registers
+ * under liveness, memory, stream positions) ends there as SDC with the golden
+ * exit code and numInst -- it can only go on as the golden run does -- unless
+ * this flag is set (A/B and parity checks; outcomes are identical) */
+#define FI_CFG_NO_SDC_EXIT 1024u
 
 typedef struct {
     uint64_t ninst, ncycles;

@@ -129,7 +129,7 @@ struct DevCtx {
     const uint8_t *zero_page;
     uint64_t snap_interval;          // I: snapshot k is at numInst == k * I
     uint32_t n_snap;
-    uint32_t early_exit;             // compare with snapshots after the injection
+    uint32_t early_exit;             // compare with snapshots after the injection (bit 1: also with wrong output)
     // golden reference output (or record buffers in golden mode)
     const uint8_t *gout, *gerr;
     uint64_t gout_len, gerr_len;

@@ -1544,7 +1544,10 @@ __device__ __forceinline__ void trial_body() {
                 const bool grp = !L.done && m.req_vpn == kNone && L.ninst == L.next_chk && L.ninst == kn;
                 pend &= ~wballot<kNL>(grp);
                 const SnapState *S = CX->snaps + (uint32_t)(kn / CX->snap_interval);
-                bool eq = grp && L.pc == S->pc && L.out_pos == S->out_pos && L.err_pos == S->err_pos && !L.out_bad &&
+                // (with wrong output so far, bit 1: the trial can only go on as the
+                // golden run does from here, so it ends as SDC with the golden exit)
+                bool eq = grp && L.pc == S->pc && L.out_pos == S->out_pos && L.err_pos == S->err_pos &&
+                          (!L.out_bad || (CX->early_exit & 2)) &&
                           m.stack_min == S->stack_min && !L.fp && L.injected != 3 && m.resv == kNone &&
                           m.lock == kNone && !m.vm;
                 if (wballot<kNL>(eq)) {
@@ -1568,7 +1571,7 @@ __device__ __forceinline__ void trial_body() {
                 }
                 if (grp) {
                     if (eq) {
-                        finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
+                        finish(L, L.out_bad ? FI_SDC : FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
                         L.res.ninst = CX->gninst;
                     } else {
                         // back off after repeated mismatches (any schedule is exact)

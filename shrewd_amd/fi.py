@@ -104,6 +104,8 @@ CFG_FIXED_RESUME = 32
 CFG_NO_SOLO = 64
 CFG_SOLO_ALL = 128
 CFG_SIMT = 256
+CFG_NO_FORWARD = 512
+CFG_NO_SDC_EXIT = 1024
 
 
 class GoldenInfo(C.Structure):

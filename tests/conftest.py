@@ -7,7 +7,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-WORKLOADS = ["hello", "crc32", "qsort", "intmix", "fpamo"]
+WORKLOADS = ["hello", "crc32", "qsort", "intmix", "fpamo", "crcblk"]
 
 
 def pytest_configure(config):

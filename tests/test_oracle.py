@@ -22,6 +22,16 @@ def ref_crc32():
     return b"%08x\n" % zlib.crc32(buf)
 
 
+def ref_crcblk():
+    x, buf = 0x12345678, b""
+    for _ in range(1024):
+        x ^= (x << 13) & 0xFFFFFFFF
+        x ^= x >> 17
+        x ^= (x << 5) & 0xFFFFFFFF
+        buf += struct.pack("<I", x)
+    return b"".join(b"%08x\n" % zlib.crc32(buf[k:k + 512]) for k in range(0, 4096, 512))
+
+
 def ref_qsort():
     x, a = 1, []
     for _ in range(1024):
@@ -144,7 +154,7 @@ def ref_fpamo():
 
 
 EXPECTED = {"hello": b"Hello world!\n", "crc32": ref_crc32(), "qsort": ref_qsort(), "intmix": ref_intmix(),
-            "fpamo": ref_fpamo()}
+            "fpamo": ref_fpamo(), "crcblk": ref_crcblk()}
 
 
 @pytest.mark.parametrize("name", list(EXPECTED))
