@@ -224,6 +224,11 @@ fi_status fi_set_bits(fi_engine *e, uint64_t bits_mask);
  * (curTick at a tick = (cycles so far - 1) x period; default 500 = 2 GHz) and
  * gem5's Random global seed for getrandom (default 5489, base/random.cc:79). */
 fi_status fi_set_clock(fi_engine *e, uint64_t period_ticks, uint64_t random_seed);
+/* The realpath of the workload executable, what gem5's readlinkat on
+ * "/proc/self/exe" answers (realpath(Process::progName()),
+ * src/sim/syscall_emul.hh:1089-1111); NULL / "" (default): that call ends the
+ * trial as escape/host.  FaultCampaign sets it from the workload path. */
+fi_status fi_set_exe_path(fi_engine *e, const char *path);
 /* selective-replication mask over x0..x31 (bits 0..31) and pc (bit 32) */
 fi_status fi_set_protect(fi_engine *e, uint64_t protect_mask);
 /* SHREWD selective replication by instruction class (the reference's

@@ -112,6 +112,7 @@ def lib():
         L.or_sys_class.argtypes = [C.c_int]
         L.or_set_protect_opclasses.argtypes = [C.c_void_p, C.c_uint64]
         L.or_set_clock.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+        L.or_set_exe_path.argtypes = [C.c_void_p, C.c_char_p]
         L.or_issue_model.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(IssueParams), C.c_void_p,
                                      C.POINTER(IssueStats)]
         L.or_set_issue_model.argtypes = [C.c_void_p, C.POINTER(IssueParams)]
@@ -213,6 +214,10 @@ class Oracle:
                                 out.ctypes.data, threads) != 0:
             raise RuntimeError(self.L.or_error(self.h).decode())
         return out
+
+    def set_exe_path(self, path: str):
+        """What readlinkat("/proc/self/exe") answers (realpath of the executable)."""
+        self.L.or_set_exe_path(self.h, path.encode())
 
     def set_clock(self, period_ticks=500, random_seed=5489):
         self.L.or_set_clock(self.h, period_ticks, random_seed)

@@ -201,6 +201,7 @@ struct or_campaign {
     u64 stack_vma_lo, stack_vma_hi;  /* the "stack" VMA created by argsInit */
     u64 brk0;
     u64 clk_period;        /* ticks per CPU cycle (1 ps ticks; 500 = 2 GHz) */
+    char exe_path[4096];   /* realpath of the process' executable ("" unknown): readlinkat /proc/self/exe */
     u64 rnd_seed;          /* gem5 Random::globalSeed (base/random.cc:79) */
     u64 *mem_pages;        /* writable pages at process start (memory fault candidates) */
     u64 n_mem_pages;
@@ -1164,8 +1165,8 @@ static const uint16_t sys_impl_escape[] = {
 /* modelled: the deterministic handlers (syscall_emul.{cc,hh}, se_workload.cc) */
 static int sys_modelled(int num) {
     switch (num) {
-    case 29: case 57: case 64: case 66: case 93: case 94: case 96: case 113: case 160: case 163: case 214:
-    case 215: case 222: case 261: case 278: case 1058:
+    case 29: case 57: case 63: case 64: case 66: case 78: case 93: case 94: case 96: case 113: case 160: case 163:
+    case 214: case 215: case 222: case 258: case 261: case 278: case 1058:
         return 1;
     default:
         return num >= 172 && num <= 178;
@@ -1309,6 +1310,149 @@ static void sys_mmap(mach_t *m) {
     m->x[10] = start;
 }
 
+/* readlinkatFunc (syscall_emul.hh:1066-1129): the path string is read through
+ * the proxy (an unmapped byte: -EFAULT); a relative path with a dirfd other
+ * than AT_FDCWD takes atSyscallPath (:356-374: (*fds)[dirfd] asserts the
+ * range, no FileFDEntry -> -EBADF, an open stdio entry prefixes its host file
+ * name: host); "/proc/self/exe" answers realpath(progName()) strncpy'd into a
+ * BufferArg of bufsiz bytes (NUL-padded) copied out through the proxy, the
+ * result min(strlen, bufsiz); any other path reads the host file system. */
+#define OR_AT_FDCWD (-100)
+static void sys_readlinkat(mach_t *m) {
+    const int dirfd = (int)(s32)(u32)m->x[10];
+    const u64 pathp = m->x[11], buf = m->x[12], bufsiz = m->x[13];
+    char path[4096];
+    u64 n = 0;
+    for (;; n++) {
+        if (n == sizeof path) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* longer than PATH_MAX */
+        const uint8_t *pg = translate(m, pathp + n);
+        if (!pg || pathp + n < pathp) { m->x[10] = (u64)(s64)-14; return; }    /* -EFAULT */
+        path[n] = (char)pg[(pathp + n) & (PAGE - 1)];
+        if (!path[n]) break;
+    }
+    if (path[0] != '/' && dirfd != OR_AT_FDCWD) {
+        if (dirfd < 0 || dirfd >= 1024) { finish(m, OR_CRASH, OR_CRASH_FD_ASSERT, 134); return; }
+        if (dirfd > 2 || ((m->fdc >> dirfd) & 1)) { m->x[10] = (u64)(s64)-EBADF_; return; }
+        finish(m, OR_ESCAPE, OR_ESC_HOST, 0);
+        return;
+    }
+    if (strcmp(path, "/proc/self/exe") || !m->c->exe_path[0] || bufsiz > (1ULL << 20)) {
+        finish(m, OR_ESCAPE, OR_ESC_HOST, 0);
+        return;
+    }
+    const u64 len = strlen(m->c->exe_path);
+    uint8_t *tmp = (uint8_t *)calloc(bufsiz ? bufsiz : 1, 1);
+    memcpy(tmp, m->c->exe_path, len < bufsiz ? len : bufsiz);
+    const int h = proxy_writable(m, buf, bufsiz);
+    if (h == 0) { free(tmp); finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+    if (h < 0) { free(tmp); finish(m, OR_CRASH, OR_CRASH_STACK_LIMIT, 1); return; }
+    proxy_write(m, buf, tmp, bufsiz);
+    free(tmp);
+    m->x[10] = len > bufsiz ? bufsiz : len;
+}
+
+/* riscvHWProbeFunc (arch/riscv/linux/se_workload.cc:221-527) for one thread
+ * context (cpumask_malloc: 8 bytes, CPU 0 online) under the SE ISA (misa
+ * IMAFDCV + S/U, mvendorid = marchid = mimpid = 0, isa.cc:359-364).
+ * pairs are {int64 key, uint64 value}; BufferArg copyIn / copyOut are
+ * readBlob (fatal if unmapped) / writeBlob through the allocating proxy. */
+static int hw_read(mach_t *m, u64 a, u64 n, uint8_t *dst) {
+    if (!proxy_readable(m, a, n)) return 0;
+    for (u64 i = 0; i < n; i++) dst[i] = translate(m, a + i)[(a + i) & (PAGE - 1)];
+    return 1;
+}
+static u64 hw_one(mach_t *m, s64 *key) {
+    switch (*key) {
+    case 0: case 1: case 2: return 0;                 /* mvendorid / marchid / mimpid */
+    case 3: return 1;                                 /* BaseBehavior: ima */
+    case 4: return (1ULL << 0) | (1ULL << 1) | (1ULL << 2) | (0x3FFFULL << 3) | (1ULL << 28) | (1ULL << 29) |
+                   (1ULL << 31) | (1ULL << 32) | (1ULL << 33) | (1ULL << 36) | (1ULL << 42) | (1ULL << 45) |
+                   (1ULL << 46) | (1ULL << 47);      /* IMAExt0 (linux.hh:68-118) */
+    case 5: case 9: return 2;                         /* Cpuperf0 / MisalignedScalarPerf: Slow */
+    case 6: return 64;                                /* ZicbozBlockSize: cacheLineSize() */
+    case 7: return m->mmap_end;                       /* HighestVirtAddress: MemState::getMmapEnd() */
+    default: *key = -1; return 0;                     /* unknown (incl. TimeCsrFreq) */
+    }
+}
+static void sys_hwprobe(mach_t *m) {
+    const u64 pairs = m->x[10], count = m->x[11], cpus_user = m->x[13];
+    u64 cpusetsize = m->x[12];
+    const u32 flags = (u32)m->x[14];
+    if (count > (1ULL << 16)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* BufferArg(int size) */
+    const u64 psz = 16 * count;
+    uint8_t *pb = (uint8_t *)malloc(psz ? psz : 1);
+    uint8_t ub[8] = {0};
+    int ret = 0;
+    if (flags & 1) {   /* hwprobe_get_cpus */
+        if (flags != 1 || cpusetsize == 0 || !cpus_user) { ret = -EINVAL_; goto out; }
+        if (cpusetsize > 8) cpusetsize = 8;
+        const u64 usz = cpusetsize;
+        if (!hw_read(m, cpus_user, usz, ub)) { free(pb); finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        u64 cpus = 0;
+        memcpy(&cpus, ub, usz);
+        if (!cpus) { cpus = 1; cpusetsize = 8; }
+        cpus &= 1;
+        if (!hw_read(m, pairs, psz, pb)) { free(pb); finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        for (u64 i = 0; i < count; i++) {
+            s64 key; u64 val;
+            memcpy(&key, pb + 16 * i, 8); memcpy(&val, pb + 16 * i + 8, 8);
+            if (key < 0 || key > 9) {
+                key = -1; val = 0;
+                memcpy(pb + 16 * i, &key, 8); memcpy(pb + 16 * i + 8, &val, 8);
+                /* memset(cpus_user_buf, 0, cpusetsize): past the buffer when the size grew */
+                if (cpusetsize > usz) { free(pb); finish(m, OR_ESCAPE, OR_ESC_UNDEF, 0); return; }
+                memset(ub, 0, cpusetsize);
+                break;
+            }
+            /* cpumask_test_cpu reads bits[cpu / 8]: beyond the one-word mask
+             * (undefined) once the loop passes cpu 7 */
+            if (cpusetsize > 1) { free(pb); finish(m, OR_ESCAPE, OR_ESC_UNDEF, 0); return; }
+            if (cpus & 1) {
+                s64 k2 = key;
+                const u64 v2 = hw_one(m, &k2);
+                const int bitmask = key == 3 || key == 4 || key == 5;
+                const int match = k2 == key && (bitmask ? (v2 & val) == val : v2 == val);
+                if (!match) cpus &= ~1ULL;
+            }
+        }
+        const int h = proxy_writable(m, pairs, psz);
+        if (h == 0) { free(pb); finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        if (h < 0) { free(pb); finish(m, OR_CRASH, OR_CRASH_STACK_LIMIT, 1); return; }
+        proxy_write(m, pairs, pb, psz);
+        const int h2 = proxy_writable(m, cpus_user, usz);
+        if (h2 == 0) { free(pb); finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        if (h2 < 0) { free(pb); finish(m, OR_CRASH, OR_CRASH_STACK_LIMIT, 1); return; }
+        proxy_write(m, cpus_user, ub, usz);
+        goto out;
+    }
+    /* hwprobe_get_values */
+    if (flags != 0) { ret = -EINVAL_; goto out; }
+    if (cpusetsize > 8) cpusetsize = 8;
+    if (!(cpusetsize == 0 && !cpus_user)) {
+        if (!hw_read(m, cpus_user, cpusetsize, ub)) { free(pb); finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        u64 cpus = 0;
+        memcpy(&cpus, ub, cpusetsize);
+        /* cpumask_and / cpumask_empty walk cpusetsize / 8 words */
+        if (cpusetsize < 8 || !(cpus & 1)) { ret = -EINVAL_; goto out; }
+    }
+    if (!hw_read(m, pairs, psz, pb)) { free(pb); finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+    for (u64 i = 0; i < count; i++) {
+        s64 key;
+        memcpy(&key, pb + 16 * i, 8);
+        const u64 val = hw_one(m, &key);
+        memcpy(pb + 16 * i, &key, 8); memcpy(pb + 16 * i + 8, &val, 8);
+    }
+    {
+        const int h = proxy_writable(m, pairs, psz);
+        if (h == 0) { free(pb); finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        if (h < 0) { free(pb); finish(m, OR_CRASH, OR_CRASH_STACK_LIMIT, 1); return; }
+        proxy_write(m, pairs, pb, psz);
+    }
+out:
+    free(pb);
+    m->x[10] = (u64)(s64)ret;
+}
+
 static void do_syscall(mach_t *m) {
     /* EmuLinux::syscall: num = (int) a7 (se_workload.cc:95-106, syscall_desc.hh:204) */
     int num = (int)(s32)(u32)m->x[17];
@@ -1446,6 +1590,16 @@ static void do_syscall(mach_t *m) {
         m->x[10] = 0;
         return;
     }
+    case 63: {  /* readFunc (syscall_emul.hh:2798-2822): (*fds)[fd] asserts 0 <= fd < 1024 (fd_array.cc:322);
+                 * an fd without a host-backed entry reads as -EBADF; the open stdio entries read host files */
+        int fd = (int)(s32)(u32)m->x[10];
+        if (fd < 0 || fd >= 1024) { finish(m, OR_CRASH, OR_CRASH_FD_ASSERT, 134); return; }
+        if (fd > 2 || ((m->fdc >> fd) & 1)) { m->x[10] = (u64)(s64)-EBADF_; return; }
+        finish(m, OR_ESCAPE, OR_ESC_HOST, 0);
+        return;
+    }
+    case 78: sys_readlinkat(m); return;
+    case 258: sys_hwprobe(m); return;
     case 64: {  /* writeFunc<RiscvLinux64>(int fd, VPtr buf, size_t n) syscall_emul.hh:2826-2860 */
         int fd = (int)(s32)(u32)m->x[10];
         u64 buf = m->x[11], n = m->x[12];
@@ -2834,6 +2988,9 @@ static void *worker(void *arg) {
 }
 
 void or_set_protect_opclasses(or_campaign_t *c, u64 mask) { c->protect_opc = mask; }
+void or_set_exe_path(or_campaign_t *c, const char *path) {
+    snprintf(c->exe_path, sizeof c->exe_path, "%s", path ? path : "");
+}
 void or_set_clock(or_campaign_t *c, u64 period_ticks, u64 random_seed) {
     c->clk_period = period_ticks;
     c->rnd_seed = random_seed;

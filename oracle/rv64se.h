@@ -138,6 +138,9 @@ uint64_t or_golden_ops(or_campaign_t *c, or_issue_op_t *out, uint64_t cap);
 /* shadow per golden numInst index; returns the count (golden ninst) */
 uint64_t or_shadow_map(or_campaign_t *c, uint8_t *buf, uint64_t cap, or_issue_stats_t *stats);
 
+/* realpath of the executable, what readlinkat("/proc/self/exe") answers
+ * (syscall_emul.hh:1089-1111); "" (default): that call escapes as host */
+void or_set_exe_path(or_campaign_t *c, const char *path);
 /* SE time and randomness: ticks per CPU cycle (clock_gettime; default 500 =
  * 2 GHz) and gem5's Random global seed (getrandom; default 5489) */
 void or_set_clock(or_campaign_t *c, uint64_t period_ticks, uint64_t random_seed);

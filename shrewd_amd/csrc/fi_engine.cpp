@@ -121,6 +121,8 @@ struct fi_engine {
     uint64_t bits = ~0ULL;      // eligible lowest-bit positions (fi_set_bits)
     uint64_t clk_period = 500, rnd_seed = 5489;   // fi_set_clock
     uint8_t *d_rnd = nullptr;   // getrandom's byte stream (kRndLen bytes)
+    std::string exe_path;       // fi_set_exe_path
+    uint8_t *d_exe = nullptr;
     uint64_t protect = 0;
     uint64_t protect_opc = 0;   // SHREWD replication by OpClass (fi_set_protect_opclasses)
     // SHREWD FU contention (fi_set_issue_model): shadow issued per golden numInst index
@@ -287,7 +289,7 @@ static void free_tx(fi_engine *e) {
 }
 static void free_image(fi_engine *e) {
     dfree(e->d_pre); dfree(e->d_zero); dfree(e->d_sink);
-    dfree(e->d_text); dfree(e->d_mem_pages); dfree(e->d_gout); dfree(e->d_gerr);
+    dfree(e->d_text); dfree(e->d_mem_pages); dfree(e->d_gout); dfree(e->d_gerr); dfree(e->d_exe);
     free_snaps(e);
     free_mem_index(e);
     free_fw(e);
@@ -650,6 +652,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.brk0 = e->brk0; c.svma_lo = e->svma_lo; c.svma_hi = e->svma_hi; c.vm = e->d_vm;
     c.simt_min = (e->cfg.flags & FI_CFG_SIMT) ? 8u : 0u;
     c.rnd_tab = e->d_rnd; c.rnd_len = e->d_rnd ? kRndLen : 0; c.clk_period = e->clk_period;
+    c.exe_path = e->d_exe; c.exe_len = e->d_exe ? e->exe_path.size() : 0;
     c.lanes = e->cfg.lanes_per_wave;
     c.mem_live = (e->mem_live && !(e->cfg.flags & FI_CFG_NO_EARLY_EXIT)) ? 1 : 0;
     c.mw_n = e->mw_n; c.mw_addr = e->d_mw_addr; c.mw_off = e->d_mw_off; c.mw_ev = e->d_mw_ev;
@@ -1060,6 +1063,19 @@ fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint
     if (burst < 1 || burst > 64) return fail(e, FI_E_ARG, "burst must be 1..64");
     e->seed = seed; e->structures = structures; e->burst = burst;
     e->bits = ~0ULL;
+    return FI_OK;
+}
+
+fi_status fi_set_exe_path(fi_engine *e, const char *path) {
+    if (!e) return FI_E_ARG;
+    HIPCHK(hipSetDevice(e->dev));
+    e->exe_path = path ? path : "";
+    if (e->exe_path.size() >= 4096) { e->exe_path.clear(); return FI_E_ARG; }   // PATH_MAX
+    dfree(e->d_exe);
+    if (!e->exe_path.empty()) {
+        HIPCHK(hipMalloc(&e->d_exe, e->exe_path.size()));
+        HIPCHK(hipMemcpy(e->d_exe, e->exe_path.data(), e->exe_path.size(), hipMemcpyHostToDevice));
+    }
     return FI_OK;
 }
 

@@ -188,6 +188,8 @@ struct DevCtx {
     VmState *vm;                     // [n_slots]
     const uint8_t *rnd_tab;          // getrandom's byte stream: mt19937_64(seed)() % 255, rnd_len bytes
     uint64_t rnd_len;
+    const uint8_t *exe_path;         // realpath of the executable (readlinkat /proc/self/exe), exe_len bytes
+    uint64_t exe_len;                // 0: unknown (that call escapes as host)
     uint64_t clk_period;             // ticks per CPU cycle (clock_gettime)
     uint32_t simt_min;               // diverged-lanes step loop: least lanes to enter it (0 = off)
     // memory liveness: record mode appends the golden run's data accesses to

@@ -1039,6 +1039,144 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         set_ret((int64_t)total);
         return false;
     }
+    case 63: {   // readFunc (syscall_emul.hh:2798-2822): (*fds)[fd] asserts the range; no host-backed
+                 // entry -> -EBADF; the open stdio entries read the host's files
+        const int fd = (int)(uint32_t)a0;
+        if (fd < 0 || fd >= 1024) { finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, pc32); return false; }
+        if (fd > 2 || ((fdc >> fd) & 1)) { set_ret(-9); return false; }
+        finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32);
+        return false;
+    }
+    case 78: {   // readlinkatFunc (syscall_emul.hh:1066-1129; oracle/rv64se.c sys_readlinkat)
+        const int dirfd = (int)(uint32_t)a0;
+        const char *want = "/proc/self/exe";
+        bool exe = true;
+        uint8_t first = 0;
+        uint64_t n = 0;
+        for (;; n++) {   // the path string through the proxy: -EFAULT at an unmapped byte
+            if (n == 4096) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+            if (a1 + n < a1 || !proxy_readable(c, w, m, slot, a1 + n, 1)) { set_ret(-14); return false; }
+            const uint8_t ch = proxy_byte(c, w, m, slot, a1 + n);
+            if (c->record) rec_mem(c, a1 + n, 1, L.ninst, 1u);
+            if (n == 0) first = ch;
+            if (n < 15) exe = exe && ch == (uint8_t)want[n];
+            if (!ch) break;
+        }
+        if (first != '/' && dirfd != -100) {   // atSyscallPath (:356-374)
+            if (dirfd < 0 || dirfd >= 1024) { finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, pc32); return false; }
+            if (dirfd > 2 || ((fdc >> dirfd) & 1)) { set_ret(-9); return false; }
+            finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32);
+            return false;
+        }
+        if (!exe || n != 14 || !c->exe_len || a3 > (1ULL << 20)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+        const int h = proxy_writable(c, w, m, slot, a2, a3);
+        if (h == 0) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+        if (h == -1) { finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, pc32); return false; }
+        if (h == -2) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        const uint64_t k = c->exe_len < a3 ? c->exe_len : a3;   // strncpy: the path, then NULs to bufsiz
+        if (k && !pwrite(a2, (const char *)c->exe_path, k)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        const char zero[16] = {};
+        for (uint64_t i = k; i < a3; i += 16) {
+            if (!pwrite(a2 + i, zero, a3 - i < 16 ? a3 - i : 16)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        }
+        set_ret((int64_t)k);
+        return a2 < c->code_hi && a2 + a3 > c->code_lo;
+    }
+    case 258: {   // riscvHWProbeFunc (arch/riscv/linux/se_workload.cc:221-527; oracle/rv64se.c sys_hwprobe)
+        const uint64_t pairs = a0, count = a1, cpus_user = a3;
+        uint64_t cpusetsize = a2;
+        const uint32_t flags = (uint32_t)a4;
+        if (count > (1ULL << 16)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+        const uint64_t psz = 16 * count;
+        auto pw8 = [&](uint64_t a, uint64_t v) {
+            char b[8];
+            for (int q = 0; q < 8; q++) b[q] = (char)(v >> (8 * q));
+            return pwrite(a, b, 8);
+        };
+        auto copy_out_ok = [&](uint64_t a, uint64_t n) {
+            const int h = proxy_writable(c, w, m, slot, a, n);
+            if (h == 0) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+            if (h == -1) { finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, pc32); return false; }
+            if (h == -2) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            return true;
+        };
+        auto one = [&](int64_t &key) -> uint64_t {
+            switch (key) {
+            case 0: case 1: case 2: return 0;
+            case 3: return 1;
+            case 4: return (1ULL << 0) | (1ULL << 1) | (1ULL << 2) | (0x3FFFULL << 3) | (1ULL << 28) | (1ULL << 29) |
+                           (1ULL << 31) | (1ULL << 32) | (1ULL << 33) | (1ULL << 36) | (1ULL << 42) | (1ULL << 45) |
+                           (1ULL << 46) | (1ULL << 47);
+            case 5: case 9: return 2;
+            case 6: return 64;
+            case 7: return m.vm ? c->vm[slot].mmap_end : 0x4000000000000000ULL;   // MemState::getMmapEnd()
+            default: key = -1; return 0;
+            }
+        };
+        if (flags & 1) {   // hwprobe_get_cpus
+            if (flags != 1 || cpusetsize == 0 || !cpus_user) { set_ret(-22); return false; }
+            if (cpusetsize > 8) cpusetsize = 8;
+            const uint64_t usz = cpusetsize;
+            if (!proxy_readable(c, w, m, slot, cpus_user, usz)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+            uint64_t ub = 0;
+            for (uint64_t q = 0; q < usz; q++) ub |= (uint64_t)proxy_byte(c, w, m, slot, cpus_user + q) << (8 * q);
+            if (c->record) rec_mem(c, cpus_user, usz, L.ninst, 1u);
+            uint64_t cpus = ub ? ub : 1;
+            if (!ub) cpusetsize = 8;
+            cpus &= 1;
+            if (psz && !proxy_readable(c, w, m, slot, pairs, psz)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+            if (c->record) rec_mem(c, pairs, psz, L.ninst, 1u);
+            int64_t bad = -1;   // the first invalid key's index
+            for (uint64_t i = 0; i < count; i++) {
+                const int64_t key = (int64_t)rd64(pairs + 16 * i);
+                const uint64_t val = rd64(pairs + 16 * i + 8);
+                if (key < 0 || key > 9) {
+                    if (cpusetsize > usz) { finish(L, FI_ESCAPE, FI_ESC_UNDEF, 0, pc32); return false; }
+                    bad = (int64_t)i;
+                    ub = 0;
+                    break;
+                }
+                if (cpusetsize > 1) { finish(L, FI_ESCAPE, FI_ESC_UNDEF, 0, pc32); return false; }
+                if (cpus & 1) {
+                    int64_t k2 = key;
+                    const uint64_t v2 = one(k2);
+                    const bool bitmask = key == 3 || key == 4 || key == 5;
+                    if (!(k2 == key && (bitmask ? (v2 & val) == val : v2 == val))) cpus &= ~1ULL;
+                }
+            }
+            if (!copy_out_ok(pairs, psz)) return false;
+            if (bad >= 0 && (!pw8(pairs + 16 * bad, ~0ULL) || !pw8(pairs + 16 * bad + 8, 0))) {
+                finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32);
+                return false;
+            }
+            if (!copy_out_ok(cpus_user, usz)) return false;
+            char b[8];
+            for (int q = 0; q < 8; q++) b[q] = (char)(ub >> (8 * q));
+            if (!pwrite(cpus_user, b, usz)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            set_ret(0);
+            return (pairs < c->code_hi && pairs + psz > c->code_lo) || (cpus_user < c->code_hi && cpus_user + usz > c->code_lo);
+        }
+        if (flags != 0) { set_ret(-22); return false; }   // hwprobe_get_values
+        if (cpusetsize > 8) cpusetsize = 8;
+        if (!(cpusetsize == 0 && !cpus_user)) {
+            if (!proxy_readable(c, w, m, slot, cpus_user, cpusetsize)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+            if (c->record) rec_mem(c, cpus_user, cpusetsize, L.ninst, 1u);
+            if (cpusetsize < 8 || !(proxy_byte(c, w, m, slot, cpus_user) & 1)) { set_ret(-22); return false; }
+        }
+        if (psz && !proxy_readable(c, w, m, slot, pairs, psz)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+        if (c->record) rec_mem(c, pairs, psz, L.ninst, 1u);
+        if (!copy_out_ok(pairs, psz)) return false;
+        for (uint64_t i = 0; i < count; i++) {
+            int64_t key = (int64_t)rd64(pairs + 16 * i);
+            const uint64_t val = one(key);
+            if (!pw8(pairs + 16 * i, (uint64_t)key) || !pw8(pairs + 16 * i + 8, val)) {
+                finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32);
+                return false;
+            }
+        }
+        set_ret(0);
+        return pairs < c->code_hi && pairs + psz > c->code_lo;
+    }
     default: break;   // 64: write
     }
     // writeFunc (src/sim/syscall_emul.hh:2826-2860): int fd, buffer copied in

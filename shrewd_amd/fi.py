@@ -201,6 +201,7 @@ def lib():
         L.fi_set_campaign.argtypes = [vp, C.c_uint64, C.c_uint64, C.c_uint32]
         L.fi_set_bits.argtypes = [vp, C.c_uint64]
         L.fi_set_clock.argtypes = [vp, C.c_uint64, C.c_uint64]
+        L.fi_set_exe_path.argtypes = [vp, C.c_char_p]
         L.fi_set_protect.argtypes = [vp, C.c_uint64]
         L.fi_set_protect_opclasses.argtypes = [vp, C.c_uint64]
         L.fi_sample_sites.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
@@ -304,6 +305,10 @@ class Engine:
     def set_bits(self, bits: int):
         """Eligible lowest flipped bit positions (mask; ~0 = all): fi_set_bits."""
         self._chk(self.L.fi_set_bits(self.h, bits & (2**64 - 1)), "fi_set_bits")
+
+    def set_exe_path(self, path: str):
+        """What readlinkat("/proc/self/exe") answers: the executable's realpath."""
+        self._chk(self.L.fi_set_exe_path(self.h, path.encode()), "fi_set_exe_path")
 
     def set_clock(self, period_ticks: int = 500, random_seed: int = 5489):
         """clock_gettime's ticks per CPU cycle and getrandom's gem5 Random seed."""
@@ -542,6 +547,8 @@ class FaultCampaign:
                 self.engine.load_checkpoint(checkpoint, f.read())
             else:
                 self.engine.load_elf(f.read(), self.cmd, self.env)
+        # Process.executable defaults to cmd[0]; gem5 answers /proc/self/exe with its realpath
+        self.engine.set_exe_path(os.path.realpath(self.cmd[0] if os.path.exists(self.cmd[0]) else workload))
         self.golden = self.engine.golden_run()
         self.engine.set_campaign(seed, structures, burst)
         self.bits = bits_mask(bits)

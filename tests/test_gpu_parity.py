@@ -424,7 +424,7 @@ def test_native_driver_matches_engine(engine_factory, tmp_path):
     assert hist["counts"].tobytes() == rh["counts"].tobytes()
 
 
-@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp", "rnd", "xop"])
+@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp", "rnd", "xop", "sys2"])
 def test_known_answer_programs(oracle_mod, prog):
     """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
@@ -443,7 +443,8 @@ def test_known_answer_programs(oracle_mod, prog):
     rounding mode and fcsr (answers from the reference SoftFloat).
     rnd: getrandom (gem5's mt19937_64 stream) and clock_gettime (curTick).
     xop: scalar crypto, Zfa (fli / fround / fcvtmod.w.d), M5 pseudo-ops, the
-    warn-only privileged no-ops and the cache-block ops.  The device golden run (general interpreter)
+    warn-only privileged no-ops and the cache-block ops.
+    sys2: read, readlinkat (/proc/self/exe) and riscv_hwprobe.  The device golden run (general interpreter)
     must print exactly the reference-derived models; no-fault trials
     (pre-decoded and translated paths, from snapshots) must end masked with
     the oracle's records; faulted trials must match the oracle bit for bit."""
@@ -458,7 +459,8 @@ def test_known_answer_programs(oracle_mod, prog):
                      "vm": (kat.vm_program_elf, kat.vm_program_expected),
                      "fp": (kat.fp_program_elf, kat.fp_program_expected),
                      "rnd": (kat.rnd_program_elf, kat.rnd_program_expected),
-                     "xop": (kat.xop_program_elf, kat.xop_program_expected)}[prog]
+                     "xop": (kat.xop_program_elf, kat.xop_program_expected),
+                     "sys2": (kat.sys2_program_elf, kat.sys2_program_expected)}[prog]
     if prog in ("fp", "xop") and not oracle_mod.has_softfloat():
         pytest.skip("oracle without the reference SoftFloat")
     if prog == "xop" and not oracle_mod.has_rvk():
@@ -467,12 +469,16 @@ def test_known_answer_programs(oracle_mod, prog):
     elf, expected = elf(), expected()
     e = Engine(private_pages=64)
     e.load_elf(elf, [prog])
+    if prog == "sys2":
+        e.set_exe_path(kat.SYS2_EXE)
     g = e.golden_run()
     assert g.exit_code == (300 & 0xFF if prog == "sys" else 0)
     assert g.stderr_len == len(stderr)
     assert e.golden_stdout() == expected
     assert e.golden_stderr() == stderr
     o = oracle_mod.Oracle(elf, prog)
+    if prog == "sys2":
+        o.set_exe_path(kat.SYS2_EXE)
     o.run_golden()
     assert o.golden_stderr() == e.golden_stderr()
     e.set_campaign(0x5EED00A1, REGS | PC, 1)

@@ -1558,3 +1558,83 @@ def test_vector_actions_before_vset(oracle_mod):
     for w, (name, fault) in cases.items():
         assert oracle_mod.mnemonic(w) == name, (hex(w), oracle_mod.mnemonic(w))
         assert P(w, 0x1000, regs).fault == fault, hex(w)
+
+
+# ---------------------------------------------------------------- sys2 program
+# read (63), readlinkat (78) and riscv_hwprobe (258) (oracle/rv64se.c:
+# sys_readlinkat / sys_hwprobe; se_workload.cc:221-527, syscall_emul.hh:
+# 1066-1129,2798-2822): every result a0 and every buffer is printed.
+SYS2_EXE = "/opt/workloads/sys2.riscv"
+HW_IMA = ((1 << 0) | (1 << 1) | (1 << 2) | (0x3FFF << 3) | (1 << 28) | (1 << 29) | (1 << 31) | (1 << 32) | (1 << 33) |
+          (1 << 36) | (1 << 42) | (1 << 45) | (1 << 46) | (1 << 47))
+
+
+def sys2_program_source() -> str:
+    def call(num, *args):
+        out = [f"    li    a{k}, {v}" if isinstance(v, int) else f"    la    a{k}, {v}" for k, v in enumerate(args)]
+        return out + [f"    li    a7, {num}", "    ecall", "    sd    a0, 0(s2)", "    addi  s2, s2, 8"]
+    L = ["    .text", "_start:", "    la    s2, out", "    mv    s3, s2"]
+    L += call(63, 5, "buf", 8)                          # read: fd 5 has no entry -> -EBADF
+    L += call(57, 0)                                    # close(0), then read(0) -> -EBADF
+    L += call(63, 0, "buf", 8)
+    L += call(78, -100, "exe", "buf", 64)              # /proc/self/exe -> the path, NUL-padded to 64
+    L += call(78, -100, "exe", "buf2", 5)              # truncated to bufsiz
+    L += call(78, 7, "rel", "buf3", 16)                # relative path, dirfd 7: -EBADF
+    L += call(78, -100, 0x10, "buf3", 16)              # unmapped path: -EFAULT
+    # hwprobe, get values for keys 0..10 on all CPUs
+    L += ["    la    t0, pairs"] + [f"    li    t1, {k}\n    sd    t1, {16 * k}(t0)" for k in range(11)]
+    L += call(258, "pairs", 11, 0, 0, 0)
+    L += call(258, "pairs", 1, 4, "mask", 0)            # cpusetsize 4: -EINVAL
+    L += call(258, "pairs", 1, 8, "mask", 2)            # unknown flags: -EINVAL
+    L += call(258, "pairs", 2, 16, "mask", 0)           # cpusetsize clamped to 8, CPU 0 set
+    # which-cpus with a one-byte mask: pair {IMAExt0, FD|C} holds on CPU 0; then an unknown key
+    L += ["    la    t0, pq", "    li    t1, 4", "    sd    t1, 0(t0)", "    li    t1, 3", "    sd    t1, 8(t0)",
+          "    li    t1, 3", "    sd    t1, 16(t0)", "    li    t1, 2", "    sd    t1, 24(t0)",
+          "    li    t1, 77", "    sd    t1, 32(t0)"]
+    L += call(258, "pq", 2, 1, "mask1", 1)
+    L += call(258, "pq", 3, 1, "mask1", 1)
+    L += ["    li    a0, 1", "    mv    a1, s3", "    la    a2, end", "    sub   a2, a2, s3", "    li    a7, 64",
+          "    ecall", "    li    a0, 0", "    li    a7, 93", "    ecall",
+          "    .data", "    .balign 8", "exe:", '    .asciz "/proc/self/exe"', "rel:", '    .asciz "x/y"',
+          "    .balign 8", "mask:", "    .dword 1", "    .dword 0", "mask1:", "    .dword 0x0101",
+          "    .bss", "    .balign 8", "out:", "    .zero 128", "buf:", "    .zero 64", "buf2:", "    .zero 8",
+          "buf3:", "    .zero 16", "pairs:", "    .zero 176", "pq:", "    .zero 48", "end:"]
+    return "\n".join(L) + "\n"
+
+
+def sys2_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(sys2_program_source(), compress=False)
+
+
+def sys2_program_expected() -> bytes:
+    """The output from the reference's handlers, restated by hand."""
+    M = (1 << 64) - 1
+    exe = SYS2_EXE.encode()
+    res = [-9, 0, -9, len(exe), 5, -9, -14, 0, -22, -22, 0, 0, 0]
+    out = b"".join((v & M).to_bytes(8, "little") for v in res)
+    out += bytes(128 - len(out))
+    out += exe + bytes(64 - len(exe))                           # buf
+    out += exe[:5] + bytes(3)                                   # buf2
+    out += bytes(16)                                            # buf3
+    vals = {0: 0, 1: 0, 2: 0, 3: 1, 4: HW_IMA, 5: 2, 6: 64, 7: 0x4000000000000000, 9: 2}
+    pairs = b""
+    for k in range(11):   # the third call rewrote pairs 0, 1 once more (same answers)
+        key = k if k in vals else -1
+        pairs += (key & M).to_bytes(8, "little") + vals.get(k, 0).to_bytes(8, "little")
+    out += pairs
+    # pq after the which-cpus calls: unchanged, then the unknown key's pair set to {-1, 0}
+    pq = [4, 3, 3, 2, M, 0]
+    out += b"".join(v.to_bytes(8, "little") for v in pq)
+    return out
+
+
+def test_sys2_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(sys2_program_elf(), "sys2")
+    o.set_exe_path(SYS2_EXE)
+    g = o.run_golden()
+    assert g.exit_code == 0, g
+    got, exp = o.golden_stdout(), sys2_program_expected()
+    assert len(got) == len(exp), (len(got), len(exp))
+    for k in range(0, len(exp), 8):
+        assert got[k:k + 8] == exp[k:k + 8], (k, got[k:k + 8].hex(), exp[k:k + 8].hex())
