@@ -168,7 +168,6 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_ms, launches = eng.kernel_timer_read()
 
     local_h = np.frombuffer(d_hist.cpu().numpy().tobytes(), HIST_DT)[0]
     node_h = np.frombuffer(d_hist_node.cpu().numpy().tobytes(), HIST_DT)[0]
@@ -178,28 +177,48 @@ def main():
         value = trials_total / elapsed
         guest_ips = int(node_h["guest_insts"]) * a.steps / elapsed
         device_ips = int(node_h["device_insts"]) * a.steps / elapsed
-        # roofline of the dominant kernel (fi_trial_kernel), per launch:
-        # algorithmic bytes = fetched instruction bytes + load/store bytes of all
-        # executed guest instructions + 264 B initial state + 16 B outcome per
-        # trial + 4096 B per copy-on-write page
-        # a step runs one chunk = one dispatch per epoch; every step does the
-        # same work, so bytes per dispatch = bytes per step x steps / dispatches
-        per_step_bytes = (int(local_h["fetch_bytes"]) + int(local_h["data_bytes"]) + T * (264 + 16)
-                          + 4096 * int(local_h["cow_pages"]))
-        per_launch_bytes = per_step_bytes * a.steps // max(launches, 1)
-        avg_kernel_s = (kern_ms / max(launches, 1)) / 1e3
-        achieved = per_launch_bytes / avg_kernel_s / 1e9
-        traffic, issue = None, None
+        # roofline per trial kernel, per launch:
+        # algorithmic bytes = fetched instruction bytes + load/store bytes of the
+        # guest instructions the kernel executed + 4096 B per copy-on-write page
+        # it made, and for the 64-lane kernel (every trial starts there) 264 B of
+        # initial state + 16 B of outcome per trial; counted on the device per
+        # kernel (DevCtx::stats[40..51]) over the last step -- every step runs
+        # the same trial ids, so the last step's counts are every step's.
+        # Duration = the mean of that kernel's dispatches (HIP events on its
+        # stream); the dominant kernel is the one with the most device time.
+        st = eng.debug_stats()
+        kinds, dms = eng.debug_dispatch_kinds(), eng.debug_dispatch_ms()
+        tx = eng.translate_status() == ""
+        names = (["fi_trial_kernel_tx", "fi_trial_kernel_tx_solo", "fi_trial_kernel_tx_solo_odd"] if tx
+                 else ["fi_trial_kernel", "fi_trial_kernel_solo", "fi_trial_kernel_solo_odd"])
+        tj = {}
         if os.path.exists(a.traffic_json):
             try:
                 with open(a.traffic_json) as f:
                     tj = json.load(f)
-                if (tj.get("workload") == a.workload and tj.get("trials") == T
+                if not (tj.get("workload") == a.workload and tj.get("trials") == T
                         and tj.get("lanes_per_wave", 64) == lanes):
-                    traffic = tj.get("hbm_bytes_per_launch")
-                    issue = tj.get("issue")
+                    tj = {}
             except (OSError, ValueError):
-                traffic, issue = None, None
+                tj = {}
+        per_kernel = {}
+        for k, name in enumerate(names):
+            ms_k = [m for m, kk in zip(dms, kinds) if kk == k]
+            if not ms_k:
+                continue
+            disp = len(ms_k) / a.steps
+            b = int(st[40 + 4 * k]) + int(st[41 + 4 * k]) + 4096 * int(st[42 + 4 * k]) + (T * (264 + 16) if k == 0 else 0)
+            avg_ms = sum(ms_k) / len(ms_k)
+            per_launch = b / disp
+            ach = per_launch / (avg_ms / 1e3) / 1e9
+            tk = tj.get("per_kernel", {}).get(name, {})
+            per_kernel[name] = {"avg_kernel_ms": avg_ms, "dispatches_per_step": disp,
+                                "ms_per_step": avg_ms * disp, "algorithmic_bytes_per_launch": per_launch,
+                                "achieved": ach, "frac": ach / HBM_PEAK_GBS,
+                                "device_insts_per_launch": int(st[43 + 4 * k]) / disp,
+                                "traffic": tk.get("hbm_bytes_per_launch"), "issue": tk.get("issue")}
+        dom = max(per_kernel, key=lambda n: per_kernel[n]["ms_per_step"])
+        D = per_kernel[dom]
         cls = node_h["counts"].sum(axis=(0, 1))
         res = {
             "metric": "fault-injection trials/sec (whole node)",
@@ -225,14 +244,13 @@ def main():
             # actually executed
             "guest_inst_per_s_gem5_equiv": guest_ips,
             "device_inst_per_s": device_ips,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "fi_trial_kernel", "avg_kernel_ms": avg_kernel_s * 1e3,
-                         "dispatches_per_step": launches / a.steps,
-                         "algorithmic_bytes_per_launch": per_launch_bytes,
+            "roofline": {"bound": "hbm", "achieved": D["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": D["frac"], "traffic": D["traffic"], "kernel": dom,
+                         "avg_kernel_ms": D["avg_kernel_ms"], "dispatches_per_step": D["dispatches_per_step"],
+                         "algorithmic_bytes_per_launch": D["algorithmic_bytes_per_launch"],
                          # the roof that binds: issue slots (SQ counters of the same
                          # command, profiles/)
-                         "issue": issue},
+                         "issue": D["issue"], "per_kernel": per_kernel},
             "outcomes": {n: int(cls[i]) for i, n in enumerate(["masked", "sdc", "crash", "hang", "detected",
                                                                  "escape"])},
             "golden_s": golden_s,

@@ -15,8 +15,9 @@ fi_status fi_debug_decode(fi_engine *e, const uint32_t *raws, uint64_t n, void *
  * shrewd_amd/csrc/fi_types.h): fetch/data bytes, private pages, golden
  * cycles/output, loop iterations, lane-instructions, slow fetches, min-PC
  * reductions, snapshot comparisons and early exits, translated instructions
- * and entries, the slowest wave, wave-0 clock; [24..27] -DFI_PROF builds only. */
-fi_status fi_debug_stats(fi_engine *e, uint64_t *out40);
+ * and entries, the slowest wave, wave-0 clock, per-kernel bytes; [32..39]
+ * -DFI_PROF builds only.  64 entries. */
+fi_status fi_debug_stats(fi_engine *e, uint64_t *out64);
 /* The engine's IEEE arithmetic port (shrewd_amd/csrc/hip/fi_softfp.h) over
  * operand vectors, on the host (on_device = 0) or the device: op / fmt codes of
  * fi::sf::op; out = result bits, fl = fflags raised. */
@@ -28,6 +29,10 @@ fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves);
 /* Device time of each interpreter dispatch since fi_kernel_timer_reset, in
  * launch order (epochs of each chunk); *n = dispatches (at most cap written). */
 fi_status fi_debug_dispatch_ms(fi_engine *e, float *ms, uint32_t cap, uint32_t *n);
+/* The kernel of each of those dispatches: 0 fi_trial_kernel_tx (64 lanes; the
+ * static fi_trial_kernel without a load-time build), 1 the solo kernel, 2 the
+ * solo-odd kernel (odd-pc survivors, on a second stream beside the solo one). */
+fi_status fi_debug_dispatch_kinds(fi_engine *e, uint32_t *kinds, uint32_t cap, uint32_t *n);
 /* Lanes suspended at the end of each epoch of the last chunk (16 x u32). */
 fi_status fi_debug_epochs(fi_engine *e, uint32_t *out16);
 /* The translator's inputs of the last fi_golden_run: the pre-decoded text

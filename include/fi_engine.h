@@ -158,6 +158,16 @@ typedef struct {
  * exit code and numInst -- it can only go on as the golden run does -- unless
  * this flag is set (A/B and parity checks; outcomes are identical) */
 #define FI_CFG_NO_SDC_EXIT 1024u
+/* no second pass for trials that ran out of copy-on-write pages: by default a
+ * chunk's FI_ESC_RESOURCE trials run again with 16x the private pages (at
+ * least 256) before the histogram, so that the engine's capacity does not
+ * decide an outcome; one host synchronisation per chunk */
+#define FI_CFG_NO_REDO 2048u
+/* resumed solo epochs run every survivor on the solo kernel (by default the
+ * survivors standing at an odd pc -- a pc bit-0 flip -- run on the solo-odd
+ * kernel, whose translated blocks also cover the odd-pc instruction streams,
+ * on a second stream beside it) (A/B and parity checks; outcomes are identical) */
+#define FI_CFG_NO_ODD_KERNEL 4096u
 
 typedef struct {
     uint64_t ninst, ncycles;

@@ -200,6 +200,15 @@ struct or_campaign {
     u64 text_lo, text_hi;  /* page-aligned executable range (PT_LOAD with PF_X) */
     u64 stack_vma_lo, stack_vma_hi;  /* the "stack" VMA created by argsInit */
     u64 brk0;
+    /* the rest of the initial machine (process start: zero / the stack VMA;
+     * a checkpoint: what it holds) */
+    u64 f0[32]; u32 fflags0, frm0;   /* FP registers, MISCREG_FFLAGS / MISCREG_FRM */
+    struct { u64 lo, hi; } vma0[64]; /* MemState VMA list */
+    int nvma0;
+    u64 mmap_end0;
+    u64 tick0;                       /* curTick at the start ([Globals] curTick of a checkpoint) */
+    struct { u64 lo, hi; int w; } seg[32];   /* PT_LOAD page ranges, w = PF_W */
+    int nseg;
     u64 clk_period;        /* ticks per CPU cycle (1 ps ticks; 500 = 2 GHz) */
     char exe_path[4096];   /* realpath of the process' executable ("" unknown): readlinkat /proc/self/exe */
     u64 rnd_seed;          /* gem5 Random::globalSeed (base/random.cc:79) */
@@ -1573,7 +1582,7 @@ static void do_syscall(mach_t *m) {
         const u64 tp = m->x[11];
         if (!tp) { se_panic(m); return; }
         if (!proxy_readable(m, tp, 16)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
-        const u64 ns = (m->num_cycles - 1) * m->c->clk_period / 1000;
+        const u64 ns = (m->c->tick0 + (m->num_cycles - 1) * m->c->clk_period) / 1000;
         const u64 sec = ns / 1000000000ULL + 1000000000ULL, nsec = ns % 1000000000ULL;
         uint8_t b[16];
         for (int k = 0; k < 8; k++) { b[k] = (uint8_t)(sec >> (8 * k)); b[8 + k] = (uint8_t)(nsec >> (8 * k)); }
@@ -2189,7 +2198,7 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
     case OP_m5op: {
         u64 res = 0;
         switch (imm) {
-        case 0x07: res = (m->num_cycles - 1) * m->c->clk_period / 1000; break;   /* rpns: curTick() / ns */
+        case 0x07: res = (m->c->tick0 + (m->num_cycles - 1) * m->c->clk_period) / 1000; break;   /* rpns: curTick() / ns */
         case 0x23:   /* m5sum(a0..a5) */
             if (m->watch >= 10 && m->watch <= 15) return 100;
             for (int k = 10; k <= 15; k++) res += m->x[k];
@@ -2733,6 +2742,12 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
         if (off <= phoff && off + filesz > phoff) phdr_vaddr = vaddr + (phoff - off);   /* :396-402 */
         if (flags & 2)
             for (u64 pg = paddr & PAGE_MASK; pg < paddr + memsz && nw < 4096; pg += PAGE) wpages[nw++] = pg;
+        if (c->nseg < 32) {
+            c->seg[c->nseg].lo = paddr & PAGE_MASK;
+            c->seg[c->nseg].hi = (paddr + memsz + PAGE - 1) & PAGE_MASK;
+            c->seg[c->nseg].w = (flags & 2) != 0;
+            c->nseg++;
+        }
         if (flags & 1) {
             u64 lo = paddr & PAGE_MASK, hi = (paddr + memsz + PAGE - 1) & PAGE_MASK;
             if (!c->text_hi || lo < c->text_lo) c->text_lo = lo;
@@ -2756,6 +2771,8 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
     u64 stack_size = STACK_BASE - stack_top;
     c->stack_vma_lo = stack_top & PAGE_MASK;
     c->stack_vma_hi = c->stack_vma_lo + ((stack_size + PAGE - 1) & PAGE_MASK);
+    c->vma0[0].lo = c->stack_vma_lo; c->vma0[0].hi = c->stack_vma_hi; c->nvma0 = 1;
+    c->mmap_end0 = 0x4000000000000000ULL;   /* RiscvProcess64 (process.cc:79) */
     /* AT_RANDOM */
     stack_min -= 16;
     mt64_t mt; mt_seed(&mt, 5489);
@@ -2817,10 +2834,12 @@ static void mach_init(mach_t *m, const or_campaign_t *c) {
     m->stack_min = c->stack_min0;
     m->watch = -1;
     m->resv = m->lock = OR_NONE;
-    m->fflags = m->frm = 0;
-    m->vma[0].lo = c->stack_vma_lo; m->vma[0].hi = c->stack_vma_hi; m->nvma = 1;   /* argsInit's "stack" VMA */
+    memcpy(m->f, c->f0, sizeof m->f);
+    m->fflags = c->fflags0; m->frm = c->frm0;
+    memcpy(m->vma, c->vma0, sizeof m->vma);   /* process start: argsInit's "stack" VMA */
+    m->nvma = c->nvma0;
     m->brk = c->brk0;
-    m->mmap_end = 0x4000000000000000ULL;
+    m->mmap_end = c->mmap_end0;
 }
 static void mach_free(mach_t *m) { pm_free(&m->mem); free(m->out.buf); free(m->err.buf); free(m->mt); }
 
@@ -3070,6 +3089,9 @@ int or_probe(u32 inst, u64 pc, const u64 regs[32], or_probe_t *o) {
  * [system.physmem] (physical.cc:340-405), frames assigned in vpn order.  The
  * reader is the oracle's own restatement of the restore
  * (Process::unserialize, sim/process.cc:427-441). */
+/* MiscRegIndex (src/arch/riscv/regs/misc.hh) positions the checkpoint uses */
+enum { CPT_MISC_FFLAGS = 120, CPT_MISC_FRM = 121, CPT_NUM_MISC = 193 };
+
 static void cpt_bytes(FILE *f, const char *name, const uint8_t *b, int n) {
     fprintf(f, "%s=", name);
     for (int i = 0; i < n; i++) fprintf(f, i ? " %u" : "%u", b[i]);
@@ -3106,7 +3128,7 @@ int or_write_checkpoint(or_campaign_t *c, uint64_t ninst, const char *dir) {
     if (!gz || !f) { free(vpns); free(data); mach_free(&m); if (f) fclose(f); snprintf(c->err, sizeof c->err, "write %s", dir); return -1; }
     fprintf(f, "## checkpoint generated by oracle/rv64se.c:or_write_checkpoint at numInst %llu\n\n",
             (unsigned long long)ninst);
-    fprintf(f, "[Globals]\ncurTick=%llu\n\n", (unsigned long long)(m.num_cycles * c->clk_period));
+    fprintf(f, "[Globals]\ncurTick=%llu\n\n", (unsigned long long)(c->tick0 + m.num_cycles * c->clk_period));
     fprintf(f, "[system.cpu.xc.0]\n_status=1\n");
     uint8_t ib[33 * 8], fb[32 * 8];
     memset(ib, 0, sizeof ib);
@@ -3114,8 +3136,18 @@ int or_write_checkpoint(or_campaign_t *c, uint64_t ninst, const char *dir) {
     for (int r = 0; r < 32; r++) for (int b = 0; b < 8; b++) fb[r * 8 + b] = (uint8_t)(m.f[r] >> (8 * b));
     cpt_bytes(f, "regs.integer", ib, 33 * 8);
     cpt_bytes(f, "regs.floating_point", fb, 32 * 8);
-    fprintf(f, "_pc=%llu\n_upc=0\n_npc=%llu\n_nupc=1\n_rvType=1\n_compressed=false\n\n", (unsigned long long)m.pc,
-            (unsigned long long)(m.pc + 4));
+    /* PCState (generic/pcstate.hh:141-145, 329-333; riscv/pcstate.hh:146-156): vtype/vl as at
+     * process start (vill), the only vector configuration the engine models */
+    fprintf(f, "_pc=%llu\n_upc=0\n_npc=%llu\n_nupc=1\n_rvType=1\n_new_vconf=false\n_vtype=%llu\n_vl=0\n"
+               "_compressed=false\n_zcmtSecondFetch=false\n_zcmtPc=0\n\n",
+            (unsigned long long)m.pc, (unsigned long long)(m.pc + 4), 1ULL << 63);
+    /* the ISA's misc registers (ISA::serialize, isa.cc:977-983: miscRegFile,
+     * NUM_PHYS_MISCREGS values in MiscRegIndex order, regs/misc.hh); the
+     * oracle models fflags and frm (indices in tests/golden/riscv_miscreg.json) */
+    fprintf(f, "[system.cpu.isa]\nmiscRegFile=");
+    for (int i = 0; i < CPT_NUM_MISC; i++)
+        fprintf(f, i ? " %u" : "%u", i == CPT_MISC_FFLAGS ? m.fflags : i == CPT_MISC_FRM ? m.frm : 0u);
+    fprintf(f, "\n\n");
     fprintf(f, "[system.cpu.workload]\nbrkPoint=%llu\nstackBase=%llu\nstackSize=%llu\nmaxStackSize=%llu\n"
                "stackMin=%llu\nnextThreadStackBase=%llu\nmmapEnd=%llu\n\n",
             (unsigned long long)m.brk, (unsigned long long)STACK_BASE, (unsigned long long)(STACK_BASE - m.stack_min),
@@ -3190,6 +3222,19 @@ static u64 cpt_u64(const cpt_t *t, const char *sec, const char *key, int *ok) {
     return strtoull(v, NULL, 0);
 }
 
+/* Memory-fault candidates of a checkpoint start: as at process start (the
+ * ELF's writable segments and the stack), every mapped page that no read-only
+ * PT_LOAD segment covers -- writable segments, stack, heap and mmap pages. */
+static int cpt_fault_page(const or_campaign_t *c, u64 va) {
+    int ro = 0;
+    for (int i = 0; i < c->nseg; i++)
+        if (va >= c->seg[i].lo && va < c->seg[i].hi) {
+            if (c->seg[i].w) return 1;
+            ro = 1;
+        }
+    return !ro;
+}
+
 or_campaign_t *or_create_checkpoint(const char *dir, const uint8_t *elf, size_t len) {
     or_campaign_t *c = or_create(elf, len, "checkpoint");
     if (c->err[0]) return c;
@@ -3213,28 +3258,57 @@ or_campaign_t *or_create_checkpoint(const char *dir, const uint8_t *elf, size_t 
         v = e;
     }
     const char *fv = cpt_get(&t, xc, "regs.floating_point");
-    while (fv && *fv) {
+    memset(c->f0, 0, sizeof c->f0);
+    for (int i = 0; i < 32 * 8 && fv && *fv; i++) {
         char *e;
         unsigned long b = strtoul(fv, &e, 10);
         if (e == fv) break;
-        if (b) { snprintf(c->err, sizeof c->err, "FP registers hold state (not supported)"); cpt_free(&t); return c; }
+        c->f0[i / 8] |= (u64)(b & 0xFF) << (8 * (i % 8));
         fv = e;
     }
+    /* fflags / frm from the ISA's miscRegFile (absent: zero) */
+    c->fflags0 = c->frm0 = 0;
+    char isa[512];
+    if (!cpt_find(&t, "miscRegFile", isa, sizeof isa)) {
+        const char *mv = cpt_get(&t, isa, "miscRegFile");
+        for (int i = 0; mv && *mv && i <= CPT_MISC_FRM; i++) {
+            char *e;
+            unsigned long long v = strtoull(mv, &e, 10);
+            if (e == mv) break;
+            if (i == CPT_MISC_FFLAGS) c->fflags0 = (u32)(v & 0x1F);
+            if (i == CPT_MISC_FRM) c->frm0 = (u32)(v & 7);
+            mv = e;
+        }
+    }
+    /* vector configuration: only the process-start one (vtype.vill, vl 0) */
+    const char *vt = cpt_get(&t, xc, "_vtype"), *vlv = cpt_get(&t, xc, "_vl");
+    if ((vt && strtoull(vt, NULL, 0) != (1ULL << 63)) || (vlv && strtoull(vlv, NULL, 0) != 0)) {
+        snprintf(c->err, sizeof c->err, "unsupported checkpoint (vector configuration set: vtype/vl)");
+        cpt_free(&t); return c;
+    }
+    const char *gt = cpt_get(&t, "Globals", "curTick");
+    c->tick0 = gt ? strtoull(gt, NULL, 0) : 0;
     c->pc0 = cpt_u64(&t, xc, "_pc", &ok);
     c->brk0 = cpt_u64(&t, ps, "brkPoint", &ok);
     u64 sbase = cpt_u64(&t, ps, "stackBase", &ok), smax = cpt_u64(&t, ps, "maxStackSize", &ok);
     u64 smin = cpt_u64(&t, ps, "stackMin", &ok), mend = cpt_u64(&t, ps, "mmapEnd", &ok);
     snprintf(sec, sizeof sec, "%s.vmalist", ps);
     u64 nv = cpt_u64(&t, sec, "size", &ok);
-    snprintf(sec, sizeof sec, "%s.vmalist.Vma0", ps);
-    const char *vn = cpt_get(&t, sec, "name");
-    if (!ok || sbase != STACK_BASE || smax != MAX_STACK || mend != 0x4000000000000000ULL || nv != 1 || !vn ||
-        strcmp(vn, "stack")) {
-        snprintf(c->err, sizeof c->err, "unsupported checkpoint (process state beyond RiscvProcess64's stack VMA)");
+    if (!ok || sbase != STACK_BASE || smax != MAX_STACK || nv > 64) {
+        snprintf(c->err, sizeof c->err, "unsupported checkpoint (stack base / max stack differ from RiscvProcess64's, "
+                                        "or more than 64 VMAs)");
         cpt_free(&t); return c;
     }
-    c->stack_vma_lo = cpt_u64(&t, sec, "addrRangeStart", &ok);
-    c->stack_vma_hi = cpt_u64(&t, sec, "addrRangeEnd", &ok);
+    /* MemState VMA list (mem_state.hh:199-209), in order */
+    c->nvma0 = (int)nv;
+    for (u64 i = 0; i < nv; i++) {
+        snprintf(sec, sizeof sec, "%s.vmalist.Vma%llu", ps, (unsigned long long)i);
+        c->vma0[i].lo = cpt_u64(&t, sec, "addrRangeStart", &ok);
+        c->vma0[i].hi = cpt_u64(&t, sec, "addrRangeEnd", &ok);
+        const char *vn = cpt_get(&t, sec, "name");
+        if (vn && !strcmp(vn, "stack")) { c->stack_vma_lo = c->vma0[i].lo; c->stack_vma_hi = c->vma0[i].hi; }
+    }
+    c->mmap_end0 = mend;
     c->stack_min0 = smin & PAGE_MASK;
     c->sp0 = c->regs0[2];
     /* page table + memory store (frames read in paddr order) */
@@ -3268,7 +3342,7 @@ or_campaign_t *or_create_checkpoint(const char *dir, const uint8_t *elf, size_t 
         if (!ok || at != pa[i] || gzread(gz, pg, (unsigned)PAGE) != (int)PAGE) { free(pg); ok = 0; break; }
         at += PAGE;
         pm_insert(&c->image, va[i] >> 12, pg, 1);
-        if (va[i] >= c->text_hi || va[i] + PAGE <= c->text_lo) mp[nmem++] = va[i];
+        if (cpt_fault_page(c, va[i])) mp[nmem++] = va[i];
     }
     gzclose(gz);
     for (u64 i = 1; i < nmem; i++)

@@ -19,8 +19,10 @@
 //   memory            [<system>.physmem] nbr_of_stores + [.storeN] filename,
 //                     range_size; the file is the store's bytes, gzip-compressed
 //                     (PhysicalMemory::serializeStore, src/mem/physical.cc:363-405)
-// Host code; the product reads only what SE trials need: pages, registers,
-// pc, brk point, the stack VMA.  Parity with a checkpoint written by a real
+//   ISA               [<cpu>.isa] miscRegFile (fflags, frm); the PC state's
+//                     _vtype/_vl (riscv/pcstate.hh:146-156); [Globals] curTick
+// Host code; the product reads what SE trials need: pages, integer and FP
+// registers, fcsr, pc, brk point, the VMA list, mmap end and curTick.  Parity with a checkpoint written by a real
 // gem5 is unpinned (no gem5 build here); the format is pinned by the
 // oracle's writer (oracle/rv64se.c:or_write_checkpoint) and by round trips
 // against runs from process start (tests/test_checkpoint.py).
@@ -42,6 +44,8 @@
 namespace fi {
 
 namespace {
+
+constexpr int kMiscFflags = 120, kMiscFrm = 121;   // MiscRegIndex: MISCREG_FFLAGS, MISCREG_FRM
 
 using Ini = std::map<std::string, std::map<std::string, std::string>>;
 
@@ -101,9 +105,32 @@ std::string read_gem5_checkpoint(const std::string &dir, CptImage &img) {
         for (int b = 0; b < 8; b++) v |= (uint64_t)ir[r * 8 + b] << (8 * b);
         img.regs[r] = r ? v : 0;
     }
-    if (X.count("regs.floating_point"))
-        for (uint8_t b : byte_array(X.at("regs.floating_point"))) img.fp_state |= b != 0;
+    if (X.count("regs.floating_point")) {
+        const std::vector<uint8_t> fr = byte_array(X.at("regs.floating_point"));
+        for (size_t i = 0; i < fr.size() && i < 32 * 8; i++) img.fregs[i / 8] |= (uint64_t)fr[i] << (8 * (i % 8));
+    }
+    // fflags and frm: the ISA's misc registers (ISA::serialize, src/arch/riscv/
+    // isa.cc:977-983, miscRegFile in MiscRegIndex order, regs/misc.hh;
+    // indices pinned by tests/golden/riscv_miscreg.json)
+    if (const std::string *is = find_section_with(ini, "miscRegFile")) {
+        std::istringstream in(ini.at(*is).at("miscRegFile"));
+        unsigned long long v;
+        for (int i = 0; i <= kMiscFrm && (in >> v); i++) {
+            if (i == kMiscFflags) img.fflags = (uint32_t)(v & 0x1F);
+            if (i == kMiscFrm) img.frm = (uint32_t)(v & 7);
+        }
+    }
+    for (uint64_t f : img.fregs) img.fp_state |= f != 0;
+    img.fp_state |= img.fflags != 0 || img.frm != 0;
+    // the vector configuration lives in the PC state (riscv/pcstate.hh:146-156):
+    // only the process-start one (vtype.vill, vl = 0) is modelled
+    uint64_t vt = 1ULL << 63, vlen = 0;
+    get_u64(X, "_vtype", vt);
+    get_u64(X, "_vl", vlen);
+    if (vt != (1ULL << 63) || vlen != 0) return "vector configuration set (vtype/vl): not supported";
     if (!get_u64(X, "_pc", img.pc)) return "no _pc in " + *xc;
+    auto gl = ini.find("Globals");
+    if (gl != ini.end()) get_u64(gl->second, "curTick", img.tick0);
     // the process: MemState, VMA list, page table
     const std::string *ps = find_section_with(ini, "brkPoint");
     if (!ps) return "no process (brkPoint) in m5.cpt";

@@ -42,14 +42,22 @@ hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, 
 hipError_t sort_pairs_bytes(uint64_t n, size_t &bytes);
 hipError_t launch_pack_runs(const uint64_t *keys, const uint32_t *cnt, uint64_t cap, uint32_t *wrange,
                             uint32_t *n_waves, hipStream_t st);
+hipError_t launch_redo_collect(const fi_outcome *out, uint64_t n, uint32_t *idx, uint32_t *cnt,
+                               unsigned long long *stats, hipStream_t st);
+hipError_t launch_redo_gather(const fi_site *sites, const uint32_t *idx, uint64_t n, fi_site *rsites, uint64_t *keys,
+                              uint32_t *perm, hipStream_t st);
+hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome *rout, fi_outcome *out,
+                               hipStream_t st);
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
-                            uint64_t text_lo,
-                            uint64_t *keys, uint32_t *vals, hipStream_t st);
+                            uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, hipStream_t st);
+hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,
+                            hipStream_t st);
 std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
                              const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
-                             uint32_t &n_insts);
+                             uint32_t &n_insts, bool odd_streams);
 std::vector<fi_issue_op> issue_ops_from_trace(const std::vector<PreInst> &pre, const std::vector<uint32_t> &trace);
 std::string jit_compile(const std::string &body, const char *arch, std::vector<char> &code, bool &cached);
+bool jit_has_odd(const std::string &body);
 hipError_t sort_pairs(void *tmp, size_t bytes, const uint64_t *kin, uint64_t *kout, const uint32_t *vin,
                       uint32_t *vout, uint64_t n, int end_bit, hipStream_t st);
 }  // namespace fi
@@ -69,6 +77,7 @@ struct fi_engine {
     double last_ms = 0;
     // per-launch timing of the interpreter kernel (bench roofline)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tpool;
+    std::vector<uint32_t> tkind;
     size_t tused = 0;
 
     // process image (host copy)
@@ -77,6 +86,16 @@ struct fi_engine {
     uint64_t entry = 0, sp0 = 0, stack_min0 = 0, svma_lo = 0, svma_hi = 0;
     uint64_t text_lo = 0, text_hi = 0, code_lo = 0, code_hi = 0;
     std::vector<uint64_t> mem_pages;   // memory fault candidates (sorted)
+    struct Seg { uint64_t lo, hi; bool w; };
+    std::vector<Seg> segs;             // PT_LOAD page ranges of the ELF (w = PF_W)
+    // checkpoint start state beyond registers, pages and the stack VMA
+    bool fp0_on = false, vm0_on = false;
+    uint64_t fp0[32] = {};
+    uint32_t fcsr0 = 0;
+    uint64_t tick0 = 0;
+    VmState vm0{};
+    uint64_t *d_fp0 = nullptr;
+    VmState *d_vm0 = nullptr;
 
     // device image: snapshot 0 = the process-start image; the golden run
     // appends snapshots 1..n-1
@@ -105,6 +124,10 @@ struct fi_engine {
     // load-time build of the trial kernel with the translated golden blocks
     hipModule_t tx_mod = nullptr;
     hipFunction_t tx_fn = nullptr, tx_fn_solo = nullptr;
+    hipFunction_t tx_fn_odd = nullptr;   // solo kernel with the odd-pc blocks (nullptr: none translated)
+    // the solo-odd kernel runs beside the solo kernel on its own stream
+    hipStream_t stream_odd = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::string tx_status = "no golden run";
     std::string tx_body;   // last generated translation (diagnostics)
 
@@ -158,6 +181,11 @@ struct fi_engine {
     uint64_t *d_skeys = nullptr, *d_skeys2 = nullptr;
     uint32_t *d_svals = nullptr, *d_svals2 = nullptr;
     uint32_t *d_wrange = nullptr, *d_nwaves = nullptr;   // packed resume (FI_CFG_PACK_RUNS)
+    uint32_t *d_split = nullptr;   // per epoch: odd-pc survivors, then the solo kernel's share of the list
+    // second pass of the trials that ran out of private pages (run_chunk)
+    uint32_t *d_redo_idx = nullptr, *d_redo_cnt = nullptr, *h_redo_cnt = nullptr;
+    fi_site *d_redo_sites = nullptr;
+    fi_outcome *d_redo_out = nullptr;
 };
 
 static fi_status fail(fi_engine *e, fi_status code, const char *fmt, ...) {
@@ -240,7 +268,10 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
         return FI_E_ARG;
     }
     if (hipSetDevice(e->dev) != hipSuccess || hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess) {
+        hipStreamCreateWithFlags(&e->stream_odd, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&e->ev0) != hipSuccess || hipEventCreate(&e->ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess) {
         g_create_err = "fi_create: HIP stream/event creation failed on device " + std::to_string(e->dev);
         delete e;
         return FI_E_HIP;
@@ -269,7 +300,8 @@ static void free_work(fi_engine *e) {
     dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg); dfree(e->d_fregs);
     dfree(e->d_save); dfree(e->d_surv[0]); dfree(e->d_surv[1]); dfree(e->d_cnt);
     dfree(e->d_eff);
-    dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_wrange); dfree(e->d_nwaves); dfree(e->d_priv); dfree(e->d_priv_vpn); dfree(e->d_vm);
+    dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_wrange); dfree(e->d_nwaves); dfree(e->d_split); dfree(e->d_priv); dfree(e->d_priv_vpn); dfree(e->d_vm);
+    dfree(e->d_redo_idx); dfree(e->d_redo_cnt); dfree(e->d_redo_sites); dfree(e->d_redo_out);
     e->cap = 0;
 }
 static void free_snaps(fi_engine *e) { dfree(e->d_snaps); dfree(e->d_tab); dfree(e->d_pool); }
@@ -285,11 +317,14 @@ static void free_fw(fi_engine *e) {
 static void free_tx(fi_engine *e) {
     if (e->tx_mod) (void)hipModuleUnload(e->tx_mod);
     e->tx_mod = nullptr;
-    e->tx_fn = e->tx_fn_solo = nullptr;
+    e->tx_fn = e->tx_fn_solo = e->tx_fn_odd = nullptr;
 }
 static void free_image(fi_engine *e) {
     dfree(e->d_pre); dfree(e->d_zero); dfree(e->d_sink);
     dfree(e->d_text); dfree(e->d_mem_pages); dfree(e->d_gout); dfree(e->d_gerr); dfree(e->d_exe);
+    dfree(e->d_fp0); dfree(e->d_vm0);
+    e->fp0_on = e->vm0_on = false;
+    e->tick0 = 0;
     free_snaps(e);
     free_mem_index(e);
     free_fw(e);
@@ -310,6 +345,10 @@ void fi_destroy(fi_engine *e) {
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->stream_odd) (void)hipStreamDestroy(e->stream_odd);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+    if (e->h_redo_cnt) (void)hipHostFree(e->h_redo_cnt);
     delete e;
 }
 
@@ -417,6 +456,7 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
     free_image(e);
     e->pages.clear();
     e->mem_pages.clear();
+    e->segs.clear();
     if (len < 64 || memcmp(elf, "\x7f" "ELF", 4) || elf[4] != 2 || elf[5] != 1 || le16(elf + 18) != 243)
         return fail(e, FI_E_ELF, "not an ELF64 little-endian RISC-V executable");
     e->entry = le64(elf + 24);
@@ -437,6 +477,7 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
         img_write(e, paddr, elf + off, filesz);          // loaded at p_paddr (elf_object.cc:383)
         if (memsz > filesz) img_write(e, paddr + filesz, nullptr, memsz - filesz);
         max_addr = std::max(max_addr, paddr + memsz);
+        e->segs.push_back({paddr & ~(kPage - 1), (paddr + memsz + kPage - 1) & ~(kPage - 1), (flags & 2) != 0});
         if (off <= phoff && off + filesz > phoff) phdr_vaddr = vaddr + (phoff - off);
         if (flags & 1) {
             xlo = std::min(xlo, paddr & ~(kPage - 1));
@@ -566,27 +607,56 @@ fi_status fi_load_checkpoint(fi_engine *e, const char *cpt_dir, const uint8_t *e
     CptImage img;
     const std::string err = read_gem5_checkpoint(cpt_dir, img);
     if (!err.empty()) return fail(e, FI_E_ARG, "fi_load_checkpoint: %s", err.c_str());
-    // what the engine's SE model starts from (RiscvProcess64, process.cc:71-82)
-    if (img.fp_state) return fail(e, FI_E_ARG, "fi_load_checkpoint: FP registers hold state (not supported)");
-    if (img.stack_base != kStackBase || img.max_stack != kMaxStack || img.mmap_end != 0x4000000000000000ULL)
-        return fail(e, FI_E_ARG, "fi_load_checkpoint: stack base / max stack / mmap end differ from RiscvProcess64's");
-    if (img.vmas.size() != 1 || img.vma_names[0] != "stack")
-        return fail(e, FI_E_ARG, "fi_load_checkpoint: %zu VMAs (only the stack VMA is supported)", img.vmas.size());
+    // the engine's SE model keeps RiscvProcess64's stack (process.cc:71-82)
+    if (img.stack_base != kStackBase || img.max_stack != kMaxStack)
+        return fail(e, FI_E_ARG, "fi_load_checkpoint: stack base / max stack differ from RiscvProcess64's");
+    if (img.vmas.size() > kMaxVma)
+        return fail(e, FI_E_ARG, "fi_load_checkpoint: %zu VMAs (at most %u)", img.vmas.size(), kMaxVma);
+    const std::vector<fi_engine::Seg> segs = e->segs;   // (fi_load_elf's; free_image keeps them)
     free_image(e);
     e->pages.clear();
     for (auto &kv : img.pages) e->pages[kv.first] = kv.second;
-    // memory-fault candidates: every mapped page outside the executable range
+    // memory-fault candidates, as at process start (the ELF's writable
+    // segments and the stack): every mapped page no read-only PT_LOAD covers
     e->mem_pages.clear();
     for (auto &kv : img.pages) {
         const uint64_t a = kv.first << 12;
-        if (a >= e->text_hi || a + kPage <= e->text_lo) e->mem_pages.push_back(a);
+        bool ro = false, w = false;
+        for (const fi_engine::Seg &g : segs)
+            if (a >= g.lo && a < g.hi) (g.w ? w : ro) = true;
+        if (w || !ro) e->mem_pages.push_back(a);
     }
     e->brk0 = img.brk;
-    e->svma_lo = img.vmas[0].first;
-    e->svma_hi = img.vmas[0].second;
+    e->svma_lo = e->svma_hi = 0;
+    for (size_t i = 0; i < img.vmas.size(); i++)
+        if (img.vma_names[i] == "stack") { e->svma_lo = img.vmas[i].first; e->svma_hi = img.vmas[i].second; }
+    // a VMA list other than argsInit's lone stack VMA, or another mmap end:
+    // the trials start from it (DevCtx::vm0)
+    const bool plain = img.vmas.size() == 1 && img.vma_names[0] == "stack" && img.mmap_end == 0x4000000000000000ULL;
+    e->vm0_on = !plain;
+    if (e->vm0_on) {
+        e->vm0 = VmState{};
+        e->vm0.brk = img.brk; e->vm0.mmap_end = img.mmap_end;
+        e->vm0.nvma = (uint32_t)img.vmas.size();
+        for (size_t i = 0; i < img.vmas.size(); i++) { e->vm0.vma[i][0] = img.vmas[i].first; e->vm0.vma[i][1] = img.vmas[i].second; }
+    }
+    e->fp0_on = img.fp_state;
+    memcpy(e->fp0, img.fregs, sizeof e->fp0);
+    e->fcsr0 = img.fflags | (img.frm << 5);
+    e->tick0 = img.tick0;
     e->sp0 = img.regs[2];
     e->stack_min0 = img.stack_min & ~(kPage - 1);
-    return finish_load(e, img.regs, img.pc);
+    fi_status st2 = finish_load(e, img.regs, img.pc);
+    if (st2) return st2;
+    if (e->vm0_on) {
+        HIPCHK(hipMalloc(&e->d_vm0, sizeof(VmState)));
+        HIPCHK(hipMemcpy(e->d_vm0, &e->vm0, sizeof(VmState), hipMemcpyHostToDevice));
+    }
+    if (e->fp0_on) {
+        HIPCHK(hipMalloc(&e->d_fp0, 32 * 8));
+        HIPCHK(hipMemcpy(e->d_fp0, e->fp0, 32 * 8, hipMemcpyHostToDevice));
+    }
+    return FI_OK;
 }
 
 static fi_status ensure_work(fi_engine *e, uint64_t n) {
@@ -619,6 +689,12 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_svals2, c * 4));
     HIPCHK(hipMalloc(&e->d_wrange, c * 8));
     HIPCHK(hipMalloc(&e->d_nwaves, 16 * 4));
+    HIPCHK(hipMalloc(&e->d_split, 64 * 4));
+    HIPCHK(hipMalloc(&e->d_redo_idx, c * 4));
+    HIPCHK(hipMalloc(&e->d_redo_cnt, 16));
+    HIPCHK(hipMalloc(&e->d_redo_sites, c * sizeof(fi_site)));
+    HIPCHK(hipMalloc(&e->d_redo_out, c * sizeof(fi_outcome)));
+    if (!e->h_redo_cnt) HIPCHK(hipHostMalloc(&e->h_redo_cnt, 16));
     e->cap = c;
     return FI_OK;
 }
@@ -653,6 +729,10 @@ static DevCtx base_ctx(fi_engine *e) {
     c.simt_min = (e->cfg.flags & FI_CFG_SIMT) ? 8u : 0u;
     c.rnd_tab = e->d_rnd; c.rnd_len = e->d_rnd ? kRndLen : 0; c.clk_period = e->clk_period;
     c.exe_path = e->d_exe; c.exe_len = e->d_exe ? e->exe_path.size() : 0;
+    c.tick0 = e->tick0;
+    c.fp0 = e->fp0_on ? e->d_fp0 : nullptr;
+    c.fcsr0 = e->fcsr0;
+    c.vm0 = e->vm0_on ? e->d_vm0 : nullptr;
     c.lanes = e->cfg.lanes_per_wave;
     c.mem_live = (e->mem_live && !(e->cfg.flags & FI_CFG_NO_EARLY_EXIT)) ? 1 : 0;
     c.mw_n = e->mw_n; c.mw_addr = e->d_mw_addr; c.mw_off = e->d_mw_off; c.mw_ev = e->d_mw_ev;
@@ -991,7 +1071,11 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         const std::vector<uint64_t> pcs;
         std::vector<uint32_t> leaders;
         uint32_t n_tx = 0;
-        const std::string body = translate_blocks(pre, e->text_lo, trace, pcs, leaders, n_tx);
+        std::string body = translate_blocks(pre, e->text_lo, trace, pcs, leaders, n_tx, true);
+        if (n_tx > 24000) {   // the odd-pc streams make it too large: without them
+            leaders.clear();
+            body = translate_blocks(pre, e->text_lo, trace, pcs, leaders, n_tx, false);
+        }
         e->tx_body = body;
         hipDeviceProp_t prop;
         HIPCHK(hipGetDeviceProperties(&prop, e->dev));
@@ -1013,7 +1097,9 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
             e->tx_status = err;
         } else if (hipModuleLoadData(&e->tx_mod, code.data()) != hipSuccess ||
                    hipModuleGetFunction(&e->tx_fn, e->tx_mod, "fi_trial_kernel_tx") != hipSuccess ||
-                   hipModuleGetFunction(&e->tx_fn_solo, e->tx_mod, "fi_trial_kernel_tx_solo") != hipSuccess) {
+                   hipModuleGetFunction(&e->tx_fn_solo, e->tx_mod, "fi_trial_kernel_tx_solo") != hipSuccess ||
+                   (jit_has_odd(body) &&
+                    hipModuleGetFunction(&e->tx_fn_odd, e->tx_mod, "fi_trial_kernel_tx_solo_odd") != hipSuccess)) {
             free_tx(e);
             e->tx_status = "code object did not load";
         } else {
@@ -1180,8 +1266,23 @@ static hipError_t launch_trial_kernel(fi_engine *e, DevCtx &c, hipStream_t st, b
                                  nullptr);
 }
 
-// One launch: d_sites[0..k) holds the sites in trial order, keys/perm set.
-static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histogram *d_hist, hipStream_t st) {
+// The event pair of the next trial-kernel dispatch (kind: 0 the 64-lane
+// kernel, 1 solo, 2 solo-odd; fi_debug_dispatch_ms).
+static std::pair<hipEvent_t, hipEvent_t> &timer_slot(fi_engine *e, uint32_t kind) {
+    if (e->tused == e->tpool.size()) {
+        hipEvent_t a = nullptr, b = nullptr;
+        (void)hipEventCreate(&a);
+        (void)hipEventCreate(&b);
+        e->tpool.emplace_back(a, b);
+        e->tkind.push_back(0);
+    }
+    e->tkind[e->tused] = kind;
+    return e->tpool[e->tused++];
+}
+
+// One pass over sites[0..k) (keys/perm set) with P private pages per slot:
+// forwarding, sort by inject time, the epochs.  Outcomes to d_out.
+static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *d_out, uint32_t P, hipStream_t st) {
     int end_bit = 64 - __builtin_clzll(std::max<uint64_t>(e->golden.ninst, 1));
     // (a dead site ends at injection: an early exit, so not with FI_CFG_NO_EARLY_EXIT)
     const bool fwd = e->fw_ok && !(e->cfg.flags & (FI_CFG_NO_FORWARD | FI_CFG_NO_EARLY_EXIT));
@@ -1195,18 +1296,18 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
         fc.mw_addr = e->d_mw_addr; fc.mw_off = e->d_mw_off; fc.mw_ev = e->d_mw_ev;
         fc.snaps = e->d_snaps; fc.snap_tab = e->d_tab; fc.n_snap = (uint32_t)e->snaps.size();
         fc.snap_interval = e->snap_I; fc.text_lo = e->text_lo; fc.text_hi = e->text_hi;
-        HIPCHK(launch_forward(e->d_sites, k, fc, e->d_keys, e->d_eff, st));
+        HIPCHK(launch_forward(sites, k, fc, e->d_keys, e->d_eff, st));
     }
     HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_keys, e->d_keys2, e->d_perm, e->d_perm2, k, end_bit, st));
     DevCtx c = base_ctx(e);
-    c.sites = e->d_sites;
+    c.sites = sites;
     c.perm = e->d_perm2;
     c.eff = fwd ? e->d_eff : nullptr;
     c.out = d_out;
     c.n = k;
     c.n_slots = (uint32_t)k;
     c.save = e->d_save;
-    HIPCHK(hipMemsetAsync(e->d_stats, 0, kNStats * sizeof(unsigned long long), st));
+    c.priv_pages = P;
     HIPCHK(hipMemsetAsync(e->d_cnt, 0, 16 * 4, st));
     HIPCHK(hipMemsetAsync(e->d_wave_dbg, 0, k * 10 * sizeof(uint64_t), st));
     const bool pack = (e->cfg.flags & FI_CFG_PACK_RUNS) != 0;
@@ -1231,9 +1332,15 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
         for (uint32_t i = 0; i + 1 < n_ep; i++) budgets.push_back(b << (2 * std::min(i, 2u)));
         budgets.push_back(0);
     }
-    HIPCHK(hipEventRecord(e->ev0, st));
+    // the odd-pc survivors of a resumed solo epoch run on the solo-odd kernel
+    // (at most kOddGrid of them; the rest stay with the solo kernel), on its
+    // own stream beside the solo kernel
+    constexpr uint32_t kOddGrid = 2048;
+    const bool odd_on = e->tx_fn_odd && e->tx_fn_solo && !(e->cfg.flags & FI_CFG_NO_ODD_KERNEL);
+    if (odd_on) HIPCHK(hipMemsetAsync(e->d_split, 0, 64 * 4, st));
     for (size_t ep = 0; ep < budgets.size(); ep++) {
         const bool solo = (e->cfg.flags & FI_CFG_SOLO_ALL) || (ep > 0 && !(e->cfg.flags & FI_CFG_NO_SOLO));
+        const bool odd = odd_on && solo && ep > 0 && ep < 16;
         c.wave_budget = budgets[ep];
         c.surv = e->d_surv[ep & 1];
         c.surv_n = e->d_cnt + ep;
@@ -1246,10 +1353,26 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
             c.resume_n = nullptr;
         } else {
             HIPCHK(launch_surv_keys(e->d_save, e->d_surv[(ep - 1) & 1], e->d_cnt + ep - 1, k, c.text_lo, e->d_skeys,
-                                    e->d_svals, st));
+                                    e->d_svals, odd ? e->d_split + 4 * ep : nullptr, st));
             HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_skeys, e->d_skeys2, e->d_svals, e->d_svals2, k, 64, st));
             c.resume = e->d_svals2;
             c.resume_n = e->d_cnt + ep - 1;
+            if (odd) {   // odd survivors sort last: the solo kernel takes [0, split), the solo-odd kernel the rest
+                const uint32_t grid = (uint32_t)std::min<uint64_t>(k, kOddGrid);
+                HIPCHK(launch_odd_split(c.resume_n, e->d_split + 4 * ep, e->d_split + 4 * ep + 1, grid, st));
+                DevCtx co = c;
+                co.lanes = 1; co.resume_waves = 0; co.wrange = nullptr; co.n_waves = nullptr;
+                co.resume_lo = e->d_split + 4 * ep + 1;
+                c.resume_n = e->d_split + 4 * ep + 1;
+                HIPCHK(hipEventRecord(e->ev_fork, st));
+                HIPCHK(hipStreamWaitEvent(e->stream_odd, e->ev_fork, 0));
+                auto &tq = timer_slot(e, 2);
+                HIPCHK(hipEventRecord(tq.first, e->stream_odd));
+                void *args[] = {&co};
+                HIPCHK(hipModuleLaunchKernel(e->tx_fn_odd, grid, 1, 1, 1, 1, 1, 0, e->stream_odd, args, nullptr));
+                HIPCHK(hipEventRecord(tq.second, e->stream_odd));
+                HIPCHK(hipEventRecord(e->ev_join, e->stream_odd));
+            }
             if (pack && !solo) {
                 // one wave per same-pc run of survivors (<= 64 lanes); the grid
                 // covers the worst case (every survivor alone), surplus waves exit
@@ -1262,17 +1385,47 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
         }
         // every dispatch of the trial kernel is bracketed by its own event
         // pair on the launch stream (the bench's per-dispatch kernel time)
-        if (e->tused == e->tpool.size()) {
-            hipEvent_t a, b;
-            HIPCHK(hipEventCreate(&a));
-            HIPCHK(hipEventCreate(&b));
-            e->tpool.emplace_back(a, b);
-        }
-        auto &tp = e->tpool[e->tused++];
+        auto &tp = timer_slot(e, solo ? 1 : 0);
         HIPCHK(hipEventRecord(tp.first, st));
         if (solo) { c.lanes = 1; c.resume_waves = 0; c.wrange = nullptr; c.n_waves = nullptr; }
         HIPCHK(launch_trial_kernel(e, c, st, solo));
         HIPCHK(hipEventRecord(tp.second, st));
+        if (odd) HIPCHK(hipStreamWaitEvent(st, e->ev_join, 0));
+    }
+    return FI_OK;
+}
+
+// One launch: d_sites[0..k) holds the sites in trial order, keys/perm set.
+// Trials that ran out of private pages (FI_ESC_RESOURCE: an engine capacity
+// limit, not gem5 behaviour) run again with kRedoPages-fold pages, in batches
+// that reuse the same frames (batch x P' <= k x P), and their outcomes replace
+// the escapes before the histogram.  Costs one host sync per chunk for the
+// count; FI_CFG_NO_REDO skips it.
+static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histogram *d_hist, hipStream_t st) {
+    const uint32_t P = e->cfg.private_pages;
+    HIPCHK(hipMemsetAsync(e->d_stats, 0, kNStats * sizeof(unsigned long long), st));
+    HIPCHK(hipEventRecord(e->ev0, st));
+    fi_status s = run_pass(e, e->d_sites, k, d_out, P, st);
+    if (s) return s;
+    if (!(e->cfg.flags & FI_CFG_NO_REDO)) {
+        HIPCHK(hipMemsetAsync(e->d_redo_cnt, 0, 4, st));
+        HIPCHK(launch_redo_collect(d_out, k, e->d_redo_idx, e->d_redo_cnt, e->d_stats, st));
+        HIPCHK(hipMemcpyAsync(e->h_redo_cnt, e->d_redo_cnt, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        const uint64_t nr = *e->h_redo_cnt;
+        if (nr) {
+            const uint64_t pool = k * P;   // page frames the pass had
+            const uint64_t P2 = std::min<uint64_t>(pool, std::max<uint64_t>(P * 16ull, 256));
+            const uint64_t B = std::max<uint64_t>(1, pool / P2);
+            for (uint64_t d = 0; d < nr; d += B) {
+                const uint64_t b = std::min(B, nr - d);
+                HIPCHK(launch_redo_gather(e->d_sites, e->d_redo_idx + d, b, e->d_redo_sites, e->d_keys, e->d_perm,
+                                          st));
+                s = run_pass(e, e->d_redo_sites, b, e->d_redo_out, (uint32_t)P2, st);
+                if (s) return s;
+                HIPCHK(launch_redo_scatter(e->d_redo_idx + d, b, e->d_redo_out, d_out, st));
+            }
+        }
     }
     HIPCHK(hipEventRecord(e->ev1, st));
     HIPCHK(launch_hist(e->d_sites, d_out, k, d_hist, e->d_stats, st));
@@ -1420,7 +1573,7 @@ fi_status fi_debug_translate(const void *pre, uint64_t n_pre, uint64_t text_lo, 
     std::vector<uint32_t> t(trace, trace + n_trace);
     std::vector<uint32_t> leaders;
     uint32_t n_tx = 0;
-    const std::string body = translate_blocks(p, text_lo, t, {}, leaders, n_tx);
+    const std::string body = translate_blocks(p, text_lo, t, {}, leaders, n_tx, true);
     if (out && cap) {
         const uint64_t n = std::min<uint64_t>(cap - 1, body.size());
         memcpy(out, body.data(), n);
@@ -1441,10 +1594,10 @@ fi_status fi_debug_translation(fi_engine *e, char *buf, uint64_t cap, uint64_t *
     return FI_OK;
 }
 
-fi_status fi_debug_stats(fi_engine *e, uint64_t *out40) {
-    if (!e || !out40) return FI_E_ARG;
+fi_status fi_debug_stats(fi_engine *e, uint64_t *out64) {
+    if (!e || !out64) return FI_E_ARG;
     HIPCHK(hipStreamSynchronize(e->stream));
-    HIPCHK(hipMemcpy(out40, e->d_stats, kNStats * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out64, e->d_stats, kNStats * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return FI_OK;
 }
 
@@ -1481,6 +1634,13 @@ fi_status fi_debug_dispatch_ms(fi_engine *e, float *ms, uint32_t cap, uint32_t *
         HIPCHK(hipEventSynchronize(e->tpool[i].second));
         HIPCHK(hipEventElapsedTime(&ms[i], e->tpool[i].first, e->tpool[i].second));
     }
+    if (n) *n = (uint32_t)e->tused;
+    return FI_OK;
+}
+
+fi_status fi_debug_dispatch_kinds(fi_engine *e, uint32_t *kinds, uint32_t cap, uint32_t *n) {
+    if (!e || (!kinds && cap)) return FI_E_ARG;
+    for (size_t i = 0; i < e->tused && i < cap; i++) kinds[i] = e->tkind[i];
     if (n) *n = (uint32_t)e->tused;
     return FI_OK;
 }

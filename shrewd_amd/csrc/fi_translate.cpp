@@ -345,14 +345,15 @@ struct Block {
 // statically reachable from the executed code.  trace = halfword index per
 // golden event (bit 31: ecall).
 //
-// Two bodies are generated (joined by the marker FI_TX_SPLIT): the 64-lane one
-// (blocks B_*, guest registers X1..X31 in VGPRs, register writes as selects on
-// the running group, divergence parked and merged by the min-PC rule) and the
-// solo one for the one-trial-per-wave kernel (blocks S_*, every value
-// uniform, no groups).
+// Three bodies are generated (joined by the marker FI_TX_SPLIT): the 64-lane
+// one (blocks B_*, guest registers X1..X31 in VGPRs, register writes as
+// selects on the running group, divergence parked and merged by the min-PC
+// rule), the solo one for the one-trial-per-wave kernel (blocks S_*, every
+// value uniform, no groups) and the solo-odd one (the solo blocks again as Q_*
+// plus the odd-pc streams as QO_*; empty when there are none).
 std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
                              const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
-                             uint32_t &n_insts) {
+                             uint32_t &n_insts, bool odd_streams) {
     std::set<uint32_t> executed, leaders;
     auto valid = [&](uint32_t h) { return h < pre.size() && (pre[h].flags & kPreValid); };
     // only code the golden run executed more than once is translated: straight-
@@ -444,15 +445,15 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     // stays as the structurer made it).  Both odd pcs of a word lead together:
     // they share the key's kPreOddLeader flag, at which the interpreter hands
     // over.
-    // Off by default (SHREWD_FI_TX_ODD=1 turns it on): the odd blocks take a
-    // crc32 pc bit-0 tail trial from ~600 to ~128 ns per instruction and a
-    // qsort one from ~676 to ~275 ns, but they are ~2.7x the solo body's even
-    // code on crc32, and the larger solo kernel (SGPR spills 1.7k -> 8.3k)
-    // slows the whole solo epoch: crc32 bench 13.1M -> 11.7M trials/s,
-    // intmix 90k -> 83k, qsort 438k -> 444k (profiles/r02p_odd_ab.txt).
-    static const bool tx_odd = getenv("SHREWD_FI_TX_ODD") && atoi(getenv("SHREWD_FI_TX_ODD")) != 0;
+    // The odd blocks take a crc32 pc bit-0 tail trial from ~600 to ~128 ns
+    // per instruction and a qsort one from ~676 to ~275 ns, but they are ~2.7x
+    // the solo body's even code on crc32, and in the solo kernel itself (SGPR
+    // spills 1.7k -> 8.3k) they slowed the whole solo epoch by ~10 %
+    // (profiles/r02p_odd_ab.txt).  So they go into a third body (solo-odd: the
+    // even blocks again plus the odd ones, labels Q*) that only the survivors
+    // standing at an odd pc run (fi_trial_kernel_tx_solo_odd, fi_engine.cpp).
     std::set<uint64_t> odd;
-    if (tx_odd) {
+    if (odd_streams) {
         const size_t cap = 2 * golden_exec.size() + 1024;
         std::vector<uint64_t> work;
         for (uint32_t h : golden_exec) work.push_back(text_lo + 2ULL * h + 1);
@@ -560,6 +561,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         blocks.push_back(b);
     }
     bool cur_odd = false;   // generating an odd-pc block: every edge goes through the dispatch
+    bool oddon = false;     // generating the solo-odd body (even and odd blocks, labels Q*)
+    std::string SB = "S_", SD = "S_dispatch", SOB = "SO_";
 
     enum Edge { E_DIRECT, E_DISPATCH, E_OUT };
     auto edge = [&](uint32_t from, uint64_t pc) {
@@ -570,6 +573,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
 
     Gen g{pre, text_lo, leaders, executed, {}};
     Gen so{pre, text_lo, leaders, executed, {}};
+    Gen sq{pre, text_lo, leaders, executed, {}};
     n_insts = 0;
     auto hex = [](uint64_t v) {
         char b[32];
@@ -585,46 +589,61 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto tx_dispatch; }" : "; goto tx_out; }");
     };
     auto sgo = [&](uint32_t from, uint64_t pc) {
-        if (cur_odd || (pc & 1))
-            return "{ spc = " + hex(pc) + ((!(pc & 1) || olead.count(pc)) ? "; goto S_dispatch; }" : "; goto S_out; }");
+        if (oddon && (cur_odd || (pc & 1)))
+            return "{ spc = " + hex(pc) + ((!(pc & 1) || olead.count(pc)) ? "; goto " + SD + "; }" : "; goto S_out; }");
         const Edge k = edge(from, pc);
         uint32_t t = 0;
         hof(pc, t);
-        if (k == E_DIRECT) return "goto S_" + std::to_string(t) + ";";
-        return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto S_dispatch; }" : "; goto S_out; }");
+        if (k == E_DIRECT) return "goto " + SB + std::to_string(t) + ";";
+        return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto " + SD + "; }" : "; goto S_out; }");
     };
     g.put("tx_dispatch: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", (unsigned long long)text_lo);
     g.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto tx_out;\n  switch ((uint32_t)off_ >> 1) {\n");
-    so.put("S_dispatch: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", (unsigned long long)text_lo);
-    if (odd.empty()) {
-        so.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto S_out;\n  switch ((uint32_t)off_ >> 1) {\n");
-    } else {
-        so.put("  if ((off_ >> 32) != 0) goto S_out;\n  if (off_ & 1) switch ((uint32_t)off_ >> 1) {\n");
-        for (uint64_t pc : olead) {
-            const uint32_t i = (uint32_t)((pc - text_lo) >> 1);
-            so.put("  case %u: goto SO_%u;\n", i, i);
-        }
-        so.put("  default: goto S_out;\n  }\n  switch ((uint32_t)off_ >> 1) {\n");
-    }
     for (uint32_t h : leaders) {
         auto it = S.chain.find(h);
-        if (it == S.chain.end() || (it->second.size() == 1 && it->second[0] == h)) {
-            g.put("  case %u: goto B_%u;\n", h, h);
-            so.put("  case %u: goto S_%u;\n", h, h);
-        } else {
-            g.put("  case %u: etgt = %uu; goto B_%u;\n", h, h, it->second[0]);
-            so.put("  case %u: etgt = %uu; goto S_%u;\n", h, h, it->second[0]);
-        }
+        if (it == S.chain.end() || (it->second.size() == 1 && it->second[0] == h)) g.put("  case %u: goto B_%u;\n", h, h);
+        else g.put("  case %u: etgt = %uu; goto B_%u;\n", h, h, it->second[0]);
     }
     g.put("  default: goto tx_out;\n  }\n}\n");
-    so.put("  default: goto S_out;\n  }\n}\n");
+    // solo dispatch (plain or with the odd-pc entries)
+    auto sdispatch = [&](Gen &sx) {
+        sx.put("%s: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", SD.c_str(), (unsigned long long)text_lo);
+        if (!oddon) {
+            sx.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto S_out;\n  switch ((uint32_t)off_ >> 1) {\n");
+        } else {
+            sx.put("  if ((off_ >> 32) != 0) goto S_out;\n  if (off_ & 1) switch ((uint32_t)off_ >> 1) {\n");
+            for (uint64_t pc : olead) {
+                const uint32_t i = (uint32_t)((pc - text_lo) >> 1);
+                sx.put("  case %u: goto %s%u;\n", i, SOB.c_str(), i);
+            }
+            sx.put("  default: goto S_out;\n  }\n  switch ((uint32_t)off_ >> 1) {\n");
+        }
+        for (uint32_t h : leaders) {
+            auto it = S.chain.find(h);
+            if (it == S.chain.end() || (it->second.size() == 1 && it->second[0] == h))
+                sx.put("  case %u: goto %s%u;\n", h, SB.c_str(), h);
+            else
+                sx.put("  case %u: etgt = %uu; goto %s%u;\n", h, h, SB.c_str(), it->second[0]);
+        }
+        sx.put("  default: goto S_out;\n  }\n}\n");
+    };
 
-    static const bool tx_watch = !getenv("SHREWD_FI_TX_NOWATCH");   // A/B switch (diagnostics)
+    // mode 0: the 64-lane body and the plain solo body (even blocks); mode 1:
+    // the solo-odd body (even and odd blocks; its wave text is dropped)
+    for (int mode = 0; mode < 2; mode++) {
+    oddon = mode == 1;
+    if (oddon && odd.empty()) break;
+    SB = oddon ? "Q_" : "S_"; SD = oddon ? "Q_dispatch" : "S_dispatch"; SOB = oddon ? "QO_" : "SO_";
+    Gen &so_ = oddon ? sq : so;
+    std::string g_mode;
+    if (oddon) g_mode.swap(g.out);
+    sdispatch(so_);
     for (const Block &b : blocks) {
+        if (!oddon && b.opc != 0) continue;
         const uint32_t h0 = b.h0;
         const std::vector<uint32_t> &insts = b.insts;
         const uint32_t n = (uint32_t)insts.size();
-        n_insts += n;
+        if (!oddon || b.opc != 0) n_insts += n;
         cur_odd = b.opc != 0;
         std::string g_keep;   // an odd-pc block has no wave form: its wave text is dropped
         if (cur_odd) g_keep.swap(g.out);
@@ -637,7 +656,6 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             if ((p.flags & kPreRs2) && p.rs2) rw |= 1u << p.rs2;
             if ((p.flags & kPreRd) && p.rd) rw |= 1u << p.rd;
         }
-        if (!tx_watch) rw = 0;
         uint64_t blo = pc0 & ~3ULL, bhi = g.pc_of(insts.empty() ? h0 : insts.back()) + 6;
         if (cur_odd) {   // the bytes the keys cover
             blo = ~0ULL; bhi = 0;
@@ -648,9 +666,10 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         }
         g.put("B_%u: { // pc 0x%llx, %u insts\n", h0, (unsigned long long)pc0, n);
         if (cur_odd)
-            so.put("SO_%u: { // pc 0x%llx (odd)\n", (uint32_t)((pc0 - text_lo) >> 1), (unsigned long long)pc0);
+            so_.put("%s%u: { // pc 0x%llx (odd)\n", SOB.c_str(), (uint32_t)((pc0 - text_lo) >> 1),
+                    (unsigned long long)pc0);
         else
-            so.put("S_%u: { // pc 0x%llx, %u insts\n", h0, (unsigned long long)pc0, n);
+            so_.put("%s%u: { // pc 0x%llx, %u insts\n", SB.c_str(), h0, (unsigned long long)pc0, n);
         if (!cur_odd && S.headers.count(h0)) {   // a cycle header routes an entry into its cycle one level on (etgt)
             std::string rw_, rs_;
             for (uint32_t x : leaders) {
@@ -663,12 +682,12 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 // a nested header routes further, and clears etgt when it is the target
                 const std::string clr = S.headers.count(next) ? "" : "etgt = 0xFFFFFFFFu; ";
                 rw_ += "case " + std::to_string(x) + ": " + clr + "goto B_" + std::to_string(next) + "; ";
-                rs_ += "case " + std::to_string(x) + ": " + clr + "goto S_" + std::to_string(next) + "; ";
+                rs_ += "case " + std::to_string(x) + ": " + clr + "goto " + SB + std::to_string(next) + "; ";
             }
             const char *fmt = "  if (etgt != 0xFFFFFFFFu) { if (etgt == %uu) etgt = 0xFFFFFFFFu; "
                               "else switch (etgt) { %sdefault: break; } }\n";
             g.put(fmt, h0, rw_.c_str());
-            so.put(fmt, h0, rs_.c_str());
+            so_.put(fmt, h0, rs_.c_str());
         }
         // ---- wave block prologue: merge a parked group waiting here, leave or
         // switch groups when lanes outside run first, then one combined check
@@ -680,9 +699,9 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         g.put(" |\n      (wdirty & (TXB(mine && ldlo < %s && ldhi > %s) != 0))) { spc = %s; goto tx_out; }\n",
               hex(bhi).c_str(), hex(blo).c_str(), P0.c_str());
         // ---- solo block prologue: one uniform check
-        so.put("  if ((st + %uu > bud)", n);
-        if (rw) so.put(" | ((lwm & 0x%xu) != 0)", rw);
-        so.put(" | ((sdlo < %uu) & (sdhi > %uu))) { spc = %s; goto S_out; }\n", (uint32_t)(bhi - text_lo),
+        so_.put("  if ((st + %uu > bud)", n);
+        if (rw) so_.put(" | ((lwm & 0x%xu) != 0)", rw);
+        so_.put(" | ((sdlo < %uu) & (sdhi > %uu))) { spc = %s; goto S_out; }\n", (uint32_t)(bhi - text_lo),
                (uint32_t)(blo - text_lo), P0.c_str());
         uint32_t k_st = 0, k_xt = 0, k_fb = 0, k_db = 0;   // committed so far in this block
         auto commit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
@@ -723,7 +742,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 const std::string v = subst(e, A, B, immb, pcb);
                 if (p.rd) {
                     g.put("  TXSET(%u, %s);\n", p.rd, v.c_str());
-                    so.put("  SX(%u, %s);\n", p.rd, v.c_str());
+                    so_.put("  SX(%u, %s);\n", p.rd, v.c_str());
                 }
                 break;
             }
@@ -732,20 +751,20 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             case C_LOAD:
                 g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, false, p_, tx);\n", A.c_str(), immb, sz);
                 g.put("    if (TXB(mine && !ok_)) %s\n", leave_here.c_str());
-                so.put("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, false, p_, tx))) %s\n", A.c_str(), immb, sz,
+                so_.put("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, false, p_, tx))) %s\n", A.c_str(), immb, sz,
                        sleave_here.c_str());
                 if (p.rd) {
                     g.put("    p_ = ok_ ? p_ : const_cast<uint8_t *>(zp);\n");
                     if (sx) {
                         g.put("    TXSET(%u, (int64_t)(int%d_t)*(const g_%s *)p_); }\n", p.rd, sx, gtype(sz));
-                        so.put("    X%u = (uint64_t)(int64_t)(int%d_t)*(const g_%s *)p_; }\n", p.rd, sx, gtype(sz));
+                        so_.put("    X%u = (uint64_t)(int64_t)(int%d_t)*(const g_%s *)p_; }\n", p.rd, sx, gtype(sz));
                     } else {
                         g.put("    TXSET(%u, *(const g_%s *)p_); }\n", p.rd, gtype(sz));
-                        so.put("    X%u = *(const g_%s *)p_; }\n", p.rd, gtype(sz));
+                        so_.put("    X%u = *(const g_%s *)p_; }\n", p.rd, gtype(sz));
                     }
                 } else {
                     g.put("  }\n");
-                    so.put("  }\n");
+                    so_.put("  }\n");
                 }
                 break;
             case C_STORE:
@@ -754,10 +773,10 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 g.put("    p_ = (mine && ok_) ? p_ : sink; *(g_%s *)p_ = (%s)%s; }\n", gtype(sz), ltype(sz), B.c_str());
                 // solo: a store into the code range is performed too; it marks the
                 // bytes rewritten and leaves after itself if they lie ahead in this block
-                so.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s; const uint32_t cs_ = tx_probe_st(m, ea_, %uu, "
+                so_.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s; const uint32_t cs_ = tx_probe_st(m, ea_, %uu, "
                        "p_, tx); if (SCOND(!cs_)) %s\n", A.c_str(), immb, sz, sleave_here.c_str());
-                so.put("    *(g_%s *)p_ = (%s)%s;\n", gtype(sz), ltype(sz), B.c_str());
-                so.put("    if (SCOND(cs_ & 2u)) { TXCODE(ea_, %uu); if (SCOND(ea_ < %s && ea_ + %uu > %s)) { %sspc = %s; "
+                so_.put("    *(g_%s *)p_ = (%s)%s;\n", gtype(sz), ltype(sz), B.c_str());
+                so_.put("    if (SCOND(cs_ & 2u)) { TXCODE(ea_, %uu); if (SCOND(ea_ < %s && ea_ + %uu > %s)) { %sspc = %s; "
                        "goto S_out; } } }\n", sz, hex(bhi).c_str(), sz, ftb.c_str(),
                        scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db + sz).c_str(), ftb.c_str());
                 break;
@@ -782,7 +801,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                           ftb.c_str(), ftb.c_str());
                     g.put("    %s }\n", wgo(h0, tgt).c_str());
                 }
-                so.put("  %s\n  if (SCOND(%s)) %s\n  %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), c.c_str(),
+                so_.put("  %s\n  if (SCOND(%s)) %s\n  %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), c.c_str(),
                        sgo(h0, tgt).c_str(), sgo(h0, ft).c_str());
                 break;
             }
@@ -790,10 +809,10 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 const uint64_t tgt = pc + (int64_t)p.imm;
                 if (p.rd) {
                     g.put("  TXSET(%u, %s);\n", p.rd, ftb.c_str());
-                    so.put("  SX(%u, %s);\n", p.rd, ftb.c_str());
+                    so_.put("  SX(%u, %s);\n", p.rd, ftb.c_str());
                 }
                 g.put("  %s %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), wgo(h0, tgt).c_str());
-                so.put("  %s %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), sgo(h0, tgt).c_str());
+                so_.put("  %s %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), sgo(h0, tgt).c_str());
                 break;
             }
             case C_JALR: {
@@ -805,9 +824,9 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 g.put("    const uint64_t t0_ = rdl64<kNL>(t_, __ffsll((unsigned long long)gmr) - 1);\n");
                 g.put("    if (TXB(mine && t_ != t0_)) { dpc = t_; jdiv = mine; goto tx_out; }\n");
                 g.put("    spc = uni64(t0_); goto tx_dispatch; }\n");
-                so.put("  { const uint64_t t_ = (%s + (uint64_t)(int64_t)%lldLL) & ~1ULL;\n", A.c_str(), (long long)im);
-                if (rd) so.put("    SX(%u, %s);\n", rd, ftb.c_str());
-                so.put("    %s spc = SUNI(t_); goto S_dispatch; }\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str());
+                so_.put("  { const uint64_t t_ = (%s + (uint64_t)(int64_t)%lldLL) & ~1ULL;\n", A.c_str(), (long long)im);
+                if (rd) so_.put("    SX(%u, %s);\n", rd, ftb.c_str());
+                so_.put("    %s spc = SUNI(t_); goto %s; }\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), SD.c_str());
                 break;
             }
             default:
@@ -819,17 +838,19 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             const uint64_t nxt = cur_odd ? (n ? b.opcs[n - 1] + pre[insts[n - 1]].len : pc0)
                                          : n ? g.pc_of(insts[n - 1]) + pre[insts[n - 1]].len : pc0;
             g.put("  %s %s\n", commit(k_st, k_xt, k_fb, k_db).c_str(), wgo(h0, nxt).c_str());
-            so.put("  %s %s\n", scommit(k_st, k_xt, k_fb, k_db).c_str(), sgo(h0, nxt).c_str());
+            so_.put("  %s %s\n", scommit(k_st, k_xt, k_fb, k_db).c_str(), sgo(h0, nxt).c_str());
         }
         g.put("}\n");
-        so.put("}\n");
+        so_.put("}\n");
         if (cur_odd) g.out.swap(g_keep);
+    }
+    if (oddon) g.out.swap(g_mode);
     }
     cur_odd = false;
     leaders_out.assign(leaders.begin(), leaders.end());
     // odd-pc entries: bit 31 + the pre-decoded index of their key (kPreOddLeader)
     for (uint64_t pc : olead) leaders_out.push_back(0x80000000u | okey(pc));
-    return g.out + FI_TX_SPLIT + so.out;
+    return g.out + FI_TX_SPLIT + so.out + FI_TX_SPLIT + sq.out;
 }
 
 }  // namespace fi

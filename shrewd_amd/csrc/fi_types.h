@@ -30,8 +30,9 @@ static_assert(sizeof(PreInst) == 16, "PreInst must stay 16 bytes (one s_load_dwo
 constexpr uint8_t kPreValid = 1, kPreStraddle = 2, kPreRs1 = 4, kPreRs2 = 8, kPreRd = 16;
 constexpr uint8_t kPreLeader = 32;   // translated code may be entered here (load-time build)
 constexpr uint8_t kPreOddLeader = 64;   // ... and (solo kernel) at the odd pcs that fetch this halfword
-// Separates the 64-lane and the solo translated bodies in the generated text
-// (fi_translate.cpp -> fi_jit.cpp splices them at /*@TX_BODY@*/ and /*@TX_SOLO@*/).
+// Separates the 64-lane, solo and solo-odd translated bodies in the generated
+// text (fi_translate.cpp -> fi_jit.cpp splices them at /*@TX_BODY@*/,
+// /*@TX_SOLO@*/ and /*@TX_SOLO_ODD@*/).
 #define FI_TX_SPLIT "\n/*@TX_SPLIT@*/\n"
 
 // Golden snapshot: the architectural state at the top of the first tick with
@@ -111,7 +112,7 @@ struct FwdCtx {
 
 // Everything one launch of the trial kernel needs.  Passed by value as the
 // kernel argument (lives in the kernarg segment -> scalar loads).
-constexpr int kNStats = 40;          // DevCtx::stats entries
+constexpr int kNStats = 64;          // DevCtx::stats entries
 
 struct DevCtx {
     // golden text, pre-decoded (pre_ok = 0 if the golden run rewrote its text)
@@ -170,6 +171,7 @@ struct DevCtx {
                                      // >= 1); 0 = always `lanes` per wave
     const uint32_t *resume;          // NULL = fresh launch: lane slot = global lane index
     const uint32_t *resume_n;        // number of entries in resume[]
+    const uint32_t *resume_lo;       // solo-odd launch: its entries are resume[*resume_lo .. *resume_n) (else NULL)
     const uint32_t *wrange;          // packed resume (FI_CFG_PACK_RUNS): wave b runs resume[wrange[2b] .. wrange[2b+1])
     const uint32_t *n_waves;         //   number of valid wrange pairs (waves b >= it exit at once)
     uint32_t *surv;                  // suspended lanes' slots are appended here
@@ -191,6 +193,10 @@ struct DevCtx {
     const uint8_t *exe_path;         // realpath of the executable (readlinkat /proc/self/exe), exe_len bytes
     uint64_t exe_len;                // 0: unknown (that call escapes as host)
     uint64_t clk_period;             // ticks per CPU cycle (clock_gettime)
+    uint64_t tick0;                  // curTick at the campaign start (a checkpoint's [Globals] curTick; else 0)
+    const uint64_t *fp0;             // a checkpoint's FP registers (NULL: none -- zero, no FP state)
+    uint32_t fcsr0;                  //   and its fflags | frm << 5
+    const VmState *vm0;              // a checkpoint's SE memory map (NULL: the process-start one, brk0 / svma_*)
     uint32_t simt_min;               // diverged-lanes step loop: least lanes to enter it (0 = off)
     // memory liveness: record mode appends the golden run's data accesses to
     // rec_mem; trials look a memory fault's word up in the per-word index built
@@ -212,7 +218,11 @@ struct DevCtx {
                                      // [23] instructions executed on the device
                                      // [24] lane-instructions of the diverged-lanes step loop
                                      // [25] golden data-access events [26] memory faults ended at injection
+                                     // [27] register faults dead at injection [30] trials re-run with more private
+                                     // pages (FI_ESC_RESOURCE, fi_engine.cpp run_chunk)
                                      // [32..39] FI_PROF phase cycles
+                                     // [40 + 4k + {0,1,2,3}] fetch B, data B, pages, device insts of kernel k
+                                     // (0 the 64-lane kernel, 1 solo, 2 solo-odd)
 };
 
 struct SampleCtx {

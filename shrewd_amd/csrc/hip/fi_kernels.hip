@@ -223,18 +223,36 @@ __global__ void __launch_bounds__(256) fi_hist_kernel(const fi_site *sites, cons
 // up in the same wave); entries past the survivor count sort last.
 // Survivor sort key: pc offset from the text base (low 32 bits) above the
 // low 32 bits of numInst, so that survivors standing at the same pc are
-// adjacent and ordered by progress.
+// adjacent and ordered by progress.  With n_odd (a solo-odd launch follows)
+// the key is shifted down one bit under a top bit set for odd pcs, so that
+// the odd-pc survivors sort last, and they are counted.
 __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
-                                    uint64_t text_lo, uint64_t *keys, uint32_t *vals) {
+                                    uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cap) return;
     if (i < *cnt) {
         const uint32_t sl = list[i];
-        keys[i] = ((save[sl].pc - text_lo) << 32) | (save[sl].ninst & 0xFFFFFFFFu);
+        const uint64_t pc = save[sl].pc;
+        uint64_t k = ((pc - text_lo) << 32) | (save[sl].ninst & 0xFFFFFFFFu);
+        if (n_odd) {
+            k = ((pc & 1) << 63) | (k >> 1);
+            if (pc & 1) atomicAdd(n_odd, 1u);
+        }
+        keys[i] = k;
         vals[i] = sl;
     } else {
         keys[i] = ~0ULL;
         vals[i] = 0;
+    }
+}
+
+// The solo kernel's share of a sorted survivor list whose odd-pc survivors
+// come last: all but the last min(n_odd, grid), which the solo-odd kernel's
+// grid takes.
+__global__ void fi_odd_split_kernel(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        const uint32_t o = *n_odd < grid ? *n_odd : grid;
+        *split = *cnt - o;
     }
 }
 
@@ -254,6 +272,32 @@ __global__ void fi_pack_runs_kernel(const uint64_t *keys, const uint32_t *cnt, u
     const uint32_t w = atomicAdd(n_waves, 1u);
     wrange[2 * w] = (uint32_t)i;
     wrange[2 * w + 1] = e;
+}
+
+// Second pass of the trials that ran out of private pages (fi_engine.cpp
+// run_chunk): list them, gather their sites densely, scatter the new outcomes.
+__global__ void fi_redo_collect_kernel(const fi_outcome *out, uint64_t n, uint32_t *idx, uint32_t *cnt,
+                                       unsigned long long *stats) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const fi_outcome o = out[i];
+    if (o.cls == FI_ESCAPE && o.sub == FI_ESC_RESOURCE) {
+        idx[atomicAdd(cnt, 1u)] = (uint32_t)i;
+        atomicAdd(&stats[30], 1ull);
+    }
+}
+__global__ void fi_redo_gather_kernel(const fi_site *sites, const uint32_t *idx, uint64_t n, fi_site *rsites,
+                                      uint64_t *keys, uint32_t *perm) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const fi_site s = sites[idx[j]];
+    rsites[j] = s;
+    keys[j] = s.inst;
+    perm[j] = (uint32_t)j;
+}
+__global__ void fi_redo_scatter_kernel(const uint32_t *idx, uint64_t n, const fi_outcome *rout, fi_outcome *out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < n) out[idx[j]] = rout[j];
 }
 
 __global__ void fi_hist_stats_kernel(const unsigned long long *stats, fi_histogram *h) {
@@ -298,10 +342,30 @@ hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, 
     hipLaunchKernelGGL(fi_hist_stats_kernel, dim3(1), dim3(64), 0, st, stats, h);
     return hipGetLastError();
 }
+hipError_t launch_redo_collect(const fi_outcome *out, uint64_t n, uint32_t *idx, uint32_t *cnt,
+                               unsigned long long *stats, hipStream_t st) {
+    hipLaunchKernelGGL(fi_redo_collect_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, out, n, idx, cnt, stats);
+    return hipGetLastError();
+}
+hipError_t launch_redo_gather(const fi_site *sites, const uint32_t *idx, uint64_t n, fi_site *rsites, uint64_t *keys,
+                              uint32_t *perm, hipStream_t st) {
+    hipLaunchKernelGGL(fi_redo_gather_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, sites, idx, n, rsites, keys, perm);
+    return hipGetLastError();
+}
+hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome *rout, fi_outcome *out,
+                               hipStream_t st) {
+    hipLaunchKernelGGL(fi_redo_scatter_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, idx, n, rout, out);
+    return hipGetLastError();
+}
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
-                            uint64_t text_lo, uint64_t *keys, uint32_t *vals, hipStream_t st) {
+                            uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, hipStream_t st) {
     hipLaunchKernelGGL(fi_surv_keys_kernel, dim3(nblk(cap, 256)), dim3(256), 0, st, save, list, cnt, cap, text_lo,
-                       keys, vals);
+                       keys, vals, n_odd);
+    return hipGetLastError();
+}
+hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(fi_odd_split_kernel, dim3(1), dim3(64), 0, st, cnt, n_odd, split, grid);
     return hipGetLastError();
 }
 hipError_t launch_pack_runs(const uint64_t *keys, const uint32_t *cnt, uint64_t cap, uint32_t *wrange,

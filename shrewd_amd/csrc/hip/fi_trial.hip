@@ -154,11 +154,7 @@ __device__ __forceinline__ bool dirty_at(const LaneMem &m, uint64_t pc) {
 // few instructions), so such lanes stay in the pre-decoded path instead.
 constexpr uint64_t kTxNear = 256;
 __device__ __forceinline__ bool dirty_near(const LaneMem &m, uint64_t pc) {
-#ifdef FI_DIRTY_NO_TX
-    return m.code_dirty;
-#else
     return m.code_dirty && (pc & ~3ULL) < m.dhi && pc + kTxNear > m.dlo;
-#endif
 }
 __device__ __forceinline__ void mark_dirty(LaneMem &m, uint64_t lo, uint64_t hi) {
     m.dlo = m.code_dirty ? (lo < m.dlo ? lo : m.dlo) : lo;
@@ -256,22 +252,30 @@ __device__ uint8_t *priv_new(KCtx *c, LaneMem &m, uint64_t slot, uint64_t vpn, c
     tlb_flush(m);
     return (uint8_t *)d;
 }
-// The trial's VM state, materialised from the process-start one on first use.
+// The trial's VM state, materialised from the start one on first use: the
+// checkpoint's (vm0) or the process-start one.
 __device__ VmState *vm_of(KCtx *c, LaneMem &m, uint64_t slot) {
     VmState *v = c->vm + slot;
     if (!m.vm) {
-        v->brk = c->brk0; v->mmap_end = 0x4000000000000000ULL; v->ctid = 0;   // RiscvProcess64 (process.cc:79)
-        v->rnd_pos = 0;
-        v->nvma = 1; v->fdc = 0;
-        v->vma[0][0] = c->svma_lo; v->vma[0][1] = c->svma_hi;                 // argsInit's "stack" VMA
+        if (c->vm0) {
+            const VmState *z = c->vm0;
+            v->brk = z->brk; v->mmap_end = z->mmap_end; v->ctid = z->ctid; v->rnd_pos = z->rnd_pos;
+            v->nvma = z->nvma; v->fdc = z->fdc;
+            for (uint32_t i = 0; i < z->nvma; i++) { v->vma[i][0] = z->vma[i][0]; v->vma[i][1] = z->vma[i][1]; }
+        } else {
+            v->brk = c->brk0; v->mmap_end = 0x4000000000000000ULL; v->ctid = 0;   // RiscvProcess64 (process.cc:79)
+            v->rnd_pos = 0;
+            v->nvma = 1; v->fdc = 0;
+            v->vma[0][0] = c->svma_lo; v->vma[0][1] = c->svma_hi;                 // argsInit's "stack" VMA
+        }
         m.vm = true;
         if (c->record) c->stats[22] = 1;   // the golden VM state is not in the snapshots
     }
     return v;
 }
 __device__ bool in_vma(KCtx *c, const LaneMem &m, uint64_t slot, uint64_t a) {
-    if (!m.vm) return a >= c->svma_lo && a < c->svma_hi;
-    const VmState *v = c->vm + slot;
+    if (!m.vm && !c->vm0) return a >= c->svma_lo && a < c->svma_hi;
+    const VmState *v = m.vm ? c->vm + slot : c->vm0;
     for (uint32_t i = 0; i < v->nvma; i++)
         if (a >= v->vma[i][0] && a < v->vma[i][1]) return true;
     return false;
@@ -994,7 +998,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
     case 113: {   // clock_gettimeFunc (syscall_emul.hh:2266-2278): curTick() in ns + 1e9 s
         if (!a1) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }
         if (!proxy_readable(c, w, m, slot, a1, 16)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
-        const uint64_t ns = (L.ncyc - 1) * c->clk_period / 1000;
+        const uint64_t ns = (c->tick0 + (L.ncyc - 1) * c->clk_period) / 1000;
         const uint64_t sec = ns / 1000000000ULL + 1000000000ULL, nsec = ns % 1000000000ULL;
         char b[16];
         for (int k = 0; k < 8; k++) { b[k] = (char)(sec >> (8 * k)); b[8 + k] = (char)(nsec >> (8 * k)); }
@@ -1109,7 +1113,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
                            (1ULL << 46) | (1ULL << 47);
             case 5: case 9: return 2;
             case 6: return 64;
-            case 7: return m.vm ? c->vm[slot].mmap_end : 0x4000000000000000ULL;   // MemState::getMmapEnd()
+            case 7: return m.vm ? c->vm[slot].mmap_end : c->vm0 ? c->vm0->mmap_end : 0x4000000000000000ULL;   // MemState::getMmapEnd()
             default: key = -1; return 0;
             }
         };
@@ -1272,28 +1276,15 @@ typedef __attribute__((address_space(1), aligned(1))) uint64_t g_u64;
         X##r = mine ? t_ : X##r;                            \
     } while (0)
 
-// Solo translated code: where the trial's guest registers live.  By default
-// the compiler keeps them (uniform in a one-lane wave) in SGPRs; with
-// FI_SOLO_VREG they are pinned in VGPRs (an asm barrier on every write) and
-// only branch conditions and jump targets are made uniform again, which
-// trades SGPR spills for VALU work (A/B knob SHREWD_FI_SOLO_VREG).
-#ifdef FI_SOLO_VREG
-#define SVREG(v) __asm__ volatile("" : "+v"(v))
-#define SCOND(x) (__builtin_amdgcn_readfirstlane((int)(bool)(x)) != 0)
-#define SUNI(x) uni64(x)
-#define SUNI32(x) ((uint32_t)__builtin_amdgcn_readfirstlane((int)(x)))
-#else
-#define SVREG(v) ((void)0)
+// Solo translated code: the trial's guest registers are uniform in a
+// one-lane wave and the compiler keeps them in SGPRs.  (Pinning them in VGPRs
+// instead -- an asm barrier on every write, conditions and jump targets made
+// uniform again -- traded SGPR spills for VALU work and lost: crc32 3.2-3.7M
+// against 7.06M trials/s, profiles/r02j_solo_ab.txt.)
 #define SCOND(x) (x)
 #define SUNI(x) (x)
 #define SUNI32(x) (x)
-#endif
-#define SX(r, e)                         \
-    do {                                 \
-        uint64_t s_ = (uint64_t)(e);     \
-        SVREG(s_);                       \
-        X##r = s_;                       \
-    } while (0)
+#define SX(r, e) X##r = (uint64_t)(e)
 
 // The pre-decoded text (uniform): table, text range, exact code range.
 struct TextRef { const PreInst *pre; uint32_t lo, hi, bytes; uint64_t clo, chi; };
@@ -1374,7 +1365,7 @@ __device__ __forceinline__ bool ult64(uint64_t a, uint64_t b) {
 // solo kernel register budget: 4 waves per SIMD (<= 128 VGPRs).  A/B on
 // crc32 (tools/gpu/solo_ab.sh, profiles/r02j_solo_ab.txt): 1 (no bound, 136-140
 // VGPRs, 3 waves) 6.44M, 4: 7.06M trials/s; VGPR-pinned guest registers
-// (FI_SOLO_VREG) 3.2-3.7M.
+// 3.2-3.7M.
 #ifndef FI_SOLO_WAVES_PER_EU
 #define FI_SOLO_WAVES_PER_EU 4
 #endif
@@ -1384,37 +1375,24 @@ __device__ __forceinline__ bool ult64(uint64_t a, uint64_t b) {
 // Solo kernel: the launch context through a plain pointer, so that the
 // compiler can keep loop-invariant fields in registers (a one-lane wave has
 // VGPR lanes to spill them to) instead of a scalar load + wait at each use
-// (A/B knob SHREWD_FI_SOLO_CX=0).
-#ifndef FI_SOLO_CX_DIRECT
-#define FI_SOLO_CX_DIRECT 1
-#endif
-template <uint32_t kNL>
+// (through the opaque pointer: crc32 10.05M against 11.20M trials/s,
+// profiles/r02l_ab.txt).
+// kOdd: the solo-odd instantiation, whose translated blocks (the solo body
+// again plus the odd-pc streams) are entered at odd pcs too.
+template <uint32_t kNL, bool kOdd = false>
 __device__ __forceinline__ void trial_body() {
     KCtx *const kc = (KCtx *)__builtin_amdgcn_kernarg_segment_ptr();
-#define CX ((kNL == 1 && FI_SOLO_CX_DIRECT) ? kc : opq(kc))
-// An out-of-line helper that takes the lane's memory state (or the wave's
-// page table) by reference runs on copies: a reference to the interpreter's
-// own LaneMem would pin it in scratch memory for the whole kernel, and every
-// TLB probe of the hot loops would become a scratch load.
-// (A/B knob SHREWD_FI_SOLO_OOL=1, solo kernel only: with the copies the
-// interpreter-bound tail trials ran 10-20 % faster, but the crc32 bench lost
-// 12 %, 10.0M -> 8.8M trials/s, profiles/r02l_ab.txt)
-#ifndef FI_SOLO_OOL_COPY
-#define FI_SOLO_OOL_COPY 0
-#endif
+#define CX (kNL == 1 ? kc : opq(kc))
+// Out-of-line helpers take the lane's memory state and the wave's page table
+// by reference.  (Running them on copies, so that the reference does not pin
+// LaneMem in scratch, made the interpreter-bound solo tail trials 10-20 %
+// faster but cost the crc32 bench 12 %, 10.0M -> 8.8M trials/s,
+// profiles/r02l_ab.txt.)
 #define OOL(stmt)                                 \
     do {                                          \
-        if constexpr (kNL == 1 && FI_SOLO_OOL_COPY) { \
-            LaneMem mc_ = m;                      \
-            WaveMem wc_ = w;                      \
-            stmt;                                 \
-            m = mc_;                              \
-            (void)wc_;                            \
-        } else {                                  \
-            LaneMem &mc_ = m;                     \
-            const WaveMem &wc_ = w;               \
-            stmt;                                 \
-        }                                         \
+        LaneMem &mc_ = m;                         \
+        const WaveMem &wc_ = w;                   \
+        stmt;                                     \
     } while (0)
     __shared__ uint64_t R[kRows * kNL];
     const uint64_t t_start = __builtin_amdgcn_s_memtime(), rt_start = __builtin_amdgcn_s_memrealtime();
@@ -1429,9 +1407,11 @@ __device__ __forceinline__ void trial_body() {
         while (l < per && l < nlw) l <<= 1;
         nlw = l;
     }
-    // surplus waves of a resume grid (sized for the fewest lanes per wave) leave at once
-    if (resume && (CX->wrange ? blockIdx.x >= *CX->n_waves : (uint64_t)blockIdx.x * nlw >= *CX->resume_n)) return;
-    uint64_t gidx = (uint64_t)blockIdx.x * nlw + lane;
+    // surplus waves of a resume grid (sized for the fewest lanes per wave) leave
+    // at once; a solo-odd launch takes the list from *resume_lo on
+    const uint32_t rlo = (resume && CX->resume_lo) ? *CX->resume_lo : 0u;
+    if (resume && (CX->wrange ? blockIdx.x >= *CX->n_waves : (uint64_t)blockIdx.x * nlw + rlo >= *CX->resume_n)) return;
+    uint64_t gidx = (uint64_t)blockIdx.x * nlw + lane + rlo;
     bool live = lane < nlw && (resume ? gidx < *CX->resume_n : gidx < CX->n);
     if (resume && CX->wrange) {   // packed resume: this wave's same-pc run of survivors
         const uint32_t b = blockIdx.x;
@@ -1490,13 +1470,9 @@ __device__ __forceinline__ void trial_body() {
     // the solo kernel's LaneMem lives in LDS: the out-of-line helpers take it
     // by reference, which would otherwise pin it in scratch, and every TLB
     // probe and dirty-range check of the hot loops would be a scratch load
-    // (FI_SOLO_M_LDS=0: the private copy, A/B)
-#ifndef FI_SOLO_M_LDS
-#define FI_SOLO_M_LDS 1
-#endif
     __shared__ LaneMem m_lds[1];
     LaneMem m_priv;
-    LaneMem &m = (kNL == 1 && FI_SOLO_M_LDS) ? m_lds[0] : m_priv;
+    LaneMem &m = kNL == 1 ? m_lds[0] : m_priv;
     m.stack_min = S0->stack_min;
     tlb_flush(m);
     m.tp0 = m.tp1 = m.tp2 = m.tp3 = 0;
@@ -1505,6 +1481,12 @@ __device__ __forceinline__ void trial_body() {
     m.resv = m.lock = kNone;
     m.vm = false;
     m.nmiss = 0;
+    if (CX->fp0 && live && !resume) {   // a checkpoint with FP state: every lane starts with it
+        for (int r = 0; r < 32; r++) CX->fregs[(uint64_t)r * CX->n_slots + slot] = CX->fp0[r];
+        L.fp = true;
+        L.fflags = (uint8_t)(CX->fcsr0 & 0x1F); L.frm = (uint8_t)((CX->fcsr0 >> 5) & 7);
+        if (CX->record) CX->stats[22] = 1;   // FP state outside the snapshots (host disables snapshot starts)
+    }
     if (resume && live) {
         L.pc = SV->pc; L.ninst = SV->ninst; L.ncyc = SV->ncyc; L.out_pos = SV->out_pos; L.err_pos = SV->err_pos;
         L.next_chk = SV->next_chk; L.nfail = SV->nfail; L.watch = SV->watch;
@@ -1929,13 +1911,9 @@ __device__ __forceinline__ void trial_body() {
             tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
             tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
             const PreRef E0 = pre_entry(tx, lpc);
-#ifdef FI_TX_ODD
-            // (odd pcs: the solo body's odd-pc blocks, flagged on their key's entry)
-            const bool tx_entry = E0.in && ((lpc & 1) ? (kNL == 1 && ((uni32(E0.e.w) >> 8) & kPreOddLeader))
+            // (odd pcs: the solo-odd body's odd-pc blocks, flagged on their key's entry)
+            const bool tx_entry = E0.in && ((lpc & 1) ? (kOdd && ((uni32(E0.e.w) >> 8) & kPreOddLeader))
                                                       : ((uni32(E0.e.w) >> 8) & kPreLeader));
-#else
-            const bool tx_entry = !(lpc & 1) && E0.in && ((uni32(E0.e.w) >> 8) & kPreLeader);
-#endif
             if constexpr (kNL == 1) {
                 // ---- solo: one trial, every value uniform -- no groups, no
                 // parking, plain register writes; the same exits and counters
@@ -1966,13 +1944,21 @@ __device__ __forceinline__ void trial_body() {
                     uint32_t st = 0, xt = 0, fb = 0, db = 0;   // instructions, straddles, fetch/data bytes
                     uint64_t spc = lpc;
                     uint32_t etgt = 0xFFFFFFFFu;   // block an entry is routed to through its cycle headers
-#define TXR(r) uint64_t X##r = RREG(r); SVREG(X##r);
+#define TXR(r) uint64_t X##r = RREG(r);
                     TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
                     TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
                     TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
 #undef TXR
-                    goto S_dispatch;
-                    /*@TX_SOLO@*/
+#ifdef FI_TX_SOLO_ODD
+                    if constexpr (kOdd) {
+                        goto Q_dispatch;
+                        /*@TX_SOLO_ODD@*/
+                    } else
+#endif
+                    {
+                        goto S_dispatch;
+                        /*@TX_SOLO@*/
+                    }
                 S_out:
 #define TXW(r) RREG(r) = X##r;
                     TXW(1) TXW(2) TXW(3) TXW(4) TXW(5) TXW(6) TXW(7) TXW(8) TXW(9) TXW(10) TXW(11) TXW(12) TXW(13)
@@ -2156,13 +2142,9 @@ __device__ __forceinline__ void trial_body() {
                 const uint32_t aux = q3 >> 16, kind = aux & 63;
                 if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
 #ifdef FI_TX
-                // translated blocks take over here (odd pcs: only the solo kernel's
-                // odd-pc blocks, flagged on the entry of the halfword they fetch)
-#ifdef FI_TX_ODD
-                const bool lead = ((uint32_t)spc & 1) ? (kNL == 1 && ((q3 >> 8) & kPreOddLeader)) : ((q3 >> 8) & kPreLeader);
-#else
-                const bool lead = ((q3 >> 8) & kPreLeader) && !((uint32_t)spc & 1);
-#endif
+                // translated blocks take over here (odd pcs: only the solo-odd
+                // kernel's odd-pc blocks, flagged on the entry of the halfword they fetch)
+                const bool lead = ((uint32_t)spc & 1) ? (kOdd && ((q3 >> 8) & kPreOddLeader)) : ((q3 >> 8) & kPreLeader);
                 if (steps && lead &&
                     !(any_dirty && wballot<kNL>(mine && dirty_near(m, spc)) != 0) && n_iter + steps >= tx_skip_until)
                     break;
@@ -2692,7 +2674,9 @@ __device__ __forceinline__ void trial_body() {
             case OP_m5op: {   // a0 = result, a1 = 0 (M5Op::execute); pseudoInstWork under SE defaults
                 m5 = true;
                 switch ((uint32_t)d.imm) {
-                case 0x07: v = (L.ncyc - 1) * CX->clk_period / 1000; break;   // rpns
+                // rpns: curTick() in ns during this instruction's execute -- its
+                // fetch tick(s) already elapsed (the commit adds them to ncyc)
+                case 0x07: v = (CX->tick0 + (L.ncyc + ticks - 1) * CX->clk_period) / 1000; break;
                 case 0x23:   // m5sum(a0..a5)
                     xdet = L.watch >= 10 && L.watch <= 15;
                     v = RREG(10) + RREG(11) + RREG(12) + RREG(13) + RREG(14) + RREG(15);
@@ -2901,6 +2885,13 @@ __device__ __forceinline__ void trial_body() {
         atomicAdd(&CX->stats[0], (unsigned long long)fb);
         atomicAdd(&CX->stats[1], (unsigned long long)db);
         atomicAdd(&CX->stats[2], (unsigned long long)pm);
+        {   // the same per kernel: 0 64-lane, 1 solo, 2 solo-odd (the bench's per-kernel roofline)
+            constexpr uint32_t kk = kNL > 1 ? 0u : (kOdd ? 2u : 1u);
+            atomicAdd(&CX->stats[40 + 4 * kk], (unsigned long long)fb);
+            atomicAdd(&CX->stats[41 + 4 * kk], (unsigned long long)db);
+            atomicAdd(&CX->stats[42 + 4 * kk], (unsigned long long)pm);
+            atomicAdd(&CX->stats[43 + 4 * kk], (unsigned long long)xi);
+        }
         atomicAdd(&CX->stats[6], (unsigned long long)n_iter);
         atomicAdd(&CX->stats[7], (unsigned long long)n_exec);
         atomicAdd(&CX->stats[8], (unsigned long long)n_slow);
@@ -2928,10 +2919,15 @@ __device__ __forceinline__ void trial_body() {
     }
 }
 
-// The two instantiations (load-time build: with the translated blocks).
+// The instantiations (load-time build: with the translated blocks).
 #ifdef __HIPCC_RTC__
 extern "C" __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel_tx(DevCtx) { trial_body<64>(); }
 extern "C" __global__ void __launch_bounds__(1, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_tx_solo(DevCtx) { trial_body<1>(); }
+#ifdef FI_TX_SOLO_ODD
+extern "C" __global__ void __launch_bounds__(1, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_tx_solo_odd(DevCtx) {
+    trial_body<1, true>();
+}
+#endif
 #else
 __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx) { trial_body<64>(); }
 __global__ void __launch_bounds__(1, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_solo(DevCtx) { trial_body<1>(); }

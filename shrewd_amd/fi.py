@@ -106,6 +106,8 @@ CFG_SOLO_ALL = 128
 CFG_SIMT = 256
 CFG_NO_FORWARD = 512
 CFG_NO_SDC_EXIT = 1024
+CFG_NO_REDO = 2048
+CFG_NO_ODD_KERNEL = 4096
 
 
 class GoldenInfo(C.Structure):
@@ -221,6 +223,7 @@ def lib():
         L.fi_debug_waves.argtypes = [vp, vp, C.c_uint64]
         L.fi_debug_epochs.argtypes = [vp, vp]
         L.fi_debug_dispatch_ms.argtypes = [vp, vp, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.fi_debug_dispatch_kinds.argtypes = [vp, vp, C.c_uint32, C.POINTER(C.c_uint32)]
         L.fi_debug_golden_trace.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), vp, C.c_uint64,
                                             C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.fi_debug_translate.argtypes = [vp, C.c_uint64, C.c_uint64, vp, C.c_uint64, C.c_char_p, C.c_uint64,
@@ -387,6 +390,13 @@ class Engine:
         self._chk(self.L.fi_debug_dispatch_ms(self.h, ms.ctypes.data, 256, C.byref(n)), "fi_debug_dispatch_ms")
         return [round(float(x), 3) for x in ms[:min(n.value, 256)]]
 
+    def debug_dispatch_kinds(self) -> list:
+        """Kernel of each dispatch of debug_dispatch_ms: 0 64-lane, 1 solo, 2 solo-odd."""
+        k = np.zeros(256, np.uint32)
+        n = C.c_uint32()
+        self._chk(self.L.fi_debug_dispatch_kinds(self.h, k.ctypes.data, 256, C.byref(n)), "fi_debug_dispatch_kinds")
+        return k[:min(n.value, 256)].tolist()
+
     def debug_golden_trace(self):
         """(pre-decoded text as uint8[n,16], golden trace uint32[m], text_lo)"""
         npre, ntr, lo = C.c_uint64(), C.c_uint64(), C.c_uint64()
@@ -408,7 +418,7 @@ class Engine:
         return self.L.fi_last_kernel_ms(self.h)
 
     def debug_stats(self) -> np.ndarray:
-        out = np.zeros(40, np.uint64)
+        out = np.zeros(64, np.uint64)
         self._chk(self.L.fi_debug_stats(self.h, out.ctypes.data), "fi_debug_stats")
         return out
 
@@ -588,7 +598,10 @@ class FaultCampaign:
         self.outcomes, self._hist = self.engine.run_trials(self.first, cnt)
         if world > 1:
             import torch
-            self._hist = allreduce_histogram(self._hist, torch.device("cuda", torch.cuda.current_device()))
+            import torch.distributed as dist
+            # RCCL reduces device tensors; other backends (gloo) host ones
+            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else None
+            self._hist = allreduce_histogram(self._hist, dev)
         if self.output:
             np.save(self.output if world == 1 else f"{self.output}.rank{rank}", self.outcomes)
         return self.outcomes

@@ -72,3 +72,51 @@ def test_two_rank_histogram_allreduce(oracle_mod):
     assert outs.tobytes() == ref.tobytes()
     assert hists[0].tobytes() == np_histogram(sites, ref).tobytes()
     assert int(hists[0]["trials"]) == TRIALS
+
+
+def test_engine_two_ranks_one_gpu_script_is_cpu_importable():
+    """The rank script of the GPU test below imports on CPU (no work at import)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("dist_engine_rank", os.path.join(ROOT, "tests", "dist_engine_rank.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert callable(mod.main)
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_engine_two_ranks_one_gpu(tmp_path):
+    """The product's multi-rank path on one GPU: two processes (gloo, both on
+    device 0), each FaultCampaign.run(num_gpus=2) over its contiguous shard of
+    the trial ids, the outcome histogram all-reduced.  The ranks' outcomes in
+    shard order and the reduced histogram equal a single-process run of the
+    same campaign."""
+    import subprocess
+    import sys
+    from shrewd_amd.fi import HIST_DT, FaultCampaign
+    trials, seed, world = 3001, 0x5EED2222, 2
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dist_engine_rank.py"),
+                                       str(tmp_path), str(trials), hex(seed)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    logs = [p.communicate(timeout=240)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), logs
+    outs = [np.load(tmp_path / f"out{r}.npy") for r in range(world)]
+    hists = [np.frombuffer(np.load(tmp_path / f"hist{r}.npy").tobytes(), HIST_DT)[0] for r in range(world)]
+    firsts = [int((tmp_path / f"first{r}.txt").read_text()) for r in range(world)]
+    assert firsts == [0, len(outs[0])] and len(outs[0]) + len(outs[1]) == trials
+    assert hists[0].tobytes() == hists[1].tobytes()
+    fc = FaultCampaign(os.path.join(ROOT, "workloads", "crc32.elf"), cmd=["crc32"], trials=trials, seed=seed,
+                       structures=("int_reg", "pc"))
+    ref = fc.run()
+    h = fc.histogram()
+    fc.engine.close()
+    assert np.concatenate(outs).tobytes() == ref.tobytes()
+    for f in ("counts", "crash_sub", "escape_sub", "trials", "guest_insts"):
+        assert np.array_equal(hists[0][f], h[f]), f

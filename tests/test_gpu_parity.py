@@ -323,6 +323,8 @@ PATH_FLAGS = {
     "no_forward": 512,                      # FI_CFG_NO_FORWARD: inject at the sampled time
     "no_sdc_exit": 1024,                    # FI_CFG_NO_SDC_EXIT: SDC trials run to their end
     "simt_no_solo_interp": 256 | 64 | 4,    # the step loop for every epoch, no translated blocks
+    "no_odd_kernel": 4096,                  # FI_CFG_NO_ODD_KERNEL: odd-pc survivors on the solo kernel
+    "no_redo": 2048,                        # FI_CFG_NO_REDO: no second pass for private-page exhaustion
 }
 _PATH_REF = {}
 
@@ -511,3 +513,50 @@ def test_sdc_early_exit(engine_factory, oracle_mod):
     assert int(ha["device_insts"]) < int(hb["device_insts"])
     sites = on.sample(0, 3000)
     compare(a[:3000], oracle_for(oracle_mod, "crcblk").run_trials(sites, protect_mask=0), sites)
+
+
+@pytest.mark.parametrize("name", ["qsort", "intmix"])
+def test_resource_redo(engine_factory, oracle_mod, name):
+    """Trials that run out of copy-on-write pages (FI_ESC_RESOURCE, an engine
+    capacity limit) run again with more pages before the histogram: with one
+    private page per trial the outcomes equal the default engine's and the
+    oracle's, while the same engine without the second pass escapes."""
+    n = 3000
+    tight = engine_factory(name, private_pages=1, max_trials_per_launch=n)
+    noredo = engine_factory(name, private_pages=1, flags=2048, max_trials_per_launch=n)   # FI_CFG_NO_REDO
+    for e in (tight, noredo):
+        e.set_campaign(0x5EED0BED, REGS | PC | MEM, 1)
+        e.set_protect(0)
+    sites = tight.sample(0, n)
+    b, hb = noredo.run_sites(sites)
+    esc = (b["cls"] == 5) & (b["sub"] == 5)
+    assert esc.sum() > 0
+    a, ha = tight.run_sites(sites)
+    assert int(tight.debug_stats()[30]) == int(esc.sum())
+    assert not ((a["cls"] == 5) & (a["sub"] == 5)).any()
+    assert int(ha["escape_sub"][5]) == 0 and int(ha["trials"]) == n
+    compare(a, oracle_for(oracle_mod, name).run_trials(sites, protect_mask=0), sites)
+    assert np.array_equal(a[~esc], b[~esc])
+
+
+@pytest.mark.parametrize("name", ["crc32", "qsort"])
+def test_odd_pc_kernel(engine_factory, oracle_mod, name):
+    """pc bit-0 flips leave the pc odd: their survivors run on the solo-odd
+    kernel (translated odd-pc streams, second stream) -- the same outcomes as
+    on the solo kernel and as the oracle."""
+    e = engine_factory(name)
+    off = engine_factory(name, flags=4096)   # FI_CFG_NO_ODD_KERNEL
+    for x in (e, off):
+        x.set_campaign(0x5EED0DD, REGS | PC, 1)
+        x.set_protect(0)
+    sites = e.sample(0, 200_000)
+    sites = sites[(sites["target"] == 32) & (sites["mask"] == 1)][:600]
+    assert len(sites) > 100
+    e.kernel_timer_reset()
+    a, _ = e.run_sites(sites)
+    kinds = e.debug_dispatch_kinds()
+    assert e.translate_status() == "" and 2 in kinds, kinds
+    b, _ = off.run_sites(sites)
+    assert 2 not in off.debug_dispatch_kinds()
+    assert np.array_equal(a, b)
+    compare(a, oracle_for(oracle_mod, name).run_trials(sites, protect_mask=0), sites)
