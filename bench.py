@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0002)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--parity-trials", type=int, default=0,
+                    help="check at least this many trial ids against the oracle (beyond the timed CPU sample)")
     ap.add_argument("--lanes", type=int, default=0, help="trials per 64-lane wave (0: engine default)")
     ap.add_argument("--resume-lanes", type=int, default=0, help="trials per wave in resumed epochs (0: default)")
     ap.add_argument("--epochs", type=int, default=0, help="epochs per chunk (0: default)")
@@ -260,6 +262,13 @@ def main():
         res["parity"] = None
         if world == 1 and not a.no_cpu_baseline:
             res["cpu_baseline"], ref = cpu_baseline(elf, a.workload, a.seed, a.cpu_seconds)
+            if a.parity_trials > len(ref):   # more checked trials, untimed (not part of the baseline)
+                from oracle.pyoracle import Oracle
+                o = Oracle(elf, a.workload)
+                o.run_golden()
+                more = o.sample(a.seed, len(ref), a.parity_trials - len(ref), REGS_PC, 1)
+                ref = np.concatenate([ref, o.run_trials(more, threads=host_cores()[0])])
+                o.close()
             # the same trial ids through the device (the timed campaign's first
             # trials): every outcome must equal the oracle's, bit for bit
             dev, _ = eng.run_trials(0, len(ref))

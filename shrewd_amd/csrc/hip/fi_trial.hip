@@ -540,8 +540,8 @@ __device__ int fetch_lane(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, 
 // 4 modelled.
 __device__ int sys_class(int num) {
     switch (num) {   // modelled (oracle/rv64se.c:sys_modelled)
-    case 29: case 57: case 64: case 66: case 93: case 94: case 96: case 113: case 160: case 163: case 214:
-    case 215: case 222: case 261: case 278: case 1058:
+    case 29: case 57: case 63: case 64: case 66: case 78: case 93: case 94: case 96: case 113: case 160: case 163:
+    case 214: case 215: case 222: case 258: case 261: case 278: case 1058:
         return 4;
     default:
         if (num >= 172 && num <= 178) return 4;
@@ -2860,7 +2860,7 @@ __device__ __forceinline__ void trial_body() {
         for (int k = 0; k < 8; k++) atomicAdd(&CX->stats[32 + k], (unsigned long long)pacc[k]);
 #endif
     if (lane == 0 && CX->wave_dbg) {
-        uint64_t *wd = CX->wave_dbg + 10 * (uint64_t)blockIdx.x;
+        uint64_t *wd = CX->wave_dbg + 10 * ((uint64_t)blockIdx.x + rlo);   // (solo-odd: after the solo entries)
         wd[0] = __builtin_amdgcn_s_memtime() - t_start;
         wd[1] = n_iter;
         wd[2] = n_tx;

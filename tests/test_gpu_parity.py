@@ -549,7 +549,7 @@ def test_odd_pc_kernel(engine_factory, oracle_mod, name):
     for x in (e, off):
         x.set_campaign(0x5EED0DD, REGS | PC, 1)
         x.set_protect(0)
-    sites = e.sample(0, 200_000)
+    sites = e.sample(0, 400_000)
     sites = sites[(sites["target"] == 32) & (sites["mask"] == 1)][:600]
     assert len(sites) > 100
     e.kernel_timer_reset()

@@ -370,3 +370,20 @@ def test_sampler_bits_mask(oracle_mod):
     lows = {int(x & -x).bit_length() - 1 for x in s4["mask"]}
     assert lows == {58, 59, 60}
     assert bits_mask(0xF0) == 0xF0 and bits_mask(None) == 2**64 - 1
+
+
+def test_device_modelled_syscalls_equal_oracle():
+    """The device's modelled-syscall set (fi_trial.hip sys_class, first switch)
+    is the oracle's (rv64se.c sys_modelled): a call the oracle models must not
+    escape on the device."""
+    import re
+    from conftest import ROOT
+    dev = open(os.path.join(ROOT, "shrewd_amd", "csrc", "hip", "fi_trial.hip")).read()
+    ora = open(os.path.join(ROOT, "oracle", "rv64se.c")).read()
+    d = dev[dev.index("__device__ int sys_class(int num)"):]
+    d = d[:d.index("return 4;")]
+    o = ora[ora.index("static int sys_modelled(int num)"):]
+    o = o[:o.index("return 1;")]
+    cases = lambda t: {int(x) for x in re.findall(r"case (\d+):", t)}
+    assert cases(d) == cases(o) and 63 in cases(d)
+    assert "num >= 172 && num <= 178" in dev[dev.index("__device__ int sys_class(int num)"):][:600]
