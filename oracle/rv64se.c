@@ -266,6 +266,8 @@ typedef struct {
     int done; or_outcome_t res;
     /* counters for the roofline bookkeeping */
     u64 fetch_bytes, data_bytes;
+    /* diagnostics (or_debug_trace): committed pcs, store addresses into the text */
+    u64 *dbg_pc, dbg_pc_n, dbg_pc_cap, *dbg_wr, dbg_wr_n, dbg_wr_cap;
     const or_campaign_t *c;
 } mach_t;
 
@@ -1038,6 +1040,10 @@ static int mem_write(mach_t *m, u64 addr, unsigned size, u64 val, u64 *fault_va)
         /* AbstractMemory::checkLockedAddrList: a store erases the lock records
          * of its fragment's 16-byte granule (abstract_mem.cc:290-345) */
         if (m->lock == (a & ~0xFULL)) m->lock = OR_NONE;
+        if (m->dbg_wr && a < m->c->text_hi && a + frag > m->c->text_lo) {
+            if (m->dbg_wr_n < m->dbg_wr_cap) m->dbg_wr[m->dbg_wr_n] = a;
+            m->dbg_wr_n++;
+        }
         done += frag; a += frag;
     }
     m->data_bytes += size;
@@ -2653,6 +2659,8 @@ static void tick(mach_t *m, u64 cap) {
             }
             if (f == F_NONE) {
                 m->num_inst++;   /* countInst only on NoFault (atomic.cc:687-689) */
+                if (m->dbg_pc && m->dbg_pc_n < m->dbg_pc_cap) m->dbg_pc[m->dbg_pc_n] = m->pc;
+                if (m->dbg_pc) m->dbg_pc_n++;
                 if (m->rarm && result_fault(m, &d)) return;
             }
         }
@@ -3044,6 +3052,21 @@ int or_run_one_capture(or_campaign_t *c, const or_site_t *site, u64 protect, u64
     if (n) memcpy(buf, b.buf, n);
     *len = b.len;
     free(b.buf);
+    return 0;
+}
+
+/* Diagnostics: one trial with its committed pcs (first pcap) and the
+ * addresses of its stores into the text range (first wcap); *pn / *wn = the
+ * totals.  Tooling only (tools/trial_trace.py). */
+int or_debug_trace(or_campaign_t *c, const or_site_t *site, u64 f16, or_outcome_t *out, u64 *pcs, u64 pcap, u64 *pn,
+                   u64 *wrs, u64 wcap, u64 *wn) {
+    if (!c->have_golden) { snprintf(c->err, sizeof c->err, "golden run required"); return -1; }
+    mach_t m; mach_init(&m, c);
+    m.site = site;
+    m.dbg_pc = pcs; m.dbg_pc_cap = pcap; m.dbg_wr = wrs; m.dbg_wr_cap = wcap;
+    run(&m, hang_cap(c, f16));
+    *out = m.res; *pn = m.dbg_pc_n; *wn = m.dbg_wr_n;
+    mach_free(&m);
     return 0;
 }
 

@@ -182,6 +182,7 @@ struct fi_engine {
     uint32_t *d_svals = nullptr, *d_svals2 = nullptr;
     uint32_t *d_wrange = nullptr, *d_nwaves = nullptr;   // packed resume (FI_CFG_PACK_RUNS)
     uint32_t *d_split = nullptr;   // per epoch: odd-pc survivors, then the solo kernel's share of the list
+    uint32_t *d_dmap = nullptr;    // per slot: rewritten-code map (DevCtx::dmap, kDmapWords words)
     // second pass of the trials that ran out of private pages (run_chunk)
     uint32_t *d_redo_idx = nullptr, *d_redo_cnt = nullptr, *h_redo_cnt = nullptr;
     fi_site *d_redo_sites = nullptr;
@@ -286,7 +287,7 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
         // holds (each launch ends in its own serial tail of long trials), at
         // ~(4 KiB + 8 B) per private page + ~2.5 KiB of per-trial state
         size_t free_b = 0, total_b = 0;
-        const uint64_t per = (uint64_t)e->cfg.private_pages * (kPage + 8) + 2560;
+        const uint64_t per = (uint64_t)e->cfg.private_pages * (kPage + 8) + 2560 + kDmapWords * 4;
         uint64_t cap = 65536;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = (uint64_t)free_b / 2 / per;
         e->cfg.max_trials_per_launch = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(cap, 65536), 1u << 21);
@@ -300,7 +301,7 @@ static void free_work(fi_engine *e) {
     dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg); dfree(e->d_fregs);
     dfree(e->d_save); dfree(e->d_surv[0]); dfree(e->d_surv[1]); dfree(e->d_cnt);
     dfree(e->d_eff);
-    dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_wrange); dfree(e->d_nwaves); dfree(e->d_split); dfree(e->d_priv); dfree(e->d_priv_vpn); dfree(e->d_vm);
+    dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_wrange); dfree(e->d_nwaves); dfree(e->d_split); dfree(e->d_dmap); dfree(e->d_priv); dfree(e->d_priv_vpn); dfree(e->d_vm);
     dfree(e->d_redo_idx); dfree(e->d_redo_cnt); dfree(e->d_redo_sites); dfree(e->d_redo_out);
     e->cap = 0;
 }
@@ -690,6 +691,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_wrange, c * 8));
     HIPCHK(hipMalloc(&e->d_nwaves, 16 * 4));
     HIPCHK(hipMalloc(&e->d_split, 64 * 4));
+    HIPCHK(hipMalloc(&e->d_dmap, c * kDmapWords * 4));
     HIPCHK(hipMalloc(&e->d_redo_idx, c * 4));
     HIPCHK(hipMalloc(&e->d_redo_cnt, 16));
     HIPCHK(hipMalloc(&e->d_redo_sites, c * sizeof(fi_site)));
@@ -697,6 +699,16 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     if (!e->h_redo_cnt) HIPCHK(hipHostMalloc(&e->h_redo_cnt, 16));
     e->cap = c;
     return FI_OK;
+}
+
+// The rewritten-code map's granule: 16 bytes, coarser for large code so that
+// a slot's map stays within kDmapWords x 32 bits (the solo kernel's LDS
+// copy, fi_trial.hip kDmapWords).
+static void dmap_params(const fi_engine *e, uint32_t &shift, uint32_t &words) {
+    const uint64_t cb = e->code_hi > e->code_lo ? e->code_hi - e->code_lo : 1;
+    shift = 4;
+    while ((cb >> shift) >= kDmapWords * 32) shift++;
+    words = (uint32_t)((((cb + (1ULL << shift) - 1) >> shift) + 31) / 32);
 }
 
 static DevCtx base_ctx(fi_engine *e) {
@@ -733,6 +745,8 @@ static DevCtx base_ctx(fi_engine *e) {
     c.fp0 = e->fp0_on ? e->d_fp0 : nullptr;
     c.fcsr0 = e->fcsr0;
     c.vm0 = e->vm0_on ? e->d_vm0 : nullptr;
+    c.dmap = e->d_dmap;
+    dmap_params(e, c.dmap_shift, c.dmap_words);
     c.lanes = e->cfg.lanes_per_wave;
     c.mem_live = (e->mem_live && !(e->cfg.flags & FI_CFG_NO_EARLY_EXIT)) ? 1 : 0;
     c.mw_n = e->mw_n; c.mw_addr = e->d_mw_addr; c.mw_off = e->d_mw_off; c.mw_ev = e->d_mw_ev;
@@ -753,6 +767,7 @@ static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_
     HIPCHK(hipMalloc(&d_gfregs, 32 * sizeof(uint64_t)));
     DevCtx c = base_ctx(e);
     c.fregs = d_gfregs;
+    c.dmap = nullptr;
     c.record = 1;
     c.early_exit = 0;
     c.snap_start = 0;

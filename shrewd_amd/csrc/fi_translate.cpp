@@ -589,8 +589,13 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto tx_dispatch; }" : "; goto tx_out; }");
     };
     auto sgo = [&](uint32_t from, uint64_t pc) {
-        if (oddon && (cur_odd || (pc & 1)))
-            return "{ spc = " + hex(pc) + ((!(pc & 1) || olead.count(pc)) ? "; goto " + SD + "; }" : "; goto S_out; }");
+        // solo-odd body: an odd target with a block is a direct edge (the
+        // odd blocks are entered at their first pc only); an even one goes
+        // through the dispatch
+        if (oddon && (pc & 1))
+            return olead.count(pc) ? "goto " + SOB + std::to_string((uint32_t)((pc - text_lo) >> 1)) + ";"
+                                   : "{ spc = " + hex(pc) + "; goto S_out; }";
+        if (oddon && cur_odd) return "{ spc = " + hex(pc) + "; goto " + SD + "; }";
         const Edge k = edge(from, pc);
         uint32_t t = 0;
         hof(pc, t);
@@ -701,8 +706,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         // ---- solo block prologue: one uniform check
         so_.put("  if ((st + %uu > bud)", n);
         if (rw) so_.put(" | ((lwm & 0x%xu) != 0)", rw);
-        so_.put(" | ((sdlo < %uu) & (sdhi > %uu))) { spc = %s; goto S_out; }\n", (uint32_t)(bhi - text_lo),
-               (uint32_t)(blo - text_lo), P0.c_str());
+        so_.put(" | SDIRTY(%uu, %uu)) { spc = %s; goto S_out; }\n", (uint32_t)(blo - text_lo),
+                (uint32_t)(bhi - text_lo), P0.c_str());
         uint32_t k_st = 0, k_xt = 0, k_fb = 0, k_db = 0;   // committed so far in this block
         auto commit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
             // per-lane counters of the running lanes (zero terms omitted), wave iterations

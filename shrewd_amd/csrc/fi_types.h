@@ -8,6 +8,7 @@
 namespace fi {
 
 constexpr uint64_t kPage = 4096;
+constexpr uint32_t kDmapWords = 128;  // rewritten-code map: at most 4096 granules per slot (DevCtx::dmap)
 constexpr uint64_t kFwDead = ~0ULL;  // DevCtx::eff: the flipped register is dead at injection
 // RiscvProcess64 constants, src/arch/riscv/process.cc:73-80
 constexpr uint64_t kStackBase = 0x7FFFFFFFFFFFFFFFULL;
@@ -197,6 +198,8 @@ struct DevCtx {
     const uint64_t *fp0;             // a checkpoint's FP registers (NULL: none -- zero, no FP state)
     uint32_t fcsr0;                  //   and its fflags | frm << 5
     const VmState *vm0;              // a checkpoint's SE memory map (NULL: the process-start one, brk0 / svma_*)
+    uint32_t *dmap;                  // per slot: rewritten-code granules of [code_lo, code_hi), dmap_words u32 each
+    uint32_t dmap_words, dmap_shift; //   (granule = 2^dmap_shift bytes); NULL: the bounding range only
     uint32_t simt_min;               // diverged-lanes step loop: least lanes to enter it (0 = off)
     // memory liveness: record mode appends the golden run's data accesses to
     // rec_mem; trials look a memory fault's word up in the per-word index built

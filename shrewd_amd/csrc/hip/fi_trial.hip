@@ -142,12 +142,33 @@ struct LaneMem {
     uint64_t resv, lock;
     bool vm;                       // VmState of the slot is live (the trial made a VM syscall)
     uint32_t nmiss;                // diagnostics: full page-table lookups (TLB misses)
+    uint32_t *dl;                  // solo kernel: LDS copy of the slot's rewritten-code map (else NULL)
 };
 
+// Rewritten code, exactly: DevCtx::dmap holds per slot one bit per
+// 2^dmap_shift-byte granule of [code_lo, code_hi) the lane stored into
+// (zeroed at its first such store); [dlo, dhi) bounds them.  The solo kernel
+// keeps an LDS copy (LaneMem::dl) and asks the map; the 64-lane kernel asks
+// the bounding range only (conservative).
+// (out of line: called only for a lane whose bounding range meets [lo, hi),
+// and the translated bodies check at every block)
+__device__ __noinline__ bool dmap_test(KCtx *c, const uint32_t *dl, uint64_t lo, uint64_t hi) {
+    const uint64_t a = lo > c->code_lo ? lo : c->code_lo, b = hi < c->code_hi ? hi : c->code_hi;
+    if (a >= b) return false;
+    const uint32_t sh = c->dmap_shift;
+    const uint32_t g0 = (uint32_t)((a - c->code_lo) >> sh), g1 = (uint32_t)((b - 1 - c->code_lo) >> sh);
+    for (uint32_t g = g0; g <= g1; g++)
+        if ((dl[g >> 5] >> (g & 31)) & 1) return true;
+    return false;
+}
+__device__ __forceinline__ bool dirty_range(KCtx *c, const LaneMem &m, uint64_t lo, uint64_t hi) {
+    if (!m.code_dirty || lo >= m.dhi || hi <= m.dlo) return false;
+    return !m.dl || dmap_test(c, m.dl, lo, hi);
+}
 // The golden pre-decode of the instruction at pc is stale for this lane only if
 // the lane rewrote one of its bytes (conservatively [pc & ~3, pc + 6)).
-__device__ __forceinline__ bool dirty_at(const LaneMem &m, uint64_t pc) {
-    return m.code_dirty && (pc & ~3ULL) < m.dhi && pc + 6 > m.dlo;
+__device__ __forceinline__ bool dirty_at(KCtx *c, const LaneMem &m, uint64_t pc) {
+    return m.code_dirty && dirty_range(c, m, pc & ~3ULL, pc + 6);
 }
 // Does the lane's rewritten range come within kTxNear bytes after pc?  A
 // translated block that would meet it exits there (an entry and an exit for a
@@ -156,10 +177,40 @@ constexpr uint64_t kTxNear = 256;
 __device__ __forceinline__ bool dirty_near(const LaneMem &m, uint64_t pc) {
     return m.code_dirty && (pc & ~3ULL) < m.dhi && pc + kTxNear > m.dlo;
 }
-__device__ __forceinline__ void mark_dirty(LaneMem &m, uint64_t lo, uint64_t hi) {
-    m.dlo = m.code_dirty ? (lo < m.dlo ? lo : m.dlo) : lo;
-    m.dhi = m.code_dirty ? (hi > m.dhi ? hi : m.dhi) : hi;
+__device__ __noinline__ void dmap_mark(KCtx *c, uint32_t *dl, uint64_t slot, uint64_t lo, uint64_t hi, bool fresh) {
+    uint32_t *g = c->dmap + slot * c->dmap_words;
+    if (fresh)
+        for (uint32_t i = 0; i < c->dmap_words; i++) g[i] = 0;   // (the solo kernel's LDS copy starts zeroed)
+    const uint64_t a = lo > c->code_lo ? lo : c->code_lo, b = hi < c->code_hi ? hi : c->code_hi;
+    if (a >= b) return;
+    const uint32_t sh = c->dmap_shift;
+    for (uint32_t q = (uint32_t)((a - c->code_lo) >> sh); q <= (uint32_t)((b - 1 - c->code_lo) >> sh); q++) {
+        g[q >> 5] |= 1u << (q & 31);
+        if (dl) dl[q >> 5] |= 1u << (q & 31);
+    }
+}
+__device__ __forceinline__ void mark_dirty(KCtx *c, LaneMem &m, uint64_t slot, uint64_t lo, uint64_t hi) {
+    const bool fresh = !m.code_dirty;
+    m.dlo = fresh ? lo : (lo < m.dlo ? lo : m.dlo);
+    m.dhi = fresh ? hi : (hi > m.dhi ? hi : m.dhi);
     m.code_dirty = true;
+    if (c->dmap) dmap_mark(c, m.dl, slot, lo, hi, fresh);
+}
+// A translated solo store into the code range (at most 8 bytes): the bounding
+// range and the LDS map only -- the solo kernel's map lives in LDS (copied to
+// the slot's global map when the lane suspends), which it zeroes at a fresh
+// start, so nothing needs clearing here.
+__device__ __forceinline__ void mark_dirty_solo(KCtx *c, LaneMem &m, uint64_t lo, uint64_t hi) {
+    const bool fresh = !m.code_dirty;
+    m.dlo = fresh ? lo : (lo < m.dlo ? lo : m.dlo);
+    m.dhi = fresh ? hi : (hi > m.dhi ? hi : m.dhi);
+    m.code_dirty = true;
+    if (!m.dl) return;
+    const uint64_t a = lo > c->code_lo ? lo : c->code_lo, b = hi < c->code_hi ? hi : c->code_hi;
+    if (a >= b) return;
+    const uint32_t q0 = (uint32_t)((a - c->code_lo) >> c->dmap_shift), q1 = (uint32_t)((b - 1 - c->code_lo) >> c->dmap_shift);
+    m.dl[q0 >> 5] |= 1u << (q0 & 31);
+    m.dl[q1 >> 5] |= 1u << (q1 & 31);
 }
 
 // The lane's start-snapshot page table (uniform in a fresh launch; per lane
@@ -369,7 +420,7 @@ __device__ int vm_unmap(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, Vm
         return true;
     });
     tlb_flush(m);
-    if (lo < c->code_hi && hi > c->code_lo) mark_dirty(m, lo, hi);   // the pre-decoded text no longer applies
+    if (lo < c->code_hi && hi > c->code_lo) mark_dirty(c, m, slot, lo, hi);   // the pre-decoded text no longer applies
     return full ? 1 : 0;
 }
 // Readable through SETranslatingPortProxy (no fixups on reads)
@@ -411,7 +462,7 @@ __device__ bool proxy_write(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot
         }
         const_cast<uint8_t *>(page_of(p))[x & 4095] = (uint8_t)src[i];
     }
-    if (a < c->code_hi && a + n > c->code_lo) mark_dirty(m, a, a + n);
+    if (a < c->code_hi && a + n > c->code_lo) mark_dirty(c, m, slot, a, a + n);
     return true;
 }
 
@@ -448,7 +499,7 @@ __device__ int mem_access(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, 
         if (ok) {
             uint8_t *w1 = const_cast<uint8_t *>(page_of(p1));
             for (uint32_t i = 0; i < n1; i++) w1[off + i] = (uint8_t)(val >> (8 * i));
-            if (ea < c->code_hi && ea + n1 > c->code_lo) mark_dirty(m, ea, ea + n1);
+            if (ea < c->code_hi && ea + n1 > c->code_lo) mark_dirty(c, m, slot, ea, ea + n1);
             m.lock = kNone;
         }
         val = ok ? 1 : 0;
@@ -467,7 +518,7 @@ __device__ int mem_access(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, 
     if (wr) {
         if (!(p1 & 1)) { m.req_vpn = ea >> 12; m.req_src = page_of(p1); return F_NEEDPAGE; }
         if (!(p2 & 1)) { m.req_vpn = ea2 >> 12; m.req_src = page_of(p2); return F_NEEDPAGE; }
-        if (ea < c->code_hi && ea + size > c->code_lo) mark_dirty(m, ea, ea + size);   // the lane rewrote its code
+        if (ea < c->code_hi && ea + size > c->code_lo) mark_dirty(c, m, slot, ea, ea + size);   // the lane rewrote its code
         uint8_t *w1 = const_cast<uint8_t *>(page_of(p1));
         if (n1 == size && (off & (size - 1)) == 0) {
             switch (size) {
@@ -1481,6 +1532,11 @@ __device__ __forceinline__ void trial_body() {
     m.resv = m.lock = kNone;
     m.vm = false;
     m.nmiss = 0;
+    // the solo kernel's LDS copy of the slot's rewritten-code map
+    __shared__ uint32_t DMAP[kNL == 1 ? kDmapWords : 1];
+    m.dl = (kNL == 1 && CX->dmap) ? DMAP : nullptr;
+    if (m.dl)
+        for (uint32_t i = 0; i < CX->dmap_words; i++) m.dl[i] = 0;
     if (CX->fp0 && live && !resume) {   // a checkpoint with FP state: every lane starts with it
         for (int r = 0; r < 32; r++) CX->fregs[(uint64_t)r * CX->n_slots + slot] = CX->fp0[r];
         L.fp = true;
@@ -1496,6 +1552,8 @@ __device__ __forceinline__ void trial_body() {
         m.dlo = CX->code_lo + SV->dlo; m.dhi = CX->code_lo + SV->dhi;
         m.resv = SV->resv; m.lock = SV->lock;
         m.vm = (SV->flags >> 5) & 1;
+        if (m.dl && m.code_dirty)
+            for (uint32_t i = 0; i < CX->dmap_words; i++) m.dl[i] = CX->dmap[slot * CX->dmap_words + i];
     }
     if (fw_dead && !resume) {   // dead at injection: the trial is the golden run
         L.injected = 1;
@@ -1574,6 +1632,8 @@ __device__ __forceinline__ void trial_body() {
                             (L.fp ? 16u : 0u) | (m.vm ? 32u : 0u);
                 sv->resv = m.resv; sv->lock = m.lock;
                 sv->pad = (uint32_t)L.fflags | ((uint32_t)L.frm << 5);
+                if (m.dl && m.code_dirty)   // the solo kernel's map lives in LDS
+                    for (uint32_t i = 0; i < CX->dmap_words; i++) CX->dmap[slot * CX->dmap_words + i] = m.dl[i];
                 CX->surv[atomicAdd(CX->surv_n, 1u)] = (uint32_t)slot;
                 suspended = true;
                 L.done = true;
@@ -1640,7 +1700,7 @@ __device__ __forceinline__ void trial_body() {
                 } else {
                     uint64_t *wp = (uint64_t *)(const_cast<uint8_t *>(page_of(p)) + (s.addr & 4095));
                     *wp ^= s.mask;
-                    if (s.addr < CX->code_hi && s.addr + 8 > CX->code_lo) mark_dirty(m, s.addr, s.addr + 8);
+                    if (s.addr < CX->code_hi && s.addr + 8 > CX->code_lo) mark_dirty(CX, m, slot, s.addr, s.addr + 8);
                     DC_INVAL(s.addr, 8);
                     L.injected = 1;
                 }
@@ -1777,7 +1837,7 @@ __device__ __forceinline__ void trial_body() {
                     const uint4 *const pre4 = (const uint4 *)CX->pre;
                     for (;;) {
                         const uint64_t toff = pc - tlo;
-                        bool go = run && toff < tby && !(pc & 1) && !dirty_at(m, pc);
+                        bool go = run && toff < tby && !(pc & 1) && !dirty_at(CX, m, pc);
                         uint4 e = make_uint4(0u, 0u, 0u, 0u);
                         if (go) e = pre4[toff >> 1];
                         const uint32_t aux = e.w >> 16, kind = aux & 63, pf = (e.w >> 8) & 0xFF;
@@ -1917,8 +1977,7 @@ __device__ __forceinline__ void trial_body() {
             if constexpr (kNL == 1) {
                 // ---- solo: one trial, every value uniform -- no groups, no
                 // parking, plain register writes; the same exits and counters
-                if (tx_entry && mine && n_iter >= tx_skip_until && !dirty_near(m, lpc) && L.injected != 3 &&
-                    m.lock == kNone) {
+                if (tx_entry && mine && n_iter >= tx_skip_until && L.injected != 3 && m.lock == kNone) {
                     const uint64_t rem64 = next_ev - L.ninst;
                     const uint32_t rem = rem64 > (1u << 30) ? (1u << 30) : (uint32_t)rem64;
                     const uint32_t wbud = CX->wave_budget ? CX->wave_budget - n_iter : (1u << 30);
@@ -1939,7 +1998,10 @@ __device__ __forceinline__ void trial_body() {
         cslo = o_ < cslo ? o_ : cslo;                                                           \
         cshi = o_ + (sz_) > cshi ? o_ + (sz_) : cshi;                                           \
         schg = true;                                                                            \
+        mark_dirty_solo(CX, m, (ea_), (ea_) + (sz_));                                           \
     } while (0)
+// a block's bytes [tlo + lo_, tlo + hi_) hold code the lane rewrote (exact map)
+#define SDIRTY(lo_, hi_) (((sdlo < (hi_)) & (sdhi > (lo_))) && dirty_range(CX, m, tlo + (lo_), tlo + (hi_)))
                     const uint32_t lwm = L.watch > 0 ? (1u << L.watch) : 0u;
                     uint32_t st = 0, xt = 0, fb = 0, db = 0;   // instructions, straddles, fetch/data bytes
                     uint64_t spc = lpc;
@@ -1966,6 +2028,7 @@ __device__ __forceinline__ void trial_body() {
                     TXW(26) TXW(27) TXW(28) TXW(29) TXW(30) TXW(31)
 #undef TXW
 #undef TXCODE
+#undef SDIRTY
                     if (schg) {
                         m.code_dirty = true; m.dlo = tlo + sdlo; m.dhi = tlo + sdhi;
 #pragma unroll 8
@@ -2102,7 +2165,7 @@ __device__ __forceinline__ void trial_body() {
             while (budget) {
                 PSTAMP(3);
                 spc = uni64(spc);
-                if (any_dirty && wballot<kNL>(mine && dirty_at(m, spc)) != 0) {
+                if (any_dirty && wballot<kNL>(mine && dirty_at(CX, m, spc)) != 0) {
                     // the group rewrote this instruction: decode the bytes the
                     // lanes hold now (Decoder::moreBytes on their own pages) when
                     // they all hold the same; otherwise the general path
@@ -2145,8 +2208,8 @@ __device__ __forceinline__ void trial_body() {
                 // translated blocks take over here (odd pcs: only the solo-odd
                 // kernel's odd-pc blocks, flagged on the entry of the halfword they fetch)
                 const bool lead = ((uint32_t)spc & 1) ? (kOdd && ((q3 >> 8) & kPreOddLeader)) : ((q3 >> 8) & kPreLeader);
-                if (steps && lead &&
-                    !(any_dirty && wballot<kNL>(mine && dirty_near(m, spc)) != 0) && n_iter + steps >= tx_skip_until)
+                if (steps && lead && (kNL == 1 || !(any_dirty && wballot<kNL>(mine && dirty_near(m, spc)) != 0)) &&
+                    n_iter + steps >= tx_skip_until)
                     break;
 #endif
                 const uint32_t rd = q1 >> 8 & 0xFF, rs1 = q1 >> 16 & 0xFF, rs2 = q1 >> 24;
@@ -2243,7 +2306,7 @@ __device__ __forceinline__ void trial_body() {
                     if (CX->record && mine) rec_mem(CX, ea, msz, L.ninst + steps, st ? 2u : 1u);
                     if constexpr (kNL == 1) {
                         if (code_st) {
-                            mark_dirty(m, ea, ea + msz);
+                            mark_dirty(CX, m, slot, ea, ea + msz);
                             DC_INVAL(ea, msz);
                             any_dirty = true;
                         }
@@ -2321,7 +2384,7 @@ __device__ __forceinline__ void trial_body() {
         uint32_t ticks = 1;
         bool fast = false;
         const uint64_t key = (lpc & 3) ? ((lpc & ~3ULL) | 2) : lpc;
-        if (CX->pre_ok && key >= CX->text_lo && key < CX->text_hi && wballot<kNL>(mine && dirty_at(m, lpc)) == 0) {
+        if (CX->pre_ok && key >= CX->text_lo && key < CX->text_hi && wballot<kNL>(mine && dirty_at(CX, m, lpc)) == 0) {
             const Pre4 q = pre_load(CX->pre + ((key - CX->text_lo) >> 1));
             const uint32_t pflags = (q.w >> 8) & 0xFF;
             if (pflags & kPreValid) {
@@ -2835,7 +2898,7 @@ __device__ __forceinline__ void trial_body() {
             const uint32_t wn = uni32(En.e.w);
             // (solo: a lane in rewritten code goes back too; the pre-decoded
             // path decodes its own bytes through the decode cache)
-            const bool dty = wballot<kNL>(cont && dirty_at(m, npc0)) != 0;
+            const bool dty = wballot<kNL>(cont && dirty_at(CX, m, npc0)) != 0;
             const bool lck = wballot<kNL>(cont && m.lock != kNone) != 0;
             if (!lck && En.in && ((wn >> 8) & kPreValid) &&
                 ((kNL == 1 && dty) || (((wn >> 16) & 63) != K_SLOW && !dty)))

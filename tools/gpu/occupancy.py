@@ -60,3 +60,16 @@ for b in np.argsort(-dur_all)[:8]:
                       "mask": hex(int(s["mask"])) if s is not None else None,
                       "inst": int(s["inst"]) if s is not None else None,
                       "cls": int(out["cls"][tr]) if tr < n else None}), flush=True)
+# where the dispatch's wave-time goes, by the outcome class of each wave's
+# (lane 0) trial: waves, summed wave-microseconds, summed instructions
+trs = wv[live, 6]
+ok = trs < n
+cls_of = np.where(ok, out["cls"][np.minimum(trs, n - 1)], 255)
+us = (wv[live, 5] - wv[live, 4]) / 100.0
+agg = {}
+for c in np.unique(cls_of):
+    m = cls_of == c
+    agg[["masked", "sdc", "crash", "hang", "detected", "escape"][c] if c < 6 else "?"] = {
+        "waves": int(m.sum()), "wave_us": round(float(us[m].sum()), 1), "insts": int(wv[live, 7][m].sum()),
+        "median_insts": int(np.median(wv[live, 7][m]))}
+print(json.dumps({"by_class": agg}), flush=True)
