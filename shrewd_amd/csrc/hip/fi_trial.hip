@@ -161,6 +161,17 @@ __device__ __noinline__ bool dmap_test(KCtx *c, const uint32_t *dl, uint64_t lo,
         if ((dl[g >> 5] >> (g & 31)) & 1) return true;
     return false;
 }
+// The same test inline, on the solo kernel's LDS copy of the map (at most a
+// few granules: an instruction's 6 bytes, or one translated block).
+__device__ __forceinline__ bool dmap_any(const __attribute__((address_space(3))) uint32_t *dl, uint64_t clo,
+                                         uint64_t chi, uint32_t sh, uint64_t lo, uint64_t hi) {
+    const uint64_t a = lo > clo ? lo : clo, b = hi < chi ? hi : chi;
+    if (a >= b) return false;
+    const uint32_t g0 = (uint32_t)((a - clo) >> sh), g1 = (uint32_t)((b - 1 - clo) >> sh);
+    uint32_t r = 0;
+    for (uint32_t g = g0; g <= g1; g++) r |= dl[g >> 5] >> (g & 31);
+    return (r & 1) != 0;
+}
 __device__ __forceinline__ bool dirty_range(KCtx *c, const LaneMem &m, uint64_t lo, uint64_t hi) {
     if (!m.code_dirty || lo >= m.dhi || hi <= m.dlo) return false;
     return !m.dl || dmap_test(c, m.dl, lo, hi);
@@ -1411,6 +1422,309 @@ __device__ __forceinline__ bool ult64(uint64_t a, uint64_t b) {
     return ah < bh || (ah == bh && (uint32_t)a < (uint32_t)b);
 }
 
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+typedef __attribute__((address_space(3))) LaneMem lds_mem;
+
+#ifdef FI_TX
+// ---- solo translated blocks, out of line.  Inlined into trial_body<1> they
+// shared one register allocation with the whole interpreter: thousands of
+// SGPR spills and VGPR scratch spills, some inside the hot blocks.  Here the
+// allocator sees only the guest registers, the lane's TLB and the block
+// counters.  The caller passes everything through LDS (its register file R,
+// its LaneMem and this record); the function reads them back as uniform
+// values, runs the blocks from `spc` and writes the registers and the
+// counters back.
+struct SoloTxIO {
+    uint64_t spc;                        // in: entry pc; out: where the blocks left
+    uint32_t bud, lwm, sdlo, sdhi;       // in: instruction budget, watched-register mask, rewritten range
+    uint32_t st, xt, fb, db;             // out: instructions, straddle ticks, fetch / data bytes
+    uint32_t cslo, cshi, schg;           // out: code bytes the blocks rewrote (offsets from text_lo)
+};
+typedef __attribute__((address_space(3))) SoloTxIO lds_io;
+
+template <bool kOdd>
+__device__ __noinline__ void solo_tx_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds_io *io) {
+    // the arguments arrive in VGPRs: make the LDS addresses (and so every
+    // value read through them) uniform
+    CX = (KCtx *)(uintptr_t)uni64((uint64_t)(uintptr_t)CX);
+    R = (lds_u64 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)R);
+    mp = (lds_mem *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)mp);
+    io = (lds_io *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)io);
+    LaneMem m = *mp;   // TLB and rewritten-code state in registers (the blocks never insert into the TLB)
+    TextRef tx;
+    tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
+    tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
+    const uint64_t tlo = CX->text_lo;
+    uint64_t spc = io->spc;
+    const uint32_t bud = io->bud, lwm = io->lwm;
+    uint32_t sdlo = io->sdlo, sdhi = io->sdhi;
+    uint32_t etgt = 0xFFFFFFFFu;   // block an entry is routed to through its cycle headers
+    bool schg = false;
+    uint32_t cslo = 0xFFFFFFFFu, cshi = 0u;
+    uint32_t st = 0, xt = 0, fb = 0, db = 0;
+// a translated store rewrote code bytes [ea_, ea_ + sz_): later blocks see the
+// grown range; the decode cache forgets them when the blocks are left
+#define TXCODE(ea_, sz_)                                                                        \
+    do {                                                                                        \
+        const uint32_t o_ = SUNI32((uint32_t)((ea_) - tlo));                                    \
+        sdlo = o_ < sdlo ? o_ : sdlo;                                                           \
+        sdhi = o_ + (sz_) > sdhi ? o_ + (sz_) : sdhi;                                           \
+        cslo = o_ < cslo ? o_ : cslo;                                                           \
+        cshi = o_ + (sz_) > cshi ? o_ + (sz_) : cshi;                                           \
+        schg = true;                                                                            \
+        mark_dirty_solo(CX, m, (ea_), (ea_) + (sz_));                                           \
+    } while (0)
+// a block's bytes [tlo + lo_, tlo + hi_) hold code the lane rewrote (exact map)
+    const __attribute__((address_space(3))) uint32_t *const dl = (const __attribute__((address_space(3))) uint32_t *)m.dl;
+    const bool have_dl = m.dl != nullptr;
+    const uint32_t dsh = CX->dmap_shift;
+#define SDIRTY(lo_, hi_) \
+    (((sdlo < (hi_)) & (sdhi > (lo_))) && (!have_dl || dmap_any(dl, tx.clo, tx.chi, dsh, tlo + (lo_), tlo + (hi_))))
+#define TXR(r) uint64_t X##r = R[r];
+    TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
+    TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
+    TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
+#undef TXR
+#ifdef FI_TX_SOLO_ODD
+    if constexpr (kOdd) {
+        goto Q_dispatch;
+        /*@TX_SOLO_ODD@*/
+    } else
+#endif
+    {
+        goto S_dispatch;
+        /*@TX_SOLO@*/
+    }
+S_out:
+#define TXW(r) R[r] = X##r;
+    TXW(1) TXW(2) TXW(3) TXW(4) TXW(5) TXW(6) TXW(7) TXW(8) TXW(9) TXW(10) TXW(11) TXW(12) TXW(13)
+    TXW(14) TXW(15) TXW(16) TXW(17) TXW(18) TXW(19) TXW(20) TXW(21) TXW(22) TXW(23) TXW(24) TXW(25)
+    TXW(26) TXW(27) TXW(28) TXW(29) TXW(30) TXW(31)
+#undef TXW
+#undef TXCODE
+#undef SDIRTY
+    if (schg) {   // mark_dirty_solo changed the bounding range (its LDS map bits are written already)
+        mp->code_dirty = true; mp->dlo = m.dlo; mp->dhi = m.dhi;
+    }
+    io->spc = spc; io->st = st; io->xt = xt; io->fb = fb; io->db = db;
+    io->cslo = cslo; io->cshi = cshi; io->schg = schg ? 1u : 0u;
+}
+#endif
+
+// ---- solo pre-decoded run, out of line: the fast path of trial_body<1>
+// (one trial, every value uniform) with its own register allocation.  Same
+// rules as the 64-lane fast path below: pre-decoded micro-ops from pc until
+// the budget is spent, an instruction the path does not own (K_SLOW, a fault,
+// a TLB miss lookup_full cannot resolve, copy-on-write, a page-crossing
+// access, a watched register read), or (translated build) a block leader the
+// translated blocks take over.  Rewritten code is decoded from the lane's own
+// bytes through the decode cache (DCT/DCE), and stores into the code range
+// mark the bytes rewritten.  Nothing commits unless the whole instruction does.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) Pre4 lds_pre4;
+struct SoloPreIO {
+    uint64_t spc;          // in: start pc; out: next pc
+    uint64_t slot;         // in: the trial's slot
+    const PageEnt *tab;    // in: start-snapshot page table
+    uint32_t tab_n;
+    uint32_t budget;       // in: instructions at most
+    uint32_t tx_gate;      // in: leaders stop the run once steps >= tx_gate (translated build)
+    int32_t watch;         // in/out: watched flipped register (-1 none)
+    uint32_t steps, xticks, fbytes, dbytes;   // out
+};
+typedef __attribute__((address_space(3))) SoloPreIO lds_pio;
+constexpr uint32_t kSoloDC = 64;   // decode-cache entries (power of two)
+
+template <bool kOdd>
+__device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds_u32 *DCT, lds_pre4 *DCE,
+                                          lds_pio *io) {
+    CX = (KCtx *)(uintptr_t)uni64((uint64_t)(uintptr_t)CX);
+    R = (lds_u64 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)R);
+    mp = (lds_mem *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)mp);
+    DCT = (lds_u32 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)DCT);
+    DCE = (lds_pre4 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)DCE);
+    io = (lds_pio *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)io);
+    LaneMem &m = *(LaneMem *)mp;   // lookup_full / fetch_lane / mark_dirty take it by reference
+    const uint64_t slot = uni64(io->slot);
+    WaveMem w;
+    w.tab = (const PageEnt *)uni64((uint64_t)io->tab);
+    w.tab_n = uni32(io->tab_n);
+    const uint32_t budget = io->budget;
+#ifdef FI_TX
+    const uint32_t tx_gate = io->tx_gate;
+#endif
+    int32_t watch = io->watch;
+    TextRef tx;
+    tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
+    tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
+    const uint64_t tlo = CX->text_lo;
+    // the TLB in registers (refreshed after lookup_full inserts)
+    uint64_t tv0 = m.tv0, tv1 = m.tv1, tv2 = m.tv2, tv3 = m.tv3, tp0 = m.tp0, tp1 = m.tp1, tp2 = m.tp2, tp3 = m.tp3;
+    bool dirty = m.code_dirty;
+    uint64_t dlo = m.dlo, dhi = m.dhi;
+    // the rewritten-code map (LDS; null: the bounding range decides)
+    const __attribute__((address_space(3))) uint32_t *const dl = (const __attribute__((address_space(3))) uint32_t *)m.dl;
+    const bool have_dl = m.dl != nullptr;
+    const uint32_t dsh = CX->dmap_shift;
+    uint64_t spc = io->spc;
+    uint32_t steps = 0, xticks = 0, fbytes = 0, dbytes = 0;
+    PreRef E = pre_entry(tx, spc);
+    while (steps < budget) {
+        spc = uni64(spc);
+        // the lane rewrote bytes of this instruction: its own bytes, decoded
+        // (through the decode cache); conservatively [pc & ~3, pc + 6)
+        // (a decode-cache hit is the decode of the lane's current bytes: stores
+        // drop the entries they overlap; only a miss asks the map)
+        const uint32_t ci = (uint32_t)(spc >> 1) & (kSoloDC - 1);
+        if (dirty && (spc & ~3ULL) < dhi && spc + 6 > dlo) {
+            const bool in_code = spc >= tx.clo && spc < tx.chi;
+            if (in_code && DCT[ci] == (uint32_t)(spc - tlo)) {
+                E.e.x = DCE[ci].x; E.e.y = DCE[ci].y; E.e.z = DCE[ci].z; E.e.w = DCE[ci].w; E.in = true;
+            } else if (!have_dl || dmap_any(dl, tx.clo, tx.chi, dsh, spc & ~3ULL, spc + 6)) {
+                uint32_t raw = 0, t = 1;
+                uint64_t fva = 0;
+                if (fetch_lane(CX, w, m, slot, spc, raw, t, fva) != 0) break;
+                tv0 = m.tv0; tv1 = m.tv1; tv2 = m.tv2; tv3 = m.tv3; tp0 = m.tp0; tp1 = m.tp1; tp2 = m.tp2; tp3 = m.tp3;
+                Dec dd = rv_decode(uni32(raw));
+                const uint32_t u = uop_of(dd);
+                E.in = true;
+                E.e.x = dd.raw;
+                E.e.y = (uint32_t)dd.op | ((uint32_t)dd.rd << 8) | ((uint32_t)dd.rs1 << 16) | ((uint32_t)dd.rs2 << 24);
+                E.e.z = (uint32_t)dd.imm;
+                E.e.w = (uint32_t)dd.len | ((uint32_t)(kPreValid | (uni32(t) == 2 ? kPreStraddle : 0) | dd.flags) << 8) |
+                        (u << 16);
+                if (in_code) {
+                    DCT[ci] = (uint32_t)(spc - tlo);
+                    DCE[ci].x = E.e.x; DCE[ci].y = E.e.y; DCE[ci].z = E.e.z; DCE[ci].w = E.e.w;
+                }
+            }
+        }
+        const uint32_t q1 = uni32(E.e.y), q2 = uni32(E.e.z), q3 = uni32(E.e.w);
+        const uint32_t aux = q3 >> 16, kind = aux & 63;
+        if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
+#ifdef FI_TX
+        const bool lead = ((uint32_t)spc & 1) ? (kOdd && ((q3 >> 8) & kPreOddLeader)) : ((q3 >> 8) & kPreLeader);
+        if (steps && lead && steps >= tx_gate) break;
+#endif
+        const uint32_t rd = q1 >> 8 & 0xFF, rs1 = q1 >> 16 & 0xFF, rs2 = q1 >> 24;
+        if (watch > 0 && ((((q3 >> 8) & kPreRs1) && rs1 == (uint32_t)watch) ||
+                          (((q3 >> 8) & kPreRs2) && rs2 == (uint32_t)watch)))
+            break;
+        const int64_t imm = (int32_t)q2;
+        const uint32_t len = q3 & 0xFF, straddle = ((q3 >> 8) & kPreStraddle) ? 1 : 0;
+        const uint64_t a0 = R[rs1], b0 = R[rs2];
+        const uint64_t ft = spc + len;
+        const PreRef Eft = pre_entry(tx, ft);   // successors' entries load while this one executes
+        const PreRef Etg = pre_entry(tx, spc + imm);
+        const uint64_t av = (aux & U_APC) ? spc : a0;
+        const uint64_t bv = (aux & U_BIMM) ? (uint64_t)imm : b0;
+        const bool w32 = aux & U_W32;
+        const uint32_t shm = w32 ? 31 : 63;
+        uint64_t v = 0, npc = ft;
+        uint32_t msz = 0;
+        bool wr = true, took = false, ind = false;
+        switch (kind) {
+        case K_ADD: v = av + bv; break;
+        case K_SUB: v = av - bv; break;
+        case K_AND: v = av & bv; break;
+        case K_OR: v = av | bv; break;
+        case K_XOR: v = av ^ bv; break;
+        case K_SLT: v = (int64_t)av < (int64_t)bv ? 1 : 0; break;
+        case K_SLTU: v = av < bv ? 1 : 0; break;
+        case K_SLL: v = av << (bv & shm); break;
+        case K_SRL: v = (w32 ? (av & 0xFFFFFFFFULL) : av) >> (bv & shm); break;
+        case K_SRA: v = (uint64_t)((w32 ? (int64_t)(int32_t)av : (int64_t)av) >> (bv & shm)); break;
+        case K_MUL: v = av * bv; break;
+        case K_MULH: v = (uint64_t)__mul64hi((int64_t)av, (int64_t)bv); break;
+        case K_MULHU: v = __umul64hi(av, bv); break;
+        case K_MULHSU: v = __umul64hi(av, bv) - (((int64_t)av < 0) ? bv : 0); break;
+        case K_DIV: v = w32 ? divw(av, bv) : div64(av, bv); break;
+        case K_DIVU:
+            v = w32 ? ((uint32_t)bv == 0 ? ~0ULL : sx32((uint32_t)av / (uint32_t)bv)) : (bv == 0 ? ~0ULL : av / bv);
+            break;
+        case K_REM: v = w32 ? remw(av, bv) : rem64(av, bv); break;
+        case K_REMU:
+            v = w32 ? ((uint32_t)bv == 0 ? sx32(av) : sx32((uint32_t)av % (uint32_t)bv)) : (bv == 0 ? av : av % bv);
+            break;
+        case K_NOP: wr = false; break;
+        case K_JAL: v = ft; npc = spc + imm; took = true; break;
+        case K_JALR: v = ft; npc = uni64((a0 + imm) & ~1ULL); ind = true; break;
+        case K_BEQ: wr = false; took = a0 == b0; break;
+        case K_BNE: wr = false; took = a0 != b0; break;
+        case K_BLT: wr = false; took = (int64_t)a0 < (int64_t)b0; break;
+        case K_BGE: wr = false; took = (int64_t)a0 >= (int64_t)b0; break;
+        case K_BLTU: wr = false; took = a0 < b0; break;
+        case K_BGEU: wr = false; took = a0 >= b0; break;
+        default: {   // K_LOAD / K_STORE: the whole access inside one mapped page
+            const bool st = kind == K_STORE;
+            msz = 1u << ((aux >> 12) & 3);
+            const uint64_t ea = a0 + imm, vpn = ea >> 12;
+            const uint32_t off = (uint32_t)(ea & 4095);
+            uint64_t p = 0;
+            p = tv0 == vpn ? tp0 : p;
+            p = tv1 == vpn ? tp1 : p;
+            p = tv2 == vpn ? tp2 : p;
+            p = tv3 == vpn ? tp3 : p;
+            if (!p) {
+                p = uni64(lookup_full(CX, w, m, slot, vpn));
+                tv0 = m.tv0; tv1 = m.tv1; tv2 = m.tv2; tv3 = m.tv3; tp0 = m.tp0; tp1 = m.tp1; tp2 = m.tp2; tp3 = m.tp3;
+            }
+            if (!(p && (!st || (p & 1)) && off + msz <= 4096)) { msz = 0xFFFFFFFFu; break; }   // the general path's
+            uint8_t *pg = const_cast<uint8_t *>(page_of(p));
+            const bool al = (off & (msz - 1)) == 0;
+            if (st) {
+                wr = false;
+                if (!(ea >= tx.chi || ea + msz <= tx.clo)) {   // rewrites the lane's code
+                    // (the LDS map only: the kernel writes it to the slot's map when the lane suspends)
+                    mark_dirty_solo(CX, m, ea, ea + msz);
+                    dirty = true; dlo = m.dlo; dhi = m.dhi;
+                    const uint64_t e_ = ea + msz;
+                    for (uint64_t q = (ea > 3 ? ea - 3 : 0); q < e_; q++) {   // decode-cache entries over those bytes
+                        const uint32_t i = (uint32_t)(q >> 1) & (kSoloDC - 1);
+                        if (DCT[i] == (uint32_t)(q - tlo)) DCT[i] = 0xFFFFFFFFu;
+                    }
+                }
+                if (al) {
+                    switch (msz) {
+                    case 1: pg[off] = (uint8_t)b0; break;
+                    case 2: *(uint16_t *)(pg + off) = (uint16_t)b0; break;
+                    case 4: *(uint32_t *)(pg + off) = (uint32_t)b0; break;
+                    default: *(uint64_t *)(pg + off) = b0; break;
+                    }
+                } else {
+                    for (uint32_t i = 0; i < msz; i++) pg[off + i] = (uint8_t)(b0 >> (8 * i));
+                }
+            } else {
+                uint64_t t = 0;
+                if (al) {
+                    switch (msz) {
+                    case 1: t = pg[off]; break;
+                    case 2: t = *(const uint16_t *)(pg + off); break;
+                    case 4: t = *(const uint32_t *)(pg + off); break;
+                    default: t = *(const uint64_t *)(pg + off); break;
+                    }
+                } else {
+                    for (uint32_t i = 0; i < msz; i++) t |= (uint64_t)pg[off + i] << (8 * i);
+                }
+                v = (aux & U_SEXT) ? (uint64_t)sext64(t, 8 * msz) : t;
+            }
+            break;
+        }
+        }
+        if (msz == 0xFFFFFFFFu) break;   // nothing committed for this instruction
+        if (kind >= K_BEQ && kind <= K_BGEU && took) npc = spc + imm;
+        if (w32) v = sx32(v);
+        const uint32_t row = (wr && rd) ? rd : kSinkRow;
+        R[row] = v;
+        if (watch > 0 && row == (uint32_t)watch) watch = -1;   // overwritten before read
+        steps++; xticks += straddle; fbytes += len; dbytes += msz;
+        spc = npc;
+        E = ind ? pre_entry(tx, npc) : (took ? Etg : Eft);
+    }
+    io->spc = spc; io->watch = watch;
+    io->steps = steps; io->xticks = xticks; io->fbytes = fbytes; io->dbytes = dbytes;
+}
+
 // Waves per SIMD the register allocation must allow (the translated build
 // sets it per engine; see fi_jit.cpp).
 // solo kernel register budget: 4 waves per SIMD (<= 128 VGPRs).  A/B on
@@ -1797,6 +2111,7 @@ __device__ __forceinline__ void trial_body() {
         const int leader = __ffsll((unsigned long long)act) - 1;
         uint64_t lpc = rdl64<kNL>(L.pc, leader);
         n_iter++;
+        if constexpr (kNL == 1) n_min++;   // solo (no groups to reduce): counts the trips through this loop
         if (wballot<kNL>(ready && L.pc == lpc) != act) { lpc = wmin64<kNL>(ready ? L.pc : kNone); n_min++; }
         lpc = uni64(lpc);   // wave-uniform: keeps fetch/decode/dispatch on the scalar unit
         bool mine = ready && L.pc == lpc;
@@ -1984,53 +2299,15 @@ __device__ __forceinline__ void trial_body() {
                     const uint32_t bud = rem < wbud ? rem : wbud;
                     // rewritten code bytes as offsets from the text base (empty range if none)
                     const uint64_t tlo = CX->text_lo;
-                    uint32_t sdlo = m.code_dirty ? (uint32_t)((m.dlo > tlo ? m.dlo : tlo) - tlo) : 0xFFFFFFFFu;
-                    uint32_t sdhi = m.code_dirty ? (uint32_t)((m.dhi > tlo ? m.dhi : tlo) - tlo) : 0u;
-                    bool schg = false;                             // the blocks rewrote code
-                    uint32_t cslo = 0xFFFFFFFFu, cshi = 0u;        // ... these bytes (offsets)
-// a translated store rewrote code bytes [ea_, ea_ + sz_): later blocks see the
-// grown range; the decode cache forgets them when the blocks are left
-#define TXCODE(ea_, sz_)                                                                        \
-    do {                                                                                        \
-        const uint32_t o_ = SUNI32((uint32_t)((ea_) - tlo));                                    \
-        sdlo = o_ < sdlo ? o_ : sdlo;                                                           \
-        sdhi = o_ + (sz_) > sdhi ? o_ + (sz_) : sdhi;                                           \
-        cslo = o_ < cslo ? o_ : cslo;                                                           \
-        cshi = o_ + (sz_) > cshi ? o_ + (sz_) : cshi;                                           \
-        schg = true;                                                                            \
-        mark_dirty_solo(CX, m, (ea_), (ea_) + (sz_));                                           \
-    } while (0)
-// a block's bytes [tlo + lo_, tlo + hi_) hold code the lane rewrote (exact map)
-#define SDIRTY(lo_, hi_) (((sdlo < (hi_)) & (sdhi > (lo_))) && dirty_range(CX, m, tlo + (lo_), tlo + (hi_)))
-                    const uint32_t lwm = L.watch > 0 ? (1u << L.watch) : 0u;
-                    uint32_t st = 0, xt = 0, fb = 0, db = 0;   // instructions, straddles, fetch/data bytes
-                    uint64_t spc = lpc;
-                    uint32_t etgt = 0xFFFFFFFFu;   // block an entry is routed to through its cycle headers
-#define TXR(r) uint64_t X##r = RREG(r);
-                    TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
-                    TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
-                    TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
-#undef TXR
-#ifdef FI_TX_SOLO_ODD
-                    if constexpr (kOdd) {
-                        goto Q_dispatch;
-                        /*@TX_SOLO_ODD@*/
-                    } else
-#endif
-                    {
-                        goto S_dispatch;
-                        /*@TX_SOLO@*/
-                    }
-                S_out:
-#define TXW(r) RREG(r) = X##r;
-                    TXW(1) TXW(2) TXW(3) TXW(4) TXW(5) TXW(6) TXW(7) TXW(8) TXW(9) TXW(10) TXW(11) TXW(12) TXW(13)
-                    TXW(14) TXW(15) TXW(16) TXW(17) TXW(18) TXW(19) TXW(20) TXW(21) TXW(22) TXW(23) TXW(24) TXW(25)
-                    TXW(26) TXW(27) TXW(28) TXW(29) TXW(30) TXW(31)
-#undef TXW
-#undef TXCODE
-#undef SDIRTY
-                    if (schg) {
-                        m.code_dirty = true; m.dlo = tlo + sdlo; m.dhi = tlo + sdhi;
+                    __shared__ SoloTxIO sio[1];
+                    sio->spc = lpc; sio->bud = bud; sio->lwm = L.watch > 0 ? (1u << L.watch) : 0u;
+                    sio->sdlo = m.code_dirty ? (uint32_t)((m.dlo > tlo ? m.dlo : tlo) - tlo) : 0xFFFFFFFFu;
+                    sio->sdhi = m.code_dirty ? (uint32_t)((m.dhi > tlo ? m.dhi : tlo) - tlo) : 0u;
+                    solo_tx_run<kOdd>(CX, (lds_u64 *)R, (lds_mem *)&m, (lds_io *)sio);
+                    const uint32_t st = uni32(sio->st), xt = uni32(sio->xt), fb = uni32(sio->fb), db = uni32(sio->db);
+                    const uint64_t spc = uni64(sio->spc);
+                    if (sio->schg) {
+                        const uint32_t cslo = uni32(sio->cslo), cshi = uni32(sio->cshi);
 #pragma unroll 8
                         for (uint32_t k = 0; k < kDC; k++) {   // decode-cache entries whose bytes were rewritten
                             const uint32_t tg = DCT[k];
@@ -2155,6 +2432,25 @@ __device__ __forceinline__ void trial_body() {
             uint64_t budget64 = uni64(wmin64<kNL>(mine ? next_ev - L.ninst : kNone));
             if (CX->wave_budget && budget64 > CX->wave_budget - n_iter) budget64 = CX->wave_budget - n_iter;
             const uint32_t budget = budget64 > (1u << 30) ? (1u << 30) : (uint32_t)budget64;
+            if constexpr (kNL == 1) {
+                if (!CX->record) {   // solo: the out-of-line run (solo_pre_run), then the general path
+                    __shared__ SoloPreIO pio[1];
+                    pio->spc = lpc; pio->slot = slot; pio->tab = w.tab; pio->tab_n = w.tab_n;
+                    pio->budget = budget; pio->watch = L.watch;
+                    pio->tx_gate = tx_skip_until > n_iter ? tx_skip_until - n_iter : 0u;
+                    solo_pre_run<kOdd>(CX, (lds_u64 *)R, (lds_mem *)&m, (lds_u32 *)DCT, (lds_pre4 *)DCE,
+                                       (lds_pio *)pio);
+                    const uint32_t steps = uni32(pio->steps);
+                    if (steps) {
+                        L.ninst += steps; L.ncyc += steps + uni32(pio->xticks);
+                        L.fetch_b += uni32(pio->fbytes); L.data_b += uni32(pio->dbytes);
+                        L.pc = uni64(pio->spc); L.watch = (int)uni32((uint32_t)pio->watch);
+                        n_iter += steps;
+                        n_exec += steps;
+                        continue;
+                    }
+                }
+            }
             uint64_t spc = lpc;
             uint32_t steps = 0, xticks = 0, fbytes = 0, dbytes = 0;
             bool div = false;
@@ -2927,7 +3223,7 @@ __device__ __forceinline__ void trial_body() {
         wd[0] = __builtin_amdgcn_s_memtime() - t_start;
         wd[1] = n_iter;
         wd[2] = n_tx;
-        wd[3] = n_slow;
+        wd[3] = n_slow | ((uint64_t)n_min << 32);         // slow fetches | min-PC reductions (solo: loop trips)
         wd[4] = rt_start;                                // s_memrealtime (100 MHz) at the wave's start / end
         wd[5] = __builtin_amdgcn_s_memrealtime();
         wd[6] = live ? (uint64_t)sidx : ~0ULL;           // lane 0's trial (index into the sites)

@@ -47,14 +47,16 @@ print(json.dumps({"workload": name, "flags": flags, "structures": hex(structures
                                             for p in (0.5, 0.9, 0.99, 0.999, 1.0)},
                   **q}), flush=True)
 # the slowest waves: lane 0's trial, its instructions in the dispatch, loop
-# iterations, translated instructions, slow fetches
+# iterations, translated instructions, slow fetches, loop trips (solo) or
+# min-PC reductions (64-lane)
 dur_all = np.where(live, wv[:, 5] - wv[:, 4], 0)
 for b in np.argsort(-dur_all)[:8]:
     tr = int(wv[b, 6])
     s = sites[tr] if tr < n else None
     print(json.dumps({"wave": int(b), "us": round(dur_all[b] / 100.0, 1), "trial": tr, "insts": int(wv[b, 7]),
                       "ns_per_inst": round(dur_all[b] * 10.0 / max(1, int(wv[b, 7])), 1), "iters": int(wv[b, 1]),
-                      "tx": int(wv[b, 2]), "slow": int(wv[b, 3]), "tx_entries": int(wv[b, 8]),
+                      "tx": int(wv[b, 2]), "slow": int(wv[b, 3]) & 0xFFFFFFFF, "trips": int(wv[b, 3]) >> 32,
+                      "tx_entries": int(wv[b, 8]),
                       "page_lookups": int(wv[b, 9]),
                       "target": int(s["target"]) if s is not None else None,
                       "mask": hex(int(s["mask"])) if s is not None else None,
