@@ -53,6 +53,16 @@ struct Gen {
     uint64_t pc_of(uint32_t h) const { return text_lo + 2ULL * h; }
 };
 
+std::string sfmt(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+std::string sfmt(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    return std::string(buf);
+}
+
 enum Cls { C_STOP, C_ALU, C_NOP, C_LOAD, C_STORE, C_BR, C_JAL, C_JALR };
 
 // Classify an instruction and, for ALU ops, produce its value expression in
@@ -345,12 +355,16 @@ struct Block {
 // statically reachable from the executed code.  trace = halfword index per
 // golden event (bit 31: ecall).
 //
-// Three bodies are generated (joined by the marker FI_TX_SPLIT): the 64-lane
+// Four bodies are generated (joined by the marker FI_TX_SPLIT): the 64-lane
 // one (blocks B_*, guest registers X1..X31 in VGPRs, register writes as
 // selects on the running group, divergence parked and merged by the min-PC
 // rule), the solo one for the one-trial-per-wave kernel (blocks S_*, every
-// value uniform, no groups) and the solo-odd one (the solo blocks again as Q_*
-// plus the odd-pc streams as QO_*; empty when there are none).
+// value uniform, no groups), the solo-odd one (the solo blocks again as Q_*
+// plus the odd-pc streams as QO_*; empty when there are none) and the clean
+// solo one: the solo blocks for a trial that rewrote no code and watches no
+// register -- no rewritten-byte or watch checks, and a store into the code
+// range leaves before it (the interpreter marks the bytes; the trial then
+// takes the full solo body).
 std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
                              const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
                              uint32_t &n_insts, bool odd_streams) {
@@ -574,6 +588,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     Gen g{pre, text_lo, leaders, executed, {}};
     Gen so{pre, text_lo, leaders, executed, {}};
     Gen sq{pre, text_lo, leaders, executed, {}};
+    Gen sc{pre, text_lo, leaders, executed, {}};   // the clean solo body (mode 0 only)
     n_insts = 0;
     auto hex = [](uint64_t v) {
         char b[32];
@@ -643,6 +658,9 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     std::string g_mode;
     if (oddon) g_mode.swap(g.out);
     sdispatch(so_);
+    if (!oddon) sdispatch(sc);
+    // text that the full and the clean solo bodies share (mode 0)
+    auto sboth = [&](const std::string &t) { so_.out += t; if (!oddon) sc.out += t; };
     for (const Block &b : blocks) {
         if (!oddon && b.opc != 0) continue;
         const uint32_t h0 = b.h0;
@@ -674,7 +692,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             so_.put("%s%u: { // pc 0x%llx (odd)\n", SOB.c_str(), (uint32_t)((pc0 - text_lo) >> 1),
                     (unsigned long long)pc0);
         else
-            so_.put("%s%u: { // pc 0x%llx, %u insts\n", SB.c_str(), h0, (unsigned long long)pc0, n);
+            sboth(sfmt("%s%u: { // pc 0x%llx, %u insts\n", SB.c_str(), h0, (unsigned long long)pc0, n));
         if (!cur_odd && S.headers.count(h0)) {   // a cycle header routes an entry into its cycle one level on (etgt)
             std::string rw_, rs_;
             for (uint32_t x : leaders) {
@@ -692,7 +710,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             const char *fmt = "  if (etgt != 0xFFFFFFFFu) { if (etgt == %uu) etgt = 0xFFFFFFFFu; "
                               "else switch (etgt) { %sdefault: break; } }\n";
             g.put(fmt, h0, rw_.c_str());
-            so_.put(fmt, h0, rs_.c_str());
+            sboth(sfmt(fmt, h0, rs_.c_str()));
         }
         // ---- wave block prologue: merge a parked group waiting here, leave or
         // switch groups when lanes outside run first, then one combined check
@@ -708,6 +726,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         if (rw) so_.put(" | ((lwm & 0x%xu) != 0)", rw);
         so_.put(" | SDIRTY(%uu, %uu)) { spc = %s; goto S_out; }\n", (uint32_t)(blo - text_lo),
                 (uint32_t)(bhi - text_lo), P0.c_str());
+        if (!oddon) sc.put("  if (st + %uu > bud) { spc = %s; goto S_out; }\n", n, P0.c_str());
         uint32_t k_st = 0, k_xt = 0, k_fb = 0, k_db = 0;   // committed so far in this block
         auto commit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
             // per-lane counters of the running lanes (zero terms omitted), wave iterations
@@ -747,7 +766,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 const std::string v = subst(e, A, B, immb, pcb);
                 if (p.rd) {
                     g.put("  TXSET(%u, %s);\n", p.rd, v.c_str());
-                    so_.put("  SX(%u, %s);\n", p.rd, v.c_str());
+                    sboth(sfmt("  SX(%u, %s);\n", p.rd, v.c_str()));
                 }
                 break;
             }
@@ -756,20 +775,20 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             case C_LOAD:
                 g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, false, p_, tx);\n", A.c_str(), immb, sz);
                 g.put("    if (TXB(mine && !ok_)) %s\n", leave_here.c_str());
-                so_.put("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, false, p_, tx))) %s\n", A.c_str(), immb, sz,
-                       sleave_here.c_str());
+                sboth(sfmt("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, false, p_, tx))) %s\n", A.c_str(), immb,
+                         sz, sleave_here.c_str()));
                 if (p.rd) {
                     g.put("    p_ = ok_ ? p_ : const_cast<uint8_t *>(zp);\n");
                     if (sx) {
                         g.put("    TXSET(%u, (int64_t)(int%d_t)*(const g_%s *)p_); }\n", p.rd, sx, gtype(sz));
-                        so_.put("    X%u = (uint64_t)(int64_t)(int%d_t)*(const g_%s *)p_; }\n", p.rd, sx, gtype(sz));
+                        sboth(sfmt("    X%u = (uint64_t)(int64_t)(int%d_t)*(const g_%s *)p_; }\n", p.rd, sx, gtype(sz)));
                     } else {
                         g.put("    TXSET(%u, *(const g_%s *)p_); }\n", p.rd, gtype(sz));
-                        so_.put("    X%u = *(const g_%s *)p_; }\n", p.rd, gtype(sz));
+                        sboth(sfmt("    X%u = *(const g_%s *)p_; }\n", p.rd, gtype(sz)));
                     }
                 } else {
                     g.put("  }\n");
-                    so_.put("  }\n");
+                    sboth("  }\n");
                 }
                 break;
             case C_STORE:
@@ -784,6 +803,11 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 so_.put("    if (SCOND(cs_ & 2u)) { TXCODE(ea_, %uu); if (SCOND(ea_ < %s && ea_ + %uu > %s)) { %sspc = %s; "
                        "goto S_out; } } }\n", sz, hex(bhi).c_str(), sz, ftb.c_str(),
                        scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db + sz).c_str(), ftb.c_str());
+                // clean: a store into the code range (or any the probe refuses) leaves before itself
+                if (!oddon)
+                    sc.put("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, true, p_, tx))) %s\n"
+                           "    *(g_%s *)p_ = (%s)%s; }\n", A.c_str(), immb, sz, sleave_here.c_str(), gtype(sz),
+                           ltype(sz), B.c_str());
                 break;
             case C_BR: {
                 const std::string c = subst(cond, A, B, immb, pcb);
@@ -806,18 +830,18 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                           ftb.c_str(), ftb.c_str());
                     g.put("    %s }\n", wgo(h0, tgt).c_str());
                 }
-                so_.put("  %s\n  if (SCOND(%s)) %s\n  %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), c.c_str(),
-                       sgo(h0, tgt).c_str(), sgo(h0, ft).c_str());
+                sboth(sfmt("  %s\n  if (SCOND(%s)) %s\n  %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(),
+                         c.c_str(), sgo(h0, tgt).c_str(), sgo(h0, ft).c_str()));
                 break;
             }
             case C_JAL: {
                 const uint64_t tgt = pc + (int64_t)p.imm;
                 if (p.rd) {
                     g.put("  TXSET(%u, %s);\n", p.rd, ftb.c_str());
-                    so_.put("  SX(%u, %s);\n", p.rd, ftb.c_str());
+                    sboth(sfmt("  SX(%u, %s);\n", p.rd, ftb.c_str()));
                 }
                 g.put("  %s %s\n", commit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), wgo(h0, tgt).c_str());
-                so_.put("  %s %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), sgo(h0, tgt).c_str());
+                sboth(sfmt("  %s %s\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), sgo(h0, tgt).c_str()));
                 break;
             }
             case C_JALR: {
@@ -829,9 +853,10 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 g.put("    const uint64_t t0_ = rdl64<kNL>(t_, __ffsll((unsigned long long)gmr) - 1);\n");
                 g.put("    if (TXB(mine && t_ != t0_)) { dpc = t_; jdiv = mine; goto tx_out; }\n");
                 g.put("    spc = uni64(t0_); goto tx_dispatch; }\n");
-                so_.put("  { const uint64_t t_ = (%s + (uint64_t)(int64_t)%lldLL) & ~1ULL;\n", A.c_str(), (long long)im);
-                if (rd) so_.put("    SX(%u, %s);\n", rd, ftb.c_str());
-                so_.put("    %s spc = SUNI(t_); goto %s; }\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(), SD.c_str());
+                sboth(sfmt("  { const uint64_t t_ = (%s + (uint64_t)(int64_t)%lldLL) & ~1ULL;\n", A.c_str(), (long long)im));
+                if (rd) sboth(sfmt("    SX(%u, %s);\n", rd, ftb.c_str()));
+                sboth(sfmt("    %s spc = SUNI(t_); goto %s; }\n", scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db).c_str(),
+                         SD.c_str()));
                 break;
             }
             default:
@@ -843,10 +868,10 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             const uint64_t nxt = cur_odd ? (n ? b.opcs[n - 1] + pre[insts[n - 1]].len : pc0)
                                          : n ? g.pc_of(insts[n - 1]) + pre[insts[n - 1]].len : pc0;
             g.put("  %s %s\n", commit(k_st, k_xt, k_fb, k_db).c_str(), wgo(h0, nxt).c_str());
-            so_.put("  %s %s\n", scommit(k_st, k_xt, k_fb, k_db).c_str(), sgo(h0, nxt).c_str());
+            sboth(sfmt("  %s %s\n", scommit(k_st, k_xt, k_fb, k_db).c_str(), sgo(h0, nxt).c_str()));
         }
         g.put("}\n");
-        so_.put("}\n");
+        sboth("}\n");
         if (cur_odd) g.out.swap(g_keep);
     }
     if (oddon) g.out.swap(g_mode);
@@ -855,7 +880,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     leaders_out.assign(leaders.begin(), leaders.end());
     // odd-pc entries: bit 31 + the pre-decoded index of their key (kPreOddLeader)
     for (uint64_t pc : olead) leaders_out.push_back(0x80000000u | okey(pc));
-    return g.out + FI_TX_SPLIT + so.out + FI_TX_SPLIT + sq.out;
+    return g.out + FI_TX_SPLIT + so.out + FI_TX_SPLIT + sq.out + FI_TX_SPLIT + sc.out;
 }
 
 }  // namespace fi

@@ -1511,6 +1511,43 @@ S_out:
 }
 #endif
 
+#ifdef FI_TX
+// The clean solo body (fi_translate.cpp): for a trial that rewrote no code and
+// watches no register, blocks without those checks (a store into the code
+// range leaves before itself).  Same calling convention as solo_tx_run.
+__device__ __noinline__ void solo_tx_clean_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds_io *io) {
+    CX = (KCtx *)(uintptr_t)uni64((uint64_t)(uintptr_t)CX);
+    R = (lds_u64 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)R);
+    mp = (lds_mem *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)mp);
+    io = (lds_io *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)io);
+    LaneMem m;   // the TLB only (tx_probe)
+    m.tv0 = mp->tv0; m.tv1 = mp->tv1; m.tv2 = mp->tv2; m.tv3 = mp->tv3;
+    m.tp0 = mp->tp0; m.tp1 = mp->tp1; m.tp2 = mp->tp2; m.tp3 = mp->tp3;
+    TextRef tx;
+    tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
+    tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
+    uint64_t spc = io->spc;
+    const uint32_t bud = io->bud;
+    uint32_t etgt = 0xFFFFFFFFu;
+    uint32_t st = 0, xt = 0, fb = 0, db = 0;
+#define TXR(r) uint64_t X##r = R[r];
+    TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
+    TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
+    TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
+#undef TXR
+    goto S_dispatch;
+    /*@TX_SOLO_CLEAN@*/
+S_out:
+#define TXW(r) R[r] = X##r;
+    TXW(1) TXW(2) TXW(3) TXW(4) TXW(5) TXW(6) TXW(7) TXW(8) TXW(9) TXW(10) TXW(11) TXW(12) TXW(13)
+    TXW(14) TXW(15) TXW(16) TXW(17) TXW(18) TXW(19) TXW(20) TXW(21) TXW(22) TXW(23) TXW(24) TXW(25)
+    TXW(26) TXW(27) TXW(28) TXW(29) TXW(30) TXW(31)
+#undef TXW
+    io->spc = spc; io->st = st; io->xt = xt; io->fb = fb; io->db = db;
+    io->cslo = 0xFFFFFFFFu; io->cshi = 0u; io->schg = 0u;
+}
+#endif
+
 // ---- solo pre-decoded run, out of line: the fast path of trial_body<1>
 // (one trial, every value uniform) with its own register allocation.  Same
 // rules as the 64-lane fast path below: pre-decoded micro-ops from pc until
@@ -2303,7 +2340,10 @@ __device__ __forceinline__ void trial_body() {
                     sio->spc = lpc; sio->bud = bud; sio->lwm = L.watch > 0 ? (1u << L.watch) : 0u;
                     sio->sdlo = m.code_dirty ? (uint32_t)((m.dlo > tlo ? m.dlo : tlo) - tlo) : 0xFFFFFFFFu;
                     sio->sdhi = m.code_dirty ? (uint32_t)((m.dhi > tlo ? m.dhi : tlo) - tlo) : 0u;
-                    solo_tx_run<kOdd>(CX, (lds_u64 *)R, (lds_mem *)&m, (lds_io *)sio);
+                    if (!kOdd && !m.code_dirty && L.watch <= 0)
+                        solo_tx_clean_run(CX, (lds_u64 *)R, (lds_mem *)&m, (lds_io *)sio);
+                    else
+                        solo_tx_run<kOdd>(CX, (lds_u64 *)R, (lds_mem *)&m, (lds_io *)sio);
                     const uint32_t st = uni32(sio->st), xt = uni32(sio->xt), fb = uni32(sio->fb), db = uni32(sio->db);
                     const uint64_t spc = uni64(sio->spc);
                     if (sio->schg) {
