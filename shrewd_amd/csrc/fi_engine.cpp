@@ -701,12 +701,13 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     return FI_OK;
 }
 
-// The rewritten-code map's granule: 16 bytes, coarser for large code so that
+// The rewritten-code map's granule: one byte, coarser for large code so that
 // a slot's map stays within kDmapWords x 32 bits (the solo kernel's LDS
-// copy, fi_trial.hip kDmapWords).
+// copy, fi_trial.hip kDmapWords).  (Byte granules: a store next to a loop's
+// instructions leaves the loop's translated blocks usable.)
 static void dmap_params(const fi_engine *e, uint32_t &shift, uint32_t &words) {
     const uint64_t cb = e->code_hi > e->code_lo ? e->code_hi - e->code_lo : 1;
-    shift = 4;
+    shift = 0;
     while ((cb >> shift) >= kDmapWords * 32) shift++;
     words = (uint32_t)((((cb + (1ULL << shift) - 1) >> shift) + 31) / 32);
 }

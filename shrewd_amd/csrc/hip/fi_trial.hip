@@ -152,14 +152,23 @@ struct LaneMem {
 // the bounding range only (conservative).
 // (out of line: called only for a lane whose bounding range meets [lo, hi),
 // and the translated bodies check at every block)
+// (word-wise: granules g0..g1, the end words masked)
+template <typename P>
+__device__ __forceinline__ bool dmap_bits(P dl, uint32_t g0, uint32_t g1) {
+    const uint32_t w0 = g0 >> 5, w1 = g1 >> 5;
+    for (uint32_t wi = w0; wi <= w1; wi++) {
+        uint32_t b = dl[wi];
+        if (wi == w0) b &= ~0u << (g0 & 31);
+        if (wi == w1) b &= ~0u >> (31 - (g1 & 31));
+        if (b) return true;
+    }
+    return false;
+}
 __device__ __noinline__ bool dmap_test(KCtx *c, const uint32_t *dl, uint64_t lo, uint64_t hi) {
     const uint64_t a = lo > c->code_lo ? lo : c->code_lo, b = hi < c->code_hi ? hi : c->code_hi;
     if (a >= b) return false;
     const uint32_t sh = c->dmap_shift;
-    const uint32_t g0 = (uint32_t)((a - c->code_lo) >> sh), g1 = (uint32_t)((b - 1 - c->code_lo) >> sh);
-    for (uint32_t g = g0; g <= g1; g++)
-        if ((dl[g >> 5] >> (g & 31)) & 1) return true;
-    return false;
+    return dmap_bits(dl, (uint32_t)((a - c->code_lo) >> sh), (uint32_t)((b - 1 - c->code_lo) >> sh));
 }
 // The same test inline, on the solo kernel's LDS copy of the map (at most a
 // few granules: an instruction's 6 bytes, or one translated block).
@@ -167,10 +176,7 @@ __device__ __forceinline__ bool dmap_any(const __attribute__((address_space(3)))
                                          uint64_t chi, uint32_t sh, uint64_t lo, uint64_t hi) {
     const uint64_t a = lo > clo ? lo : clo, b = hi < chi ? hi : chi;
     if (a >= b) return false;
-    const uint32_t g0 = (uint32_t)((a - clo) >> sh), g1 = (uint32_t)((b - 1 - clo) >> sh);
-    uint32_t r = 0;
-    for (uint32_t g = g0; g <= g1; g++) r |= dl[g >> 5] >> (g & 31);
-    return (r & 1) != 0;
+    return dmap_bits(dl, (uint32_t)((a - clo) >> sh), (uint32_t)((b - 1 - clo) >> sh));
 }
 __device__ __forceinline__ bool dirty_range(KCtx *c, const LaneMem &m, uint64_t lo, uint64_t hi) {
     if (!m.code_dirty || lo >= m.dhi || hi <= m.dlo) return false;
@@ -220,8 +226,7 @@ __device__ __forceinline__ void mark_dirty_solo(KCtx *c, LaneMem &m, uint64_t lo
     const uint64_t a = lo > c->code_lo ? lo : c->code_lo, b = hi < c->code_hi ? hi : c->code_hi;
     if (a >= b) return;
     const uint32_t q0 = (uint32_t)((a - c->code_lo) >> c->dmap_shift), q1 = (uint32_t)((b - 1 - c->code_lo) >> c->dmap_shift);
-    m.dl[q0 >> 5] |= 1u << (q0 & 31);
-    m.dl[q1 >> 5] |= 1u << (q1 & 31);
+    for (uint32_t q = q0; q <= q1; q++) m.dl[q >> 5] |= 1u << (q & 31);   // (at most 8 granules)
 }
 
 // The lane's start-snapshot page table (uniform in a fresh launch; per lane
@@ -1568,9 +1573,20 @@ struct SoloPreIO {
     uint32_t tx_gate;      // in: leaders stop the run once steps >= tx_gate (translated build)
     int32_t watch;         // in/out: watched flipped register (-1 none)
     uint32_t steps, xticks, fbytes, dbytes;   // out
+#ifdef FI_PROF
+    uint64_t prof[4];      // out: s_memtime cycles per phase (diagnostic build)
+#endif
 };
 typedef __attribute__((address_space(3))) SoloPreIO lds_pio;
 constexpr uint32_t kSoloDC = 64;   // decode-cache entries (power of two)
+
+// 64-bit unsigned / signed compares of uniform values on the scalar unit
+// (SALU compares are 32-bit; a 64-bit one otherwise goes through VALU + VCC)
+__device__ __forceinline__ bool slt64(uint64_t a, uint64_t b) {
+    const int32_t ah = (int32_t)(a >> 32), bh = (int32_t)(b >> 32);
+    return ah < bh || (ah == bh && (uint32_t)a < (uint32_t)b);
+}
+__device__ __forceinline__ uint64_t r64(const lds_u64 *R, uint32_t r) { return uni64(R[r]); }
 
 template <bool kOdd>
 __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds_u32 *DCT, lds_pre4 *DCE,
@@ -1581,185 +1597,256 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
     DCT = (lds_u32 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)DCT);
     DCE = (lds_pre4 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)DCE);
     io = (lds_pio *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)io);
-    LaneMem &m = *(LaneMem *)mp;   // lookup_full / fetch_lane / mark_dirty take it by reference
+    LaneMem &m = *(LaneMem *)mp;   // lookup_full / fetch_lane / mark_dirty_solo take it by reference
     const uint64_t slot = uni64(io->slot);
     WaveMem w;
     w.tab = (const PageEnt *)uni64((uint64_t)io->tab);
     w.tab_n = uni32(io->tab_n);
-    const uint32_t budget = io->budget;
+    const uint32_t budget = uni32(io->budget);
 #ifdef FI_TX
-    const uint32_t tx_gate = io->tx_gate;
+    const uint32_t tx_gate = uni32(io->tx_gate), tx_gate1 = tx_gate > 1 ? tx_gate : 1u;
 #endif
-    int32_t watch = io->watch;
-    TextRef tx;
-    tx.pre = CX->pre; tx.lo = (uint32_t)CX->text_lo; tx.hi = (uint32_t)(CX->text_lo >> 32);
-    tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
-    const uint64_t tlo = CX->text_lo;
+    int32_t watch = (int32_t)uni32((uint32_t)io->watch);
+    // pcs as 32-bit offsets from the text base while the run stays in the text
+    // (the host keeps the text inside one 4 GiB window)
+    const uint64_t tlo = CX->text_lo, clo = CX->code_lo, chi = CX->code_hi;
+    const uint32_t tby = CX->text_bytes, tlo32 = (uint32_t)tlo;
+    const const_u32 *const pre = (const const_u32 *)(uintptr_t)CX->pre;
     // the TLB in registers (refreshed after lookup_full inserts)
-    uint64_t tv0 = m.tv0, tv1 = m.tv1, tv2 = m.tv2, tv3 = m.tv3, tp0 = m.tp0, tp1 = m.tp1, tp2 = m.tp2, tp3 = m.tp3;
-    bool dirty = m.code_dirty;
-    uint64_t dlo = m.dlo, dhi = m.dhi;
-    // the rewritten-code map (LDS; null: the bounding range decides)
-    const __attribute__((address_space(3))) uint32_t *const dl = (const __attribute__((address_space(3))) uint32_t *)m.dl;
+    uint64_t tv0 = uni64(m.tv0), tv1 = uni64(m.tv1), tv2 = uni64(m.tv2), tv3 = uni64(m.tv3);
+    uint64_t tp0 = uni64(m.tp0), tp1 = uni64(m.tp1), tp2 = uni64(m.tp2), tp3 = uni64(m.tp3);
+    // rewritten code: the bounding range as text offsets [ddlo, ddhi) (empty
+    // when clean), the LDS map for the exact test
     const bool have_dl = m.dl != nullptr;
+    const __attribute__((address_space(3))) uint32_t *const dl = (const __attribute__((address_space(3))) uint32_t *)m.dl;
     const uint32_t dsh = CX->dmap_shift;
-    uint64_t spc = io->spc;
-    uint32_t steps = 0, xticks = 0, fbytes = 0, dbytes = 0;
-    PreRef E = pre_entry(tx, spc);
-    while (steps < budget) {
-        spc = uni64(spc);
-        // the lane rewrote bytes of this instruction: its own bytes, decoded
-        // (through the decode cache); conservatively [pc & ~3, pc + 6)
-        // (a decode-cache hit is the decode of the lane's current bytes: stores
-        // drop the entries they overlap; only a miss asks the map)
-        const uint32_t ci = (uint32_t)(spc >> 1) & (kSoloDC - 1);
-        if (dirty && (spc & ~3ULL) < dhi && spc + 6 > dlo) {
-            const bool in_code = spc >= tx.clo && spc < tx.chi;
-            if (in_code && DCT[ci] == (uint32_t)(spc - tlo)) {
-                E.e.x = DCE[ci].x; E.e.y = DCE[ci].y; E.e.z = DCE[ci].z; E.e.w = DCE[ci].w; E.in = true;
-            } else if (!have_dl || dmap_any(dl, tx.clo, tx.chi, dsh, spc & ~3ULL, spc + 6)) {
-                uint32_t raw = 0, t = 1;
-                uint64_t fva = 0;
-                if (fetch_lane(CX, w, m, slot, spc, raw, t, fva) != 0) break;
-                tv0 = m.tv0; tv1 = m.tv1; tv2 = m.tv2; tv3 = m.tv3; tp0 = m.tp0; tp1 = m.tp1; tp2 = m.tp2; tp3 = m.tp3;
-                Dec dd = rv_decode(uni32(raw));
-                const uint32_t u = uop_of(dd);
-                E.in = true;
-                E.e.x = dd.raw;
-                E.e.y = (uint32_t)dd.op | ((uint32_t)dd.rd << 8) | ((uint32_t)dd.rs1 << 16) | ((uint32_t)dd.rs2 << 24);
-                E.e.z = (uint32_t)dd.imm;
-                E.e.w = (uint32_t)dd.len | ((uint32_t)(kPreValid | (uni32(t) == 2 ? kPreStraddle : 0) | dd.flags) << 8) |
-                        (u << 16);
-                if (in_code) {
-                    DCT[ci] = (uint32_t)(spc - tlo);
-                    DCE[ci].x = E.e.x; DCE[ci].y = E.e.y; DCE[ci].z = E.e.z; DCE[ci].w = E.e.w;
-                }
-            }
-        }
-        const uint32_t q1 = uni32(E.e.y), q2 = uni32(E.e.z), q3 = uni32(E.e.w);
-        const uint32_t aux = q3 >> 16, kind = aux & 63;
-        if (!E.in || !((q3 >> 8) & kPreValid) || kind == K_SLOW) break;
-#ifdef FI_TX
-        const bool lead = ((uint32_t)spc & 1) ? (kOdd && ((q3 >> 8) & kPreOddLeader)) : ((q3 >> 8) & kPreLeader);
-        if (steps && lead && steps >= tx_gate) break;
-#endif
-        const uint32_t rd = q1 >> 8 & 0xFF, rs1 = q1 >> 16 & 0xFF, rs2 = q1 >> 24;
-        if (watch > 0 && ((((q3 >> 8) & kPreRs1) && rs1 == (uint32_t)watch) ||
-                          (((q3 >> 8) & kPreRs2) && rs2 == (uint32_t)watch)))
-            break;
-        const int64_t imm = (int32_t)q2;
-        const uint32_t len = q3 & 0xFF, straddle = ((q3 >> 8) & kPreStraddle) ? 1 : 0;
-        const uint64_t a0 = R[rs1], b0 = R[rs2];
-        const uint64_t ft = spc + len;
-        const PreRef Eft = pre_entry(tx, ft);   // successors' entries load while this one executes
-        const PreRef Etg = pre_entry(tx, spc + imm);
-        const uint64_t av = (aux & U_APC) ? spc : a0;
-        const uint64_t bv = (aux & U_BIMM) ? (uint64_t)imm : b0;
-        const bool w32 = aux & U_W32;
-        const uint32_t shm = w32 ? 31 : 63;
-        uint64_t v = 0, npc = ft;
-        uint32_t msz = 0;
-        bool wr = true, took = false, ind = false;
-        switch (kind) {
-        case K_ADD: v = av + bv; break;
-        case K_SUB: v = av - bv; break;
-        case K_AND: v = av & bv; break;
-        case K_OR: v = av | bv; break;
-        case K_XOR: v = av ^ bv; break;
-        case K_SLT: v = (int64_t)av < (int64_t)bv ? 1 : 0; break;
-        case K_SLTU: v = av < bv ? 1 : 0; break;
-        case K_SLL: v = av << (bv & shm); break;
-        case K_SRL: v = (w32 ? (av & 0xFFFFFFFFULL) : av) >> (bv & shm); break;
-        case K_SRA: v = (uint64_t)((w32 ? (int64_t)(int32_t)av : (int64_t)av) >> (bv & shm)); break;
-        case K_MUL: v = av * bv; break;
-        case K_MULH: v = (uint64_t)__mul64hi((int64_t)av, (int64_t)bv); break;
-        case K_MULHU: v = __umul64hi(av, bv); break;
-        case K_MULHSU: v = __umul64hi(av, bv) - (((int64_t)av < 0) ? bv : 0); break;
-        case K_DIV: v = w32 ? divw(av, bv) : div64(av, bv); break;
-        case K_DIVU:
-            v = w32 ? ((uint32_t)bv == 0 ? ~0ULL : sx32((uint32_t)av / (uint32_t)bv)) : (bv == 0 ? ~0ULL : av / bv);
-            break;
-        case K_REM: v = w32 ? remw(av, bv) : rem64(av, bv); break;
-        case K_REMU:
-            v = w32 ? ((uint32_t)bv == 0 ? sx32(av) : sx32((uint32_t)av % (uint32_t)bv)) : (bv == 0 ? av : av % bv);
-            break;
-        case K_NOP: wr = false; break;
-        case K_JAL: v = ft; npc = spc + imm; took = true; break;
-        case K_JALR: v = ft; npc = uni64((a0 + imm) & ~1ULL); ind = true; break;
-        case K_BEQ: wr = false; took = a0 == b0; break;
-        case K_BNE: wr = false; took = a0 != b0; break;
-        case K_BLT: wr = false; took = (int64_t)a0 < (int64_t)b0; break;
-        case K_BGE: wr = false; took = (int64_t)a0 >= (int64_t)b0; break;
-        case K_BLTU: wr = false; took = a0 < b0; break;
-        case K_BGEU: wr = false; took = a0 >= b0; break;
-        default: {   // K_LOAD / K_STORE: the whole access inside one mapped page
-            const bool st = kind == K_STORE;
-            msz = 1u << ((aux >> 12) & 3);
-            const uint64_t ea = a0 + imm, vpn = ea >> 12;
-            const uint32_t off = (uint32_t)(ea & 4095);
-            uint64_t p = 0;
-            p = tv0 == vpn ? tp0 : p;
-            p = tv1 == vpn ? tp1 : p;
-            p = tv2 == vpn ? tp2 : p;
-            p = tv3 == vpn ? tp3 : p;
-            if (!p) {
-                p = uni64(lookup_full(CX, w, m, slot, vpn));
-                tv0 = m.tv0; tv1 = m.tv1; tv2 = m.tv2; tv3 = m.tv3; tp0 = m.tp0; tp1 = m.tp1; tp2 = m.tp2; tp3 = m.tp3;
-            }
-            if (!(p && (!st || (p & 1)) && off + msz <= 4096)) { msz = 0xFFFFFFFFu; break; }   // the general path's
-            uint8_t *pg = const_cast<uint8_t *>(page_of(p));
-            const bool al = (off & (msz - 1)) == 0;
-            if (st) {
-                wr = false;
-                if (!(ea >= tx.chi || ea + msz <= tx.clo)) {   // rewrites the lane's code
-                    // (the LDS map only: the kernel writes it to the slot's map when the lane suspends)
-                    mark_dirty_solo(CX, m, ea, ea + msz);
-                    dirty = true; dlo = m.dlo; dhi = m.dhi;
-                    const uint64_t e_ = ea + msz;
-                    for (uint64_t q = (ea > 3 ? ea - 3 : 0); q < e_; q++) {   // decode-cache entries over those bytes
-                        const uint32_t i = (uint32_t)(q >> 1) & (kSoloDC - 1);
-                        if (DCT[i] == (uint32_t)(q - tlo)) DCT[i] = 0xFFFFFFFFu;
-                    }
-                }
-                if (al) {
-                    switch (msz) {
-                    case 1: pg[off] = (uint8_t)b0; break;
-                    case 2: *(uint16_t *)(pg + off) = (uint16_t)b0; break;
-                    case 4: *(uint32_t *)(pg + off) = (uint32_t)b0; break;
-                    default: *(uint64_t *)(pg + off) = b0; break;
-                    }
-                } else {
-                    for (uint32_t i = 0; i < msz; i++) pg[off + i] = (uint8_t)(b0 >> (8 * i));
-                }
-            } else {
-                uint64_t t = 0;
-                if (al) {
-                    switch (msz) {
-                    case 1: t = pg[off]; break;
-                    case 2: t = *(const uint16_t *)(pg + off); break;
-                    case 4: t = *(const uint32_t *)(pg + off); break;
-                    default: t = *(const uint64_t *)(pg + off); break;
-                    }
-                } else {
-                    for (uint32_t i = 0; i < msz; i++) t |= (uint64_t)pg[off + i] << (8 * i);
-                }
-                v = (aux & U_SEXT) ? (uint64_t)sext64(t, 8 * msz) : t;
-            }
-            break;
-        }
-        }
-        if (msz == 0xFFFFFFFFu) break;   // nothing committed for this instruction
-        if (kind >= K_BEQ && kind <= K_BGEU && took) npc = spc + imm;
-        if (w32) v = sx32(v);
-        const uint32_t row = (wr && rd) ? rd : kSinkRow;
-        R[row] = v;
-        if (watch > 0 && row == (uint32_t)watch) watch = -1;   // overwritten before read
-        steps++; xticks += straddle; fbytes += len; dbytes += msz;
-        spc = npc;
-        E = ind ? pre_entry(tx, npc) : (took ? Etg : Eft);
+    uint32_t ddlo = 0xFFFFFFFFu, ddhi = 0u;
+    if (m.code_dirty) {
+        const uint64_t a = uni64(m.dlo), b = uni64(m.dhi);
+        ddlo = (uint32_t)((a > tlo ? a : tlo) - tlo);
+        ddhi = (uint32_t)((b > tlo ? b : tlo) - tlo);
     }
+    uint64_t spc = uni64(io->spc);
+    uint32_t steps = 0, xticks = 0, fbytes = 0, dbytes = 0;
+#ifdef FI_PROF   // phases: fetch (+ decode of rewritten code), operands, execute, commit
+    uint64_t pacc[4] = {0, 0, 0, 0}, plast = __builtin_amdgcn_s_memtime();
+#define PST(k)                                                  \
+    do {                                                        \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();       \
+        pacc[k] += _t - plast;                                  \
+        plast = _t;                                             \
+    } while (0)
+#else
+#define PST(k) do { } while (0)
+#endif
+    if ((uint32_t)((spc - tlo) >> 32) == 0 && (uint32_t)(spc - tlo) < tby) {
+        uint32_t po = (uint32_t)(spc - tlo);
+        // the entry of the instruction at po (odd pcs fetch like pc | 2 of their word)
+#define PRE_AT(o_, x_, y_, z_)                                                      \
+    do {                                                                            \
+        const uint32_t a_ = tlo32 + (o_);                                           \
+        const uint32_t k_ = (((a_ & ~1u) | ((a_ & 1u) << 1)) - tlo32) >> 1;         \
+        const const_u32 *q_ = pre + 4 * (k_ < (tby >> 1) ? k_ : 0u);                \
+        x_ = q_[1]; y_ = q_[2]; z_ = q_[3];                                         \
+        z_ = k_ < (tby >> 1) ? z_ : 0u;                                             \
+    } while (0)
+        uint32_t q1, q2, q3;
+        PRE_AT(po, q1, q2, q3);
+        while (steps < budget) {
+            PST(3);
+            // ---- rewritten bytes under this instruction: the decode cache
+            // (an entry is the decode of the lane's current bytes: stores drop
+            // the entries they overlap), else the lane's own bytes, decoded
+            if (po + 6 > ddlo && po < ddhi + 3u) {   // (a superset of [pc & ~3, pc + 6) meeting the range)
+                const uint32_t ci = (po >> 1) & (kSoloDC - 1);
+                const uint32_t tag = uni32(DCT[ci]);
+                const uint32_t e1 = uni32(DCE[ci].y), e2 = uni32(DCE[ci].z), e3 = uni32(DCE[ci].w);
+                const bool in_code = tlo + po >= clo && tlo + po < chi;
+                if (in_code && tag == po) {
+                    q1 = e1; q2 = e2; q3 = e3;
+                } else if (!have_dl || dmap_any(dl, clo, chi, dsh, (tlo + po) & ~3ULL, tlo + po + 6)) {
+                    uint32_t raw = 0, t = 1;
+                    uint64_t fva = 0;
+                    if (fetch_lane(CX, w, m, slot, tlo + po, raw, t, fva) != 0) break;
+                    tv0 = uni64(m.tv0); tv1 = uni64(m.tv1); tv2 = uni64(m.tv2); tv3 = uni64(m.tv3);
+                    tp0 = uni64(m.tp0); tp1 = uni64(m.tp1); tp2 = uni64(m.tp2); tp3 = uni64(m.tp3);
+                    Dec dd = rv_decode(uni32(raw));
+                    const uint32_t u = uop_of(dd);
+                    q1 = (uint32_t)dd.op | ((uint32_t)dd.rd << 8) | ((uint32_t)dd.rs1 << 16) | ((uint32_t)dd.rs2 << 24);
+                    q2 = (uint32_t)dd.imm;
+                    q3 = (uint32_t)dd.len | ((uint32_t)(kPreValid | (uni32(t) == 2 ? kPreStraddle : 0) | dd.flags) << 8) |
+                         (u << 16);
+                    q1 = uni32(q1); q2 = uni32(q2); q3 = uni32(q3);
+                    if (in_code) {
+                        DCT[ci] = po;
+                        DCE[ci].x = dd.raw; DCE[ci].y = q1; DCE[ci].z = q2; DCE[ci].w = q3;
+                    }
+                }
+            }
+            PST(0);
+            const uint32_t fl = (q3 >> 8) & 0xFF, kind = (q3 >> 16) & 63;
+            if (!(fl & kPreValid)) break;
+            if (kind == K_SLOW) break;
+#ifdef FI_TX
+            // a block leader (odd pcs: the solo-odd kernel's odd-pc leaders) past the first instruction
+            static_assert(kPreOddLeader == kPreLeader << 1, "leader flags");
+            const uint32_t lb = kOdd ? ((uint32_t)kPreLeader << (po & 1)) : ((po & 1) ? 0u : (uint32_t)kPreLeader);
+            if ((fl & lb) && steps >= tx_gate1) break;
+#endif
+            const uint32_t rd = (q1 >> 8) & 0xFF, rs1 = (q1 >> 16) & 0xFF, rs2 = q1 >> 24;
+            if (watch > 0 && (((fl & kPreRs1) && rs1 == (uint32_t)watch) || ((fl & kPreRs2) && rs2 == (uint32_t)watch)))
+                break;
+            const uint32_t len = q3 & 0xFF, aux = q3 >> 16;
+            const int64_t imm = (int32_t)q2;
+            const uint64_t pc = tlo + po;
+            const uint64_t a0 = r64(R, rs1), b0 = r64(R, rs2);
+            // the fall-through's entry loads while this instruction executes
+            uint32_t f1, f2, f3;
+            PRE_AT(po + len, f1, f2, f3);
+            const uint64_t av = (aux & U_APC) ? pc : a0;
+            const uint64_t bv = (aux & U_BIMM) ? (uint64_t)imm : b0;
+#ifdef FI_PROF
+            asm volatile("" :: "s"(av), "s"(bv));
+#endif
+            PST(1);
+            const bool w32 = aux & U_W32;
+            const uint32_t shm = w32 ? 31 : 63;
+            uint64_t v = 0, npc = pc + len;
+            uint32_t msz = 0;
+            bool wr = true, jump = false;   // jump: npc is not the fall-through
+            switch (kind) {
+            case K_ADD: v = av + bv; break;
+            case K_LOAD: case K_STORE: {   // the whole access inside one mapped page
+                const bool st = kind == K_STORE;
+                msz = 1u << ((aux >> 12) & 3);
+                const uint64_t ea = a0 + imm, vpn = ea >> 12;
+                const uint32_t off = (uint32_t)ea & 4095u;
+                uint64_t p = 0;
+                p = tv0 == vpn ? tp0 : p;
+                p = tv1 == vpn ? tp1 : p;
+                p = tv2 == vpn ? tp2 : p;
+                p = tv3 == vpn ? tp3 : p;
+                if (!p) {
+                    p = uni64(lookup_full(CX, w, m, slot, vpn));
+                    tv0 = uni64(m.tv0); tv1 = uni64(m.tv1); tv2 = uni64(m.tv2); tv3 = uni64(m.tv3);
+                    tp0 = uni64(m.tp0); tp1 = uni64(m.tp1); tp2 = uni64(m.tp2); tp3 = uni64(m.tp3);
+                }
+                if (!(p && (!st || (p & 1)) && off + msz <= 4096)) { msz = 0xFFFFFFFFu; break; }   // the general path's
+                __attribute__((address_space(1))) uint8_t *pg =
+                    (__attribute__((address_space(1))) uint8_t *)(uintptr_t)(p & ~1ULL);
+                const bool al = (off & (msz - 1)) == 0;
+                if (st) {
+                    wr = false;
+                    if (!(!ult64(ea, chi) || !ult64(clo, ea + msz))) {   // rewrites the lane's code
+                        // (the LDS map only: the kernel writes it to the slot's map when the lane suspends)
+                        mark_dirty_solo(CX, m, ea, ea + msz);
+                        const uint32_t o0 = (uint32_t)((ea > tlo ? ea : tlo) - tlo), o1 = (uint32_t)(ea + msz - tlo);
+                        ddlo = o0 < ddlo ? o0 : ddlo;
+                        ddhi = o1 > ddhi ? o1 : ddhi;
+                        for (uint32_t q = (o0 > 3 ? o0 - 3 : 0); q < o1; q++) {   // decode-cache entries over them
+                            const uint32_t i = (q >> 1) & (kSoloDC - 1);
+                            if (DCT[i] == q) DCT[i] = 0xFFFFFFFFu;
+                        }
+                    }
+                    if (al) {
+                        switch (msz) {
+                        case 1: pg[off] = (uint8_t)b0; break;
+                        case 2: *(__attribute__((address_space(1))) uint16_t *)(pg + off) = (uint16_t)b0; break;
+                        case 4: *(__attribute__((address_space(1))) uint32_t *)(pg + off) = (uint32_t)b0; break;
+                        default: *(__attribute__((address_space(1))) uint64_t *)(pg + off) = b0; break;
+                        }
+                    } else {
+                        for (uint32_t i = 0; i < msz; i++) pg[off + i] = (uint8_t)(b0 >> (8 * i));
+                    }
+                } else {
+                    uint64_t t = 0;
+                    if (al) {
+                        switch (msz) {
+                        case 1: t = pg[off]; break;
+                        case 2: t = *(const __attribute__((address_space(1))) uint16_t *)(pg + off); break;
+                        case 4: t = *(const __attribute__((address_space(1))) uint32_t *)(pg + off); break;
+                        default: t = *(const __attribute__((address_space(1))) uint64_t *)(pg + off); break;
+                        }
+                    } else {
+                        for (uint32_t i = 0; i < msz; i++) t |= (uint64_t)pg[off + i] << (8 * i);
+                    }
+                    t = uni64(t);
+                    v = (aux & U_SEXT) ? (uint64_t)sext64(t, 8 * msz) : t;
+                }
+                break;
+            }
+            case K_BEQ: case K_BNE: case K_BLT: case K_BGE: case K_BLTU: case K_BGEU: {
+                wr = false;
+                bool c;
+                switch (kind) {
+                case K_BEQ: c = a0 == b0; break;
+                case K_BNE: c = a0 != b0; break;
+                case K_BLT: c = slt64(a0, b0); break;
+                case K_BGE: c = !slt64(a0, b0); break;
+                case K_BLTU: c = ult64(a0, b0); break;
+                default: c = !ult64(a0, b0); break;
+                }
+                if (c) { npc = pc + imm; jump = true; }
+                break;
+            }
+            case K_SUB: v = av - bv; break;
+            case K_AND: v = av & bv; break;
+            case K_OR: v = av | bv; break;
+            case K_XOR: v = av ^ bv; break;
+            case K_SLT: v = slt64(av, bv) ? 1 : 0; break;
+            case K_SLTU: v = ult64(av, bv) ? 1 : 0; break;
+            case K_SLL: v = av << (bv & shm); break;
+            case K_SRL: v = (w32 ? (av & 0xFFFFFFFFULL) : av) >> (bv & shm); break;
+            case K_SRA: v = (uint64_t)((w32 ? (int64_t)(int32_t)av : (int64_t)av) >> (bv & shm)); break;
+            case K_JAL: v = pc + len; npc = pc + imm; jump = true; break;
+            case K_JALR: v = pc + len; npc = (a0 + imm) & ~1ULL; jump = true; break;
+            case K_NOP: wr = false; break;
+            case K_MUL: v = av * bv; break;
+            case K_MULH: v = (uint64_t)__mul64hi((int64_t)av, (int64_t)bv); break;
+            case K_MULHU: v = __umul64hi(av, bv); break;
+            case K_MULHSU: v = __umul64hi(av, bv) - (((int64_t)av < 0) ? bv : 0); break;
+            case K_DIV: v = w32 ? divw(av, bv) : div64(av, bv); break;
+            case K_DIVU:
+                v = w32 ? ((uint32_t)bv == 0 ? ~0ULL : sx32((uint32_t)av / (uint32_t)bv)) : (bv == 0 ? ~0ULL : av / bv);
+                break;
+            case K_REM: v = w32 ? remw(av, bv) : rem64(av, bv); break;
+            case K_REMU:
+                v = w32 ? ((uint32_t)bv == 0 ? sx32(av) : sx32((uint32_t)av % (uint32_t)bv)) : (bv == 0 ? av : av % bv);
+                break;
+            default: msz = 0xFFFFFFFFu; break;
+            }
+            if (msz == 0xFFFFFFFFu) break;   // nothing committed for this instruction
+            v = uni64(v);
+#ifdef FI_PROF
+            asm volatile("" :: "s"(v));
+#endif
+            PST(2);
+            if (w32) v = sx32(v);
+            if (wr && rd) R[rd] = v;
+            if (watch > 0 && wr && rd == (uint32_t)watch) watch = -1;   // overwritten before read
+            steps++; xticks += (fl & kPreStraddle) ? 1u : 0u; fbytes += len; dbytes += msz;
+            if (!jump) {
+                po += len;
+                q1 = f1; q2 = f2; q3 = f3;
+            } else {
+                npc = uni64(npc);
+                const uint64_t d = npc - tlo;
+                if ((uint32_t)(d >> 32) != 0 || (uint32_t)d >= tby) { spc = npc; goto leave; }   // left the text
+                po = (uint32_t)d;
+                PRE_AT(po, q1, q2, q3);
+            }
+            if (po >= tby) { spc = tlo + po; goto leave; }
+        }
+        spc = tlo + po;
+#undef PRE_AT
+    }
+leave:
     io->spc = spc; io->watch = watch;
     io->steps = steps; io->xticks = xticks; io->fbytes = fbytes; io->dbytes = dbytes;
+#ifdef FI_PROF
+    for (int k = 0; k < 4; k++) io->prof[k] = pacc[k];
+#endif
+#undef PST
 }
 
 // Waves per SIMD the register allocation must allow (the translated build
@@ -2481,6 +2568,9 @@ __device__ __forceinline__ void trial_body() {
                     solo_pre_run<kOdd>(CX, (lds_u64 *)R, (lds_mem *)&m, (lds_u32 *)DCT, (lds_pre4 *)DCE,
                                        (lds_pio *)pio);
                     const uint32_t steps = uni32(pio->steps);
+#ifdef FI_PROF
+                    for (int k = 0; k < 4; k++) pacc[k] += pio->prof[k];
+#endif
                     if (steps) {
                         L.ninst += steps; L.ncyc += steps + uni32(pio->xticks);
                         L.fetch_b += uni32(pio->fbytes); L.data_b += uni32(pio->dbytes);
