@@ -1269,12 +1269,12 @@ fi_status fi_sample_sites(fi_engine *e, uint64_t first, uint64_t n, fi_site *out
 
 // The trial kernel: the load-time build with translated blocks when there is
 // one, else the static (interpreter-only) kernel.
-// solo: the one-trial-per-wave build, one single-lane workgroup per slot.
+// solo: the one-trial-per-wave build, one workgroup (kSoloLanes identical lanes) per slot.
 static hipError_t launch_trial_kernel(fi_engine *e, DevCtx &c, hipStream_t st, bool solo) {
     void *args[] = {&c};
     if (solo) {
         if (!e->tx_fn_solo) return launch_trials_solo(c, st);
-        return hipModuleLaunchKernel(e->tx_fn_solo, (unsigned)c.n, 1, 1, 1, 1, 1, 0, st, args, nullptr);
+        return hipModuleLaunchKernel(e->tx_fn_solo, (unsigned)c.n, 1, 1, kSoloLanes, 1, 1, 0, st, args, nullptr);
     }
     if (!e->tx_fn) return launch_trials(c, st);
     const uint32_t gl = (c.resume && c.resume_waves) ? 1u : c.lanes;   // grid for the fewest lanes per wave
@@ -1385,7 +1385,7 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
                 auto &tq = timer_slot(e, 2);
                 HIPCHK(hipEventRecord(tq.first, e->stream_odd));
                 void *args[] = {&co};
-                HIPCHK(hipModuleLaunchKernel(e->tx_fn_odd, grid, 1, 1, 1, 1, 1, 0, e->stream_odd, args, nullptr));
+                HIPCHK(hipModuleLaunchKernel(e->tx_fn_odd, grid, 1, 1, kSoloLanes, 1, 1, 0, e->stream_odd, args, nullptr));
                 HIPCHK(hipEventRecord(tq.second, e->stream_odd));
                 HIPCHK(hipEventRecord(e->ev_join, e->stream_odd));
             }

@@ -797,10 +797,13 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 g.put("    p_ = (mine && ok_) ? p_ : sink; *(g_%s *)p_ = (%s)%s; }\n", gtype(sz), ltype(sz), B.c_str());
                 // solo: a store into the code range is performed too; it marks the
                 // bytes rewritten and leaves after itself if they lie ahead in this block
+                // (a code-range store that leaves the bytes as they were rewrites nothing)
                 so_.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s; const uint32_t cs_ = tx_probe_st(m, ea_, %uu, "
                        "p_, tx); if (SCOND(!cs_)) %s\n", A.c_str(), immb, sz, sleave_here.c_str());
+                so_.put("    const bool chg_ = SCOND(cs_ & 2u) && SUNI((uint64_t)*(g_%s *)p_) != (uint64_t)(%s)%s;\n", gtype(sz),
+                        ltype(sz), B.c_str());
                 so_.put("    *(g_%s *)p_ = (%s)%s;\n", gtype(sz), ltype(sz), B.c_str());
-                so_.put("    if (SCOND(cs_ & 2u)) { TXCODE(ea_, %uu); if (SCOND(ea_ < %s && ea_ + %uu > %s)) { %sspc = %s; "
+                so_.put("    if (SCOND(chg_)) { TXCODE(ea_, %uu); if (SCOND(ea_ < %s && ea_ + %uu > %s)) { %sspc = %s; "
                        "goto S_out; } } }\n", sz, hex(bhi).c_str(), sz, ftb.c_str(),
                        scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db + sz).c_str(), ftb.c_str());
                 // clean: a store into the code range (or any the probe refuses) leaves before itself

@@ -8,6 +8,7 @@
 namespace fi {
 
 constexpr uint64_t kPage = 4096;
+constexpr uint32_t kSoloLanes = 1;   // threads of a solo-kernel workgroup (one trial; fi_trial.hip kSoloOnce)
 constexpr uint32_t kDmapWords = 128;  // rewritten-code map: at most 4096 granules per slot (DevCtx::dmap)
 constexpr uint64_t kFwDead = ~0ULL;  // DevCtx::eff: the flipped register is dead at injection
 // RiscvProcess64 constants, src/arch/riscv/process.cc:73-80

@@ -57,6 +57,13 @@ template <uint32_t kNL> __device__ __forceinline__ uint64_t wballot(bool x) {
 }
 
 constexpr uint64_t kNone = ~0ULL;
+// The solo kernels (kNL = 1: one trial per wave) run kSoloLanes identical
+// lanes (fi_types.h); side effects that must happen once (atomics) are taken
+// by thread 0 (kSoloOnce), page copies split over the lanes.  kSoloLanes is 1:
+// with 64 lanes the compiler can no longer treat the trial state as uniform
+// (the kernel's stack objects become per-lane memory) and the solo kernel
+// spilled 16x more (84 -> 1,343 scratch instructions).
+#define kSoloOnce (kNL > 1 || threadIdx.x == 0)
 constexpr uint32_t kSinkRow = 32;
 constexpr uint32_t kRows = 33;
 
@@ -1282,11 +1289,13 @@ __device__ __forceinline__ bool page_eq(const uint8_t *a, const uint8_t *b, uint
     }
     return wballot<kNL>(!eq) == 0;
 }
-// Copy one 4 KiB page, the wave cooperating.
+// Copy one 4 KiB page, the wave cooperating (the solo kernel's 64 lanes all
+// run the one trial: they split the copy by thread index).
 template <uint32_t kNL>
 __device__ __forceinline__ void page_copy(uint4 *dst, const uint4 *src, uint32_t lane) {
+    const uint32_t l0 = kNL == 1 ? (uint32_t)threadIdx.x : lane, step = kNL == 1 ? kSoloLanes : kNL;
 #pragma unroll 4
-    for (uint32_t k = lane; k < 256; k += kNL) dst[k] = src[k];
+    for (uint32_t k = l0; k < 256; k += step) dst[k] = src[k];
 }
 
 // Is lane l's memory equal to the golden memory of snapshot S?  (wave-uniform
@@ -1737,7 +1746,17 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
                 const bool al = (off & (msz - 1)) == 0;
                 if (st) {
                     wr = false;
-                    if (!(!ult64(ea, chi) || !ult64(clo, ea + msz))) {   // rewrites the lane's code
+                    // a store into the code range that changes its bytes rewrites
+                    // the lane's code (one that writes the bytes already there
+                    // leaves them as they were: nothing to mark)
+                    bool chg = false;
+                    if (!(!ult64(ea, chi) || !ult64(clo, ea + msz))) {
+                        uint64_t old = 0;
+                        for (uint32_t i = 0; i < msz; i++) old |= (uint64_t)pg[off + i] << (8 * i);
+                        const uint64_t mk = msz == 8 ? ~0ULL : ((1ULL << (8 * msz)) - 1);
+                        chg = ((uni64(old) ^ b0) & mk) != 0;
+                    }
+                    if (chg) {   // rewrites the lane's code
                         // (the LDS map only: the kernel writes it to the slot's map when the lane suspends)
                         mark_dirty_solo(CX, m, ea, ea + msz);
                         const uint32_t o0 = (uint32_t)((ea > tlo ? ea : tlo) - tlo), o1 = (uint32_t)(ea + msz - tlo);
@@ -1997,7 +2016,7 @@ __device__ __forceinline__ void trial_body() {
         L.injected = 1;
         finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
         L.res.ninst = CX->gninst;
-        atomicAdd(&CX->stats[27], 1ull);
+        if (kSoloOnce) atomicAdd(&CX->stats[27], 1ull);
     }
     bool suspended = false;
     const uint64_t start_inst = (live && !resume) ? L.ninst : 0;
@@ -2072,7 +2091,7 @@ __device__ __forceinline__ void trial_body() {
                 sv->pad = (uint32_t)L.fflags | ((uint32_t)L.frm << 5);
                 if (m.dl && m.code_dirty)   // the solo kernel's map lives in LDS
                     for (uint32_t i = 0; i < CX->dmap_words; i++) CX->dmap[slot * CX->dmap_words + i] = m.dl[i];
-                CX->surv[atomicAdd(CX->surv_n, 1u)] = (uint32_t)slot;
+                if (kSoloOnce) CX->surv[atomicAdd(CX->surv_n, 1u)] = (uint32_t)slot;
                 suspended = true;
                 L.done = true;
             }
@@ -2126,13 +2145,13 @@ __device__ __forceinline__ void trial_body() {
                     if (CX->mem_live) {   // ... so the trial is the golden run
                         finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
                         L.res.ninst = CX->gninst;
-                        atomicAdd(&CX->stats[26], 1ull);
+                        if (kSoloOnce) atomicAdd(&CX->stats[26], 1ull);
                     }
                 } else if (CX->mem_live && mem_dead(CX, s.addr, s.mask, L.ninst)) {
                     L.injected = 1;
                     finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
                     L.res.ninst = CX->gninst;
-                    atomicAdd(&CX->stats[26], 1ull);
+                    if (kSoloOnce) atomicAdd(&CX->stats[26], 1ull);
                 } else if (!(p & 1)) {
                     m.req_vpn = s.addr >> 12; m.req_src = page_of(p);   // copy-on-write first, flip next iteration
                 } else {
@@ -3345,7 +3364,7 @@ __device__ __forceinline__ void trial_body() {
         CX->stats[15] = tpos;
     }
 #ifdef FI_PROF
-    if (lane == 0)
+    if (lane == 0 && kSoloOnce)
         for (int k = 0; k < 8; k++) atomicAdd(&CX->stats[32 + k], (unsigned long long)pacc[k]);
 #endif
     if (lane == 0 && CX->wave_dbg) {
@@ -3369,7 +3388,7 @@ __device__ __forceinline__ void trial_body() {
     const uint64_t fb = wsum64<kNL>(L.fetch_b), db = wsum64<kNL>(L.data_b), pm = wsum64<kNL>(pages_made);
     const uint64_t si = wsum64<kNL>(start_inst);
     const uint64_t xi = wsum64<kNL>(live ? L.ninst - launch_inst : 0);
-    if (lane == 0) {
+    if (lane == 0 && kSoloOnce) {
         atomicAdd(&CX->stats[23], (unsigned long long)xi);
         atomicAdd(&CX->stats[0], (unsigned long long)fb);
         atomicAdd(&CX->stats[1], (unsigned long long)db);
@@ -3411,15 +3430,15 @@ __device__ __forceinline__ void trial_body() {
 // The instantiations (load-time build: with the translated blocks).
 #ifdef __HIPCC_RTC__
 extern "C" __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel_tx(DevCtx) { trial_body<64>(); }
-extern "C" __global__ void __launch_bounds__(1, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_tx_solo(DevCtx) { trial_body<1>(); }
+extern "C" __global__ void __launch_bounds__(kSoloLanes, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_tx_solo(DevCtx) { trial_body<1>(); }
 #ifdef FI_TX_SOLO_ODD
-extern "C" __global__ void __launch_bounds__(1, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_tx_solo_odd(DevCtx) {
+extern "C" __global__ void __launch_bounds__(kSoloLanes, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_tx_solo_odd(DevCtx) {
     trial_body<1, true>();
 }
 #endif
 #else
 __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel(DevCtx) { trial_body<64>(); }
-__global__ void __launch_bounds__(1, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_solo(DevCtx) { trial_body<1>(); }
+__global__ void __launch_bounds__(kSoloLanes, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_solo(DevCtx) { trial_body<1>(); }
 
 hipError_t launch_trials(const DevCtx &c, hipStream_t st) {
     const uint32_t gl = (c.resume && c.resume_waves) ? 1u : c.lanes;   // grid for the fewest lanes per wave
@@ -3428,7 +3447,7 @@ hipError_t launch_trials(const DevCtx &c, hipStream_t st) {
 }
 // one trial per single-lane workgroup (surplus workgroups of a resume grid exit at once)
 hipError_t launch_trials_solo(const DevCtx &c, hipStream_t st) {
-    hipLaunchKernelGGL(fi_trial_kernel_solo, dim3((unsigned)c.n), dim3(1), 0, st, c);
+    hipLaunchKernelGGL(fi_trial_kernel_solo, dim3((unsigned)c.n), dim3(kSoloLanes), 0, st, c);
     return hipGetLastError();
 }
 #endif
