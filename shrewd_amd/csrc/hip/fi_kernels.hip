@@ -226,14 +226,19 @@ __global__ void __launch_bounds__(256) fi_hist_kernel(const fi_site *sites, cons
 // adjacent and ordered by progress.  With n_odd (a solo-odd launch follows)
 // the key is shifted down one bit under a top bit set for odd pcs, so that
 // the odd-pc survivors sort last, and they are counted.
+// solo != 0: the next epoch runs one trial per wave, where the order only
+// decides when a trial starts: trials that rewrote their code (interpreted at
+// ~20x the cost of translated code) start first.
 __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
-                                    uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd) {
+                                    uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd,
+                                    uint32_t solo) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cap) return;
     if (i < *cnt) {
         const uint32_t sl = list[i];
         const uint64_t pc = save[sl].pc;
         uint64_t k = ((pc - text_lo) << 32) | (save[sl].ninst & 0xFFFFFFFFu);
+        if (solo) k = ((uint64_t)(((save[sl].flags >> 3) & 1) ^ 1) << 62) | (k >> 2);
         if (n_odd) {
             k = ((pc & 1) << 63) | (k >> 1);
             if (pc & 1) atomicAdd(n_odd, 1u);
@@ -358,9 +363,10 @@ hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome
     return hipGetLastError();
 }
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
-                            uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, hipStream_t st) {
+                            uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, bool solo,
+                            hipStream_t st) {
     hipLaunchKernelGGL(fi_surv_keys_kernel, dim3(nblk(cap, 256)), dim3(256), 0, st, save, list, cnt, cap, text_lo,
-                       keys, vals, n_odd);
+                       keys, vals, n_odd, solo ? 1u : 0u);
     return hipGetLastError();
 }
 hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,

@@ -64,6 +64,7 @@ constexpr uint64_t kNone = ~0ULL;
 // (the kernel's stack objects become per-lane memory) and the solo kernel
 // spilled 16x more (84 -> 1,343 scratch instructions).
 #define kSoloOnce (kNL > 1 || threadIdx.x == 0)
+constexpr uint64_t kSoloPrioInsts = 32768;   // a solo wave past this many instructions raises its priority
 constexpr uint32_t kSinkRow = 32;
 constexpr uint32_t kRows = 33;
 
@@ -2072,7 +2073,17 @@ __device__ __forceinline__ void trial_body() {
 #define n_txin WS[6]
 #define n_simt WS[7]
 
+    bool prio_up = false;
     for (;;) {
+        // ---- solo: a trial that has run long in this dispatch takes issue
+        // priority over the short ones sharing its SIMD (the dispatch ends
+        // with the longest trials; the short ones are not on the critical path)
+        if constexpr (kNL == 1) {
+            if (!prio_up && L.ninst - launch_inst >= kSoloPrioInsts) {
+                __builtin_amdgcn_s_setprio(3);
+                prio_up = true;
+            }
+        }
         // ---- epochs: after wave_budget iterations the wave suspends its live
         // lanes (a pending copy-on-write is dropped: its tick simply retries)
         if (CX->wave_budget && n_iter >= CX->wave_budget) {
