@@ -442,7 +442,9 @@ static fi_status upload_snaps(fi_engine *e) {
     free_snaps(e);
     HIPCHK(hipMalloc(&e->d_snaps, e->snaps.size() * sizeof(SnapState)));
     HIPCHK(hipMalloc(&e->d_tab, std::max<size_t>(1, e->tab.size()) * sizeof(PageEnt)));
-    HIPCHK(hipMalloc(&e->d_pool, std::max<size_t>(kPage, e->pool.size())));
+    // (+64: solo translated code reads shared frames with dword-granular scalar
+    // loads that may run up to 11 bytes past an access at a frame's end)
+    HIPCHK(hipMalloc(&e->d_pool, std::max<size_t>(kPage, e->pool.size()) + 64));
     HIPCHK(hipMemcpy(e->d_snaps, e->snaps.data(), e->snaps.size() * sizeof(SnapState), hipMemcpyHostToDevice));
     if (!e->tab.empty())
         HIPCHK(hipMemcpy(e->d_tab, e->tab.data(), e->tab.size() * sizeof(PageEnt), hipMemcpyHostToDevice));
@@ -579,10 +581,10 @@ static fi_status finish_load(fi_engine *e, const uint64_t regs[32], uint64_t pc)
         fi_status st = upload_snaps(e);
         if (st) return st;
     }
-    HIPCHK(hipMalloc(&e->d_zero, kPage));
+    HIPCHK(hipMalloc(&e->d_zero, kPage + 64));   // (+64: as the frame pool)
     HIPCHK(hipMalloc(&e->d_sink, kPage));
     HIPCHK(hipMalloc(&e->d_mem_pages, std::max<size_t>(1, wpages.size()) * 8));
-    HIPCHK(hipMemset(e->d_zero, 0, kPage));
+    HIPCHK(hipMemset(e->d_zero, 0, kPage + 64));
     if (!wpages.empty()) HIPCHK(hipMemcpy(e->d_mem_pages, wpages.data(), wpages.size() * 8, hipMemcpyHostToDevice));
     const uint64_t tbytes = e->text_hi - e->text_lo;
     std::vector<uint8_t> text(tbytes, 0);

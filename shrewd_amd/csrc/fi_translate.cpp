@@ -775,16 +775,19 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             case C_LOAD:
                 g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, false, p_, tx);\n", A.c_str(), immb, sz);
                 g.put("    if (TXB(mine && !ok_)) %s\n", leave_here.c_str());
-                sboth(sfmt("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, false, p_, tx))) %s\n", A.c_str(), immb,
-                         sz, sleave_here.c_str()));
+                // (solo: pages the trial has not copied through the scalar cache)
+                sboth(sfmt("  { uint8_t *p_; bool pv_; if (SCOND(!tx_probe_ld(m, %s + %s, %uu, p_, pv_))) %s\n", A.c_str(),
+                           immb, sz, sleave_here.c_str()));
                 if (p.rd) {
                     g.put("    p_ = ok_ ? p_ : const_cast<uint8_t *>(zp);\n");
+                    sboth(sfmt("    uint64_t v_; if (SCOND(pv_)) v_ = *(const g_%s *)p_; else v_ = tx_sload(p_, %uu);\n",
+                               gtype(sz), sz));
                     if (sx) {
                         g.put("    TXSET(%u, (int64_t)(int%d_t)*(const g_%s *)p_); }\n", p.rd, sx, gtype(sz));
-                        sboth(sfmt("    X%u = (uint64_t)(int64_t)(int%d_t)*(const g_%s *)p_; }\n", p.rd, sx, gtype(sz)));
+                        sboth(sfmt("    X%u = (uint64_t)(int64_t)(int%d_t)v_; }\n", p.rd, sx));
                     } else {
                         g.put("    TXSET(%u, *(const g_%s *)p_); }\n", p.rd, gtype(sz));
-                        sboth(sfmt("    X%u = *(const g_%s *)p_; }\n", p.rd, gtype(sz)));
+                        sboth(sfmt("    X%u = v_; }\n", p.rd));
                     }
                 } else {
                     g.put("  }\n");

@@ -1381,6 +1381,32 @@ __device__ __forceinline__ uint32_t tx_probe_st(const LaneMem &m, uint64_t ea, u
     const bool code = !((ea >= t.chi) | (ea + size <= t.clo));
     return ok ? (code ? 3u : 1u) : 0u;
 }
+typedef __attribute__((address_space(4))) const uint32_t const_u32;
+
+// Solo translated loads: a page the trial has not copied (a shared snapshot
+// frame or the zero page -- nothing writes those during a launch) is read
+// through the scalar data cache (tx_sload), its own copies with vector loads.
+__device__ __forceinline__ bool tx_probe_ld(const LaneMem &m, uint64_t ea, uint32_t size, uint8_t *&p, bool &priv) {
+    const uint64_t e = tlb_find(m, ea >> 12);
+    p = const_cast<uint8_t *>(page_of(e)) + (ea & 4095);
+    priv = (e & 1) != 0;
+    return (e != 0) & ((uint32_t)(ea & 4095) + size <= 4096u);
+}
+// `size` bytes at p (any alignment), zero-extended, by scalar loads of the
+// dwords that hold them (may read up to 11 bytes past the access: the shared
+// frame pool and the zero page carry 64 bytes of padding, fi_engine.cpp).
+__device__ __forceinline__ uint64_t tx_sload(const uint8_t *p, uint32_t size) {
+    const uint64_t a = (uint64_t)(uintptr_t)p;
+    const const_u32 *q = (const const_u32 *)(uintptr_t)(a & ~3ULL);
+    const uint32_t sh = (uint32_t)(a & 3) * 8;
+    uint64_t v = ((uint64_t)q[1] << 32) | q[0];
+    if (size == 8) {
+        if (sh) v = (v >> sh) | ((uint64_t)q[2] << (64 - sh));
+        return v;
+    }
+    v >>= sh;
+    return v & ((1ULL << (8 * size)) - 1);
+}
 __device__ __forceinline__ bool tx_probe(const LaneMem &m, uint64_t ea, uint32_t size, bool st, uint8_t *&p,
                                          const TextRef &t) {
     const uint64_t e = tlb_find(m, ea >> 12);
@@ -1406,7 +1432,6 @@ __device__ __forceinline__ bool tx_probe(const LaneMem &m, uint64_t ea, uint32_t
 #define PSTAMP(k) do { } while (0)
 #endif
 
-typedef __attribute__((address_space(4))) const uint32_t const_u32;
 struct Pre4 { uint32_t x, y, z, w; };
 
 __device__ __forceinline__ Pre4 pre_load(const PreInst *p) {
