@@ -643,7 +643,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             if (it == S.chain.end() || (it->second.size() == 1 && it->second[0] == h))
                 sx.put("  case %u: goto %s%u;\n", h, SB.c_str(), h);
             else
-                sx.put("  case %u: etgt = %uu; goto %s%u;\n", h, h, SB.c_str(), it->second[0]);
+                sx.put("  case %u: etgt = %uu; eon = 1; goto %s%u;\n", h, h, SB.c_str(), it->second[0]);
         }
         sx.put("  default: goto S_out;\n  }\n}\n");
     };
@@ -704,13 +704,19 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 const uint32_t next = (pos + 1 != ch.end()) ? *(pos + 1) : x;
                 // a nested header routes further, and clears etgt when it is the target
                 const std::string clr = S.headers.count(next) ? "" : "etgt = 0xFFFFFFFFu; ";
+                const std::string sclr = S.headers.count(next) ? "" : "eon = 0; ";
                 rw_ += "case " + std::to_string(x) + ": " + clr + "goto B_" + std::to_string(next) + "; ";
-                rs_ += "case " + std::to_string(x) + ": " + clr + "goto " + SB + std::to_string(next) + "; ";
+                rs_ += "case " + std::to_string(x) + ": " + sclr + "goto " + SB + std::to_string(next) + "; ";
             }
             const char *fmt = "  if (etgt != 0xFFFFFFFFu) { if (etgt == %uu) etgt = 0xFFFFFFFFu; "
                               "else switch (etgt) { %sdefault: break; } }\n";
+            // solo: a separate pending flag (eon), opaque at every header --
+            // otherwise the compiler threads each back edge through a switch
+            // on etgt, a compare tree per loop iteration
+            const char *sfm = "  ETGT_OPAQUE(); if (__builtin_expect(eon != 0, 0)) { if (etgt == %uu) eon = 0; "
+                              "else switch (etgt) { %sdefault: break; } }\n";
             g.put(fmt, h0, rw_.c_str());
-            sboth(sfmt(fmt, h0, rs_.c_str()));
+            sboth(sfmt(sfm, h0, rs_.c_str()));
         }
         // ---- wave block prologue: merge a parked group waiting here, leave or
         // switch groups when lanes outside run first, then one combined check

@@ -1362,6 +1362,8 @@ typedef __attribute__((address_space(1), aligned(1))) uint64_t g_u64;
 #define SUNI(x) (x)
 #define SUNI32(x) (x)
 #define SX(r, e) X##r = (uint64_t)(e)
+// cycle headers: the pending-route flag as an opaque scalar (fi_translate.cpp)
+#define ETGT_OPAQUE() __asm__ volatile("" : "+s"(eon))
 
 // The pre-decoded text (uniform): table, text range, exact code range.
 struct TextRef { const PreInst *pre; uint32_t lo, hi, bytes; uint64_t clo, chi; };
@@ -1499,6 +1501,7 @@ __device__ __noinline__ void solo_tx_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds_
     const uint32_t bud = io->bud, lwm = io->lwm;
     uint32_t sdlo = io->sdlo, sdhi = io->sdhi;
     uint32_t etgt = 0xFFFFFFFFu;   // block an entry is routed to through its cycle headers
+    uint32_t eon = 0;              // ... while an entry is being routed
     bool schg = false;
     uint32_t cslo = 0xFFFFFFFFu, cshi = 0u;
     uint32_t st = 0, xt = 0, fb = 0, db = 0;
@@ -1568,7 +1571,7 @@ __device__ __noinline__ void solo_tx_clean_run(KCtx *CX, lds_u64 *R, lds_mem *mp
     tx.bytes = CX->text_bytes; tx.clo = CX->code_lo; tx.chi = CX->code_hi;
     uint64_t spc = io->spc;
     const uint32_t bud = io->bud;
-    uint32_t etgt = 0xFFFFFFFFu;
+    uint32_t etgt = 0xFFFFFFFFu, eon = 0;
     uint32_t st = 0, xt = 0, fb = 0, db = 0;
 #define TXR(r) uint64_t X##r = R[r];
     TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
