@@ -589,6 +589,11 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     Gen so{pre, text_lo, leaders, executed, {}};
     Gen sq{pre, text_lo, leaders, executed, {}};
     Gen sc{pre, text_lo, leaders, executed, {}};   // the clean solo body (mode 0 only)
+    // clean body: memory sites in cycles keep the last page they translated
+    // (CV_i / CP_i: vpn and TLB entry; the TLB does not change inside the
+    // blocks, so a hit equals tlb_find) -- at most kSiteCaches of them
+    constexpr uint32_t kSiteCaches = 8;
+    uint32_t n_sites = 0;
     n_insts = 0;
     auto hex = [](uint64_t v) {
         char b[32];
@@ -782,8 +787,22 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 g.put("  { uint8_t *p_; const bool ok_ = tx_probe(m, %s + %s, %uu, false, p_, tx);\n", A.c_str(), immb, sz);
                 g.put("    if (TXB(mine && !ok_)) %s\n", leave_here.c_str());
                 // (solo: pages the trial has not copied through the scalar cache)
-                sboth(sfmt("  { uint8_t *p_; bool pv_; if (SCOND(!tx_probe_ld(m, %s + %s, %uu, p_, pv_))) %s\n", A.c_str(),
-                           immb, sz, sleave_here.c_str()));
+                {
+                    const std::string pl = sfmt("  { uint8_t *p_; bool pv_; if (SCOND(!tx_probe_ld(m, %s + %s, %uu, p_, pv_))) %s\n",
+                                                A.c_str(), immb, sz, sleave_here.c_str());
+                    so_.out += pl;
+                    if (!oddon) {
+                        if (S.chain.count(h0) && n_sites < kSiteCaches) {
+                            const uint32_t i = n_sites++;
+                            sc.put("  { uint8_t *p_; bool pv_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
+                                   "    if (SCOND(vp_ != CV%u)) { CV%u = vp_; CP%u = tlb_find(m, vp_); }\n"
+                                   "    if (SCOND(!tx_probe_e(CP%u, ea_, %uu, p_, pv_))) %s\n",
+                                   A.c_str(), immb, i, i, i, i, sz, sleave_here.c_str());
+                        } else {
+                            sc.out += pl;
+                        }
+                    }
+                }
                 if (p.rd) {
                     g.put("    p_ = ok_ ? p_ : const_cast<uint8_t *>(zp);\n");
                     sboth(sfmt("    uint64_t v_; if (SCOND(pv_)) v_ = *(const g_%s *)p_; else v_ = tx_sload(p_, %uu);\n",
@@ -816,10 +835,20 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                        "goto S_out; } } }\n", sz, hex(bhi).c_str(), sz, ftb.c_str(),
                        scommit(k_st + 1, k_xt + xt, k_fb + p.len, k_db + sz).c_str(), ftb.c_str());
                 // clean: a store into the code range (or any the probe refuses) leaves before itself
-                if (!oddon)
-                    sc.put("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, true, p_, tx))) %s\n"
-                           "    *(g_%s *)p_ = (%s)%s; }\n", A.c_str(), immb, sz, sleave_here.c_str(), gtype(sz),
-                           ltype(sz), B.c_str());
+                if (!oddon) {
+                    if (S.chain.count(h0) && n_sites < kSiteCaches) {
+                        const uint32_t i = n_sites++;
+                        sc.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
+                               "    if (SCOND(vp_ != CV%u)) { CV%u = vp_; CP%u = tlb_find(m, vp_); }\n"
+                               "    if (SCOND(!tx_probe_st_e(CP%u, ea_, %uu, p_, tx))) %s\n"
+                               "    *(g_%s *)p_ = (%s)%s; }\n", A.c_str(), immb, i, i, i, i, sz, sleave_here.c_str(),
+                               gtype(sz), ltype(sz), B.c_str());
+                    } else {
+                        sc.put("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, true, p_, tx))) %s\n"
+                               "    *(g_%s *)p_ = (%s)%s; }\n", A.c_str(), immb, sz, sleave_here.c_str(), gtype(sz),
+                               ltype(sz), B.c_str());
+                    }
+                }
                 break;
             case C_BR: {
                 const std::string c = subst(cond, A, B, immb, pcb);
@@ -892,7 +921,14 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     leaders_out.assign(leaders.begin(), leaders.end());
     // odd-pc entries: bit 31 + the pre-decoded index of their key (kPreOddLeader)
     for (uint64_t pc : olead) leaders_out.push_back(0x80000000u | okey(pc));
-    return g.out + FI_TX_SPLIT + so.out + FI_TX_SPLIT + sq.out + FI_TX_SPLIT + sc.out;
+    // the clean body's entry: its site caches start empty (declared without an
+    // initializer: the dispatch label below them is also a jump target)
+    std::string sc_head;
+    for (uint32_t i = 0; i < kSiteCaches; i++) sc_head += sfmt("  uint64_t CV%u, CP%u;\n", i, i);
+    sc_head += "S_entry:\n";
+    for (uint32_t i = 0; i < kSiteCaches; i++) sc_head += sfmt("  CV%u = ~0ULL; CP%u = 0;\n", i, i);
+    sc_head += "  goto S_dispatch;\n";
+    return g.out + FI_TX_SPLIT + so.out + FI_TX_SPLIT + sq.out + FI_TX_SPLIT + sc_head + sc.out;
 }
 
 }  // namespace fi

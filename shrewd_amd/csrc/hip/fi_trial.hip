@@ -1409,6 +1409,17 @@ __device__ __forceinline__ uint64_t tx_sload(const uint8_t *p, uint32_t size) {
     v >>= sh;
     return v & ((1ULL << (8 * size)) - 1);
 }
+// The same given the TLB entry e of ea's page (the clean body's site caches).
+__device__ __forceinline__ bool tx_probe_e(uint64_t e, uint64_t ea, uint32_t size, uint8_t *&p, bool &priv) {
+    p = const_cast<uint8_t *>(page_of(e)) + (ea & 4095);
+    priv = (e & 1) != 0;
+    return (e != 0) & ((uint32_t)(ea & 4095) + size <= 4096u);
+}
+__device__ __forceinline__ bool tx_probe_st_e(uint64_t e, uint64_t ea, uint32_t size, uint8_t *&p, const TextRef &t) {
+    p = const_cast<uint8_t *>(page_of(e)) + (ea & 4095);
+    const bool code_ok = (ea >= t.chi) | (ea + size <= t.clo);
+    return ((e & 1) != 0) & code_ok & ((uint32_t)(ea & 4095) + size <= 4096u);
+}
 __device__ __forceinline__ bool tx_probe(const LaneMem &m, uint64_t ea, uint32_t size, bool st, uint8_t *&p,
                                          const TextRef &t) {
     const uint64_t e = tlb_find(m, ea >> 12);
@@ -1578,7 +1589,7 @@ __device__ __noinline__ void solo_tx_clean_run(KCtx *CX, lds_u64 *R, lds_mem *mp
     TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
     TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
 #undef TXR
-    goto S_dispatch;
+    goto S_entry;
     /*@TX_SOLO_CLEAN@*/
 S_out:
 #define TXW(r) R[r] = X##r;
