@@ -1734,7 +1734,8 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
             }
             PST(0);
             const uint32_t fl = (q3 >> 8) & 0xFF, kind = (q3 >> 16) & 63;
-            if (!(fl & kPreValid)) break;
+            // (an invalid entry has kind K_SLOW too: fi_predecode_kernel leaves aux 0,
+            // PRE_AT zeroes it past the text, decoded entries are valid)
             if (kind == K_SLOW) break;
 #ifdef FI_TX
             // a block leader (odd pcs: the solo-odd kernel's odd-pc leaders) past the first instruction
