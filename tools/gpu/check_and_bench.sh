@@ -8,8 +8,8 @@ rc=$?; tail -4 gpurun_out/pytest_gpu.log; grep -E "FAILED|Error" gpurun_out/pyte
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
 cat gpurun_out/bench.json
-# (intmix: a 12 s CPU sample, so that its parity leg checks >= 20k trials)
-for w in qsort:3 intmix:12; do
+# (intmix: a 15 s CPU sample, so that its parity leg checks >= 20k trials)
+for w in qsort:3 intmix:15; do
     s=${w#*:}; w=${w%%:*}
     timeout -k 10 300 python -u bench.py --workload $w --cpu-seconds $s > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err || exit $?
     python -c "import json; d=json.load(open('gpurun_out/bench_$w.json')); print('$w', round(d['value']), d['ms_per_step'], d['parity'])"
