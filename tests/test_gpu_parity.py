@@ -560,3 +560,20 @@ def test_odd_pc_kernel(engine_factory, oracle_mod, name):
     assert 2 not in off.debug_dispatch_kinds()
     assert np.array_equal(a, b)
     compare(a, oracle_for(oracle_mod, name).run_trials(sites, protect_mask=0), sites)
+
+
+@pytest.mark.parametrize("name,ids", [("qsort", [11487, 46948]), ("intmix", [64617, 53499, 34535])])
+def test_rewritten_code_loops_bit_exact(engine_factory, oracle_mod, name, ids):
+    """The campaign tails: trials whose flipped base pointer stored into the
+    text and that then loop through the rewritten code (intmix 64617: 1.33M
+    instructions, 6 clean and 4 rewritten per iteration).  The solo
+    translated body steps the instructions its blocks do not cover in place
+    (S_interp) instead of leaving for the interpreter -- outcomes equal the
+    oracle's."""
+    e = engine_factory(name)
+    o = oracle_for(oracle_mod, name)
+    e.set_campaign(0x5EED0002, REGS | PC, 1)
+    e.set_protect(0)
+    sites = e.sample(0, max(ids) + 1)[ids]
+    dev, _ = e.run_sites(sites)
+    compare(dev, o.run_trials(sites, protect_mask=0), sites)
