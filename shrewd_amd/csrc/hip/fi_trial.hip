@@ -1661,9 +1661,9 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
     const uint64_t tlo = CX->text_lo, clo = CX->code_lo, chi = CX->code_hi;
     const uint32_t tby = CX->text_bytes, tlo32 = (uint32_t)tlo;
     const const_u32 *const pre = (const const_u32 *)(uintptr_t)CX->pre;
-    // the TLB in registers (refreshed after lookup_full inserts)
-    uint64_t tv0 = uni64(m.tv0), tv1 = uni64(m.tv1), tv2 = uni64(m.tv2), tv3 = uni64(m.tv3);
-    uint64_t tp0 = uni64(m.tp0), tp1 = uni64(m.tp1), tp2 = uni64(m.tp2), tp3 = uni64(m.tp3);
+    // the last page translated, in registers (the TLB itself stays in LDS:
+    // mappings do not change inside a run, lookup_full only inserts)
+    uint64_t cvpn = ~0ULL, cpg = 0;
     // rewritten code: the bounding range as text offsets [ddlo, ddhi) (empty
     // when clean), the LDS map for the exact test
     const bool have_dl = m.dl != nullptr;
@@ -1717,8 +1717,6 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
                     uint32_t raw = 0, t = 1;
                     uint64_t fva = 0;
                     if (fetch_lane(CX, w, m, slot, tlo + po, raw, t, fva) != 0) break;
-                    tv0 = uni64(m.tv0); tv1 = uni64(m.tv1); tv2 = uni64(m.tv2); tv3 = uni64(m.tv3);
-                    tp0 = uni64(m.tp0); tp1 = uni64(m.tp1); tp2 = uni64(m.tp2); tp3 = uni64(m.tp3);
                     Dec dd = rv_decode(uni32(raw));
                     const uint32_t u = uop_of(dd);
                     q1 = (uint32_t)dd.op | ((uint32_t)dd.rd << 8) | ((uint32_t)dd.rs1 << 16) | ((uint32_t)dd.rs2 << 24);
@@ -1771,15 +1769,11 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
                 msz = 1u << ((aux >> 12) & 3);
                 const uint64_t ea = a0 + imm, vpn = ea >> 12;
                 const uint32_t off = (uint32_t)ea & 4095u;
-                uint64_t p = 0;
-                p = tv0 == vpn ? tp0 : p;
-                p = tv1 == vpn ? tp1 : p;
-                p = tv2 == vpn ? tp2 : p;
-                p = tv3 == vpn ? tp3 : p;
-                if (!p) {
-                    p = uni64(lookup_full(CX, w, m, slot, vpn));
-                    tv0 = uni64(m.tv0); tv1 = uni64(m.tv1); tv2 = uni64(m.tv2); tv3 = uni64(m.tv3);
-                    tp0 = uni64(m.tp0); tp1 = uni64(m.tp1); tp2 = uni64(m.tp2); tp3 = uni64(m.tp3);
+                uint64_t p = cpg;
+                if (vpn != cvpn) {
+                    p = uni64(tlb_find(m, vpn));
+                    if (!p) p = uni64(lookup_full(CX, w, m, slot, vpn));
+                    if (p) { cvpn = vpn; cpg = p; }
                 }
                 if (!(p && (!st || (p & 1)) && off + msz <= 4096)) { msz = 0xFFFFFFFFu; break; }   // the general path's
                 __attribute__((address_space(1))) uint8_t *pg =
