@@ -228,7 +228,7 @@ __global__ void __launch_bounds__(256) fi_hist_kernel(const fi_site *sites, cons
 // the odd-pc survivors sort last, and they are counted.
 // solo != 0: the next epoch runs one trial per wave, where the order only
 // decides when a trial starts: trials that rewrote their code (interpreted at
-// ~20x the cost of translated code) start first.
+// ~20x the cost of translated code) start first, then the rest longest-first.
 __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
                                     uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd,
                                     uint32_t solo) {
@@ -238,7 +238,11 @@ __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, 
         const uint32_t sl = list[i];
         const uint64_t pc = save[sl].pc;
         uint64_t k = ((pc - text_lo) << 32) | (save[sl].ninst & 0xFFFFFFFFu);
-        if (solo) k = ((uint64_t)(((save[sl].flags >> 3) & 1) ^ 1) << 62) | (k >> 2);
+        // solo epoch: code-rewriting survivors first, then longest-first -- the
+        // fewest committed instructions have the most left to run (golden
+        // suffix or hang cap); one survivor per wave, so no pc grouping
+        // (profiles/r03k_ab_lpt.jsonl: crc32 +4 %, intmix +5 %)
+        if (solo) k = ((uint64_t)(((save[sl].flags >> 3) & 1) ^ 1) << 62) | (save[sl].ninst & ((1ULL << 46) - 1));
         if (n_odd) {
             k = ((pc & 1) << 63) | (k >> 1);
             if (pc & 1) atomicAdd(n_odd, 1u);
