@@ -171,6 +171,7 @@ struct fi_engine {
     uint64_t *d_wave_dbg = nullptr;
     uint64_t *d_fregs = nullptr;     // FP registers of the work slots
     bool golden_fp = false;          // the golden run wrote FP state: no snapshot start / early exit
+    uint64_t clk_until = 0;          // 1 + numInst of the golden run's last curTick read (0: none; DevCtx::clk_until)
     uint8_t *d_priv = nullptr;
     uint64_t *d_priv_vpn = nullptr;
     VmState *d_vm = nullptr;         // [cap] per-slot SE memory map (trials that made a VM syscall)
@@ -746,6 +747,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.rnd_tab = e->d_rnd; c.rnd_len = e->d_rnd ? kRndLen : 0; c.clk_period = e->clk_period;
     c.exe_path = e->d_exe; c.exe_len = e->d_exe ? e->exe_path.size() : 0;
     c.tick0 = e->tick0;
+    c.clk_until = e->clk_until;
     c.fp0 = e->fp0_on ? e->d_fp0 : nullptr;
     c.fcsr0 = e->fcsr0;
     c.vm0 = e->vm0_on ? e->d_vm0 : nullptr;
@@ -909,6 +911,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     e->golden.data_bytes = stats[1];
     e->gdetail = o.detail;
     e->golden_fp = stats[22] != 0;
+    e->clk_until = stats[52];
 
     // ---- pass 2: the same run again, capturing a snapshot every I committed
     // instructions (state + every page written so far), within ~1 GiB

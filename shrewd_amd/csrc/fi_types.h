@@ -196,6 +196,8 @@ struct DevCtx {
     uint64_t exe_len;                // 0: unknown (that call escapes as host)
     uint64_t clk_period;             // ticks per CPU cycle (clock_gettime)
     uint64_t tick0;                  // curTick at the campaign start (a checkpoint's [Globals] curTick; else 0)
+    uint64_t clk_until;              // the golden run reads curTick (clock_gettime, rpns) at numInst < clk_until:
+                                     // before that a trial equals a snapshot only with the same ncyc (0 = never)
     const uint64_t *fp0;             // a checkpoint's FP registers (NULL: none -- zero, no FP state)
     uint32_t fcsr0;                  //   and its fflags | frm << 5
     const VmState *vm0;              // a checkpoint's SE memory map (NULL: the process-start one, brk0 / svma_*)
@@ -224,6 +226,7 @@ struct DevCtx {
                                      // [25] golden data-access events [26] memory faults ended at injection
                                      // [27] register faults dead at injection [30] trials re-run with more private
                                      // pages (FI_ESC_RESOURCE, fi_engine.cpp run_chunk)
+                                     // [52] record mode: 1 + numInst of the golden run's last curTick read
                                      // [32..39] FI_PROF phase cycles
                                      // [40 + 4k + {0,1,2,3}] fetch B, data B, pages, device insts of kernel k
                                      // (0 the 64-lane kernel, 1 solo, 2 solo-odd)

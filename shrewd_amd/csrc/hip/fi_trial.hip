@@ -1074,6 +1074,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         if (!a1) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }
         if (!proxy_readable(c, w, m, slot, a1, 16)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
         const uint64_t ns = (c->tick0 + (L.ncyc - 1) * c->clk_period) / 1000;
+        if (c->record) c->stats[52] = L.ninst + 1;   // the golden future reads curTick up to here
         const uint64_t sec = ns / 1000000000ULL + 1000000000ULL, nsec = ns % 1000000000ULL;
         char b[16];
         for (int k = 0; k < 8; k++) { b[k] = (char)(sec >> (8 * k)); b[8 + k] = (char)(nsec >> (8 * k)); }
@@ -2231,7 +2232,11 @@ __device__ __forceinline__ void trial_body() {
                 bool eq = grp && L.pc == S->pc && L.out_pos == S->out_pos && L.err_pos == S->err_pos &&
                           (!L.out_bad || (CX->early_exit & 2)) &&
                           m.stack_min == S->stack_min && !L.fp && L.injected != 3 && m.resv == kNone &&
-                          m.lock == kNone && !m.vm;
+                          m.lock == kNone && !m.vm &&
+                          // the golden suffix reads curTick: the same future needs the same tick count
+                          // too (a path with other non-counting ticks -- ecalls, straddled fetches --
+                          // reconverges with the same numInst but would print another time)
+                          (kn >= CX->clk_until || L.ncyc == S->ncyc);
                 if (wballot<kNL>(eq)) {
                     // a register the golden future writes before reading it cannot
                     // influence the outcome (liveness from the golden trace)
@@ -3229,7 +3234,10 @@ __device__ __forceinline__ void trial_body() {
                 switch ((uint32_t)d.imm) {
                 // rpns: curTick() in ns during this instruction's execute -- its
                 // fetch tick(s) already elapsed (the commit adds them to ncyc)
-                case 0x07: v = (CX->tick0 + (L.ncyc + ticks - 1) * CX->clk_period) / 1000; break;
+                case 0x07:
+                    v = (CX->tick0 + (L.ncyc + ticks - 1) * CX->clk_period) / 1000;
+                    if (CX->record) CX->stats[52] = L.ninst + 1;
+                    break;
                 case 0x23:   // m5sum(a0..a5)
                     xdet = L.watch >= 10 && L.watch <= 15;
                     v = RREG(10) + RREG(11) + RREG(12) + RREG(13) + RREG(14) + RREG(15);

@@ -426,7 +426,7 @@ def test_native_driver_matches_engine(engine_factory, tmp_path):
     assert hist["counts"].tobytes() == rh["counts"].tobytes()
 
 
-@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp", "rnd", "xop", "sys2"])
+@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp", "rnd", "xop", "sys2", "clk"])
 def test_known_answer_programs(oracle_mod, prog):
     """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
@@ -444,6 +444,7 @@ def test_known_answer_programs(oracle_mod, prog):
     fp: F/D/Zfh arithmetic in every rounding mode with fflags, the dynamic
     rounding mode and fcsr (answers from the reference SoftFloat).
     rnd: getrandom (gem5's mt19937_64 stream) and clock_gettime (curTick).
+    clk: clock_gettime after a branch whose arms differ only in ticks.
     xop: scalar crypto, Zfa (fli / fround / fcvtmod.w.d), M5 pseudo-ops, the
     warn-only privileged no-ops and the cache-block ops.
     sys2: read, readlinkat (/proc/self/exe) and riscv_hwprobe.  The device golden run (general interpreter)
@@ -462,7 +463,8 @@ def test_known_answer_programs(oracle_mod, prog):
                      "fp": (kat.fp_program_elf, kat.fp_program_expected),
                      "rnd": (kat.rnd_program_elf, kat.rnd_program_expected),
                      "xop": (kat.xop_program_elf, kat.xop_program_expected),
-                     "sys2": (kat.sys2_program_elf, kat.sys2_program_expected)}[prog]
+                     "sys2": (kat.sys2_program_elf, kat.sys2_program_expected),
+                     "clk": (kat.clk_program_elf, kat.clk_program_expected)}[prog]
     if prog in ("fp", "xop") and not oracle_mod.has_softfloat():
         pytest.skip("oracle without the reference SoftFloat")
     if prog == "xop" and not oracle_mod.has_rvk():
@@ -493,6 +495,34 @@ def test_known_answer_programs(oracle_mod, prog):
     assert (dev["cls"] == 0).all()
     dev, _ = e.run_sites(sites)
     compare(dev, o.run_trials(sites, protect_mask=0), sites)
+
+
+def test_clock_read_blocks_tick_blind_early_exit(oracle_mod):
+    """Exact early exit when the golden suffix reads curTick: the clk program's
+    branch-register faults take an arm with 16 extra non-counting ticks
+    (ignored-syscall ecalls) and reconverge with the golden pc, registers,
+    memory and numInst at every later snapshot -- but print a later time.
+    The comparator must also require the golden tick count there
+    (fi_trial.hip, DevCtx::clk_until): every such trial is SDC, as on the
+    oracle, with early exit on (the golden run touches no FP/VM/LR-SC state,
+    so snapshots and early exit stay enabled) and off."""
+    from shrewd_amd import Engine
+    import test_isa_vectors as kat
+    elf = kat.clk_program_elf()
+    o = oracle_mod.Oracle(elf, "clk")
+    o.run_golden()
+    sites = kat.clk_branch_sites(64)
+    ref = o.run_trials(sites, protect_mask=0)
+    assert (ref["cls"] == 1).all()
+    for flags in (0, 2):   # default, FI_CFG_NO_EARLY_EXIT
+        e = Engine(flags=flags, snapshot_interval=64)
+        e.load_elf(elf, ["clk"])
+        e.golden_run()
+        dev, _ = e.run_sites(sites)
+        if flags == 0:
+            assert int(e.debug_stats()[11]) > 0, "early-exit comparisons did not run"
+        compare(dev, ref, sites)
+        e.close()
 
 
 def test_sdc_early_exit(engine_factory, oracle_mod):

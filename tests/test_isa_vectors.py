@@ -1359,6 +1359,104 @@ def rnd_program_expected() -> bytes:
     return out
 
 
+# ---------------------------------------------------------------- clk program
+# A branch on s3 whose two arms commit the same instructions but take
+# different numbers of ticks: the taken arm (s3 != 0, a fault) adds CLK_ECALLS
+# ignored-syscall ecalls, each one tick that does not count as an instruction
+# (SyscallFault: atomic.cc:688-700 counts numInst only on NoFault).  Both arms
+# leave a0 = 0, a7 = 99, and s3 is rewritten after the merge, so a trial that
+# took the slow arm reaches every later snapshot with the golden registers,
+# memory, pc and numInst -- only curTick differs.  The program then reads
+# clock_gettime (curTick in ns, syscall_emul.hh:2266-2278) and prints it: the
+# trial prints CLK_ECALLS * 500 / 1000 ns more than the golden run (SDC).
+CLK_PRE = 300      # instructions before the branch (fault sites)
+CLK_POST = 700     # instructions between the merge and the clock read (snapshot boundaries)
+CLK_ECALLS = 16
+
+
+def clk_program_source() -> str:
+    pre = "\n".join(["    addi  t3, t3, 1"] * CLK_PRE)
+    post = "\n".join(["    addi  t4, t4, 3"] * CLK_POST)
+    ecalls = "\n".join(["    ecall"] * CLK_ECALLS)
+    return f"""    .text
+_start:
+    la    s2, out
+    li    s3, 0
+{pre}
+    bnez  s3, slow
+    li    a0, 0
+    li    a7, 99
+    j     merge
+slow:
+    li    a7, 99
+{ecalls}
+    li    a0, 0
+    j     merge
+merge:
+    li    s3, 0
+{post}
+    li    a0, 0
+    mv    a1, s2
+    li    a7, 113
+    ecall
+    li    a0, 1
+    mv    a1, s2
+    li    a2, 16
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 93
+    ecall
+    .bss
+    .balign 8
+out:
+    .zero 16
+"""
+
+
+def clk_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(clk_program_source(), compress=False)
+
+
+def clk_branch_sites(n=64):
+    """Faults on s3 (x19) before the branch: every bit sends the trial down the slow arm."""
+    import numpy as np
+    from oracle.pyoracle import SITE_DT
+    s = np.zeros(n, SITE_DT)
+    s["inst"] = 3 + np.arange(n) * (CLK_PRE // n)
+    s["mask"] = np.uint64(1) << (np.arange(n) % 64).astype(np.uint64)
+    s["target"] = 19
+    s["trial"] = np.arange(n)
+    return s
+
+
+def clk_program_expected() -> bytes:
+    from oracle import pyoracle
+    o = pyoracle.Oracle(clk_program_elf(), "clk")
+    o.run_golden()
+    return o.golden_stdout()
+
+
+def test_clk_program_on_oracle(oracle_mod):
+    """The oracle's golden run prints curTick at the clock read; a branch-register
+    fault (slow arm) ends SDC, its output later by exactly the extra ticks."""
+    o = oracle_mod.Oracle(clk_program_elf(), "clk")
+    g = o.run_golden()
+    assert g.exit_code == 0
+    out = o.golden_stdout()
+    sec, nsec = int.from_bytes(out[:8], "little"), int.from_bytes(out[8:16], "little")
+    assert sec == 10**9
+    assert 0 < nsec < g.ncycles * 500 // 1000
+    sites = clk_branch_sites(8)
+    res = o.run_trials(sites, protect_mask=0)
+    assert (res["cls"] == 1).all()              # SDC: the printed time differs
+    assert (res["ninst"] == g.ninst).all()      # ... with the golden instruction count
+    _, t = o.run_one(sites[0], protect_mask=0)
+    t_ns = int.from_bytes(t[8:16], "little")
+    assert t_ns - nsec == CLK_ECALLS * 500 // 1000
+
+
 # ---------------------------------------------------------------- xop program
 # The instruction groups gem5 executes outside the base ISA (oracle/rv64se.c
 # refine_misc, the Zfa ops): scalar crypto on operand pairs (answers from the
