@@ -13,6 +13,10 @@ golden snapshot -- exact), outcome histogram, and the RCCL
 all-reduce of the histogram (the campaign's only exchange; N > 1).
 Trials shard by id across ranks (weak scaling: per-GPU work fixed).
 
+The same line carries the other C2 workload (qsort, 100k trials per GPU) and
+C3's per-GPU shard (intmix, 125k trials per GPU) under "workloads", each with
+its own steps, roofline, cold start and (N = 1) a >= 20k-trial parity leg.
+
 Launch: python bench.py [--gpus 1] [--steps 5] [--warmup 1]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
@@ -44,7 +48,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--parity-trials", type=int, default=0,
-                    help="check at least this many trial ids against the oracle (beyond the timed CPU sample)")
+                    help="check at least this many trial ids of the headline workload against the oracle")
+    ap.add_argument("--workloads", default="qsort:100000:5,intmix:125000:2",
+                    help="further workloads on the same line, name:trials_per_gpu:steps (\"\" = none)")
+    ap.add_argument("--extra-parity", type=int, default=20000,
+                    help="trial ids of each further workload checked against the oracle (N = 1)")
     ap.add_argument("--lanes", type=int, default=0, help="trials per 64-lane wave (0: engine default)")
     ap.add_argument("--resume-lanes", type=int, default=0, help="trials per wave in resumed epochs (0: default)")
     ap.add_argument("--epochs", type=int, default=0, help="epochs per chunk (0: default)")
@@ -75,7 +83,7 @@ def host_cores():
     return max(1, avail), os.cpu_count() or 1, model
 
 
-def cpu_baseline(elf: bytes, argv0: str, seed: int, budget_s: float):
+def cpu_baseline(elf: bytes, argv0: str, seed: int, budget_s: float, min_trials: int = 0):
     """The oracle (plain-C restatement of gem5 RV64 SE, test infrastructure)
     on every host core this process may use, same campaign, bounded sample.
     Like a serial gem5 run, the oracle runs every trial from process start to
@@ -89,7 +97,7 @@ def cpu_baseline(elf: bytes, argv0: str, seed: int, budget_s: float):
     t0 = time.perf_counter()
     o.run_trials(calib, threads=threads)
     dt = max(time.perf_counter() - t0, 1e-3)
-    n = int(min(2_000_000, max(len(calib), len(calib) * budget_s / dt)))
+    n = int(min(2_000_000, max(len(calib), min_trials, len(calib) * budget_s / dt)))
     sites = o.sample(seed, 0, n, REGS_PC, 1)
     t0 = time.perf_counter()
     out = o.run_trials(sites, threads=threads)
@@ -103,6 +111,171 @@ def cpu_baseline(elf: bytes, argv0: str, seed: int, budget_s: float):
            "host_cpus_total": machine_cpus, "cpu_model": model,
            "guest_inst_per_s": insts / dt}
     return rec, out
+
+
+def load_traffic(path, workload, trials, lanes):
+    """HBM bytes per launch from the PMC passes of the same configuration
+    (profiles/pmc_traffic.json), if they were taken on it."""
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return {}
+    if tj.get("workload") == workload and tj.get("trials") == trials and tj.get("lanes_per_wave", 64) == lanes:
+        return tj
+    return {}
+
+
+def run_workload(a, name, T, steps, warmup, rank, world, dev, cpu_seconds, min_parity):
+    """One workload's bench record: cold start (golden run, the first campaign
+    step while the translated kernels build in the background), then `warmup`
+    + `steps` timed steps of T trials per GPU on the translated kernels, the
+    per-kernel roofline, and (N = 1) the CPU baseline + parity leg."""
+    import torch
+    import torch.distributed as dist
+    from shrewd_amd import ESCAPE_NAMES, HIST_DT, Engine
+    from shrewd_amd.fi import CFG_JIT_NO_CACHE, escape_breakdown
+    with open(os.path.join(ROOT, "workloads", f"{name}.elf"), "rb") as f:
+        elf = f.read()
+    # no code-object cache: the cold start below is the one a fresh campaign pays
+    eng = Engine(device=dev.index, max_trials_per_launch=max(T, 1024), lanes_per_wave=a.lanes,
+                 resume_lanes=a.resume_lanes, epoch_iters=a.epoch_iters, epochs=a.epochs, flags=CFG_JIT_NO_CACHE)
+    lanes = eng.config()["lanes_per_wave"]
+    # ---- cold start: load + golden run (+ snapshots, liveness, translation
+    # text) until trials can run; the first step runs while the translated
+    # kernels build (static kernels, 16k-trial chunks, switching when it lands)
+    t0 = time.perf_counter()
+    eng.load_elf(elf, [name])
+    g = eng.golden_run(wait_translation=False)
+    golden_s = time.perf_counter() - t0
+    eng.set_campaign(a.seed, REGS_PC, 1)
+    t1 = time.perf_counter()
+    eng.run_trials(rank * T, T, want_outcomes=False)
+    first_step_s = time.perf_counter() - t1
+    g = eng.wait_translation()
+    jit_ready_s = time.perf_counter() - t0
+    cold = {"golden_s": golden_s, "first_step_s": first_step_s,
+            "campaign_s": golden_s + first_step_s, "campaign_trials_per_s": T / (golden_s + first_step_s),
+            "translated_ready_s": jit_ready_s, "translate_us": int(g.translate_us),
+            "translated_blocks": int(g.translated_blocks),
+            "note": "load + golden run, then one step of T trials through the product path while the "
+                    "translated kernels build in the background (no code-object cache)"}
+
+    d_out = torch.empty(T * 16, dtype=torch.uint8, device=dev)
+    hist_words = HIST_DT.itemsize // 8
+    d_hist = torch.zeros(hist_words, dtype=torch.int64, device=dev)
+    d_hist_node = torch.zeros_like(d_hist)
+    # one dedicated stream for engine kernels, histogram copies and RCCL
+    tstream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(tstream)
+    stream = tstream.cuda_stream
+
+    def step():
+        d_hist.zero_()
+        eng.run_trials_device(rank * T, T, d_out.data_ptr(), d_hist.data_ptr(), stream)
+        d_hist_node.copy_(d_hist)
+        if world > 1:
+            dist.all_reduce(d_hist_node)      # RCCL over xGMI: outcome histogram only
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    eng.kernel_timer_reset()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    node_h = np.frombuffer(d_hist_node.cpu().numpy().tobytes(), HIST_DT)[0]
+    if rank != 0:
+        eng.close()
+        return None
+    trials_total = world * T * steps
+    # roofline per trial kernel, per launch (DESIGN.md §4, SURVEY.md §8d):
+    # algorithmic bytes = fetched instruction bytes + load/store bytes of the
+    # guest instructions the kernel executed + 4096 B per copy-on-write page
+    # it made, and for the 64-lane kernel (every trial starts there) 264 B of
+    # initial state + 16 B of outcome per trial; counted on the device per
+    # kernel (DevCtx::stats[40..51]) over the last step -- every step runs
+    # the same trial ids, so the last step's counts are every step's.
+    # Duration = the mean of that kernel's dispatches (HIP events on its
+    # stream); the dominant kernel is the one with the most device time.
+    st = eng.debug_stats()
+    kinds, dms = eng.debug_dispatch_kinds(), eng.debug_dispatch_ms()
+    tx = eng.translate_status() == ""
+    names = (["fi_trial_kernel_tx", "fi_trial_kernel_tx_solo", "fi_trial_kernel_tx_solo_odd"] if tx
+             else ["fi_trial_kernel", "fi_trial_kernel_solo", "fi_trial_kernel_solo_odd"])
+    tj = load_traffic(a.traffic_json, name, T, lanes)
+    per_kernel = {}
+    for k, kname in enumerate(names):
+        ms_k = [m for m, kk in zip(dms, kinds) if kk == k]
+        if not ms_k:
+            continue
+        disp = len(ms_k) / steps
+        b = int(st[40 + 4 * k]) + int(st[41 + 4 * k]) + 4096 * int(st[42 + 4 * k]) + (T * (264 + 16) if k == 0 else 0)
+        avg_ms = sum(ms_k) / len(ms_k)
+        per_launch = b / disp
+        ach = per_launch / (avg_ms / 1e3) / 1e9
+        tk = tj.get("per_kernel", {}).get(kname, {})
+        per_kernel[kname] = {"avg_kernel_ms": avg_ms, "dispatches_per_step": disp,
+                             "ms_per_step": avg_ms * disp, "algorithmic_bytes_per_launch": per_launch,
+                             "achieved": ach, "frac": ach / HBM_PEAK_GBS,
+                             "device_insts_per_launch": int(st[43 + 4 * k]) / disp,
+                             "traffic": tk.get("hbm_bytes_per_launch"), "issue": tk.get("issue")}
+    dom = max(per_kernel, key=lambda n: per_kernel[n]["ms_per_step"])
+    D = per_kernel[dom]
+    cls = node_h["counts"].sum(axis=(0, 1))
+    rec = {
+        "value": trials_total / elapsed,
+        "ms_per_step": elapsed / steps * 1e3,
+        "steps": steps, "warmup": warmup,
+        "config": {"workload": f"{name} (RV64, {g.ninst} golden insts), {T} single-bit x1..x31+pc trials "
+                               f"per GPU per step",
+                   "trials_per_gpu": T, "seed": hex(a.seed), "structures": "x1-x31,pc", "burst": 1,
+                   "lanes_per_wave": lanes,
+                   "parallelism": f"trial-sharded x{world}, RCCL histogram all-reduce"},
+        # gem5-equivalent: each trial's numInst at its end, as a serial gem5
+        # run commits it (restored snapshot prefix and skipped golden suffix
+        # of early-masked trials included); device: instructions the GPU
+        # actually executed
+        "guest_inst_per_s_gem5_equiv": int(node_h["guest_insts"]) * steps / elapsed,
+        "device_inst_per_s": int(node_h["device_insts"]) * steps / elapsed,
+        "roofline": {"bound": "hbm", "achieved": D["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": D["frac"], "traffic": D["traffic"], "kernel": dom,
+                     "avg_kernel_ms": D["avg_kernel_ms"], "dispatches_per_step": D["dispatches_per_step"],
+                     "algorithmic_bytes_per_launch": D["algorithmic_bytes_per_launch"],
+                     # the roof that binds: issue slots (SQ counters of the same
+                     # command, profiles/; DESIGN.md §4)
+                     "issue": D["issue"], "per_kernel": per_kernel},
+        "outcomes": {n: int(cls[i]) for i, n in enumerate(["masked", "sdc", "crash", "hang", "detected", "escape"])},
+        "escape_sub": {ESCAPE_NAMES.get(i, str(i)): int(node_h["escape_sub"][i]) for i in range(8)
+                       if node_h["escape_sub"][i]},
+        "cold_start": cold,
+        "golden_s": golden_s,
+        "parity": None,
+        "cpu_baseline": None,
+    }
+    if world == 1 and not a.no_cpu_baseline:
+        rec["cpu_baseline"], ref = cpu_baseline(elf, name, a.seed, cpu_seconds, min_parity)
+        rec["cold_start"]["campaign_vs_cpu_baseline"] = cold["campaign_trials_per_s"] / rec["cpu_baseline"]["value"]
+        # the same trial ids through the device (the timed campaign's first
+        # trials): every outcome must equal the oracle's, bit for bit
+        dev_out, _ = eng.run_trials(0, len(ref))
+        rec["escapes_in_checked"] = escape_breakdown(dev_out)
+        rec["parity"] = {"checked": int(len(ref)), "mismatches": int((dev_out != ref).sum()),
+                         "against": "oracle/rv64se.c, trial ids [0, checked) of the benched campaign"}
+    eng.close()
+    return rec
 
 
 def main():
@@ -120,166 +293,36 @@ def main():
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from shrewd_amd import ESCAPE_NAMES, HIST_DT, Engine
-    from shrewd_amd.fi import escape_breakdown
-    with open(os.path.join(ROOT, "workloads", f"{a.workload}.elf"), "rb") as f:
-        elf = f.read()
-    eng = Engine(device=local, max_trials_per_launch=max(a.trials, 1024), lanes_per_wave=a.lanes,
-                 resume_lanes=a.resume_lanes, epoch_iters=a.epoch_iters,
-                 epochs=a.epochs)
-    lanes = eng.config()["lanes_per_wave"]
-    t0 = time.perf_counter()
-    eng.load_elf(elf, [a.workload])
-    g = eng.golden_run()
-    golden_s = time.perf_counter() - t0
-    eng.set_campaign(a.seed, REGS_PC, 1)
-
-    T = a.trials
-    d_out = torch.empty(T * 16, dtype=torch.uint8, device=dev)
-    hist_words = HIST_DT.itemsize // 8
-    d_hist = torch.zeros(hist_words, dtype=torch.int64, device=dev)
-    d_hist_node = torch.zeros_like(d_hist)
-    # one dedicated stream for engine kernels, histogram copies and RCCL
-    tstream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(tstream)
-    stream = tstream.cuda_stream
-
-    def step():
-        d_hist.zero_()
-        eng.run_trials_device(rank * T, T, d_out.data_ptr(), d_hist.data_ptr(), stream)
-        d_hist_node.copy_(d_hist)
-        if world > 1:
-            dist.all_reduce(d_hist_node)      # RCCL over xGMI: outcome histogram only
-
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    eng.kernel_timer_reset()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    local_h = np.frombuffer(d_hist.cpu().numpy().tobytes(), HIST_DT)[0]
-    node_h = np.frombuffer(d_hist_node.cpu().numpy().tobytes(), HIST_DT)[0]
-
+    head = run_workload(a, a.workload, a.trials, a.steps, a.warmup, rank, world, dev, a.cpu_seconds,
+                        a.parity_trials)
+    # the other C2 / C3 workloads on the same line (BASELINE.json configs[1], [2]):
+    # qsort 100k trials per GPU, intmix 125k per GPU (C3's 1M over 8 GPUs)
+    extra = {}
+    for spec in [w for w in a.workloads.split(",") if w]:
+        name, _, rest = spec.partition(":")
+        T, _, steps = rest.partition(":")
+        T, steps = int(T or a.trials), int(steps or a.steps)
+        if name == a.workload:
+            continue
+        extra[name] = run_workload(a, name, T, steps, 1, rank, world, dev, 2.0, a.extra_parity)
     if rank == 0:
-        trials_total = world * T * a.steps
-        value = trials_total / elapsed
-        guest_ips = int(node_h["guest_insts"]) * a.steps / elapsed
-        device_ips = int(node_h["device_insts"]) * a.steps / elapsed
-        # roofline per trial kernel, per launch:
-        # algorithmic bytes = fetched instruction bytes + load/store bytes of the
-        # guest instructions the kernel executed + 4096 B per copy-on-write page
-        # it made, and for the 64-lane kernel (every trial starts there) 264 B of
-        # initial state + 16 B of outcome per trial; counted on the device per
-        # kernel (DevCtx::stats[40..51]) over the last step -- every step runs
-        # the same trial ids, so the last step's counts are every step's.
-        # Duration = the mean of that kernel's dispatches (HIP events on its
-        # stream); the dominant kernel is the one with the most device time.
-        st = eng.debug_stats()
-        kinds, dms = eng.debug_dispatch_kinds(), eng.debug_dispatch_ms()
-        tx = eng.translate_status() == ""
-        names = (["fi_trial_kernel_tx", "fi_trial_kernel_tx_solo", "fi_trial_kernel_tx_solo_odd"] if tx
-                 else ["fi_trial_kernel", "fi_trial_kernel_solo", "fi_trial_kernel_solo_odd"])
-        tj = {}
-        if os.path.exists(a.traffic_json):
-            try:
-                with open(a.traffic_json) as f:
-                    tj = json.load(f)
-                if not (tj.get("workload") == a.workload and tj.get("trials") == T
-                        and tj.get("lanes_per_wave", 64) == lanes):
-                    tj = {}
-            except (OSError, ValueError):
-                tj = {}
-        per_kernel = {}
-        for k, name in enumerate(names):
-            ms_k = [m for m, kk in zip(dms, kinds) if kk == k]
-            if not ms_k:
-                continue
-            disp = len(ms_k) / a.steps
-            b = int(st[40 + 4 * k]) + int(st[41 + 4 * k]) + 4096 * int(st[42 + 4 * k]) + (T * (264 + 16) if k == 0 else 0)
-            avg_ms = sum(ms_k) / len(ms_k)
-            per_launch = b / disp
-            ach = per_launch / (avg_ms / 1e3) / 1e9
-            tk = tj.get("per_kernel", {}).get(name, {})
-            per_kernel[name] = {"avg_kernel_ms": avg_ms, "dispatches_per_step": disp,
-                                "ms_per_step": avg_ms * disp, "algorithmic_bytes_per_launch": per_launch,
-                                "achieved": ach, "frac": ach / HBM_PEAK_GBS,
-                                "device_insts_per_launch": int(st[43 + 4 * k]) / disp,
-                                "traffic": tk.get("hbm_bytes_per_launch"), "issue": tk.get("issue")}
-        dom = max(per_kernel, key=lambda n: per_kernel[n]["ms_per_step"])
-        D = per_kernel[dom]
-        cls = node_h["counts"].sum(axis=(0, 1))
         res = {
             "metric": "fault-injection trials/sec (whole node)",
-            "value": value,
+            "value": head["value"],
             "unit": "trials/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": elapsed / a.steps * 1e3,
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": "synthetic (seeded SplitMix64 fault sites over a hand-assembled RV64 ELF)",
-            "config": {"workload": f"{a.workload} (RV64 MiBench-style, {g.ninst} golden insts), "
-                                   f"{T} single-bit x1..x31+pc trials per GPU per step",
-                       "trials_per_gpu": T, "seed": hex(a.seed), "structures": "x1-x31,pc", "burst": 1,
-                       "lanes_per_wave": lanes,
-                       "parallelism": f"trial-sharded x{world}, RCCL histogram all-reduce"},
-            # gem5-equivalent: each trial's numInst at its end, as a serial gem5
-            # run commits it (restored snapshot prefix and skipped golden suffix
-            # of early-masked trials included); device: instructions the GPU
-            # actually executed
-            "guest_inst_per_s_gem5_equiv": guest_ips,
-            "device_inst_per_s": device_ips,
-            "roofline": {"bound": "hbm", "achieved": D["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": D["frac"], "traffic": D["traffic"], "kernel": dom,
-                         "avg_kernel_ms": D["avg_kernel_ms"], "dispatches_per_step": D["dispatches_per_step"],
-                         "algorithmic_bytes_per_launch": D["algorithmic_bytes_per_launch"],
-                         # the roof that binds: issue slots (SQ counters of the same
-                         # command, profiles/)
-                         "issue": D["issue"], "per_kernel": per_kernel},
-            "outcomes": {n: int(cls[i]) for i, n in enumerate(["masked", "sdc", "crash", "hang", "detected",
-                                                                 "escape"])},
-            "golden_s": golden_s,
         }
-        res["escape_sub"] = {ESCAPE_NAMES.get(i, str(i)): int(node_h["escape_sub"][i]) for i in range(8)
-                             if node_h["escape_sub"][i]}
-        res["parity"] = None
-        if world == 1 and not a.no_cpu_baseline:
-            res["cpu_baseline"], ref = cpu_baseline(elf, a.workload, a.seed, a.cpu_seconds)
-            if a.parity_trials > len(ref):   # more checked trials, untimed (not part of the baseline)
-                from oracle.pyoracle import Oracle
-                o = Oracle(elf, a.workload)
-                o.run_golden()
-                more = o.sample(a.seed, len(ref), a.parity_trials - len(ref), REGS_PC, 1)
-                ref = np.concatenate([ref, o.run_trials(more, threads=host_cores()[0])])
-                o.close()
-            # the same trial ids through the device (the timed campaign's first
-            # trials): every outcome must equal the oracle's, bit for bit
-            dev, _ = eng.run_trials(0, len(ref))
-            bad = int((dev != ref).sum())
-            res["escapes_in_checked"] = escape_breakdown(dev)
-            res["parity"] = {"checked": int(len(ref)), "mismatches": bad,
-                             "against": "oracle/rv64se.c, trial ids [0, checked) of the benched campaign"}
-        else:
-            res["cpu_baseline"] = None
+        res.update({k: v for k, v in head.items() if k not in ("value", "ms_per_step", "steps", "warmup")})
+        res["workloads"] = extra
         print(json.dumps(res), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

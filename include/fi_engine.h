@@ -168,6 +168,10 @@ typedef struct {
  * kernel, whose translated blocks also cover the odd-pc instruction streams,
  * on a second stream beside it) (A/B and parity checks; outcomes are identical) */
 #define FI_CFG_NO_ODD_KERNEL 4096u
+/* Build the translated kernels even when the code-object caches (in process
+ * and $SHREWD_FI_JIT_CACHE) hold them: cold-start measurements and tests of
+ * the background build. */
+#define FI_CFG_JIT_NO_CACHE 8192u
 
 typedef struct {
     uint64_t ninst, ncycles;
@@ -211,11 +215,22 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
  * memory (page table + physical memory store), brk point and stack VMA come
  * from cpt_dir/m5.cpt; the workload ELF gives the executable range for
  * pre-decode and translation.  numInst counts from the restore point (gem5
- * does not checkpoint statistics).  Supported: one CPU thread, no FP state,
- * the stack as the only VMA, the default mmap end; anything else is
- * FI_E_ARG with the reason in fi_last_error. */
+ * does not checkpoint statistics).  Restored besides: FP registers and fcsr,
+ * the whole VMA list, the mmap end and curTick.  Supported: one CPU thread and
+ * the process-start vector configuration; anything else is FI_E_ARG with the
+ * reason in fi_last_error. */
 fi_status fi_load_checkpoint(fi_engine *e, const char *cpt_dir, const uint8_t *elf, size_t len);
+/* The golden run (record mode on the device), then the golden snapshots and
+ * the translation of the golden basic blocks.  The translated kernels build
+ * in the background (hipRTC in parallel helper processes): until they land,
+ * trials run on the static kernels -- identical outcomes, bit for bit -- in
+ * chunks of at most 16,384 trials, and each chunk boundary picks the build
+ * up.  fi_translate_status() is "compiling" meanwhile. */
 fi_status fi_golden_run(fi_engine *e, fi_golden_info *out);
+/* Block until the background build has landed (or failed: see
+ * fi_translate_status) and return the golden info with translated_blocks,
+ * translated_insts and translate_us filled in. */
+fi_status fi_wait_translation(fi_engine *e, fi_golden_info *out);
 /* copies up to cap bytes of golden stdout; returns the full length in *len */
 fi_status fi_golden_stdout(fi_engine *e, uint8_t *buf, uint64_t cap, uint64_t *len);
 /* same for the golden run's stderr (fd 2) stream */
@@ -230,15 +245,32 @@ fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint
  * flipped bit may be b (for a burst of k bits, b <= 64 - k).  Default (and
  * ~0): every position, sampled as before.  Set after fi_set_campaign. */
 fi_status fi_set_bits(fi_engine *e, uint64_t bits_mask);
-/* SE time and randomness model: ticks (1 ps) per CPU cycle for clock_gettime
+/* The process settings below shape the golden run as much as the trials:
+ * set them after loading (or before it: they survive fi_load_elf /
+ * fi_load_checkpoint) and before fi_golden_run; once a golden run exists they
+ * return FI_E_STATE.
+ *
+ * SE time and randomness model: ticks (1 ps) per CPU cycle for clock_gettime
  * (curTick at a tick = (cycles so far - 1) x period; default 500 = 2 GHz) and
  * gem5's Random global seed for getrandom (default 5489, base/random.cc:79). */
 fi_status fi_set_clock(fi_engine *e, uint64_t period_ticks, uint64_t random_seed);
 /* The realpath of the workload executable, what gem5's readlinkat on
  * "/proc/self/exe" answers (realpath(Process::progName()),
  * src/sim/syscall_emul.hh:1089-1111); NULL / "" (default): that call ends the
- * trial as escape/host.  FaultCampaign sets it from the workload path. */
+ * trial as escape/host.  FaultCampaign sets it from `executable` (gem5's
+ * Process.executable, default cmd[0]) resolved against the host working
+ * directory. */
 fi_status fi_set_exe_path(fi_engine *e, const char *path);
+/* Process.input (src/sim/Process.py:44): data = the bytes of the input file
+ * fd 0 reads (FDArray opens it O_RDONLY, src/sim/fd_array.cc:69-75; readFunc,
+ * src/sim/syscall_emul.hh:2798-2822, takes min(n, left) bytes at the file
+ * offset and copies n zero-padded bytes out; write/writev to fd 0 return
+ * -EBADF).  Every trial starts at the golden run's offset at its start
+ * snapshot; a checkpoint restart reads from offset 0, as gem5 reopens the
+ * file without restoring fd 0-2 (fd_array.cc:371-380).  data = NULL (the
+ * default, "cin"): fd 0 is the host's stdin and a trial that reads it ends
+ * as escape/host. */
+fi_status fi_set_stdin(fi_engine *e, const uint8_t *data, uint64_t len);
 /* selective-replication mask over x0..x31 (bits 0..31) and pc (bit 32) */
 fi_status fi_set_protect(fi_engine *e, uint64_t protect_mask);
 /* SHREWD selective replication by instruction class (the reference's

@@ -113,6 +113,7 @@ def lib():
         L.or_set_protect_opclasses.argtypes = [C.c_void_p, C.c_uint64]
         L.or_set_clock.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
         L.or_set_exe_path.argtypes = [C.c_void_p, C.c_char_p]
+        L.or_set_stdin.argtypes = [C.c_void_p, C.c_char_p, C.c_uint64]
         L.or_issue_model.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(IssueParams), C.c_void_p,
                                      C.POINTER(IssueStats)]
         L.or_set_issue_model.argtypes = [C.c_void_p, C.POINTER(IssueParams)]
@@ -218,6 +219,11 @@ class Oracle:
     def set_exe_path(self, path: str):
         """What readlinkat("/proc/self/exe") answers (realpath of the executable)."""
         self.L.or_set_exe_path(self.h, path.encode())
+
+    def set_stdin(self, data: bytes | None):
+        """Process.input: the bytes of the input file (None = "cin", host stdin)."""
+        if self.L.or_set_stdin(self.h, data, 0 if data is None else len(data)) != 0:
+            raise MemoryError("or_set_stdin")
 
     def set_clock(self, period_ticks=500, random_seed=5489):
         self.L.or_set_clock(self.h, period_ticks, random_seed)

@@ -211,6 +211,8 @@ struct or_campaign {
     int nseg;
     u64 clk_period;        /* ticks per CPU cycle (1 ps ticks; 500 = 2 GHz) */
     char exe_path[4096];   /* realpath of the process' executable ("" unknown): readlinkat /proc/self/exe */
+    uint8_t *in_data;      /* Process.input as a file: its bytes (NULL: "cin", the host's stdin) */
+    u64 in_len;
     u64 rnd_seed;          /* gem5 Random::globalSeed (base/random.cc:79) */
     u64 *mem_pages;        /* writable pages at process start (memory fault candidates) */
     u64 n_mem_pages;
@@ -261,6 +263,7 @@ typedef struct {
      * process, created at the first call from the global seed) */
     u64 *mt; int mt_i;
     u64 rnd_pos;          /* bytes drawn (the engine's table holds OR_RND_CAP) */
+    u64 in_pos;           /* fd 0's file offset (Process.input a file); a checkpoint restart starts at 0 */
     u64 protect_mask;
     /* termination */
     int done; or_outcome_t res;
@@ -1247,7 +1250,7 @@ static void sys_writev(mach_t *m) {
     const u64 iov = m->x[11], cnt = m->x[12];
     if (fd < 0 || fd >= 1024) { finish(m, OR_CRASH, OR_CRASH_FD_ASSERT, 134); return; }   /* fd_array.cc:322 */
     if (fd > 2 || ((m->fdc >> fd) & 1)) { m->x[10] = (u64)(s64)-EBADF_; return; }
-    if (fd == 0) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }             /* host stdin */
+    if (fd == 0 && !m->c->in_data) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* host stdin */
     if (cnt > (1u << 20)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }    /* host allocation */
     u64 total = 0;
     for (u64 i = 0; i < cnt; i++) {
@@ -1262,6 +1265,8 @@ static void sys_writev(mach_t *m) {
         if (!proxy_readable(m, base, len)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
         total += len;
     }
+    /* the input file (O_RDONLY): host writev fails with EBADF before it looks at IOV_MAX */
+    if (fd == 0) { m->x[10] = (u64)(s64)-EBADF_; return; }
     if (cnt > 1024) { m->x[10] = (u64)(s64)-EINVAL_; return; }   /* host writev: IOV_MAX */
     if (total > (1ULL << 31)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }
     bytes_t *dst = fd == 1 ? &m->out : &m->err;
@@ -1610,7 +1615,24 @@ static void do_syscall(mach_t *m) {
         int fd = (int)(s32)(u32)m->x[10];
         if (fd < 0 || fd >= 1024) { finish(m, OR_CRASH, OR_CRASH_FD_ASSERT, 134); return; }
         if (fd > 2 || ((m->fdc >> fd) & 1)) { m->x[10] = (u64)(s64)-EBADF_; return; }
-        finish(m, OR_ESCAPE, OR_ESC_HOST, 0);
+        if (fd != 0 || !m->c->in_data) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* host stdin/stdout */
+        /* Process.input is a file (fd_array.cc:69-75): poll() on a regular
+         * file is ready (no retry); read() takes min(n, left) bytes at the
+         * file offset; BufferArg (zero-filled, syscall_emul_buf.hh:55-85)
+         * copies all n bytes out when the read returned any */
+        const u64 buf = m->x[11], n = m->x[12];
+        if (n > (1ULL << 31)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* host buffer */
+        const u64 left = m->c->in_len - m->in_pos, k = n < left ? n : left;
+        if (k) {
+            const int h = proxy_writable(m, buf, n);
+            if (h == 0) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+            if (h < 0) { finish(m, OR_CRASH, OR_CRASH_STACK_LIMIT, 1); return; }
+            proxy_write(m, buf, m->c->in_data + m->in_pos, k);
+            static const uint8_t zero[256];
+            for (u64 i = k; i < n; i += sizeof zero) proxy_write(m, buf + i, zero, n - i < sizeof zero ? n - i : sizeof zero);
+        }
+        m->in_pos += k;
+        m->x[10] = k;
         return;
     }
     case 78: sys_readlinkat(m); return;
@@ -1620,7 +1642,7 @@ static void do_syscall(mach_t *m) {
         u64 buf = m->x[11], n = m->x[12];
         if (fd < 0 || fd >= 1024) { finish(m, OR_CRASH, OR_CRASH_FD_ASSERT, 134); return; }  /* fd_array.cc:322 */
         if (fd > 2 || ((m->fdc >> fd) & 1)) { m->x[10] = (u64)(s64)-9; return; }   /* no entry: -EBADF */
-        if (fd == 0) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* host stdin poll/write */
+        if (fd == 0 && !m->c->in_data) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* host stdin poll/write */
         if (n > (1ULL << 31)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; } /* host allocation */
         /* BufferArg::copyIn -> readBlob: fatal if any byte is unmapped (no fixup on reads) */
         if (n) {
@@ -1629,6 +1651,9 @@ static void do_syscall(mach_t *m) {
             for (u64 v = buf >> 12; v <= (last >> 12); v++)
                 if (!pm_find(&m->mem, v)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
         }
+        /* fd 0 is the input file, opened O_RDONLY (fd_array.cc:69-75): the
+         * host write() fails with EBADF (a regular file polls writable) */
+        if (fd == 0) { m->x[10] = (u64)(s64)-EBADF_; return; }
         bytes_t *dst = fd == 1 ? &m->out : &m->err;
         for (u64 i = 0; i < n; i++) {
             uint8_t *pg = translate(m, buf + i);
@@ -2826,7 +2851,7 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
 void or_destroy(or_campaign_t *c) {
     if (!c) return;
     pm_free(&c->image);
-    free(c->mem_pages); free(c->gout.buf); free(c->gerr.buf); free(c->shadow);
+    free(c->mem_pages); free(c->gout.buf); free(c->gerr.buf); free(c->shadow); free(c->in_data);
     free(c);
 }
 
@@ -3017,6 +3042,16 @@ static void *worker(void *arg) {
 void or_set_protect_opclasses(or_campaign_t *c, u64 mask) { c->protect_opc = mask; }
 void or_set_exe_path(or_campaign_t *c, const char *path) {
     snprintf(c->exe_path, sizeof c->exe_path, "%s", path ? path : "");
+}
+int or_set_stdin(or_campaign_t *c, const uint8_t *data, u64 len) {
+    free(c->in_data);
+    c->in_data = NULL; c->in_len = 0;
+    if (!data) return 0;
+    c->in_data = (uint8_t *)malloc(len ? len : 1);
+    if (!c->in_data) return -1;
+    memcpy(c->in_data, data, len);
+    c->in_len = len;
+    return 0;
 }
 void or_set_clock(or_campaign_t *c, u64 period_ticks, u64 random_seed) {
     c->clk_period = period_ticks;

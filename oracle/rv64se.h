@@ -141,6 +141,10 @@ uint64_t or_shadow_map(or_campaign_t *c, uint8_t *buf, uint64_t cap, or_issue_st
 /* realpath of the executable, what readlinkat("/proc/self/exe") answers
  * (syscall_emul.hh:1089-1111); "" (default): that call escapes as host */
 void or_set_exe_path(or_campaign_t *c, const char *path);
+/* Process.input (src/sim/Process.py:44): data = the input file's bytes, read
+ * by read(0) from offset 0 (syscall_emul.hh:2798-2822); NULL (default) =
+ * "cin", the host's stdin (reads of fd 0 escape as host).  Returns 0 / -1. */
+int or_set_stdin(or_campaign_t *c, const uint8_t *data, uint64_t len);
 /* SE time and randomness: ticks per CPU cycle (clock_gettime; default 500 =
  * 2 GHz) and gem5's Random global seed (getrandom; default 5489) */
 void or_set_clock(or_campaign_t *c, uint64_t period_ticks, uint64_t random_seed);

@@ -10,7 +10,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -57,8 +62,10 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                              const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
                              uint32_t &n_insts, bool odd_streams);
 std::vector<fi_issue_op> issue_ops_from_trace(const std::vector<PreInst> &pre, const std::vector<uint32_t> &trace);
-std::string jit_compile(const std::string &body, const char *arch, std::vector<char> &code, bool &cached);
+std::string jit_compile(const std::string &body, const char *arch, std::vector<char> &code, bool &cached, int part,
+                        bool use_cache);
 bool jit_has_odd(const std::string &body);
+bool jit_parallel_ok();
 hipError_t sort_pairs(void *tmp, size_t bytes, const uint64_t *kin, uint64_t *kout, const uint32_t *vin,
                       uint32_t *vout, uint64_t n, int end_bit, hipStream_t st);
 }  // namespace fi
@@ -68,6 +75,50 @@ using namespace fi;
 // trials per wave when fi_config.lanes_per_wave is 0
 static constexpr uint32_t kDefaultLanes = 64;
 static constexpr uint32_t kDefaultResumeLanes = 8;   // measured: profiles/README.md (r01b sweep)
+// trials per launch while the translated kernels are still being built: the
+// static kernels run small chunks so the campaign picks the build up soon
+static constexpr uint64_t kJitWindowChunk = 16384;
+
+// The background build of the translated kernels (fi_golden_run starts it;
+// run_chunk installs the result at a chunk boundary): the 64-lane, solo and,
+// with odd-pc streams, solo-odd kernels as one code object each, compiled in
+// parallel processes (fi_jit.cpp).  Until it lands the static kernels run
+// every trial -- the same outcomes, bit for bit, more slowly.
+struct JitJob {
+    std::string body, arch;
+    bool odd = false;
+    bool use_cache = true;   // FI_CFG_JIT_NO_CACHE: always compile (cold-start measurements, tests)
+    std::vector<char> code[3];
+    std::string err;
+    bool cached = true;
+    uint64_t us = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+};
+static const char *const kTxKernel[3] = {"fi_trial_kernel_tx", "fi_trial_kernel_tx_solo",
+                                         "fi_trial_kernel_tx_solo_odd"};
+
+static void jit_job_run(std::shared_ptr<JitJob> j) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int np = j->odd ? 3 : 2;
+    std::string err[3];
+    bool cached[3] = {true, true, true};
+    if (jit_parallel_ok()) {
+        std::vector<std::thread> th;
+        for (int k = 0; k < np; k++)
+            th.emplace_back([&, k] { err[k] = jit_compile(j->body, j->arch.c_str(), j->code[k], cached[k], k + 1, j->use_cache); });
+        for (auto &t : th) t.join();
+    } else {   // in-process hipRTC: one build at a time
+        for (int k = 0; k < np; k++) err[k] = jit_compile(j->body, j->arch.c_str(), j->code[k], cached[k], k + 1, j->use_cache);
+    }
+    std::lock_guard<std::mutex> lk(j->mu);
+    for (int k = 0; k < np && j->err.empty(); k++) j->err = err[k];
+    j->cached = cached[0] && cached[1] && cached[2];
+    j->us = (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    j->done = true;
+    j->cv.notify_all();
+}
 
 struct fi_engine {
     fi_config cfg{};
@@ -123,7 +174,10 @@ struct fi_engine {
     uint32_t *d_mw_off = nullptr;
     bool pre_ok = true;
     // load-time build of the trial kernel with the translated golden blocks
-    hipModule_t tx_mod = nullptr;
+    hipModule_t tx_mod[3] = {nullptr, nullptr, nullptr};
+    std::shared_ptr<JitJob> jit;     // the build in flight (nullptr: none)
+    std::vector<PreInst> jit_pre;    // golden pre-decoded text with the leader flags, uploaded when it lands
+    uint64_t jit_blocks = 0, jit_insts = 0;
     hipFunction_t tx_fn = nullptr, tx_fn_solo = nullptr;
     hipFunction_t tx_fn_odd = nullptr;   // solo kernel with the odd-pc blocks (nullptr: none translated)
     // the solo-odd kernel runs beside the solo kernel on its own stream
@@ -147,6 +201,10 @@ struct fi_engine {
     uint8_t *d_rnd = nullptr;   // getrandom's byte stream (kRndLen bytes)
     std::string exe_path;       // fi_set_exe_path
     uint8_t *d_exe = nullptr;
+    bool stdin_on = false;      // fi_set_stdin: Process.input is a file (else "cin")
+    std::vector<uint8_t> stdin_data;
+    uint8_t *d_stdin = nullptr;
+    uint64_t *d_inpos = nullptr;   // per work slot: fd 0's file offset
     uint64_t protect = 0;
     uint64_t protect_opc = 0;   // SHREWD replication by OpClass (fi_set_protect_opclasses)
     // SHREWD FU contention (fi_set_issue_model): shadow issued per golden numInst index
@@ -301,6 +359,7 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
 static void free_work(fi_engine *e) {
     dfree(e->d_sites); dfree(e->d_keys); dfree(e->d_keys2); dfree(e->d_perm); dfree(e->d_perm2);
     dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg); dfree(e->d_fregs);
+    dfree(e->d_inpos);
     dfree(e->d_save); dfree(e->d_surv[0]); dfree(e->d_surv[1]); dfree(e->d_cnt);
     dfree(e->d_eff);
     dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_wrange); dfree(e->d_nwaves); dfree(e->d_split); dfree(e->d_dmap); dfree(e->d_priv); dfree(e->d_priv_vpn); dfree(e->d_vm);
@@ -318,13 +377,53 @@ static void free_fw(fi_engine *e) {
     e->fw_ok = false;
 }
 static void free_tx(fi_engine *e) {
-    if (e->tx_mod) (void)hipModuleUnload(e->tx_mod);
-    e->tx_mod = nullptr;
+    for (auto &m : e->tx_mod) {
+        if (m) (void)hipModuleUnload(m);
+        m = nullptr;
+    }
     e->tx_fn = e->tx_fn_solo = e->tx_fn_odd = nullptr;
+    e->jit.reset();   // a build in flight finishes on its own (its thread holds the job)
+}
+
+// Install a finished background build (at a chunk boundary, before anything
+// of the chunk is queued on st): load the code objects and flag the block
+// leaders in the pre-decoded text.  wait = block until the build is done.
+static void jit_install(fi_engine *e, hipStream_t st, bool wait) {
+    std::shared_ptr<JitJob> j = e->jit;
+    if (!j) return;
+    {
+        std::unique_lock<std::mutex> lk(j->mu);
+        if (wait) j->cv.wait(lk, [&] { return j->done; });
+        if (!j->done) return;
+    }
+    e->jit.reset();
+    if (!j->err.empty()) {
+        e->tx_status = j->err;
+        return;
+    }
+    hipFunction_t *fn[3] = {&e->tx_fn, &e->tx_fn_solo, &e->tx_fn_odd};
+    for (int k = 0; k < (j->odd ? 3 : 2); k++) {
+        if (hipModuleLoadData(&e->tx_mod[k], j->code[k].data()) != hipSuccess ||
+            hipModuleGetFunction(fn[k], e->tx_mod[k], kTxKernel[k]) != hipSuccess) {
+            free_tx(e);
+            e->tx_status = "code object did not load";
+            return;
+        }
+    }
+    if (hipMemcpyAsync(e->d_pre, e->jit_pre.data(), e->jit_pre.size() * sizeof(PreInst), hipMemcpyHostToDevice, st) !=
+        hipSuccess) {
+        free_tx(e);
+        e->tx_status = "pre-decoded text upload failed";
+        return;
+    }
+    e->tx_status = "";
+    e->golden.translated_blocks = e->jit_blocks;
+    e->golden.translated_insts = e->jit_insts;
+    e->golden.translate_us = j->cached ? 0 : j->us;
 }
 static void free_image(fi_engine *e) {
     dfree(e->d_pre); dfree(e->d_zero); dfree(e->d_sink);
-    dfree(e->d_text); dfree(e->d_mem_pages); dfree(e->d_gout); dfree(e->d_gerr); dfree(e->d_exe);
+    dfree(e->d_text); dfree(e->d_mem_pages); dfree(e->d_gout); dfree(e->d_gerr);
     dfree(e->d_fp0); dfree(e->d_vm0);
     e->fp0_on = e->vm0_on = false;
     e->tick0 = 0;
@@ -343,7 +442,7 @@ void fi_destroy(fi_engine *e) {
     (void)hipSetDevice(e->dev);
     free_work(e);
     free_image(e);
-    dfree(e->d_rnd);
+    dfree(e->d_rnd); dfree(e->d_exe); dfree(e->d_stdin);
     for (auto &tp : e->tpool) { (void)hipEventDestroy(tp.first); (void)hipEventDestroy(tp.second); }
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -685,6 +784,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_save, c * sizeof(LaneSave)));
     HIPCHK(hipMalloc(&e->d_vm, c * sizeof(VmState)));
     HIPCHK(hipMalloc(&e->d_fregs, c * 32 * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&e->d_inpos, c * sizeof(uint64_t)));
     HIPCHK(hipMalloc(&e->d_surv[0], c * 4));
     HIPCHK(hipMalloc(&e->d_surv[1], c * 4));
     HIPCHK(hipMalloc(&e->d_cnt, 16 * 4));
@@ -748,6 +848,9 @@ static DevCtx base_ctx(fi_engine *e) {
     c.exe_path = e->d_exe; c.exe_len = e->d_exe ? e->exe_path.size() : 0;
     c.tick0 = e->tick0;
     c.clk_until = e->clk_until;
+    c.stdin_data = e->stdin_on ? e->d_stdin : nullptr;
+    c.stdin_len = e->stdin_on ? e->stdin_data.size() : 0;
+    c.in_pos = e->d_inpos;
     c.fp0 = e->fp0_on ? e->d_fp0 : nullptr;
     c.fcsr0 = e->fcsr0;
     c.vm0 = e->vm0_on ? e->d_vm0 : nullptr;
@@ -770,9 +873,10 @@ static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_
     HIPCHK(hipMalloc(&d_gpriv, (uint64_t)P * kPage));
     HIPCHK(hipMalloc(&d_gvpn, (uint64_t)P * 8));
     uint64_t *d_gfregs = nullptr;
-    HIPCHK(hipMalloc(&d_gfregs, 32 * sizeof(uint64_t)));
+    HIPCHK(hipMalloc(&d_gfregs, 33 * sizeof(uint64_t)));   // 32 FP registers + fd 0's offset
     DevCtx c = base_ctx(e);
     c.fregs = d_gfregs;
+    c.in_pos = d_gfregs + 32;
     c.dmap = nullptr;
     c.record = 1;
     c.early_exit = 0;
@@ -1086,7 +1190,6 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     else if (!e->pre_ok) e->tx_status = "golden run rewrites its text";
     else if (!live_ok || trace.empty()) e->tx_status = "golden trace unavailable";
     else {
-        const auto t0 = std::chrono::steady_clock::now();
         // (snapshot pcs are not leaders: they fall all over the hot loops and
         // would cut the blocks into single instructions; a wave that starts
         // mid-block steps to the next leader in the interpreter)
@@ -1104,36 +1207,23 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         if (const char *dump = getenv("SHREWD_FI_DUMP_TX")) {   // diagnostics: the generated blocks
             if (FILE *f = fopen(dump, "w")) { fputs(body.c_str(), f); fclose(f); }
         }
-        const bool trace_jit = getenv("SHREWD_FI_TRACE") != nullptr;
-#define JTRACE(...) do { if (trace_jit) { fprintf(stderr, "[fi jit] " __VA_ARGS__); fflush(stderr); } } while (0)
-        JTRACE("compile (%zu bytes of blocks)\n", body.size());
-        std::vector<char> code;
-        bool cached = false;
-        // nothing hot, or more than the load-time compiler handles in reasonable time:
-        // the static kernels (pre-decoded + general interpreter) run everything
-        const std::string err = leaders.empty() ? std::string("nothing to translate (no code run twice)")
-                              : n_tx > 24000 ? std::string("translation too large")
-                                             : jit_compile(body, prop.gcnArchName, code, cached);
-        JTRACE("load module (err=%s, %zu bytes)\n", err.c_str(), code.size());
-        if (!err.empty()) {
-            e->tx_status = err;
-        } else if (hipModuleLoadData(&e->tx_mod, code.data()) != hipSuccess ||
-                   hipModuleGetFunction(&e->tx_fn, e->tx_mod, "fi_trial_kernel_tx") != hipSuccess ||
-                   hipModuleGetFunction(&e->tx_fn_solo, e->tx_mod, "fi_trial_kernel_tx_solo") != hipSuccess ||
-                   (jit_has_odd(body) &&
-                    hipModuleGetFunction(&e->tx_fn_odd, e->tx_mod, "fi_trial_kernel_tx_solo_odd") != hipSuccess)) {
-            free_tx(e);
-            e->tx_status = "code object did not load";
+        if (leaders.empty()) {   // nothing hot: the static kernels (pre-decoded + general interpreter) run everything
+            e->tx_status = "nothing to translate (no code run twice)";
+        } else if (n_tx > 24000) {   // more than the load-time compiler handles in reasonable time
+            e->tx_status = "translation too large";
         } else {
-            JTRACE("loaded\n");
-#undef JTRACE
+            auto j = std::make_shared<JitJob>();
+            j->body = body;
+            j->arch = prop.gcnArchName;
+            j->odd = jit_has_odd(body);
+            j->use_cache = !(e->cfg.flags & FI_CFG_JIT_NO_CACHE);
             for (uint32_t h : leaders) pre[h & 0x7FFFFFFFu].flags |= (h >> 31) ? kPreOddLeader : kPreLeader;
-            HIPCHK(hipMemcpy(e->d_pre, pre.data(), pre.size() * sizeof(PreInst), hipMemcpyHostToDevice));
-            e->tx_status = "";
-            e->golden.translated_blocks = leaders.size();
-            e->golden.translated_insts = n_tx;
-            e->golden.translate_us = cached ? 0 : (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
-                                                          std::chrono::steady_clock::now() - t0).count();
+            e->jit_pre = std::move(pre);
+            e->jit_blocks = leaders.size();
+            e->jit_insts = n_tx;
+            e->jit = j;
+            e->tx_status = "compiling";
+            std::thread(jit_job_run, j).detach();
         }
     }
     e->last_ms = golden_ms;
@@ -1176,6 +1266,7 @@ fi_status fi_set_campaign(fi_engine *e, uint64_t seed, uint64_t structures, uint
 
 fi_status fi_set_exe_path(fi_engine *e, const char *path) {
     if (!e) return FI_E_ARG;
+    if (e->have_golden) return fail(e, FI_E_STATE, "fi_set_exe_path: set before fi_golden_run (the golden run sees it)");
     HIPCHK(hipSetDevice(e->dev));
     e->exe_path = path ? path : "";
     if (e->exe_path.size() >= 4096) { e->exe_path.clear(); return FI_E_ARG; }   // PATH_MAX
@@ -1187,8 +1278,24 @@ fi_status fi_set_exe_path(fi_engine *e, const char *path) {
     return FI_OK;
 }
 
+fi_status fi_set_stdin(fi_engine *e, const uint8_t *data, uint64_t len) {
+    if (!e) return FI_E_ARG;
+    if (e->have_golden) return fail(e, FI_E_STATE, "fi_set_stdin: set before fi_golden_run (the golden run reads it)");
+    if (data && len >= (1ULL << 40)) return fail(e, FI_E_ARG, "fi_set_stdin: input larger than 1 TiB");
+    HIPCHK(hipSetDevice(e->dev));
+    dfree(e->d_stdin);
+    e->stdin_data.clear();
+    e->stdin_on = data != nullptr;
+    if (!data) return FI_OK;
+    e->stdin_data.assign(data, data + len);
+    HIPCHK(hipMalloc(&e->d_stdin, std::max<uint64_t>(len, 1)));
+    if (len) HIPCHK(hipMemcpy(e->d_stdin, data, len, hipMemcpyHostToDevice));
+    return FI_OK;
+}
+
 fi_status fi_set_clock(fi_engine *e, uint64_t period_ticks, uint64_t random_seed) {
     if (!e || !period_ticks) return FI_E_ARG;
+    if (e->have_golden) return fail(e, FI_E_STATE, "fi_set_clock: set before fi_golden_run (the golden run sees it)");
     HIPCHK(hipSetDevice(e->dev));
     e->clk_period = period_ticks;
     e->rnd_seed = random_seed;
@@ -1425,6 +1532,7 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
 // count; FI_CFG_NO_REDO skips it.
 static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histogram *d_hist, hipStream_t st) {
     const uint32_t P = e->cfg.private_pages;
+    jit_install(e, st, false);   // the translated kernels, once their build has landed
     HIPCHK(hipMemsetAsync(e->d_stats, 0, kNStats * sizeof(unsigned long long), st));
     HIPCHK(hipEventRecord(e->ev0, st));
     fi_status s = run_pass(e, e->d_sites, k, d_out, P, st);
@@ -1480,7 +1588,8 @@ static fi_status run_common(fi_engine *e, uint64_t first, const fi_site *sites, 
     HIPCHK(hipMemsetAsync(e->d_hist, 0, sizeof(fi_histogram), e->stream));
     double ms = 0;
     for (uint64_t done = 0; done < n;) {
-        const uint64_t k = std::min<uint64_t>(n - done, e->cap);
+        jit_install(e, e->stream, false);
+        const uint64_t k = std::min<uint64_t>({n - done, e->cap, e->jit ? kJitWindowChunk : e->cap});
         if (sites) {
             HIPCHK(hipMemcpyAsync(e->d_sites, sites + done, k * sizeof(fi_site), hipMemcpyHostToDevice, e->stream));
             HIPCHK(launch_keys(e->d_sites, k, e->d_keys, e->d_perm, e->stream));
@@ -1503,6 +1612,16 @@ static fi_status run_common(fi_engine *e, uint64_t first, const fi_site *sites, 
     return FI_OK;
 }
 
+fi_status fi_wait_translation(fi_engine *e, fi_golden_info *out) {
+    if (!e) return FI_E_ARG;
+    if (!e->have_golden) return fail(e, FI_E_STATE, "no golden run");
+    HIPCHK(hipSetDevice(e->dev));
+    jit_install(e, e->stream, true);
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (out) *out = e->golden;
+    return FI_OK;
+}
+
 fi_status fi_run_trials(fi_engine *e, uint64_t first, uint64_t n, fi_outcome *out, fi_histogram *hist) {
     return run_common(e, first, nullptr, n, out, hist);
 }
@@ -1522,7 +1641,8 @@ fi_status fi_run_trials_device(fi_engine *e, uint64_t first, uint64_t n, void *d
     fi_status s = ensure_work(e, std::min<uint64_t>(std::max<uint64_t>(n, 1), chunk));
     if (s) return s;
     for (uint64_t done = 0; done < n;) {
-        const uint64_t k = std::min<uint64_t>(n - done, e->cap);
+        jit_install(e, st, false);
+        const uint64_t k = std::min<uint64_t>({n - done, e->cap, e->jit ? kJitWindowChunk : e->cap});
         HIPCHK(launch_sample(sample_ctx(e, first + done), k, e->d_sites, e->d_keys, e->d_perm, st));
         s = run_chunk(e, k, (fi_outcome *)d_out + done, (fi_histogram *)d_hist, st);
         if (s) return s;
@@ -1550,7 +1670,7 @@ fi_status fi_debug_jit_compile(const char *body, const char *arch, void *code, u
                                char *err, uint64_t err_cap) {
     std::vector<char> co;
     bool cached = false;
-    const std::string msg = jit_compile(body ? body : "", arch ? arch : "gfx950", co, cached);
+    const std::string msg = jit_compile(body ? body : "", arch ? arch : "gfx950", co, cached, 0, true);
     if (err && err_cap) {
         const uint64_t n = std::min<uint64_t>(err_cap - 1, msg.size());
         memcpy(err, msg.data(), n);

@@ -49,8 +49,9 @@ struct SnapState {
     uint32_t tab_off, tab_n;         // entries [tab_off, tab_off + tab_n) of DevCtx::snap_tab
     uint32_t live;                   // x_r whose value here the golden future reads before writing
     uint32_t trace_pos;              // record mode: golden trace events before this snapshot
+    uint64_t in_pos;                 // fd 0's file offset (Process.input a file; DevCtx::stdin_data)
 };
-static_assert(sizeof(SnapState) == 320, "SnapState layout");
+static_assert(sizeof(SnapState) == 328, "SnapState layout");
 // One mapped guest page of a snapshot: vpn -> frame in the snapshot pool.
 struct PageEnt {
     uint64_t vpn;
@@ -196,6 +197,9 @@ struct DevCtx {
     uint64_t exe_len;                // 0: unknown (that call escapes as host)
     uint64_t clk_period;             // ticks per CPU cycle (clock_gettime)
     uint64_t tick0;                  // curTick at the campaign start (a checkpoint's [Globals] curTick; else 0)
+    const uint8_t *stdin_data;       // Process.input as a file: its bytes (NULL: "cin", reads of fd 0 escape)
+    uint64_t stdin_len;
+    uint64_t *in_pos;                // per slot: fd 0's file offset (used only with stdin_data)
     uint64_t clk_until;              // the golden run reads curTick (clock_gettime, rpns) at numInst < clk_until:
                                      // before that a trial equals a snapshot only with the same ncyc (0 = never)
     const uint64_t *fp0;             // a checkpoint's FP registers (NULL: none -- zero, no FP state)

@@ -1100,7 +1100,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         const int fd = (int)(uint32_t)a0;
         if (fd < 0 || fd >= 1024) { finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, pc32); return false; }
         if (fd > 2 || ((fdc >> fd) & 1)) { set_ret(-9); return false; }
-        if (fd == 0 || a2 > (1u << 20)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+        if ((fd == 0 && !c->stdin_data) || a2 > (1u << 20)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
         uint64_t total = 0;
         for (uint64_t i = 0; i < a2; i++) {
             const uint64_t e = a1 + 16 * i;
@@ -1110,6 +1110,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
             if (!proxy_readable(c, w, m, slot, base, n)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
             total += n;
         }
+        if (fd == 0) { set_ret(-9); return false; }       // the input file (O_RDONLY): EBADF before IOV_MAX
         if (a2 > 1024) { set_ret(-22); return false; }   // host writev: IOV_MAX
         if (total > (1ULL << 31)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
         for (uint64_t i = 0; i < a2; i++) {
@@ -1124,8 +1125,28 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         const int fd = (int)(uint32_t)a0;
         if (fd < 0 || fd >= 1024) { finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, pc32); return false; }
         if (fd > 2 || ((fdc >> fd) & 1)) { set_ret(-9); return false; }
-        finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32);
-        return false;
+        if (fd != 0 || !c->stdin_data) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+        // Process.input is a file (fd_array.cc:69-75): poll() on a regular file
+        // is ready; read() takes min(n, left) bytes at the file offset, and the
+        // zero-filled BufferArg (syscall_emul_buf.hh:55-85) copies all n bytes
+        // out when the read returned any
+        if (a2 > (1ULL << 31)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+        uint64_t &pos = c->in_pos[slot];
+        const uint64_t left = c->stdin_len - pos, k = a2 < left ? a2 : left;
+        if (k) {
+            const int h = proxy_writable(c, w, m, slot, a1, a2);
+            if (h == 0) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
+            if (h == -1) { finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, pc32); return false; }
+            if (h == -2) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            if (!pwrite(a1, (const char *)(c->stdin_data + pos), k)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            const char zero[16] = {};
+            for (uint64_t i = k; i < a2; i += 16) {
+                if (!pwrite(a1 + i, zero, a2 - i < 16 ? a2 - i : 16)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            }
+        }
+        pos += k;
+        set_ret((int64_t)k);
+        return k && a1 < c->code_hi && a1 + a2 > c->code_lo;
     }
     case 78: {   // readlinkatFunc (syscall_emul.hh:1066-1129; oracle/rv64se.c sys_readlinkat)
         const int dirfd = (int)(uint32_t)a0;
@@ -1266,12 +1287,17 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
     const uint64_t buf = a1, n = a2;
     if (fd < 0 || fd >= 1024) { finish(L, FI_CRASH, FI_CRASH_FD_ASSERT, 134, pc32); return false; }
     if (fd > 2 || ((fdc >> fd) & 1)) { set_ret(-9); return false; }   // no fd entry: -EBADF
-    if (fd == 0) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
+    if (fd == 0 && !c->stdin_data) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
     if (n > (1ULL << 31)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
     if (n) {
         if (!proxy_readable(c, w, m, slot, buf, n)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
-        emit(fd, buf, n);
+        if (fd == 0) {   // the input file, opened O_RDONLY (fd_array.cc:69-75): host write() -> EBADF
+            if (c->record) rec_mem(c, buf, n, L.ninst, 1u);
+        } else {
+            emit(fd, buf, n);
+        }
     }
+    if (fd == 0) { set_ret(-9); return false; }
     RREG(10) = n;
     return false;
 }
@@ -2048,6 +2074,7 @@ __device__ __forceinline__ void trial_body() {
         if (m.dl && m.code_dirty)
             for (uint32_t i = 0; i < CX->dmap_words; i++) m.dl[i] = CX->dmap[slot * CX->dmap_words + i];
     }
+    if (CX->stdin_data && live && !resume) CX->in_pos[slot] = S0->in_pos;
     if (fw_dead && !resume) {   // dead at injection: the trial is the golden run
         L.injected = 1;
         finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
@@ -2236,7 +2263,8 @@ __device__ __forceinline__ void trial_body() {
                           // the golden suffix reads curTick: the same future needs the same tick count
                           // too (a path with other non-counting ticks -- ecalls, straddled fetches --
                           // reconverges with the same numInst but would print another time)
-                          (kn >= CX->clk_until || L.ncyc == S->ncyc);
+                          (kn >= CX->clk_until || L.ncyc == S->ncyc) &&
+                          (!CX->stdin_data || CX->in_pos[slot] == S->in_pos);
                 if (wballot<kNL>(eq)) {
                     // a register the golden future writes before reading it cannot
                     // influence the outcome (liveness from the golden trace)
@@ -2283,6 +2311,7 @@ __device__ __forceinline__ void trial_body() {
                     S->pc = L.pc; S->ninst = L.ninst; S->ncyc = L.ncyc; S->out_pos = L.out_pos; S->err_pos = L.err_pos;
                     S->stack_min = m.stack_min; S->tab_off = 0; S->tab_n = np;
                     S->live = 0; S->trace_pos = tpos;
+                    S->in_pos = CX->stdin_data ? CX->in_pos[0] : 0;
                 }
                 for (uint32_t i = 0; i < np; i++) {
                     if (lane == 0) CX->rec_vpns[(uint64_t)snaps_taken * CX->priv_pages + i] = CX->priv_vpn[i * CX->n_slots];
@@ -3481,10 +3510,20 @@ __device__ __forceinline__ void trial_body() {
 }
 
 // The instantiations (load-time build: with the translated blocks).
+// FI_TX_PART (fi_jit.cpp): 0 = every kernel in one module; k = only kernel k
+// (1 the 64-lane, 2 the solo, 3 the solo-odd), one module each, built in
+// parallel at load time.
 #ifdef __HIPCC_RTC__
+#ifndef FI_TX_PART
+#define FI_TX_PART 0
+#endif
+#if FI_TX_PART == 0 || FI_TX_PART == 1
 extern "C" __global__ void __launch_bounds__(64, FI_WAVES_PER_EU) fi_trial_kernel_tx(DevCtx) { trial_body<64>(); }
+#endif
+#if FI_TX_PART == 0 || FI_TX_PART == 2
 extern "C" __global__ void __launch_bounds__(kSoloLanes, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_tx_solo(DevCtx) { trial_body<1>(); }
-#ifdef FI_TX_SOLO_ODD
+#endif
+#if defined(FI_TX_SOLO_ODD) && (FI_TX_PART == 0 || FI_TX_PART == 3)
 extern "C" __global__ void __launch_bounds__(kSoloLanes, FI_SOLO_WAVES_PER_EU) fi_trial_kernel_tx_solo_odd(DevCtx) {
     trial_body<1, true>();
 }

@@ -108,6 +108,7 @@ CFG_NO_FORWARD = 512
 CFG_NO_SDC_EXIT = 1024
 CFG_NO_REDO = 2048
 CFG_NO_ODD_KERNEL = 4096
+CFG_JIT_NO_CACHE = 8192
 
 
 class GoldenInfo(C.Structure):
@@ -197,6 +198,7 @@ def lib():
         L.fi_last_error.argtypes = [vp]
         L.fi_load_elf.argtypes = [vp, C.c_char_p, C.c_size_t, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]
         L.fi_golden_run.argtypes = [vp, C.POINTER(GoldenInfo)]
+        L.fi_wait_translation.argtypes = [vp, C.POINTER(GoldenInfo)]
         L.fi_load_checkpoint.argtypes = [vp, C.c_char_p, C.c_char_p, C.c_size_t]
         L.fi_golden_stdout.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
         L.fi_golden_stderr.argtypes = [vp, C.c_char_p, C.c_uint64, C.POINTER(C.c_uint64)]
@@ -204,6 +206,7 @@ def lib():
         L.fi_set_bits.argtypes = [vp, C.c_uint64]
         L.fi_set_clock.argtypes = [vp, C.c_uint64, C.c_uint64]
         L.fi_set_exe_path.argtypes = [vp, C.c_char_p]
+        L.fi_set_stdin.argtypes = [vp, C.c_char_p, C.c_uint64]
         L.fi_set_protect.argtypes = [vp, C.c_uint64]
         L.fi_set_protect_opclasses.argtypes = [vp, C.c_uint64]
         L.fi_sample_sites.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
@@ -286,9 +289,20 @@ class Engine:
         """Start from a gem5 SE checkpoint (fi_load_checkpoint); elf = the workload."""
         self._chk(self.L.fi_load_checkpoint(self.h, directory.encode(), elf, len(elf)), "fi_load_checkpoint")
 
-    def golden_run(self) -> GoldenInfo:
+    def golden_run(self, wait_translation: bool = True) -> GoldenInfo:
+        """fi_golden_run; wait_translation: also wait for the background build
+        of the translated kernels (fi_wait_translation) -- otherwise trials
+        start on the static kernels and pick the build up when it lands."""
         g = GoldenInfo()
         self._chk(self.L.fi_golden_run(self.h, C.byref(g)), "fi_golden_run")
+        if wait_translation:
+            self._chk(self.L.fi_wait_translation(self.h, C.byref(g)), "fi_wait_translation")
+        self.golden = g
+        return g
+
+    def wait_translation(self) -> GoldenInfo:
+        g = GoldenInfo()
+        self._chk(self.L.fi_wait_translation(self.h, C.byref(g)), "fi_wait_translation")
         self.golden = g
         return g
 
@@ -312,6 +326,12 @@ class Engine:
     def set_exe_path(self, path: str):
         """What readlinkat("/proc/self/exe") answers: the executable's realpath."""
         self._chk(self.L.fi_set_exe_path(self.h, path.encode()), "fi_set_exe_path")
+
+    def set_stdin(self, data: bytes | None):
+        """Process.input as a file: the bytes read(0) returns (fi_set_stdin);
+        None = "cin", the host's stdin (reads of fd 0 escape as host).  Before
+        golden_run()."""
+        self._chk(self.L.fi_set_stdin(self.h, data, 0 if data is None else len(data)), "fi_set_stdin")
 
     def set_clock(self, period_ticks: int = 500, random_seed: int = 5489):
         """clock_gettime's ticks per CPU cycle and getrandom's gem5 Random seed."""
@@ -534,6 +554,10 @@ class FaultCampaign:
     Params (same names/meaning as the SimObject): workload (binary path), cmd
     (argv, cmd[0] defaults to workload), env, trials, seed, structures, bits,
     burst, protect_mask, protect_opclasses, num_gpus, max_insts_factor, output;
+    executable (gem5's Process.executable: what /proc/self/exe resolves to;
+    default the workload path, as gem5's se configs set it), input
+    (Process.input: "cin" = the host's stdin, reads of fd 0 escape; else a
+    file, opened relative to the working directory, that fd 0 reads);
     checkpoint (a gem5 SE checkpoint directory to start from),
     shadow_fu_model (SHREWD FU contention for result faults, off by default),
     priority_to_shadow and issue_params (the O3 issue model's parameters).
@@ -544,7 +568,7 @@ class FaultCampaign:
                  protect_mask: int = 0, num_gpus: int = 1, max_insts_factor: float = 2.0, output: str = "",
                  device: int = 0, private_pages: int = 16, protect_opclasses=(), bits=None,
                  shadow_fu_model: bool = False, priority_to_shadow: bool = False, issue_params: dict | None = None,
-                 checkpoint: str = ""):
+                 checkpoint: str = "", executable: str | None = None, input: str = "cin"):
         self.workload, self.cmd, self.env = workload, list(cmd or [workload]), list(env or [])
         self.trials, self.seed, self.structures, self.burst = trials, seed, structures, burst
         self.protect_mask, self.num_gpus, self.output = protect_mask, num_gpus, output
@@ -557,9 +581,24 @@ class FaultCampaign:
                 self.engine.load_checkpoint(checkpoint, f.read())
             else:
                 self.engine.load_elf(f.read(), self.cmd, self.env)
-        # Process.executable defaults to cmd[0]; gem5 answers /proc/self/exe with its realpath
-        self.engine.set_exe_path(os.path.realpath(self.cmd[0] if os.path.exists(self.cmd[0]) else workload))
-        self.golden = self.engine.golden_run()
+        # gem5 answers /proc/self/exe with realpath(Process.executable or cmd[0])
+        # (process.cc:124, syscall_emul.hh:1089-1111); the se configs set
+        # executable to the workload path.  A path that does not resolve on
+        # this host is left unset (that call then escapes as host).
+        self.executable = workload if executable is None else executable
+        exe = self.executable or self.cmd[0]
+        if os.path.exists(exe):
+            self.engine.set_exe_path(os.path.realpath(exe))
+        # Process.input (Process.py:44; FDArray, fd_array.cc:50-75): the stdio
+        # names map to the host's stdin, anything else is opened as a file
+        self.input = input
+        if input not in ("cin", "stdin"):
+            if input == "":
+                raise ValueError("input='': gem5 polls fd -1 and retries read(0) forever")
+            with open(input, "rb") as f:
+                self.engine.set_stdin(f.read())
+        # trials start at once; the translated kernels join when their build lands
+        self.golden = self.engine.golden_run(wait_translation=False)
         self.engine.set_campaign(seed, structures, burst)
         self.bits = bits_mask(bits)
         self.engine.set_bits(self.bits)

@@ -2,6 +2,8 @@
 #include "campaign.hh"
 
 #include <chrono>
+#include <climits>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -17,9 +19,15 @@ namespace shrewd {
 namespace {
 
 const char *kClass[FI_N_CLASS] = {"masked", "sdc", "crash", "hang", "detected", "escape"};
-const char *kCrash[] = {"", "unknown_inst", "illegal_inst", "page_fault", "syscall_range", "syscall_unimpl",
-                        "proxy", "fd_assert", "sigtrap", "stack_limit", "amo_line"};
-const char *kEscape[] = {"", "inst", "syscall", "csr", "host", "resource"};
+// sub-code names (include/fi_engine.h FI_CRASH_* / FI_ESC_*; the same as
+// shrewd_amd/fi.py CRASH_NAMES / ESCAPE_NAMES)
+const char *kCrash[] = {"", "panic_unknown_inst", "panic_illegal_inst", "panic_page_fault", "fatal_syscall_range",
+                        "fatal_syscall_unimpl", "fatal_proxy", "abort_fd_assert", "sigtrap", "fatal_stack_limit",
+                        "panic_amo_line", "abort_sc_line", "panic_se_handler", "panic_m5op"};
+const char *kEscape[] = {"", "inst", "syscall", "csr", "host", "resource", "undefined"};
+constexpr int kNCrash = sizeof(kCrash) / sizeof(kCrash[0]);
+constexpr int kNEscape = sizeof(kEscape) / sizeof(kEscape[0]);
+static_assert(kNCrash == FI_CRASH_M5_PANIC + 1 && kNEscape == FI_ESC_UNDEF + 1, "sub-code names");
 
 void check(fi_engine *e, fi_status s, const char *what) {
     if (s != FI_OK) {
@@ -111,7 +119,7 @@ uint64_t opclass_mask(const std::vector<std::string> &names) {
 
 Campaign::Campaign(const CampaignParams &p) : p_(p) {
     if (p_.cmd.empty()) p_.cmd.push_back(p_.workload);
-    if (p_.num_gpus == 0) throw std::runtime_error("num_gpus must be >= 1");
+    if (p_.num_gpus == 0 && p_.devices.empty()) throw std::runtime_error("num_gpus must be >= 1");
     const std::vector<uint8_t> elf = read_file(p_.workload);
     std::vector<const char *> argv, envp;
     for (auto &s : p_.cmd) argv.push_back(s.c_str());
@@ -119,9 +127,29 @@ Campaign::Campaign(const CampaignParams &p) : p_(p) {
     for (auto &s : p_.env) envp.push_back(s.c_str());
     envp.push_back(nullptr);
     const uint64_t smask = structures_mask(p_.structures);
-    for (uint32_t g = 0; g < p_.num_gpus; g++) {
+    // Process.input: the stdio names are the host's stdin (fd_array.cc:50-75),
+    // anything else a file opened relative to the working directory
+    std::vector<uint8_t> input;
+    const bool input_file = !(p_.input == "cin" || p_.input == "stdin");
+    if (input_file) {
+        if (p_.input.empty()) throw std::runtime_error("input '': gem5 polls fd -1 and retries read(0) forever");
+        std::ifstream f(p_.input, std::ios::binary);
+        if (!f) throw std::runtime_error("cannot open input " + p_.input);
+        input.assign(std::istreambuf_iterator<char>(f), {});
+    }
+    // /proc/self/exe: realpath(Process.executable) (syscall_emul.hh:1089-1111);
+    // unresolvable on this host -> unset (readlinkat escapes as host)
+    std::string exe;
+    {
+        const std::string x = p_.executable.empty() ? p_.workload : p_.executable;
+        if (char *rp = realpath(x.c_str(), nullptr)) { exe = rp; free(rp); }
+    }
+    std::vector<int32_t> devs = p_.devices;
+    if (devs.empty())
+        for (uint32_t g = 0; g < p_.num_gpus; g++) devs.push_back((int32_t)(p_.first_device + g));
+    for (size_t g = 0; g < devs.size(); g++) {
         fi_config cfg{};
-        cfg.device = (int32_t)(p_.first_device + g);
+        cfg.device = devs[g];
         cfg.private_pages = p_.private_pages;
         cfg.hang_factor_x16 = (uint32_t)(p_.max_insts_factor * 16 + 0.5);
         fi_engine *e = nullptr;
@@ -136,6 +164,8 @@ Campaign::Campaign(const CampaignParams &p) : p_(p) {
             check(e, fi_load_elf(e, elf.data(), elf.size(), argv.data(), envp.data()), "fi_load_elf");
         else
             check(e, fi_load_checkpoint(e, p_.checkpoint.c_str(), elf.data(), elf.size()), "fi_load_checkpoint");
+        if (!exe.empty()) check(e, fi_set_exe_path(e, exe.c_str()), "fi_set_exe_path");
+        if (input_file) check(e, fi_set_stdin(e, input.data(), input.size()), "fi_set_stdin");
         fi_golden_info gi{};
         check(e, fi_golden_run(e, &gi), "fi_golden_run");
         check(e, fi_set_campaign(e, p_.seed, smask, p_.burst), "fi_set_campaign");
@@ -219,11 +249,11 @@ std::string Campaign::summaryJson() const {
     for (int c = 0; c < FI_N_CLASS; c++) o << ", \"" << kClass[c] << "\": " << cls[c];
     o << ", \"crash_sub\": {";
     bool first = true;
-    for (int i = 1; i < 11; i++)
+    for (int i = 1; i < kNCrash; i++)
         if (hist_.crash_sub[i]) { o << (first ? "" : ", ") << "\"" << kCrash[i] << "\": " << hist_.crash_sub[i]; first = false; }
     o << "}, \"escape_sub\": {";
     first = true;
-    for (int i = 1; i < 6; i++)
+    for (int i = 1; i < kNEscape; i++)
         if (hist_.escape_sub[i]) { o << (first ? "" : ", ") << "\"" << kEscape[i] << "\": " << hist_.escape_sub[i]; first = false; }
     o << "}, \"guest_insts\": " << hist_.guest_insts << ", \"seconds\": " << seconds_
       << ", \"trials_per_s\": " << (seconds_ > 0 ? (double)hist_.trials / seconds_ : 0.0) << "}";

@@ -26,6 +26,10 @@ struct CampaignParams {
     std::string checkpoint;               // gem5 SE checkpoint directory to start from ("" = process start)
     std::vector<std::string> cmd;         // argv; empty -> {workload}
     std::vector<std::string> env;
+    std::string executable;               // Process.executable: /proc/self/exe resolves to its realpath
+                                          // ("" = the workload path, as gem5's se configs set it)
+    std::string input = "cin";            // Process.input (src/sim/Process.py:44): "cin"/"stdin" = the host's
+                                          // stdin (reads of fd 0 escape); else a file fd 0 reads
     uint64_t trials = 1000;
     uint64_t first_trial = 0;
     uint64_t seed = 0x5EED0001ULL;
@@ -40,6 +44,8 @@ struct CampaignParams {
     uint32_t load_latency = 2;            // issue model: cycles from a load's issue to its value
     uint32_t num_gpus = 1;
     uint32_t first_device = 0;
+    std::vector<int32_t> devices;         // explicit HIP device per engine (overrides num_gpus/first_device;
+                                          // a device may repeat: several engines share it)
     double max_insts_factor = 2.0;        // hang cap = golden * f + 1000
     uint32_t private_pages = 16;
     std::string output;                   // prefix: <output>.outcomes.bin + <output>.json

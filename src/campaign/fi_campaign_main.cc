@@ -5,6 +5,7 @@
 //               [--trials N] [--first-trial F] [--seed S] [--structures int_reg,pc,mem]
 //               [--burst K] [--bits 0-31,63] [--protect-mask M] [--protect-opclasses IntAlu,IntMult] [--num-gpus G] [--device D]
 //               [--max-insts-factor F] [--private-pages P] [--output PREFIX]
+//               [--executable PATH] [--input FILE|cin] [--devices 0,0,1]
 //
 // Prints one JSON summary line; with --output also writes PREFIX.outcomes.bin
 // (fi_outcome records in trial order), PREFIX.hist.bin and PREFIX.json.
@@ -39,6 +40,12 @@ int main(int argc, char **argv) {
         else if (k == "--cmd") p.cmd = split(v);
         else if (k == "--checkpoint") p.checkpoint = v;
         else if (k == "--env") p.env = split(v);
+        else if (k == "--executable") p.executable = v;
+        else if (k == "--input") p.input = v;
+        else if (k == "--devices") {
+            p.devices.clear();
+            for (auto &d : split(v)) p.devices.push_back((int32_t)strtol(d.c_str(), nullptr, 0));
+        }
         else if (k == "--trials") p.trials = strtoull(v.c_str(), nullptr, 0);
         else if (k == "--first-trial") p.first_trial = strtoull(v.c_str(), nullptr, 0);
         else if (k == "--seed") p.seed = strtoull(v.c_str(), nullptr, 0);

@@ -30,6 +30,11 @@ class FaultCampaign(SimObject):
         "", "gem5 SE checkpoint directory the trials start from (m5.cpt + memory store); "
         "empty: process start")
     env = VectorParam.String([], "environment of the workload")
+    executable = Param.String(
+        "", "Process.executable: readlinkat('/proc/self/exe') answers its realpath (empty: the workload path)")
+    input = Param.String(
+        "cin", "Process.input: 'cin' = the host's stdin (reads of fd 0 end the trial as escape/host); "
+        "else a file fd 0 reads, deterministically per trial")
     trials = Param.UInt64(1000, "number of fault-injection trials")
     first_trial = Param.UInt64(0, "first trial id (sites are keyed by (seed, trial id))")
     seed = Param.UInt64(0x5EED0001, "campaign seed")

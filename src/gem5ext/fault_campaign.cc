@@ -20,6 +20,8 @@ FaultCampaign::init()
     cp.checkpoint = params().checkpoint;
     cp.cmd = params().cmd;
     cp.env = params().env;
+    cp.executable = params().executable;
+    cp.input = params().input;
     cp.trials = params().trials;
     cp.first_trial = params().first_trial;
     cp.seed = params().seed;

@@ -405,28 +405,42 @@ def test_full_size_properties(engine_factory):
 
 def test_native_driver_matches_engine(engine_factory, tmp_path):
     """src/campaign (the FaultCampaign SimObject's core) over the C ABI gives the
-    same per-trial outcomes and histogram as the Python binding."""
+    same per-trial outcomes and histogram as the Python binding, with one
+    engine and with two engines on device 0 (--devices 0,0: the in-process
+    multi-device path, one host thread per engine, histograms summed on the
+    host); its JSON summary names every class and sub-code as the Python
+    mirror's summary() does."""
+    import json
     import subprocess
     from shrewd_amd import HIST_DT, OUTCOME_DT
     from shrewd_amd import build as b
+    from shrewd_amd.fi import CLASS_NAMES, CRASH_NAMES, ESCAPE_NAMES
     exe = b.build_cli()
     n, seed = 3000, 0x5EED0003
-    prefix = str(tmp_path / "camp")
-    r = subprocess.run([exe, "--workload", os.path.join(ROOT, "workloads", "crc32.elf"), "--cmd", "crc32",
-                        "--trials", str(n), "--seed", hex(seed), "--structures", "int_reg,pc,mem",
-                        "--output", prefix], capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stderr
-    out = np.fromfile(prefix + ".outcomes.bin", OUTCOME_DT)
-    hist = np.fromfile(prefix + ".hist.bin", HIST_DT)[0]
     e = engine_factory("crc32")
     e.set_campaign(seed, (1 << 34) - 2, 1)
     e.set_protect(0)
     ref, rh = e.run_trials(0, n)
-    assert out.tobytes() == ref.tobytes()
-    assert hist["counts"].tobytes() == rh["counts"].tobytes()
+    for devices in ("0", "0,0"):
+        prefix = str(tmp_path / f"camp{devices.count(',')}")
+        r = subprocess.run([exe, "--workload", os.path.join(ROOT, "workloads", "crc32.elf"), "--cmd", "crc32",
+                            "--trials", str(n), "--seed", hex(seed), "--structures", "int_reg,pc,mem",
+                            "--devices", devices, "--output", prefix], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        out = np.fromfile(prefix + ".outcomes.bin", OUTCOME_DT)
+        hist = np.fromfile(prefix + ".hist.bin", HIST_DT)[0]
+        assert out.tobytes() == ref.tobytes()
+        assert hist["counts"].tobytes() == rh["counts"].tobytes()
+        js = json.loads(r.stdout)
+        assert js["num_gpus"] == devices.count(",") + 1
+        cls = rh["counts"].sum(axis=(0, 1))
+        assert {c: js[c] for c in CLASS_NAMES} == {CLASS_NAMES[i]: int(cls[i]) for i in range(6)}
+        assert js["crash_sub"] == {CRASH_NAMES[i]: int(rh["crash_sub"][i]) for i in range(16) if rh["crash_sub"][i]}
+        assert js["escape_sub"] == {ESCAPE_NAMES[i]: int(rh["escape_sub"][i]) for i in range(8) if rh["escape_sub"][i]}
 
 
-@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp", "rnd", "xop", "sys2", "clk"])
+@pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp", "rnd", "xop", "sys2", "clk",
+                                  "stdin"])
 def test_known_answer_programs(oracle_mod, prog):
     """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
@@ -445,6 +459,7 @@ def test_known_answer_programs(oracle_mod, prog):
     rounding mode and fcsr (answers from the reference SoftFloat).
     rnd: getrandom (gem5's mt19937_64 stream) and clock_gettime (curTick).
     clk: clock_gettime after a branch whose arms differ only in ticks.
+    stdin: read / write / writev of fd 0 with Process.input a file.
     xop: scalar crypto, Zfa (fli / fround / fcvtmod.w.d), M5 pseudo-ops, the
     warn-only privileged no-ops and the cache-block ops.
     sys2: read, readlinkat (/proc/self/exe) and riscv_hwprobe.  The device golden run (general interpreter)
@@ -464,7 +479,8 @@ def test_known_answer_programs(oracle_mod, prog):
                      "rnd": (kat.rnd_program_elf, kat.rnd_program_expected),
                      "xop": (kat.xop_program_elf, kat.xop_program_expected),
                      "sys2": (kat.sys2_program_elf, kat.sys2_program_expected),
-                     "clk": (kat.clk_program_elf, kat.clk_program_expected)}[prog]
+                     "clk": (kat.clk_program_elf, kat.clk_program_expected),
+                     "stdin": (kat.stdin_program_elf, kat.stdin_program_expected)}[prog]
     if prog in ("fp", "xop") and not oracle_mod.has_softfloat():
         pytest.skip("oracle without the reference SoftFloat")
     if prog == "xop" and not oracle_mod.has_rvk():
@@ -475,6 +491,8 @@ def test_known_answer_programs(oracle_mod, prog):
     e.load_elf(elf, [prog])
     if prog == "sys2":
         e.set_exe_path(kat.SYS2_EXE)
+    if prog == "stdin":
+        e.set_stdin(kat.STDIN_DATA)
     g = e.golden_run()
     assert g.exit_code == (300 & 0xFF if prog == "sys" else 0)
     assert g.stderr_len == len(stderr)
@@ -483,6 +501,8 @@ def test_known_answer_programs(oracle_mod, prog):
     o = oracle_mod.Oracle(elf, prog)
     if prog == "sys2":
         o.set_exe_path(kat.SYS2_EXE)
+    if prog == "stdin":
+        o.set_stdin(kat.STDIN_DATA)
     o.run_golden()
     assert o.golden_stderr() == e.golden_stderr()
     e.set_campaign(0x5EED00A1, REGS | PC, 1)
@@ -523,6 +543,81 @@ def test_clock_read_blocks_tick_blind_early_exit(oracle_mod):
             assert int(e.debug_stats()[11]) > 0, "early-exit comparisons did not run"
         compare(dev, ref, sites)
         e.close()
+
+
+def test_stdin_file_classifies_fd0_trials(oracle_mod):
+    """hello with bit 0 of a0 flipped before its write: write(0) touches the
+    host's stdin, which only escapes while Process.input is "cin".  With an
+    input file (fi_set_stdin) the write to the O_RDONLY fd 0 returns -EBADF
+    and the trial is classified (SDC: nothing printed).  Outcomes equal the
+    oracle's with the same input, also on C1's 1,000 sites (whose host
+    escapes are write lengths of 2 GiB and more: a flipped a2 makes gem5's
+    BufferArg allocate and zero that many host bytes, which a host may or may
+    not survive); the engine refuses process settings after the golden run."""
+    from shrewd_amd import Engine, EngineError, SITE_DT
+    elf = workload_elf("hello")
+    o = oracle_mod.Oracle(elf, "hello")
+    o.set_stdin(b"some input\n")
+    g = o.run_golden()
+    fd0 = np.zeros(g.ninst + 1, SITE_DT)
+    fd0["inst"] = np.arange(g.ninst + 1)
+    fd0["mask"] = 1
+    fd0["target"] = 10
+    fd0["trial"] = np.arange(g.ninst + 1)
+    cin = Engine()
+    cin.load_elf(elf, ["hello"])
+    cin.golden_run()
+    cin.set_campaign(0x5EED0001, REGS, 1)
+    c1 = cin.sample(0, 1000)
+    a, _ = cin.run_sites(fd0)
+    assert ((a["cls"] == 5) & (a["sub"] == 4)).sum() > 0
+    a1, _ = cin.run_sites(c1)
+    with pytest.raises(EngineError):
+        cin.set_stdin(b"x")
+    cin.close()
+    e = Engine()
+    e.load_elf(elf, ["hello"])
+    e.set_stdin(b"some input\n")
+    e.golden_run()
+    b, _ = e.run_sites(fd0)
+    assert not ((b["cls"] == 5) & (b["sub"] == 4)).any()
+    compare(b, o.run_trials(fd0, protect_mask=0), fd0)
+    b1, _ = e.run_sites(c1)
+    compare(b1, o.run_trials(c1, protect_mask=0), c1)
+    host = (b1["cls"] == 5) & (b1["sub"] == 4)
+    assert (c1["target"][host] == 12).all() and (c1["mask"][host] >= 1 << 31).all()
+    assert np.array_equal(a1, b1)
+    e.close()
+
+
+@pytest.mark.parametrize("name", ["crc32", "qsort"])
+def test_background_translation_same_outcomes(engine_factory, oracle_mod, name):
+    """The translated kernels build in the background (three code objects in
+    parallel helper processes, no cache: FI_CFG_JIT_NO_CACHE): trials run at
+    once on the static kernels in 16k-trial chunks and pick the build up at a
+    chunk boundary.  Outcomes before, across and after the switch equal the
+    waited engine's and the oracle's."""
+    from shrewd_amd import Engine
+    from shrewd_amd.fi import CFG_JIT_NO_CACHE
+    n = 60000
+    ref_e = engine_factory(name)
+    ref_e.set_campaign(0x5EED0B6, REGS | PC, 1)
+    ref_e.set_protect(0)
+    ref, _ = ref_e.run_trials(0, n)
+    e = Engine(flags=CFG_JIT_NO_CACHE)
+    e.load_elf(workload_elf(name), [name])
+    e.golden_run(wait_translation=False)
+    assert e.translate_status() == "compiling"
+    e.set_campaign(0x5EED0B6, REGS | PC, 1)
+    e.set_protect(0)
+    a, _ = e.run_trials(0, n)
+    g = e.wait_translation()
+    assert e.translate_status() == "" and g.translated_blocks > 0 and g.translate_us > 0
+    b, _ = e.run_trials(0, n)
+    assert np.array_equal(a, ref) and np.array_equal(b, ref)
+    sites = e.sample(0, 2000)
+    compare(a[:2000], oracle_for(oracle_mod, name).run_trials(sites, protect_mask=0), sites)
+    e.close()
 
 
 def test_sdc_early_exit(engine_factory, oracle_mod):

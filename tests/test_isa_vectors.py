@@ -1359,6 +1359,96 @@ def rnd_program_expected() -> bytes:
     return out
 
 
+# ---------------------------------------------------------------- stdin program
+# Process.input as a file (src/sim/Process.py:44, fd_array.cc:69-75) and
+# readFunc (syscall_emul.hh:2798-2822): read(0) takes min(n, left) bytes at
+# the file offset and the zero-filled BufferArg copies all n bytes out when the
+# read returned any (syscall_emul_buf.hh:55-85); at EOF nothing is copied (a
+# null buffer is fine); write / writev to the O_RDONLY fd 0 give -EBADF.
+STDIN_DATA = b"abcdefghij0123456789XYZ"
+STDIN_CALLS = [(0, 8), (8, 4), (16, 32), (48, 8), (None, 8)]   # (buffer offset | None = null, n)
+
+
+def stdin_program_source() -> str:
+    body = []
+    for k, (off, n) in enumerate(STDIN_CALLS):
+        buf = "    li    a1, 0" if off is None else f"    addi  a1, s2, {off}"
+        body += ["    li    a0, 0", buf, f"    li    a2, {n}", "    li    a7, 63", "    ecall",
+                 f"    sd    a0, {8 * k}(s3)"]
+    k = len(STDIN_CALLS)
+    body += ["    li    a0, 0", "    mv    a1, s2", "    li    a2, 4", "    li    a7, 64", "    ecall",
+             f"    sd    a0, {8 * k}(s3)"]
+    body += ["    sd    s2, 0(s4)", "    li    t0, 4", "    sd    t0, 8(s4)",
+             "    li    a0, 0", "    mv    a1, s4", "    li    a2, 1", "    li    a7, 66", "    ecall",
+             f"    sd    a0, {8 * (k + 1)}(s3)"]
+    body = "\n".join(body)
+    return f"""    .text
+_start:
+    la    s2, buf
+    la    s3, res
+    la    s4, iov
+{body}
+    li    a0, 1
+    mv    a1, s2
+    li    a2, 56
+    li    a7, 64
+    ecall
+    li    a0, 1
+    mv    a1, s3
+    li    a2, {8 * (len(STDIN_CALLS) + 2)}
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 93
+    ecall
+    .data
+    .balign 8
+buf:
+""" + "\n".join(["    .dword 0xaaaaaaaaaaaaaaaa"] * 7) + f"""
+res:
+    .zero {8 * (len(STDIN_CALLS) + 2)}
+iov:
+    .zero 16
+"""
+
+
+def stdin_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(stdin_program_source(), compress=False)
+
+
+def stdin_program_expected() -> bytes:
+    """Model: the buffer after the reads, then each call's return value."""
+    buf = bytearray(b"\xaa" * 56)
+    pos, rets = 0, []
+    for off, n in STDIN_CALLS:
+        k = min(n, len(STDIN_DATA) - pos)
+        if k and off is not None:
+            buf[off:off + n] = STDIN_DATA[pos:pos + k] + bytes(n - k)
+        pos += k
+        rets.append(k)
+    rets += [-9, -9]
+    return bytes(buf) + b"".join((r & (2**64 - 1)).to_bytes(8, "little") for r in rets)
+
+
+def test_stdin_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(stdin_program_elf(), "stdin")
+    o.set_stdin(STDIN_DATA)
+    g = o.run_golden()
+    assert g.exit_code == 0
+    assert o.golden_stdout() == stdin_program_expected()
+
+
+def test_stdin_cin_escapes_on_oracle(oracle_mod):
+    """Process.input = "cin" (the default): the read of the host's stdin is not
+    reproducible -- the golden run itself ends as escape/host."""
+    o = oracle_mod.Oracle(stdin_program_elf(), "stdin")
+    with pytest.raises(RuntimeError):
+        o.run_golden()
+    out, _ = o.run_one()
+    assert (out["cls"], out["sub"]) == (5, 4)
+
+
 # ---------------------------------------------------------------- clk program
 # A branch on s3 whose two arms commit the same instructions but take
 # different numbers of ticks: the taken arm (s3 != 0, a fault) adds CLK_ECALLS

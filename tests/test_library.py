@@ -69,3 +69,12 @@ def test_structures_mask_names():
     from shrewd_amd import structures_mask
     assert structures_mask(["int_reg", "pc"]) == 0x1FFFFFFFE
     assert structures_mask(["a0", "x5", "mem"]) == (1 << 10) | (1 << 5) | (1 << 33)
+
+
+def test_native_driver_names_every_subcode():
+    """Every crash / escape sub-code of include/fi_engine.h has the Python
+    mirror's name in src/campaign/campaign.cc (its JSON keys)."""
+    from shrewd_amd.fi import CRASH_NAMES, ESCAPE_NAMES
+    src = open(os.path.join(ROOT, "src", "campaign", "campaign.cc")).read()
+    for name in list(CRASH_NAMES.values()) + list(ESCAPE_NAMES.values()):
+        assert f'"{name}"' in src, name

@@ -1,16 +1,18 @@
 #!/bin/bash
-# GPU parity suite, then the default bench line and a qsort/intmix bench (run via gpurun).
+# A pytest -m gpu selection (or all of it), then the default bench line
+# (crc32 headline + qsort / intmix under "workloads").  Run via gpurun:
+#   bash tools/gpu/check_and_bench.sh TAG ["pytest -k expr" | all | none]
 set -o pipefail
+TAG=${1:-r04}
+SEL=${2:-all}
 mkdir -p gpurun_out
 export SHREWD_FI_JIT_CACHE=$PWD/gpurun_out/jitcache
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; tail -4 gpurun_out/pytest_gpu.log; grep -E "FAILED|Error" gpurun_out/pytest_gpu.log | head -5
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
-cat gpurun_out/bench.json
-# (intmix: a 15 s CPU sample, so that its parity leg checks >= 20k trials)
-for w in qsort:3 intmix:15; do
-    s=${w#*:}; w=${w%%:*}
-    timeout -k 10 300 python -u bench.py --workload $w --cpu-seconds $s > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err || exit $?
-    python -c "import json; d=json.load(open('gpurun_out/bench_$w.json')); print('$w', round(d['value']), d['ms_per_step'], d['parity'])"
-done
+if [ "$SEL" != "none" ]; then
+    if [ "$SEL" = "all" ]; then K=(); else K=(-k "$SEL"); fi
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread "${K[@]}" \
+        > gpurun_out/pytest_gpu_$TAG.log 2>&1
+    rc=$?; tail -3 gpurun_out/pytest_gpu_$TAG.log; grep -E "FAILED|Error" gpurun_out/pytest_gpu_$TAG.log | head -5
+    [ $rc -eq 0 ] || exit $rc
+fi
+timeout -k 10 400 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
+python tools/bench_summary.py gpurun_out/bench_$TAG.json
