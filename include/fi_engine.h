@@ -81,7 +81,8 @@ typedef int32_t fi_status;
 #define FI_ESC_SYSCALL 2
 #define FI_ESC_CSR 3
 #define FI_ESC_HOST 4
-#define FI_ESC_RESOURCE 5
+#define FI_ESC_RESOURCE 5   /* an engine bound: exit_code 0 = private pages (re-run with more before the
+                              histogram), 1 = the VMA list / getrandom table (bounded in the oracle too) */
 #define FI_ESC_UNDEF 6      /* gem5's own behaviour is undefined (GEM5_UNREACHABLE: an RVV floating-point op at SEW = 8) */
 
 /* Fault-site structures: 1..31 = x1..x31, 32 = pc, 33 = 8-byte memory word,
@@ -224,7 +225,7 @@ fi_status fi_load_checkpoint(fi_engine *e, const char *cpt_dir, const uint8_t *e
  * the translation of the golden basic blocks.  The translated kernels build
  * in the background (hipRTC in parallel helper processes): until they land,
  * trials run on the static kernels -- identical outcomes, bit for bit -- in
- * chunks of at most 16,384 trials, and each chunk boundary picks the build
+ * chunks of at most 131,072 trials, and each chunk boundary picks the build
  * up.  fi_translate_status() is "compiling" meanwhile. */
 fi_status fi_golden_run(fi_engine *e, fi_golden_info *out);
 /* Block until the background build has landed (or failed: see

@@ -1204,6 +1204,11 @@ int or_sys_class(int num) {
     return 1;
 }
 
+/* resource escapes here are the bounds the engine shares (the VMA list, the
+ * precomputed getrandom stream): exit code 1 marks them, as on the device
+ * (fi_trial.hip kEscTable); 0 is the device's private-page exhaustion, which
+ * the oracle does not have */
+#define ESC_TABLE 1
 #define EBADF_ 9
 #define EINVAL_ 22
 #define ENOTTY_ 25
@@ -1324,9 +1329,9 @@ static void sys_mmap(mach_t *m) {
             start = s2;
         }
     } else if (!vma_unmap(m, start, start + len)) {
-        finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return;
+        finish(m, OR_ESCAPE, OR_ESC_RESOURCE, ESC_TABLE); return;
     }
-    if (!vma_add(m, start, start + len)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return; }
+    if (!vma_add(m, start, start + len)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, ESC_TABLE); return; }
     m->x[10] = start;
 }
 
@@ -1528,7 +1533,7 @@ static void do_syscall(mach_t *m) {
         if (len > VM_MAX_LEN) { vm_escape(m, 215); return; }
         len = round_up(len);
         if (st + len < st) { vm_escape(m, 215); return; }
-        if (!vma_unmap(m, st, st + len)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return; }
+        if (!vma_unmap(m, st, st + len)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, ESC_TABLE); return; }
         m->x[10] = 0;
         return;
     }
@@ -1538,7 +1543,7 @@ static void do_syscall(mach_t *m) {
         const u64 na = round_up(nb), oa = round_up(ob);
         if ((na > oa ? na - oa : oa - na) > VM_MAX_LEN) { vm_escape(m, 214); return; }
         if (nb < ob) {
-            if (oa - na > 0 && !vma_unmap(m, na, oa)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return; }
+            if (oa - na > 0 && !vma_unmap(m, na, oa)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, ESC_TABLE); return; }
             m->brk = nb;
             m->x[10] = nb;
             return;
@@ -1547,7 +1552,7 @@ static void do_syscall(mach_t *m) {
             const int u = is_unmapped(m, oa, na - oa);
             if (u < 0) { se_panic(m); return; }
             if (!u) { m->x[10] = ob; return; }   /* existing mappings impede the heap */
-            if (!vma_add(m, oa, na)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return; }
+            if (!vma_add(m, oa, na)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, ESC_TABLE); return; }
         }
         m->brk = nb;
         m->x[10] = nb;
@@ -1576,7 +1581,7 @@ static void do_syscall(mach_t *m) {
         if (cnt > (1ULL << 31)) { finish(m, OR_ESCAPE, OR_ESC_HOST, 0); return; }   /* host buffer */
         /* the engine precomputes the first 1 MiB of the stream: beyond it, a
          * resource escape on both sides */
-        if (m->rnd_pos + cnt > (1ULL << 20)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, 0); return; }
+        if (m->rnd_pos + cnt > (1ULL << 20)) { finish(m, OR_ESCAPE, OR_ESC_RESOURCE, ESC_TABLE); return; }
         m->rnd_pos += cnt;
         uint8_t *tmp = (uint8_t *)malloc(cnt ? cnt : 1);
         for (u64 i = 0; i < cnt; i++) tmp[i] = (uint8_t)(mt64_next(m) % 255);

@@ -75,9 +75,12 @@ using namespace fi;
 // trials per wave when fi_config.lanes_per_wave is 0
 static constexpr uint32_t kDefaultLanes = 64;
 static constexpr uint32_t kDefaultResumeLanes = 8;   // measured: profiles/README.md (r01b sweep)
-// trials per launch while the translated kernels are still being built: the
-// static kernels run small chunks so the campaign picks the build up soon
-static constexpr uint64_t kJitWindowChunk = 16384;
+// trials per launch while the translated kernels are still being built, so
+// that a long campaign picks the build up at a chunk boundary.  Not smaller:
+// a chunk lasts at least as long as its longest trial (the hang trials), so
+// the static kernels' throughput grows with the chunk (crc32, 100k trials:
+// 0.36 s in 16k chunks; profiles/r04e_bench.json)
+static constexpr uint64_t kJitWindowChunk = 131072;
 
 // The background build of the translated kernels (fi_golden_run starts it;
 // run_chunk installs the result at a chunk boundary): the 64-lane, solo and,

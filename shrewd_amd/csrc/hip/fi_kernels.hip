@@ -285,12 +285,14 @@ __global__ void fi_pack_runs_kernel(const uint64_t *keys, const uint32_t *cnt, u
 
 // Second pass of the trials that ran out of private pages (fi_engine.cpp
 // run_chunk): list them, gather their sites densely, scatter the new outcomes.
+// (A resource escape with exit code 1 hit a table bound -- the VMA list, the
+// getrandom stream -- that more pages would not lift: fi_trial.hip kEscTable.)
 __global__ void fi_redo_collect_kernel(const fi_outcome *out, uint64_t n, uint32_t *idx, uint32_t *cnt,
                                        unsigned long long *stats) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const fi_outcome o = out[i];
-    if (o.cls == FI_ESCAPE && o.sub == FI_ESC_RESOURCE) {
+    if (o.cls == FI_ESCAPE && o.sub == FI_ESC_RESOURCE && o.exit_code == 0) {
         idx[atomicAdd(cnt, 1u)] = (uint32_t)i;
         atomicAdd(&stats[30], 1ull);
     }

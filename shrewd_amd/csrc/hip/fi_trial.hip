@@ -399,6 +399,11 @@ __device__ int vm_is_unmapped(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t sl
     for_mapped(c, w, m, slot, lo >> 12, (hi + 4095) >> 12, [&](uint64_t, int) { any = true; return false; });
     return any ? -1 : 1;
 }
+// A resource escape's exit code: 0 = the trial ran out of private pages (the
+// redo pass runs it again with more, fi_kernels.hip fi_redo_collect_kernel),
+// kEscTable = a table both the engine and the oracle bound (the VMA list, the
+// precomputed getrandom stream): more pages would not change it.
+constexpr int kEscTable = 1;
 // MemState::mapRegion (mem_state.cc:172-189); false = the list is full
 __device__ bool vm_add(VmState *v, uint64_t lo, uint64_t hi) {
     if (lo >= hi) return true;
@@ -409,7 +414,8 @@ __device__ bool vm_add(VmState *v, uint64_t lo, uint64_t hi) {
 // MemState::unmapRegion (mem_state.cc:191-276) + Process::deallocateMem
 // (process.cc:348-382): the VMAs lose [lo, hi), the mapped pages in it leave
 // the trial's set (a private entry turns into a tombstone, a snapshot or zero
-// stack page gets one).  0 ok, 1 no room (resource escape).
+// stack page gets one).  0 ok, 1 no private page left, 2 the VMA list is full
+// (resource escapes; exit code kEscTable for the latter, vm_esc).
 __device__ int vm_unmap(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, VmState *v, uint64_t lo, uint64_t hi) {
     const uint32_t n = v->nvma;
     for (uint32_t i = 0; i < n; i++) {
@@ -417,7 +423,7 @@ __device__ int vm_unmap(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, Vm
         if (!(a < hi && lo < b)) continue;
         if (a < lo && b > hi) {
             v->vma[i][1] = lo;
-            if (!vm_add(v, hi, b)) return 1;
+            if (!vm_add(v, hi, b)) return 2;
         } else if (a >= lo && b <= hi) {
             v->vma[i][0] = v->vma[i][1] = 0;
         } else if (a < lo) {
@@ -966,7 +972,8 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         const uint64_t na = (nb + 4095) & ~4095ULL, oa = (ob + 4095) & ~4095ULL;
         if ((na > oa ? na - oa : oa - na) > kVmMaxLen) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, 214u); return false; }
         if (nb < ob) {
-            if (oa != na && vm_unmap(c, w, m, slot, v, na, oa)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            const int r = oa != na ? vm_unmap(c, w, m, slot, v, na, oa) : 0;
+            if (r) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, r == 2 ? kEscTable : 0, pc32); return false; }
             v->brk = nb;
             set_ret((int64_t)nb);
             return true;
@@ -975,7 +982,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
             const int u = vm_is_unmapped(c, w, m, slot, oa, na - oa);
             if (u < 0) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }
             if (!u) { set_ret((int64_t)ob); return false; }
-            if (!vm_add(v, oa, na)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            if (!vm_add(v, oa, na)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, kEscTable, pc32); return false; }
         }
         v->brk = nb;
         set_ret((int64_t)nb);
@@ -1020,10 +1027,11 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
                 start = s2;
             }
         } else {
-            if (vm_unmap(c, w, m, slot, v, start, start + len)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+            const int r = vm_unmap(c, w, m, slot, v, start, start + len);
+            if (r) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, r == 2 ? kEscTable : 0, pc32); return false; }
             changed = true;
         }
-        if (!vm_add(v, start, start + len)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        if (!vm_add(v, start, start + len)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, kEscTable, pc32); return false; }
         set_ret((int64_t)start);
         return changed;
     }
@@ -1032,7 +1040,8 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         if (a1 > kVmMaxLen) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, 215u); return false; }
         const uint64_t len = (a1 + 4095) & ~4095ULL;
         if (a0 + len < a0) { finish(L, FI_ESCAPE, FI_ESC_SYSCALL, 0, 215u); return false; }
-        if (vm_unmap(c, w, m, slot, vm_of(c, m, slot), a0, a0 + len)) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        const int r = vm_unmap(c, w, m, slot, vm_of(c, m, slot), a0, a0 + len);
+        if (r) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, r == 2 ? kEscTable : 0, pc32); return false; }
         set_ret(0);
         return true;
     }
@@ -1057,7 +1066,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
     case 278: {   // getrandomFunc (syscall_emul.hh:3222-3236): count bytes of mt19937_64() % 255
         VmState *v = vm_of(c, m, slot);
         if (a1 > (1ULL << 31)) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
-        if (v->rnd_pos + a1 > c->rnd_len) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, pc32); return false; }
+        if (v->rnd_pos + a1 > c->rnd_len) { finish(L, FI_ESCAPE, FI_ESC_RESOURCE, kEscTable, pc32); return false; }
         const int h = proxy_writable(c, w, m, slot, a0, a1);
         if (h == 0) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
         if (h == -1) { finish(L, FI_CRASH, FI_CRASH_STACK_LIMIT, 1, pc32); return false; }

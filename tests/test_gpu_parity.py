@@ -594,8 +594,7 @@ def test_stdin_file_classifies_fd0_trials(oracle_mod):
 def test_background_translation_same_outcomes(engine_factory, oracle_mod, name):
     """The translated kernels build in the background (three code objects in
     parallel helper processes, no cache: FI_CFG_JIT_NO_CACHE): trials run at
-    once on the static kernels in 16k-trial chunks and pick the build up at a
-    chunk boundary.  Outcomes before, across and after the switch equal the
+    once on the static kernels and pick the build up at a chunk boundary.  Outcomes before, across and after the switch equal the
     waited engine's and the oracle's."""
     from shrewd_amd import Engine
     from shrewd_amd.fi import CFG_JIT_NO_CACHE
