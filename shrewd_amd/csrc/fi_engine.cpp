@@ -74,6 +74,7 @@ using namespace fi;
 
 // trials per wave when fi_config.lanes_per_wave is 0
 static constexpr uint32_t kDefaultLanes = 64;
+static constexpr uint32_t kPreTail = 4;   // zero PreInst entries past the text (fi_trial.hip solo_pre_run)
 static constexpr uint32_t kDefaultResumeLanes = 8;   // measured: profiles/README.md (r01b sweep)
 // trials per launch while the translated kernels are still being built, so
 // that a long campaign picks the build up at a chunk boundary.  Not smaller:
@@ -697,7 +698,10 @@ static fi_status finish_load(fi_engine *e, const uint64_t regs[32], uint64_t pc)
     }
     HIPCHK(hipMalloc(&e->d_text, tbytes));
     HIPCHK(hipMemcpy(e->d_text, text.data(), tbytes, hipMemcpyHostToDevice));
-    HIPCHK(hipMalloc(&e->d_pre, (tbytes / 2) * sizeof(PreInst)));
+    // + kPreTail zero entries (kind K_SLOW): the solo interpreter prefetches
+    // the fall-through entry of the text's last instruction without a clamp
+    HIPCHK(hipMalloc(&e->d_pre, (tbytes / 2 + kPreTail) * sizeof(PreInst)));
+    HIPCHK(hipMemset(e->d_pre + tbytes / 2, 0, kPreTail * sizeof(PreInst)));
     HIPCHK(launch_predecode(e->d_text, e->code_lo - e->text_lo, e->code_hi - e->text_lo, tbytes / 2, e->d_pre,
                             e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));

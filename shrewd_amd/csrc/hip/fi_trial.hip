@@ -1695,7 +1695,8 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
     // pcs as 32-bit offsets from the text base while the run stays in the text
     // (the host keeps the text inside one 4 GiB window)
     const uint64_t tlo = CX->text_lo, clo = CX->code_lo, chi = CX->code_hi;
-    const uint32_t tby = CX->text_bytes, tlo32 = (uint32_t)tlo;
+    const uint32_t tby = CX->text_bytes;
+    const uint32_t clo_o = (uint32_t)(clo - tlo), chi_o = (uint32_t)(chi - tlo);   // the code range as text offsets
     const const_u32 *const pre = (const const_u32 *)(uintptr_t)CX->pre;
     // the last page translated, in registers (the TLB itself stays in LDS:
     // mappings do not change inside a run, lookup_full only inserts)
@@ -1726,14 +1727,14 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
 #endif
     if ((uint32_t)((spc - tlo) >> 32) == 0 && (uint32_t)(spc - tlo) < tby) {
         uint32_t po = (uint32_t)(spc - tlo);
-        // the entry of the instruction at po (odd pcs fetch like pc | 2 of their word)
+        // the entry of the instruction at po (odd pcs fetch like pc | 2 of their
+        // word: halfword (po >> 1) | 1; text_lo is page-aligned).  Offsets up to
+        // tby + 5 land on the zero (K_SLOW) entries past the text
+        // (fi_engine.cpp kPreTail), so no clamp.
 #define PRE_AT(o_, x_, y_, z_)                                                      \
     do {                                                                            \
-        const uint32_t a_ = tlo32 + (o_);                                           \
-        const uint32_t k_ = (((a_ & ~1u) | ((a_ & 1u) << 1)) - tlo32) >> 1;         \
-        const const_u32 *q_ = pre + 4 * (k_ < (tby >> 1) ? k_ : 0u);                \
+        const const_u32 *q_ = pre + 4 * (((o_) >> 1) | ((o_) & 1u));                \
         x_ = q_[1]; y_ = q_[2]; z_ = q_[3];                                         \
-        z_ = k_ < (tby >> 1) ? z_ : 0u;                                             \
     } while (0)
         uint32_t q1, q2, q3;
         PRE_AT(po, q1, q2, q3);
@@ -1746,7 +1747,7 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
                 const uint32_t ci = (po >> 1) & (kSoloDC - 1);
                 const uint32_t tag = uni32(DCT[ci]);
                 const uint32_t e1 = uni32(DCE[ci].y), e2 = uni32(DCE[ci].z), e3 = uni32(DCE[ci].w);
-                const bool in_code = tlo + po >= clo && tlo + po < chi;
+                const bool in_code = po >= clo_o && po < chi_o;
                 if (in_code && tag == po) {
                     q1 = e1; q2 = e2; q3 = e3;
                 } else if (!have_dl || dmap_any(dl, clo, chi, dsh, (tlo + po) & ~3ULL, tlo + po + 6)) {
@@ -1769,7 +1770,7 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
             PST(0);
             const uint32_t fl = (q3 >> 8) & 0xFF, kind = (q3 >> 16) & 63;
             // (an invalid entry has kind K_SLOW too: fi_predecode_kernel leaves aux 0,
-            // PRE_AT zeroes it past the text, decoded entries are valid)
+            // the entries past the text are zero, decoded entries are valid)
             if (kind == K_SLOW) break;
 #ifdef FI_TX
             // a block leader (odd pcs: the solo-odd kernel's odd-pc leaders) past the first instruction
@@ -1798,8 +1799,11 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
             uint64_t v = 0, npc = pc + len;
             uint32_t msz = 0;
             bool wr = true, jump = false;   // jump: npc is not the fall-through
-            switch (kind) {
-            case K_ADD: v = av + bv; break;
+            // (add/addi/mv/li and the compressed forms are the most common op:
+            // tested before the compare tree of the switch)
+            if (__builtin_expect(kind == K_ADD, 1)) {
+                v = av + bv;
+            } else switch (kind) {
             case K_LOAD: case K_STORE: {   // the whole access inside one mapped page
                 const bool st = kind == K_STORE;
                 msz = 1u << ((aux >> 12) & 3);

@@ -690,10 +690,11 @@ def test_odd_pc_kernel(engine_factory, oracle_mod, name):
 def test_rewritten_code_loops_bit_exact(engine_factory, oracle_mod, name, ids):
     """The campaign tails: trials whose flipped base pointer stored into the
     text and that then loop through the rewritten code (intmix 64617: 1.33M
-    instructions, 6 clean and 4 rewritten per iteration).  The solo
-    translated body steps the instructions its blocks do not cover in place
-    (S_interp) instead of leaving for the interpreter -- outcomes equal the
-    oracle's."""
+    instructions, 6 clean and 4 rewritten per iteration).  These trials leave
+    the translated blocks at the rewritten instructions for the solo
+    kernel's pre-decoded interpreter (which decodes the trial's own bytes)
+    and come back at the next block leader; the test pins that path against
+    the oracle."""
     e = engine_factory(name)
     o = oracle_for(oracle_mod, name)
     e.set_campaign(0x5EED0002, REGS | PC, 1)
