@@ -152,6 +152,9 @@ struct LaneMem {
     uint32_t nmiss;                // diagnostics: full page-table lookups (TLB misses)
     uint32_t *dl;                  // solo kernel: LDS copy of the slot's rewritten-code map (else NULL)
 };
+// solo_fast_run reads the TLB as tv0..tv3 then tp0..tp3, 8-byte aligned
+static_assert(__builtin_offsetof(LaneMem, tv0) % 8 == 0 &&
+              __builtin_offsetof(LaneMem, tp0) == __builtin_offsetof(LaneMem, tv0) + 32, "LaneMem TLB layout");
 
 // Rewritten code, exactly: DevCtx::dmap holds per slot one bit per
 // 2^dmap_shift-byte granule of [code_lo, code_hi) the lane stored into
@@ -1665,6 +1668,599 @@ struct SoloPreIO {
 typedef __attribute__((address_space(3))) SoloPreIO lds_pio;
 constexpr uint32_t kSoloDC = 64;   // decode-cache entries (power of two)
 
+// ---- the solo interpreter's inner loop in CDNA4 assembly (solo_fast_run).
+// The C++ loop of solo_pre_run costs ~140 machine instructions per guest
+// instruction (a single wave issues one every 4 cycles: ~400 ns); most of it
+// is the guest register file in LDS (address, ds_read, wait, readfirstlane
+// per operand, a ds_write per result) and the compiler's compare tree on the
+// micro-op kind.  Here the 31 guest registers live in VGPRs v64..v127 of the
+// one active lane (x_r = v[64 + 2r] lo, v[65 + 2r] hi), read and written
+// through VGPR index mode (s_set_gpr_idx_on), and everything else is SALU:
+// ~40 instructions for an ALU op.  It runs the common micro-ops -- add / sub
+// / and / or / xor / slt(u) / shifts / mul (also the W forms), aligned in-page
+// loads and stores through a two-entry page cache in front of the lane's TLB,
+// the six branches, jal, jalr -- with the exact rules of solo_pre_run, and
+// leaves to the C++ loop, before the instruction, at anything else (reason 1):
+// another kind, a decode-cache miss in the rewritten window, a page the TLB
+// does not hold, a page crossing, a misaligned access, a store into the code
+// range or to a page the lane has not copied.  Outcomes are those of the C++
+// loop bit for bit (every parity test runs through it).
+struct alignas(16) SoloFastIO {
+    uint32_t po, steps, budget, xticks;     // 0   in/out (budget in)
+    uint32_t fbytes, dbytes, tby, ddlo;     // 16  counters in/out; text bytes; rewritten window lo
+    uint32_t ddhi3, clo_o, csz, gate;       // 32  window hi + 3; code range (text offset, size); leader gate
+    uint32_t lbe, lbo, reason, r_lds;       // 48  leader flag bits (even / odd pc); out: why it left; LDS of R
+    uint32_t dct_lds, dce_lds, tlb_lds, pad;// 64  LDS of the decode cache tags / entries, of LaneMem::tv0
+    uint64_t pre, tlo;                      // 80  pre-decoded text, text base
+    uint64_t clo, cvpn;                     // 96  code range base; page cache (in/out)
+    uint64_t cpg, npc;                      // 112 its page; out: the pc that left the text (reason 3)
+};
+static_assert(sizeof(SoloFastIO) == 128, "SoloFastIO layout");
+typedef __attribute__((address_space(3))) SoloFastIO lds_fio;
+// reasons: 0 budget spent, 1 the instruction at po is the C++ loop's, 2 a
+// block leader stops the run, 3 a jump left the text (npc), 4 the fall-through
+// left the text (po >= tby)
+__device__ __noinline__ void solo_fast_run(lds_fio *io) {
+    const uint32_t a = (uint32_t)(uintptr_t)io;
+    asm volatile(
+        // ---- state in: the io record (LDS) into SGPRs, R into v64..v127
+        "s_mov_b32 s4, m0\n"
+        "v_mov_b32 v31, %[io]\n"
+        "ds_read2_b64 v[0:3], v31 offset0:0 offset1:1\n"
+        "ds_read2_b64 v[4:7], v31 offset0:2 offset1:3\n"
+        "ds_read2_b64 v[8:11], v31 offset0:4 offset1:5\n"
+        "ds_read2_b64 v[12:15], v31 offset0:6 offset1:7\n"
+        "ds_read2_b64 v[16:19], v31 offset0:8 offset1:9\n"
+        "ds_read2_b64 v[20:23], v31 offset0:10 offset1:11\n"
+        "ds_read2_b64 v[24:27], v31 offset0:12 offset1:13\n"
+        "ds_read_b64 v[28:29], v31 offset:112\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_readfirstlane_b32 s5, v0\n"      // po
+        "v_readfirstlane_b32 s6, v1\n"      // steps
+        "v_readfirstlane_b32 s7, v2\n"      // budget
+        "v_readfirstlane_b32 s8, v3\n"      // xticks
+        "v_readfirstlane_b32 s9, v4\n"      // fbytes
+        "v_readfirstlane_b32 s10, v5\n"     // dbytes
+        "v_readfirstlane_b32 s11, v6\n"     // tby
+        "v_readfirstlane_b32 s12, v7\n"     // ddlo
+        "v_readfirstlane_b32 s13, v8\n"     // ddhi + 3
+        "v_readfirstlane_b32 s14, v9\n"     // clo_o
+        "v_readfirstlane_b32 s15, v10\n"    // csz
+        "v_readfirstlane_b32 s16, v11\n"    // gate
+        "v_readfirstlane_b32 s17, v12\n"    // lbe
+        "v_readfirstlane_b32 s18, v13\n"    // lbo
+        "v_readfirstlane_b32 s20, v20\n"    // pre
+        "v_readfirstlane_b32 s21, v21\n"
+        "v_readfirstlane_b32 s22, v22\n"    // tlo
+        "v_readfirstlane_b32 s23, v23\n"
+        "v_readfirstlane_b32 s24, v24\n"    // clo
+        "v_readfirstlane_b32 s25, v25\n"
+        "v_readfirstlane_b32 s26, v26\n"    // cvpn (slot 0)
+        "v_readfirstlane_b32 s27, v27\n"
+        "v_readfirstlane_b32 s28, v28\n"    // cpg
+        "v_readfirstlane_b32 s29, v29\n"
+        // v15 = R, v16 = DCT, v17 = DCE, v18 = &tv0 (LDS addresses; v12..v14 free again)
+        "s_mov_b64 s[70:71], -1\n"          // page cache slot 1: empty
+        "s_mov_b64 s[72:73], 0\n"
+        "ds_read2_b64 v[64:67], v15 offset0:0 offset1:1\n"
+        "ds_read2_b64 v[68:71], v15 offset0:2 offset1:3\n"
+        "ds_read2_b64 v[72:75], v15 offset0:4 offset1:5\n"
+        "ds_read2_b64 v[76:79], v15 offset0:6 offset1:7\n"
+        "ds_read2_b64 v[80:83], v15 offset0:8 offset1:9\n"
+        "ds_read2_b64 v[84:87], v15 offset0:10 offset1:11\n"
+        "ds_read2_b64 v[88:91], v15 offset0:12 offset1:13\n"
+        "ds_read2_b64 v[92:95], v15 offset0:14 offset1:15\n"
+        "ds_read2_b64 v[96:99], v15 offset0:16 offset1:17\n"
+        "ds_read2_b64 v[100:103], v15 offset0:18 offset1:19\n"
+        "ds_read2_b64 v[104:107], v15 offset0:20 offset1:21\n"
+        "ds_read2_b64 v[108:111], v15 offset0:22 offset1:23\n"
+        "ds_read2_b64 v[112:115], v15 offset0:24 offset1:25\n"
+        "ds_read2_b64 v[116:119], v15 offset0:26 offset1:27\n"
+        "ds_read2_b64 v[120:123], v15 offset0:28 offset1:29\n"
+        "ds_read2_b64 v[124:127], v15 offset0:30 offset1:31\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        // ================================================================ loop
+        "L_top%=:\n"
+        "s_cmp_ge_u32 s6, s7\n"
+        "s_cbranch_scc1 L_budget%=\n"
+        // ---- the entry: the decode cache inside the rewritten window, else pre[]
+        "s_add_u32 s62, s5, 6\n"
+        "s_cmp_gt_u32 s62, s12\n"
+        "s_cbranch_scc0 L_pre%=\n"
+        "s_cmp_lt_u32 s5, s13\n"
+        "s_cbranch_scc0 L_pre%=\n"
+        "s_sub_u32 s62, s5, s14\n"          // in the code range?
+        "s_cmp_lt_u32 s62, s15\n"
+        "s_cbranch_scc0 L_slow%=\n"
+        "s_bfe_u32 s62, s5, 0x60001\n"      // ci = (po >> 1) & 63
+        "v_lshl_add_u32 v0, s62, 2, v16\n"
+        "v_lshl_add_u32 v1, s62, 4, v17\n"
+        "ds_read_b32 v2, v0\n"
+        "ds_read2_b64 v[4:7], v1 offset0:0 offset1:1\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_readfirstlane_b32 s62, v2\n"     // tag
+        "v_readfirstlane_b32 s37, v5\n"
+        "v_readfirstlane_b32 s38, v6\n"
+        "v_readfirstlane_b32 s39, v7\n"
+        "s_cmp_eq_u32 s62, s5\n"
+        "s_cbranch_scc0 L_slow%=\n"         // a miss: the C++ loop decodes and fills the cache
+        "s_branch L_have%=\n"
+        "L_pre%=:\n"
+        "s_lshr_b32 s62, s5, 1\n"           // halfword (po >> 1) | (po & 1)
+        "s_and_b32 s63, s5, 1\n"
+        "s_or_b32 s62, s62, s63\n"
+        "s_lshl_b32 s62, s62, 4\n"
+        "s_add_u32 s64, s20, s62\n"
+        "s_addc_u32 s65, s21, 0\n"
+        "s_load_dwordx4 s[36:39], s[64:65], 0x0\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "L_have%=:\n"
+        "s_bfe_u32 s56, s39, 0x60010\n"     // kind
+        "s_cmp_eq_u32 s56, 0\n"
+        "s_cbranch_scc1 L_slow%=\n"
+        "s_bitcmp1_b32 s5, 0\n"             // a block leader the translated code takes
+        "s_cselect_b32 s62, s18, s17\n"
+        "s_bfe_u32 s63, s39, 0x80008\n"
+        "s_and_b32 s62, s62, s63\n"
+        "s_cbranch_scc0 L_nolead%=\n"
+        "s_cmp_ge_u32 s6, s16\n"
+        "s_cbranch_scc1 L_leader%=\n"
+        "L_nolead%=:\n"
+        "s_and_b32 s60, s39, 0xff\n"        // len
+        "s_lshr_b32 s61, s39, 16\n"         // aux
+        "s_bfe_u32 s57, s37, 0x50008\n"     // rd
+        "s_bfe_u32 s58, s37, 0x50010\n"     // rs1
+        "s_bfe_u32 s59, s37, 0x50018\n"     // rs2
+        "s_lshl_b32 s62, s58, 1\n"
+        "s_lshl_b32 s63, s59, 1\n"
+        "s_set_gpr_idx_on s62, gpr_idx(SRC0)\n"
+        "v_mov_b32 v0, v64\n"
+        "v_mov_b32 v1, v65\n"
+        "s_set_gpr_idx_off\n"
+        "s_set_gpr_idx_on s63, gpr_idx(SRC0)\n"
+        "v_mov_b32 v2, v64\n"
+        "v_mov_b32 v3, v65\n"
+        "s_set_gpr_idx_off\n"
+        "s_add_u32 s50, s22, s5\n"          // pc
+        "s_addc_u32 s51, s23, 0\n"
+        "s_ashr_i32 s53, s38, 31\n"         // imm, sign-extended
+        "s_mov_b32 s52, s38\n"
+        "s_mov_b32 s63, 0\n"                // msz (data bytes)
+        "v_readfirstlane_b32 s40, v0\n"     // a = x[rs1]
+        "v_readfirstlane_b32 s41, v1\n"
+        "v_readfirstlane_b32 s42, v2\n"     // b = x[rs2]
+        "v_readfirstlane_b32 s43, v3\n"
+        "s_bitcmp1_b32 s61, 9\n"            // U_APC
+        "s_cselect_b64 s[44:45], s[50:51], s[40:41]\n"
+        "s_bitcmp1_b32 s61, 8\n"            // U_BIMM
+        "s_cselect_b64 s[46:47], s[52:53], s[42:43]\n"
+        // ---- dispatch on the kind (rv64_isa.h Kind)
+        "s_cmp_eq_u32 s56, 1\n"
+        "s_cbranch_scc1 L_add%=\n"
+        "s_cmp_eq_u32 s56, 12\n"
+        "s_cbranch_scc1 L_mem%=\n"
+        "s_cmp_eq_u32 s56, 13\n"
+        "s_cbranch_scc1 L_mem%=\n"
+        "s_sub_u32 s62, s56, 14\n"
+        "s_cmp_lt_u32 s62, 6\n"
+        "s_cbranch_scc1 L_br%=\n"
+        "s_cmp_eq_u32 s56, 20\n"
+        "s_cbranch_scc1 L_jal%=\n"
+        "s_cmp_eq_u32 s56, 21\n"
+        "s_cbranch_scc1 L_jalr%=\n"
+        "s_cmp_eq_u32 s56, 2\n"
+        "s_cbranch_scc1 L_sub%=\n"
+        "s_cmp_eq_u32 s56, 3\n"
+        "s_cbranch_scc1 L_and%=\n"
+        "s_cmp_eq_u32 s56, 4\n"
+        "s_cbranch_scc1 L_or%=\n"
+        "s_cmp_eq_u32 s56, 5\n"
+        "s_cbranch_scc1 L_xor%=\n"
+        "s_cmp_eq_u32 s56, 6\n"
+        "s_cbranch_scc1 L_slt%=\n"
+        "s_cmp_eq_u32 s56, 7\n"
+        "s_cbranch_scc1 L_sltu%=\n"
+        "s_cmp_eq_u32 s56, 8\n"
+        "s_cbranch_scc1 L_sll%=\n"
+        "s_cmp_eq_u32 s56, 9\n"
+        "s_cbranch_scc1 L_srl%=\n"
+        "s_cmp_eq_u32 s56, 10\n"
+        "s_cbranch_scc1 L_sra%=\n"
+        "s_cmp_eq_u32 s56, 11\n"
+        "s_cbranch_scc1 L_mul%=\n"
+        "s_cmp_eq_u32 s56, 22\n"
+        "s_cbranch_scc1 L_nowb%=\n"         // K_NOP
+        "s_branch L_slow%=\n"
+        // ---- ALU
+        "L_add%=:\n"
+        "s_add_u32 s48, s44, s46\n"
+        "s_addc_u32 s49, s45, s47\n"
+        "s_branch L_wb%=\n"
+        "L_sub%=:\n"
+        "s_sub_u32 s48, s44, s46\n"
+        "s_subb_u32 s49, s45, s47\n"
+        "s_branch L_wb%=\n"
+        "L_and%=:\n"
+        "s_and_b64 s[48:49], s[44:45], s[46:47]\n"
+        "s_branch L_wb%=\n"
+        "L_or%=:\n"
+        "s_or_b64 s[48:49], s[44:45], s[46:47]\n"
+        "s_branch L_wb%=\n"
+        "L_xor%=:\n"
+        "s_xor_b64 s[48:49], s[44:45], s[46:47]\n"
+        "s_branch L_wb%=\n"
+        "L_slt%=:\n"                        // signed av < bv
+        "s_mov_b64 s[48:49], 0\n"
+        "s_cmp_lt_i32 s45, s47\n"
+        "s_cbranch_scc1 L_one%=\n"
+        "s_cmp_lg_u32 s45, s47\n"
+        "s_cbranch_scc1 L_wb%=\n"
+        "s_cmp_lt_u32 s44, s46\n"
+        "s_cbranch_scc0 L_wb%=\n"
+        "L_one%=:\n"
+        "s_mov_b32 s48, 1\n"
+        "s_branch L_wb%=\n"
+        "L_sltu%=:\n"                       // unsigned av < bv
+        "s_mov_b64 s[48:49], 0\n"
+        "s_cmp_lt_u32 s45, s47\n"
+        "s_cbranch_scc1 L_one%=\n"
+        "s_cmp_lg_u32 s45, s47\n"
+        "s_cbranch_scc1 L_wb%=\n"
+        "s_cmp_lt_u32 s44, s46\n"
+        "s_cbranch_scc1 L_one%=\n"
+        "s_branch L_wb%=\n"
+        "L_sll%=:\n"                        // av << (bv & shm)
+        "s_bitcmp1_b32 s61, 10\n"           // U_W32: 5-bit amount
+        "s_cselect_b32 s62, 31, 63\n"
+        "s_and_b32 s62, s46, s62\n"
+        "s_lshl_b64 s[48:49], s[44:45], s62\n"
+        "s_branch L_wb%=\n"
+        "L_srl%=:\n"                        // (w32 ? av & 0xffffffff : av) >> (bv & shm)
+        "s_mov_b32 s64, s44\n"
+        "s_bitcmp1_b32 s61, 10\n"
+        "s_cselect_b32 s62, 31, 63\n"
+        "s_cselect_b32 s65, 0, s45\n"
+        "s_and_b32 s62, s46, s62\n"
+        "s_lshr_b64 s[48:49], s[64:65], s62\n"
+        "s_branch L_wb%=\n"
+        "L_sra%=:\n"                        // (w32 ? (int32)av : (int64)av) >> (bv & shm)
+        "s_mov_b32 s64, s44\n"
+        "s_ashr_i32 s66, s44, 31\n"
+        "s_bitcmp1_b32 s61, 10\n"
+        "s_cselect_b32 s62, 31, 63\n"
+        "s_cselect_b32 s65, s66, s45\n"
+        "s_and_b32 s62, s46, s62\n"
+        "s_ashr_i64 s[48:49], s[64:65], s62\n"
+        "s_branch L_wb%=\n"
+        "L_mul%=:\n"                        // low 64 bits of av * bv
+        "s_mul_i32 s48, s44, s46\n"
+        "s_mul_hi_u32 s62, s44, s46\n"
+        "s_mul_i32 s64, s44, s47\n"
+        "s_mul_i32 s65, s45, s46\n"
+        "s_add_u32 s62, s62, s64\n"
+        "s_add_u32 s49, s62, s65\n"
+        "s_branch L_wb%=\n"
+        // ---- branches on a, b (not av / bv): s62 = kind - K_BEQ
+        "L_br%=:\n"
+        "s_cmp_eq_u32 s62, 0\n"
+        "s_cbranch_scc1 L_beq%=\n"
+        "s_cmp_eq_u32 s62, 1\n"
+        "s_cbranch_scc1 L_bne%=\n"
+        "s_cmp_eq_u32 s62, 2\n"
+        "s_cbranch_scc1 L_blt%=\n"
+        "s_cmp_eq_u32 s62, 3\n"
+        "s_cbranch_scc1 L_bge%=\n"
+        "s_cmp_eq_u32 s62, 4\n"
+        "s_cbranch_scc1 L_bltu%=\n"
+        // bgeu: taken unless a <u b
+        "s_cmp_lt_u32 s41, s43\n"
+        "s_cbranch_scc1 L_nowb%=\n"
+        "s_cmp_lg_u32 s41, s43\n"
+        "s_cbranch_scc1 L_taken%=\n"
+        "s_cmp_lt_u32 s40, s42\n"
+        "s_cbranch_scc1 L_nowb%=\n"
+        "s_branch L_taken%=\n"
+        "L_beq%=:\n"
+        "s_cmp_eq_u64 s[40:41], s[42:43]\n"
+        "s_cbranch_scc1 L_taken%=\n"
+        "s_branch L_nowb%=\n"
+        "L_bne%=:\n"
+        "s_cmp_lg_u64 s[40:41], s[42:43]\n"
+        "s_cbranch_scc1 L_taken%=\n"
+        "s_branch L_nowb%=\n"
+        "L_blt%=:\n"
+        "s_cmp_lt_i32 s41, s43\n"
+        "s_cbranch_scc1 L_taken%=\n"
+        "s_cmp_lg_u32 s41, s43\n"
+        "s_cbranch_scc1 L_nowb%=\n"
+        "s_cmp_lt_u32 s40, s42\n"
+        "s_cbranch_scc1 L_taken%=\n"
+        "s_branch L_nowb%=\n"
+        "L_bge%=:\n"
+        "s_cmp_lt_i32 s41, s43\n"
+        "s_cbranch_scc1 L_nowb%=\n"
+        "s_cmp_lg_u32 s41, s43\n"
+        "s_cbranch_scc1 L_taken%=\n"
+        "s_cmp_lt_u32 s40, s42\n"
+        "s_cbranch_scc1 L_nowb%=\n"
+        "s_branch L_taken%=\n"
+        "L_bltu%=:\n"
+        "s_cmp_lt_u32 s41, s43\n"
+        "s_cbranch_scc1 L_taken%=\n"
+        "s_cmp_lg_u32 s41, s43\n"
+        "s_cbranch_scc1 L_nowb%=\n"
+        "s_cmp_lt_u32 s40, s42\n"
+        "s_cbranch_scc1 L_taken%=\n"
+        "s_branch L_nowb%=\n"
+        "L_taken%=:\n"                      // npc = pc + imm
+        "s_add_u32 s50, s50, s52\n"
+        "s_addc_u32 s51, s51, s53\n"
+        "s_branch L_jump%=\n"
+        "L_jal%=:\n"                        // v = pc + len, npc = pc + imm
+        "s_add_u32 s48, s50, s60\n"
+        "s_addc_u32 s49, s51, 0\n"
+        "s_add_u32 s50, s50, s52\n"
+        "s_addc_u32 s51, s51, s53\n"
+        "s_branch L_jwb%=\n"
+        "L_jalr%=:\n"                       // v = pc + len, npc = (a + imm) & ~1
+        "s_add_u32 s48, s50, s60\n"
+        "s_addc_u32 s49, s51, 0\n"
+        "s_add_u32 s50, s40, s52\n"
+        "s_addc_u32 s51, s41, s53\n"
+        "s_and_b32 s50, s50, -2\n"
+        "L_jwb%=:\n"
+        "s_lshl_b32 s62, s57, 1\n"
+        "s_set_gpr_idx_on s62, gpr_idx(DST)\n"
+        "v_mov_b32 v64, s48\n"
+        "v_mov_b32 v65, s49\n"
+        "s_set_gpr_idx_off\n"
+        "v_mov_b32 v64, 0\n"                // x0 stays zero
+        "v_mov_b32 v65, 0\n"
+        "L_jump%=:\n"
+        "s_add_u32 s6, s6, 1\n"             // commit
+        "s_bfe_u32 s62, s39, 0x10009\n"     // straddle tick (kPreStraddle)
+        "s_add_u32 s8, s8, s62\n"
+        "s_add_u32 s9, s9, s60\n"
+        "s_sub_u32 s62, s50, s22\n"         // d = npc - tlo inside the text?
+        "s_subb_u32 s64, s51, s23\n"
+        "s_cmp_lg_u32 s64, 0\n"
+        "s_cbranch_scc1 L_left%=\n"
+        "s_cmp_ge_u32 s62, s11\n"
+        "s_cbranch_scc1 L_left%=\n"
+        "s_mov_b32 s5, s62\n"
+        "s_branch L_top%=\n"
+        // ---- loads and stores: the whole access in one mapped page
+        "L_mem%=:\n"
+        "s_bfe_u32 s54, s61, 0x2000c\n"     // log2 size
+        "s_lshl_b32 s63, 1, s54\n"          // msz
+        "s_add_u32 s64, s40, s52\n"         // ea = a + imm
+        "s_addc_u32 s65, s41, s53\n"
+        "s_lshr_b64 s[66:67], s[64:65], 12\n"
+        "s_cmp_eq_u64 s[66:67], s[26:27]\n"
+        "s_cbranch_scc1 L_pg%=\n"
+        "s_cmp_eq_u64 s[66:67], s[70:71]\n"
+        "s_cbranch_scc0 L_tlb%=\n"
+        "s_mov_b64 s[74:75], s[26:27]\n"    // slot 1 hit: swap the slots
+        "s_mov_b64 s[26:27], s[70:71]\n"
+        "s_mov_b64 s[70:71], s[74:75]\n"
+        "s_mov_b64 s[74:75], s[28:29]\n"
+        "s_mov_b64 s[28:29], s[72:73]\n"
+        "s_mov_b64 s[72:73], s[74:75]\n"
+        "s_branch L_pg%=\n"
+        "L_tlb%=:\n"                        // the lane's TLB (LaneMem tv0..tv3, tp0..tp3)
+        "ds_read2_b64 v[0:3], v18 offset0:0 offset1:1\n"
+        "ds_read2_b64 v[4:7], v18 offset0:2 offset1:3\n"
+        "ds_read2_b64 v[8:11], v18 offset0:4 offset1:5\n"
+        "ds_read2_b64 v[20:23], v18 offset0:6 offset1:7\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_readfirstlane_b32 s68, v0\n"
+        "v_readfirstlane_b32 s69, v1\n"
+        "s_cmp_eq_u64 s[68:69], s[66:67]\n"
+        "s_cbranch_scc1 L_t0%=\n"
+        "v_readfirstlane_b32 s68, v2\n"
+        "v_readfirstlane_b32 s69, v3\n"
+        "s_cmp_eq_u64 s[68:69], s[66:67]\n"
+        "s_cbranch_scc1 L_t1%=\n"
+        "v_readfirstlane_b32 s68, v4\n"
+        "v_readfirstlane_b32 s69, v5\n"
+        "s_cmp_eq_u64 s[68:69], s[66:67]\n"
+        "s_cbranch_scc1 L_t2%=\n"
+        "v_readfirstlane_b32 s68, v6\n"
+        "v_readfirstlane_b32 s69, v7\n"
+        "s_cmp_eq_u64 s[68:69], s[66:67]\n"
+        "s_cbranch_scc0 L_slow%=\n"         // not in the TLB: the C++ loop's full lookup
+        "v_readfirstlane_b32 s68, v22\n"
+        "v_readfirstlane_b32 s69, v23\n"
+        "s_branch L_tins%=\n"
+        "L_t0%=:\n"
+        "v_readfirstlane_b32 s68, v8\n"
+        "v_readfirstlane_b32 s69, v9\n"
+        "s_branch L_tins%=\n"
+        "L_t1%=:\n"
+        "v_readfirstlane_b32 s68, v10\n"
+        "v_readfirstlane_b32 s69, v11\n"
+        "s_branch L_tins%=\n"
+        "L_t2%=:\n"
+        "v_readfirstlane_b32 s68, v20\n"
+        "v_readfirstlane_b32 s69, v21\n"
+        "L_tins%=:\n"                       // slot 1 = slot 0, slot 0 = (vpn, page)
+        "s_mov_b64 s[70:71], s[26:27]\n"
+        "s_mov_b64 s[72:73], s[28:29]\n"
+        "s_mov_b64 s[26:27], s[66:67]\n"
+        "s_mov_b64 s[28:29], s[68:69]\n"
+        "L_pg%=:\n"
+        "s_and_b32 s78, s64, 0xfff\n"       // offset in the page
+        "s_add_u32 s62, s78, s63\n"
+        "s_cmp_gt_u32 s62, 0x1000\n"
+        "s_cbranch_scc1 L_slow%=\n"         // crosses the page
+        "s_sub_u32 s62, s63, 1\n"
+        "s_and_b32 s62, s78, s62\n"
+        "s_cbranch_scc1 L_slow%=\n"         // misaligned
+        "s_and_b32 s76, s28, -2\n"          // address in the page
+        "s_mov_b32 s77, s29\n"
+        "s_add_u32 s76, s76, s78\n"
+        "s_addc_u32 s77, s77, 0\n"
+        "v_mov_b32 v0, s76\n"
+        "v_mov_b32 v1, s77\n"
+        "s_cmp_eq_u32 s56, 13\n"
+        "s_cbranch_scc1 L_st%=\n"
+        // load
+        "s_cmp_eq_u32 s54, 3\n"
+        "s_cbranch_scc1 L_ld8%=\n"
+        "s_cmp_eq_u32 s54, 2\n"
+        "s_cbranch_scc1 L_ld4%=\n"
+        "s_cmp_eq_u32 s54, 1\n"
+        "s_cbranch_scc1 L_ld2%=\n"
+        "global_load_ubyte v2, v[0:1], off\n"
+        "s_branch L_ldn%=\n"
+        "L_ld2%=:\n"
+        "global_load_ushort v2, v[0:1], off\n"
+        "s_branch L_ldn%=\n"
+        "L_ld4%=:\n"
+        "global_load_dword v2, v[0:1], off\n"
+        "s_branch L_ldn%=\n"
+        "L_ld8%=:\n"
+        "global_load_dwordx2 v[2:3], v[0:1], off\n"
+        "s_waitcnt vmcnt(0)\n"
+        "v_readfirstlane_b32 s48, v2\n"
+        "v_readfirstlane_b32 s49, v3\n"
+        "s_branch L_wb%=\n"
+        "L_ldn%=:\n"                        // 1, 2 or 4 bytes: zero- or sign-extended (U_SEXT)
+        "s_waitcnt vmcnt(0)\n"
+        "v_readfirstlane_b32 s48, v2\n"
+        "s_mov_b32 s49, 0\n"
+        "s_bitcmp1_b32 s61, 11\n"
+        "s_cbranch_scc0 L_wb%=\n"
+        "s_lshl_b32 s62, s63, 19\n"         // width 8 * msz, offset 0
+        "s_bfe_i64 s[48:49], s[48:49], s62\n"
+        "s_branch L_wb%=\n"
+        // store: a page the lane owns, nothing of the code range
+        "L_st%=:\n"
+        "s_bitcmp1_b32 s28, 0\n"
+        "s_cbranch_scc0 L_slow%=\n"
+        "s_add_u32 s74, s64, s63\n"         // u = ea + msz - 1 - clo
+        "s_addc_u32 s75, s65, 0\n"
+        "s_sub_u32 s74, s74, 1\n"
+        "s_subb_u32 s75, s75, 0\n"
+        "s_sub_u32 s74, s74, s24\n"
+        "s_subb_u32 s75, s75, s25\n"
+        "s_cmp_lg_u32 s75, 0\n"
+        "s_cbranch_scc1 L_stok%=\n"
+        "s_add_u32 s62, s15, s63\n"         // overlaps [clo, clo + csz) iff u < csz + msz - 1
+        "s_sub_u32 s62, s62, 1\n"
+        "s_cmp_lt_u32 s74, s62\n"
+        "s_cbranch_scc1 L_slow%=\n"
+        "L_stok%=:\n"
+        "v_mov_b32 v2, s42\n"
+        "v_mov_b32 v3, s43\n"
+        "s_cmp_eq_u32 s54, 3\n"
+        "s_cbranch_scc1 L_st8%=\n"
+        "s_cmp_eq_u32 s54, 2\n"
+        "s_cbranch_scc1 L_st4%=\n"
+        "s_cmp_eq_u32 s54, 1\n"
+        "s_cbranch_scc1 L_st2%=\n"
+        "global_store_byte v[0:1], v2, off\n"
+        "s_branch L_std%=\n"
+        "L_st2%=:\n"
+        "global_store_short v[0:1], v2, off\n"
+        "s_branch L_std%=\n"
+        "L_st4%=:\n"
+        "global_store_dword v[0:1], v2, off\n"
+        "s_branch L_std%=\n"
+        "L_st8%=:\n"
+        "global_store_dwordx2 v[0:1], v[2:3], off\n"
+        "L_std%=:\n"
+        "s_nop 1\n"
+        "s_branch L_nowb%=\n"
+        // ---- write back x[rd] (w32: sign-extended low word), then fall through
+        "L_wb%=:\n"
+        "s_bitcmp1_b32 s61, 10\n"
+        "s_cbranch_scc0 L_wb64%=\n"
+        "s_ashr_i32 s49, s48, 31\n"
+        "L_wb64%=:\n"
+        "s_lshl_b32 s62, s57, 1\n"
+        "s_set_gpr_idx_on s62, gpr_idx(DST)\n"
+        "v_mov_b32 v64, s48\n"
+        "v_mov_b32 v65, s49\n"
+        "s_set_gpr_idx_off\n"
+        "v_mov_b32 v64, 0\n"
+        "v_mov_b32 v65, 0\n"
+        "L_nowb%=:\n"
+        "s_add_u32 s6, s6, 1\n"             // commit
+        "s_bfe_u32 s62, s39, 0x10009\n"
+        "s_add_u32 s8, s8, s62\n"
+        "s_add_u32 s9, s9, s60\n"
+        "s_add_u32 s10, s10, s63\n"
+        "s_add_u32 s5, s5, s60\n"           // the fall-through
+        "s_cmp_lt_u32 s5, s11\n"
+        "s_cbranch_scc1 L_top%=\n"
+        "s_mov_b32 s19, 4\n"
+        "s_branch L_out%=\n"
+        // ================================================================ exits
+        "L_left%=:\n"
+        "s_mov_b32 s19, 3\n"
+        "s_branch L_out%=\n"
+        "L_budget%=:\n"
+        "s_mov_b32 s19, 0\n"
+        "s_branch L_out%=\n"
+        "L_leader%=:\n"
+        "s_mov_b32 s19, 2\n"
+        "s_branch L_out%=\n"
+        "L_slow%=:\n"
+        "s_mov_b32 s19, 1\n"
+        "L_out%=:\n"
+        "v_mov_b32 v0, s5\n"
+        "v_mov_b32 v1, s6\n"
+        "v_mov_b32 v2, s8\n"
+        "v_mov_b32 v3, s9\n"
+        "v_mov_b32 v4, s10\n"
+        "v_mov_b32 v5, s19\n"
+        "v_mov_b32 v6, s26\n"
+        "v_mov_b32 v7, s27\n"
+        "v_mov_b32 v8, s28\n"
+        "v_mov_b32 v9, s29\n"
+        "v_mov_b32 v10, s50\n"
+        "v_mov_b32 v11, s51\n"
+        "ds_write2_b32 v31, v0, v1 offset0:0 offset1:1\n"
+        "ds_write2_b32 v31, v2, v3 offset0:3 offset1:4\n"
+        "ds_write_b32 v31, v4 offset:20\n"
+        "ds_write_b32 v31, v5 offset:56\n"
+        "ds_write2_b64 v31, v[6:7], v[8:9] offset0:13 offset1:14\n"
+        "ds_write_b64 v31, v[10:11] offset:120\n"
+        "ds_write2_b64 v15, v[64:65], v[66:67] offset0:0 offset1:1\n"
+        "ds_write2_b64 v15, v[68:69], v[70:71] offset0:2 offset1:3\n"
+        "ds_write2_b64 v15, v[72:73], v[74:75] offset0:4 offset1:5\n"
+        "ds_write2_b64 v15, v[76:77], v[78:79] offset0:6 offset1:7\n"
+        "ds_write2_b64 v15, v[80:81], v[82:83] offset0:8 offset1:9\n"
+        "ds_write2_b64 v15, v[84:85], v[86:87] offset0:10 offset1:11\n"
+        "ds_write2_b64 v15, v[88:89], v[90:91] offset0:12 offset1:13\n"
+        "ds_write2_b64 v15, v[92:93], v[94:95] offset0:14 offset1:15\n"
+        "ds_write2_b64 v15, v[96:97], v[98:99] offset0:16 offset1:17\n"
+        "ds_write2_b64 v15, v[100:101], v[102:103] offset0:18 offset1:19\n"
+        "ds_write2_b64 v15, v[104:105], v[106:107] offset0:20 offset1:21\n"
+        "ds_write2_b64 v15, v[108:109], v[110:111] offset0:22 offset1:23\n"
+        "ds_write2_b64 v15, v[112:113], v[114:115] offset0:24 offset1:25\n"
+        "ds_write2_b64 v15, v[116:117], v[118:119] offset0:26 offset1:27\n"
+        "ds_write2_b64 v15, v[120:121], v[122:123] offset0:28 offset1:29\n"
+        "ds_write2_b64 v15, v[124:125], v[126:127] offset0:30 offset1:31\n"
+        "s_waitcnt vmcnt(0) lgkmcnt(0)\n"
+        "s_mov_b32 m0, s4\n"
+        :
+        : [io] "v"(a)
+        : "s4", "s5", "s6", "s7", "s8", "s9", "s10", "s11", "s12", "s13", "s14", "s15", "s16", "s17", "s18", "s19",
+          "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "s28", "s29",
+          "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50",
+          "s51", "s52", "s53", "s54", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",
+          "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78",
+          "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
+          "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
+          "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77",
+          "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92",
+          "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106",
+          "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119",
+          "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", "memory");
+}
+
 // 64-bit unsigned / signed compares of uniform values on the scalar unit
 // (SALU compares are 32-bit; a 64-bit one otherwise goes through VALU + VCC)
 __device__ __forceinline__ bool slt64(uint64_t a, uint64_t b) {
@@ -1738,8 +2334,41 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
     } while (0)
         uint32_t q1, q2, q3;
         PRE_AT(po, q1, q2, q3);
+#ifndef FI_PROF
+        // the assembly inner loop (solo_fast_run) takes over once a run has
+        // gone 8 instructions (short runs stay here: its entry costs ~200
+        // instructions), and again after each instruction it hands back
+        uint32_t fast_at = 8;
+        __shared__ SoloFastIO fio[1];
+#endif
         while (steps < budget) {
             PST(3);
+#ifndef FI_PROF
+            if (steps >= fast_at && watch <= 0) {
+                lds_fio *F = (lds_fio *)fio;
+                F->po = po; F->steps = steps; F->budget = budget; F->xticks = xticks;
+                F->fbytes = fbytes; F->dbytes = dbytes; F->tby = tby; F->ddlo = ddlo;
+                F->ddhi3 = ddhi + 3u; F->clo_o = clo_o; F->csz = chi_o - clo_o;
+#ifdef FI_TX
+                F->gate = tx_gate1; F->lbe = kPreLeader; F->lbo = kOdd ? kPreOddLeader : 0u;
+#else
+                F->gate = 0xFFFFFFFFu; F->lbe = 0; F->lbo = 0;
+#endif
+                F->r_lds = (uint32_t)(uintptr_t)R; F->dct_lds = (uint32_t)(uintptr_t)DCT;
+                F->dce_lds = (uint32_t)(uintptr_t)DCE; F->tlb_lds = (uint32_t)(uintptr_t)&mp->tv0;
+                F->pre = (uint64_t)(uintptr_t)CX->pre; F->tlo = tlo; F->clo = clo; F->cvpn = cvpn; F->cpg = cpg;
+                solo_fast_run(F);
+                po = uni32(F->po); steps = uni32(F->steps); xticks = uni32(F->xticks);
+                fbytes = uni32(F->fbytes); dbytes = uni32(F->dbytes);
+                cvpn = uni64(F->cvpn); cpg = uni64(F->cpg);
+                const uint32_t why = uni32(F->reason);
+                if (why == 3) { spc = uni64(F->npc); goto leave; }   // a jump left the text
+                if (why == 4) { spc = tlo + po; goto leave; }         // so did the fall-through
+                if (why == 0) break;                                  // budget spent
+                PRE_AT(po, q1, q2, q3);                               // the instruction it hands back
+                fast_at = steps + 1;
+            }
+#endif
             // ---- rewritten bytes under this instruction: the decode cache
             // (an entry is the decode of the lane's current bytes: stores drop
             // the entries they overlap), else the lane's own bytes, decoded
@@ -1765,6 +2394,9 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
                         DCT[ci] = po;
                         DCE[ci].x = dd.raw; DCE[ci].y = q1; DCE[ci].z = q2; DCE[ci].w = q3;
                     }
+                } else if (in_code) {   // clean bytes in the window: the pre-decoded entry, cached for solo_fast_run
+                    DCT[ci] = po;
+                    DCE[ci].x = pre[4 * ((po >> 1) | (po & 1u))]; DCE[ci].y = q1; DCE[ci].z = q2; DCE[ci].w = q3;
                 }
             }
             PST(0);
@@ -2123,7 +2755,7 @@ __device__ __forceinline__ void trial_body() {
     // it overlaps, so a hit equals a fresh fetch + decode.
     constexpr uint32_t kDC = kNL == 1 ? 64u : 1u;
     __shared__ uint32_t DCT[kDC];   // tag: pc - text_lo (0xFFFFFFFF empty)
-    __shared__ Pre4 DCE[kDC];
+    __shared__ alignas(16) Pre4 DCE[kDC];
     if constexpr (kNL == 1) {
 #pragma unroll 8
         for (uint32_t k = 0; k < kDC; k++) DCT[k] = 0xFFFFFFFFu;
