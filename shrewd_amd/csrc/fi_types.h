@@ -231,6 +231,7 @@ struct DevCtx {
                                      // [27] register faults dead at injection [30] trials re-run with more private
                                      // pages (FI_ESC_RESOURCE, fi_engine.cpp run_chunk)
                                      // [52] record mode: 1 + numInst of the golden run's last curTick read
+                                     // [53] solo_fast_run calls [54] instructions they ran [55] hand-backs
                                      // [32..39] FI_PROF phase cycles
                                      // [40 + 4k + {0,1,2,3}] fetch B, data B, pages, device insts of kernel k
                                      // (0 the 64-lane kernel, 1 solo, 2 solo-odd)

@@ -1676,12 +1676,13 @@ constexpr uint32_t kSoloDC = 64;   // decode-cache entries (power of two)
 // micro-op kind.  Here the 31 guest registers live in VGPRs v64..v127 of the
 // one active lane (x_r = v[64 + 2r] lo, v[65 + 2r] hi), read and written
 // through VGPR index mode (s_set_gpr_idx_on), and everything else is SALU:
-// ~40 instructions for an ALU op.  It runs the common micro-ops -- add / sub
-// / and / or / xor / slt(u) / shifts / mul (also the W forms), aligned in-page
-// loads and stores through a two-entry page cache in front of the lane's TLB,
-// the six branches, jal, jalr -- with the exact rules of solo_pre_run, and
-// leaves to the C++ loop, before the instruction, at anything else (reason 1):
-// another kind, a decode-cache miss in the rewritten window, a page the TLB
+// ~40 instructions for an ALU op, the kind dispatched through a jump table.
+// It runs every micro-op but K_SLOW -- add / sub / and / or / xor / slt(u) /
+// shifts / mul / mulh(s)(u) / div(u) / rem(u) (also the W forms), aligned
+// in-page loads and stores through a two-entry page cache in front of the
+// lane's TLB, the six branches, jal, jalr -- with the exact rules of
+// solo_pre_run, and leaves to the C++ loop, before the instruction, at
+// anything else (reason 1): K_SLOW, a decode-cache miss in the rewritten window, a page the TLB
 // does not hold, a page crossing, a misaligned access, a store into the code
 // range or to a page the lane has not copied.  Outcomes are those of the C++
 // loop bit for bit (every parity test runs through it).
@@ -1740,6 +1741,10 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "v_readfirstlane_b32 s28, v28\n"    // cpg
         "v_readfirstlane_b32 s29, v29\n"
         // v15 = R, v16 = DCT, v17 = DCE, v18 = &tv0 (LDS addresses; v12..v14 free again)
+        "s_getpc_b64 s[80:81]\n"            // the jump table's address
+        "L_gp%=:\n"
+        "s_add_u32 s80, s80, L_jt%= - L_gp%=\n"
+        "s_addc_u32 s81, s81, 0\n"
         "s_mov_b64 s[70:71], -1\n"          // page cache slot 1: empty
         "s_mov_b64 s[72:73], 0\n"
         "ds_read2_b64 v[64:67], v15 offset0:0 offset1:1\n"
@@ -1835,42 +1840,47 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_bitcmp1_b32 s61, 8\n"            // U_BIMM
         "s_cselect_b64 s[46:47], s[52:53], s[42:43]\n"
         // ---- dispatch on the kind (rv64_isa.h Kind)
+        // (add first: the most frequent kind; the rest through a jump table
+        // of s_branch instructions, one per kind, at s[80:81])
         "s_cmp_eq_u32 s56, 1\n"
         "s_cbranch_scc1 L_add%=\n"
-        "s_cmp_eq_u32 s56, 12\n"
-        "s_cbranch_scc1 L_mem%=\n"
-        "s_cmp_eq_u32 s56, 13\n"
-        "s_cbranch_scc1 L_mem%=\n"
-        "s_sub_u32 s62, s56, 14\n"
-        "s_cmp_lt_u32 s62, 6\n"
-        "s_cbranch_scc1 L_br%=\n"
-        "s_cmp_eq_u32 s56, 20\n"
-        "s_cbranch_scc1 L_jal%=\n"
-        "s_cmp_eq_u32 s56, 21\n"
-        "s_cbranch_scc1 L_jalr%=\n"
-        "s_cmp_eq_u32 s56, 2\n"
-        "s_cbranch_scc1 L_sub%=\n"
-        "s_cmp_eq_u32 s56, 3\n"
-        "s_cbranch_scc1 L_and%=\n"
-        "s_cmp_eq_u32 s56, 4\n"
-        "s_cbranch_scc1 L_or%=\n"
-        "s_cmp_eq_u32 s56, 5\n"
-        "s_cbranch_scc1 L_xor%=\n"
-        "s_cmp_eq_u32 s56, 6\n"
-        "s_cbranch_scc1 L_slt%=\n"
-        "s_cmp_eq_u32 s56, 7\n"
-        "s_cbranch_scc1 L_sltu%=\n"
-        "s_cmp_eq_u32 s56, 8\n"
-        "s_cbranch_scc1 L_sll%=\n"
-        "s_cmp_eq_u32 s56, 9\n"
-        "s_cbranch_scc1 L_srl%=\n"
-        "s_cmp_eq_u32 s56, 10\n"
-        "s_cbranch_scc1 L_sra%=\n"
-        "s_cmp_eq_u32 s56, 11\n"
-        "s_cbranch_scc1 L_mul%=\n"
-        "s_cmp_eq_u32 s56, 22\n"
-        "s_cbranch_scc1 L_nowb%=\n"         // K_NOP
-        "s_branch L_slow%=\n"
+        "s_cmp_gt_u32 s56, 29\n"
+        "s_cbranch_scc1 L_slow%=\n"
+        "s_lshl_b32 s62, s56, 2\n"
+        "s_add_u32 s64, s80, s62\n"
+        "s_addc_u32 s65, s81, 0\n"
+        "s_setpc_b64 s[64:65]\n"
+        "L_jt%=:\n"
+        "s_branch L_slow%=\n"               // 0 K_SLOW
+        "s_branch L_add%=\n"                // 1 K_ADD
+        "s_branch L_sub%=\n"
+        "s_branch L_and%=\n"
+        "s_branch L_or%=\n"
+        "s_branch L_xor%=\n"
+        "s_branch L_slt%=\n"
+        "s_branch L_sltu%=\n"
+        "s_branch L_sll%=\n"
+        "s_branch L_srl%=\n"
+        "s_branch L_sra%=\n"
+        "s_branch L_mul%=\n"                // 11 K_MUL
+        "s_branch L_mem%=\n"                // 12 K_LOAD
+        "s_branch L_mem%=\n"                // 13 K_STORE
+        "s_branch L_beq%=\n"                // 14 K_BEQ
+        "s_branch L_bne%=\n"
+        "s_branch L_blt%=\n"
+        "s_branch L_bge%=\n"
+        "s_branch L_bltu%=\n"
+        "s_branch L_bgeu%=\n"               // 19 K_BGEU
+        "s_branch L_jal%=\n"                // 20 K_JAL
+        "s_branch L_jalr%=\n"               // 21 K_JALR
+        "s_branch L_nowb%=\n"               // 22 K_NOP
+        "s_branch L_mulh%=\n"               // 23 K_MULH
+        "s_branch L_mulhu%=\n"
+        "s_branch L_mulhsu%=\n"
+        "s_branch L_div%=\n"                // 26 K_DIV
+        "s_branch L_divu%=\n"
+        "s_branch L_rem%=\n"
+        "s_branch L_remu%=\n"               // 29 K_REMU
         // ---- ALU
         "L_add%=:\n"
         "s_add_u32 s48, s44, s46\n"
@@ -1940,19 +1950,268 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_add_u32 s62, s62, s64\n"
         "s_add_u32 s49, s62, s65\n"
         "s_branch L_wb%=\n"
-        // ---- branches on a, b (not av / bv): s62 = kind - K_BEQ
-        "L_br%=:\n"
-        "s_cmp_eq_u32 s62, 0\n"
-        "s_cbranch_scc1 L_beq%=\n"
-        "s_cmp_eq_u32 s62, 1\n"
-        "s_cbranch_scc1 L_bne%=\n"
-        "s_cmp_eq_u32 s62, 2\n"
-        "s_cbranch_scc1 L_blt%=\n"
-        "s_cmp_eq_u32 s62, 3\n"
-        "s_cbranch_scc1 L_bge%=\n"
-        "s_cmp_eq_u32 s62, 4\n"
-        "s_cbranch_scc1 L_bltu%=\n"
-        // bgeu: taken unless a <u b
+        // ---- M extension.  mulh*: the high word of the 128-bit product from
+        // 32-bit partial products, then the signed corrections (a < 0: - b,
+        // b < 0: - a).  div* / rem*: RISC-V rules (x / 0 = ~0, x % 0 = x,
+        // overflow through the unsigned magnitudes); W forms on the sign- or
+        // zero-extended low words (L_wb sign-extends the result).  The
+        // unsigned core is the compiler's expansion of a uniform u64 divide
+        // (reciprocal estimate + two refinements + two corrections), with a
+        // 32-bit short path.
+        "L_mulhu%=:\n"
+        "s_mov_b32 s36, 0\n"
+        "s_branch L_mh%=\n"
+        "L_mulh%=:\n"
+        "s_mov_b32 s36, 3\n"
+        "s_branch L_mh%=\n"
+        "L_mulhsu%=:\n"
+        "s_mov_b32 s36, 1\n"
+        "L_mh%=:\n"
+        "s_mul_hi_u32 s62, s44, s46\n"     // hi(a0 b0)
+        "s_mul_i32 s64, s44, s47\n"        // a0 b1
+        "s_mul_hi_u32 s65, s44, s47\n"
+        "s_mul_i32 s66, s45, s46\n"        // a1 b0
+        "s_mul_hi_u32 s67, s45, s46\n"
+        "s_mul_i32 s68, s45, s47\n"        // a1 b1
+        "s_mul_hi_u32 s69, s45, s47\n"
+        "s_add_u32 s62, s62, s64\n"        // carries out of bits 32..63
+        "s_addc_u32 s65, s65, 0\n"
+        "s_add_u32 s62, s62, s66\n"
+        "s_addc_u32 s67, s67, 0\n"
+        "s_add_u32 s48, s68, s65\n"
+        "s_addc_u32 s49, s69, 0\n"
+        "s_add_u32 s48, s48, s67\n"
+        "s_addc_u32 s49, s49, 0\n"
+        "s_bitcmp1_b32 s36, 0\n"           // signed a (mulh, mulhsu): a < 0 -> - b
+        "s_cbranch_scc0 L_wb%=\n"
+        "s_cmp_lt_i32 s45, 0\n"
+        "s_cselect_b64 s[64:65], s[46:47], 0\n"
+        "s_sub_u32 s48, s48, s64\n"
+        "s_subb_u32 s49, s49, s65\n"
+        "s_bitcmp1_b32 s36, 1\n"           // signed b (mulh): b < 0 -> - a
+        "s_cbranch_scc0 L_wb%=\n"
+        "s_cmp_lt_i32 s47, 0\n"
+        "s_cselect_b64 s[64:65], s[44:45], 0\n"
+        "s_sub_u32 s48, s48, s64\n"
+        "s_subb_u32 s49, s49, s65\n"
+        "s_branch L_wb%=\n"
+        // s36: bit 0 remainder, bit 1 signed
+        "L_divu%=:\n"
+        "s_mov_b32 s36, 0\n"
+        "s_branch L_dv%=\n"
+        "L_div%=:\n"
+        "s_mov_b32 s36, 2\n"
+        "s_branch L_dv%=\n"
+        "L_rem%=:\n"
+        "s_mov_b32 s36, 3\n"
+        "s_branch L_dv%=\n"
+        "L_remu%=:\n"
+        "s_mov_b32 s36, 1\n"
+        "L_dv%=:\n"
+        "s_mov_b64 s[64:65], s[44:45]\n"   // N, D
+        "s_mov_b64 s[66:67], s[46:47]\n"
+        "s_bitcmp1_b32 s61, 10\n"          // U_W32: the low words, sign- or zero-extended
+        "s_cbranch_scc0 L_dv64%=\n"
+        "s_ashr_i32 s65, s64, 31\n"
+        "s_ashr_i32 s67, s66, 31\n"
+        "s_bitcmp1_b32 s36, 1\n"
+        "s_cbranch_scc1 L_dv64%=\n"
+        "s_mov_b32 s65, 0\n"
+        "s_mov_b32 s67, 0\n"
+        "L_dv64%=:\n"
+        "s_cmp_lg_u64 s[66:67], 0\n"
+        "s_cbranch_scc1 L_dvnz%=\n"
+        "s_mov_b64 s[68:69], -1\n"         // x / 0 = ~0, x % 0 = x
+        "s_mov_b64 s[74:75], s[64:65]\n"
+        "s_branch L_dvsel%=\n"
+        "L_dvnz%=:\n"
+        "s_mov_b32 s52, 0\n"               // negate the quotient / the remainder
+        "s_mov_b32 s53, 0\n"
+        "s_bitcmp1_b32 s36, 1\n"
+        "s_cbranch_scc0 L_dvu%=\n"
+        "s_cmp_lt_i32 s65, 0\n"
+        "s_cbranch_scc0 L_dvpa%=\n"
+        "s_sub_u32 s64, 0, s64\n"
+        "s_subb_u32 s65, 0, s65\n"
+        "s_mov_b32 s53, 1\n"
+        "s_mov_b32 s52, 1\n"
+        "L_dvpa%=:\n"
+        "s_cmp_lt_i32 s67, 0\n"
+        "s_cbranch_scc0 L_dvu%=\n"
+        "s_sub_u32 s66, 0, s66\n"
+        "s_subb_u32 s67, 0, s67\n"
+        "s_xor_b32 s52, s52, 1\n"
+        "L_dvu%=:\n"
+        "s_mov_b64 s[44:45], s[64:65]\n"   // |N|, |D| (the core consumes its inputs)
+        "s_mov_b64 s[46:47], s[66:67]\n"
+        "s_or_b32 s62, s65, s67\n"
+        "s_cmp_lg_u32 s62, 0\n"
+        "s_cbranch_scc0 L_dv32%=\n"
+        "v_cvt_f32_u32 v0, s66\n"
+        "v_cvt_f32_u32 v1, s67\n"
+        "s_sub_u32 s74, 0, s66\n"
+        "s_subb_u32 s75, 0, s67\n"
+        "v_fmamk_f32 v0, v1, 0x4f800000, v0\n"
+        "v_rcp_f32 v0, v0\n"
+        "s_nop 0\n"
+        "v_mul_f32 v0, 0x5f7ffffc, v0\n"
+        "v_mul_f32 v1, 0x2f800000, v0\n"
+        "v_trunc_f32 v1, v1\n"
+        "v_fmamk_f32 v0, v1, 0xcf800000, v0\n"
+        "v_cvt_u32_f32 v1, v1\n"
+        "v_cvt_u32_f32 v0, v0\n"
+        "v_readfirstlane_b32 s76, v1\n"
+        "v_readfirstlane_b32 s68, v0\n"
+        "s_mul_i32 s69, s74, s76\n"
+        "s_mul_hi_u32 s78, s74, s68\n"
+        "s_mul_i32 s77, s75, s68\n"
+        "s_add_i32 s69, s78, s69\n"
+        "s_add_i32 s69, s69, s77\n"
+        "s_mul_i32 s37, s74, s68\n"
+        "s_mul_i32 s78, s68, s69\n"
+        "s_mul_hi_u32 s38, s68, s37\n"
+        "s_mul_hi_u32 s77, s68, s69\n"
+        "s_add_u32 s78, s38, s78\n"
+        "s_addc_u32 s77, 0, s77\n"
+        "s_mul_hi_u32 s40, s76, s37\n"
+        "s_mul_i32 s37, s76, s37\n"
+        "s_add_u32 s78, s78, s37\n"
+        "s_mul_hi_u32 s38, s76, s69\n"
+        "s_addc_u32 s77, s77, s40\n"
+        "s_addc_u32 s78, s38, 0\n"
+        "s_mul_i32 s69, s76, s69\n"
+        "s_add_u32 s69, s77, s69\n"
+        "s_addc_u32 s77, 0, s78\n"
+        "s_add_u32 s78, s68, s69\n"
+        "s_cselect_b64 s[68:69], -1, 0\n"
+        "s_cmp_lg_u64 s[68:69], 0\n"
+        "s_addc_u32 s76, s76, s77\n"
+        "s_mul_i32 s68, s74, s76\n"
+        "s_mul_hi_u32 s69, s74, s78\n"
+        "s_add_i32 s68, s69, s68\n"
+        "s_mul_i32 s75, s75, s78\n"
+        "s_add_i32 s68, s68, s75\n"
+        "s_mul_i32 s74, s74, s78\n"
+        "s_mul_hi_u32 s75, s76, s74\n"
+        "s_mul_i32 s77, s76, s74\n"
+        "s_mul_i32 s38, s78, s68\n"
+        "s_mul_hi_u32 s74, s78, s74\n"
+        "s_mul_hi_u32 s37, s78, s68\n"
+        "s_add_u32 s74, s74, s38\n"
+        "s_addc_u32 s37, 0, s37\n"
+        "s_add_u32 s74, s74, s77\n"
+        "s_mul_hi_u32 s69, s76, s68\n"
+        "s_addc_u32 s74, s37, s75\n"
+        "s_addc_u32 s69, s69, 0\n"
+        "s_mul_i32 s68, s76, s68\n"
+        "s_add_u32 s68, s74, s68\n"
+        "s_addc_u32 s74, 0, s69\n"
+        "s_add_u32 s75, s78, s68\n"
+        "s_cselect_b64 s[68:69], -1, 0\n"
+        "s_cmp_lg_u64 s[68:69], 0\n"
+        "s_addc_u32 s68, s76, s74\n"
+        "s_mul_i32 s74, s64, s68\n"
+        "s_mul_hi_u32 s76, s64, s75\n"
+        "s_mul_hi_u32 s69, s64, s68\n"
+        "s_add_u32 s74, s76, s74\n"
+        "s_addc_u32 s69, 0, s69\n"
+        "s_mul_hi_u32 s77, s65, s75\n"
+        "s_mul_i32 s75, s65, s75\n"
+        "s_add_u32 s74, s74, s75\n"
+        "s_mul_hi_u32 s76, s65, s68\n"
+        "s_addc_u32 s69, s69, s77\n"
+        "s_addc_u32 s74, s76, 0\n"
+        "s_mul_i32 s68, s65, s68\n"
+        "s_add_u32 s76, s69, s68\n"
+        "s_addc_u32 s77, 0, s74\n"
+        "s_mul_i32 s68, s66, s77\n"
+        "s_mul_hi_u32 s69, s66, s76\n"
+        "s_add_i32 s68, s69, s68\n"
+        "s_mul_i32 s69, s67, s76\n"
+        "s_add_i32 s78, s68, s69\n"
+        "s_sub_i32 s74, s65, s78\n"
+        "s_mul_i32 s68, s66, s76\n"
+        "s_sub_u32 s37, s64, s68\n"
+        "s_cselect_b64 s[68:69], -1, 0\n"
+        "s_cmp_lg_u64 s[68:69], 0\n"
+        "s_subb_u32 s38, s74, s67\n"
+        "s_sub_u32 s40, s37, s66\n"
+        "s_cselect_b64 s[74:75], -1, 0\n"
+        "s_cmp_lg_u64 s[74:75], 0\n"
+        "s_subb_u32 s74, s38, 0\n"
+        "s_cmp_ge_u32 s74, s67\n"
+        "s_cselect_b32 s75, -1, 0\n"
+        "s_cmp_ge_u32 s40, s66\n"
+        "s_cselect_b32 s38, -1, 0\n"
+        "s_cmp_eq_u32 s74, s67\n"
+        "s_cselect_b32 s74, s38, s75\n"
+        "s_add_u32 s75, s76, 1\n"
+        "s_addc_u32 s38, s77, 0\n"
+        "s_add_u32 s40, s76, 2\n"
+        "s_addc_u32 s41, s77, 0\n"
+        "s_cmp_lg_u32 s74, 0\n"
+        "s_cselect_b32 s74, s40, s75\n"
+        "s_cselect_b32 s75, s41, s38\n"
+        "s_cmp_lg_u64 s[68:69], 0\n"
+        "s_subb_u32 s65, s65, s78\n"
+        "s_cmp_ge_u32 s65, s67\n"
+        "s_cselect_b32 s68, -1, 0\n"
+        "s_cmp_ge_u32 s37, s66\n"
+        "s_cselect_b32 s69, -1, 0\n"
+        "s_cmp_eq_u32 s65, s67\n"
+        "s_cselect_b32 s67, s69, s68\n"
+        "s_cmp_lg_u32 s67, 0\n"
+        "s_cselect_b32 s69, s75, s77\n"
+        "s_cselect_b32 s68, s74, s76\n"
+        "s_branch L_dvr%=\n"
+        "L_dv32%=:\n"
+        "v_cvt_f32_u32 v0, s66\n"
+        "s_sub_i32 s62, 0, s66\n"
+        "s_mov_b32 s69, 0\n"
+        "v_rcp_iflag_f32 v0, v0\n"
+        "s_nop 0\n"
+        "v_mul_f32 v0, 0x4f7ffffe, v0\n"
+        "v_cvt_u32_f32 v0, v0\n"
+        "s_nop 0\n"
+        "v_readfirstlane_b32 s76, v0\n"
+        "s_mul_i32 s62, s62, s76\n"
+        "s_mul_hi_u32 s62, s76, s62\n"
+        "s_add_i32 s76, s76, s62\n"
+        "s_mul_hi_u32 s62, s64, s76\n"
+        "s_mul_i32 s67, s62, s66\n"
+        "s_sub_i32 s67, s64, s67\n"
+        "s_add_i32 s76, s62, 1\n"
+        "s_sub_i32 s64, s67, s66\n"
+        "s_cmp_ge_u32 s67, s66\n"
+        "s_cselect_b32 s62, s76, s62\n"
+        "s_cselect_b32 s67, s64, s67\n"
+        "s_add_i32 s76, s62, 1\n"
+        "s_cmp_ge_u32 s67, s66\n"
+        "s_cselect_b32 s68, s76, s62\n"
+        "L_dvr%=:\n"                       // Q = s[68:69]; R = |N| - Q |D|
+        "s_mul_i32 s74, s68, s46\n"
+        "s_mul_hi_u32 s75, s68, s46\n"
+        "s_mul_i32 s62, s68, s47\n"
+        "s_add_u32 s75, s75, s62\n"
+        "s_mul_i32 s62, s69, s46\n"
+        "s_add_u32 s75, s75, s62\n"
+        "s_sub_u32 s74, s44, s74\n"
+        "s_subb_u32 s75, s45, s75\n"
+        "s_cmp_eq_u32 s52, 0\n"
+        "s_cbranch_scc1 L_dvq%=\n"
+        "s_sub_u32 s68, 0, s68\n"
+        "s_subb_u32 s69, 0, s69\n"
+        "L_dvq%=:\n"
+        "s_cmp_eq_u32 s53, 0\n"
+        "s_cbranch_scc1 L_dvsel%=\n"
+        "s_sub_u32 s74, 0, s74\n"
+        "s_subb_u32 s75, 0, s75\n"
+        "L_dvsel%=:\n"
+        "s_bitcmp1_b32 s36, 0\n"
+        "s_cselect_b64 s[48:49], s[74:75], s[68:69]\n"
+        "s_branch L_wb%=\n"
+        // ---- branches on a, b (not av / bv)
+        "L_bgeu%=:\n"                      // taken unless a <u b
         "s_cmp_lt_u32 s41, s43\n"
         "s_cbranch_scc1 L_nowb%=\n"
         "s_cmp_lg_u32 s41, s43\n"
@@ -2251,7 +2510,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
           "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "s28", "s29",
           "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50",
           "s51", "s52", "s53", "s54", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",
-          "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78",
+          "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s80", "s81",
           "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
           "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
           "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77",
@@ -2310,6 +2569,7 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
     }
     uint64_t spc = uni64(io->spc);
     uint32_t steps = 0, xticks = 0, fbytes = 0, dbytes = 0;
+    uint32_t n_fast = 0, n_fast_steps = 0, n_fast_back = 0;   // diagnostics: stats[53..55]
 #ifdef FI_PROF   // phases: fetch (+ decode of rewritten code), operands, execute, commit
     uint64_t pacc[4] = {0, 0, 0, 0}, plast = __builtin_amdgcn_s_memtime();
 #define PST(k)                                                  \
@@ -2358,6 +2618,8 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
                 F->dce_lds = (uint32_t)(uintptr_t)DCE; F->tlb_lds = (uint32_t)(uintptr_t)&mp->tv0;
                 F->pre = (uint64_t)(uintptr_t)CX->pre; F->tlo = tlo; F->clo = clo; F->cvpn = cvpn; F->cpg = cpg;
                 solo_fast_run(F);
+                n_fast++;
+                n_fast_steps += uni32(F->steps) - steps;
                 po = uni32(F->po); steps = uni32(F->steps); xticks = uni32(F->xticks);
                 fbytes = uni32(F->fbytes); dbytes = uni32(F->dbytes);
                 cvpn = uni64(F->cvpn); cpg = uni64(F->cpg);
@@ -2365,6 +2627,7 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
                 if (why == 3) { spc = uni64(F->npc); goto leave; }   // a jump left the text
                 if (why == 4) { spc = tlo + po; goto leave; }         // so did the fall-through
                 if (why == 0) break;                                  // budget spent
+                n_fast_back++;
                 PRE_AT(po, q1, q2, q3);                               // the instruction it hands back
                 fast_at = steps + 1;
             }
@@ -2567,6 +2830,11 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
 #undef PRE_AT
     }
 leave:
+    if (n_fast) {
+        atomicAdd(&CX->stats[53], (unsigned long long)n_fast);
+        atomicAdd(&CX->stats[54], (unsigned long long)n_fast_steps);
+        atomicAdd(&CX->stats[55], (unsigned long long)n_fast_back);
+    }
     io->spc = spc; io->watch = watch;
     io->steps = steps; io->xticks = xticks; io->fbytes = fbytes; io->dbytes = dbytes;
 #ifdef FI_PROF

@@ -517,6 +517,39 @@ def test_known_answer_programs(oracle_mod, prog):
     compare(dev, o.run_trials(sites, protect_mask=0), sites)
 
 
+@pytest.mark.parametrize("prog", ["alu", "cmp", "rvc", "mem"])
+def test_known_answer_programs_solo_interpreter(oracle_mod, prog):
+    """The known-answer programs from process start through the solo
+    pre-decoded interpreter only (FI_CFG_SOLO_ALL | NO_TRANSLATE |
+    NO_SNAPSHOT_START | NO_EARLY_EXIT): every op of the alu program -- the
+    M-extension edge pairs (x / 0, INT_MIN / -1, the W forms, mulh*) among
+    them -- runs in the assembly inner loop (solo_fast_run), no-fault trials
+    print the models and end masked, faulted trials match the oracle."""
+    from shrewd_amd import Engine
+    import test_isa_vectors as kat
+    elf = {"alu": kat.program_elf, "cmp": kat.cmp_program_elf, "rvc": kat.rvc_program_elf,
+           "mem": kat.mem_program_elf}[prog]()
+    e = Engine(private_pages=64, flags=128 | 4 | 1 | 2)
+    e.load_elf(elf, [prog])
+    e.golden_run()
+    o = oracle_mod.Oracle(elf, prog)
+    o.run_golden()
+    e.set_campaign(0x5EED00A5, REGS | PC, 1)
+    e.set_protect(0)
+    sites = e.sample(0, 1500)
+    nofault = sites[:64].copy()
+    nofault["inst"] = 1 << 40
+    dev, h = e.run_sites(nofault)
+    assert (dev["cls"] == 0).all()
+    assert int(h["device_insts"]) == int(h["guest_insts"])
+    compare(dev, o.run_trials(nofault, protect_mask=0), nofault)
+    dev, _ = e.run_sites(sites)
+    compare(dev, o.run_trials(sites, protect_mask=0), sites)
+    st = e.debug_stats()
+    assert int(st[54]) > 0, "the assembly inner loop did not run"
+    e.close()
+
+
 def test_clock_read_blocks_tick_blind_early_exit(oracle_mod):
     """Exact early exit when the golden suffix reads curTick: the clk program's
     branch-register faults take an arm with 16 extra non-counting ticks
