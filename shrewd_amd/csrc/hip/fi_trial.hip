@@ -1741,6 +1741,8 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "v_readfirstlane_b32 s28, v28\n"    // cpg
         "v_readfirstlane_b32 s29, v29\n"
         // v15 = R, v16 = DCT, v17 = DCE, v18 = &tv0 (LDS addresses; v12..v14 free again)
+        "s_or_b32 s79, s17, s18\n"          // leader flag bits of either parity, in place in w
+        "s_lshl_b32 s79, s79, 8\n"
         "s_getpc_b64 s[80:81]\n"            // the jump table's address
         "L_gp%=:\n"
         "s_add_u32 s80, s80, L_jt%= - L_gp%=\n"
@@ -1768,10 +1770,76 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "L_top%=:\n"
         "s_cmp_ge_u32 s6, s7\n"
         "s_cbranch_scc1 L_budget%=\n"
-        // ---- the entry: the decode cache inside the rewritten window, else pre[]
+        // ---- the entry: the decode cache inside the rewritten window (L_win,
+        // out of line: the common path falls through), else pre[]
         "s_add_u32 s62, s5, 6\n"
         "s_cmp_gt_u32 s62, s12\n"
-        "s_cbranch_scc0 L_pre%=\n"
+        "s_cbranch_scc1 L_win%=\n"
+        "L_pre%=:\n"                        // entry (po >> 1) | (po & 1), 16 bytes each
+        "s_bitcmp1_b32 s5, 0\n"
+        "s_cbranch_scc1 L_preo%=\n"         // (odd pc: out of line)
+        "s_lshl_b32 s62, s5, 3\n"
+        "L_prel%=:\n"
+        "s_load_dwordx4 s[36:39], s[20:21], s62\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "L_have%=:\n"
+        // (K_SLOW leaves through the jump table)
+        "s_bfe_u32 s56, s39, 0x60010\n"     // kind
+        "s_and_b32 s62, s39, s79\n"         // maybe a block leader the translated code takes
+        "s_cbranch_scc1 L_lead%=\n"         // (out of line)
+        "L_nolead%=:\n"
+        "s_and_b32 s60, s39, 0xff\n"        // len
+        "s_bfe_u32 s57, s37, 0x50008\n"     // rd
+        "s_bfe_u32 s58, s37, 0x6000f\n"     // 2 rs1 (bit 15: the top of the 8-bit rd field, 0)
+        "s_bfe_u32 s59, s37, 0x60017\n"     // 2 rs2 (bit 23: the top of the rs1 field, 0)
+        "s_set_gpr_idx_on s58, gpr_idx(SRC0)\n"
+        "v_mov_b64 v[0:1], v[64:65]\n"
+        "s_set_gpr_idx_off\n"
+        "s_set_gpr_idx_on s59, gpr_idx(SRC0)\n"
+        "v_mov_b64 v[2:3], v[64:65]\n"
+        "s_set_gpr_idx_off\n"
+        "s_ashr_i32 s53, s38, 31\n"         // imm, sign-extended
+        "s_mov_b32 s52, s38\n"
+        "v_readfirstlane_b32 s44, v0\n"     // a = x[rs1] (av but for U_APC)
+        "v_readfirstlane_b32 s45, v1\n"
+        "v_readfirstlane_b32 s42, v2\n"     // b = x[rs2]
+        "v_readfirstlane_b32 s43, v3\n"
+        "s_bitcmp1_b32 s39, 25\n"           // U_APC (aux = w >> 16): av = pc (out of line)
+        "s_cbranch_scc1 L_apc%=\n"
+        "L_apcb%=:\n"
+        "s_bitcmp1_b32 s39, 24\n"           // U_BIMM
+        "s_cselect_b64 s[46:47], s[52:53], s[42:43]\n"
+        // ---- dispatch on the kind (rv64_isa.h Kind): add inline (the most
+        // frequent kind; it falls through into the write-back), the rest
+        // through a jump table of s_branch instructions, one per kind, at
+        // s[80:81] (L_disp, out of line)
+        "s_cmp_lg_u32 s56, 1\n"
+        "s_cbranch_scc1 L_disp%=\n"
+        "L_add%=:\n"
+        "s_add_u32 s48, s44, s46\n"
+        "s_addc_u32 s49, s45, s47\n"
+        // ---- write back x[rd] (w32: sign-extended low word), then fall through
+        "L_wb%=:\n"
+        "s_bitcmp1_b32 s39, 26\n"           // U_W32: sign-extend the low word (out of line)
+        "s_cbranch_scc1 L_wbw%=\n"
+        "L_wb64%=:\n"
+        "s_lshl_b32 s62, s57, 1\n"
+        "s_set_gpr_idx_on s62, gpr_idx(DST)\n"
+        "v_mov_b64 v[64:65], s[48:49]\n"
+        "s_set_gpr_idx_off\n"
+        "v_mov_b64 v[64:65], 0\n"           // x0 stays zero
+        "L_nowb%=:\n"
+        "s_add_u32 s6, s6, 1\n"             // commit (data bytes: in the memory paths)
+        "s_bfe_u32 s62, s39, 0x10009\n"     // straddle tick (kPreStraddle)
+        "s_add_u32 s8, s8, s62\n"
+        "s_add_u32 s9, s9, s60\n"
+        "s_add_u32 s5, s5, s60\n"           // the fall-through
+        "s_cmp_lt_u32 s5, s11\n"
+        "s_cbranch_scc1 L_top%=\n"
+        "s_mov_b32 s19, 4\n"
+        "s_branch L_out%=\n"
+        // ---- out of line: the rewritten window, a leader, the jump table
+        "L_win%=:\n"
         "s_cmp_lt_u32 s5, s13\n"
         "s_cbranch_scc0 L_pre%=\n"
         "s_sub_u32 s62, s5, s14\n"          // in the code range?
@@ -1790,60 +1858,28 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_cmp_eq_u32 s62, s5\n"
         "s_cbranch_scc0 L_slow%=\n"         // a miss: the C++ loop decodes and fills the cache
         "s_branch L_have%=\n"
-        "L_pre%=:\n"
-        "s_lshr_b32 s62, s5, 1\n"           // halfword (po >> 1) | (po & 1)
-        "s_and_b32 s63, s5, 1\n"
-        "s_or_b32 s62, s62, s63\n"
-        "s_lshl_b32 s62, s62, 4\n"
-        "s_add_u32 s64, s20, s62\n"
-        "s_addc_u32 s65, s21, 0\n"
-        "s_load_dwordx4 s[36:39], s[64:65], 0x0\n"
-        "s_waitcnt lgkmcnt(0)\n"
-        "L_have%=:\n"
-        "s_bfe_u32 s56, s39, 0x60010\n"     // kind
-        "s_cmp_eq_u32 s56, 0\n"
-        "s_cbranch_scc1 L_slow%=\n"
-        "s_bitcmp1_b32 s5, 0\n"             // a block leader the translated code takes
+        "L_lead%=:\n"                       // a block leader the translated code takes?
+        "s_bitcmp1_b32 s5, 0\n"
         "s_cselect_b32 s62, s18, s17\n"
         "s_bfe_u32 s63, s39, 0x80008\n"
         "s_and_b32 s62, s62, s63\n"
         "s_cbranch_scc0 L_nolead%=\n"
         "s_cmp_ge_u32 s6, s16\n"
         "s_cbranch_scc1 L_leader%=\n"
-        "L_nolead%=:\n"
-        "s_and_b32 s60, s39, 0xff\n"        // len
-        "s_lshr_b32 s61, s39, 16\n"         // aux
-        "s_bfe_u32 s57, s37, 0x50008\n"     // rd
-        "s_bfe_u32 s58, s37, 0x50010\n"     // rs1
-        "s_bfe_u32 s59, s37, 0x50018\n"     // rs2
-        "s_lshl_b32 s62, s58, 1\n"
-        "s_lshl_b32 s63, s59, 1\n"
-        "s_set_gpr_idx_on s62, gpr_idx(SRC0)\n"
-        "v_mov_b32 v0, v64\n"
-        "v_mov_b32 v1, v65\n"
-        "s_set_gpr_idx_off\n"
-        "s_set_gpr_idx_on s63, gpr_idx(SRC0)\n"
-        "v_mov_b32 v2, v64\n"
-        "v_mov_b32 v3, v65\n"
-        "s_set_gpr_idx_off\n"
-        "s_add_u32 s50, s22, s5\n"          // pc
-        "s_addc_u32 s51, s23, 0\n"
-        "s_ashr_i32 s53, s38, 31\n"         // imm, sign-extended
-        "s_mov_b32 s52, s38\n"
-        "s_mov_b32 s63, 0\n"                // msz (data bytes)
-        "v_readfirstlane_b32 s40, v0\n"     // a = x[rs1]
-        "v_readfirstlane_b32 s41, v1\n"
-        "v_readfirstlane_b32 s42, v2\n"     // b = x[rs2]
-        "v_readfirstlane_b32 s43, v3\n"
-        "s_bitcmp1_b32 s61, 9\n"            // U_APC
-        "s_cselect_b64 s[44:45], s[50:51], s[40:41]\n"
-        "s_bitcmp1_b32 s61, 8\n"            // U_BIMM
-        "s_cselect_b64 s[46:47], s[52:53], s[42:43]\n"
-        // ---- dispatch on the kind (rv64_isa.h Kind)
-        // (add first: the most frequent kind; the rest through a jump table
-        // of s_branch instructions, one per kind, at s[80:81])
-        "s_cmp_eq_u32 s56, 1\n"
-        "s_cbranch_scc1 L_add%=\n"
+        "s_branch L_nolead%=\n"
+        "L_preo%=:\n"
+        "s_lshr_b32 s62, s5, 1\n"
+        "s_or_b32 s62, s62, 1\n"
+        "s_lshl_b32 s62, s62, 4\n"
+        "s_branch L_prel%=\n"
+        "L_wbw%=:\n"
+        "s_ashr_i32 s49, s48, 31\n"
+        "s_branch L_wb64%=\n"
+        "L_apc%=:\n"                        // av = pc
+        "s_add_u32 s44, s22, s5\n"
+        "s_addc_u32 s45, s23, 0\n"
+        "s_branch L_apcb%=\n"
+        "L_disp%=:\n"
         "s_cmp_gt_u32 s56, 29\n"
         "s_cbranch_scc1 L_slow%=\n"
         "s_lshl_b32 s62, s56, 2\n"
@@ -1882,10 +1918,6 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_branch L_rem%=\n"
         "s_branch L_remu%=\n"               // 29 K_REMU
         // ---- ALU
-        "L_add%=:\n"
-        "s_add_u32 s48, s44, s46\n"
-        "s_addc_u32 s49, s45, s47\n"
-        "s_branch L_wb%=\n"
         "L_sub%=:\n"
         "s_sub_u32 s48, s44, s46\n"
         "s_subb_u32 s49, s45, s47\n"
@@ -1920,14 +1952,14 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_cbranch_scc1 L_one%=\n"
         "s_branch L_wb%=\n"
         "L_sll%=:\n"                        // av << (bv & shm)
-        "s_bitcmp1_b32 s61, 10\n"           // U_W32: 5-bit amount
+        "s_bitcmp1_b32 s39, 26\n"           // U_W32: 5-bit amount
         "s_cselect_b32 s62, 31, 63\n"
         "s_and_b32 s62, s46, s62\n"
         "s_lshl_b64 s[48:49], s[44:45], s62\n"
         "s_branch L_wb%=\n"
         "L_srl%=:\n"                        // (w32 ? av & 0xffffffff : av) >> (bv & shm)
         "s_mov_b32 s64, s44\n"
-        "s_bitcmp1_b32 s61, 10\n"
+        "s_bitcmp1_b32 s39, 26\n"
         "s_cselect_b32 s62, 31, 63\n"
         "s_cselect_b32 s65, 0, s45\n"
         "s_and_b32 s62, s46, s62\n"
@@ -1936,7 +1968,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "L_sra%=:\n"                        // (w32 ? (int32)av : (int64)av) >> (bv & shm)
         "s_mov_b32 s64, s44\n"
         "s_ashr_i32 s66, s44, 31\n"
-        "s_bitcmp1_b32 s61, 10\n"
+        "s_bitcmp1_b32 s39, 26\n"
         "s_cselect_b32 s62, 31, 63\n"
         "s_cselect_b32 s65, s66, s45\n"
         "s_and_b32 s62, s46, s62\n"
@@ -2010,7 +2042,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "L_dv%=:\n"
         "s_mov_b64 s[64:65], s[44:45]\n"   // N, D
         "s_mov_b64 s[66:67], s[46:47]\n"
-        "s_bitcmp1_b32 s61, 10\n"          // U_W32: the low words, sign- or zero-extended
+        "s_bitcmp1_b32 s39, 26\n"          // U_W32: the low words, sign- or zero-extended
         "s_cbranch_scc0 L_dv64%=\n"
         "s_ashr_i32 s65, s64, 31\n"
         "s_ashr_i32 s67, s66, 31\n"
@@ -2212,69 +2244,73 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_branch L_wb%=\n"
         // ---- branches on a, b (not av / bv)
         "L_bgeu%=:\n"                      // taken unless a <u b
-        "s_cmp_lt_u32 s41, s43\n"
+        "s_cmp_lt_u32 s45, s43\n"
         "s_cbranch_scc1 L_nowb%=\n"
-        "s_cmp_lg_u32 s41, s43\n"
+        "s_cmp_lg_u32 s45, s43\n"
         "s_cbranch_scc1 L_taken%=\n"
-        "s_cmp_lt_u32 s40, s42\n"
+        "s_cmp_lt_u32 s44, s42\n"
         "s_cbranch_scc1 L_nowb%=\n"
         "s_branch L_taken%=\n"
         "L_beq%=:\n"
-        "s_cmp_eq_u64 s[40:41], s[42:43]\n"
+        "s_cmp_eq_u64 s[44:45], s[42:43]\n"
         "s_cbranch_scc1 L_taken%=\n"
         "s_branch L_nowb%=\n"
         "L_bne%=:\n"
-        "s_cmp_lg_u64 s[40:41], s[42:43]\n"
+        "s_cmp_lg_u64 s[44:45], s[42:43]\n"
         "s_cbranch_scc1 L_taken%=\n"
         "s_branch L_nowb%=\n"
         "L_blt%=:\n"
-        "s_cmp_lt_i32 s41, s43\n"
+        "s_cmp_lt_i32 s45, s43\n"
         "s_cbranch_scc1 L_taken%=\n"
-        "s_cmp_lg_u32 s41, s43\n"
+        "s_cmp_lg_u32 s45, s43\n"
         "s_cbranch_scc1 L_nowb%=\n"
-        "s_cmp_lt_u32 s40, s42\n"
+        "s_cmp_lt_u32 s44, s42\n"
         "s_cbranch_scc1 L_taken%=\n"
         "s_branch L_nowb%=\n"
         "L_bge%=:\n"
-        "s_cmp_lt_i32 s41, s43\n"
+        "s_cmp_lt_i32 s45, s43\n"
         "s_cbranch_scc1 L_nowb%=\n"
-        "s_cmp_lg_u32 s41, s43\n"
+        "s_cmp_lg_u32 s45, s43\n"
         "s_cbranch_scc1 L_taken%=\n"
-        "s_cmp_lt_u32 s40, s42\n"
+        "s_cmp_lt_u32 s44, s42\n"
         "s_cbranch_scc1 L_nowb%=\n"
         "s_branch L_taken%=\n"
         "L_bltu%=:\n"
-        "s_cmp_lt_u32 s41, s43\n"
+        "s_cmp_lt_u32 s45, s43\n"
         "s_cbranch_scc1 L_taken%=\n"
-        "s_cmp_lg_u32 s41, s43\n"
+        "s_cmp_lg_u32 s45, s43\n"
         "s_cbranch_scc1 L_nowb%=\n"
-        "s_cmp_lt_u32 s40, s42\n"
+        "s_cmp_lt_u32 s44, s42\n"
         "s_cbranch_scc1 L_taken%=\n"
         "s_branch L_nowb%=\n"
         "L_taken%=:\n"                      // npc = pc + imm
+        "s_add_u32 s50, s22, s5\n"
+        "s_addc_u32 s51, s23, 0\n"
         "s_add_u32 s50, s50, s52\n"
         "s_addc_u32 s51, s51, s53\n"
         "s_branch L_jump%=\n"
         "L_jal%=:\n"                        // v = pc + len, npc = pc + imm
+        "s_add_u32 s50, s22, s5\n"
+        "s_addc_u32 s51, s23, 0\n"
         "s_add_u32 s48, s50, s60\n"
         "s_addc_u32 s49, s51, 0\n"
         "s_add_u32 s50, s50, s52\n"
         "s_addc_u32 s51, s51, s53\n"
         "s_branch L_jwb%=\n"
         "L_jalr%=:\n"                       // v = pc + len, npc = (a + imm) & ~1
+        "s_add_u32 s50, s22, s5\n"
+        "s_addc_u32 s51, s23, 0\n"
         "s_add_u32 s48, s50, s60\n"
         "s_addc_u32 s49, s51, 0\n"
-        "s_add_u32 s50, s40, s52\n"
-        "s_addc_u32 s51, s41, s53\n"
+        "s_add_u32 s50, s44, s52\n"
+        "s_addc_u32 s51, s45, s53\n"
         "s_and_b32 s50, s50, -2\n"
         "L_jwb%=:\n"
         "s_lshl_b32 s62, s57, 1\n"
         "s_set_gpr_idx_on s62, gpr_idx(DST)\n"
-        "v_mov_b32 v64, s48\n"
-        "v_mov_b32 v65, s49\n"
+        "v_mov_b64 v[64:65], s[48:49]\n"
         "s_set_gpr_idx_off\n"
-        "v_mov_b32 v64, 0\n"                // x0 stays zero
-        "v_mov_b32 v65, 0\n"
+        "v_mov_b64 v[64:65], 0\n"           // x0 stays zero
         "L_jump%=:\n"
         "s_add_u32 s6, s6, 1\n"             // commit
         "s_bfe_u32 s62, s39, 0x10009\n"     // straddle tick (kPreStraddle)
@@ -2290,10 +2326,10 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_branch L_top%=\n"
         // ---- loads and stores: the whole access in one mapped page
         "L_mem%=:\n"
-        "s_bfe_u32 s54, s61, 0x2000c\n"     // log2 size
+        "s_bfe_u32 s54, s39, 0x2001c\n"     // log2 size
         "s_lshl_b32 s63, 1, s54\n"          // msz
-        "s_add_u32 s64, s40, s52\n"         // ea = a + imm
-        "s_addc_u32 s65, s41, s53\n"
+        "s_add_u32 s64, s44, s52\n"         // ea = a + imm
+        "s_addc_u32 s65, s45, s53\n"
         "s_lshr_b64 s[66:67], s[64:65], 12\n"
         "s_cmp_eq_u64 s[66:67], s[26:27]\n"
         "s_cbranch_scc1 L_pg%=\n"
@@ -2363,7 +2399,8 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "v_mov_b32 v1, s77\n"
         "s_cmp_eq_u32 s56, 13\n"
         "s_cbranch_scc1 L_st%=\n"
-        // load
+        // load (nothing leaves from here on: its data bytes count)
+        "s_add_u32 s10, s10, s63\n"
         "s_cmp_eq_u32 s54, 3\n"
         "s_cbranch_scc1 L_ld8%=\n"
         "s_cmp_eq_u32 s54, 2\n"
@@ -2388,7 +2425,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_waitcnt vmcnt(0)\n"
         "v_readfirstlane_b32 s48, v2\n"
         "s_mov_b32 s49, 0\n"
-        "s_bitcmp1_b32 s61, 11\n"
+        "s_bitcmp1_b32 s39, 27\n"
         "s_cbranch_scc0 L_wb%=\n"
         "s_lshl_b32 s62, s63, 19\n"         // width 8 * msz, offset 0
         "s_bfe_i64 s[48:49], s[48:49], s62\n"
@@ -2410,6 +2447,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_cmp_lt_u32 s74, s62\n"
         "s_cbranch_scc1 L_slow%=\n"
         "L_stok%=:\n"
+        "s_add_u32 s10, s10, s63\n"         // data bytes
         "v_mov_b32 v2, s42\n"
         "v_mov_b32 v3, s43\n"
         "s_cmp_eq_u32 s54, 3\n"
@@ -2431,30 +2469,6 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "L_std%=:\n"
         "s_nop 1\n"
         "s_branch L_nowb%=\n"
-        // ---- write back x[rd] (w32: sign-extended low word), then fall through
-        "L_wb%=:\n"
-        "s_bitcmp1_b32 s61, 10\n"
-        "s_cbranch_scc0 L_wb64%=\n"
-        "s_ashr_i32 s49, s48, 31\n"
-        "L_wb64%=:\n"
-        "s_lshl_b32 s62, s57, 1\n"
-        "s_set_gpr_idx_on s62, gpr_idx(DST)\n"
-        "v_mov_b32 v64, s48\n"
-        "v_mov_b32 v65, s49\n"
-        "s_set_gpr_idx_off\n"
-        "v_mov_b32 v64, 0\n"
-        "v_mov_b32 v65, 0\n"
-        "L_nowb%=:\n"
-        "s_add_u32 s6, s6, 1\n"             // commit
-        "s_bfe_u32 s62, s39, 0x10009\n"
-        "s_add_u32 s8, s8, s62\n"
-        "s_add_u32 s9, s9, s60\n"
-        "s_add_u32 s10, s10, s63\n"
-        "s_add_u32 s5, s5, s60\n"           // the fall-through
-        "s_cmp_lt_u32 s5, s11\n"
-        "s_cbranch_scc1 L_top%=\n"
-        "s_mov_b32 s19, 4\n"
-        "s_branch L_out%=\n"
         // ================================================================ exits
         "L_left%=:\n"
         "s_mov_b32 s19, 3\n"
@@ -2510,7 +2524,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
           "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "s28", "s29",
           "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50",
           "s51", "s52", "s53", "s54", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",
-          "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s80", "s81",
+          "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81",
           "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
           "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
           "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77",
