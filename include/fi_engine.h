@@ -96,7 +96,7 @@ typedef int32_t fi_status;
 
 typedef struct {
     uint8_t cls, sub, exit_code, flags;  /* flags bit0: injected, bit1: memory site unmapped at t */
-    uint32_t detail;                     /* low 32 bits of pc at termination / fault va / syscall # */
+    uint32_t detail;                     /* low 32 bits of pc at termination / fault va / syscall #; 0 for a hang */
     uint64_t ninst;                      /* committed guest instructions (numInst) at termination */
 } fi_outcome;
 
@@ -173,6 +173,10 @@ typedef struct {
  * and $SHREWD_FI_JIT_CACHE) hold them: cold-start measurements and tests of
  * the background build. */
 #define FI_CFG_JIT_NO_CACHE 8192u
+/* No counted-loop hang proofs in the clean translated body (fi_translate.cpp):
+ * every hang trial runs to the cap (A/B and parity checks; outcomes are
+ * identical -- a hang's record is the same either way). */
+#define FI_CFG_NO_HANG_PROOF 16384u
 
 typedef struct {
     uint64_t ninst, ncycles;

@@ -2639,7 +2639,9 @@ static void tick(mach_t *m, u64 cap) {
         inject(m);
         if (m->done) return;
     }
-    if (m->num_inst >= cap) { finish(m, OR_HANG, OR_HANG_INSTS, 0); return; }
+    /* (a hang's record names no pc: the engine proves some hangs before the
+       cap, shrewd_amd/csrc/fi_translate.cpp counted-loop proofs) */
+    if (m->num_inst >= cap) { finish(m, OR_HANG, OR_HANG_INSTS, 0); m->res.detail = 0; return; }
     /* setupFetchRequest: 4 bytes at (pc & ~3) + fetchOffset (base.cc:304-318) */
     u64 fetch_pc = (m->pc & ~3ULL) + m->fetch_offset;
     uint8_t *pg = translate(m, fetch_pc);

@@ -835,6 +835,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.snap_interval = e->snap_I;
     c.early_exit = (!(e->cfg.flags & FI_CFG_NO_EARLY_EXIT) && e->snaps.size() > 1 && !e->golden_fp) ? 1 : 0;
     if (c.early_exit && !(e->cfg.flags & FI_CFG_NO_SDC_EXIT)) c.early_exit = 3;   // bit 1: SDC early exit
+    c.hang_proof = (e->cfg.flags & FI_CFG_NO_HANG_PROOF) ? 0 : 1;
     c.gout = e->d_gout; c.gerr = e->d_gerr; c.gout_len = e->gout.size(); c.gerr_len = e->gerr.size();
     c.gexit = e->golden.exit_code;
     c.gdetail = e->gdetail;

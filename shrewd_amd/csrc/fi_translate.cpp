@@ -622,6 +622,166 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         if (k == E_DIRECT) return "goto " + SB + std::to_string(t) + ";";
         return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto " + SD + "; }" : "; goto S_out; }");
     };
+    // ---- counted-loop hang proofs (clean body).  A cycle of blocks with no
+    // nested cycle, no memory access and no indirect jump, left only by one
+    // branch on a register Xk against zero (it stays in the cycle while Xk !=
+    // 0) right after the cycle's only write of Xk, Xk = Xk + c with c = +-1 in
+    // the same block: from any block boundary in the cycle the branch is
+    // passed n more times, Xk + n c = 0 (mod 2^64; n = 2^64 for Xk = 0), and
+    // between two passes the trial commits at least m instructions (the
+    // shortest way around the cycle).  It cannot terminate, fault or call
+    // inside, so it commits at least (n - 1) m instructions before it leaves
+    // -- once that reaches the hang cap the trial is a hang, and nothing it
+    // would do until then can change its outcome: it cannot meet a golden
+    // snapshot either (the golden run would then run that loop past the cap
+    // too).  The clean body's dispatch tests it (TXHANG) whenever it enters
+    // such a cycle, i.e. once per call.
+    struct HangProof { uint32_t reg; int step; uint32_t m; };
+    std::map<uint32_t, HangProof> hang_proof;
+    for (uint32_t H : S.headers) {
+        std::vector<uint32_t> cyc;
+        bool nested = false;
+        for (const auto &kv : S.chain) {
+            const auto pos = std::find(kv.second.begin(), kv.second.end(), H);
+            if (pos == kv.second.end()) continue;
+            if (pos + 1 != kv.second.end()) nested = true;
+            cyc.push_back(kv.first);
+        }
+        if (nested || cyc.empty()) continue;
+        const std::set<uint32_t> in(cyc.begin(), cyc.end());
+        std::map<uint32_t, const Block *> bl;
+        for (const Block &b : blocks)
+            if (b.opc == 0 && in.count(b.h0)) bl[b.h0] = &b;
+        if (bl.size() != in.size()) continue;
+        bool ok = true;
+        uint32_t writes[32] = {0};
+        std::map<uint32_t, std::vector<uint32_t>> nx;   // edges inside the cycle
+        uint32_t n_exit = 0, eblk = 0;
+        bool exit_on_taken = false;
+        for (const auto &kv : bl) {
+            const Block &b = *kv.second;
+            if (b.insts.empty()) { ok = false; break; }
+            auto to = [&](uint64_t pc, bool taken) {
+                uint32_t t;
+                if (hof(pc, t) && in.count(t) && !S.exits.count({b.h0, t})) nx[b.h0].push_back(t);
+                else { n_exit++; eblk = b.h0; exit_on_taken = taken; }
+            };
+            for (size_t i = 0; i < b.insts.size() && ok; i++) {
+                std::string e;
+                uint32_t sz;
+                int sx;
+                const char *cond;
+                const PreInst &p = pre[b.insts[i]];
+                const uint64_t pc = text_lo + 2ULL * b.insts[i];
+                const Cls k = classify(p, e, sz, sx, cond);
+                if (k == C_LOAD || k == C_STORE || k == C_JALR || k == C_STOP) ok = false;
+                if ((k == C_ALU || k == C_JAL) && p.rd) writes[p.rd]++;
+                if (k == C_BR) { to(pc + (int64_t)p.imm, true); to(pc + p.len, false); }
+                if (k == C_JAL) to(pc + (int64_t)p.imm, true);
+            }
+            if (ok && !b.term) to(text_lo + 2ULL * b.insts.back() + pre[b.insts.back()].len, false);
+        }
+        if (!ok || n_exit != 1) continue;
+        const Block &E = *bl[eblk];
+        const PreInst &br = pre[E.insts.back()];
+        uint32_t reg = 0;
+        bool exit_when_zero = false;   // the exit edge is taken when Xk == 0
+        if (br.op == OP_c_beqz || br.op == OP_c_bnez) {
+            reg = br.rs1;
+            exit_when_zero = (br.op == OP_c_beqz) == exit_on_taken;
+        } else if ((br.op == OP_beq || br.op == OP_bne) && (br.rs1 == 0) != (br.rs2 == 0)) {
+            reg = br.rs1 ? br.rs1 : br.rs2;
+            exit_when_zero = (br.op == OP_beq) == exit_on_taken;
+        }
+        if (!reg || !exit_when_zero || writes[reg] != 1) continue;
+        int step = 0;
+        for (size_t i = 0; i + 1 < E.insts.size(); i++) {
+            const PreInst &p = pre[E.insts[i]];
+            if ((p.op == OP_addi || p.op == OP_c_addi) && p.rd == reg && p.rs1 == reg && (p.imm == 1 || p.imm == -1))
+                step = p.imm;
+        }
+        if (!step) continue;
+        // m: the fewest instructions from E's successor in the cycle around to E's end
+        std::map<uint32_t, uint32_t> dist;
+        std::set<std::pair<uint32_t, uint32_t>> q;
+        for (uint32_t t : nx[eblk]) {
+            const uint32_t d = (uint32_t)bl[t]->insts.size();
+            if (!dist.count(t) || d < dist[t]) { dist[t] = d; q.insert({d, t}); }
+        }
+        uint32_t m = 0;
+        while (!q.empty()) {
+            const auto [d, v] = *q.begin();
+            q.erase(q.begin());
+            if (d != dist[v]) continue;
+            if (v == eblk) { m = d; break; }
+            for (uint32_t t : nx[v]) {
+                const uint32_t nd = d + (uint32_t)bl[t]->insts.size();
+                if (!dist.count(t) || nd < dist[t]) { dist[t] = nd; q.insert({nd, t}); }
+            }
+        }
+        if (!m) continue;
+        for (uint32_t h : cyc) hang_proof[h] = {reg, step, m};
+    }
+
+    // ---- clean body budget tests.  Only a check point tests the budget: a
+    // top-level block or a cycle header (the dispatch and the back edges enter
+    // those), or a block routed to through its headers (the routing tests it).
+    // The test covers the longest run of direct edges through blocks that are
+    // not check points (the blocks inside a cycle below its header), so a loop
+    // iteration tests once.  (A test that fails leaves with the budget not
+    // spent; the kernel then interprets up to its event, fi_trial.hip.)
+    std::map<uint32_t, uint32_t> run_len;   // instructions from a block to the next check point
+    std::set<uint32_t> forced_cp;
+    auto is_cp = [&](uint32_t h) { return forced_cp.count(h) || !(S.chain.count(h) && !S.headers.count(h)); };
+    {
+        std::map<uint32_t, const Block *> blk;
+        for (const Block &b : blocks)
+            if (b.opc == 0) blk[b.h0] = &b;
+        auto direct_succ = [&](const Block &b) {
+            std::vector<uint32_t> r;
+            auto add = [&](uint64_t pc) {
+                uint32_t t;
+                if (hof(pc, t) && !S.exits.count({b.h0, t})) r.push_back(t);
+            };
+            for (uint32_t h : b.insts) {
+                std::string e;
+                uint32_t sz;
+                int sx;
+                const char *cond;
+                const PreInst &p = pre[h];
+                const uint64_t pc = text_lo + 2ULL * h;
+                const Cls k = classify(p, e, sz, sx, cond);
+                if (k == C_BR) { add(pc + (int64_t)p.imm); add(pc + p.len); }
+                if (k == C_JAL) add(pc + (int64_t)p.imm);
+            }
+            if (!b.term && !b.insts.empty()) add(text_lo + 2ULL * b.insts.back() + pre[b.insts.back()].len);
+            return r;
+        };
+        std::set<uint32_t> on_path;
+        std::function<uint32_t(uint32_t)> longest = [&](uint32_t h) -> uint32_t {
+            auto it = run_len.find(h);
+            if (it != run_len.end()) return it->second;
+            auto bi = blk.find(h);
+            if (bi == blk.end()) return 0;
+            on_path.insert(h);
+            uint32_t best = 0;
+            for (uint32_t t : direct_succ(*bi->second)) {
+                if (is_cp(t)) continue;
+                if (on_path.count(t)) { forced_cp.insert(t); continue; }   // (defensive: a cycle of non-headers)
+                best = std::max(best, longest(t));
+            }
+            on_path.erase(h);
+            return run_len[h] = (uint32_t)bi->second->insts.size() + best;
+        };
+        for (const Block &b : blocks)
+            if (b.opc == 0) longest(b.h0);
+        if (!forced_cp.empty()) {   // recompute with those as check points
+            run_len.clear();
+            for (const Block &b : blocks)
+                if (b.opc == 0) longest(b.h0);
+        }
+    }
+
     g.put("tx_dispatch: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", (unsigned long long)text_lo);
     g.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto tx_out;\n  switch ((uint32_t)off_ >> 1) {\n");
     for (uint32_t h : leaders) {
@@ -631,7 +791,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     }
     g.put("  default: goto tx_out;\n  }\n}\n");
     // solo dispatch (plain or with the odd-pc entries)
-    auto sdispatch = [&](Gen &sx) {
+    auto sdispatch = [&](Gen &sx, bool clean) {
         sx.put("%s: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", SD.c_str(), (unsigned long long)text_lo);
         if (!oddon) {
             sx.put("  if ((off_ >> 32) != 0 || (off_ & 1)) goto S_out;\n  switch ((uint32_t)off_ >> 1) {\n");
@@ -645,10 +805,15 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         }
         for (uint32_t h : leaders) {
             auto it = S.chain.find(h);
+            auto hp = hang_proof.find(h);
+            sx.put("  case %u: ", h);
+            if (clean && hp != hang_proof.end())
+                sx.put("if (TXHANG(X%u, %d, %uu)) { spc = %s; hang = 1u; goto S_out; } ", hp->second.reg,
+                       hp->second.step, hp->second.m, hex(g.pc_of(h)).c_str());
             if (it == S.chain.end() || (it->second.size() == 1 && it->second[0] == h))
-                sx.put("  case %u: goto %s%u;\n", h, SB.c_str(), h);
+                sx.put("goto %s%u;\n", SB.c_str(), h);
             else
-                sx.put("  case %u: etgt = %uu; eon = 1; goto %s%u;\n", h, h, SB.c_str(), it->second[0]);
+                sx.put("etgt = %uu; eon = 1; goto %s%u;\n", h, SB.c_str(), it->second[0]);
         }
         sx.put("  default: goto S_out;\n  }\n}\n");
     };
@@ -662,8 +827,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     Gen &so_ = oddon ? sq : so;
     std::string g_mode;
     if (oddon) g_mode.swap(g.out);
-    sdispatch(so_);
-    if (!oddon) sdispatch(sc);
+    sdispatch(so_, false);
+    if (!oddon) sdispatch(sc, true);
     // text that the full and the clean solo bodies share (mode 0)
     auto sboth = [&](const std::string &t) { so_.out += t; if (!oddon) sc.out += t; };
     for (const Block &b : blocks) {
@@ -699,7 +864,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         else
             sboth(sfmt("%s%u: { // pc 0x%llx, %u insts\n", SB.c_str(), h0, (unsigned long long)pc0, n));
         if (!cur_odd && S.headers.count(h0)) {   // a cycle header routes an entry into its cycle one level on (etgt)
-            std::string rw_, rs_;
+            std::string rw_, rs_, rc_;
             for (uint32_t x : leaders) {
                 auto it = S.chain.find(x);
                 if (it == S.chain.end() || x == h0) continue;
@@ -712,6 +877,11 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 const std::string sclr = S.headers.count(next) ? "" : "eon = 0; ";
                 rw_ += "case " + std::to_string(x) + ": " + clr + "goto B_" + std::to_string(next) + "; ";
                 rs_ += "case " + std::to_string(x) + ": " + sclr + "goto " + SB + std::to_string(next) + "; ";
+                // clean body: a routed block that is no check point tests the budget here
+                const std::string chk = (!oddon && next == x && !is_cp(x))
+                    ? sfmt("if (st + %uu > bud) { spc = %s; bst = 1u; goto S_out; } ", run_len[x], hex(g.pc_of(x)).c_str())
+                    : std::string();
+                rc_ += "case " + std::to_string(x) + ": " + sclr + chk + "goto " + SB + std::to_string(next) + "; ";
             }
             const char *fmt = "  if (etgt != 0xFFFFFFFFu) { if (etgt == %uu) etgt = 0xFFFFFFFFu; "
                               "else switch (etgt) { %sdefault: break; } }\n";
@@ -721,7 +891,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             const char *sfm = "  ETGT_OPAQUE(); if (__builtin_expect(eon != 0, 0)) { if (etgt == %uu) eon = 0; "
                               "else switch (etgt) { %sdefault: break; } }\n";
             g.put(fmt, h0, rw_.c_str());
-            sboth(sfmt(sfm, h0, rs_.c_str()));
+            so_.put(sfm, h0, rs_.c_str());
+            if (!oddon) sc.put(sfm, h0, rc_.c_str());
         }
         // ---- wave block prologue: merge a parked group waiting here, leave or
         // switch groups when lanes outside run first, then one combined check
@@ -737,7 +908,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         if (rw) so_.put(" | ((lwm & 0x%xu) != 0)", rw);
         so_.put(" | SDIRTY(%uu, %uu)) { spc = %s; goto S_out; }\n", (uint32_t)(blo - text_lo),
                 (uint32_t)(bhi - text_lo), P0.c_str());
-        if (!oddon) sc.put("  if (st + %uu > bud) { spc = %s; goto S_out; }\n", n, P0.c_str());
+        if (!oddon && is_cp(h0)) sc.put("  if (st + %uu > bud) { spc = %s; bst = 1u; goto S_out; }\n", run_len[h0], P0.c_str());
         uint32_t k_st = 0, k_xt = 0, k_fb = 0, k_db = 0;   // committed so far in this block
         auto commit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
             // per-lane counters of the running lanes (zero terms omitted), wave iterations

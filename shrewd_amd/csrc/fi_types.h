@@ -134,6 +134,7 @@ struct DevCtx {
     uint64_t snap_interval;          // I: snapshot k is at numInst == k * I
     uint32_t n_snap;
     uint32_t early_exit;             // compare with snapshots after the injection (bit 1: also with wrong output)
+    uint32_t hang_proof;             // the clean translated body may prove hangs (counted loops)
     // golden reference output (or record buffers in golden mode)
     const uint8_t *gout, *gerr;
     uint64_t gout_len, gerr_len;
@@ -232,6 +233,7 @@ struct DevCtx {
                                      // pages (FI_ESC_RESOURCE, fi_engine.cpp run_chunk)
                                      // [52] record mode: 1 + numInst of the golden run's last curTick read
                                      // [53] solo_fast_run calls [54] instructions they ran [55] hand-backs
+                                     // [56] hangs proved by the clean body's counted-loop test
                                      // [32..39] FI_PROF phase cycles
                                      // [40 + 4k + {0,1,2,3}] fetch B, data B, pages, device insts of kernel k
                                      // (0 the 64-lane kernel, 1 solo, 2 solo-odd)

@@ -1531,6 +1531,8 @@ struct SoloTxIO {
     uint32_t bud, lwm, sdlo, sdhi;       // in: instruction budget, watched-register mask, rewritten range
     uint32_t st, xt, fb, db;             // out: instructions, straddle ticks, fetch / data bytes
     uint32_t cslo, cshi, schg;           // out: code bytes the blocks rewrote (offsets from text_lo)
+    uint32_t hleft, hok, hang;           // in: instructions to the hang cap, proofs allowed; out: proved a hang
+    uint32_t bst;                        // out: left at a budget test (clean body: the budget may be unspent)
 };
 typedef __attribute__((address_space(3))) SoloTxIO lds_io;
 
@@ -1600,11 +1602,21 @@ S_out:
         mp->code_dirty = true; mp->dlo = m.dlo; mp->dhi = m.dhi;
     }
     io->spc = spc; io->st = st; io->xt = xt; io->fb = fb; io->db = db;
-    io->cslo = cslo; io->cshi = cshi; io->schg = schg ? 1u : 0u;
+    io->cslo = cslo; io->cshi = cshi; io->schg = schg ? 1u : 0u; io->hang = 0u; io->bst = 0u;
 }
 #endif
 
 #ifdef FI_TX
+// A counted loop (fi_translate.cpp) whose counter x steps by c = +-1 and ends
+// it at zero passes its branch n more times, x + n c = 0 (mod 2^64; 2^64 for
+// x = 0), at least m instructions apart: it commits (n - 1) m of them before
+// it can leave -- a hang if that reaches `left`, the instructions to the cap.
+__device__ __forceinline__ bool tx_hang_proof(uint64_t x, int c, uint32_t m, uint32_t left) {
+    const uint64_t n = c < 0 ? x : 0 - x;
+    if (n == 0) return true;
+    return n - 1 >= ((uint64_t)left + m - 1) / m;
+}
+
 // The clean solo body (fi_translate.cpp): for a trial that rewrote no code and
 // watches no register, blocks without those checks (a store into the code
 // range leaves before itself).  Same calling convention as solo_tx_run.
@@ -1623,6 +1635,11 @@ __device__ __noinline__ void solo_tx_clean_run(KCtx *CX, lds_u64 *R, lds_mem *mp
     const uint32_t bud = io->bud;
     uint32_t etgt = 0xFFFFFFFFu, eon = 0;
     uint32_t st = 0, xt = 0, fb = 0, db = 0;
+    // counted-loop hang proofs (fi_translate.cpp): entering such a cycle with
+    // its counter this far from zero, the trial reaches the hang cap inside it
+    const uint32_t hleft = io->hleft, hok = io->hok;
+    uint32_t hang = 0, bst = 0;
+#define TXHANG(x_, c_, m_) (hok && tx_hang_proof((x_), (c_), (m_), hleft - st))
 #define TXR(r) uint64_t X##r = R[r];
     TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
     TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
@@ -1636,8 +1653,9 @@ S_out:
     TXW(14) TXW(15) TXW(16) TXW(17) TXW(18) TXW(19) TXW(20) TXW(21) TXW(22) TXW(23) TXW(24) TXW(25)
     TXW(26) TXW(27) TXW(28) TXW(29) TXW(30) TXW(31)
 #undef TXW
+#undef TXHANG
     io->spc = spc; io->st = st; io->xt = xt; io->fb = fb; io->db = db;
-    io->cslo = 0xFFFFFFFFu; io->cshi = 0u; io->schg = 0u;
+    io->cslo = 0xFFFFFFFFu; io->cshi = 0u; io->schg = 0u; io->hang = hang; io->bst = bst;
 }
 #endif
 
@@ -3011,6 +3029,7 @@ __device__ __forceinline__ void trial_body() {
     bool suspended = false;
     const uint64_t start_inst = (live && !resume) ? L.ninst : 0;
     const uint64_t launch_inst = live ? L.ninst : 0;   // executed instructions = L.ninst - this at the end
+    uint64_t proved_skip = 0;                           // ... less those a proved hang skipped
     uint64_t pages_made = 0;
     uint64_t next_snap = (CX->record && CX->rec_interval) ? 0 : kNone;   // record mode: capture points
     uint32_t snaps_taken = 0;
@@ -3169,7 +3188,8 @@ __device__ __forceinline__ void trial_body() {
                 L.next_chk = k < CX->n_snap ? k * CX->snap_interval : kNone;
             }
         }
-        if (!L.done && L.ninst >= CX->hang_cap) finish(L, FI_HANG, 1, 0, (uint32_t)L.pc);
+        // (a hang's record names no pc: a proved hang, below, ends before the cap)
+        if (!L.done && L.ninst >= CX->hang_cap) finish(L, FI_HANG, 1, 0, 0u);
 
         // ---- B'. golden comparator at snapshot boundaries (exact early exit)
         if (CX->early_exit) {
@@ -3450,6 +3470,11 @@ __device__ __forceinline__ void trial_body() {
                     const uint64_t tlo = CX->text_lo;
                     __shared__ SoloTxIO sio[1];
                     sio->spc = lpc; sio->bud = bud; sio->lwm = L.watch > 0 ? (1u << L.watch) : 0u;
+                    {
+                        const uint64_t hl = CX->hang_cap - L.ninst;
+                        sio->hleft = hl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)hl;
+                        sio->hok = CX->hang_proof && (L.injected == 1 || L.injected == 2) ? 1u : 0u;
+                    }
                     sio->sdlo = m.code_dirty ? (uint32_t)((m.dlo > tlo ? m.dlo : tlo) - tlo) : 0xFFFFFFFFu;
                     sio->sdhi = m.code_dirty ? (uint32_t)((m.dhi > tlo ? m.dhi : tlo) - tlo) : 0u;
                     if (!kOdd && !m.code_dirty && L.watch <= 0)
@@ -3470,11 +3495,22 @@ __device__ __forceinline__ void trial_body() {
                     n_iter += st;
                     n_tx += st;
                     n_txin++;
+                    if (uni32(sio->hang)) {   // a proved hang: the record of one that ran to the cap
+                        proved_skip = CX->hang_cap - L.ninst;
+                        L.ninst = CX->hang_cap;
+                        finish(L, FI_HANG, 1, 0, 0u);
+                        atomicAdd(&CX->stats[56], 1ull);
+                        continue;
+                    }
                     if (m.code_dirty && st < 8) {
                         if (++tx_short >= 4) { tx_short = 0; tx_skip_until = n_iter + 4096; }
                     } else {
                         tx_short = 0;
                     }
+                    // the clean body tests its budget once per run of blocks: one that
+                    // stops at a test with nothing run leaves the rest up to the event
+                    // (fewer instructions than the run) to the interpreter
+                    if (!st && uni32(sio->bst)) tx_skip_until = n_iter + bud;
                     if (st) continue;
                 }
             } else if (tx_entry &&
@@ -4385,7 +4421,7 @@ __device__ __forceinline__ void trial_body() {
         wd[4] = rt_start;                                // s_memrealtime (100 MHz) at the wave's start / end
         wd[5] = __builtin_amdgcn_s_memrealtime();
         wd[6] = live ? (uint64_t)sidx : ~0ULL;           // lane 0's trial (index into the sites)
-        wd[7] = live ? L.ninst - launch_inst : 0;        // lane 0's instructions in this dispatch
+        wd[7] = live ? L.ninst - launch_inst - proved_skip : 0;   // lane 0's instructions in this dispatch
         wd[8] = n_txin;                                  // translated-code entries
         wd[9] = m.nmiss;                                 // lane 0's full page-table lookups
     }
@@ -4396,7 +4432,7 @@ __device__ __forceinline__ void trial_body() {
     if (CX->record) pages_made = m.n_priv;   // golden: every private entry (pages, tombstones)
     const uint64_t fb = wsum64<kNL>(L.fetch_b), db = wsum64<kNL>(L.data_b), pm = wsum64<kNL>(pages_made);
     const uint64_t si = wsum64<kNL>(start_inst);
-    const uint64_t xi = wsum64<kNL>(live ? L.ninst - launch_inst : 0);
+    const uint64_t xi = wsum64<kNL>(live ? L.ninst - launch_inst - proved_skip : 0);
     if (lane == 0 && kSoloOnce) {
         atomicAdd(&CX->stats[23], (unsigned long long)xi);
         atomicAdd(&CX->stats[0], (unsigned long long)fb);

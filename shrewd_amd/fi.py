@@ -109,6 +109,7 @@ CFG_NO_SDC_EXIT = 1024
 CFG_NO_REDO = 2048
 CFG_NO_ODD_KERNEL = 4096
 CFG_JIT_NO_CACHE = 8192
+CFG_NO_HANG_PROOF = 16384
 
 
 class GoldenInfo(C.Structure):

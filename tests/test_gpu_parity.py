@@ -312,7 +312,7 @@ def test_dead_memory_faults_end_at_injection(engine_factory, oracle_mod):
 PATH_FLAGS = {
     "default": 0,
     "no_translate": 4,                      # FI_CFG_NO_TRANSLATE: interpreter only
-    "from_start": 1 | 2,                    # FI_CFG_NO_SNAPSHOT_START | FI_CFG_NO_EARLY_EXIT
+    "from_start": 1 | 2 | 16384,            # FI_CFG_NO_SNAPSHOT_START | NO_EARLY_EXIT | NO_HANG_PROOF
     "no_epochs": 8,                         # FI_CFG_NO_EPOCHS
     "pack_runs": 16,                        # FI_CFG_PACK_RUNS
     "fixed_resume": 32,                     # FI_CFG_FIXED_RESUME
@@ -350,8 +350,34 @@ def test_execution_paths_bit_exact(engine_factory, oracle_mod, name, path):
     dev, hist = e.run_sites(sites)
     compare(dev, ref, sites)
     assert int(hist["device_insts"]) <= int(hist["guest_insts"])
-    if PATH_FLAGS[path] & 1:   # from process start with no early exit: the device runs every instruction
+    if PATH_FLAGS[path] & 1:   # from process start, no early exit, no hang proofs: the device runs every instruction
         assert int(hist["device_insts"]) == int(hist["guest_insts"])
+
+
+def test_counted_loop_hang_proofs(engine_factory, oracle_mod):
+    """crc32's t6 flips loop in the table's inner bit loop (a counted loop:
+    addi t6, t6, -1; bnez t6) until the hang cap.  The clean translated body
+    proves those hangs when it enters the loop (fi_translate.cpp): the records
+    equal a run without the proofs (FI_CFG_NO_HANG_PROOF: every hang runs to
+    the cap) and the oracle's, with fewer instructions executed."""
+    from shrewd_amd.fi import CFG_NO_HANG_PROOF
+    n = 20000
+    on = engine_factory("crc32", max_trials_per_launch=n)
+    off = engine_factory("crc32", flags=CFG_NO_HANG_PROOF, max_trials_per_launch=n)
+    for e in (on, off):
+        e.set_campaign(0x5EED0002, REGS | PC, 1)
+        e.set_protect(0)
+    a, ha = on.run_trials(0, n)
+    proved = int(on.debug_stats()[56])
+    b, hb = off.run_trials(0, n)
+    assert int(off.debug_stats()[56]) == 0
+    assert np.array_equal(a, b)
+    hang = np.nonzero(a["cls"] == 3)[0]
+    assert len(hang) > 20 and proved > 0 and proved <= len(hang)
+    assert (a["detail"][hang] == 0).all()
+    assert int(ha["device_insts"]) < int(hb["device_insts"])
+    sites = on.sample(0, n)[hang]
+    compare(a[hang], oracle_for(oracle_mod, "crc32").run_trials(sites), sites)
 
 
 def test_run_trials_equals_run_sites(engine_factory):
