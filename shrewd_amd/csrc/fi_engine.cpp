@@ -55,7 +55,7 @@ hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome
                                hipStream_t st);
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
                             uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, bool solo,
-                            hipStream_t st);
+                            uint64_t golden_ninst, hipStream_t st);
 hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,
                             hipStream_t st);
 std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
@@ -1490,7 +1490,8 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
             c.resume_n = nullptr;
         } else {
             HIPCHK(launch_surv_keys(e->d_save, e->d_surv[(ep - 1) & 1], e->d_cnt + ep - 1, k, c.text_lo, e->d_skeys,
-                                    e->d_svals, odd ? e->d_split + 4 * ep : nullptr, solo && !pack, st));
+                                    e->d_svals, odd ? e->d_split + 4 * ep : nullptr, solo && !pack, e->golden.ninst,
+                                    st));
             HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_skeys, e->d_skeys2, e->d_svals, e->d_svals2, k, 64, st));
             c.resume = e->d_svals2;
             c.resume_n = e->d_cnt + ep - 1;

@@ -231,18 +231,24 @@ __global__ void __launch_bounds__(256) fi_hist_kernel(const fi_site *sites, cons
 // ~20x the cost of translated code) start first, then the rest longest-first.
 __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
                                     uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd,
-                                    uint32_t solo) {
+                                    uint32_t solo, uint64_t golden_ninst) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cap) return;
     if (i < *cnt) {
         const uint32_t sl = list[i];
         const uint64_t pc = save[sl].pc;
         uint64_t k = ((pc - text_lo) << 32) | (save[sl].ninst & 0xFFFFFFFFu);
-        // solo epoch: code-rewriting survivors first, then longest-first -- the
-        // fewest committed instructions have the most left to run (golden
-        // suffix or hang cap); one survivor per wave, so no pc grouping
-        // (profiles/r03k_ab_lpt.jsonl: crc32 +4 %, intmix +5 %)
-        if (solo) k = ((uint64_t)(((save[sl].flags >> 3) & 1) ^ 1) << 62) | (save[sl].ninst & ((1ULL << 46) - 1));
+        // solo epoch: code-rewriting survivors and those already past the
+        // golden run's end first (the first are interpreted, the second went
+        // somewhere the golden run did not -- a re-run of the program, a loop
+        // to the hang cap: profiles/r04v_solo_timeline_crc32.jsonl), then
+        // longest-first -- the fewest committed instructions have the most
+        // left to run (golden suffix or hang cap); one survivor per wave, so
+        // no pc grouping (profiles/r03k_ab_lpt.jsonl: crc32 +4 %, intmix +5 %)
+        if (solo) {
+            const bool first = ((save[sl].flags >> 3) & 1) || save[sl].ninst > golden_ninst;
+            k = ((uint64_t)(first ? 0 : 1) << 62) | (save[sl].ninst & ((1ULL << 46) - 1));
+        }
         if (n_odd) {
             k = ((pc & 1) << 63) | (k >> 1);
             if (pc & 1) atomicAdd(n_odd, 1u);
@@ -370,9 +376,9 @@ hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome
 }
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
                             uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, bool solo,
-                            hipStream_t st) {
+                            uint64_t golden_ninst, hipStream_t st) {
     hipLaunchKernelGGL(fi_surv_keys_kernel, dim3(nblk(cap, 256)), dim3(256), 0, st, save, list, cnt, cap, text_lo,
-                       keys, vals, n_odd, solo ? 1u : 0u);
+                       keys, vals, n_odd, solo ? 1u : 0u, golden_ninst);
     return hipGetLastError();
 }
 hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,
