@@ -1694,7 +1694,10 @@ constexpr uint32_t kSoloDC = 64;   // decode-cache entries (power of two)
 // micro-op kind.  Here the 31 guest registers live in VGPRs v64..v127 of the
 // one active lane (x_r = v[64 + 2r] lo, v[65 + 2r] hi), read and written
 // through VGPR index mode (s_set_gpr_idx_on), and everything else is SALU:
-// ~40 instructions for an ALU op, the kind dispatched through a jump table.
+// ~40 instructions for an ALU op, the kind dispatched through a jump table;
+// the entries of the pcs it runs are kept in a 64-entry cache in VGPR lanes
+// (v24..v27, lane (po >> 1) & 63, read with v_readlane), so a loop reads no
+// LDS (rewritten code) after its first iteration.
 // It runs every micro-op but K_SLOW -- add / sub / and / or / xor / slt(u) /
 // shifts / mul / mulh(s)(u) / div(u) / rem(u) (also the W forms), aligned
 // in-page loads and stores through a two-entry page cache in front of the
@@ -1767,6 +1770,12 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_addc_u32 s81, s81, 0\n"
         "s_mov_b64 s[70:71], -1\n"          // page cache slot 1: empty
         "s_mov_b64 s[72:73], 0\n"
+        // the entry cache in VGPR lanes: v24 tag (po) / v25..v27 entry words
+        // y z w, lane (po >> 1) & 63; empty at every call (all 64 lanes)
+        "s_mov_b64 s[74:75], exec\n"
+        "s_mov_b64 exec, -1\n"
+        "v_mov_b32 v24, -1\n"
+        "s_mov_b64 exec, s[74:75]\n"
         "ds_read2_b64 v[64:67], v15 offset0:0 offset1:1\n"
         "ds_read2_b64 v[68:71], v15 offset0:2 offset1:3\n"
         "ds_read2_b64 v[72:75], v15 offset0:4 offset1:5\n"
@@ -1788,18 +1797,16 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "L_top%=:\n"
         "s_cmp_ge_u32 s6, s7\n"
         "s_cbranch_scc1 L_budget%=\n"
-        // ---- the entry: the decode cache inside the rewritten window (L_win,
-        // out of line: the common path falls through), else pre[]
-        "s_add_u32 s62, s5, 6\n"
-        "s_cmp_gt_u32 s62, s12\n"
-        "s_cbranch_scc1 L_win%=\n"
-        "L_pre%=:\n"                        // entry (po >> 1) | (po & 1), 16 bytes each
-        "s_bitcmp1_b32 s5, 0\n"
-        "s_cbranch_scc1 L_preo%=\n"         // (odd pc: out of line)
-        "s_lshl_b32 s62, s5, 3\n"
-        "L_prel%=:\n"
-        "s_load_dwordx4 s[36:39], s[20:21], s62\n"
-        "s_waitcnt lgkmcnt(0)\n"
+        // ---- the entry: the VGPR-lane entry cache (a loop runs from it with
+        // no memory wait), else (L_lmiss, out of line) the decode cache inside
+        // the rewritten window or pre[], then filled into the lane cache
+        "s_bfe_u32 s82, s5, 0x60001\n"
+        "v_readlane_b32 s63, v24, s82\n"
+        "s_cmp_eq_u32 s63, s5\n"
+        "s_cbranch_scc0 L_lmiss%=\n"
+        "v_readlane_b32 s37, v25, s82\n"
+        "v_readlane_b32 s38, v26, s82\n"
+        "v_readlane_b32 s39, v27, s82\n"
         "L_have%=:\n"
         // (K_SLOW leaves through the jump table)
         "s_bfe_u32 s56, s39, 0x60010\n"     // kind
@@ -1856,7 +1863,26 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_cbranch_scc1 L_top%=\n"
         "s_mov_b32 s19, 4\n"
         "s_branch L_out%=\n"
-        // ---- out of line: the rewritten window, a leader, the jump table
+        // ---- out of line: the entry fetch, the rewritten window, a leader,
+        // the jump table
+        "L_lmiss%=:\n"
+        "s_add_u32 s62, s5, 6\n"
+        "s_cmp_gt_u32 s62, s12\n"
+        "s_cbranch_scc1 L_win%=\n"
+        "L_pre%=:\n"                        // entry (po >> 1) | (po & 1), 16 bytes each
+        "s_bitcmp1_b32 s5, 0\n"
+        "s_cbranch_scc1 L_preo%=\n"         // (odd pc: out of line)
+        "s_lshl_b32 s62, s5, 3\n"
+        "L_prel%=:\n"
+        "s_load_dwordx4 s[36:39], s[20:21], s62\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "L_fill%=:\n"                       // (lane select in M0: one SGPR operand per VALU op)
+        "s_mov_b32 m0, s82\n"
+        "v_writelane_b32 v24, s5, m0\n"
+        "v_writelane_b32 v25, s37, m0\n"
+        "v_writelane_b32 v26, s38, m0\n"
+        "v_writelane_b32 v27, s39, m0\n"
+        "s_branch L_have%=\n"
         "L_win%=:\n"
         "s_cmp_lt_u32 s5, s13\n"
         "s_cbranch_scc0 L_pre%=\n"
@@ -1875,7 +1901,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "v_readfirstlane_b32 s39, v7\n"
         "s_cmp_eq_u32 s62, s5\n"
         "s_cbranch_scc0 L_slow%=\n"         // a miss: the C++ loop decodes and fills the cache
-        "s_branch L_have%=\n"
+        "s_branch L_fill%=\n"
         "L_lead%=:\n"                       // a block leader the translated code takes?
         "s_bitcmp1_b32 s5, 0\n"
         "s_cselect_b32 s62, s18, s17\n"
@@ -2542,7 +2568,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
           "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27", "s28", "s29",
           "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50",
           "s51", "s52", "s53", "s54", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66",
-          "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81",
+          "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82",
           "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
           "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
           "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77",
