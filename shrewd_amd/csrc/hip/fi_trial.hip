@@ -1817,18 +1817,18 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_bfe_u32 s57, s37, 0x50008\n"     // rd
         "s_bfe_u32 s58, s37, 0x6000f\n"     // 2 rs1 (bit 15: the top of the 8-bit rd field, 0)
         "s_bfe_u32 s59, s37, 0x60017\n"     // 2 rs2 (bit 23: the top of the rs1 field, 0)
+        // a = x[rs1] (av but for U_APC), b = x[rs2]: the index applies to
+        // v_readlane's VGPR source too (lane 0: the solo wave's one lane)
         "s_set_gpr_idx_on s58, gpr_idx(SRC0)\n"
-        "v_mov_b64 v[0:1], v[64:65]\n"
+        "v_readlane_b32 s44, v64, 0\n"
+        "v_readlane_b32 s45, v65, 0\n"
         "s_set_gpr_idx_off\n"
         "s_set_gpr_idx_on s59, gpr_idx(SRC0)\n"
-        "v_mov_b64 v[2:3], v[64:65]\n"
+        "v_readlane_b32 s42, v64, 0\n"
+        "v_readlane_b32 s43, v65, 0\n"
         "s_set_gpr_idx_off\n"
         "s_ashr_i32 s53, s38, 31\n"         // imm, sign-extended
         "s_mov_b32 s52, s38\n"
-        "v_readfirstlane_b32 s44, v0\n"     // a = x[rs1] (av but for U_APC)
-        "v_readfirstlane_b32 s45, v1\n"
-        "v_readfirstlane_b32 s42, v2\n"     // b = x[rs2]
-        "v_readfirstlane_b32 s43, v3\n"
         "s_bitcmp1_b32 s39, 25\n"           // U_APC (aux = w >> 16): av = pc (out of line)
         "s_cbranch_scc1 L_apc%=\n"
         "L_apcb%=:\n"
