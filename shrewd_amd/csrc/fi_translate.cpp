@@ -636,8 +636,35 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     // snapshot either (the golden run would then run that loop past the cap
     // too).  The clean body's dispatch tests it (TXHANG) whenever it enters
     // such a cycle, i.e. once per call.
-    struct HangProof { uint32_t reg; int step; uint32_t m; };
+    //
+    // Run-off loops (one block that branches to itself): the same counter
+    // test, the exit also against a register the block does not write (bne
+    // a0, a1), steps of +-1, 2, 4, 8, and plain loads whose address is either
+    // the counter plus a constant or a register the block does not write plus
+    // a bounded offset (andi / slli / shNadd chains: a table lookup).  Such a
+    // loop that cannot leave before the cap either faults on a counter load's
+    // first page that is not mapped (a crash at an exact instruction) or
+    // reaches the cap; the kernel decides which from the lane's page set
+    // (loop_outcome, fi_trial.hip), so the body only passes the loads on.
+    struct ProofLoad { uint32_t reg, kind, size, pos; int64_t off; uint64_t span; };   // kind 0 counter, 1 bounded
+    struct HangProof { uint32_t reg, treg; int step; uint32_t m; std::vector<ProofLoad> loads; };
     std::map<uint32_t, HangProof> hang_proof;
+    // abstract value of a register inside a run-off block: TOP unknown; CNT the
+    // counter's value at the iteration's start + lo; BND base register (0: none)
+    // plus an offset in [lo, hi]
+    struct AVal { int k; uint32_t base; int64_t lo, hi; };
+    enum { AV_TOP, AV_CNT, AV_BND };
+    const int64_t kAvLim = (int64_t)1 << 40;
+    auto av_ok = [&](AVal v) { return v.k == AV_BND && v.lo > -kAvLim && v.hi < kAvLim && v.lo <= v.hi ? v : AVal{AV_TOP, 0, 0, 0}; };
+    auto av_add = [&](AVal a, AVal b) -> AVal {
+        if (a.k != AV_BND || b.k != AV_BND || (a.base && b.base)) return AVal{AV_TOP, 0, 0, 0};
+        return av_ok(AVal{AV_BND, a.base | b.base, a.lo + b.lo, a.hi + b.hi});
+    };
+    auto av_shl = [&](AVal a, int64_t k) -> AVal {
+        if (a.k != AV_BND || a.base || a.lo < 0 || k < 0 || k > 20) return AVal{AV_TOP, 0, 0, 0};
+        return av_ok(AVal{AV_BND, 0, a.lo << k, a.hi << k});
+    };
+    auto av_const = [&](int64_t lo, int64_t hi) { return av_ok(AVal{AV_BND, 0, lo, hi}); };
     for (uint32_t H : S.headers) {
         std::vector<uint32_t> cyc;
         bool nested = false;
@@ -674,8 +701,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 const PreInst &p = pre[b.insts[i]];
                 const uint64_t pc = text_lo + 2ULL * b.insts[i];
                 const Cls k = classify(p, e, sz, sx, cond);
-                if (k == C_LOAD || k == C_STORE || k == C_JALR || k == C_STOP) ok = false;
-                if ((k == C_ALU || k == C_JAL) && p.rd) writes[p.rd]++;
+                if (k == C_STORE || k == C_JALR || k == C_STOP || (k == C_LOAD && in.size() != 1)) ok = false;
+                if ((k == C_ALU || k == C_JAL || k == C_LOAD) && p.rd) writes[p.rd]++;
                 if (k == C_BR) { to(pc + (int64_t)p.imm, true); to(pc + p.len, false); }
                 if (k == C_JAL) to(pc + (int64_t)p.imm, true);
             }
@@ -684,23 +711,76 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         if (!ok || n_exit != 1) continue;
         const Block &E = *bl[eblk];
         const PreInst &br = pre[E.insts.back()];
-        uint32_t reg = 0;
-        bool exit_when_zero = false;   // the exit edge is taken when Xk == 0
+        uint32_t reg = 0, treg = 0;    // counter, and the register it is compared with (0: zero)
+        bool exit_when_zero = false;   // the exit edge is taken when Xk == X[treg]
         if (br.op == OP_c_beqz || br.op == OP_c_bnez) {
             reg = br.rs1;
             exit_when_zero = (br.op == OP_c_beqz) == exit_on_taken;
         } else if ((br.op == OP_beq || br.op == OP_bne) && (br.rs1 == 0) != (br.rs2 == 0)) {
             reg = br.rs1 ? br.rs1 : br.rs2;
             exit_when_zero = (br.op == OP_beq) == exit_on_taken;
+        } else if ((br.op == OP_beq || br.op == OP_bne) && br.rs1 && br.rs2 && br.rs1 != br.rs2) {
+            if (writes[br.rs1] == 1 && writes[br.rs2] == 0) { reg = br.rs1; treg = br.rs2; }
+            else if (writes[br.rs2] == 1 && writes[br.rs1] == 0) { reg = br.rs2; treg = br.rs1; }
+            exit_when_zero = (br.op == OP_beq) == exit_on_taken;
         }
         if (!reg || !exit_when_zero || writes[reg] != 1) continue;
         int step = 0;
         for (size_t i = 0; i + 1 < E.insts.size(); i++) {
             const PreInst &p = pre[E.insts[i]];
-            if ((p.op == OP_addi || p.op == OP_c_addi) && p.rd == reg && p.rs1 == reg && (p.imm == 1 || p.imm == -1))
+            const int a = p.imm < 0 ? -p.imm : p.imm;
+            if ((p.op == OP_addi || p.op == OP_c_addi) && p.rd == reg && p.rs1 == reg && (a == 1 || a == 2 || a == 4 || a == 8))
                 step = p.imm;
         }
         if (!step) continue;
+        // run-off block: the loads' addresses
+        std::vector<ProofLoad> loads;
+        if (in.size() == 1) {
+            AVal av[32];
+            for (uint32_t r = 0; r < 32; r++) av[r] = writes[r] ? AVal{AV_TOP, 0, 0, 0} : AVal{AV_BND, r, 0, 0};
+            av[reg] = AVal{AV_CNT, 0, 0, 0};
+            for (size_t i = 0; i < E.insts.size() && ok; i++) {
+                std::string e;
+                uint32_t sz;
+                int sx;
+                const char *cond;
+                const PreInst &p = pre[E.insts[i]];
+                const Cls k = classify(p, e, sz, sx, cond);
+                const AVal A = av[p.rs1], B = av[p.rs2];
+                const int64_t imm = p.imm;
+                if (k == C_LOAD) {
+                    if (A.k == AV_CNT) loads.push_back({reg, 0u, sz, (uint32_t)i, A.lo + imm, 0u});
+                    else if (A.k == AV_BND) loads.push_back({A.base, 1u, sz, (uint32_t)i, A.lo + imm, (uint64_t)(A.hi - A.lo)});
+                    else ok = false;
+                    if (p.rd) av[p.rd] = AVal{AV_TOP, 0, 0, 0};
+                    continue;
+                }
+                if (!p.rd || (k != C_ALU && k != C_JAL)) continue;
+                AVal v{AV_TOP, 0, 0, 0};
+                if (k == C_ALU) switch (p.op) {
+                case OP_addi: case OP_c_addi: case OP_c_addi4spn: case OP_c_addi16sp:
+                    if (A.k == AV_CNT) v = AVal{AV_CNT, 0, A.lo + imm, A.lo + imm};
+                    else v = av_add(A, av_const(imm, imm));
+                    break;
+                case OP_add: case OP_c_add: v = av_add(A, B); break;
+                case OP_c_mv: v = B; break;
+                case OP_andi: case OP_c_andi: if (imm >= 0) v = av_const(0, imm); break;
+                case OP_c_zext_b: v = av_const(0, 0xFF); break;
+                case OP_c_zext_h: v = av_const(0, 0xFFFF); break;
+                case OP_slli: case OP_c_slli: v = av_shl(A, imm); break;
+                case OP_srli: case OP_c_srli: if (imm >= 44 && imm < 64) v = av_const(0, (int64_t)((1ULL << (64 - imm)) - 1)); break;
+                case OP_sh1add: v = av_add(av_shl(A, 1), B); break;
+                case OP_sh2add: v = av_add(av_shl(A, 2), B); break;
+                case OP_sh3add: v = av_add(av_shl(A, 3), B); break;
+                case OP_c_li: case OP_lui: v = av_const(imm, imm); break;
+                default: break;
+                }
+                av[p.rd] = v;
+            }
+            for (const ProofLoad &l : loads)
+                if (l.off <= -((int64_t)1 << 31) || l.off >= ((int64_t)1 << 31) || l.span >= (1u << 20)) ok = false;
+            if (!ok || loads.size() > 4) continue;
+        }
         // m: the fewest instructions from E's successor in the cycle around to E's end
         std::map<uint32_t, uint32_t> dist;
         std::set<std::pair<uint32_t, uint32_t>> q;
@@ -720,7 +800,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             }
         }
         if (!m) continue;
-        for (uint32_t h : cyc) hang_proof[h] = {reg, step, m};
+        for (uint32_t h : cyc) hang_proof[h] = {reg, treg, step, m, loads};
     }
 
     // ---- clean body budget tests.  Only a check point tests the budget: a
@@ -807,9 +887,19 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             auto it = S.chain.find(h);
             auto hp = hang_proof.find(h);
             sx.put("  case %u: ", h);
-            if (clean && hp != hang_proof.end())
-                sx.put("if (TXHANG(X%u, %d, %uu)) { spc = %s; hang = 1u; goto S_out; } ", hp->second.reg,
-                       hp->second.step, hp->second.m, hex(g.pc_of(h)).c_str());
+            if (clean && hp != hang_proof.end()) {
+                const HangProof &P = hp->second;
+                const std::string x = P.treg ? sfmt("X%u - X%u", P.reg, P.treg) : sfmt("X%u", P.reg);
+                sx.put("if (TXHANG(%s, %d, %uu)) { spc = %s; hang = 1u; TXLOOP(%uu, %uu, %uu); ", x.c_str(), P.step, P.m,
+                       hex(g.pc_of(h)).c_str(), P.reg | P.treg << 8 | (uint32_t)(uint8_t)(int8_t)P.step << 16, P.m,
+                       (uint32_t)P.loads.size());
+                for (size_t j = 0; j < P.loads.size(); j++) {
+                    const ProofLoad &l = P.loads[j];
+                    sx.put("TXLD(%u, %uu, %d, %uu); ", (uint32_t)j, l.reg | l.kind << 8 | l.size << 12 | l.pos << 16,
+                           (int)l.off, (uint32_t)l.span);
+                }
+                sx.put("goto S_out; } ");
+            }
             if (it == S.chain.end() || (it->second.size() == 1 && it->second[0] == h))
                 sx.put("goto %s%u;\n", SB.c_str(), h);
             else

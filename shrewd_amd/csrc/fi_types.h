@@ -234,6 +234,7 @@ struct DevCtx {
                                      // [52] record mode: 1 + numInst of the golden run's last curTick read
                                      // [53] solo_fast_run calls [54] instructions they ran [55] hand-backs
                                      // [56] hangs proved by the clean body's counted-loop test
+                                     // [57] page-fault crashes proved in run-off loops [58] loop proofs undecided
                                      // [32..39] FI_PROF phase cycles
                                      // [40 + 4k + {0,1,2,3}] fetch B, data B, pages, device insts of kernel k
                                      // (0 the 64-lane kernel, 1 solo, 2 solo-odd)

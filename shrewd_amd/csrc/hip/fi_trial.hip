@@ -1531,8 +1531,15 @@ struct SoloTxIO {
     uint32_t bud, lwm, sdlo, sdhi;       // in: instruction budget, watched-register mask, rewritten range
     uint32_t st, xt, fb, db;             // out: instructions, straddle ticks, fetch / data bytes
     uint32_t cslo, cshi, schg;           // out: code bytes the blocks rewrote (offsets from text_lo)
-    uint32_t hleft, hok, hang;           // in: instructions to the hang cap, proofs allowed; out: proved a hang
+    uint32_t hleft, hok, hang;           // in: instructions to the hang cap, proofs allowed; out: a loop that
+                                         // cannot leave before the cap (a hang, or a crash on one of its loads)
     uint32_t bst;                        // out: left at a budget test (clean body: the budget may be unspent)
+    // out with `hang`: the loop (fi_translate.cpp run-off blocks) -- counter |
+    // compared register << 8 | (uint8) step << 16, instructions per iteration,
+    // loads (0: a counted loop without memory access, a hang); per load: reg |
+    // kind << 8 | size << 12 | position << 16, offset, span (loop_outcome)
+    uint32_t lp_cnt, lp_m, lp_n;
+    uint32_t lp_ld[4][3];
 };
 typedef __attribute__((address_space(3))) SoloTxIO lds_io;
 
@@ -1611,10 +1618,95 @@ S_out:
 // it at zero passes its branch n more times, x + n c = 0 (mod 2^64; 2^64 for
 // x = 0), at least m instructions apart: it commits (n - 1) m of them before
 // it can leave -- a hang if that reaches `left`, the instructions to the cap.
+// Steps of +-2, 4, 8: a counter whose distance to zero is not a multiple of
+// the step never reaches it.
+__device__ __forceinline__ uint64_t loop_passes(uint64_t x, int c) {
+    const uint64_t d = c < 0 ? x : 0 - x;
+    const uint32_t a = (uint32_t)(c < 0 ? -c : c);
+    if (d & (a - 1)) return ~0ULL;
+    const uint64_t n = d / a;
+    return n ? n : ~0ULL;   // (0: 2^64 / a passes)
+}
 __device__ __forceinline__ bool tx_hang_proof(uint64_t x, int c, uint32_t m, uint32_t left) {
-    const uint64_t n = c < 0 ? x : 0 - x;
-    if (n == 0) return true;
+    const uint64_t n = loop_passes(x, c);
     return n - 1 >= ((uint64_t)left + m - 1) / m;
+}
+
+// Is vpn in the lane's page set?  (lookup_full without the TLB insert)
+__device__ __forceinline__ bool page_mapped(KCtx *c, const WaveMem &w, const LaneMem &m, uint64_t slot, uint64_t vpn) {
+    for (uint32_t i = m.n_priv; i-- > 0;) {
+        const uint64_t e = c->priv_vpn[(uint64_t)i * c->n_slots + slot];
+        if ((e & ~kTomb) == vpn) return !(e & kTomb);
+    }
+    return tab_find(w.tab, w.tab_n, vpn) >= 0 || (vpn >= (m.stack_min >> 12) && vpn <= kStackTopVpn);
+}
+
+// The outcome of a run-off loop that the clean body found unable to leave
+// before the hang cap (fi_translate.cpp; the registers are the ones at the
+// loop's first instruction, `left` the instructions to the cap).  Iteration i
+// runs the block's instruction at position p as the (i m + p)-th from here,
+// if i < n (the n-th pass of the branch leaves) and i m + p < left.  Loads at
+// the counter plus a constant walk through memory; bounded loads (a table
+// lookup) stay inside [base + off, base + off + span + size).
+//   2: a counter load first touches a page outside the lane's set that
+//      MemState::fixupFault would not map (mem_state.cc:387-447) -- the
+//      process dies there with GenericPageTableFault (sim/faults.cc:95-105):
+//      *k instructions commit first, *fva is the address;
+//   1: no load faults before the cap: a hang;
+//   0: undecided (a page the fault handler would map, a table page outside
+//      the set, a counter load that could straddle a line, many pages, or
+//      the loop leaves before the cap): the trial runs on.
+__device__ __noinline__ int loop_outcome(KCtx *c, const WaveMem &w, const LaneMem &m, uint64_t slot, const lds_u64 *R,
+                                         const lds_io *io, uint64_t left, uint64_t &k, uint64_t &fva) {
+    const uint32_t cnt = io->lp_cnt, mm = io->lp_m, nl = io->lp_n;
+    const uint32_t cr = cnt & 0xFF, tr = (cnt >> 8) & 0xFF;
+    const int cs = (int)(int8_t)(uint8_t)(cnt >> 16);
+    if (!mm || nl > 4 || !cr) return 0;
+    const uint64_t x = R[cr], n = loop_passes(x - (tr ? R[tr] : 0ULL), cs);
+    uint64_t best_k = ~0ULL, best_a = 0;
+    for (uint32_t j = 0; j < nl; j++) {
+        const uint32_t d = io->lp_ld[j][0], br = d & 0xFF, kind = (d >> 8) & 15, size = (d >> 12) & 15, pos = d >> 16;
+        const int64_t off = (int64_t)(int32_t)io->lp_ld[j][1];
+        if (kind == 1) {   // bounded: every page of its range in the set
+            const uint64_t lo = (br ? R[br] : 0ULL) + (uint64_t)off, hi = lo + io->lp_ld[j][2] + size - 1;
+            if (hi < lo || (hi >> 12) - (lo >> 12) > 8) return 0;
+            for (uint64_t v = lo >> 12; v <= (hi >> 12); v++)
+                if (!page_mapped(c, w, m, slot, v)) return 0;
+            continue;
+        }
+        const uint64_t a0 = x + (uint64_t)off, ac = (uint64_t)(cs < 0 ? -cs : cs);
+        if (size > 1 && ((a0 & (size - 1)) || (ac & (size - 1)))) return 0;   // could straddle a 64-byte line
+        if (pos >= left) continue;
+        uint64_t ilim = (left - pos + mm - 1) / mm;   // iterations in which it runs
+        if (n < ilim) ilim = n;
+        uint64_t i = 0;
+        for (uint32_t pg = 0; i < ilim; pg++) {
+            if (pg > 512) return 0;
+            const uint64_t a = a0 + i * (uint64_t)(int64_t)cs, vpn = a >> 12;
+            if (!page_mapped(c, w, m, slot, vpn)) {
+                const uint64_t kj = i * mm + pos;
+                if (kj < best_k) { best_k = kj; best_a = a; }
+                break;
+            }
+            if (cs > 0) {   // the first iteration past this page
+                const uint64_t nx = (vpn + 1) << 12;
+                if (!nx) return 0;
+                i = (nx - a0 + ac - 1) / ac;
+            } else {
+                const uint64_t lo = vpn << 12;
+                if (!lo) return 0;
+                i = (a0 - lo) / ac + 1;
+            }
+        }
+    }
+    if (best_k != ~0ULL) {
+        const uint64_t f = best_a;
+        if (in_vma(c, m, slot, f) || (f >= m.stack_min && f < kStackBase) || (f < m.stack_min && f >= kStackBase - kMaxStack))
+            return 0;
+        k = best_k; fva = f;
+        return 2;
+    }
+    return n - 1 >= (left + mm - 1) / mm ? 1 : 0;
 }
 
 // The clean solo body (fi_translate.cpp): for a trial that rewrote no code and
@@ -1640,6 +1732,8 @@ __device__ __noinline__ void solo_tx_clean_run(KCtx *CX, lds_u64 *R, lds_mem *mp
     const uint32_t hleft = io->hleft, hok = io->hok;
     uint32_t hang = 0, bst = 0;
 #define TXHANG(x_, c_, m_) (hok && tx_hang_proof((x_), (c_), (m_), hleft - st))
+#define TXLOOP(c_, m_, n_) (io->lp_cnt = (c_), io->lp_m = (m_), io->lp_n = (n_))
+#define TXLD(j_, d_, o_, s_) (io->lp_ld[j_][0] = (d_), io->lp_ld[j_][1] = (uint32_t)(o_), io->lp_ld[j_][2] = (s_))
 #define TXR(r) uint64_t X##r = R[r];
     TXR(1) TXR(2) TXR(3) TXR(4) TXR(5) TXR(6) TXR(7) TXR(8) TXR(9) TXR(10) TXR(11) TXR(12) TXR(13)
     TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
@@ -1654,6 +1748,8 @@ S_out:
     TXW(26) TXW(27) TXW(28) TXW(29) TXW(30) TXW(31)
 #undef TXW
 #undef TXHANG
+#undef TXLOOP
+#undef TXLD
     io->spc = spc; io->st = st; io->xt = xt; io->fb = fb; io->db = db;
     io->cslo = 0xFFFFFFFFu; io->cshi = 0u; io->schg = 0u; io->hang = hang; io->bst = bst;
 }
@@ -3055,7 +3151,8 @@ __device__ __forceinline__ void trial_body() {
     bool suspended = false;
     const uint64_t start_inst = (live && !resume) ? L.ninst : 0;
     const uint64_t launch_inst = live ? L.ninst : 0;   // executed instructions = L.ninst - this at the end
-    uint64_t proved_skip = 0;                           // ... less those a proved hang skipped
+    uint64_t proved_skip = 0;                           // ... less those a proved hang or crash skipped
+    bool no_proof = false;                              // a loop proof came out undecided: no more
     uint64_t pages_made = 0;
     uint64_t next_snap = (CX->record && CX->rec_interval) ? 0 : kNone;   // record mode: capture points
     uint32_t snaps_taken = 0;
@@ -3499,7 +3596,7 @@ __device__ __forceinline__ void trial_body() {
                     {
                         const uint64_t hl = CX->hang_cap - L.ninst;
                         sio->hleft = hl > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)hl;
-                        sio->hok = CX->hang_proof && (L.injected == 1 || L.injected == 2) ? 1u : 0u;
+                        sio->hok = CX->hang_proof && !no_proof && (L.injected == 1 || L.injected == 2) ? 1u : 0u;
                     }
                     sio->sdlo = m.code_dirty ? (uint32_t)((m.dlo > tlo ? m.dlo : tlo) - tlo) : 0xFFFFFFFFu;
                     sio->sdhi = m.code_dirty ? (uint32_t)((m.dhi > tlo ? m.dhi : tlo) - tlo) : 0u;
@@ -3521,11 +3618,25 @@ __device__ __forceinline__ void trial_body() {
                     n_iter += st;
                     n_tx += st;
                     n_txin++;
-                    if (uni32(sio->hang)) {   // a proved hang: the record of one that ran to the cap
-                        proved_skip = CX->hang_cap - L.ninst;
-                        L.ninst = CX->hang_cap;
-                        finish(L, FI_HANG, 1, 0, 0u);
-                        atomicAdd(&CX->stats[56], 1ull);
+                    if (uni32(sio->hang)) {   // a loop that cannot leave before the cap
+                        uint64_t kf = 0, fva = 0;
+                        const uint64_t left = L.ninst < CX->hang_cap ? CX->hang_cap - L.ninst : 0;
+                        const int r = uni32(sio->lp_n) ? loop_outcome(CX, w, m, slot, (const lds_u64 *)R,
+                                                                      (const lds_io *)sio, left, kf, fva) : 1;
+                        if (r == 1) {   // a proved hang: the record of one that ran to the cap
+                            proved_skip = left;
+                            L.ninst += left;
+                            finish(L, FI_HANG, 1, 0, 0u);
+                            atomicAdd(&CX->stats[56], 1ull);
+                        } else if (r == 2) {   // a proved page fault kf instructions on
+                            proved_skip = kf;
+                            L.ninst += kf;
+                            finish(L, FI_CRASH, FI_CRASH_PAGE_FAULT, 134, (uint32_t)fva);
+                            atomicAdd(&CX->stats[57], 1ull);
+                        } else {   // undecided: the trial runs on, without asking again
+                            no_proof = true;
+                            atomicAdd(&CX->stats[58], 1ull);
+                        }
                         continue;
                     }
                     if (m.code_dirty && st < 8) {

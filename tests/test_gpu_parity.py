@@ -355,7 +355,7 @@ def test_execution_paths_bit_exact(engine_factory, oracle_mod, name, path):
 
 
 def test_counted_loop_hang_proofs(engine_factory, oracle_mod):
-    """crc32's t6 flips loop in the table's inner bit loop (a counted loop:
+    """(And the run-off loop proofs: see below.)  crc32's t6 flips loop in the table's inner bit loop (a counted loop:
     addi t6, t6, -1; bnez t6) until the hang cap.  The clean translated body
     proves those hangs when it enters the loop (fi_translate.cpp): the records
     equal a run without the proofs (FI_CFG_NO_HANG_PROOF: every hang runs to
@@ -368,16 +368,52 @@ def test_counted_loop_hang_proofs(engine_factory, oracle_mod):
         e.set_campaign(0x5EED0002, REGS | PC, 1)
         e.set_protect(0)
     a, ha = on.run_trials(0, n)
-    proved = int(on.debug_stats()[56])
+    proved, crashed = int(on.debug_stats()[56]), int(on.debug_stats()[57])
     b, hb = off.run_trials(0, n)
-    assert int(off.debug_stats()[56]) == 0
+    assert int(off.debug_stats()[56]) == 0 and int(off.debug_stats()[57]) == 0
     assert np.array_equal(a, b)
     hang = np.nonzero(a["cls"] == 3)[0]
     assert len(hang) > 20 and proved > 0 and proved <= len(hang)
     assert (a["detail"][hang] == 0).all()
+    # the crc loop's end-pointer (a1) flips run off the buffer: page-fault
+    # crashes proved at the loop's entry (run-off loop proofs)
+    crash = np.nonzero((a["cls"] == 2) & (a["sub"] == 3))[0]
+    assert crashed > 20 and crashed <= len(crash)
     assert int(ha["device_insts"]) < int(hb["device_insts"])
-    sites = on.sample(0, n)[hang]
-    compare(a[hang], oracle_for(oracle_mod, "crc32").run_trials(sites), sites)
+    sel = np.concatenate([hang, crash])
+    sites = on.sample(0, n)[sel]
+    compare(a[sel], oracle_for(oracle_mod, "crc32").run_trials(sites), sites)
+
+
+def test_runoff_loop_proofs(oracle_mod):
+    """Run-off loops (fi_translate.cpp, fi_trial.hip loop_outcome): faults on
+    the scan pointer / end of the runoff program's three scan loops.  Trials
+    that walk off a .bss buffer or below the text end as page-fault crashes
+    proved at the loop's entry (stats[57]); those that walk into heap pages
+    the fault handler would map stay undecided (stats[58]) and run on.  Every
+    record equals the oracle's, with the proofs on and off."""
+    from shrewd_amd import Engine
+    from shrewd_amd.fi import CFG_NO_HANG_PROOF
+    import test_isa_vectors as kat
+    elf = kat.runoff_program_elf()
+    o = oracle_mod.Oracle(elf, "runoff")
+    g = o.run_golden()
+    sites = kat.runoff_sites(g.ninst, 3000)
+    ref = o.run_trials(sites, protect_mask=0)
+    got = []
+    for flags in (0, CFG_NO_HANG_PROOF):
+        e = Engine(flags=flags)
+        e.load_elf(elf, ["runoff"])
+        e.golden_run()
+        dev, h = e.run_sites(sites)
+        assert e.translate_status() == ""
+        compare(dev, ref, sites)
+        st = e.debug_stats()
+        got.append((int(st[57]), int(st[58]), int(h["device_insts"])))
+        e.close()
+    (crash_on, und_on, ins_on), (crash_off, und_off, ins_off) = got
+    assert crash_on > 10 and und_on > 0 and crash_off == 0 and und_off == 0
+    assert ins_on < ins_off
 
 
 def test_run_trials_equals_run_sites(engine_factory):

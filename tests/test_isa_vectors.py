@@ -1826,3 +1826,159 @@ def test_sys2_program_on_oracle(oracle_mod):
     assert len(got) == len(exp), (len(got), len(exp))
     for k in range(0, len(exp), 8):
         assert got[k:k + 8] == exp[k:k + 8], (k, got[k:k + 8].hex(), exp[k:k + 8].hex())
+
+
+# ------------------------------------------------------------ runoff program
+# Scan loops whose faulted trials run off their buffers (the run-off loop
+# proofs of the clean translated body, fi_translate.cpp / fi_trial.hip
+# loop_outcome): a forward byte scan of a .bss buffer (past its end: the page
+# after .bss is outside every VMA -- a page-fault crash), a backward word scan
+# with a table lookup per word (down through .data and the text, then below
+# it), and a byte scan of the first brk page (past it: heap pages the fault
+# handler maps, MemState::fixupFault -- the proof stays undecided there).
+RUNOFF_BUF = 4096
+
+
+def runoff_program_source() -> str:
+    return f"""    .text
+_start:
+    la    s0, buf
+    la    s4, table
+    li    s6, 0
+    li    t0, 0
+    li    t1, {RUNOFF_BUF}
+fill:
+    add   t2, s0, t0
+    andi  t3, t0, 255
+    sb    t3, 0(t2)
+    addi  t0, t0, 1
+    bne   t0, t1, fill
+    li    t0, 0
+    li    t1, 64
+tfill:
+    slli  t2, t0, 3
+    add   t2, t2, s4
+    mul   t3, t0, t0
+    sd    t3, 0(t2)
+    addi  t0, t0, 1
+    bne   t0, t1, tfill
+    li    s5, 4
+passA:
+    mv    a0, s0
+    li    t0, {RUNOFF_BUF}
+    add   a1, s0, t0
+    li    t4, 0
+scanA:
+    lbu   t1, 0(a0)
+    add   t4, t4, t1
+    addi  a0, a0, 1
+    bne   a0, a1, scanA
+    add   s6, s6, t4
+    addi  s5, s5, -1
+    bnez  s5, passA
+    li    s5, 2
+passB:
+    li    t0, {RUNOFF_BUF - 4}
+    add   a0, s0, t0
+    addi  a1, s0, -4
+    li    t4, 0
+scanB:
+    lw    t1, 0(a0)
+    andi  t2, t1, 63
+    slli  t2, t2, 3
+    add   t2, t2, s4
+    ld    t3, 0(t2)
+    xor   t4, t4, t3
+    addi  a0, a0, -4
+    bne   a0, a1, scanB
+    add   s6, s6, t4
+    addi  s5, s5, -1
+    bnez  s5, passB
+    li    a0, 0
+    li    a7, 214
+    ecall
+    mv    s7, a0
+    li    t0, 0x10000
+    add   a0, s7, t0
+    li    a7, 214
+    ecall
+    li    t0, 0
+    li    t1, 64
+hfill:
+    add   t2, s7, t0
+    sb    t0, 0(t2)
+    addi  t0, t0, 1
+    bne   t0, t1, hfill
+    li    s5, 8
+passC:
+    mv    a0, s7
+    addi  a1, s7, 64
+    li    t4, 0
+scanC:
+    lbu   t1, 0(a0)
+    add   t4, t4, t1
+    addi  a0, a0, 1
+    bne   a0, a1, scanC
+    add   s6, s6, t4
+    addi  s5, s5, -1
+    bnez  s5, passC
+    la    a1, out
+    sd    s6, 0(a1)
+    li    a0, 1
+    li    a2, 8
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 93
+    ecall
+    .bss
+    .balign 8
+out:
+    .zero 8
+table:
+    .zero 512
+buf:
+    .zero {RUNOFF_BUF}
+"""
+
+
+def runoff_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(runoff_program_source(), compress=False)
+
+
+def runoff_program_expected() -> bytes:
+    M = (1 << 64) - 1
+    buf = [i & 255 for i in range(RUNOFF_BUF)]
+    table = [(i * i) & M for i in range(64)]
+    s6 = 4 * sum(buf)
+    words = [int.from_bytes(bytes(buf[k:k + 4]), "little") for k in range(0, RUNOFF_BUF, 4)]
+    t4 = 0
+    for w in reversed(words):
+        w = w - (1 << 32) if w >> 31 else w   # lw sign-extends (andi 63 sees the low bits only)
+        t4 ^= table[w & 63]
+    s6 += 2 * t4
+    s6 += 8 * sum(range(64))
+    return (s6 & M).to_bytes(8, "little")
+
+
+def runoff_sites(ninst, n=3000, seed=11):
+    """Single-bit faults on the scan pointer (a0) and the scan end (a1)."""
+    import numpy as np
+    from oracle.pyoracle import SITE_DT
+    r = np.random.default_rng(seed)
+    s = np.zeros(n, SITE_DT)
+    s["inst"] = r.integers(1, ninst, n)
+    s["mask"] = np.uint64(1) << r.integers(0, 64, n).astype(np.uint64)
+    s["target"] = r.choice([10, 11], n)
+    s["trial"] = np.arange(n)
+    return s
+
+
+def test_runoff_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(runoff_program_elf(), "runoff")
+    g = o.run_golden()
+    assert g.exit_code == 0, g
+    assert o.golden_stdout() == runoff_program_expected()
+    res = o.run_trials(runoff_sites(g.ninst, 400), protect_mask=0)
+    assert (res["cls"] == 2).sum() > 20 and (res["sub"][res["cls"] == 2] == 3).any()

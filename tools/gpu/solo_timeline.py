@@ -52,6 +52,13 @@ print(json.dumps({"ninst_at_solo_start_quantiles": {q: int(np.quantile(n0[ok], q
                   if late.any() else {},
                   "start_rank_corr": round(float(np.corrcoef(np.argsort(np.argsort(start[ok])),
                                                              np.argsort(np.argsort(n0[ok])))[0, 1]), 3)}), flush=True)
+# where the solo work goes: instructions by outcome class and injected register
+grp = {}
+for c, t, k in zip(out["cls"][tids[busy]], sites["target"][tids[busy]], ins[busy]):
+    g = grp.setdefault(f"{int(c)}/{int(t)}", [0, 0])
+    g[0] += 1
+    g[1] += int(k)
+print(json.dumps({"insts_by_cls_target": dict(sorted(grp.items(), key=lambda kv: -kv[1][1])[:24])}), flush=True)
 order = np.argsort(-end)[:top]
 for i in order:
     tid = int(w[i, 6])
