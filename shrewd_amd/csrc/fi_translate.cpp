@@ -574,6 +574,15 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         }
         blocks.push_back(b);
     }
+    // clean-body variants (SHREWD_FI_TXV bits, default all: A/B in
+    // profiles/r04ao, r04ap): 1 = a load site caches only a mapped page (the
+    // probe's checks move to the miss), 2 = the budget counts down (one
+    // compare per check point, no add), 4 = a store site caches only a
+    // private page outside the code range
+    const char *txv_env = getenv("SHREWD_FI_TXV");
+    const unsigned txv = txv_env ? (unsigned)strtoul(txv_env, nullptr, 0) : 15u;
+    // 8 = the site caches' miss and leave tests and the budget tests hinted cold
+    const char *cold = (txv & 8u) ? "SCOLD" : "SCOND";
     bool cur_odd = false;   // generating an odd-pc block: every edge goes through the dispatch
     bool oddon = false;     // generating the solo-odd body (even and odd blocks, labels Q*)
     std::string SB = "S_", SD = "S_dispatch", SOB = "SO_";
@@ -969,7 +978,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 rs_ += "case " + std::to_string(x) + ": " + sclr + "goto " + SB + std::to_string(next) + "; ";
                 // clean body: a routed block that is no check point tests the budget here
                 const std::string chk = (!oddon && next == x && !is_cp(x))
-                    ? sfmt("if (st + %uu > bud) { spc = %s; bst = 1u; goto S_out; } ", run_len[x], hex(g.pc_of(x)).c_str())
+                    ? sfmt("if (SOVER(%uu)) { spc = %s; bst = 1u; goto S_out; } ", run_len[x], hex(g.pc_of(x)).c_str())
                     : std::string();
                 rc_ += "case " + std::to_string(x) + ": " + sclr + chk + "goto " + SB + std::to_string(next) + "; ";
             }
@@ -998,7 +1007,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         if (rw) so_.put(" | ((lwm & 0x%xu) != 0)", rw);
         so_.put(" | SDIRTY(%uu, %uu)) { spc = %s; goto S_out; }\n", (uint32_t)(blo - text_lo),
                 (uint32_t)(bhi - text_lo), P0.c_str());
-        if (!oddon && is_cp(h0)) sc.put("  if (st + %uu > bud) { spc = %s; bst = 1u; goto S_out; }\n", run_len[h0], P0.c_str());
+        if (!oddon && is_cp(h0)) sc.put("  if (SOVER(%uu)) { spc = %s; bst = 1u; goto S_out; }\n", run_len[h0], P0.c_str());
         uint32_t k_st = 0, k_xt = 0, k_fb = 0, k_db = 0;   // committed so far in this block
         auto commit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
             // per-lane counters of the running lanes (zero terms omitted), wave iterations
@@ -1011,7 +1020,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         };
         auto scommit = [&](uint32_t st, uint32_t xt, uint32_t fb, uint32_t db) {
             if (!st) return std::string();
-            std::string r = "st += " + std::to_string(st) + "u; ";
+            std::string r = "SADD(" + std::to_string(st) + "u); ";
             if (xt) r += "xt += " + std::to_string(xt) + "u; ";
             if (fb) r += "fb += " + std::to_string(fb) + "u; ";
             if (db) r += "db += " + std::to_string(db) + "u; ";
@@ -1055,10 +1064,20 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                     if (!oddon) {
                         if (S.chain.count(h0) && n_sites < kSiteCaches) {
                             const uint32_t i = n_sites++;
-                            sc.put("  { uint8_t *p_; bool pv_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
-                                   "    if (SCOND(vp_ != CV%u)) { CV%u = vp_; CP%u = tlb_find(m, vp_); }\n"
-                                   "    if (SCOND(!tx_probe_e(CP%u, ea_, %uu, p_, pv_))) %s\n",
-                                   A.c_str(), immb, i, i, i, i, sz, sleave_here.c_str());
+                            if (txv & 1u) {
+                                sc.put("  { uint8_t *p_; bool pv_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
+                                       "    if (%s(vp_ != CV%u)) { const uint64_t e_ = tlb_find(m, vp_); if (SCOND(!e_)) %s "
+                                       "CV%u = vp_; CP%u = e_; }\n", A.c_str(), immb, cold, i, sleave_here.c_str(), i, i);
+                                if (sz > 1)
+                                    sc.put("    if (%s(((uint32_t)ea_ & 4095u) > %uu)) %s\n", cold, 4096u - sz, sleave_here.c_str());
+                                sc.put("    p_ = (uint8_t *)(uintptr_t)((CP%u & ~1ULL) + (ea_ & 4095u)); pv_ = (CP%u & 1u) != 0;\n",
+                                       i, i);
+                            } else {
+                                sc.put("  { uint8_t *p_; bool pv_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
+                                       "    if (%s(vp_ != CV%u)) { CV%u = vp_; CP%u = tlb_find(m, vp_); }\n"
+                                       "    if (%s(!tx_probe_e(CP%u, ea_, %uu, p_, pv_))) %s\n",
+                                       A.c_str(), immb, cold, i, i, i, cold, i, sz, sleave_here.c_str());
+                            }
                         } else {
                             sc.out += pl;
                         }
@@ -1099,11 +1118,24 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 if (!oddon) {
                     if (S.chain.count(h0) && n_sites < kSiteCaches) {
                         const uint32_t i = n_sites++;
-                        sc.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
-                               "    if (SCOND(vp_ != CV%u)) { CV%u = vp_; CP%u = tlb_find(m, vp_); }\n"
-                               "    if (SCOND(!tx_probe_st_e(CP%u, ea_, %uu, p_, tx))) %s\n"
-                               "    *(g_%s *)p_ = (%s)%s; }\n", A.c_str(), immb, i, i, i, i, sz, sleave_here.c_str(),
-                               gtype(sz), ltype(sz), B.c_str());
+                        if (txv & 4u) {   // (a page meeting the code range is never cached: every store probes it)
+                            sc.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
+                                   "    if (SCOND(vp_ == CV%u)) {\n", A.c_str(), immb, i);
+                            if (sz > 1)
+                                sc.put("      if (SCOND(((uint32_t)ea_ & 4095u) > %uu)) %s\n", 4096u - sz, sleave_here.c_str());
+                            sc.put("      p_ = (uint8_t *)(uintptr_t)((CP%u & ~1ULL) + (ea_ & 4095u));\n"
+                                   "    } else {\n      const uint64_t e_ = tlb_find(m, vp_);\n"
+                                   "      if (SCOND(!tx_probe_st_e(e_, ea_, %uu, p_, tx))) %s\n"
+                                   "      if (SCOND((vp_ << 12) >= tx.chi || ((vp_ + 1) << 12) <= tx.clo)) { CV%u = vp_; CP%u = e_; }\n"
+                                   "    }\n    *(g_%s *)p_ = (%s)%s; }\n", i, sz, sleave_here.c_str(), i, i, gtype(sz), ltype(sz),
+                                   B.c_str());
+                        } else {
+                            sc.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
+                                   "    if (%s(vp_ != CV%u)) { CV%u = vp_; CP%u = tlb_find(m, vp_); }\n"
+                                   "    if (%s(!tx_probe_st_e(CP%u, ea_, %uu, p_, tx))) %s\n"
+                                   "    *(g_%s *)p_ = (%s)%s; }\n", A.c_str(), immb, cold, i, i, i, cold, i, sz,
+                                   sleave_here.c_str(), gtype(sz), ltype(sz), B.c_str());
+                        }
                     } else {
                         sc.put("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, true, p_, tx))) %s\n"
                                "    *(g_%s *)p_ = (%s)%s; }\n", A.c_str(), immb, sz, sleave_here.c_str(), gtype(sz),
@@ -1185,6 +1217,14 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     // the clean body's entry: its site caches start empty (declared without an
     // initializer: the dispatch label below them is also a jump target)
     std::string sc_head;
+    if (txv & 2u)   // the budget counts down (solo_tx_clean_run: SADD / SOVER / SDONE)
+        sc_head += "#undef SADD\n#undef SOVER\n#undef SDONE\n#define SADD(n_) (brem -= (n_))\n"
+                   "#define SOVER(n_) (brem < (n_))\n#define SDONE() (bud - brem)\n";
+    if (txv & 8u) {
+        sc_head += "#define SCOLD(x) __builtin_expect(!!(x), 0)\n";
+        if (txv & 2u) sc_head += "#undef SOVER\n#define SOVER(n_) __builtin_expect(brem < (n_), 0)\n";
+        else sc_head += "#undef SOVER\n#define SOVER(n_) __builtin_expect(st + (n_) > bud, 0)\n";
+    }
     for (uint32_t i = 0; i < kSiteCaches; i++) sc_head += sfmt("  uint64_t CV%u, CP%u;\n", i, i);
     sc_head += "S_entry:\n";
     for (uint32_t i = 0; i < kSiteCaches; i++) sc_head += sfmt("  CV%u = ~0ULL; CP%u = 0;\n", i, i);

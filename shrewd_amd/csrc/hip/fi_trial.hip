@@ -1564,6 +1564,7 @@ __device__ __noinline__ void solo_tx_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds_
     bool schg = false;
     uint32_t cslo = 0xFFFFFFFFu, cshi = 0u;
     uint32_t st = 0, xt = 0, fb = 0, db = 0;
+#define SADD(n_) (st += (n_))
 // a translated store rewrote code bytes [ea_, ea_ + sz_): later blocks see the
 // grown range; the decode cache forgets them when the blocks are left
 #define TXCODE(ea_, sz_)                                                                        \
@@ -1605,6 +1606,7 @@ S_out:
 #undef TXW
 #undef TXCODE
 #undef SDIRTY
+#undef SADD
     if (schg) {   // mark_dirty_solo changed the bounding range (its LDS map bits are written already)
         mp->code_dirty = true; mp->dlo = m.dlo; mp->dhi = m.dhi;
     }
@@ -1731,7 +1733,13 @@ __device__ __noinline__ void solo_tx_clean_run(KCtx *CX, lds_u64 *R, lds_mem *mp
     // its counter this far from zero, the trial reaches the hang cap inside it
     const uint32_t hleft = io->hleft, hok = io->hok;
     uint32_t hang = 0, bst = 0;
-#define TXHANG(x_, c_, m_) (hok && tx_hang_proof((x_), (c_), (m_), hleft - st))
+    // instructions: counted up (st) or, in the count-down variant the body
+    // selects (fi_translate.cpp, SHREWD_FI_TXV), the budget left (brem)
+    uint32_t brem = bud;
+#define SADD(n_) (st += (n_))
+#define SOVER(n_) (st + (n_) > bud)
+#define SDONE() (st)
+#define TXHANG(x_, c_, m_) (hok && tx_hang_proof((x_), (c_), (m_), hleft - SDONE()))
 #define TXLOOP(c_, m_, n_) (io->lp_cnt = (c_), io->lp_m = (m_), io->lp_n = (n_))
 #define TXLD(j_, d_, o_, s_) (io->lp_ld[j_][0] = (d_), io->lp_ld[j_][1] = (uint32_t)(o_), io->lp_ld[j_][2] = (s_))
 #define TXR(r) uint64_t X##r = R[r];
@@ -1750,7 +1758,13 @@ S_out:
 #undef TXHANG
 #undef TXLOOP
 #undef TXLD
-    io->spc = spc; io->st = st; io->xt = xt; io->fb = fb; io->db = db;
+    io->spc = spc; io->st = SDONE(); io->xt = xt; io->fb = fb; io->db = db;
+#undef SADD
+#undef SOVER
+#undef SDONE
+#ifdef SCOLD
+#undef SCOLD
+#endif
     io->cslo = 0xFFFFFFFFu; io->cshi = 0u; io->schg = 0u; io->hang = hang; io->bst = bst;
 }
 #endif
