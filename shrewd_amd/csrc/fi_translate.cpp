@@ -1085,7 +1085,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 }
                 if (p.rd) {
                     g.put("    p_ = ok_ ? p_ : const_cast<uint8_t *>(zp);\n");
-                    sboth(sfmt("    uint64_t v_; if (SCOND(pv_)) v_ = *(const g_%s *)p_; else v_ = tx_sload(p_, %uu);\n",
+                    sboth(sfmt("    uint64_t v_; if (SPRIV(pv_)) v_ = *(const g_%s *)p_; else v_ = tx_sload(p_, %uu);\n",
                                gtype(sz), sz));
                     if (sx) {
                         g.put("    TXSET(%u, (int64_t)(int%d_t)*(const g_%s *)p_); }\n", p.rd, sx, gtype(sz));
@@ -1220,6 +1220,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     if (txv & 2u)   // the budget counts down (solo_tx_clean_run: SADD / SOVER / SDONE)
         sc_head += "#undef SADD\n#undef SOVER\n#undef SDONE\n#define SADD(n_) (brem -= (n_))\n"
                    "#define SOVER(n_) (brem < (n_))\n#define SDONE() (bud - brem)\n";
+    if (txv & 16u)   // loads from the trial's own pages hinted cold (shared snapshot frames straight-line)
+        sc_head += "#undef SPRIV\n#define SPRIV(x) __builtin_expect(!!(x), 0)\n";
     if (txv & 8u) {
         sc_head += "#define SCOLD(x) __builtin_expect(!!(x), 0)\n";
         if (txv & 2u) sc_head += "#undef SOVER\n#define SOVER(n_) __builtin_expect(brem < (n_), 0)\n";

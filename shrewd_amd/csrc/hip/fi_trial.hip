@@ -1398,6 +1398,7 @@ typedef __attribute__((address_space(1), aligned(1))) uint64_t g_u64;
 // uniform again -- traded SGPR spills for VALU work and lost: crc32 3.2-3.7M
 // against 7.06M trials/s, profiles/r02j_solo_ab.txt.)
 #define SCOND(x) (x)
+#define SPRIV(x) (x)   // a translated load from the trial's own page (the clean body may hint it)
 #define SUNI(x) (x)
 #define SUNI32(x) (x)
 #define SX(r, e) X##r = (uint64_t)(e)
@@ -1765,6 +1766,8 @@ S_out:
 #ifdef SCOLD
 #undef SCOLD
 #endif
+#undef SPRIV
+#define SPRIV(x) (x)
     io->cslo = 0xFFFFFFFFu; io->cshi = 0u; io->schg = 0u; io->hang = hang; io->bst = bst;
 }
 #endif
