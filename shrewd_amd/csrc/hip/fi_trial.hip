@@ -3026,6 +3026,15 @@ leave:
 #ifndef FI_WAVES_PER_EU
 #define FI_WAVES_PER_EU 1
 #endif
+// A trial that rewrote code and leaves the translated blocks after fewer than
+// FI_TX_SHORT instructions four times running stays in the interpreter for
+// the next FI_TX_SKIP (a round trip costs more than the blocks save)
+#ifndef FI_TX_SHORT
+#define FI_TX_SHORT 8
+#endif
+#ifndef FI_TX_SKIP
+#define FI_TX_SKIP 4096
+#endif
 // Solo kernel: the launch context through a plain pointer, so that the
 // compiler can keep loop-invariant fields in registers (a one-lane wave has
 // VGPR lanes to spill them to) instead of a scalar load + wait at each use
@@ -3656,8 +3665,8 @@ __device__ __forceinline__ void trial_body() {
                         }
                         continue;
                     }
-                    if (m.code_dirty && st < 8) {
-                        if (++tx_short >= 4) { tx_short = 0; tx_skip_until = n_iter + 4096; }
+                    if (m.code_dirty && st < FI_TX_SHORT) {
+                        if (++tx_short >= 4) { tx_short = 0; tx_skip_until = n_iter + FI_TX_SKIP; }
                     } else {
                         tx_short = 0;
                     }

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Clean translated body variants (SHREWD_FI_TXV bits, fi_translate.cpp): the
-# crc32 bench line per variant, in the order given (repeat one to see the
-# noise).  bash tools/gpu/txv_bench.sh TAG "TXV TXV ..." [WORKLOADS]
+# Build variants chosen by environment: the crc32 bench line (and WORKLOADS)
+# per variant, in the order given (repeat one to see the noise).  A variant
+# is a SHREWD_FI_TXV value (clean-body bits, fi_translate.cpp) or VAR=VAL[,VAR=VAL]
+# (e.g. SHREWD_FI_TX_WPE=2, fi_jit.cpp).  bash tools/gpu/txv_bench.sh TAG "V V ..." [WORKLOADS]
 set -o pipefail
 mkdir -p gpurun_out
 TAG=$1; W=${3:-}
@@ -11,7 +12,8 @@ export SHREWD_FI_JIT_CACHE=$PWD/gpurun_out/jitcache
 k=0
 for txv in $2; do
     k=$((k + 1))
-    export SHREWD_FI_TXV=$txv
+    unset SHREWD_FI_TXV SHREWD_FI_TX_WPE
+    if [[ $txv == *=* ]]; then for a in ${txv//,/ }; do export "$a"; done; else export SHREWD_FI_TXV=$txv; fi
     timeout -k 10 300 python -u bench.py --no-cpu-baseline --workloads "$W" --extra-parity 0 \
         > gpurun_out/txv_${TAG}_$k.json 2> gpurun_out/txv_${TAG}.err || exit $?
     python - >> $O <<PY
