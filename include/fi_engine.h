@@ -173,9 +173,11 @@ typedef struct {
  * and $SHREWD_FI_JIT_CACHE) hold them: cold-start measurements and tests of
  * the background build. */
 #define FI_CFG_JIT_NO_CACHE 8192u
-/* No counted-loop hang proofs in the clean translated body (fi_translate.cpp):
- * every hang trial runs to the cap (A/B and parity checks; outcomes are
- * identical -- a hang's record is the same either way). */
+/* No loop proofs in the clean translated body (fi_translate.cpp): neither
+ * counted-loop hangs nor run-off loops that end in a page fault or a hang
+ * (fi_trial.hip loop_outcome) -- every such trial runs to its cap or its
+ * faulting load (A/B and parity checks; outcomes are identical: the records
+ * are the same either way). */
 #define FI_CFG_NO_HANG_PROOF 16384u
 
 typedef struct {

@@ -1,0 +1,64 @@
+"""The load-time translator's loop proofs on the CPU (fi_translate.cpp; no GPU:
+fi_debug_translate runs on the host).  Inputs: crc32's pre-decoded text and
+golden block trace, as the engine dumps them (tools/gpu/dump_golden.py ->
+tests/golden/tx_inputs_crc32.npz, the engine's own output, not reference
+data).  The device side of the same proofs is tested against the oracle in
+tests/test_gpu_parity.py (test_counted_loop_hang_proofs,
+test_runoff_loop_proofs)."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+from conftest import ROOT
+
+
+def _translate(env=None):
+    from shrewd_amd.fi import lib
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        L = lib()
+        L.fi_debug_translate.restype = C.c_int
+        z = np.load(os.path.join(ROOT, "tests", "golden", "tx_inputs_crc32.npz"))
+        pre, tr = np.ascontiguousarray(z["pre"]), np.ascontiguousarray(z["trace"])
+        n = C.c_uint64()
+        L.fi_debug_translate(pre.ctypes.data, len(pre), int(z["text_lo"]), tr.ctypes.data, len(tr), None, 0, C.byref(n))
+        buf = C.create_string_buffer(n.value + 1)
+        L.fi_debug_translate(pre.ctypes.data, len(pre), int(z["text_lo"]), tr.ctypes.data, len(tr), buf, n.value + 1,
+                             C.byref(n))
+        return buf.value.decode()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_crc32_loop_proofs():
+    body = _translate()
+    # the table's inner bit loop (addi t6, t6, -1; bnez t6): a counted loop of
+    # three blocks, no memory access -- a hang proof without loads, at every
+    # block of the cycle
+    hang = re.findall(r"TXHANG\(X31, -1, 5u\).*?TXLOOP\((\d+)u, 5u, 0u\)", body)
+    assert len(hang) == 3 and all(int(c) & 0xFF == 31 for c in hang)
+    # the crc loop (lbu t1, 0(a0) ... addi a0, a0, 1; bne a0, a1): a run-off
+    # block against a1, a counter load at a0 and a table load at s2 + [0, 1020]
+    m = re.search(r"TXHANG\(X10 - X11, 1, 10u\).*?TXLOOP\((\d+)u, 10u, 2u\); TXLD\(0, (\d+)u, (-?\d+), (\d+)u\); "
+                  r"TXLD\(1, (\d+)u, (-?\d+), (\d+)u\);", body)
+    assert m, "crc loop has no run-off proof"
+    cnt, d0, o0, s0, d1, o1, s1 = (int(x) for x in m.groups())
+    assert cnt == 10 | 11 << 8 | 1 << 16
+    assert (d0 & 0xFF, (d0 >> 8) & 15, (d0 >> 12) & 15, d0 >> 16, o0, s0) == (10, 0, 1, 0, 0, 0)   # lbu at a0
+    assert (d1 & 0xFF, (d1 >> 8) & 15, (d1 >> 12) & 15, d1 >> 16, o1, s1) == (18, 1, 4, 5, 0, 1020)   # lwu at s2+
+
+
+def test_clean_body_variants_translate():
+    """Every SHREWD_FI_TXV variant of the clean body still carries the same proofs."""
+    base = _translate()
+    for v in ("0", "8", "31"):
+        body = _translate({"SHREWD_FI_TXV": v})
+        assert body.count("TXLOOP(") == base.count("TXLOOP(")
+        assert ("SCOLD(" in body) == (int(v) & 8 != 0)
