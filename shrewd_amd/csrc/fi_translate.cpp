@@ -574,15 +574,6 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         }
         blocks.push_back(b);
     }
-    // clean-body variants (SHREWD_FI_TXV bits, default all: A/B in
-    // profiles/r04ao, r04ap): 1 = a load site caches only a mapped page (the
-    // probe's checks move to the miss), 2 = the budget counts down (one
-    // compare per check point, no add), 4 = a store site caches only a
-    // private page outside the code range
-    const char *txv_env = getenv("SHREWD_FI_TXV");
-    const unsigned txv = txv_env ? (unsigned)strtoul(txv_env, nullptr, 0) : 15u;
-    // 8 = the site caches' miss and leave tests and the budget tests hinted cold
-    const char *cold = (txv & 8u) ? "SCOLD" : "SCOND";
     bool cur_odd = false;   // generating an odd-pc block: every edge goes through the dispatch
     bool oddon = false;     // generating the solo-odd body (even and odd blocks, labels Q*)
     std::string SB = "S_", SD = "S_dispatch", SOB = "SO_";
@@ -617,6 +608,21 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         if (k == E_DIRECT) return "goto B_" + std::to_string(t) + ";";
         return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto tx_dispatch; }" : "; goto tx_out; }");
     };
+    // clean-body variants (SHREWD_FI_TXV bits, default all: A/B in
+    // profiles/r04ao, r04ap): 1 = a load site caches only a mapped page (the
+    // probe's checks move to the miss), 2 = the budget counts down (one
+    // compare per check point, no add), 4 = a store site caches only a
+    // private page outside the code range
+    const char *txv_env = getenv("SHREWD_FI_TXV");
+    const unsigned txv = txv_env ? (unsigned)strtoul(txv_env, nullptr, 0) : 15u;
+    // 8 = the site caches' miss and leave tests and the budget tests hinted cold
+    const char *cold = (txv & 8u) ? "SCOLD" : "SCOND";
+    // 16 = loads from the trial's own pages hinted cold; 32 = loop proofs also
+    // tested on direct entries into a proved loop (SR_ labels)
+    // blocks of a proved loop (below) -> the loop's header: a direct entry
+    // from outside the loop goes through SR_<block>, which tests the proof as
+    // the dispatch does (the clean body; a plain forward in the full one)
+    std::map<uint32_t, uint32_t> proof_cycle;
     auto sgo = [&](uint32_t from, uint64_t pc) {
         // solo-odd body: an odd target with a block is a direct edge (the
         // odd blocks are entered at their first pc only); an even one goes
@@ -628,6 +634,11 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         const Edge k = edge(from, pc);
         uint32_t t = 0;
         hof(pc, t);
+        if (k == E_DIRECT && !oddon && !cur_odd && (txv & 32u)) {
+            const auto it = proof_cycle.find(t), fi = proof_cycle.find(from);
+            if (it != proof_cycle.end() && (fi == proof_cycle.end() || fi->second != it->second))
+                return "goto SR_" + std::to_string(t) + ";";
+        }
         if (k == E_DIRECT) return "goto " + SB + std::to_string(t) + ";";
         return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto " + SD + "; }" : "; goto S_out; }");
     };
@@ -809,7 +820,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             }
         }
         if (!m) continue;
-        for (uint32_t h : cyc) hang_proof[h] = {reg, treg, step, m, loads};
+        for (uint32_t h : cyc) { hang_proof[h] = {reg, treg, step, m, loads}; proof_cycle[h] = H; }
     }
 
     // ---- clean body budget tests.  Only a check point tests the budget: a
@@ -879,6 +890,22 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         else g.put("  case %u: etgt = %uu; goto B_%u;\n", h, h, it->second[0]);
     }
     g.put("  default: goto tx_out;\n  }\n}\n");
+    // the clean body's loop-proof test on entering block h ("" if none)
+    auto proof_test = [&](uint32_t h) {
+        auto hp = hang_proof.find(h);
+        if (hp == hang_proof.end()) return std::string();
+        const HangProof &P = hp->second;
+        const std::string x = P.treg ? sfmt("X%u - X%u", P.reg, P.treg) : sfmt("X%u", P.reg);
+        std::string r = sfmt("if (TXHANG(%s, %d, %uu)) { spc = %s; hang = 1u; TXLOOP(%uu, %uu, %uu); ", x.c_str(), P.step,
+                             P.m, hex(g.pc_of(h)).c_str(), P.reg | P.treg << 8 | (uint32_t)(uint8_t)(int8_t)P.step << 16,
+                             P.m, (uint32_t)P.loads.size());
+        for (size_t j = 0; j < P.loads.size(); j++) {
+            const ProofLoad &l = P.loads[j];
+            r += sfmt("TXLD(%u, %uu, %d, %uu); ", (uint32_t)j, l.reg | l.kind << 8 | l.size << 12 | l.pos << 16,
+                      (int)l.off, (uint32_t)l.span);
+        }
+        return r + "goto S_out; } ";
+    };
     // solo dispatch (plain or with the odd-pc entries)
     auto sdispatch = [&](Gen &sx, bool clean) {
         sx.put("%s: {\n  const uint64_t off_ = spc - 0x%llxULL;\n", SD.c_str(), (unsigned long long)text_lo);
@@ -894,21 +921,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         }
         for (uint32_t h : leaders) {
             auto it = S.chain.find(h);
-            auto hp = hang_proof.find(h);
             sx.put("  case %u: ", h);
-            if (clean && hp != hang_proof.end()) {
-                const HangProof &P = hp->second;
-                const std::string x = P.treg ? sfmt("X%u - X%u", P.reg, P.treg) : sfmt("X%u", P.reg);
-                sx.put("if (TXHANG(%s, %d, %uu)) { spc = %s; hang = 1u; TXLOOP(%uu, %uu, %uu); ", x.c_str(), P.step, P.m,
-                       hex(g.pc_of(h)).c_str(), P.reg | P.treg << 8 | (uint32_t)(uint8_t)(int8_t)P.step << 16, P.m,
-                       (uint32_t)P.loads.size());
-                for (size_t j = 0; j < P.loads.size(); j++) {
-                    const ProofLoad &l = P.loads[j];
-                    sx.put("TXLD(%u, %uu, %d, %uu); ", (uint32_t)j, l.reg | l.kind << 8 | l.size << 12 | l.pos << 16,
-                           (int)l.off, (uint32_t)l.span);
-                }
-                sx.put("goto S_out; } ");
-            }
+            if (clean) sx.out += proof_test(h);
             if (it == S.chain.end() || (it->second.size() == 1 && it->second[0] == h))
                 sx.put("goto %s%u;\n", SB.c_str(), h);
             else
@@ -1208,6 +1222,11 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         sboth("}\n");
         if (cur_odd) g.out.swap(g_keep);
     }
+    if (!oddon && (txv & 32u))   // direct entries into proved loops (sgo)
+        for (const auto &kv : proof_cycle) {
+            so.put("SR_%u: goto S_%u;\n", kv.first, kv.first);
+            sc.put("SR_%u: %sgoto S_%u;\n", kv.first, proof_test(kv.first).c_str(), kv.first);
+        }
     if (oddon) g.out.swap(g_mode);
     }
     cur_odd = false;

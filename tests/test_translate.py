@@ -41,9 +41,13 @@ def test_crc32_loop_proofs():
     body = _translate()
     # the table's inner bit loop (addi t6, t6, -1; bnez t6): a counted loop of
     # three blocks, no memory access -- a hang proof without loads, at every
-    # block of the cycle
+    # block of the cycle (tested on dispatch entries; with SHREWD_FI_TXV bit
+    # 32 also on direct entries from outside the loop, SR_ labels)
     hang = re.findall(r"TXHANG\(X31, -1, 5u\).*?TXLOOP\((\d+)u, 5u, 0u\)", body)
     assert len(hang) == 3 and all(int(c) & 0xFF == 31 for c in hang)
+    sr = _translate({"SHREWD_FI_TXV": "47"})
+    assert len(re.findall(r"TXHANG\(X31, -1, 5u\)", sr)) == 6
+    assert "goto SR_130;" in sr and "goto SR_182;" in sr and "goto SR_" not in body
     # the crc loop (lbu t1, 0(a0) ... addi a0, a0, 1; bne a0, a1): a run-off
     # block against a1, a counter load at a0 and a table load at s2 + [0, 1020]
     m = re.search(r"TXHANG\(X10 - X11, 1, 10u\).*?TXLOOP\((\d+)u, 10u, 2u\); TXLD\(0, (\d+)u, (-?\d+), (\d+)u\); "
