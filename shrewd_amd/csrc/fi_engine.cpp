@@ -54,7 +54,7 @@ hipError_t launch_redo_gather(const fi_site *sites, const uint32_t *idx, uint64_
 hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome *rout, fi_outcome *out,
                                hipStream_t st);
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
-                            uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, bool solo,
+                            uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, uint32_t solo,
                             uint64_t golden_ninst, hipStream_t st);
 hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,
                             hipStream_t st);
@@ -1489,9 +1489,13 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
             c.resume = nullptr;
             c.resume_n = nullptr;
         } else {
+            // survivors not yet injected form a tier right after the first
+            // (fi_surv_keys_kernel; profiles/r04au: intmix -3 %, qsort -3 %
+            // per step; SHREWD_FI_SOLO_ORDER=0 for the two-tier order)
+            static const bool uninj_tier = !(getenv("SHREWD_FI_SOLO_ORDER") && atoi(getenv("SHREWD_FI_SOLO_ORDER")) == 0);
+            const uint32_t skey = (solo && !pack) ? (uninj_tier ? 3u : 1u) : 0u;
             HIPCHK(launch_surv_keys(e->d_save, e->d_surv[(ep - 1) & 1], e->d_cnt + ep - 1, k, c.text_lo, e->d_skeys,
-                                    e->d_svals, odd ? e->d_split + 4 * ep : nullptr, solo && !pack, e->golden.ninst,
-                                    st));
+                                    e->d_svals, odd ? e->d_split + 4 * ep : nullptr, skey, e->golden.ninst, st));
             HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_skeys, e->d_skeys2, e->d_svals, e->d_svals2, k, 64, st));
             c.resume = e->d_svals2;
             c.resume_n = e->d_cnt + ep - 1;

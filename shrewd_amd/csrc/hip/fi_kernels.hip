@@ -247,7 +247,10 @@ __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, 
         // no pc grouping (profiles/r03k_ab_lpt.jsonl: crc32 +4 %, intmix +5 %)
         if (solo) {
             const bool first = ((save[sl].flags >> 3) & 1) || save[sl].ninst > golden_ninst;
-            k = ((uint64_t)(first ? 0 : 1) << 62) | (save[sl].ninst & ((1ULL << 46) - 1));
+            // (solo bit 1: survivors not yet injected -- their outcome still
+            // unknown -- form a tier of their own after the first)
+            const bool uninj = (solo & 2u) && ((save[sl].flags >> 1) & 3) == 0;
+            k = ((uint64_t)(first ? 0 : uninj ? 1 : 2) << 61) | (save[sl].ninst & ((1ULL << 46) - 1));
         }
         if (n_odd) {
             k = ((pc & 1) << 63) | (k >> 1);
@@ -375,10 +378,10 @@ hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome
     return hipGetLastError();
 }
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
-                            uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, bool solo,
+                            uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, uint32_t solo,
                             uint64_t golden_ninst, hipStream_t st) {
     hipLaunchKernelGGL(fi_surv_keys_kernel, dim3(nblk(cap, 256)), dim3(256), 0, st, save, list, cnt, cap, text_lo,
-                       keys, vals, n_odd, solo ? 1u : 0u, golden_ninst);
+                       keys, vals, n_odd, solo, golden_ninst);
     return hipGetLastError();
 }
 hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,
