@@ -271,6 +271,7 @@ typedef struct {
     u64 fetch_bytes, data_bytes;
     /* diagnostics (or_debug_trace): committed pcs, store addresses into the text */
     u64 *dbg_pc, dbg_pc_n, dbg_pc_cap, *dbg_wr, dbg_wr_n, dbg_wr_cap;
+    int dbg_raw;   /* or_debug_trace_raw: pc | instruction word << 32 */
     const or_campaign_t *c;
 } mach_t;
 
@@ -2691,7 +2692,7 @@ static void tick(mach_t *m, u64 cap) {
             }
             if (f == F_NONE) {
                 m->num_inst++;   /* countInst only on NoFault (atomic.cc:687-689) */
-                if (m->dbg_pc && m->dbg_pc_n < m->dbg_pc_cap) m->dbg_pc[m->dbg_pc_n] = m->pc;
+                if (m->dbg_pc && m->dbg_pc_n < m->dbg_pc_cap) m->dbg_pc[m->dbg_pc_n] = m->dbg_raw ? (m->pc & 0xFFFFFFFFULL) | ((u64)d.raw << 32) : m->pc;
                 if (m->dbg_pc) m->dbg_pc_n++;
                 if (m->rarm && result_fault(m, &d)) return;
             }
@@ -3100,16 +3101,26 @@ int or_run_one_capture(or_campaign_t *c, const or_site_t *site, u64 protect, u64
 /* Diagnostics: one trial with its committed pcs (first pcap) and the
  * addresses of its stores into the text range (first wcap); *pn / *wn = the
  * totals.  Tooling only (tools/trial_trace.py). */
-int or_debug_trace(or_campaign_t *c, const or_site_t *site, u64 f16, or_outcome_t *out, u64 *pcs, u64 pcap, u64 *pn,
-                   u64 *wrs, u64 wcap, u64 *wn) {
+static int debug_trace(or_campaign_t *c, const or_site_t *site, u64 f16, or_outcome_t *out, u64 *pcs, u64 pcap, u64 *pn,
+                       u64 *wrs, u64 wcap, u64 *wn, int raw) {
     if (!c->have_golden) { snprintf(c->err, sizeof c->err, "golden run required"); return -1; }
     mach_t m; mach_init(&m, c);
     m.site = site;
+    m.dbg_raw = raw;
     m.dbg_pc = pcs; m.dbg_pc_cap = pcap; m.dbg_wr = wrs; m.dbg_wr_cap = wcap;
     run(&m, hang_cap(c, f16));
     *out = m.res; *pn = m.dbg_pc_n; *wn = m.dbg_wr_n;
     mach_free(&m);
     return 0;
+}
+int or_debug_trace(or_campaign_t *c, const or_site_t *site, u64 f16, or_outcome_t *out, u64 *pcs, u64 pcap, u64 *pn,
+                   u64 *wrs, u64 wcap, u64 *wn) {
+    return debug_trace(c, site, f16, out, pcs, pcap, pn, wrs, wcap, wn, 0);
+}
+/* the same with each committed instruction's word in the high half (the pc's low 32 bits below) */
+int or_debug_trace_raw(or_campaign_t *c, const or_site_t *site, u64 f16, or_outcome_t *out, u64 *pcs, u64 pcap,
+                       u64 *pn, u64 *wrs, u64 wcap, u64 *wn) {
+    return debug_trace(c, site, f16, out, pcs, pcap, pn, wrs, wcap, wn, 1);
 }
 
 /* ------------------------------------------------------------- probe */

@@ -21,6 +21,14 @@
 //                     (PhysicalMemory::serializeStore, src/mem/physical.cc:363-405)
 //   ISA               [<cpu>.isa] miscRegFile (fflags, frm); the PC state's
 //                     _vtype/_vl (riscv/pcstate.hh:146-156); [Globals] curTick
+//   fd table          [<process>.fdarray.EntryN] is deliberately NOT read for
+//                     fds 0-2: FDArray::unserialize skips them
+//                     (src/sim/fd_array.cc:378-381), and restoreFileOffsets
+//                     (:126-282), the only code that would seek fd 0 to the
+//                     checkpointed _fileOffset, has no caller in the reference
+//                     tree.  A restored process's fd 0 is the one its
+//                     FDArray constructor opened from Process.input
+//                     (:50-75), at offset 0 -- what fi_load_checkpoint sets.
 // Host code; the product reads what SE trials need: pages, integer and FP
 // registers, fcsr, pc, brk point, the VMA list, mmap end and curTick.  Parity with a checkpoint written by a real
 // gem5 is unpinned (no gem5 build here); the format is pinned by the

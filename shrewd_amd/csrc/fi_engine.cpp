@@ -180,6 +180,7 @@ struct fi_engine {
     // load-time build of the trial kernel with the translated golden blocks
     hipModule_t tx_mod[3] = {nullptr, nullptr, nullptr};
     std::shared_ptr<JitJob> jit;     // the build in flight (nullptr: none)
+    std::vector<std::thread> jit_threads;   // every build this engine started: joined by fi_destroy
     std::vector<PreInst> jit_pre;    // golden pre-decoded text with the leader flags, uploaded when it lands
     uint64_t jit_blocks = 0, jit_insts = 0;
     hipFunction_t tx_fn = nullptr, tx_fn_solo = nullptr;
@@ -386,7 +387,7 @@ static void free_tx(fi_engine *e) {
         m = nullptr;
     }
     e->tx_fn = e->tx_fn_solo = e->tx_fn_odd = nullptr;
-    e->jit.reset();   // a build in flight finishes on its own (its thread holds the job)
+    e->jit.reset();   // a build in flight finishes on its own (its thread holds the job; fi_destroy joins it)
 }
 
 // Install a finished background build (at a chunk boundary, before anything
@@ -443,6 +444,12 @@ static void free_image(fi_engine *e) {
 
 void fi_destroy(fi_engine *e) {
     if (!e) return;
+    // a background build still running (a short campaign on a cold cache):
+    // wait for it, so that no thread outlives the engine and no fi_jitc child
+    // is left behind -- exiting under a running build races the static
+    // destructors of the JIT cache and of hipRTC
+    for (auto &t : e->jit_threads)
+        if (t.joinable()) t.join();
     (void)hipSetDevice(e->dev);
     free_work(e);
     free_image(e);
@@ -1231,7 +1238,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
             e->jit_insts = n_tx;
             e->jit = j;
             e->tx_status = "compiling";
-            std::thread(jit_job_run, j).detach();
+            e->jit_threads.emplace_back(jit_job_run, j);
         }
     }
     e->last_ms = golden_ms;
@@ -1491,9 +1498,8 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
         } else {
             // survivors not yet injected form a tier right after the first
             // (fi_surv_keys_kernel; profiles/r04au: intmix -3 %, qsort -3 %
-            // per step; SHREWD_FI_SOLO_ORDER=0 for the two-tier order)
-            static const bool uninj_tier = !(getenv("SHREWD_FI_SOLO_ORDER") && atoi(getenv("SHREWD_FI_SOLO_ORDER")) == 0);
-            const uint32_t skey = (solo && !pack) ? (uninj_tier ? 3u : 1u) : 0u;
+            // per step against the two-tier order)
+            const uint32_t skey = (solo && !pack) ? 3u : 0u;
             HIPCHK(launch_surv_keys(e->d_save, e->d_surv[(ep - 1) & 1], e->d_cnt + ep - 1, k, c.text_lo, e->d_skeys,
                                     e->d_svals, odd ? e->d_split + 4 * ep : nullptr, skey, e->golden.ninst, st));
             HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_skeys, e->d_skeys2, e->d_svals, e->d_svals2, k, 64, st));

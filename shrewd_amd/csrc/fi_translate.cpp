@@ -608,21 +608,14 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         if (k == E_DIRECT) return "goto B_" + std::to_string(t) + ";";
         return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto tx_dispatch; }" : "; goto tx_out; }");
     };
-    // clean-body variants (SHREWD_FI_TXV bits, default all: A/B in
-    // profiles/r04ao, r04ap): 1 = a load site caches only a mapped page (the
-    // probe's checks move to the miss), 2 = the budget counts down (one
-    // compare per check point, no add), 4 = a store site caches only a
-    // private page outside the code range
-    const char *txv_env = getenv("SHREWD_FI_TXV");
-    const unsigned txv = txv_env ? (unsigned)strtoul(txv_env, nullptr, 0) : 15u;
-    // 8 = the site caches' miss and leave tests and the budget tests hinted cold
-    const char *cold = (txv & 8u) ? "SCOLD" : "SCOND";
-    // 16 = loads from the trial's own pages hinted cold; 32 = loop proofs also
-    // tested on direct entries into a proved loop (SR_ labels)
-    // blocks of a proved loop (below) -> the loop's header: a direct entry
-    // from outside the loop goes through SR_<block>, which tests the proof as
-    // the dispatch does (the clean body; a plain forward in the full one)
-    std::map<uint32_t, uint32_t> proof_cycle;
+    // clean body (profiles/r04an-r04ap): a load site caches only a mapped page
+    // (the probe's checks move to the miss), a store site only a private page
+    // outside the code range, the budget counts down (one compare per check
+    // point), and the site caches' miss / leave tests and the budget tests are
+    // hinted cold (SCOLD) so that a block's hot path falls through.  (Losing
+    // variants removed in round 5: loads from private pages hinted cold, within
+    // noise; proofs re-tested on direct loop entries, -9 %, profiles/r04at.)
+    const char *cold = "SCOLD";
     auto sgo = [&](uint32_t from, uint64_t pc) {
         // solo-odd body: an odd target with a block is a direct edge (the
         // odd blocks are entered at their first pc only); an even one goes
@@ -634,11 +627,6 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         const Edge k = edge(from, pc);
         uint32_t t = 0;
         hof(pc, t);
-        if (k == E_DIRECT && !oddon && !cur_odd && (txv & 32u)) {
-            const auto it = proof_cycle.find(t), fi = proof_cycle.find(from);
-            if (it != proof_cycle.end() && (fi == proof_cycle.end() || fi->second != it->second))
-                return "goto SR_" + std::to_string(t) + ";";
-        }
         if (k == E_DIRECT) return "goto " + SB + std::to_string(t) + ";";
         return "{ spc = " + hex(pc) + (k == E_DISPATCH ? "; goto " + SD + "; }" : "; goto S_out; }");
     };
@@ -820,7 +808,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
             }
         }
         if (!m) continue;
-        for (uint32_t h : cyc) { hang_proof[h] = {reg, treg, step, m, loads}; proof_cycle[h] = H; }
+        for (uint32_t h : cyc) { hang_proof[h] = {reg, treg, step, m, loads}; }
     }
 
     // ---- clean body budget tests.  Only a check point tests the budget: a
@@ -1078,20 +1066,13 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                     if (!oddon) {
                         if (S.chain.count(h0) && n_sites < kSiteCaches) {
                             const uint32_t i = n_sites++;
-                            if (txv & 1u) {
-                                sc.put("  { uint8_t *p_; bool pv_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
-                                       "    if (%s(vp_ != CV%u)) { const uint64_t e_ = tlb_find(m, vp_); if (SCOND(!e_)) %s "
-                                       "CV%u = vp_; CP%u = e_; }\n", A.c_str(), immb, cold, i, sleave_here.c_str(), i, i);
-                                if (sz > 1)
-                                    sc.put("    if (%s(((uint32_t)ea_ & 4095u) > %uu)) %s\n", cold, 4096u - sz, sleave_here.c_str());
-                                sc.put("    p_ = (uint8_t *)(uintptr_t)((CP%u & ~1ULL) + (ea_ & 4095u)); pv_ = (CP%u & 1u) != 0;\n",
-                                       i, i);
-                            } else {
-                                sc.put("  { uint8_t *p_; bool pv_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
-                                       "    if (%s(vp_ != CV%u)) { CV%u = vp_; CP%u = tlb_find(m, vp_); }\n"
-                                       "    if (%s(!tx_probe_e(CP%u, ea_, %uu, p_, pv_))) %s\n",
-                                       A.c_str(), immb, cold, i, i, i, cold, i, sz, sleave_here.c_str());
-                            }
+                            sc.put("  { uint8_t *p_; bool pv_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
+                                   "    if (%s(vp_ != CV%u)) { const uint64_t e_ = tlb_find(m, vp_); if (SCOND(!e_)) %s "
+                                   "CV%u = vp_; CP%u = e_; }\n", A.c_str(), immb, cold, i, sleave_here.c_str(), i, i);
+                            if (sz > 1)
+                                sc.put("    if (%s(((uint32_t)ea_ & 4095u) > %uu)) %s\n", cold, 4096u - sz, sleave_here.c_str());
+                            sc.put("    p_ = (uint8_t *)(uintptr_t)((CP%u & ~1ULL) + (ea_ & 4095u)); pv_ = (CP%u & 1u) != 0;\n",
+                                   i, i);
                         } else {
                             sc.out += pl;
                         }
@@ -1132,24 +1113,17 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 if (!oddon) {
                     if (S.chain.count(h0) && n_sites < kSiteCaches) {
                         const uint32_t i = n_sites++;
-                        if (txv & 4u) {   // (a page meeting the code range is never cached: every store probes it)
-                            sc.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
-                                   "    if (SCOND(vp_ == CV%u)) {\n", A.c_str(), immb, i);
-                            if (sz > 1)
-                                sc.put("      if (SCOND(((uint32_t)ea_ & 4095u) > %uu)) %s\n", 4096u - sz, sleave_here.c_str());
-                            sc.put("      p_ = (uint8_t *)(uintptr_t)((CP%u & ~1ULL) + (ea_ & 4095u));\n"
-                                   "    } else {\n      const uint64_t e_ = tlb_find(m, vp_);\n"
-                                   "      if (SCOND(!tx_probe_st_e(e_, ea_, %uu, p_, tx))) %s\n"
-                                   "      if (SCOND((vp_ << 12) >= tx.chi || ((vp_ + 1) << 12) <= tx.clo)) { CV%u = vp_; CP%u = e_; }\n"
-                                   "    }\n    *(g_%s *)p_ = (%s)%s; }\n", i, sz, sleave_here.c_str(), i, i, gtype(sz), ltype(sz),
-                                   B.c_str());
-                        } else {
-                            sc.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
-                                   "    if (%s(vp_ != CV%u)) { CV%u = vp_; CP%u = tlb_find(m, vp_); }\n"
-                                   "    if (%s(!tx_probe_st_e(CP%u, ea_, %uu, p_, tx))) %s\n"
-                                   "    *(g_%s *)p_ = (%s)%s; }\n", A.c_str(), immb, cold, i, i, i, cold, i, sz,
-                                   sleave_here.c_str(), gtype(sz), ltype(sz), B.c_str());
-                        }
+                        // (a page meeting the code range is never cached: every store probes it)
+                        sc.put("  { uint8_t *p_; const uint64_t ea_ = %s + %s, vp_ = ea_ >> 12;\n"
+                               "    if (SCOND(vp_ == CV%u)) {\n", A.c_str(), immb, i);
+                        if (sz > 1)
+                            sc.put("      if (SCOND(((uint32_t)ea_ & 4095u) > %uu)) %s\n", 4096u - sz, sleave_here.c_str());
+                        sc.put("      p_ = (uint8_t *)(uintptr_t)((CP%u & ~1ULL) + (ea_ & 4095u));\n"
+                               "    } else {\n      const uint64_t e_ = tlb_find(m, vp_);\n"
+                               "      if (SCOND(!tx_probe_st_e(e_, ea_, %uu, p_, tx))) %s\n"
+                               "      if (SCOND((vp_ << 12) >= tx.chi || ((vp_ + 1) << 12) <= tx.clo)) { CV%u = vp_; CP%u = e_; }\n"
+                               "    }\n    *(g_%s *)p_ = (%s)%s; }\n", i, sz, sleave_here.c_str(), i, i, gtype(sz), ltype(sz),
+                               B.c_str());
                     } else {
                         sc.put("  { uint8_t *p_; if (SCOND(!tx_probe(m, %s + %s, %uu, true, p_, tx))) %s\n"
                                "    *(g_%s *)p_ = (%s)%s; }\n", A.c_str(), immb, sz, sleave_here.c_str(), gtype(sz),
@@ -1222,11 +1196,6 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         sboth("}\n");
         if (cur_odd) g.out.swap(g_keep);
     }
-    if (!oddon && (txv & 32u))   // direct entries into proved loops (sgo)
-        for (const auto &kv : proof_cycle) {
-            so.put("SR_%u: goto S_%u;\n", kv.first, kv.first);
-            sc.put("SR_%u: %sgoto S_%u;\n", kv.first, proof_test(kv.first).c_str(), kv.first);
-        }
     if (oddon) g.out.swap(g_mode);
     }
     cur_odd = false;
@@ -1236,16 +1205,10 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     // the clean body's entry: its site caches start empty (declared without an
     // initializer: the dispatch label below them is also a jump target)
     std::string sc_head;
-    if (txv & 2u)   // the budget counts down (solo_tx_clean_run: SADD / SOVER / SDONE)
-        sc_head += "#undef SADD\n#undef SOVER\n#undef SDONE\n#define SADD(n_) (brem -= (n_))\n"
-                   "#define SOVER(n_) (brem < (n_))\n#define SDONE() (bud - brem)\n";
-    if (txv & 16u)   // loads from the trial's own pages hinted cold (shared snapshot frames straight-line)
-        sc_head += "#undef SPRIV\n#define SPRIV(x) __builtin_expect(!!(x), 0)\n";
-    if (txv & 8u) {
-        sc_head += "#define SCOLD(x) __builtin_expect(!!(x), 0)\n";
-        if (txv & 2u) sc_head += "#undef SOVER\n#define SOVER(n_) __builtin_expect(brem < (n_), 0)\n";
-        else sc_head += "#undef SOVER\n#define SOVER(n_) __builtin_expect(st + (n_) > bud, 0)\n";
-    }
+    // the budget counts down (solo_tx_clean_run: SADD / SOVER / SDONE); cold hints
+    sc_head += "#undef SADD\n#undef SOVER\n#undef SDONE\n#define SADD(n_) (brem -= (n_))\n"
+               "#define SOVER(n_) __builtin_expect(brem < (n_), 0)\n#define SDONE() (bud - brem)\n"
+               "#define SCOLD(x) __builtin_expect(!!(x), 0)\n";
     for (uint32_t i = 0; i < kSiteCaches; i++) sc_head += sfmt("  uint64_t CV%u, CP%u;\n", i, i);
     sc_head += "S_entry:\n";
     for (uint32_t i = 0; i < kSiteCaches; i++) sc_head += sfmt("  CV%u = ~0ULL; CP%u = 0;\n", i, i);

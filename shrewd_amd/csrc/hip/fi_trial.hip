@@ -1734,8 +1734,8 @@ __device__ __noinline__ void solo_tx_clean_run(KCtx *CX, lds_u64 *R, lds_mem *mp
     // its counter this far from zero, the trial reaches the hang cap inside it
     const uint32_t hleft = io->hleft, hok = io->hok;
     uint32_t hang = 0, bst = 0;
-    // instructions: counted up (st) or, in the count-down variant the body
-    // selects (fi_translate.cpp, SHREWD_FI_TXV), the budget left (brem)
+    // instructions: counted down from the budget (brem; the body redefines
+    // SADD / SOVER / SDONE, fi_translate.cpp)
     uint32_t brem = bud;
 #define SADD(n_) (st += (n_))
 #define SOVER(n_) (st + (n_) > bud)
@@ -1771,6 +1771,176 @@ S_out:
     io->cslo = 0xFFFFFFFFu; io->cshi = 0u; io->schg = 0u; io->hang = hang; io->bst = bst;
 }
 #endif
+
+// ---- dynamic loop proofs (solo kernel).  The static proofs
+// (fi_translate.cpp) only see the golden run's translated blocks; the trials
+// that end a campaign's tail loop where no translation reaches: in rewritten
+// code, in data pages a flipped pc or return address jumped into, or through a
+// return into the middle of a block.  A trial that has spent FI_LP_START
+// instructions in the interpreters is single-stepped through the general path
+// for one pass around its current loop, each committed instruction recorded
+// (its operands and kind), and the pass is proved to repeat forever:
+//   * every branch / indirect-jump operand, load and store address and
+//     store datum is loop-invariant -- a constant, a register the pass never
+//     writes, or computed only from invariant values -- so the next pass takes
+//     the same path, reads the same addresses and writes the same data;
+//   * every store in the pass was silent (wrote the bytes already there), so
+//     memory, and with it every load and every fetched instruction, is the
+//     same from pass to pass;
+//   * no instruction with another effect (syscall, CSR, AMO, LR/SC, M5 op,
+//     cache-block or vector op) is in it, and none faulted;
+//   * a register the pass writes and is taken as invariant at its start holds
+//     the same value at the end of the recorded pass as at its start.
+// By induction every later pass equals the recorded one: the trial runs to
+// the hang cap (a hang; it can neither end nor meet a golden snapshot, whose
+// future terminates).  Registers 0..31 are x0..x31, 32..63 f0..f31.
+#ifndef FI_LP_WINDOW
+#define FI_LP_WINDOW 128   // instructions per recorded pass at most
+#endif
+#ifndef FI_LP_START
+#define FI_LP_START 4096   // interpreted instructions before the first probe (doubling after a failed one)
+#endif
+struct LoopProbe {
+    uint32_t on;            // recording a pass
+    uint32_t n;             // entries recorded
+    uint32_t tries;         // windows started in this probe
+    uint32_t fp0;           // the FP file existed at the start
+    uint32_t cnt, at;       // interpreted instructions since the last probe, the next probe's threshold
+    uint64_t pc0;           // where the pass starts (and must return)
+    uint64_t r0[32], f0[32];   // registers at the start
+    uint32_t e[FI_LP_WINDOW];  // per committed instruction: lp_entry
+};
+typedef __attribute__((address_space(3))) LoopProbe lds_lp;
+constexpr uint32_t kLpNone = 127u;                       // no register in a field
+constexpr uint32_t kLpPure = 0, kLpLoad = 1, kLpStore = 2, kLpCtrl = 3, kLpConst = 4;
+constexpr uint32_t kLpBad = 0xFFFFFFFFu;                 // an instruction the proof does not admit
+constexpr uint32_t kLpLoud = 0xFFFFFFFEu;                // a store that changed memory
+
+// An M5 pseudo-op without an architectural effect beyond a0 = 0, a1 = 0 (the
+// general path's `default` case of OP_m5op: not rpns, sum, initparam, a
+// debug break or panic, nor one that controls the simulator or host files).
+__device__ __forceinline__ bool m5_no_effect(uint32_t fn) {
+    switch (fn) {
+    case 0x07: case 0x23: case 0x30: case 0x51: case 0x54:
+    case 0x01: case 0x02: case 0x03: case 0x04: case 0x21: case 0x22: case 0x43: case 0x4f: case 0x52:
+    case 0x53: case 0x5a: case 0x5b: case 0x62: case 0x70: case 0x71:
+        return false;
+    default: return true;
+    }
+}
+
+// One committed instruction as {kind, destination, up to three sources}:
+// s1 | s2 << 7 | s3 << 14 | dst << 21 | kind << 28 (fields 127: none; x0
+// reads are constants and x0 writes vanish).  Integer operands come from the
+// decode flags (the same read / write sets the liveness pass uses); FP
+// register fields are taken per op (rv_refine_fp_arith / rv_refine_fp_amo).
+__device__ __noinline__ uint32_t lp_entry(uint32_t op, uint32_t rd, uint32_t rs1, uint32_t rs2, uint32_t fl,
+                                          int32_t imm, bool silent) {
+    uint32_t s1 = kLpNone, s2 = kLpNone, s3 = kLpNone, dst = kLpNone, kind = kLpPure;
+    if ((fl & kPreRs1) && rs1) s1 = rs1;
+    if ((fl & kPreRs2) && rs2) s2 = rs2;
+    if ((fl & kPreRd) && rd) dst = rd;
+    switch (op) {
+    case OP_UNKNOWN: case OP_ESC_FP: case OP_ESC_VEC: case OP_ESC_AMO: case OP_ESC_SYS: case OP_ESC_CRYPTO:
+    case OP_ESC_CBO: case OP_ESC_CMP: case OP_ESC_M5: case OP_ESC_HYP: case OP_c_ebreak: case OP_ebreak:
+    case OP_ecall: case OP_csr: case OP_lr_w: case OP_sc_w: case OP_lr_d: case OP_sc_d: case OP_priv:
+    case OP_cbo:
+        return kLpBad;
+    case OP_m5op:   // (the commit records a0 = 0 and a1 = 0 for the ones without an effect)
+        return kLpBad;
+    case OP_vec:    // RVV before any vset*: a no-op of one or two ticks (imm 2, 3), else a fault or escape
+        if (imm != 2 && imm != 3) return kLpBad;
+        break;
+    case OP_c_lw: case OP_c_ld: case OP_c_lbu: case OP_c_lhu: case OP_c_lh: case OP_c_lwsp: case OP_c_ldsp:
+    case OP_lb: case OP_lh: case OP_lw: case OP_ld: case OP_lbu: case OP_lhu: case OP_lwu:
+        kind = kLpLoad; break;
+    case OP_c_sb: case OP_c_sh: case OP_c_sw: case OP_c_sd: case OP_c_swsp: case OP_c_sdsp:
+    case OP_sb: case OP_sh: case OP_sw: case OP_sd:
+        if (!silent) return kLpLoud;
+        kind = kLpStore; break;
+    case OP_flh: case OP_flw: case OP_fld: case OP_c_fld: case OP_c_fldsp:
+        kind = kLpLoad; dst = 32 + rd; break;
+    case OP_fsh: case OP_fsw: case OP_fsd: case OP_c_fsd: case OP_c_fsdsp:
+        if (!silent) return kLpLoud;
+        kind = kLpStore; s2 = 32 + rs2; break;
+    case OP_beq: case OP_bne: case OP_blt: case OP_bge: case OP_bltu: case OP_bgeu: case OP_c_beqz: case OP_c_bnez:
+    case OP_jalr: case OP_c_jr: case OP_c_jalr:
+        kind = kLpCtrl; break;   // (a link register gets pc + len: a constant)
+    case OP_jal: case OP_c_j: case OP_auipc:
+        kind = kLpConst; break;
+    case OP_fmv_x_w: case OP_fmv_x_d: case OP_fmv_x_h: case OP_fclass_s: case OP_fclass_d: case OP_fclass_h:
+    case OP_fcvt_f2i: case OP_fcvtmod:
+        s1 = 32 + rs1; break;
+    case OP_feq: case OP_flt: case OP_fle:
+        s1 = 32 + rs1; s2 = 32 + rs2; break;
+    case OP_fmv_w_x: case OP_fmv_d_x: case OP_fmv_h_x: case OP_fcvt_i2f:
+        dst = 32 + rd; break;
+    case OP_fli:
+        kind = kLpConst; dst = 32 + rd; break;
+    case OP_fsgnj_s: case OP_fsgnjn_s: case OP_fsgnjx_s: case OP_fsgnj_d: case OP_fsgnjn_d: case OP_fsgnjx_d:
+    case OP_fsgnj_h: case OP_fsgnjn_h: case OP_fsgnjx_h: case OP_fadd: case OP_fsub: case OP_fmul: case OP_fdiv:
+    case OP_fsqrt: case OP_fmin: case OP_fmax: case OP_fround: case OP_fcvt_f2f:
+        s1 = 32 + rs1; s2 = 32 + rs2; dst = 32 + rd; break;   // (one-operand ops: rs2 taken too, conservatively)
+    case OP_fmadd: case OP_fmsub: case OP_fnmsub: case OP_fnmadd:
+        s1 = 32 + rs1; s2 = 32 + rs2; s3 = 32 + (((uint32_t)imm >> 8) & 31); dst = 32 + rd; break;
+    default:   // AMOs are not in any case above: they read and write memory
+        if (op >= OP_amoadd_w && op <= OP_amomaxu_d) return kLpBad;
+        break;   // integer ALU / M / B / K / Zicond, fences and prefetch hints: pure
+    }
+    return s1 | s2 << 7 | s3 << 14 | dst << 21 | kind << 28;
+}
+
+__device__ __forceinline__ bool lp_src_ok(uint32_t e, uint64_t cur) {
+    const uint32_t s1 = e & 127, s2 = (e >> 7) & 127, s3 = (e >> 14) & 127;
+    return (s1 == kLpNone || ((cur >> s1) & 1)) && (s2 == kLpNone || ((cur >> s2) & 1)) &&
+           (s3 == kLpNone || ((cur >> s3) & 1));
+}
+// The invariance of the destination after entry e, given the invariant set cur.
+__device__ __forceinline__ uint64_t lp_step(uint32_t e, uint64_t cur) {
+    const uint32_t dst = (e >> 21) & 127, kind = e >> 28;
+    if (dst == kLpNone) return cur;
+    const bool inv = kind != kLpPure || lp_src_ok(e, cur);   // loads read unchanged memory at invariant addresses
+    return inv ? (cur | (1ULL << dst)) : (cur & ~(1ULL << dst));
+}
+
+// The recorded pass repeats forever (the rules above).  xe: the integer
+// registers now, at the pass's end; fr: the slot's FP file (stride apart;
+// zeros while it does not exist, fp false).
+__device__ __noinline__ bool lp_prove(const lds_lp *P, const uint64_t *xe, const uint64_t *fr, uint64_t stride,
+                                      bool fp) {
+    const uint32_t n = P->n;
+    uint64_t W = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t dst = (P->e[i] >> 21) & 127;
+        if (dst != kLpNone) W |= 1ULL << dst;
+    }
+    W &= ~1ULL;
+    // the registers invariant at the pass's start: the least fixpoint from
+    // "never written in the pass" (one written from invariant values carries
+    // the same value into every later pass)
+    uint64_t inv = ~W;
+    for (int it = 0; it < 65; it++) {
+        uint64_t cur = inv;
+        for (uint32_t i = 0; i < n; i++) cur = lp_step(P->e[i], cur);
+        const uint64_t nin = ~W | (W & cur);
+        if (nin == inv) break;
+        inv = nin;
+    }
+    uint64_t cur = inv;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t e = P->e[i], kind = e >> 28;
+        if (kind != kLpPure && kind != kLpConst && !lp_src_ok(e, cur)) return false;
+        cur = lp_step(e, cur);
+    }
+    const uint64_t chk = W & inv;
+    for (uint32_t r = 1; r < 64; r++) {
+        if (!((chk >> r) & 1)) continue;
+        const uint64_t a = r < 32 ? P->r0[r] : P->f0[r - 32];
+        const uint64_t b = r < 32 ? xe[r] : (fp ? fr[(uint64_t)(r - 32) * stride] : 0ULL);
+        if (a != b) return false;
+    }
+    return true;
+}
 
 // ---- solo pre-decoded run, out of line: the fast path of trial_body<1>
 // (one trial, every value uniform) with its own register allocation.  Same
@@ -3026,14 +3196,20 @@ leave:
 #ifndef FI_WAVES_PER_EU
 #define FI_WAVES_PER_EU 1
 #endif
-// A trial that rewrote code and leaves the translated blocks after fewer than
-// FI_TX_SHORT instructions four times running stays in the interpreter for
-// the next FI_TX_SKIP (a round trip costs more than the blocks save)
+// A trial that leaves the translated blocks after fewer than FI_TX_SHORT
+// instructions four times running stays in the interpreter: if it rewrote
+// code, for the next FI_TX_SKIP (a round trip costs more than the blocks save)
 #ifndef FI_TX_SHORT
 #define FI_TX_SHORT 8
 #endif
 #ifndef FI_TX_SKIP
 #define FI_TX_SKIP 4096
+#endif
+// ... and a trial that rewrote nothing the next FI_TX_SKIP_CLEAN, doubling
+// while the short runs recur (qsort's returns into their own epilogue:
+// ~3 us per instruction before, tools/gpu/launch_size.py census r05c)
+#ifndef FI_TX_SKIP_CLEAN
+#define FI_TX_SKIP_CLEAN 256
 #endif
 // Solo kernel: the launch context through a plain pointer, so that the
 // compiler can keep loop-invariant fields in registers (a one-lane wave has
@@ -3191,7 +3367,7 @@ __device__ __forceinline__ void trial_body() {
     // solo: a lane whose translated runs keep ending after a few instructions
     // (its loop holds rewritten code, so every block exit writes back and
     // reloads the register file) stays in the pre-decoded path for a while
-    uint32_t tx_short = 0, tx_skip_until = 0;
+    uint32_t tx_short = 0, tx_skip_until = 0, tx_skip_n = FI_TX_SKIP_CLEAN;
     // per-wave diagnostic counters live in LDS, not SGPRs (the loop's scalar
     // registers are scarce): slow fetches, min-PC reductions, lane-instructions,
     // snapshot checks, early exits, translated instructions and entries.  Every
@@ -3210,6 +3386,31 @@ __device__ __forceinline__ void trial_body() {
 #pragma unroll 8
         for (uint32_t k = 0; k < kDC; k++) DCT[k] = 0xFFFFFFFFu;
     }
+    // solo only: the dynamic loop proof's state (LoopProbe)
+    __shared__ alignas(8) uint32_t LPB[kNL == 1 ? (sizeof(LoopProbe) + 3) / 4 : 2];
+    LoopProbe &LP = *(LoopProbe *)LPB;
+    if constexpr (kNL == 1) {
+        LP.on = 0; LP.cnt = 0; LP.at = FI_LP_START;
+    }
+    // (a constant false in the 64-lane kernel)
+#define LP_ON (kNL == 1 && LP.on != 0)
+// a new recorded pass from here (the registers now), or the end of the probe
+// after 4 windows that did not close
+#define LP_WINDOW()                                                                          \
+    do {                                                                                     \
+        if (++LP.tries > 4) { LP_FAIL(); break; }                                           \
+        LP.n = 0; LP.pc0 = L.pc; LP.fp0 = L.fp ? 1u : 0u;                                    \
+        for (int r_ = 0; r_ < 32; r_++) {                                                   \
+            LP.r0[r_] = R[r_];                                                               \
+            LP.f0[r_] = L.fp ? CX->fregs[(uint64_t)r_ * CX->n_slots + slot] : 0ULL;          \
+        }                                                                                    \
+    } while (0)
+#define LP_FAIL()                                                                            \
+    do {                                                                                     \
+        LP.on = 0; LP.cnt = 0;                                                               \
+        LP.at = LP.at < (1u << 30) ? 2 * LP.at : LP.at;                                      \
+        if (kSoloOnce) atomicAdd(&CX->stats[60], 1ull);                                      \
+    } while (0)
 #define DC_INVAL(lo_, sz_)                                                                          \
     do {                                                                                            \
         if constexpr (kNL == 1) {                                                                   \
@@ -3419,6 +3620,16 @@ __device__ __forceinline__ void trial_body() {
             next_snap += CX->rec_interval;
         }
 
+        // ---- solo: start a dynamic loop proof (LoopProbe) once the trial has
+        // spent LP.at instructions in the interpreters; the general path then
+        // records one pass (its commit below)
+        if constexpr (kNL == 1) {
+            if (!CX->record && CX->hang_proof && !LP.on && LP.cnt >= LP.at && !L.done && m.req_vpn == kNone &&
+                (L.injected == 1 || L.injected == 2) && L.watch <= 0) {
+                LP.on = 1; LP.tries = 0;
+                LP_WINDOW();
+            }
+        }
         const bool ready = !L.done && m.req_vpn == kNone;
         const uint64_t act = wballot<kNL>(ready);
         if (act == 0) {
@@ -3610,7 +3821,7 @@ __device__ __forceinline__ void trial_body() {
             if constexpr (kNL == 1) {
                 // ---- solo: one trial, every value uniform -- no groups, no
                 // parking, plain register writes; the same exits and counters
-                if (tx_entry && mine && n_iter >= tx_skip_until && L.injected != 3 && m.lock == kNone) {
+                if (tx_entry && mine && n_iter >= tx_skip_until && L.injected != 3 && m.lock == kNone && !LP_ON) {
                     const uint64_t rem64 = next_ev - L.ninst;
                     const uint32_t rem = rem64 > (1u << 30) ? (1u << 30) : (uint32_t)rem64;
                     const uint32_t wbud = CX->wave_budget ? CX->wave_budget - n_iter : (1u << 30);
@@ -3647,8 +3858,10 @@ __device__ __forceinline__ void trial_body() {
                     if (uni32(sio->hang)) {   // a loop that cannot leave before the cap
                         uint64_t kf = 0, fva = 0;
                         const uint64_t left = L.ninst < CX->hang_cap ? CX->hang_cap - L.ninst : 0;
-                        const int r = uni32(sio->lp_n) ? loop_outcome(CX, w, m, slot, (const lds_u64 *)R,
-                                                                      (const lds_io *)sio, left, kf, fva) : 1;
+                        // (always: the body proved it against hleft, capped at 2^32 - 1;
+                        // loop_outcome re-checks every loop against the 64-bit `left`)
+                        const int r = loop_outcome(CX, w, m, slot, (const lds_u64 *)R, (const lds_io *)sio, left, kf,
+                                                   fva);
                         if (r == 1) {   // a proved hang: the record of one that ran to the cap
                             proved_skip = left;
                             L.ninst += left;
@@ -3665,10 +3878,20 @@ __device__ __forceinline__ void trial_body() {
                         }
                         continue;
                     }
-                    if (m.code_dirty && st < FI_TX_SHORT) {
-                        if (++tx_short >= 4) { tx_short = 0; tx_skip_until = n_iter + FI_TX_SKIP; }
+                    // thrash guard: runs that keep ending after a few instructions
+                    // (a loop entered mid-block, e.g. a return into its own
+                    // epilogue, leaves at every dispatch) cost a round trip each;
+                    // the interpreter takes the next FI_TX_SKIP (rewritten code)
+                    // or tx_skip_n instructions, doubling while it recurs
+                    if (st < FI_TX_SHORT) {
+                        if (++tx_short >= 4) {
+                            tx_short = 0;
+                            tx_skip_until = n_iter + (m.code_dirty ? FI_TX_SKIP : tx_skip_n);
+                            tx_skip_n = tx_skip_n < (1u << 20) ? 2 * tx_skip_n : tx_skip_n;
+                        }
                     } else {
                         tx_short = 0;
+                        if (st >= 8 * FI_TX_SHORT) tx_skip_n = FI_TX_SKIP_CLEAN;
                     }
                     // the clean body tests its budget once per run of blocks: one that
                     // stops at a test with nothing run leaves the rest up to the event
@@ -3771,7 +3994,7 @@ __device__ __forceinline__ void trial_body() {
         // whole instruction commits for every group lane.
         // (an armed result fault commits in the general path, and a lane holding
         // an LR/SC lock record stays there: only its stores erase the record)
-        if (CX->pre_ok && lpc >= CX->text_lo && lpc < CX->text_hi &&
+        if (!LP_ON && CX->pre_ok && lpc >= CX->text_lo && lpc < CX->text_hi &&
             wballot<kNL>(mine && (L.injected == 3 || m.lock != kNone)) == 0) {
             // lanes that rewrote code run here too, until they reach a rewritten
             // instruction; lanes watching a protected flipped register, until an
@@ -3796,6 +4019,7 @@ __device__ __forceinline__ void trial_body() {
                     for (int k = 0; k < 4; k++) pacc[k] += pio->prof[k];
 #endif
                     if (steps) {
+                        LP.cnt += steps;   // (interpreted: counts toward a loop probe)
                         L.ninst += steps; L.ncyc += steps + uni32(pio->xticks);
                         L.fetch_b += uni32(pio->fbytes); L.data_b += uni32(pio->dbytes);
                         L.pc = uni64(pio->spc); L.watch = (int)uni32((uint32_t)pio->watch);
@@ -4429,12 +4653,22 @@ __device__ __forceinline__ void trial_body() {
             }
         }
         if (detect || xdet) f = F_DETECT;   // the op does not execute
+        bool lp_silent = false;   // a loop probe's plain store wrote the bytes already there
         if (mine) {
         if (msz && f == F_NONE) {
             // one call site (an AMO reads, then writes, in a second pass): a
             // second inlined copy of mem_access puts the lane state in scratch
             const uint64_t ea = cbo ? (a & ~63ULL) : (amo >= 0 || llsc) ? a : a + imm;
             uint64_t old = 0;
+            if constexpr (kNL == 1) {
+                if (LP.on && mst && amo < 0 && !llsc && !cbo) {   // the bytes before the store (no side effect)
+                    uint64_t ov = 0, fv = 0;
+                    int fo;
+                    OOL(fo = mem_access(CX, wc_, mc_, slot, ea, msz, false, ov, fv, 0));
+                    const uint64_t mk = msz >= 8 ? ~0ULL : ((1ULL << (8 * msz)) - 1);
+                    lp_silent = fo == F_NONE && ((ov ^ sval) & mk) == 0;
+                }
+            }
 #pragma unroll 1
             for (int pass = 0; pass < (amo >= 0 ? 2 : 1); pass++) {
                 t = pass ? amo_apply(amo, old, b, msz == 4) : (amo >= 0 ? 0 : (llsc == 2 ? b : sval));
@@ -4491,9 +4725,44 @@ __device__ __forceinline__ void trial_body() {
             L.ninst++;
             if (rdet) finish(L, FI_DETECTED, 0, 0, (uint32_t)pc);   // the shadow disagrees at commit
             else L.pc = npc;
+            if constexpr (kNL == 1) {
+                if (!LP.on) {
+                    LP.cnt++;
+                } else if (!L.done) {   // record the pass; at its start pc again, the proof
+                    uint32_t en = lp_entry(d.op, d.rd, d.rs1, d.rs2, d.flags, d.imm, lp_silent);
+                    if (d.op == OP_m5op && m5_no_effect((uint32_t)d.imm) && LP.n + 1 < FI_LP_WINDOW) {
+                        LP.e[LP.n++] = kLpNone | kLpNone << 7 | kLpNone << 14 | 10u << 21 | kLpConst << 28;
+                        en = kLpNone | kLpNone << 7 | kLpNone << 14 | 11u << 21 | kLpConst << 28;
+                    }
+                    if (en == kLpBad) {
+                        LP_FAIL();
+                    } else if (en == kLpLoud || LP.n >= FI_LP_WINDOW) {
+                        LP_WINDOW();   // memory changed, or the pass is too long: again from here
+                    } else {
+                        LP.e[LP.n++] = en;
+                        if (L.pc == LP.pc0) {
+                            const bool hang = lp_prove((const lds_lp *)&LP, (const uint64_t *)R,
+                                                       CX->fregs + slot, CX->n_slots, L.fp);
+                            if (hang) {   // the record of a hang at the cap
+                                const uint64_t left = L.ninst < CX->hang_cap ? CX->hang_cap - L.ninst : 0;
+                                proved_skip += left;
+                                L.ninst += left;
+                                finish(L, FI_HANG, 1, 0, 0u);
+                                LP.on = 0;
+                                if (kSoloOnce) atomicAdd(&CX->stats[59], 1ull);
+                            } else {
+                                LP_FAIL();
+                            }
+                        }
+                    }
+                }
+            }
         } else {
         switch (f) {
         case F_SYSCALL: {   // SyscallFault::invokeSE advances the PC first (arch/riscv/faults.cc:325-333)
+            if constexpr (kNL == 1) {
+                if (LP.on) LP_FAIL();
+            }
             L.pc = pc + d.len;
             // (out of line on copies: the interpreter's state stays in registers)
             Lane Ls = L;
@@ -4543,7 +4812,7 @@ __device__ __forceinline__ void trial_body() {
         const uint64_t npc0 = uni64(rdl64<kNL>(L.pc, __ffsll((unsigned long long)cm) - 1));
         if (wballot<kNL>(cont && L.pc == npc0) != cm || npc0 >= wait_min) break;
         if (CX->wave_budget && n_iter + 1 >= CX->wave_budget) break;
-        if (CX->pre_ok) {   // back to the fast path (or translated blocks) when they can take the next one
+        if (CX->pre_ok && !LP_ON) {   // back to the fast path (or translated blocks) when they can take the next one
             TextRef tn;
             tn.pre = CX->pre; tn.lo = (uint32_t)CX->text_lo; tn.hi = (uint32_t)(CX->text_lo >> 32);
             tn.bytes = CX->text_bytes; tn.clo = CX->code_lo; tn.chi = CX->code_hi;

@@ -385,6 +385,52 @@ def test_counted_loop_hang_proofs(engine_factory, oracle_mod):
     compare(a[sel], oracle_for(oracle_mod, "crc32").run_trials(sites), sites)
 
 
+# tail trials of the 1M-trial north-star campaigns (seed 0x5EED0003, found by
+# tools/gpu/launch_size.py): loops no translated block covers -- floating-point
+# loads and arithmetic in rewritten code with silent stores (qsort 805936,
+# 127484, 735672), a return into its own epilogue (373107), an RVV no-op in a
+# data page (775944), a no-effect M5 op in rewritten code (953708), and
+# `jal x4, 0` in a data page (intmix 990675, 682623)
+DYN_LOOP_TRIALS = {"qsort": [805936, 127484, 735672, 373107, 775944, 953708], "intmix": [990675, 682623]}
+
+
+@pytest.mark.parametrize("name", ["qsort", "intmix"])
+def test_dynamic_loop_proofs(engine_factory, oracle_mod, name):
+    """Dynamic loop proofs (fi_trial.hip LoopProbe / lp_prove):
+    a trial looping in the interpreters is single-stepped through one pass of
+    its loop and proved to repeat forever.  Every such trial is a hang whose
+    record equals the oracle's (which runs it to the cap) and the engine's
+    own without proofs (FI_CFG_NO_HANG_PROOF), and the proofs fired
+    (stats[59]) with far fewer instructions executed."""
+    from shrewd_amd.fi import CFG_NO_HANG_PROOF
+    ids = DYN_LOOP_TRIALS[name]
+    on = engine_factory(name, flags=128, max_trials_per_launch=4096)            # FI_CFG_SOLO_ALL
+    off = engine_factory(name, flags=128 | CFG_NO_HANG_PROOF, max_trials_per_launch=4096)
+    for e in (on, off):
+        e.set_campaign(0x5EED0003, REGS | PC, 1)
+        e.set_protect(0)
+    sites = on.sample(0, max(ids) + 1)[ids]
+    a, ha = on.run_sites(sites)
+    proved = int(on.debug_stats()[59])
+    b, hb = off.run_sites(sites)
+    assert int(off.debug_stats()[59]) == 0
+    assert np.array_equal(a, b)
+    assert (a["cls"] == 3).all() and (a["detail"] == 0).all()
+    assert proved >= len(ids) - 1
+    assert int(ha["device_insts"]) * 5 < int(hb["device_insts"])
+    compare(a, oracle_for(oracle_mod, name).run_trials(sites), sites)
+    # and inside a normal campaign (the 64-lane epoch first): same records as without proofs
+    n = 20000
+    on2 = engine_factory(name, max_trials_per_launch=n)
+    off2 = engine_factory(name, flags=CFG_NO_HANG_PROOF, max_trials_per_launch=n)
+    for e in (on2, off2):
+        e.set_campaign(0x5EED0003, REGS | PC, 1)
+        e.set_protect(0)
+    c, _ = on2.run_trials(0, n)
+    d, _ = off2.run_trials(0, n)
+    assert np.array_equal(c, d)
+
+
 def test_runoff_loop_proofs(oracle_mod):
     """Run-off loops (fi_translate.cpp, fi_trial.hip loop_outcome): faults on
     the scan pointer / end of the runoff program's three scan loops.  Trials

@@ -41,13 +41,10 @@ def test_crc32_loop_proofs():
     body = _translate()
     # the table's inner bit loop (addi t6, t6, -1; bnez t6): a counted loop of
     # three blocks, no memory access -- a hang proof without loads, at every
-    # block of the cycle (tested on dispatch entries; with SHREWD_FI_TXV bit
-    # 32 also on direct entries from outside the loop, SR_ labels)
+    # block of the cycle (tested on dispatch entries)
     hang = re.findall(r"TXHANG\(X31, -1, 5u\).*?TXLOOP\((\d+)u, 5u, 0u\)", body)
     assert len(hang) == 3 and all(int(c) & 0xFF == 31 for c in hang)
-    sr = _translate({"SHREWD_FI_TXV": "47"})
-    assert len(re.findall(r"TXHANG\(X31, -1, 5u\)", sr)) == 6
-    assert "goto SR_130;" in sr and "goto SR_182;" in sr and "goto SR_" not in body
+    assert "goto SR_" not in body
     # the crc loop (lbu t1, 0(a0) ... addi a0, a0, 1; bne a0, a1): a run-off
     # block against a1, a counter load at a0 and a table load at s2 + [0, 1020]
     m = re.search(r"TXHANG\(X10 - X11, 1, 10u\).*?TXLOOP\((\d+)u, 10u, 2u\); TXLD\(0, (\d+)u, (-?\d+), (\d+)u\); "
@@ -59,10 +56,12 @@ def test_crc32_loop_proofs():
     assert (d1 & 0xFF, (d1 >> 8) & 15, (d1 >> 12) & 15, d1 >> 16, o1, s1) == (18, 1, 4, 5, 0, 1020)   # lwu at s2+
 
 
-def test_clean_body_variants_translate():
-    """Every SHREWD_FI_TXV variant of the clean body still carries the same proofs."""
+def test_clean_body_shape():
+    """The clean body is generated in one shape (the A/B variants of round 4
+    are gone): the budget counts down, the cold hints are on, and the
+    translator reads no variant switch from the environment."""
     base = _translate()
-    for v in ("0", "8", "31"):
-        body = _translate({"SHREWD_FI_TXV": v})
-        assert body.count("TXLOOP(") == base.count("TXLOOP(")
-        assert ("SCOLD(" in body) == (int(v) & 8 != 0)
+    clean = base.split("/*@TX_SPLIT@*/")[-1]
+    assert "#define SADD(n_) (brem -= (n_))" in clean and "#define SCOLD(x)" in clean
+    assert "SCOLD(" in clean and "SPRIV(x) __builtin_expect" not in clean
+    assert _translate({"SHREWD_FI_TXV": "47"}) == base
