@@ -24,6 +24,11 @@ def parse(argv=None):
     ap.add_argument("--cmd", default=None, help="comma-separated argv (default: the workload path)")
     ap.add_argument("--env", default="", help="comma-separated K=V")
     ap.add_argument("--checkpoint", default="", help="gem5 SE checkpoint directory to start the trials from")
+    # Process.input / Process.executable (src/sim/Process.py:44,69), as se.py passes them
+    ap.add_argument("--input", default="cin",
+                    help="Process.input: 'cin' = the host's stdin (fd 0 reads escape), else a file fd 0 reads")
+    ap.add_argument("--executable", default="",
+                    help="Process.executable: what readlinkat('/proc/self/exe') resolves (default: the workload)")
     ap.add_argument("--trials", type=int, default=1000)
     ap.add_argument("--first-trial", type=int, default=0)
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0001)
@@ -52,7 +57,7 @@ def run_gem5(a):
     import m5
     from m5.objects import FaultCampaign, Root
     camp = FaultCampaign(workload=a.workload, cmd=_split(a.cmd) or [a.workload], env=_split(a.env),
-                         checkpoint=a.checkpoint,
+                         checkpoint=a.checkpoint, input=a.input, executable=a.executable,
                          trials=a.trials, first_trial=a.first_trial, seed=a.seed,
                          structures=_split(a.structures), bits=a.bits or "0-63", burst=a.burst,
                          protect_mask=a.protect_mask,
@@ -87,7 +92,8 @@ def run_ctypes(a):
                       device=local, private_pages=a.private_pages,
                       protect_opclasses=_split(a.protect_opclasses), bits=a.bits or None,
                       shadow_fu_model=a.shadow_fu_model, priority_to_shadow=a.priority_to_shadow, checkpoint=a.checkpoint,
-                      issue_params={"issue_width": a.issue_width, "load_latency": a.load_latency})
+                      issue_params={"issue_width": a.issue_width, "load_latency": a.load_latency},
+                      input=a.input, executable=a.executable or None)
     t0 = time.perf_counter()
     c.run(first_trial=a.first_trial)
     dt = time.perf_counter() - t0

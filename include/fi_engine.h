@@ -173,12 +173,20 @@ typedef struct {
  * and $SHREWD_FI_JIT_CACHE) hold them: cold-start measurements and tests of
  * the background build. */
 #define FI_CFG_JIT_NO_CACHE 8192u
-/* No loop proofs in the clean translated body (fi_translate.cpp): neither
- * counted-loop hangs nor run-off loops that end in a page fault or a hang
- * (fi_trial.hip loop_outcome) -- every such trial runs to its cap or its
+/* No loop proofs: neither the clean translated body's (fi_translate.cpp:
+ * counted-loop hangs, run-off loops that end in a page fault or a hang,
+ * fi_trial.hip loop_outcome) nor the solo interpreter's dynamic ones
+ * (fi_trial.hip LoopProbe) -- every such trial runs to its cap or its
  * faulting load (A/B and parity checks; outcomes are identical: the records
  * are the same either way). */
 #define FI_CFG_NO_HANG_PROOF 16384u
+/* No overflow pages: by default a trial that needs more than private_pages
+ * takes a block of more (up to the redo pass's 16x, at least 256, in all)
+ * from a pool shared by the launch, so that it goes on at once instead of
+ * ending as FI_ESC_RESOURCE and running again after the chunk (which stays
+ * the fallback when the pool is spent) (A/B and parity checks; outcomes are
+ * identical) */
+#define FI_CFG_NO_OVERFLOW 32768u
 
 typedef struct {
     uint64_t ninst, ncycles;

@@ -237,6 +237,11 @@ struct fi_engine {
     uint64_t clk_until = 0;          // 1 + numInst of the golden run's last curTick read (0: none; DevCtx::clk_until)
     uint8_t *d_priv = nullptr;
     uint64_t *d_priv_vpn = nullptr;
+    // overflow pages (DevCtx::ov_*): ov_blocks blocks of ov_pages
+    uint8_t *d_ov = nullptr;
+    uint64_t *d_ov_vpn = nullptr;
+    uint32_t *d_ov_of = nullptr, *d_ov_next = nullptr;
+    uint32_t ov_blocks = 0, ov_pages = 0;
     VmState *d_vm = nullptr;         // [cap] per-slot SE memory map (trials that made a VM syscall)
     uint64_t brk0 = 0;               // roundUp(maxAddr, page): the process-start brk point
     // epochs: suspended lanes, survivor lists, counts, sort buffers
@@ -368,6 +373,8 @@ static void free_work(fi_engine *e) {
     dfree(e->d_save); dfree(e->d_surv[0]); dfree(e->d_surv[1]); dfree(e->d_cnt);
     dfree(e->d_eff);
     dfree(e->d_skeys); dfree(e->d_skeys2); dfree(e->d_svals); dfree(e->d_svals2); dfree(e->d_wrange); dfree(e->d_nwaves); dfree(e->d_split); dfree(e->d_dmap); dfree(e->d_priv); dfree(e->d_priv_vpn); dfree(e->d_vm);
+    dfree(e->d_ov); dfree(e->d_ov_vpn); dfree(e->d_ov_of); dfree(e->d_ov_next);
+    e->ov_blocks = e->ov_pages = 0;
     dfree(e->d_redo_idx); dfree(e->d_redo_cnt); dfree(e->d_redo_sites); dfree(e->d_redo_out);
     e->cap = 0;
 }
@@ -777,6 +784,10 @@ fi_status fi_load_checkpoint(fi_engine *e, const char *cpt_dir, const uint8_t *e
     return FI_OK;
 }
 
+// Private pages per trial of the second pass (run_chunk) and, with the
+// overflow pool, a trial's capacity in the first: 16 P, at least 256.
+static uint64_t redo_pages(uint64_t P) { return std::max<uint64_t>(P * 16ull, 256); }
+
 static fi_status ensure_work(fi_engine *e, uint64_t n) {
     if (n <= e->cap) return FI_OK;
     free_work(e);
@@ -815,6 +826,19 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_redo_sites, c * sizeof(fi_site)));
     HIPCHK(hipMalloc(&e->d_redo_out, c * sizeof(fi_outcome)));
     if (!e->h_redo_cnt) HIPCHK(hipHostMalloc(&e->h_redo_cnt, 16));
+    // overflow pool: a trial past P pages takes a block of P' - P more (P' the
+    // redo pass's page count), one block per 2048 slots (at least 64)
+    {
+        const uint64_t P = e->cfg.private_pages, P2 = redo_pages(P);
+        if (!(e->cfg.flags & FI_CFG_NO_OVERFLOW) && P2 > P) {
+            e->ov_pages = (uint32_t)(P2 - P);
+            e->ov_blocks = (uint32_t)std::max<uint64_t>(64, c / 2048);
+            HIPCHK(hipMalloc(&e->d_ov, (uint64_t)e->ov_blocks * e->ov_pages * kPage));
+            HIPCHK(hipMalloc(&e->d_ov_vpn, (uint64_t)e->ov_blocks * e->ov_pages * 8));
+            HIPCHK(hipMalloc(&e->d_ov_of, c * 4));
+            HIPCHK(hipMalloc(&e->d_ov_next, 16));
+        }
+    }
     e->cap = c;
     return FI_OK;
 }
@@ -853,6 +877,8 @@ static DevCtx base_ctx(fi_engine *e) {
     c.protect_opc = e->protect_opc;
     c.shadow_bits = e->issue_on ? e->d_shadow : nullptr;
     c.priv_frames = e->d_priv; c.priv_vpn = e->d_priv_vpn;
+    c.ov_frames = e->d_ov; c.ov_vpn = e->d_ov_vpn; c.ov_of = e->d_ov_of; c.ov_next = e->d_ov_next;
+    c.ov_blocks = e->ov_blocks; c.ov_pages = e->ov_pages;
     c.tx_sink = e->d_sink;
     c.fregs = e->d_fregs;
     c.wave_dbg = e->d_wave_dbg;
@@ -893,6 +919,7 @@ static fi_status golden_launch(fi_engine *e, uint32_t P, uint64_t rec_I, uint32_
     c.fregs = d_gfregs;
     c.in_pos = d_gfregs + 32;
     c.dmap = nullptr;
+    c.ov_blocks = 0;   // (the golden run has its own P pages, no overflow pool)
     c.record = 1;
     c.early_exit = 0;
     c.snap_start = 0;
@@ -1452,6 +1479,8 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
     c.n_slots = (uint32_t)k;
     c.save = e->d_save;
     c.priv_pages = P;
+    if (P != e->cfg.private_pages) c.ov_blocks = 0;   // the second pass has its own P' (run_chunk)
+    if (c.ov_blocks) HIPCHK(hipMemsetAsync(e->d_ov_next, 0, 4, st));
     HIPCHK(hipMemsetAsync(e->d_cnt, 0, 16 * 4, st));
     HIPCHK(hipMemsetAsync(e->d_wave_dbg, 0, k * 10 * sizeof(uint64_t), st));
     const bool pack = (e->cfg.flags & FI_CFG_PACK_RUNS) != 0;
@@ -1564,7 +1593,7 @@ static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histo
         const uint64_t nr = *e->h_redo_cnt;
         if (nr) {
             const uint64_t pool = k * P;   // page frames the pass had
-            const uint64_t P2 = std::min<uint64_t>(pool, std::max<uint64_t>(P * 16ull, 256));
+            const uint64_t P2 = std::min<uint64_t>(pool, redo_pages(P));
             const uint64_t B = std::max<uint64_t>(1, pool / P2);
             for (uint64_t d = 0; d < nr; d += B) {
                 const uint64_t b = std::min(B, nr - d);

@@ -154,6 +154,14 @@ struct DevCtx {
     // per-trial private (copy-on-write) pages: frames [slot][P][4096], vpns [P][n]
     uint8_t *priv_frames;
     uint64_t *priv_vpn;
+    // overflow pages: a trial that needs more than P takes one block of
+    // ov_pages more from a shared pool (ov_next: blocks handed out in this
+    // pass; ov_of[slot]: its block, ~0 none); ov_blocks 0 = no pool
+    uint8_t *ov_frames;              // [ov_blocks][ov_pages][4096]
+    uint64_t *ov_vpn;                // [ov_blocks][ov_pages]
+    uint32_t *ov_of;                 // [n_slots]
+    uint32_t *ov_next;
+    uint32_t ov_blocks, ov_pages;
     uint8_t *tx_sink;                // translated code: stores of lanes outside the running group land here
     uint64_t *fregs;                 // FP registers [32][n_slots] (written only by a lane's FP data-movement ops)
     // record mode: snapshot capture at numInst == k * rec_interval

@@ -247,8 +247,32 @@ struct WaveMem {
     uint32_t tab_n;
 };
 
+// Private entry i of a slot: the first P in the slot's own frames and SoA
+// vpn table, the rest in its overflow block (DevCtx::ov_*; priv_room hands
+// the block out when entry P is needed).
 __device__ __forceinline__ uint8_t *priv_frame(KCtx *c, uint64_t slot, uint32_t i) {
-    return c->priv_frames + ((slot * c->priv_pages + i) << 12);
+    if (i < c->priv_pages) return c->priv_frames + ((slot * c->priv_pages + i) << 12);
+    return c->ov_frames + (((uint64_t)c->ov_of[slot] * c->ov_pages + (i - c->priv_pages)) << 12);
+}
+__device__ __forceinline__ uint64_t &priv_ent(KCtx *c, uint64_t slot, uint32_t i) {
+    if (i < c->priv_pages) return c->priv_vpn[(uint64_t)i * c->n_slots + slot];
+    return c->ov_vpn[(uint64_t)c->ov_of[slot] * c->ov_pages + (i - c->priv_pages)];
+}
+// May the slot take private entry i (= its n_priv)?  Past P it needs its
+// overflow block, taken from the pool at entry P; none left (or no pool): no.
+__device__ __noinline__ bool priv_room_ool(KCtx *c, uint64_t slot, uint32_t i) {
+    if (!c->ov_blocks || i >= c->priv_pages + c->ov_pages) return false;
+    if (c->ov_of[slot] == 0xFFFFFFFFu) {
+        if (i != c->priv_pages) return false;
+        const uint32_t b = atomicAdd(c->ov_next, 1u);
+        if (b >= c->ov_blocks) return false;
+        c->ov_of[slot] = b;
+        atomicAdd(&c->stats[61], 1ull);   // (blocks taken: diagnostics)
+    }
+    return true;
+}
+__device__ __forceinline__ bool priv_room(KCtx *c, uint64_t slot, uint32_t i) {
+    return i < c->priv_pages || priv_room_ool(c, slot, i);
 }
 
 __device__ __forceinline__ uint64_t tlb_find(const LaneMem &m, uint64_t vpn) {
@@ -291,7 +315,7 @@ __device__ uint64_t lookup_full(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t 
     uint64_t p = 0;
     bool dec = false;
     for (uint32_t i = m.n_priv; i-- > 0;) {
-        const uint64_t e = c->priv_vpn[(uint64_t)i * c->n_slots + slot];
+        const uint64_t e = priv_ent(c, slot, i);
         if ((e & ~kTomb) == vpn) { dec = true; if (!(e & kTomb)) p = (uint64_t)priv_frame(c, slot, i) | 1; break; }
     }
     if (!dec) {
@@ -314,18 +338,18 @@ __device__ __forceinline__ const uint8_t *page_of(uint64_t p) { return (const ui
 // The private entry that decides vpn (newest first), or -1.
 __device__ int priv_decider(KCtx *c, const LaneMem &m, uint64_t slot, uint64_t vpn) {
     for (uint32_t i = m.n_priv; i-- > 0;)
-        if ((c->priv_vpn[(uint64_t)i * c->n_slots + slot] & ~kTomb) == vpn) return (int)i;
+        if ((priv_ent(c, slot, i) & ~kTomb) == vpn) return (int)i;
     return -1;
 }
 // Process::allocateMem of one page for this trial: a new private entry filled
 // from src (the zero page, or the current page for a proxy write).  nullptr if
 // the trial has no free private page (resource escape).
 __device__ uint8_t *priv_new(KCtx *c, LaneMem &m, uint64_t slot, uint64_t vpn, const uint8_t *src) {
-    if (m.n_priv >= c->priv_pages) return nullptr;
+    if (!priv_room(c, slot, m.n_priv)) return nullptr;
     uint4 *d = (uint4 *)priv_frame(c, slot, m.n_priv);
     const uint4 *q = (const uint4 *)src;
     for (int k = 0; k < 256; k++) d[k] = q[k];
-    c->priv_vpn[(uint64_t)m.n_priv * c->n_slots + slot] = vpn;
+    priv_ent(c, slot, m.n_priv) = vpn;
     m.n_priv++;
     tlb_flush(m);
     return (uint8_t *)d;
@@ -377,7 +401,7 @@ template <typename F>
 __device__ __forceinline__ void for_mapped(KCtx *c, const WaveMem &w, const LaneMem &m, uint64_t slot, uint64_t lo,
                                            uint64_t hi, F f) {
     for (uint32_t i = m.n_priv; i-- > 0;) {
-        const uint64_t e = c->priv_vpn[(uint64_t)i * c->n_slots + slot];
+        const uint64_t e = priv_ent(c, slot, i);
         if ((e & kTomb) || e < lo || e >= hi || priv_decider(c, m, slot, e) != (int)i) continue;
         if (!f(e, (int)i)) return;
     }
@@ -442,9 +466,9 @@ __device__ int vm_unmap(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, Vm
     bool full = false;
     for_mapped(c, w, m, slot, lo >> 12, hi >> 12, [&](uint64_t vpn, int d) {
         if (d >= 0) {
-            c->priv_vpn[(uint64_t)d * c->n_slots + slot] = vpn | kTomb;
-        } else if (m.n_priv < c->priv_pages) {
-            c->priv_vpn[(uint64_t)m.n_priv * c->n_slots + slot] = vpn | kTomb;
+            priv_ent(c, slot, (uint32_t)d) = vpn | kTomb;
+        } else if (priv_room(c, slot, m.n_priv)) {
+            priv_ent(c, slot, m.n_priv) = vpn | kTomb;
             m.n_priv++;
         } else {
             full = true;
@@ -1350,7 +1374,7 @@ __device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32
     const uint32_t nk = S->tab_n;
     const uint64_t smin = S->stack_min >> 12;
     for (uint32_t i = 0; i < np; i++) {   // every page the lane has written
-        const uint64_t v = uni64(c->priv_vpn[(uint64_t)i * c->n_slots + lslot]);
+        const uint64_t v = uni64(priv_ent(c, lslot, i));
         const int64_t f = tab_find(tk, nk, v);
         const uint8_t *g = f >= 0 ? c->pool + ((uint64_t)f << 12)
                                   : ((v >= smin && v <= kStackTopVpn) ? c->zero_page : nullptr);
@@ -1361,7 +1385,7 @@ __device__ bool lane_mem_equal(KCtx *c, const WaveMem &w, uint64_t lslot, uint32
         const uint64_t v = uni64(tk[e].vpn);
         const uint32_t f = uni32(tk[e].frame);
         bool priv = false;
-        for (uint32_t i = 0; i < np; i++) priv = priv || c->priv_vpn[(uint64_t)i * c->n_slots + lslot] == v;
+        for (uint32_t i = 0; i < np; i++) priv = priv || priv_ent(c, lslot, i) == v;
         if (priv) continue;
         const int64_t fj = tab_find(w.tab, w.tab_n, v);
         const uint8_t *lv = fj >= 0 ? c->pool + ((uint64_t)fj << 12)
@@ -1638,7 +1662,7 @@ __device__ __forceinline__ bool tx_hang_proof(uint64_t x, int c, uint32_t m, uin
 // Is vpn in the lane's page set?  (lookup_full without the TLB insert)
 __device__ __forceinline__ bool page_mapped(KCtx *c, const WaveMem &w, const LaneMem &m, uint64_t slot, uint64_t vpn) {
     for (uint32_t i = m.n_priv; i-- > 0;) {
-        const uint64_t e = c->priv_vpn[(uint64_t)i * c->n_slots + slot];
+        const uint64_t e = priv_ent(c, slot, i);
         if ((e & ~kTomb) == vpn) return !(e & kTomb);
     }
     return tab_find(w.tab, w.tab_n, vpn) >= 0 || (vpn >= (m.stack_min >> 12) && vpn <= kStackTopVpn);
@@ -1995,7 +2019,7 @@ struct alignas(16) SoloFastIO {
     uint32_t fbytes, dbytes, tby, ddlo;     // 16  counters in/out; text bytes; rewritten window lo
     uint32_t ddhi3, clo_o, csz, gate;       // 32  window hi + 3; code range (text offset, size); leader gate
     uint32_t lbe, lbo, reason, r_lds;       // 48  leader flag bits (even / odd pc); out: why it left; LDS of R
-    uint32_t dct_lds, dce_lds, tlb_lds, pad;// 64  LDS of the decode cache tags / entries, of LaneMem::tv0
+    uint32_t dct_lds, dce_lds, tlb_lds, lc_lds;// 64  LDS of the decode cache tags / entries, of LaneMem::tv0, of the entry cache
     uint64_t pre, tlo;                      // 80  pre-decoded text, text base
     uint64_t clo, cvpn;                     // 96  code range base; page cache (in/out)
     uint64_t cpg, npc;                      // 112 its page; out: the pc that left the text (reason 3)
@@ -2054,10 +2078,16 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_mov_b64 s[70:71], -1\n"          // page cache slot 1: empty
         "s_mov_b64 s[72:73], 0\n"
         // the entry cache in VGPR lanes: v24 tag (po) / v25..v27 entry words
-        // y z w, lane (po >> 1) & 63; empty at every call (all 64 lanes)
+        // y z w, lane (po >> 1) & 63; kept in LDS between calls (lc_lds: one
+        // 16-byte record per lane, invalidated there by every code-changing
+        // store), so a loop that hands back stays warm
+        "v_readfirstlane_b32 s62, v19\n"
         "s_mov_b64 s[74:75], exec\n"
         "s_mov_b64 exec, -1\n"
-        "v_mov_b32 v24, -1\n"
+        "v_mbcnt_lo_u32_b32 v30, -1, 0\n"
+        "v_mbcnt_hi_u32_b32 v30, -1, v30\n"
+        "v_lshl_add_u32 v30, v30, 4, s62\n"
+        "ds_read_b128 v[24:27], v30\n"
         "s_mov_b64 exec, s[74:75]\n"
         "ds_read2_b64 v[64:67], v15 offset0:0 offset1:1\n"
         "ds_read2_b64 v[68:71], v15 offset0:2 offset1:3\n"
@@ -2843,6 +2873,14 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "ds_write2_b64 v15, v[116:117], v[118:119] offset0:26 offset1:27\n"
         "ds_write2_b64 v15, v[120:121], v[122:123] offset0:28 offset1:29\n"
         "ds_write2_b64 v15, v[124:125], v[126:127] offset0:30 offset1:31\n"
+        "v_readfirstlane_b32 s62, v19\n"   // the entry cache back to LDS (all lanes)
+        "s_mov_b64 s[74:75], exec\n"
+        "s_mov_b64 exec, -1\n"
+        "v_mbcnt_lo_u32_b32 v30, -1, 0\n"
+        "v_mbcnt_hi_u32_b32 v30, -1, v30\n"
+        "v_lshl_add_u32 v30, v30, 4, s62\n"
+        "ds_write_b128 v30, v[24:27]\n"
+        "s_mov_b64 exec, s[74:75]\n"
         "s_waitcnt vmcnt(0) lgkmcnt(0)\n"
         "s_mov_b32 m0, s4\n"
         :
@@ -2871,12 +2909,13 @@ __device__ __forceinline__ uint64_t r64(const lds_u64 *R, uint32_t r) { return u
 
 template <bool kOdd>
 __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds_u32 *DCT, lds_pre4 *DCE,
-                                          lds_pio *io) {
+                                          lds_u32 *LC, lds_pio *io) {
     CX = (KCtx *)(uintptr_t)uni64((uint64_t)(uintptr_t)CX);
     R = (lds_u64 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)R);
     mp = (lds_mem *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)mp);
     DCT = (lds_u32 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)DCT);
     DCE = (lds_pre4 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)DCE);
+    LC = (lds_u32 *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)LC);
     io = (lds_pio *)(uintptr_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)io);
     LaneMem &m = *(LaneMem *)mp;   // lookup_full / fetch_lane / mark_dirty_solo take it by reference
     const uint64_t slot = uni64(io->slot);
@@ -2957,6 +2996,7 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
 #endif
                 F->r_lds = (uint32_t)(uintptr_t)R; F->dct_lds = (uint32_t)(uintptr_t)DCT;
                 F->dce_lds = (uint32_t)(uintptr_t)DCE; F->tlb_lds = (uint32_t)(uintptr_t)&mp->tv0;
+                F->lc_lds = (uint32_t)(uintptr_t)LC;
                 F->pre = (uint64_t)(uintptr_t)CX->pre; F->tlo = tlo; F->clo = clo; F->cvpn = cvpn; F->cpg = cpg;
                 solo_fast_run(F);
                 n_fast++;
@@ -3076,6 +3116,7 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
                         for (uint32_t q = (o0 > 3 ? o0 - 3 : 0); q < o1; q++) {   // decode-cache entries over them
                             const uint32_t i = (q >> 1) & (kSoloDC - 1);
                             if (DCT[i] == q) DCT[i] = 0xFFFFFFFFu;
+                            if (LC[4 * i] == q) LC[4 * i] = 0xFFFFFFFFu;   // (solo_fast_run's entry cache)
                         }
                     }
                     if (al) {
@@ -3320,6 +3361,7 @@ __device__ __forceinline__ void trial_body() {
     m.resv = m.lock = kNone;
     m.vm = false;
     m.nmiss = 0;
+    if (CX->ov_blocks && live && !resume) CX->ov_of[slot] = 0xFFFFFFFFu;   // no overflow block yet
     // the solo kernel's LDS copy of the slot's rewritten-code map
     __shared__ uint32_t DMAP[kNL == 1 ? kDmapWords : 1];
     m.dl = (kNL == 1 && CX->dmap) ? DMAP : nullptr;
@@ -3382,9 +3424,14 @@ __device__ __forceinline__ void trial_body() {
     constexpr uint32_t kDC = kNL == 1 ? 64u : 1u;
     __shared__ uint32_t DCT[kDC];   // tag: pc - text_lo (0xFFFFFFFF empty)
     __shared__ alignas(16) Pre4 DCE[kDC];
+    // ... and the entry cache of solo_fast_run between its calls: per lane of
+    // its VGPR cache a 16-byte record {tag = text offset, y, z, w}
+    __shared__ alignas(16) uint32_t LC[kNL == 1 ? 4 * kSoloDC : 4];
     if constexpr (kNL == 1) {
 #pragma unroll 8
         for (uint32_t k = 0; k < kDC; k++) DCT[k] = 0xFFFFFFFFu;
+#pragma unroll 8
+        for (uint32_t k = 0; k < kSoloDC; k++) LC[4 * k] = 0xFFFFFFFFu;
     }
     // solo only: the dynamic loop proof's state (LoopProbe)
     __shared__ alignas(8) uint32_t LPB[kNL == 1 ? (sizeof(LoopProbe) + 3) / 4 : 2];
@@ -3419,6 +3466,7 @@ __device__ __forceinline__ void trial_body() {
                 for (uint64_t q_ = (a_ > 3 ? a_ - 3 : 0); q_ < e_; q_++) {                          \
                     const uint32_t i_ = (uint32_t)(q_ >> 1) & (kDC - 1);                            \
                     if (DCT[i_] == (uint32_t)(q_ - CX->text_lo)) DCT[i_] = 0xFFFFFFFFu;             \
+                    if (LC[4 * i_] == (uint32_t)(q_ - CX->text_lo)) LC[4 * i_] = 0xFFFFFFFFu;       \
                 }                                                                                   \
         }                                                                                           \
     } while (0)
@@ -3467,24 +3515,25 @@ __device__ __forceinline__ void trial_body() {
             break;
         }
         // ---- A. materialise requested pages, whole wave cooperating
-        const uint64_t want = wballot<kNL>(!L.done && m.req_vpn != kNone);
-        if (want) {
+        // (a lane past its P pages takes its overflow block first: priv_room)
+        const bool room = !L.done && m.req_vpn != kNone && priv_room(CX, slot, m.n_priv);
+        const uint64_t want = wballot<kNL>(room);
+        if (wballot<kNL>(!L.done && m.req_vpn != kNone)) {
             uint64_t wl = want;
             while (wl) {
                 const int l = __ffsll((unsigned long long)wl) - 1;
                 wl &= wl - 1;
                 const uint32_t np = (uint32_t)rdl32<kNL>((uint32_t)m.n_priv, l);
-                if (np >= CX->priv_pages) continue;
                 const uint64_t lslot = rdl64<kNL>(slot, l);
                 const uint4 *src = (const uint4 *)rdl64<kNL>((uint64_t)m.req_src, l);
                 page_copy<kNL>((uint4 *)priv_frame(CX, lslot, np), src, lane);
             }
             __syncthreads();
             if (!L.done && m.req_vpn != kNone) {
-                if (m.n_priv >= CX->priv_pages) {
+                if (!room) {
                     finish(L, FI_ESCAPE, FI_ESC_RESOURCE, 0, (uint32_t)L.pc);
                 } else {
-                    CX->priv_vpn[(uint64_t)m.n_priv * CX->n_slots + slot] = m.req_vpn;
+                    priv_ent(CX, slot, m.n_priv) = m.req_vpn;
                     m.n_priv++;
                     pages_made++;
                 }
@@ -3849,6 +3898,8 @@ __device__ __forceinline__ void trial_body() {
                         for (uint32_t k = 0; k < kDC; k++) {   // decode-cache entries whose bytes were rewritten
                             const uint32_t tg = DCT[k];
                             if (tg != 0xFFFFFFFFu && tg + 4 > cslo && tg < cshi) DCT[k] = 0xFFFFFFFFu;
+                            const uint32_t tl = LC[4 * k];
+                            if (tl != 0xFFFFFFFFu && tl + 4 > cslo && tl < cshi) LC[4 * k] = 0xFFFFFFFFu;
                         }
                     }
                     L.ninst += st; L.ncyc += st + xt; L.fetch_b += fb; L.data_b += db; L.pc = spc;
@@ -4012,7 +4063,7 @@ __device__ __forceinline__ void trial_body() {
                     pio->spc = lpc; pio->slot = slot; pio->tab = w.tab; pio->tab_n = w.tab_n;
                     pio->budget = budget; pio->watch = L.watch;
                     pio->tx_gate = tx_skip_until > n_iter ? tx_skip_until - n_iter : 0u;
-                    solo_pre_run<kOdd>(CX, (lds_u64 *)R, (lds_mem *)&m, (lds_u32 *)DCT, (lds_pre4 *)DCE,
+                    solo_pre_run<kOdd>(CX, (lds_u64 *)R, (lds_mem *)&m, (lds_u32 *)DCT, (lds_pre4 *)DCE, (lds_u32 *)LC,
                                        (lds_pio *)pio);
                     const uint32_t steps = uni32(pio->steps);
 #ifdef FI_PROF
@@ -4770,10 +4821,12 @@ __device__ __forceinline__ void trial_body() {
             const bool chg = do_syscall<kNL>(CX, w, Ls, ms, slot, R, lane);
             L = Ls;
             m = ms;
-            if (chg) {
-                if constexpr (kNL == 1) {
-                    for (uint32_t k = 0; k < kDC; k++) DCT[k] = 0xFFFFFFFFu;   // the code mapping changed
-                }
+            (void)chg;
+            if constexpr (kNL == 1) {
+                // the code mapping changed, or a proxy write (read, clock_gettime,
+                // uname, ...) may have stored into cached code: forget the decodes
+                for (uint32_t k = 0; k < kDC; k++) DCT[k] = 0xFFFFFFFFu;
+                for (uint32_t k = 0; k < kSoloDC; k++) LC[4 * k] = 0xFFFFFFFFu;
             }
             break;
         }

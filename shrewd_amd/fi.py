@@ -110,6 +110,7 @@ CFG_NO_REDO = 2048
 CFG_NO_ODD_KERNEL = 4096
 CFG_JIT_NO_CACHE = 8192
 CFG_NO_HANG_PROOF = 16384
+CFG_NO_OVERFLOW = 32768
 
 
 class GoldenInfo(C.Structure):

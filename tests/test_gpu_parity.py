@@ -783,23 +783,39 @@ def test_sdc_early_exit(engine_factory, oracle_mod):
 @pytest.mark.parametrize("name", ["qsort", "intmix"])
 def test_resource_redo(engine_factory, oracle_mod, name):
     """Trials that run out of copy-on-write pages (FI_ESC_RESOURCE, an engine
-    capacity limit) run again with more pages before the histogram: with one
-    private page per trial the outcomes equal the default engine's and the
-    oracle's, while the same engine without the second pass escapes."""
+    capacity limit) either take a block of overflow pages from the launch's
+    pool and go on, or -- the pool spent, or off (FI_CFG_NO_OVERFLOW) -- run
+    again with more pages before the histogram: with one private page per
+    trial the outcomes equal the default engine's and the oracle's either
+    way, while the same engine with neither escapes."""
+    from shrewd_amd.fi import CFG_NO_OVERFLOW, CFG_NO_REDO
     n = 3000
-    tight = engine_factory(name, private_pages=1, max_trials_per_launch=n)
-    noredo = engine_factory(name, private_pages=1, flags=2048, max_trials_per_launch=n)   # FI_CFG_NO_REDO
-    for e in (tight, noredo):
+    tight = engine_factory(name, private_pages=1, max_trials_per_launch=n)                    # overflow + redo
+    redo = engine_factory(name, private_pages=1, flags=CFG_NO_OVERFLOW, max_trials_per_launch=n)
+    ovf = engine_factory(name, private_pages=1, flags=CFG_NO_REDO, max_trials_per_launch=n)
+    neither = engine_factory(name, private_pages=1, flags=CFG_NO_REDO | CFG_NO_OVERFLOW, max_trials_per_launch=n)
+    for e in (tight, redo, ovf, neither):
         e.set_campaign(0x5EED0BED, REGS | PC | MEM, 1)
         e.set_protect(0)
     sites = tight.sample(0, n)
-    b, hb = noredo.run_sites(sites)
+    b, hb = neither.run_sites(sites)
     esc = (b["cls"] == 5) & (b["sub"] == 5)
     assert esc.sum() > 0
+    r, hr = redo.run_sites(sites)
+    assert int(redo.debug_stats()[30]) == int(esc.sum()) and int(redo.debug_stats()[61]) == 0
+    v, hv = ovf.run_sites(sites)
+    blocks = int(ovf.debug_stats()[61])
+    assert blocks > 0
+    # the pool (64 blocks) runs dry at P = 1: the rest still escape without the redo pass
+    assert int(((v["cls"] == 5) & (v["sub"] == 5)).sum()) == int(esc.sum()) - blocks
     a, ha = tight.run_sites(sites)
-    assert int(tight.debug_stats()[30]) == int(esc.sum())
-    assert not ((a["cls"] == 5) & (a["sub"] == 5)).any()
-    assert int(ha["escape_sub"][5]) == 0 and int(ha["trials"]) == n
+    assert int(tight.debug_stats()[30]) == int(esc.sum()) - int(tight.debug_stats()[61])
+    for x, h in ((a, ha), (r, hr)):
+        assert not ((x["cls"] == 5) & (x["sub"] == 5)).any()
+        assert int(h["escape_sub"][5]) == 0 and int(h["trials"]) == n
+    assert np.array_equal(a, r)
+    ok = ~((v["cls"] == 5) & (v["sub"] == 5))
+    assert np.array_equal(a[ok], v[ok])
     compare(a, oracle_for(oracle_mod, name).run_trials(sites, protect_mask=0), sites)
     assert np.array_equal(a[~esc], b[~esc])
 

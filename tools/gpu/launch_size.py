@@ -47,7 +47,7 @@ for size in SIZES:
     rec = {"workload": name, "trials": N, "per_launch": size, "private_pages": PP, "wall_s": round(wall, 4),
            "trials_per_s": round(N / wall), "device_insts": int(h["device_insts"]),
            "dispatch_ms_by_kind": {k: [round(sum(v), 2), len(v)] for k, v in by.items()},
-           "epochs_last_chunk": ep[:4], "redo_last_chunk": int(st[30]), "stats_0_24": st[:32].tolist(),
+           "epochs_last_chunk": ep[:4], "redo_last_chunk": int(st[30]), "stats_0_24": st[:64].tolist(),
            "same_as_first": None if ref is None else int((out != ref).sum())}
     if len(w):
         t0w = w[:, 4].min()
