@@ -76,6 +76,13 @@ typedef int32_t fi_status;
 #define FI_CRASH_SC_LINE 11       /* abort  SC across a cache line  cpu/simple/atomic.cc:482 assert(curr_frag_id == 0) */
 #define FI_CRASH_SE_PANIC 12      /* panic  in an SE syscall handler (null ProxyPtr, MemState::isUnmapped) */
 #define FI_CRASH_M5_PANIC 13      /* panic  in an M5 pseudo-op (m5_panic, unknown initparam key) sim/pseudo_inst.* */
+/* FI_HANG sub-codes */
+#define FI_HANG_INSTS 1           /* the max-insts cap (hang_factor_x16 x golden numInst) */
+#define FI_HANG_QUIESCE 2         /* m5_quiesce: the only context suspends for good (sim/pseudo_inst.cc:117) */
+/* FI_MASKED / FI_SDC sub-codes: how the run ended (the simulate() exit cause) */
+#define FI_END_EXIT 0             /* exit / exit_group: "exiting with last active thread context" */
+#define FI_END_M5_EXIT 1          /* m5_exit(0): "m5_exit instruction encountered" (sim/pseudo_inst.cc:178) */
+#define FI_END_M5_FAIL 2          /* m5_fail(0, code): "m5_fail instruction encountered" (:198); exit_code = code */
 /* FI_ESCAPE sub-codes */
 #define FI_ESC_INST 1
 #define FI_ESC_SYSCALL 2

@@ -272,6 +272,7 @@ typedef struct {
     /* diagnostics (or_debug_trace): committed pcs, store addresses into the text */
     u64 *dbg_pc, dbg_pc_n, dbg_pc_cap, *dbg_wr, dbg_wr_n, dbg_wr_cap;
     int dbg_raw;   /* or_debug_trace_raw: pc | instruction word << 32 */
+    int m5x, m5code;   /* an M5 op that ends the run after it commits: 1 m5_exit, 2 m5_fail, 3 quiesce */
     const or_campaign_t *c;
 } mach_t;
 
@@ -2253,10 +2254,32 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
         }
         case 0x51: return F_BREAK;      /* debugbreak: debug::breakpoint() -> SIGTRAP (base/debug.cc:64-70) */
         case 0x54: return F_M5PANIC;    /* M5OP_PANIC */
-        /* simulator control or host files: quiesce*, exit, fail, checkpoint,
-         * writefile, switchcpu, addsymbol, workbegin / workend, togglesync,
-         * workload event, hypercall */
-        case 0x01: case 0x02: case 0x03: case 0x04: case 0x21: case 0x22: case 0x43: case 0x4f: case 0x52:
+        /* quiesce: ThreadContext::quiesce suspends the only context
+         * (thread_context.cc:167, system.cc:145-151; AtomicSimpleCPU::
+         * suspendContext deschedules its tick, atomic.cc:246-269) after this
+         * instruction commits, and nothing wakes it: the simulation runs to
+         * its tick limit ("simulate() limit reached") -- a hang */
+        case 0x01: m->m5x = 3; break;
+        /* m5_exit(delay) / m5_fail(delay, code): exitSimLoop at curTick +
+         * delay ns (pseudo_inst.cc:178-204); the stdlib run script's default
+         * handler for both ends the simulation (simulate/exit_handler.py:551-
+         * 557).  delay 0: the exit event fires after this instruction's tick
+         * (Sim_Exit_Pri after CPU_Tick_Pri, sim/eventq.hh:207,237); a delayed
+         * exit lets more ticks run first -- not modelled (escape) */
+        case 0x21: case 0x22:
+            if (m->watch == 10 || (imm == 0x22 && m->watch == 11)) return 100;
+            if (m->x[10] != 0) return F_ESCAPE;
+            m->m5x = imm == 0x21 ? 1 : 2;
+            m->m5code = imm == 0x22 ? (int)(m->x[11] & 0xff) : 0;
+            break;
+        /* m5_checkpoint: the stdlib default saves a checkpoint and continues;
+         * switchcpu: switch_generator does nothing for a processor that is not
+         * switchable (BaseCPUProcessor) and continues (exit_event_generators.
+         * py:72-83, 100-114): no architectural effect, result 0 */
+        case 0x43: case 0x52: break;
+        /* simulator control or host files: quiesce for a time, writefile,
+         * addsymbol, workbegin / workend, togglesync, workload event, hypercall */
+        case 0x02: case 0x03: case 0x04: case 0x4f:
         case 0x53: case 0x5a: case 0x5b: case 0x62: case 0x70: case 0x71:
             return F_ESCAPE;
         /* arm (Workload stats), wakeCPU (the only context is active), loadsymbol
@@ -2706,6 +2729,18 @@ static void tick(mach_t *m, u64 cap) {
             invoke_fault(m, f, fva, &d);
         } else {
             m->pc = m->npc;
+        }
+    }
+    if (m->m5x && !m->done) {   /* the M5 op that ends the run has committed */
+        if (m->m5x == 3) {
+            finish(m, OR_HANG, OR_HANG_QUIESCE, 0);
+        } else {
+            const or_campaign_t *c = m->c;
+            int same = c->have_golden && m->m5code == (int)c->golden.exit_code &&
+                       m->out.len == c->gout.len && m->err.len == c->gerr.len &&
+                       (m->out.len == 0 || !memcmp(m->out.buf, c->gout.buf, m->out.len)) &&
+                       (m->err.len == 0 || !memcmp(m->err.buf, c->gerr.buf, m->err.len));
+            finish(m, same ? OR_MASKED : OR_SDC, m->m5x == 1 ? OR_END_M5_EXIT : OR_END_M5_FAIL, m->m5code);
         }
     }
 }

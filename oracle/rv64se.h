@@ -50,7 +50,12 @@ enum {
     OR_ESC_RESOURCE = 5,        /* engine resource limit (private pages) -- device only */
     OR_ESC_UNDEF = 6            /* gem5's own behaviour is undefined (GEM5_UNREACHABLE reached) */
 };
-enum { OR_HANG_INSTS = 1 };
+enum { OR_HANG_INSTS = 1,         /* the max-insts cap (scheduleInstStop, cpu/base.cc:764-770) */
+       OR_HANG_QUIESCE = 2 };      /* m5_quiesce: the only context suspends for good (thread_context.cc:167) */
+/* sub-codes of MASKED / SDC: how the simulation ended (the exit event's cause) */
+enum { OR_END_EXIT = 0,            /* exit / exit_group: "exiting with last active thread context" */
+       OR_END_M5_EXIT = 1,         /* m5_exit: "m5_exit instruction encountered" (pseudo_inst.cc:178) */
+       OR_END_M5_FAIL = 2 };       /* m5_fail: "m5_fail instruction encountered" (pseudo_inst.cc:198) */
 
 /* structure ids for fault sites */
 enum { OR_T_PC = 32, OR_T_MEM = 33, OR_T_RESULT = 34 };

@@ -194,7 +194,7 @@ struct fi_engine {
     // golden
     bool have_golden = false;
     fi_golden_info golden{};
-    uint32_t gdetail = 0;
+    uint32_t gdetail = 0, gsub = 0;
     std::vector<uint8_t> gout, gerr;
     uint8_t *d_gout = nullptr, *d_gerr = nullptr;
 
@@ -870,6 +870,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.gout = e->d_gout; c.gerr = e->d_gerr; c.gout_len = e->gout.size(); c.gerr_len = e->gerr.size();
     c.gexit = e->golden.exit_code;
     c.gdetail = e->gdetail;
+    c.gsub = e->gsub;
     c.gninst = e->golden.ninst;
     c.priv_pages = e->cfg.private_pages;
     c.hang_cap = e->golden.ninst * e->cfg.hang_factor_x16 / 16 + 1000;
@@ -1056,6 +1057,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     e->golden.fetch_bytes = stats[0];
     e->golden.data_bytes = stats[1];
     e->gdetail = o.detail;
+    e->gsub = o.sub;
     e->golden_fp = stats[22] != 0;
     e->clk_until = stats[52];
 

@@ -141,6 +141,7 @@ struct DevCtx {
     uint8_t *rec_out, *rec_err;
     uint64_t rec_cap;
     uint32_t gexit, gdetail;         // golden exit code and final pc (low 32 bits)
+    uint32_t gsub, gpad_;            // golden end sub-code: FI_END_EXIT / FI_END_M5_EXIT / FI_END_M5_FAIL
     uint64_t gninst;                 // golden numInst at exit
     uint32_t priv_pages;             // P
     uint32_t snap_start;             // 1 = a wave starts at the snapshot before its earliest inject time

@@ -250,13 +250,19 @@ struct WaveMem {
 // Private entry i of a slot: the first P in the slot's own frames and SoA
 // vpn table, the rest in its overflow block (DevCtx::ov_*; priv_room hands
 // the block out when entry P is needed).
+__device__ __noinline__ uint8_t *ov_frame(KCtx *c, uint64_t slot, uint32_t i) {
+    return c->ov_frames + (((uint64_t)c->ov_of[slot] * c->ov_pages + (i - c->priv_pages)) << 12);
+}
+__device__ __noinline__ uint64_t *ov_ent(KCtx *c, uint64_t slot, uint32_t i) {
+    return c->ov_vpn + (uint64_t)c->ov_of[slot] * c->ov_pages + (i - c->priv_pages);
+}
 __device__ __forceinline__ uint8_t *priv_frame(KCtx *c, uint64_t slot, uint32_t i) {
     if (i < c->priv_pages) return c->priv_frames + ((slot * c->priv_pages + i) << 12);
-    return c->ov_frames + (((uint64_t)c->ov_of[slot] * c->ov_pages + (i - c->priv_pages)) << 12);
+    return ov_frame(c, slot, i);   // (rare: out of line)
 }
 __device__ __forceinline__ uint64_t &priv_ent(KCtx *c, uint64_t slot, uint32_t i) {
     if (i < c->priv_pages) return c->priv_vpn[(uint64_t)i * c->n_slots + slot];
-    return c->ov_vpn[(uint64_t)c->ov_of[slot] * c->ov_pages + (i - c->priv_pages)];
+    return *ov_ent(c, slot, i);
 }
 // May the slot take private entry i (= its n_priv)?  Past P it needs its
 // overflow block, taken from the pool at entry P; none left (or no pool): no.
@@ -1846,10 +1852,10 @@ constexpr uint32_t kLpLoud = 0xFFFFFFFEu;                // a store that changed
 __device__ __forceinline__ bool m5_no_effect(uint32_t fn) {
     switch (fn) {
     case 0x07: case 0x23: case 0x30: case 0x51: case 0x54:
-    case 0x01: case 0x02: case 0x03: case 0x04: case 0x21: case 0x22: case 0x43: case 0x4f: case 0x52:
+    case 0x01: case 0x02: case 0x03: case 0x04: case 0x21: case 0x22: case 0x4f:
     case 0x53: case 0x5a: case 0x5b: case 0x62: case 0x70: case 0x71:
         return false;
-    default: return true;
+    default: return true;   // (checkpoint 0x43 and switchcpu 0x52 included: they continue)
     }
 }
 
@@ -1966,6 +1972,57 @@ __device__ __noinline__ bool lp_prove(const lds_lp *P, const uint64_t *xe, const
     return true;
 }
 
+// The probe's bookkeeping, out of line (the trial loop's registers stay
+// free): a failed probe backs off; a window starts from the registers now.
+__device__ __noinline__ void lp_fail(lds_lp *P, KCtx *c) {
+    P->on = 0; P->cnt = 0;
+    P->at = P->at < (1u << 30) ? 2 * P->at : P->at;
+    atomicAdd(&c->stats[60], 1ull);
+}
+__device__ __noinline__ void lp_window(lds_lp *P, KCtx *c, const lds_u64 *R, uint64_t slot, uint64_t pc, bool fp) {
+    if (++P->tries > 4) { lp_fail(P, c); return; }
+    P->n = 0; P->pc0 = pc; P->fp0 = fp ? 1u : 0u;
+    for (int r = 0; r < 32; r++) {
+        P->r0[r] = R[r];
+        P->f0[r] = fp ? c->fregs[(uint64_t)r * c->n_slots + slot] : 0ULL;
+    }
+}
+// `n` more interpreted instructions; a probe starts once they reach P->at
+// (eligible: injected, no watched register, live).
+__device__ __noinline__ void lp_count(lds_lp *P, KCtx *c, const lds_u64 *R, uint64_t slot, uint64_t pc, bool fp,
+                                      bool eligible, uint32_t n) {
+    P->cnt += n;
+    if (P->cnt >= P->at && eligible && !c->record && c->hang_proof) {
+        P->on = 1; P->tries = 0;
+        lp_window(P, c, R, slot, pc, fp);
+    }
+}
+// One committed instruction of a probe's pass (the general path; pc = the
+// next one); at the pass's start pc again, the proof.  1 = a proved hang.
+__device__ __noinline__ uint32_t lp_commit(lds_lp *P, KCtx *c, const lds_u64 *R, uint64_t slot, uint64_t pc, bool fp,
+                                           uint32_t op, uint32_t rd, uint32_t rs1, uint32_t rs2, uint32_t fl, int32_t imm,
+                                           bool silent) {
+    uint32_t en = lp_entry(op, rd, rs1, rs2, fl, imm, silent);
+    if (op == OP_m5op && m5_no_effect((uint32_t)imm) && P->n + 1 < FI_LP_WINDOW) {   // a0 = 0, a1 = 0
+        P->e[P->n++] = kLpNone | kLpNone << 7 | kLpNone << 14 | 10u << 21 | kLpConst << 28;
+        en = kLpNone | kLpNone << 7 | kLpNone << 14 | 11u << 21 | kLpConst << 28;
+    }
+    if (en == kLpBad) { lp_fail(P, c); return 0; }
+    if (en == kLpLoud || P->n >= FI_LP_WINDOW) {   // memory changed, or the pass is too long: again from here
+        lp_window(P, c, R, slot, pc, fp);
+        return 0;
+    }
+    P->e[P->n++] = en;
+    if (pc != P->pc0) return 0;
+    if (lp_prove(P, (const uint64_t *)R, c->fregs + slot, c->n_slots, fp)) {
+        P->on = 0;
+        atomicAdd(&c->stats[59], 1ull);
+        return 1;
+    }
+    lp_fail(P, c);
+    return 0;
+}
+
 // ---- solo pre-decoded run, out of line: the fast path of trial_body<1>
 // (one trial, every value uniform) with its own register allocation.  Same
 // rules as the 64-lane fast path below: pre-decoded micro-ops from pc until
@@ -1985,6 +2042,7 @@ struct SoloPreIO {
     uint32_t budget;       // in: instructions at most
     uint32_t tx_gate;      // in: leaders stop the run once steps >= tx_gate (translated build)
     int32_t watch;         // in/out: watched flipped register (-1 none)
+    uint32_t fps;          // in/out: FP state: the file exists (bit 0) | fflags << 8 | frm << 16
     uint32_t steps, xticks, fbytes, dbytes;   // out
 #ifdef FI_PROF
     uint64_t prof[4];      // out: s_memtime cycles per phase (diagnostic build)
@@ -1992,6 +2050,98 @@ struct SoloPreIO {
 };
 typedef __attribute__((address_space(3))) SoloPreIO lds_pio;
 constexpr uint32_t kSoloDC = 64;   // decode-cache entries (power of two)
+
+// The F/D/Zfh ops solo_pre_run executes itself (solo_fp_op) instead of
+// leaving them to the general path: data movement, sign injection, class,
+// and the arithmetic of fp_exec.
+__device__ __forceinline__ bool solo_fp_ok(uint32_t op) {
+    return (op >= OP_flh && op <= OP_fclass_h) || (op >= OP_fadd && op <= OP_fcvt_f2f) || op == OP_fli ||
+           op == OP_fround || op == OP_fcvtmod;
+}
+// One such op, exactly as the general path executes it (its OP_f* cases and
+// the FP-state commit): 0 = not here (a fault, a page to copy, a store into
+// the code range, an illegal encoding: the general path takes it, nothing
+// done), 1 = committed, 2 = committed with *v for x[rd].  *msz: data bytes.
+__device__ __noinline__ uint32_t solo_fp_op(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, const lds_u64 *R,
+                                            lds_pio *io, uint32_t q1, uint32_t q2, uint64_t &v, uint32_t &msz) {
+    const uint32_t op = q1 & 0xFF, rd = (q1 >> 8) & 0xFF, rs1 = (q1 >> 16) & 0xFF, rs2 = q1 >> 24;
+    const int64_t imm = (int32_t)q2;
+    uint32_t fps = io->fps;
+    const bool fp = fps & 1;
+    uint64_t *const F = c->fregs + slot;
+    const uint64_t st = c->n_slots;
+#define SFR(r) (fp ? F[(uint64_t)(r) * st] : 0ULL)
+    uint64_t fval = 0;
+    uint32_t fbox = 0, fpst = 0, ret = 1;
+    msz = 0;
+    switch (op) {
+    case OP_flh: case OP_flw: case OP_fld: case OP_c_fld: case OP_c_fldsp: {
+        msz = op == OP_flh ? 2 : op == OP_flw ? 4 : 8;
+        uint64_t t = 0, fva = 0;
+        if (mem_access(c, w, m, slot, R[rs1] + imm, msz, false, t, fva, 0) != F_NONE) return 0;
+        fval = msz == 2 ? (0xFFFFFFFFFFFF0000ULL | t) : msz == 4 ? (0xFFFFFFFF00000000ULL | t) : t;
+        fbox = 1;
+        break;
+    }
+    case OP_fsh: case OP_fsw: case OP_fsd: case OP_c_fsd: case OP_c_fsdsp: {
+        msz = op == OP_fsh ? 2 : op == OP_fsw ? 4 : 8;
+        const uint64_t ea = R[rs1] + imm;
+        if (ea < c->code_hi && ea + msz > c->code_lo) return 0;   // rewrites code: the general path marks it
+        const uint64_t p = lookup(c, w, m, slot, ea >> 12);
+        if (!(p & 1) || (ea & 4095) + msz > 4096) return 0;       // a copy-on-write or a page crossing first
+        uint64_t t = SFR(rs2), fva = 0;
+        if (mem_access(c, w, m, slot, ea, msz, true, t, fva, 0) != F_NONE) return 0;
+        break;
+    }
+    case OP_fmv_x_w: v = sx32(SFR(rs1)); ret = 2; break;
+    case OP_fmv_x_d: v = SFR(rs1); ret = 2; break;
+    case OP_fmv_x_h: v = (uint64_t)sext64(SFR(rs1) & 0xFFFF, 16); ret = 2; break;
+    case OP_fmv_w_x: fval = 0xFFFFFFFF00000000ULL | (R[rs1] & 0xFFFFFFFFULL); fbox = 1; break;
+    case OP_fmv_d_x: fval = R[rs1]; fbox = 1; break;
+    case OP_fmv_h_x: fval = 0xFFFFFFFFFFFF0000ULL | (R[rs1] & 0xFFFF); fbox = 1; break;
+    case OP_fsgnj_s: case OP_fsgnjn_s: case OP_fsgnjx_s: {
+        const uint64_t x = fp_unbox32(SFR(rs1)), y = fp_unbox32(SFR(rs2));
+        const uint64_t sg = op == OP_fsgnj_s ? y : op == OP_fsgnjn_s ? ~y : (x ^ y);
+        fval = 0xFFFFFFFF00000000ULL | (x & 0x7FFFFFFFULL) | (sg & 0x80000000ULL); fbox = 1;
+        break;
+    }
+    case OP_fsgnj_d: case OP_fsgnjn_d: case OP_fsgnjx_d: {
+        const uint64_t x = SFR(rs1), y = SFR(rs2);
+        const uint64_t sg = op == OP_fsgnj_d ? y : op == OP_fsgnjn_d ? ~y : (x ^ y);
+        fval = (x & 0x7FFFFFFFFFFFFFFFULL) | (sg & 0x8000000000000000ULL); fbox = 1;
+        break;
+    }
+    case OP_fsgnj_h: case OP_fsgnjn_h: case OP_fsgnjx_h: {
+        const uint64_t x = fp_unbox16(SFR(rs1)), y = fp_unbox16(SFR(rs2));
+        const uint64_t sg = op == OP_fsgnj_h ? y : op == OP_fsgnjn_h ? ~y : (x ^ y);
+        fval = 0xFFFFFFFFFFFF0000ULL | (x & 0x7FFF) | (sg & 0x8000); fbox = 1;
+        break;
+    }
+    case OP_fclass_s: v = fp_classify(fp_unbox32(SFR(rs1)), 8, 23); ret = 2; break;
+    case OP_fclass_d: v = fp_classify(SFR(rs1), 11, 52); ret = 2; break;
+    case OP_fclass_h: v = fp_classify(fp_unbox16(SFR(rs1)), 5, 10); ret = 2; break;
+    default: {   // fadd .. fcvt_f2f, fli, fround, fcvtmod
+        const uint32_t ui = (uint32_t)imm;
+        const FpRes fr = fp_exec(op, ui, rs2, SFR(rs1), SFR(rs2), SFR((ui >> 8) & 31), R[rs1], (fps >> 16) & 7);
+        if (fr.kind == 2) return 0;   // IllegalInst: the general path's crash
+        fpst = 0x100u | fr.fl;
+        if (fr.kind == 1) { v = fr.v; ret = 2; }
+        else { fval = fr.v; fbox = 1; }
+        break;
+    }
+    }
+#undef SFR
+    if (fbox || fpst) {   // FP state written: the file exists from its first write on
+        if (!fp) {
+            for (int r = 0; r < 32; r++) F[(uint64_t)r * st] = 0;
+            fps |= 1;
+        }
+        if (fbox) F[(uint64_t)rd * st] = fval;
+        if (fpst & 0x100u) fps |= (fpst & 0x1F) << 8;   // FFLAGS_EXE: accumulate
+        io->fps = fps;
+    }
+    return ret;
+}
 
 // ---- the solo interpreter's inner loop in CDNA4 assembly (solo_fast_run).
 // The C++ loop of solo_pre_run costs ~140 machine instructions per guest
@@ -3047,7 +3197,7 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
             const uint32_t fl = (q3 >> 8) & 0xFF, kind = (q3 >> 16) & 63;
             // (an invalid entry has kind K_SLOW too: fi_predecode_kernel leaves aux 0,
             // the entries past the text are zero, decoded entries are valid)
-            if (kind == K_SLOW) break;
+            if (kind == K_SLOW && !solo_fp_ok(q1 & 0xFF)) break;   // (F/D/Zfh ops: solo_fp_op below)
 #ifdef FI_TX
             // a block leader (odd pcs: the solo-odd kernel's odd-pc leaders) past the first instruction
             static_assert(kPreOddLeader == kPreLeader << 1, "leader flags");
@@ -3184,6 +3334,14 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
             case K_REMU:
                 v = w32 ? ((uint32_t)bv == 0 ? sx32(av) : sx32((uint32_t)av % (uint32_t)bv)) : (bv == 0 ? av : av % bv);
                 break;
+            case K_SLOW: {   // an F/D/Zfh op (solo_fp_ok), out of line
+                uint32_t fm = 0;
+                const uint32_t r = solo_fp_op(CX, w, m, slot, R, io, q1, q2, v, fm);
+                if (!r) { msz = 0xFFFFFFFFu; break; }
+                wr = r == 2;
+                msz = fm;
+                break;
+            }
             default: msz = 0xFFFFFFFFu; break;
             }
             if (msz == 0xFFFFFFFFu) break;   // nothing committed for this instruction
@@ -3251,6 +3409,11 @@ leave:
 // ~3 us per instruction before, tools/gpu/launch_size.py census r05c)
 #ifndef FI_TX_SKIP_CLEAN
 #define FI_TX_SKIP_CLEAN 256
+#endif
+// (a clean trial's runs count as short below FI_TX_SHORT_CLEAN instructions,
+// sixteen of them running)
+#ifndef FI_TX_SHORT_CLEAN
+#define FI_TX_SHORT_CLEAN 4
 #endif
 // Solo kernel: the launch context through a plain pointer, so that the
 // compiler can keep loop-invariant fields in registers (a one-lane wave has
@@ -3388,7 +3551,7 @@ __device__ __forceinline__ void trial_body() {
     if (CX->stdin_data && live && !resume) CX->in_pos[slot] = S0->in_pos;
     if (fw_dead && !resume) {   // dead at injection: the trial is the golden run
         L.injected = 1;
-        finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
+        finish(L, FI_MASKED, (int)CX->gsub, (int)CX->gexit, CX->gdetail);
         L.res.ninst = CX->gninst;
         if (kSoloOnce) atomicAdd(&CX->stats[27], 1ull);
     }
@@ -3441,23 +3604,8 @@ __device__ __forceinline__ void trial_body() {
     }
     // (a constant false in the 64-lane kernel)
 #define LP_ON (kNL == 1 && LP.on != 0)
-// a new recorded pass from here (the registers now), or the end of the probe
-// after 4 windows that did not close
-#define LP_WINDOW()                                                                          \
-    do {                                                                                     \
-        if (++LP.tries > 4) { LP_FAIL(); break; }                                           \
-        LP.n = 0; LP.pc0 = L.pc; LP.fp0 = L.fp ? 1u : 0u;                                    \
-        for (int r_ = 0; r_ < 32; r_++) {                                                   \
-            LP.r0[r_] = R[r_];                                                               \
-            LP.f0[r_] = L.fp ? CX->fregs[(uint64_t)r_ * CX->n_slots + slot] : 0ULL;          \
-        }                                                                                    \
-    } while (0)
-#define LP_FAIL()                                                                            \
-    do {                                                                                     \
-        LP.on = 0; LP.cnt = 0;                                                               \
-        LP.at = LP.at < (1u << 30) ? 2 * LP.at : LP.at;                                      \
-        if (kSoloOnce) atomicAdd(&CX->stats[60], 1ull);                                      \
-    } while (0)
+// (eligibility for a loop probe: injected, no watched register, live)
+#define LP_ELIGIBLE (!L.done && (L.injected == 1 || L.injected == 2) && L.watch <= 0)
 #define DC_INVAL(lo_, sz_)                                                                          \
     do {                                                                                            \
         if constexpr (kNL == 1) {                                                                   \
@@ -3515,11 +3663,10 @@ __device__ __forceinline__ void trial_body() {
             break;
         }
         // ---- A. materialise requested pages, whole wave cooperating
-        // (a lane past its P pages takes its overflow block first: priv_room)
-        const bool room = !L.done && m.req_vpn != kNone && priv_room(CX, slot, m.n_priv);
-        const uint64_t want = wballot<kNL>(room);
         if (wballot<kNL>(!L.done && m.req_vpn != kNone)) {
-            uint64_t wl = want;
+            // (a lane past its P pages takes its overflow block first: priv_room)
+            const bool room = !L.done && m.req_vpn != kNone && priv_room(CX, slot, m.n_priv);
+            uint64_t wl = wballot<kNL>(room);
             while (wl) {
                 const int l = __ffsll((unsigned long long)wl) - 1;
                 wl &= wl - 1;
@@ -3561,13 +3708,13 @@ __device__ __forceinline__ void trial_body() {
                 if (!p) {
                     L.injected = 2;    // page not mapped at t: nothing to flip
                     if (CX->mem_live) {   // ... so the trial is the golden run
-                        finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
+                        finish(L, FI_MASKED, (int)CX->gsub, (int)CX->gexit, CX->gdetail);
                         L.res.ninst = CX->gninst;
                         if (kSoloOnce) atomicAdd(&CX->stats[26], 1ull);
                     }
                 } else if (CX->mem_live && mem_dead(CX, s.addr, s.mask, L.ninst)) {
                     L.injected = 1;
-                    finish(L, FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
+                    finish(L, FI_MASKED, (int)CX->gsub, (int)CX->gexit, CX->gdetail);
                     L.res.ninst = CX->gninst;
                     if (kSoloOnce) atomicAdd(&CX->stats[26], 1ull);
                 } else if (!(p & 1)) {
@@ -3632,7 +3779,7 @@ __device__ __forceinline__ void trial_body() {
                 }
                 if (grp) {
                     if (eq) {
-                        finish(L, L.out_bad ? FI_SDC : FI_MASKED, 0, (int)CX->gexit, CX->gdetail);
+                        finish(L, L.out_bad ? FI_SDC : FI_MASKED, (int)CX->gsub, (int)CX->gexit, CX->gdetail);
                         L.res.ninst = CX->gninst;
                     } else {
                         // back off after repeated mismatches (any schedule is exact)
@@ -3669,16 +3816,6 @@ __device__ __forceinline__ void trial_body() {
             next_snap += CX->rec_interval;
         }
 
-        // ---- solo: start a dynamic loop proof (LoopProbe) once the trial has
-        // spent LP.at instructions in the interpreters; the general path then
-        // records one pass (its commit below)
-        if constexpr (kNL == 1) {
-            if (!CX->record && CX->hang_proof && !LP.on && LP.cnt >= LP.at && !L.done && m.req_vpn == kNone &&
-                (L.injected == 1 || L.injected == 2) && L.watch <= 0) {
-                LP.on = 1; LP.tries = 0;
-                LP_WINDOW();
-            }
-        }
         const bool ready = !L.done && m.req_vpn == kNone;
         const uint64_t act = wballot<kNL>(ready);
         if (act == 0) {
@@ -3934,8 +4071,8 @@ __device__ __forceinline__ void trial_body() {
                     // epilogue, leaves at every dispatch) cost a round trip each;
                     // the interpreter takes the next FI_TX_SKIP (rewritten code)
                     // or tx_skip_n instructions, doubling while it recurs
-                    if (st < FI_TX_SHORT) {
-                        if (++tx_short >= 4) {
+                    if (m.code_dirty ? st < FI_TX_SHORT : st < FI_TX_SHORT_CLEAN) {
+                        if (++tx_short >= (m.code_dirty ? 4u : 16u)) {
                             tx_short = 0;
                             tx_skip_until = n_iter + (m.code_dirty ? FI_TX_SKIP : tx_skip_n);
                             tx_skip_n = tx_skip_n < (1u << 20) ? 2 * tx_skip_n : tx_skip_n;
@@ -4062,6 +4199,7 @@ __device__ __forceinline__ void trial_body() {
                     __shared__ SoloPreIO pio[1];
                     pio->spc = lpc; pio->slot = slot; pio->tab = w.tab; pio->tab_n = w.tab_n;
                     pio->budget = budget; pio->watch = L.watch;
+                    pio->fps = (L.fp ? 1u : 0u) | ((uint32_t)L.fflags << 8) | ((uint32_t)L.frm << 16);
                     pio->tx_gate = tx_skip_until > n_iter ? tx_skip_until - n_iter : 0u;
                     solo_pre_run<kOdd>(CX, (lds_u64 *)R, (lds_mem *)&m, (lds_u32 *)DCT, (lds_pre4 *)DCE, (lds_u32 *)LC,
                                        (lds_pio *)pio);
@@ -4070,10 +4208,14 @@ __device__ __forceinline__ void trial_body() {
                     for (int k = 0; k < 4; k++) pacc[k] += pio->prof[k];
 #endif
                     if (steps) {
-                        LP.cnt += steps;   // (interpreted: counts toward a loop probe)
                         L.ninst += steps; L.ncyc += steps + uni32(pio->xticks);
                         L.fetch_b += uni32(pio->fbytes); L.data_b += uni32(pio->dbytes);
                         L.pc = uni64(pio->spc); L.watch = (int)uni32((uint32_t)pio->watch);
+                        const uint32_t fps = uni32(pio->fps);
+                        L.fp = fps & 1; L.fflags = (uint8_t)((fps >> 8) & 0x1F);
+                        // (interpreted: counts toward a loop probe)
+                        LP.cnt += steps;
+                        if (LP.cnt >= LP.at) lp_count((lds_lp *)&LP, CX, (const lds_u64 *)R, slot, L.pc, L.fp, LP_ELIGIBLE, 0u);
                         n_iter += steps;
                         n_exec += steps;
                         continue;
@@ -4412,6 +4554,7 @@ __device__ __forceinline__ void trial_body() {
         int llsc = 0;                 // 1 LR, 2 SC
         uint32_t cbo = 0;             // cache-block op: 1 translate only, 2 zero the line
         bool m5 = false;              // M5Op: a1 = 0 at commit
+        uint32_t m5x = 0, m5code = 0; // an M5 op that ends the run once it commits: 1 exit, 2 fail, 3 quiesce
         bool xdet = false;            // a replica watch read through an M5Op's ABI arguments
 #define FREG_RD(r) (L.fp ? CX->fregs[(uint64_t)(r) * CX->n_slots + slot] : 0ULL)
         // detected-by-replica: the flipped protected register is read before
@@ -4683,7 +4826,22 @@ __device__ __forceinline__ void trial_body() {
                 }
                 case 0x51: f = F_BREAK; break;       // debugbreak -> SIGTRAP
                 case 0x54: f = F_M5PANIC; break;     // m5_panic
-                case 0x01: case 0x02: case 0x03: case 0x04: case 0x21: case 0x22: case 0x43: case 0x4f: case 0x52:
+                // quiesce: the only context suspends after this commit and nothing
+                // wakes it -- a hang (oracle/rv64se.c OP_m5op, thread_context.cc:167)
+                case 0x01: m5x = 3; break;
+                // m5_exit(delay) / m5_fail(delay, code) with delay 0: the stdlib
+                // run script ends the simulation after this tick (pseudo_inst.cc:
+                // 178-204, simulate/exit_handler.py:551-557); a delayed one escapes
+                case 0x21: case 0x22:
+                    xdet = L.watch == 10 || (d.imm == 0x22 && L.watch == 11);
+                    if (RREG(10) != 0) { f = F_ESCAPE; break; }
+                    m5x = d.imm == 0x21 ? 1u : 2u;
+                    m5code = d.imm == 0x22 ? (uint32_t)(RREG(11) & 0xff) : 0u;
+                    break;
+                // checkpoint (the stdlib saves one and continues), switchcpu (not a
+                // switchable processor): no architectural effect, result 0
+                case 0x43: case 0x52: v = 0; break;
+                case 0x02: case 0x03: case 0x04: case 0x4f:
                 case 0x53: case 0x5a: case 0x5b: case 0x62: case 0x70: case 0x71:
                     f = F_ESCAPE; break;             // simulator control / host files
                 default: v = 0; break;               // no architectural effect: result 0
@@ -4776,43 +4934,36 @@ __device__ __forceinline__ void trial_body() {
             L.ninst++;
             if (rdet) finish(L, FI_DETECTED, 0, 0, (uint32_t)pc);   // the shadow disagrees at commit
             else L.pc = npc;
+            if (m5x && !L.done) {   // the M5 op that ends the run has committed
+                if (m5x == 3) {
+                    finish(L, FI_HANG, FI_HANG_QUIESCE, 0, (uint32_t)L.pc);
+                } else if (CX->record) {
+                    finish(L, FI_MASKED, m5x == 1 ? FI_END_M5_EXIT : FI_END_M5_FAIL, (int)m5code, (uint32_t)L.pc);
+                } else {
+                    const bool same = !L.out_bad && L.out_pos == CX->gout_len && L.err_pos == CX->gerr_len &&
+                                      m5code == CX->gexit;
+                    finish(L, same ? FI_MASKED : FI_SDC, m5x == 1 ? FI_END_M5_EXIT : FI_END_M5_FAIL, (int)m5code,
+                           (uint32_t)L.pc);
+                }
+            }
             if constexpr (kNL == 1) {
                 if (!LP.on) {
-                    LP.cnt++;
-                } else if (!L.done) {   // record the pass; at its start pc again, the proof
-                    uint32_t en = lp_entry(d.op, d.rd, d.rs1, d.rs2, d.flags, d.imm, lp_silent);
-                    if (d.op == OP_m5op && m5_no_effect((uint32_t)d.imm) && LP.n + 1 < FI_LP_WINDOW) {
-                        LP.e[LP.n++] = kLpNone | kLpNone << 7 | kLpNone << 14 | 10u << 21 | kLpConst << 28;
-                        en = kLpNone | kLpNone << 7 | kLpNone << 14 | 11u << 21 | kLpConst << 28;
-                    }
-                    if (en == kLpBad) {
-                        LP_FAIL();
-                    } else if (en == kLpLoud || LP.n >= FI_LP_WINDOW) {
-                        LP_WINDOW();   // memory changed, or the pass is too long: again from here
-                    } else {
-                        LP.e[LP.n++] = en;
-                        if (L.pc == LP.pc0) {
-                            const bool hang = lp_prove((const lds_lp *)&LP, (const uint64_t *)R,
-                                                       CX->fregs + slot, CX->n_slots, L.fp);
-                            if (hang) {   // the record of a hang at the cap
-                                const uint64_t left = L.ninst < CX->hang_cap ? CX->hang_cap - L.ninst : 0;
-                                proved_skip += left;
-                                L.ninst += left;
-                                finish(L, FI_HANG, 1, 0, 0u);
-                                LP.on = 0;
-                                if (kSoloOnce) atomicAdd(&CX->stats[59], 1ull);
-                            } else {
-                                LP_FAIL();
-                            }
-                        }
-                    }
+                    if (++LP.cnt >= LP.at) lp_count((lds_lp *)&LP, CX, (const lds_u64 *)R, slot, L.pc, L.fp, LP_ELIGIBLE, 0u);
+                } else if (!L.done &&
+                           lp_commit((lds_lp *)&LP, CX, (const lds_u64 *)R, slot, L.pc, L.fp, d.op, d.rd, d.rs1, d.rs2,
+                                     d.flags, d.imm, lp_silent)) {
+                    // the record of a hang at the cap
+                    const uint64_t left = L.ninst < CX->hang_cap ? CX->hang_cap - L.ninst : 0;
+                    proved_skip += left;
+                    L.ninst += left;
+                    finish(L, FI_HANG, 1, 0, 0u);
                 }
             }
         } else {
         switch (f) {
         case F_SYSCALL: {   // SyscallFault::invokeSE advances the PC first (arch/riscv/faults.cc:325-333)
             if constexpr (kNL == 1) {
-                if (LP.on) LP_FAIL();
+                if (LP.on) lp_fail((lds_lp *)&LP, CX);
             }
             L.pc = pc + d.len;
             // (out of line on copies: the interpreter's state stays in registers)

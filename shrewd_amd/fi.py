@@ -24,6 +24,8 @@ CRASH_NAMES = {1: "panic_unknown_inst", 2: "panic_illegal_inst", 3: "panic_page_
                8: "sigtrap", 9: "fatal_stack_limit", 10: "panic_amo_line", 11: "abort_sc_line", 12: "panic_se_handler",
                13: "panic_m5op"}
 ESCAPE_NAMES = {1: "inst", 2: "syscall", 3: "csr", 4: "host", 5: "resource", 6: "undefined"}
+HANG_NAMES = {1: "max_insts", 2: "m5_quiesce"}
+END_NAMES = {0: "exit", 1: "m5_exit", 2: "m5_fail"}     # sub-codes of masked / sdc: how the run ended
 T_PC, T_MEM, T_RESULT, N_STRUCT = 32, 33, 34, 35
 
 OUTCOME_DT = np.dtype([("cls", "u1"), ("sub", "u1"), ("exit_code", "u1"), ("flags", "u1"),

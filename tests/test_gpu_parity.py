@@ -658,6 +658,42 @@ def test_known_answer_programs_solo_interpreter(oracle_mod, prog):
     e.close()
 
 
+@pytest.mark.parametrize("flags", [0, 128 | 4 | 1 | 2])
+def test_m5_simulator_control_ops(oracle_mod, flags):
+    """The simulator-control M5 ops (test_isa_vectors.m5end_program_source):
+    the device golden run ends at m5_fail with code 7 (sub m5_fail); faulted
+    trials reach m5_quiesce (hang, sub m5_quiesce), an early m5_exit (sdc,
+    sub m5_exit), a delayed exit (escape) and a changed fail code, bit for bit
+    with the oracle -- default configuration (early exit from snapshots: a
+    converged trial takes the golden run's end sub-code) and the solo
+    interpreter from process start."""
+    from shrewd_amd import Engine
+    from shrewd_amd.fi import SITE_DT
+    import test_isa_vectors as kat
+    elf = kat.m5end_program_elf()
+    e = Engine(private_pages=64, flags=flags)
+    e.load_elf(elf, ["m5end"])
+    g = e.golden_run()
+    assert g.exit_code == kat.M5END_CODE & 0xFF and e.golden_stdout() == b"hi\n"
+    o = oracle_mod.Oracle(elf, "m5end")
+    o.run_golden()
+    n = g.ninst
+    L = [(i, 1 << b, reg) for reg in (5, 6, 7, 10, 11) for b in (0, 1, 9) for i in range(n)]
+    sites = np.zeros(len(L), dtype=SITE_DT)
+    for k, (i, mask, reg) in enumerate(L):
+        sites[k] = (i, mask, 0, reg, k)
+    dev, _ = e.run_sites(sites)
+    compare(dev, o.run_trials(sites, protect_mask=0), sites)
+    got = {(int(c), int(s)) for c, s in zip(dev["cls"], dev["sub"])}
+    assert {(0, 2), (1, 1), (1, 2), (3, 2), (5, 1)} <= got, got
+    e.set_campaign(0x5EED00A7, REGS | PC, 1)
+    e.set_protect(0)
+    sites = e.sample(0, 3000)
+    dev, _ = e.run_sites(sites)
+    compare(dev, o.run_trials(sites, protect_mask=0), sites)
+    e.close()
+
+
 def test_clock_read_blocks_tick_blind_early_exit(oracle_mod):
     """Exact early exit when the golden suffix reads curTick: the clk program's
     branch-register faults take an arm with 16 extra non-counting ticks

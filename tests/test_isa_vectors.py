@@ -1566,7 +1566,7 @@ XOP_FROUND = [0x3FF8000000000000, 0xC004000000000000, 0x4330000000000001, 0x3FE0
 XOP_FCVTMOD = [0x41E0000000000000, 0xC1E0000000200000, 0x4340000000000001, 0x4540000000000005,
                0x3FF8000000000000, 0xBFF0000000000000, 0x7FF8000000000000, 0x0000000000000003,
                0x45B0000000000000, 0xC3F0000000012345]
-XOP_M5_NOEFFECT = [0x00, 0x09, 0x0D, 0x10, 0x11, 0x20, 0x31, 0x40, 0x41, 0x42, 0x50, 0x55, 0x59, 0x7F]
+XOP_M5_NOEFFECT = [0x00, 0x09, 0x0D, 0x10, 0x11, 0x20, 0x31, 0x40, 0x41, 0x42, 0x43, 0x50, 0x52, 0x55, 0x59, 0x7F]
 XOP_RPNS_GAP = 40
 XOP_PRIV_NOPS = [0x16000073, 0x18000073, 0x18100073, 0x26000073, 0x66000073]
 # RVV before any vset* (vl = 0): no-ops of one micro-op tick (vadd.vv, vle8.v,
@@ -1746,6 +1746,68 @@ def test_vector_actions_before_vset(oracle_mod):
     for w, (name, fault) in cases.items():
         assert oracle_mod.mnemonic(w) == name, (hex(w), oracle_mod.mnemonic(w))
         assert P(w, 0x1000, regs).fault == fault, hex(w)
+
+
+# ---------------------------------------------------------------- m5end program
+# The simulator-control M5 ops under the stdlib run script's default exit
+# handlers (oracle/rv64se.c OP_m5op; sim/pseudo_inst.cc:117-204,
+# simulate/exit_handler.py:551-557): checkpoint and switchcpu continue with
+# a0 = a1 = 0, the golden run ends at m5_fail(0, 0x307) -- "m5_fail
+# instruction encountered", exit code 7 -- and three dead branches reach
+# m5_quiesce (the only context suspends: a hang), m5_exit(0) (ends the run
+# early, output unchanged, code 0: SDC) and m5_exit(100) (a delayed exit: not
+# modelled, escape).  A flipped t0 / t1 / t2 takes a branch; a flipped a0
+# before m5_fail delays it (escape); a flipped low byte of a1 changes the code
+# (SDC), a high bit does not (masked).
+M5END_CODE = 0x307
+
+
+def _m5(fn):
+    return f"    .word {(fn << 25) | 0x7B:#x}"
+
+
+def m5end_program_source() -> str:
+    L = ["    .text", "_start:", "    li    a0, 1", "    la    a1, msg", "    li    a2, 3", "    li    a7, 64", "    ecall",
+         "    li    a0, -1", "    li    a1, -2", _m5(0x43), "    or    s4, a0, a1", "    li    a0, -1", "    li    a1, -2",
+         _m5(0x52), "    or    s4, s4, a0", "    or    s4, s4, a1", "    bnez  s4, wrong",
+         "    li    t0, 0", "    bnez  t0, quiesce", "    li    t1, 0", "    bnez  t1, early", "    li    t2, 0",
+         "    bnez  t2, delayed", "    li    a0, 0", f"    li    a1, {M5END_CODE}", _m5(0x22),
+         "wrong:", "    li    a0, 1", "    la    a1, msg", "    li    a2, 3", "    li    a7, 64", "    ecall",
+         "    li    a0, 3", "    li    a7, 93", "    ecall",
+         "quiesce:", _m5(0x01), "    j     wrong",
+         "early:", "    li    a0, 0", _m5(0x21), "    j     wrong",
+         "delayed:", "    li    a0, 100", _m5(0x21), "    j     wrong",
+         "    .data", "msg:", "    .ascii \"hi\\n\""]
+    return "\n".join(L) + "\n"
+
+
+def m5end_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(m5end_program_source(), compress=False)
+
+
+def test_m5end_program_on_oracle(oracle_mod):
+    """Golden: ends at m5_fail with code 7 after printing "hi" once; trials on
+    t0 / t1 / t2 / a0 / a1 reach every simulator-control outcome."""
+    import numpy as np
+    o = oracle_mod.Oracle(m5end_program_elf(), "m5end")
+    g = o.run_golden()
+    assert g.exit_code == M5END_CODE & 0xFF and o.golden_stdout() == b"hi\n", g
+    from shrewd_amd.fi import SITE_DT
+    n = g.ninst
+    L = [(i, 1, reg) for reg in (5, 6, 7) for i in range(n)]
+    L += [(n - 1, 1 << 3, 10), (n - 1, 1 << 1, 11), (n - 1, 1 << 9, 11)]
+    sites = np.zeros(len(L), dtype=SITE_DT)
+    for k, (i, mask, reg) in enumerate(L):
+        sites[k] = (i, mask, 0, reg, k)
+    r = o.run_trials(sites, protect_mask=0)
+    got = {(int(c), int(s), int(x)) for c, s, x in zip(r["cls"], r["sub"], r["exit_code"])}
+    assert (0, 2, 7) in got                   # masked: ended at m5_fail, code 7
+    assert (3, 2, 0) in got                   # hang: m5_quiesce
+    assert (1, 1, 0) in got                   # sdc: m5_exit(0) before the golden end, code 0
+    assert (5, 1, 0) in got                   # escape/inst: m5_exit(100)
+    last = [(int(c), int(s), int(x)) for c, s, x in zip(r["cls"][-3:], r["sub"][-3:], r["exit_code"][-3:])]
+    assert last == [(5, 1, 0), (1, 2, 5), (0, 2, 7)], last
 
 
 # ---------------------------------------------------------------- sys2 program

@@ -66,6 +66,9 @@ for size in SIZES:
                            "tx_entries": int(w[i, 8]), "nmiss": int(w[i, 9]),
                            "ns_per_inst": round(1e3 * float(end[i] - start[i]) / max(1, int(w[i, 7])), 1)}
                           for i in order]
+    esc = np.nonzero(out["cls"] == 5)[0]
+    rec["escapes"] = [{"trial": int(i), "sub": int(out["sub"][i]), "detail": hex(int(out["detail"][i])),
+                       "ninst": int(out["ninst"][i])} for i in esc[:40]]
     if ref is None:
         ref = out
     print(json.dumps(rec), flush=True)
