@@ -51,6 +51,13 @@ fi_status fi_debug_translation(fi_engine *e, char *buf, uint64_t cap, uint64_t *
  * err the hipRTC log on failure. */
 fi_status fi_debug_jit_compile(const char *body, const char *arch, void *code, uint64_t cap, uint64_t *len,
                                char *err, uint64_t err_cap);
+/* One part (1 = the 64-lane kernel, 2 solo, 3 solo-odd) of the load-time
+ * build as an engine runs it, with the disk cache on (use_cache) or in
+ * FI_CFG_JIT_NO_CACHE mode: ranks of one node that need the same code object
+ * queue on a lock next to its cache file and one of them builds it.  No
+ * device needed; *len the code object's size, *cached 1 when it was loaded. */
+fi_status fi_debug_jit_build(const char *body, const char *arch, int part, int use_cache, uint64_t *len,
+                             int *cached, char *err, uint64_t err_cap);
 #ifdef __cplusplus
 }
 #endif

@@ -1732,6 +1732,24 @@ fi_status fi_debug_jit_compile(const char *body, const char *arch, void *code, u
     return FI_OK;
 }
 
+// One part of the load-time build as an engine runs it (part 1..3, the disk
+// cache on or off, FI_CFG_JIT_NO_CACHE), no device needed: *cached = 1 when
+// the code object came from the cache.  Tests of the per-node build lock.
+fi_status fi_debug_jit_build(const char *body, const char *arch, int part, int use_cache, uint64_t *len,
+                             int *cached, char *err, uint64_t err_cap) {
+    std::vector<char> co;
+    bool c = false;
+    const std::string msg = jit_compile(body ? body : "", arch ? arch : "gfx950", co, c, part, use_cache != 0);
+    if (err && err_cap) {
+        const uint64_t n = std::min<uint64_t>(err_cap - 1, msg.size());
+        memcpy(err, msg.data(), n);
+        err[n] = 0;
+    }
+    if (len) *len = co.size();
+    if (cached) *cached = c ? 1 : 0;
+    return msg.empty() ? FI_OK : FI_E_HIP;
+}
+
 fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves) {
     if (!e || !out) return FI_E_ARG;
     if (n_waves > e->cap) return fail(e, FI_E_ARG, "more waves than the work buffers hold");
