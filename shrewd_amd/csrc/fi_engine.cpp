@@ -44,6 +44,7 @@ hipError_t launch_trials(const DevCtx &c, hipStream_t st);
 hipError_t launch_trials_solo(const DevCtx &c, hipStream_t st);
 hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, fi_histogram *h,
                        const unsigned long long *stats, hipStream_t st);
+hipError_t launch_hist_stats(const unsigned long long *stats, fi_histogram *h, hipStream_t st);
 hipError_t sort_pairs_bytes(uint64_t n, size_t &bytes);
 hipError_t launch_pack_runs(const uint64_t *keys, const uint32_t *cnt, uint64_t cap, uint32_t *wrange,
                             uint32_t *n_waves, hipStream_t st);
@@ -84,7 +85,7 @@ static constexpr uint32_t kDefaultResumeLanes = 8;   // measured: profiles/READM
 static constexpr uint64_t kJitWindowChunk = 131072;
 
 // The background build of the translated kernels (fi_golden_run starts it;
-// run_chunk installs the result at a chunk boundary): the 64-lane, solo and,
+// run_chunks installs the result at a chunk boundary): the 64-lane, solo and,
 // with odd-pc streams, solo-odd kernels as one code object each, compiled in
 // parallel processes (fi_jit.cpp).  Until it lands the static kernels run
 // every trial -- the same outcomes, bit for bit, more slowly.
@@ -223,12 +224,12 @@ struct fi_engine {
 
     // work buffers, sized for `cap` trials per launch
     uint64_t cap = 0;
-    fi_site *d_sites = nullptr;
+    fi_site *d_sites = nullptr, *d_sites_alt = nullptr;   // the chunk being run / the one being finished
     uint64_t *d_keys = nullptr, *d_keys2 = nullptr;
     uint32_t *d_perm = nullptr, *d_perm2 = nullptr;
     void *d_tmp = nullptr;
     size_t tmp_bytes = 0;
-    fi_outcome *d_out = nullptr;
+    fi_outcome *d_out = nullptr, *d_out_alt = nullptr;
     fi_histogram *d_hist = nullptr;
     unsigned long long *d_stats = nullptr;
     uint64_t *d_wave_dbg = nullptr;
@@ -253,8 +254,13 @@ struct fi_engine {
     uint32_t *d_wrange = nullptr, *d_nwaves = nullptr;   // packed resume (FI_CFG_PACK_RUNS)
     uint32_t *d_split = nullptr;   // per epoch: odd-pc survivors, then the solo kernel's share of the list
     uint32_t *d_dmap = nullptr;    // per slot: rewritten-code map (DevCtx::dmap, kDmapWords words)
-    // second pass of the trials that ran out of private pages (run_chunk)
-    uint32_t *d_redo_idx = nullptr, *d_redo_cnt = nullptr, *h_redo_cnt = nullptr;
+    // second pass of the trials that ran out of private pages (chunk_end)
+    uint32_t *d_redo_idx = nullptr, *d_redo_cnt = nullptr, *h_redo_cnt = nullptr;   // two of each: a chunk and its predecessor
+    hipEvent_t ev_cnt[2] = {nullptr, nullptr};   // a chunk's redo count has reached h_redo_cnt
+    // pinned staging of a chunk's outcomes on their way to the caller's (pageable) array: a copy
+    // straight into pageable memory would hold the host until the stream reaches it
+    fi_outcome *h_stage[2] = {nullptr, nullptr};
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};
     fi_site *d_redo_sites = nullptr;
     fi_outcome *d_redo_out = nullptr;
 };
@@ -367,7 +373,7 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
 }
 
 static void free_work(fi_engine *e) {
-    dfree(e->d_sites); dfree(e->d_keys); dfree(e->d_keys2); dfree(e->d_perm); dfree(e->d_perm2);
+    dfree(e->d_sites); dfree(e->d_sites_alt); dfree(e->d_out_alt); dfree(e->d_keys); dfree(e->d_keys2); dfree(e->d_perm); dfree(e->d_perm2);
     dfree(e->d_tmp); dfree(e->d_out); dfree(e->d_hist); dfree(e->d_stats); dfree(e->d_wave_dbg); dfree(e->d_fregs);
     dfree(e->d_inpos);
     dfree(e->d_save); dfree(e->d_surv[0]); dfree(e->d_surv[1]); dfree(e->d_cnt);
@@ -376,6 +382,8 @@ static void free_work(fi_engine *e) {
     dfree(e->d_ov); dfree(e->d_ov_vpn); dfree(e->d_ov_of); dfree(e->d_ov_next);
     e->ov_blocks = e->ov_pages = 0;
     dfree(e->d_redo_idx); dfree(e->d_redo_cnt); dfree(e->d_redo_sites); dfree(e->d_redo_out);
+    for (auto &h : e->h_stage)
+        if (h) { (void)hipHostFree(h); h = nullptr; }
     e->cap = 0;
 }
 static void free_snaps(fi_engine *e) { dfree(e->d_snaps); dfree(e->d_tab); dfree(e->d_pool); }
@@ -469,6 +477,10 @@ void fi_destroy(fi_engine *e) {
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
     if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     if (e->h_redo_cnt) (void)hipHostFree(e->h_redo_cnt);
+    for (auto ev : e->ev_cnt)
+        if (ev) (void)hipEventDestroy(ev);
+    for (auto ev : e->ev_stage)
+        if (ev) (void)hipEventDestroy(ev);
     delete e;
 }
 
@@ -784,7 +796,7 @@ fi_status fi_load_checkpoint(fi_engine *e, const char *cpt_dir, const uint8_t *e
     return FI_OK;
 }
 
-// Private pages per trial of the second pass (run_chunk) and, with the
+// Private pages per trial of the second pass (chunk_end) and, with the
 // overflow pool, a trial's capacity in the first: 16 P, at least 256.
 static uint64_t redo_pages(uint64_t P) { return std::max<uint64_t>(P * 16ull, 256); }
 
@@ -793,6 +805,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     free_work(e);
     const uint64_t c = n;
     HIPCHK(hipMalloc(&e->d_sites, c * sizeof(fi_site)));
+    HIPCHK(hipMalloc(&e->d_sites_alt, c * sizeof(fi_site)));
     HIPCHK(hipMalloc(&e->d_keys, c * 8));
     HIPCHK(hipMalloc(&e->d_keys2, c * 8));
     HIPCHK(hipMalloc(&e->d_perm, c * 4));
@@ -800,6 +813,7 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(sort_pairs_bytes(c, e->tmp_bytes));
     HIPCHK(hipMalloc(&e->d_tmp, std::max<size_t>(e->tmp_bytes, 16)));
     HIPCHK(hipMalloc(&e->d_out, c * sizeof(fi_outcome)));
+    HIPCHK(hipMalloc(&e->d_out_alt, c * sizeof(fi_outcome)));
     HIPCHK(hipMalloc(&e->d_eff, c * 8));
     HIPCHK(hipMalloc(&e->d_hist, sizeof(fi_histogram)));
     HIPCHK(hipMalloc(&e->d_stats, kNStats * sizeof(unsigned long long)));
@@ -821,11 +835,17 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     HIPCHK(hipMalloc(&e->d_nwaves, 16 * 4));
     HIPCHK(hipMalloc(&e->d_split, 64 * 4));
     HIPCHK(hipMalloc(&e->d_dmap, c * kDmapWords * 4));
-    HIPCHK(hipMalloc(&e->d_redo_idx, c * 4));
+    HIPCHK(hipMalloc(&e->d_redo_idx, 2 * c * 4));
     HIPCHK(hipMalloc(&e->d_redo_cnt, 16));
     HIPCHK(hipMalloc(&e->d_redo_sites, c * sizeof(fi_site)));
     HIPCHK(hipMalloc(&e->d_redo_out, c * sizeof(fi_outcome)));
     if (!e->h_redo_cnt) HIPCHK(hipHostMalloc(&e->h_redo_cnt, 16));
+    for (auto &ev : e->ev_cnt)
+        if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    for (int i = 0; i < 2; i++) {
+        HIPCHK(hipHostMalloc(&e->h_stage[i], c * sizeof(fi_outcome)));
+        if (!e->ev_stage[i]) HIPCHK(hipEventCreateWithFlags(&e->ev_stage[i], hipEventDisableTiming));
+    }
     // overflow pool: a trial past P pages takes a block of P' - P more (P' the
     // redo pass's page count), one block per 2048 slots (at least 64)
     {
@@ -1481,7 +1501,7 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
     c.n_slots = (uint32_t)k;
     c.save = e->d_save;
     c.priv_pages = P;
-    if (P != e->cfg.private_pages) c.ov_blocks = 0;   // the second pass has its own P' (run_chunk)
+    if (P != e->cfg.private_pages) c.ov_blocks = 0;   // the second pass has its own P' (chunk_end)
     if (c.ov_blocks) HIPCHK(hipMemsetAsync(e->d_ov_next, 0, 4, st));
     HIPCHK(hipMemsetAsync(e->d_cnt, 0, 16 * 4, st));
     HIPCHK(hipMemsetAsync(e->d_wave_dbg, 0, k * 10 * sizeof(uint64_t), st));
@@ -1574,49 +1594,70 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
     return FI_OK;
 }
 
-// One launch: d_sites[0..k) holds the sites in trial order, keys/perm set.
-// Trials that ran out of private pages (FI_ESC_RESOURCE: an engine capacity
-// limit, not gem5 behaviour) run again with kRedoPages-fold pages, in batches
-// that reuse the same frames (batch x P' <= k x P), and their outcomes replace
-// the escapes before the histogram.  Costs one host sync per chunk for the
-// count; FI_CFG_NO_REDO skips it.
-static fi_status run_chunk(fi_engine *e, uint64_t k, fi_outcome *d_out, fi_histogram *d_hist, hipStream_t st) {
-    const uint32_t P = e->cfg.private_pages;
-    jit_install(e, st, false);   // the translated kernels, once their build has landed
-    HIPCHK(hipMemsetAsync(e->d_stats, 0, kNStats * sizeof(unsigned long long), st));
-    HIPCHK(hipEventRecord(e->ev0, st));
-    fi_status s = run_pass(e, e->d_sites, k, d_out, P, st);
+// Chunks are pipelined on the launch stream with no host wait between them
+// (DESIGN.md §4e): chunk i runs its pass and lists its resource escapes
+// (FI_ESC_RESOURCE: an engine capacity limit -- the overflow pool ran dry --
+// not gem5 behaviour) and copies their count to pinned memory; the host then
+// enqueues chunk i+1 and only after that reads chunk i's count, while the GPU
+// is busy with chunk i+1.  Chunk i's second pass (redo_pages-fold pages, in
+// batches that reuse the same frames: batch x P' <= k x P), its histogram and
+// its host copy follow chunk i+1 on the stream; their outcomes replace the
+// escapes.  Sites and outcome buffers alternate between the two chunks in
+// flight.  FI_CFG_NO_REDO keeps the escapes.
+struct Chunk {
+    uint64_t k = 0;
+    fi_site *sites = nullptr;
+    fi_outcome *out = nullptr;
+    fi_outcome *host_out = nullptr;   // run_common: where the outcomes go on the host
+    uint32_t slot = 0;                // redo list / count / event pair
+};
+
+static fi_status chunk_begin(fi_engine *e, const Chunk &ch, hipStream_t st) {
+    fi_status s = run_pass(e, ch.sites, ch.k, ch.out, e->cfg.private_pages, st);
     if (s) return s;
     if (!(e->cfg.flags & FI_CFG_NO_REDO)) {
-        HIPCHK(hipMemsetAsync(e->d_redo_cnt, 0, 4, st));
-        HIPCHK(launch_redo_collect(d_out, k, e->d_redo_idx, e->d_redo_cnt, e->d_stats, st));
-        HIPCHK(hipMemcpyAsync(e->h_redo_cnt, e->d_redo_cnt, 4, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        const uint64_t nr = *e->h_redo_cnt;
+        uint32_t *cnt = e->d_redo_cnt + ch.slot;
+        HIPCHK(hipMemsetAsync(cnt, 0, 4, st));
+        HIPCHK(launch_redo_collect(ch.out, ch.k, e->d_redo_idx + ch.slot * e->cap, cnt, e->d_stats, st));
+        HIPCHK(hipMemcpyAsync(e->h_redo_cnt + ch.slot, cnt, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(e->ev_cnt[ch.slot], st));
+    }
+    return FI_OK;
+}
+
+static fi_status chunk_end(fi_engine *e, const Chunk &ch, fi_histogram *d_hist, hipStream_t st) {
+    if (!(e->cfg.flags & FI_CFG_NO_REDO)) {
+        HIPCHK(hipEventSynchronize(e->ev_cnt[ch.slot]));   // (normally long done: a chunk later was enqueued first)
+        const uint64_t nr = e->h_redo_cnt[ch.slot];
+        const uint32_t *idx = e->d_redo_idx + ch.slot * e->cap;
         if (nr) {
-            const uint64_t pool = k * P;   // page frames the pass had
+            const uint64_t P = e->cfg.private_pages;
+            const uint64_t pool = e->cap * P;   // page frames a pass has
             const uint64_t P2 = std::min<uint64_t>(pool, redo_pages(P));
             const uint64_t B = std::max<uint64_t>(1, pool / P2);
             for (uint64_t d = 0; d < nr; d += B) {
                 const uint64_t b = std::min(B, nr - d);
-                HIPCHK(launch_redo_gather(e->d_sites, e->d_redo_idx + d, b, e->d_redo_sites, e->d_keys, e->d_perm,
-                                          st));
-                s = run_pass(e, e->d_redo_sites, b, e->d_redo_out, (uint32_t)P2, st);
+                HIPCHK(launch_redo_gather(ch.sites, idx + d, b, e->d_redo_sites, e->d_keys, e->d_perm, st));
+                fi_status s = run_pass(e, e->d_redo_sites, b, e->d_redo_out, (uint32_t)P2, st);
                 if (s) return s;
-                HIPCHK(launch_redo_scatter(e->d_redo_idx + d, b, e->d_redo_out, d_out, st));
+                HIPCHK(launch_redo_scatter(idx + d, b, e->d_redo_out, ch.out, st));
             }
         }
     }
-    HIPCHK(hipEventRecord(e->ev1, st));
-    HIPCHK(launch_hist(e->d_sites, d_out, k, d_hist, e->d_stats, st));
+    HIPCHK(launch_hist(ch.sites, ch.out, ch.k, d_hist, nullptr, st));
+    if (ch.host_out) {
+        HIPCHK(hipMemcpyAsync(e->h_stage[ch.slot], ch.out, ch.k * sizeof(fi_outcome), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(e->ev_stage[ch.slot], st));
+    }
     return FI_OK;
 }
 
-static fi_status finish_chunk(fi_engine *e, hipStream_t st, double &ms_acc) {
-    HIPCHK(hipStreamSynchronize(st));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
-    ms_acc += ms;
+// A chunk's staged outcomes to the caller's array, once their copy has landed.
+static fi_status chunk_deliver(fi_engine *e, Chunk &ch) {
+    if (!ch.host_out || !ch.k) return FI_OK;
+    HIPCHK(hipEventSynchronize(e->ev_stage[ch.slot]));
+    memcpy(ch.host_out, e->h_stage[ch.slot], ch.k * sizeof(fi_outcome));
+    ch.k = 0;
     return FI_OK;
 }
 
@@ -1624,6 +1665,57 @@ static void hist_add(fi_histogram *dst, const fi_histogram *src) {
     const uint64_t *s = (const uint64_t *)src;
     uint64_t *d = (uint64_t *)dst;
     for (size_t i = 0; i < sizeof(fi_histogram) / 8; i++) d[i] += s[i];
+}
+
+// Trials [first, first + n) (sampled on the device) or the given sites, in
+// chunks of at most e->cap; outcomes to out_dev (device, n entries) or
+// out_host (through the alternating device buffers), histogram added to
+// d_hist.  The event pair ev0 / ev1 spans the whole call.
+static fi_status run_chunks(fi_engine *e, uint64_t first, const fi_site *sites, uint64_t n, fi_outcome *out_dev,
+                            fi_outcome *out_host, fi_histogram *d_hist, hipStream_t st) {
+    HIPCHK(hipMemsetAsync(e->d_stats, 0, kNStats * sizeof(unsigned long long), st));
+    HIPCHK(hipEventRecord(e->ev0, st));
+    Chunk prev, staged[2];   // (staged: chunks whose outcomes still sit in h_stage)
+    bool have_prev = false;
+    uint32_t i = 0;
+    for (uint64_t done = 0; done < n; i++) {
+        jit_install(e, st, false);   // the translated kernels, once their build has landed
+        Chunk ch;
+        ch.k = std::min<uint64_t>({n - done, e->cap, e->jit ? kJitWindowChunk : e->cap});
+        ch.slot = i & 1;
+        ch.sites = ch.slot ? e->d_sites_alt : e->d_sites;
+        ch.out = out_dev ? out_dev + done : ch.slot ? e->d_out_alt : e->d_out;
+        ch.host_out = out_host ? out_host + done : nullptr;
+        if (sites) {
+            HIPCHK(hipMemcpyAsync(ch.sites, sites + done, ch.k * sizeof(fi_site), hipMemcpyHostToDevice, st));
+            HIPCHK(launch_keys(ch.sites, ch.k, e->d_keys, e->d_perm, st));
+        } else {
+            HIPCHK(launch_sample(sample_ctx(e, first + done), ch.k, ch.sites, e->d_keys, e->d_perm, st));
+        }
+        fi_status s = chunk_begin(e, ch, st);
+        if (s) return s;
+        if (have_prev) {
+            if ((s = chunk_deliver(e, staged[prev.slot]))) return s;   // (two chunks ago: long landed)
+            if ((s = chunk_end(e, prev, d_hist, st))) return s;
+            staged[prev.slot] = prev;
+        }
+        prev = ch;
+        have_prev = true;
+        done += ch.k;
+    }
+    if (have_prev) {
+        fi_status s = chunk_deliver(e, staged[prev.slot]);
+        if (!s) s = chunk_end(e, prev, d_hist, st);
+        if (s) return s;
+        staged[prev.slot] = prev;
+    }
+    HIPCHK(hipEventRecord(e->ev1, st));
+    HIPCHK(launch_hist_stats(e->d_stats, d_hist, st));
+    for (auto &c : staged) {
+        fi_status s = chunk_deliver(e, c);
+        if (s) return s;
+    }
+    return FI_OK;
 }
 
 static fi_status run_common(fi_engine *e, uint64_t first, const fi_site *sites, uint64_t n, fi_outcome *out,
@@ -1636,23 +1728,11 @@ static fi_status run_common(fi_engine *e, uint64_t first, const fi_site *sites, 
     fi_status s = ensure_work(e, std::min<uint64_t>(std::max<uint64_t>(n, 1), chunk));
     if (s) return s;
     HIPCHK(hipMemsetAsync(e->d_hist, 0, sizeof(fi_histogram), e->stream));
-    double ms = 0;
-    for (uint64_t done = 0; done < n;) {
-        jit_install(e, e->stream, false);
-        const uint64_t k = std::min<uint64_t>({n - done, e->cap, e->jit ? kJitWindowChunk : e->cap});
-        if (sites) {
-            HIPCHK(hipMemcpyAsync(e->d_sites, sites + done, k * sizeof(fi_site), hipMemcpyHostToDevice, e->stream));
-            HIPCHK(launch_keys(e->d_sites, k, e->d_keys, e->d_perm, e->stream));
-        } else {
-            HIPCHK(launch_sample(sample_ctx(e, first + done), k, e->d_sites, e->d_keys, e->d_perm, e->stream));
-        }
-        s = run_chunk(e, k, e->d_out, e->d_hist, e->stream);
-        if (s) return s;
-        if (out) HIPCHK(hipMemcpyAsync(out + done, e->d_out, k * sizeof(fi_outcome), hipMemcpyDeviceToHost, e->stream));
-        s = finish_chunk(e, e->stream, ms);
-        if (s) return s;
-        done += k;
-    }
+    s = run_chunks(e, first, sites, n, nullptr, out, e->d_hist, e->stream);
+    if (s) return s;
+    HIPCHK(hipStreamSynchronize(e->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e->ev0, e->ev1));
     e->last_ms = ms;
     if (hist) {
         fi_histogram h;
@@ -1690,15 +1770,7 @@ fi_status fi_run_trials_device(fi_engine *e, uint64_t first, uint64_t n, void *d
     const uint64_t chunk = e->cfg.max_trials_per_launch;
     fi_status s = ensure_work(e, std::min<uint64_t>(std::max<uint64_t>(n, 1), chunk));
     if (s) return s;
-    for (uint64_t done = 0; done < n;) {
-        jit_install(e, st, false);
-        const uint64_t k = std::min<uint64_t>({n - done, e->cap, e->jit ? kJitWindowChunk : e->cap});
-        HIPCHK(launch_sample(sample_ctx(e, first + done), k, e->d_sites, e->d_keys, e->d_perm, st));
-        s = run_chunk(e, k, (fi_outcome *)d_out + done, (fi_histogram *)d_hist, st);
-        if (s) return s;
-        done += k;
-    }
-    return FI_OK;
+    return run_chunks(e, first, nullptr, n, (fi_outcome *)d_out, nullptr, (fi_histogram *)d_hist, st);
 }
 
 fi_status fi_sync(fi_engine *e) {

@@ -293,7 +293,7 @@ __global__ void fi_pack_runs_kernel(const uint64_t *keys, const uint32_t *cnt, u
 }
 
 // Second pass of the trials that ran out of private pages (fi_engine.cpp
-// run_chunk): list them, gather their sites densely, scatter the new outcomes.
+// chunk_begin / chunk_end): list them, gather their sites densely, scatter the new outcomes.
 // (A resource escape with exit code 1 hit a table bound -- the VMA list, the
 // getrandom stream -- that more pages would not lift: fi_trial.hip kEscTable.)
 __global__ void fi_redo_collect_kernel(const fi_outcome *out, uint64_t n, uint32_t *idx, uint32_t *cnt,
@@ -359,6 +359,10 @@ hipError_t launch_debug_decode(const uint32_t *raws, uint64_t n, PreInst *out, h
 hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, fi_histogram *h,
                        const unsigned long long *stats, hipStream_t st) {
     hipLaunchKernelGGL(fi_hist_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, sites, out, n, h);
+    if (stats) hipLaunchKernelGGL(fi_hist_stats_kernel, dim3(1), dim3(64), 0, st, stats, h);
+    return hipGetLastError();
+}
+hipError_t launch_hist_stats(const unsigned long long *stats, fi_histogram *h, hipStream_t st) {
     hipLaunchKernelGGL(fi_hist_stats_kernel, dim3(1), dim3(64), 0, st, stats, h);
     return hipGetLastError();
 }

@@ -473,7 +473,12 @@ def test_run_trials_equals_run_sites(engine_factory):
 
 
 def test_chunking_invariance(engine_factory):
-    """Launch size must not change any outcome (shard invariance)."""
+    """Launch size must not change any outcome (shard invariance).  Chunks
+    are pipelined with no host wait between them (fi_engine.cpp run_chunks):
+    a chunk's second pass (resource escapes: crc32 with P = 1 and no
+    overflow pool) runs after the next chunk's first,
+    from its own sites buffer -- the outcomes, the histogram and its totals
+    equal a one-launch run's, on the host path and the device path."""
     small = engine_factory("qsort", max_trials_per_launch=1000)
     big = engine_factory("qsort")
     for e in (small, big):
@@ -482,6 +487,34 @@ def test_chunking_invariance(engine_factory):
     b, hb = big.run_trials(0, 5000)
     assert np.array_equal(a, b)
     assert np.array_equal(ha["counts"], hb["counts"])
+    from shrewd_amd.fi import CFG_NO_OVERFLOW
+    redo = [engine_factory("crc32", max_trials_per_launch=m, private_pages=1, flags=CFG_NO_OVERFLOW)
+            for m in (1000, 3000)]
+    outs = []
+    for e in redo:
+        e.set_campaign(77, REGS | PC | MEM, 2)
+        o, h = e.run_trials(0, 3000)
+        assert int(e.debug_stats()[30]) > 0, "no resource escape to redo"
+        outs.append((o, h))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    for f in ("counts", "crash_sub", "escape_sub", "trials", "guest_insts"):
+        assert np.array_equal(outs[0][1][f], outs[1][1][f]), f
+    ref = engine_factory("crc32")
+    ref.set_campaign(77, REGS | PC | MEM, 2)
+    assert np.array_equal(outs[0][0], ref.run_trials(0, 3000)[0])
+    assert int(outs[0][1]["trials"]) == 3000 and int(outs[0][1]["guest_insts"]) == int(outs[0][0]["ninst"].sum())
+    # the device path (bench.py's): chunked outcomes land in place
+    import torch
+    from shrewd_amd import HIST_DT
+    d_out = torch.zeros(3000 * a.dtype.itemsize, dtype=torch.uint8, device="cuda")
+    d_hist = torch.zeros(HIST_DT.itemsize, dtype=torch.uint8, device="cuda")
+    redo[0].run_trials_device(0, 3000, d_out.data_ptr(), d_hist.data_ptr())
+    redo[0].sync()
+    dev = np.frombuffer(d_out.cpu().numpy().tobytes(), dtype=a.dtype)
+    hd = np.frombuffer(d_hist.cpu().numpy().tobytes(), dtype=HIST_DT)[0]
+    assert np.array_equal(dev, outs[0][0])
+    for f in ("counts", "crash_sub", "escape_sub", "trials", "guest_insts"):
+        assert np.array_equal(hd[f], outs[0][1][f]), f
 
 
 def test_argv_shapes_stack(engine_factory, oracle_mod):
