@@ -76,6 +76,7 @@ typedef int32_t fi_status;
 #define FI_CRASH_SC_LINE 11       /* abort  SC across a cache line  cpu/simple/atomic.cc:482 assert(curr_frag_id == 0) */
 #define FI_CRASH_SE_PANIC 12      /* panic  in an SE syscall handler (null ProxyPtr, MemState::isUnmapped) */
 #define FI_CRASH_M5_PANIC 13      /* panic  in an M5 pseudo-op (m5_panic, unknown initparam key) sim/pseudo_inst.* */
+#define FI_CRASH_VSET_SEW 14      /* abort  vset* requesting vsew > 3: getSew's assert  arch/riscv/insts/vector.hh:55 */
 /* FI_HANG sub-codes */
 #define FI_HANG_INSTS 1           /* the max-insts cap (hang_factor_x16 x golden numInst) */
 #define FI_HANG_QUIESCE 2         /* m5_quiesce: the only context suspends for good (sim/pseudo_inst.cc:117) */

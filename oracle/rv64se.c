@@ -277,7 +277,7 @@ typedef struct {
 } mach_t;
 
 enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_ESCAPE = 5, F_PGFAULT = 6, F_AMOLINE = 7,
-       F_SCLINE = 8, F_M5PANIC = 9, F_UNDEF = 10 };
+       F_SCLINE = 8, F_M5PANIC = 9, F_UNDEF = 10, F_VSEW = 11 };
 
 /* -------------------------------------------------------------- decode */
 /* Op ids.  Names follow gem5's mnemonics (arch/riscv/isa/decoder.isa). */
@@ -314,7 +314,7 @@ enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_E
     X(lr_w) X(sc_w) X(lr_d) X(sc_d) \
     X(fadd) X(fsub) X(fmul) X(fdiv) X(fsqrt) X(fmin) X(fmax) X(fmadd) X(fmsub) X(fnmsub) X(fnmadd) \
     X(feq) X(flt) X(fle) X(fcvt_f2i) X(fcvt_i2f) X(fcvt_f2f) \
-    X(priv) X(cbo) X(m5op) X(crypto) X(fli) X(fround) X(fcvtmod) X(vec)
+    X(priv) X(cbo) X(m5op) X(crypto) X(fli) X(fround) X(fcvtmod) X(vec) X(vset)
 
 enum {
 #define X(n) OP_##n,
@@ -446,6 +446,17 @@ static void decode(u32 raw, dec_t *d) {
     if ((raw & 3) == 3 && (d->op == OP_ESC_FP || d->op == OP_ESC_AMO)) refine_fp_amo(raw, d);
     if (d->op < OP_c_addi4spn) d->rd = d->rs1 = d->rs2 = d->frd = d->frs1 = d->frs2 = -1;
     if ((raw & 3) == 3) refine_misc(raw, d);
+    if (d->op == OP_vec && d->imm == VEC_STATE && bits(raw, 6, 0) == 0x57 && bits(raw, 14, 12) == 7) {
+        /* vsetvli / vsetvl / vsetivli (decoder.isa:5838-5886): imm = the
+         * requested vtype's immediate | form << 16 (0 vsetvli, 1 vsetvl: vtype
+         * from Rs2, 2 vsetivli); Rd written, Rs1 (and Rs2) read */
+        const int form = bits(raw, 31, 31) ? (bits(raw, 30, 30) ? 2 : 1) : 0;
+        d->op = OP_vset;
+        d->rd = (int)bits(raw, 11, 7);
+        d->rs1 = form == 2 ? -1 : (int)bits(raw, 19, 15);
+        d->rs2 = form == 1 ? (int)bits(raw, 24, 20) : -1;
+        d->imm = (form == 0 ? (s64)bits(raw, 30, 20) : form == 2 ? (s64)bits(raw, 29, 20) : 0) | ((s64)form << 16);
+    }
 }
 /* The executed members of the LOAD-FP / STORE-FP / OP-FP / AMO groups, among
  * the encodings gem5 decodes to a known class (decoder.isa:567-591 flh/flw/fld,
@@ -946,6 +957,10 @@ const char *or_mnemonic(u32 inst) {
     }
     if (d.op == OP_m5op) return "M5Op";
     if (d.op == OP_vec) { snprintf(buf, sizeof buf, "vector:%d", (int)d.imm); return buf; }
+    if (d.op == OP_vset) {
+        static const char *vn[3] = {"vsetvli", "vsetvl", "vsetivli"};
+        return vn[(d.imm >> 16) & 3];
+    }
     if (d.op == OP_fli || d.op == OP_fround || d.op == OP_fcvtmod) {
         static const char *fs[3] = {"h", "s", "d"};
         const int fmt = (int)((d.imm >> 3) & 3);
@@ -2216,6 +2231,29 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
         case VEC_UNDEF: return F_UNDEF;
         default: return F_ESCAPE;
         }
+    /* ---- vset* from the process-start vector state (vtype = vill, vl = 0,
+     * decoder.hh:68-69; every other state escapes, so this is the only
+     * one): VConfOp::execute (formats/vector_conf.isa:115-186).  A request
+     * other than the current vtype is checked by getNewVtype, whose getSew
+     * asserts vsew <= 3 (insts/vector.hh:52-56: gem5.opt aborts); an illegal
+     * one -- LMUL outside [1/8, 8] (vlmul 4: 1/16), SEW > min(LMUL, 1) x ELEN
+     * (ELEN 64, RiscvISA.py:103), reserved bits 62..8 set -- gives vtype =
+     * vill and VLMAX 0, so vl = 0 and the state stays the start state; rd
+     * gets vl.  A legal vtype needs the vector unit's state: escape. */
+    case OP_vset: {
+        const int form = (int)(imm >> 16);
+        const u64 req = form == 1 ? b : (u64)(imm & 0xFFFF);
+        const u64 vill = 1ULL << 63;
+        if (req != vill) {
+            const u32 vsew = (u32)(req >> 3) & 7, vlmul = (u32)req & 7;
+            if (vsew > 3) return F_VSEW;
+            const u32 lim = vlmul <= 3 ? 64 : vlmul == 5 ? 8 : vlmul == 6 ? 16 : vlmul == 7 ? 32 : 0;
+            const int illegal = vlmul == 4 || (8u << vsew) > lim || ((req >> 8) & ((1ULL << 55) - 1)) != 0;
+            if (!illegal) return F_ESCAPE;
+        }
+        v = 0;
+        break;
+    }
     /* ---- privileged SYSTEM / hypervisor load-store from PRV_U (refine_misc) */
     case OP_priv:
         if (!imm) return F_ILLEGAL;
@@ -2350,6 +2388,7 @@ static void invoke_fault(mach_t *m, int f, u64 fault_va, const dec_t *d) {
     case F_AMOLINE: finish(m, OR_CRASH, OR_CRASH_AMO_LINE, 134); return;
     case F_SCLINE: finish(m, OR_CRASH, OR_CRASH_SC_LINE, 134); return;
     case F_M5PANIC: finish(m, OR_CRASH, OR_CRASH_M5_PANIC, 134); return;
+    case F_VSEW: finish(m, OR_CRASH, OR_CRASH_VSET_SEW, 134); return;
     case F_UNDEF: finish(m, OR_ESCAPE, OR_ESC_UNDEF, 0); m->res.detail = d->raw; return;
     case 100: finish(m, OR_DETECTED, 0, 0); return;
     case F_PGFAULT: {
@@ -3178,7 +3217,7 @@ int or_probe(u32 inst, u64 pc, const u64 regs[32], or_probe_t *o) {
     u64 fva = 0;
     int f = execute(&m, &d, &fva);
     o->fault = f == F_NONE ? 0 : f == F_SYSCALL ? 1 : f == F_BREAK ? 2 : f == F_ILLEGAL ? 3 :
-               f == F_UNKNOWN ? 4 : f == F_PGFAULT ? 6 : 5;
+               f == F_UNKNOWN ? 4 : f == F_PGFAULT ? 6 : f == F_VSEW ? 11 : 5;
     o->rd = d.rd;
     o->rd_value = d.rd > 0 ? m.x[d.rd] : 0;
     if (d.rd < 0 && d.frd >= 0) { o->rd = 32 + d.frd; o->rd_value = m.f[d.frd]; }   /* FP destination: 32 + f */

@@ -40,7 +40,8 @@ enum {
     OR_CRASH_AMO_LINE = 10,     /* panic: AMO across a cache line atomic.cc:569-570 */
     OR_CRASH_SC_LINE = 11,      /* abort: SC across a cache line  atomic.cc:482 assert(curr_frag_id == 0) */
     OR_CRASH_SE_PANIC = 12,     /* panic in an SE handler (null ProxyPtr, MemState::isUnmapped) */
-    OR_CRASH_M5_PANIC = 13      /* panic in an M5 pseudo-op (m5_panic, unknown initparam key) sim/pseudo_inst.* */
+    OR_CRASH_M5_PANIC = 13,     /* panic in an M5 pseudo-op (m5_panic, unknown initparam key) sim/pseudo_inst.* */
+    OR_CRASH_VSET_SEW = 14      /* abort: vset* requesting vsew > 3, getSew's assert  arch/riscv/insts/vector.hh:55 */
 };
 enum {
     OR_ESC_INST = 1,            /* instruction gem5 decodes but the engine does not model */
@@ -171,7 +172,8 @@ int or_run_one_capture(or_campaign_t *c, const or_site_t *site, uint64_t protect
  * the value written to rd, the next pc and the fault kind. */
 typedef struct {
     uint64_t rd_value, npc;
-    int32_t fault;      /* 0 none, 1 syscall, 2 breakpoint, 3 illegal, 4 unknown, 5 escape, 6 pagefault */
+    int32_t fault;      /* 0 none, 1 syscall, 2 breakpoint, 3 illegal, 4 unknown, 5 escape (and other
+                           ends), 6 pagefault, 11 vset's vsew assert */
     int32_t rd;         /* destination register written, -1 none (32 + f for an FP destination) */
     uint32_t len;
     uint32_t op;        /* oracle-internal op id */

@@ -530,7 +530,7 @@ __device__ bool proxy_write(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot
 }
 
 enum { F_NONE = 0, F_SYSCALL, F_BREAK, F_ILLEGAL, F_UNKNOWN, F_ESCAPE, F_ESCCSR, F_PGFAULT, F_NEEDPAGE, F_DETECT,
-       F_AMOLINE, F_SCLINE, F_M5PANIC, F_UNDEF };
+       F_AMOLINE, F_SCLINE, F_M5PANIC, F_UNDEF, F_VSEW };
 
 // AtomicSimpleCPU::readMem/writeMem (atomic.cc:331-544): the access is split
 // at 64-byte line boundaries, each fragment translated on its own; faults are
@@ -1877,6 +1877,7 @@ __device__ __noinline__ uint32_t lp_entry(uint32_t op, uint32_t rd, uint32_t rs1
     case OP_cbo:
         return kLpBad;
     case OP_m5op:   // (the commit records a0 = 0 and a1 = 0 for the ones without an effect)
+    case OP_vset:
         return kLpBad;
     case OP_vec:    // RVV before any vset*: a no-op of one or two ticks (imm 2, 3), else a fault or escape
         if (imm != 2 && imm != 3) return kLpBad;
@@ -4858,6 +4859,22 @@ __device__ __forceinline__ void trial_body() {
                 else if (d.imm == 5) f = F_UNDEF;
                 else if (d.imm == 6) f = F_ESCAPE;
                 break;
+            // vset* from the start vector state (oracle/rv64se.c OP_vset,
+            // formats/vector_conf.isa:115-186): vsew > 3 trips getSew's assert;
+            // an illegal vtype leaves the start state (vill, vl 0) and rd = 0;
+            // a legal one needs the vector unit's state (escape)
+            case OP_vset: {
+                const uint32_t form = (uint32_t)d.imm >> 16;
+                const uint64_t req = form == 1 ? b : (uint64_t)((uint32_t)d.imm & 0xFFFFu);
+                if (req != (1ULL << 63)) {
+                    const uint32_t vsew = (uint32_t)(req >> 3) & 7, vlmul = (uint32_t)req & 7;
+                    const uint32_t lim = vlmul <= 3 ? 64 : vlmul == 5 ? 8 : vlmul == 6 ? 16 : vlmul == 7 ? 32 : 0;
+                    if (vsew > 3) f = F_VSEW;
+                    else if (vlmul != 4 && (8u << vsew) <= lim && ((req >> 8) & ((1ULL << 55) - 1)) == 0) f = F_ESCAPE;
+                }
+                v = 0;
+                break;
+            }
             default: f = F_UNKNOWN; break;
             }
         }
@@ -4990,6 +5007,7 @@ __device__ __forceinline__ void trial_body() {
         case F_AMOLINE: finish(L, FI_CRASH, FI_CRASH_AMO_LINE, 134, (uint32_t)pc); break;
         case F_SCLINE: finish(L, FI_CRASH, FI_CRASH_SC_LINE, 134, (uint32_t)pc); break;
         case F_M5PANIC: finish(L, FI_CRASH, FI_CRASH_M5_PANIC, 134, (uint32_t)pc); break;
+        case F_VSEW: finish(L, FI_CRASH, FI_CRASH_VSET_SEW, 134, (uint32_t)pc); break;
         case F_UNDEF: finish(L, FI_ESCAPE, FI_ESC_UNDEF, 0, d.raw); break;
         case F_PGFAULT: {   // GenericPageTableFault::invoke -> fixupFault (sim/faults.cc:95-105)
             int h;

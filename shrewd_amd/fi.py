@@ -22,7 +22,7 @@ CLASS_NAMES = ["masked", "sdc", "crash", "hang", "detected", "escape"]
 CRASH_NAMES = {1: "panic_unknown_inst", 2: "panic_illegal_inst", 3: "panic_page_fault",
                4: "fatal_syscall_range", 5: "fatal_syscall_unimpl", 6: "fatal_proxy", 7: "abort_fd_assert",
                8: "sigtrap", 9: "fatal_stack_limit", 10: "panic_amo_line", 11: "abort_sc_line", 12: "panic_se_handler",
-               13: "panic_m5op"}
+               13: "panic_m5op", 14: "abort_vset_sew"}
 ESCAPE_NAMES = {1: "inst", 2: "syscall", 3: "csr", 4: "host", 5: "resource", 6: "undefined"}
 HANG_NAMES = {1: "max_insts", 2: "m5_quiesce"}
 END_NAMES = {0: "exit", 1: "m5_exit", 2: "m5_fail"}     # sub-codes of masked / sdc: how the run ended

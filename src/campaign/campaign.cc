@@ -23,11 +23,12 @@ const char *kClass[FI_N_CLASS] = {"masked", "sdc", "crash", "hang", "detected", 
 // shrewd_amd/fi.py CRASH_NAMES / ESCAPE_NAMES)
 const char *kCrash[] = {"", "panic_unknown_inst", "panic_illegal_inst", "panic_page_fault", "fatal_syscall_range",
                         "fatal_syscall_unimpl", "fatal_proxy", "abort_fd_assert", "sigtrap", "fatal_stack_limit",
-                        "panic_amo_line", "abort_sc_line", "panic_se_handler", "panic_m5op"};
+                        "panic_amo_line", "abort_sc_line", "panic_se_handler", "panic_m5op",
+                        "abort_vset_sew"};
 const char *kEscape[] = {"", "inst", "syscall", "csr", "host", "resource", "undefined"};
 constexpr int kNCrash = sizeof(kCrash) / sizeof(kCrash[0]);
 constexpr int kNEscape = sizeof(kEscape) / sizeof(kEscape[0]);
-static_assert(kNCrash == FI_CRASH_M5_PANIC + 1 && kNEscape == FI_ESC_UNDEF + 1, "sub-code names");
+static_assert(kNCrash == FI_CRASH_VSET_SEW + 1 && kNEscape == FI_ESC_UNDEF + 1, "sub-code names");
 
 void check(fi_engine *e, fi_status s, const char *what) {
     if (s != FI_OK) {

@@ -1740,12 +1740,86 @@ def test_vector_actions_before_vset(oracle_mod):
     cases = {0x622180d7: ("vector:4", 3),    # vmseq.vv: the first micro-op checks vill
              0x422020d7: ("vector:4", 3),    # vmv.x.s x1, v2 (non-split)
              0x02219057: ("vector:5", 5),    # vfadd.vv: no SEW = 8 instantiation
-             0x0c0071d7: ("vector:6", 5),    # vsetvli
+             0x0c0071d7: ("vsetvli", 5),     # vsetvli x3, x0, e8, m1, ta, ma: a legal vtype needs vector state
              0x02828087: ("vector:6", 5),    # vl1re8.v (whole register)
              0x02218057: ("vector:2", 0)}    # vadd.vv: a no-op at vl = 0
     for w, (name, fault) in cases.items():
         assert oracle_mod.mnemonic(w) == name, (hex(w), oracle_mod.mnemonic(w))
         assert P(w, 0x1000, regs).fault == fault, hex(w)
+
+
+def _vsetvli(rd, rs1, zimm):
+    return (zimm << 20) | (rs1 << 15) | (7 << 12) | (rd << 7) | 0x57
+
+
+def _vsetivli(rd, uimm, zimm):
+    return (3 << 30) | (zimm << 20) | (uimm << 15) | (7 << 12) | (rd << 7) | 0x57
+
+
+def _vsetvl(rd, rs1, rs2):
+    return (1 << 31) | (rs2 << 20) | (rs1 << 15) | (7 << 12) | (rd << 7) | 0x57
+
+
+def test_vset_from_the_start_state(oracle_mod):
+    """vset* (formats/vector_conf.isa:115-186) from the process-start state
+    (vtype = vill, vl = 0): a request equal to the current vtype or an
+    illegal one (LMUL 1/16, SEW > min(LMUL, 1) x ELEN, reserved bits) leaves
+    that state and writes vl = 0 to rd; vsew > 3 trips getSew's assert
+    (abort: fault 11, crash sub-code 14); a legal vtype -- including one whose
+    vill bit came from vsetvl's register -- escapes."""
+    P = oracle_mod.probe
+    regs = [0] * 32
+    regs[6], regs[7] = 5, 0x1234
+    for w, fault in ((_vsetvli(7, 6, 0x100), 0), (_vsetvli(7, 0, 0x004), 0), (_vsetvli(7, 6, 0x01D), 0),
+                     (_vsetvli(7, 6, 0x00D), 0), (_vsetivli(7, 31, 0x104), 0), (_vsetivli(7, 5, 0x016), 0),
+                     (_vsetvli(7, 6, 0x005), 5), (_vsetivli(7, 5, 0x00E), 5), (_vsetvli(7, 6, 0x0C0), 5),
+                     (_vsetvli(7, 6, 0x020), 11), (_vsetivli(7, 1, 0x3FF), 11), (_vsetvli(7, 6, 0x13C), 11)):
+        p = P(w, 0x1000, regs)
+        assert oracle_mod.mnemonic(w) == ("vsetvli" if w >> 31 == 0 else "vsetivli"), hex(w)
+        assert p.fault == fault, (hex(w), p.fault)
+        if fault == 0:
+            assert p.rd == 7 and p.rd_value == 0, hex(w)
+    for t0, fault in ((1 << 63, 0), (1 << 62, 0), (0x104, 0), ((1 << 63) | 0x8, 5), (0x8, 5), (0x38, 11)):
+        regs[5] = t0
+        p = P(_vsetvl(7, 6, 5), 0x1000, regs)
+        assert p.fault == fault, (hex(t0), p.fault)
+        if fault == 0:
+            assert p.rd == 7 and p.rd_value == 0
+
+
+VSET_WORDS = [_vsetvli(7, 6, 0x100), _vsetvli(7, 0, 0x004), _vsetvli(7, 6, 0x01D), _vsetvli(7, 6, 0x00D),
+              _vsetivli(7, 31, 0x104), _vsetivli(7, 5, 0x016)]
+VSETVL_T0 = [1 << 63, 1 << 62, 0x104]
+
+
+def vset_program_source() -> str:
+    """Illegal vset* requests (rd = t2 written 0, the start state kept), then
+    an RVV op that is a no-op in the start state; each t2 printed."""
+    L = ["    .text", "_start:", "    la    s2, out", "    mv    s3, s2", "    li    t1, 5"]
+    for w in VSET_WORDS:
+        L += ["    li    t2, -1", f"    .word {w:#x}", "    sd    t2, 0(s2)", "    addi  s2, s2, 8"]
+    for t0 in VSETVL_T0:
+        L += [f"    li    t0, {t0}", "    li    t2, -1", f"    .word {_vsetvl(7, 6, 5):#x}", "    sd    t2, 0(s2)",
+              "    addi  s2, s2, 8"]
+    L += ["    .word 0x02218057",                    # vadd.vv: a no-op at vl = 0
+          "    li    a0, 1", "    mv    a1, s3", "    sub   a2, s2, s3", "    li    a7, 64", "    ecall",
+          "    li    a0, 0", "    li    a7, 93", "    ecall", "    .bss", "    .balign 8", "out:", "    .zero 256"]
+    return "\n".join(L) + "\n"
+
+
+def vset_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(vset_program_source(), compress=False)
+
+
+def vset_program_expected() -> bytes:
+    return bytes(8 * (len(VSET_WORDS) + len(VSETVL_T0)))
+
+
+def test_vset_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(vset_program_elf(), "vset")
+    g = o.run_golden()
+    assert g.exit_code == 0 and o.golden_stdout() == vset_program_expected()
 
 
 # ---------------------------------------------------------------- m5end program

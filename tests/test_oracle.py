@@ -276,10 +276,12 @@ def test_decode_matches_gem5_decoder(oracle_mod):
             assert name != "escape:UNKNOWN"
         elif name.startswith("vector:"):
             # ... an RVV class carries its action before any vset*
-            # (gen_vector_actions.py): whole-register moves and vset* need vector state
+            # (gen_vector_actions.py): whole-register moves need vector state (vset*
+            # execute from the start state: their own mnemonics, below)
             act = int(name.split(":")[1])
             assert 2 <= act <= 6
-            if str(fmt[lf]) in ("VConfOp", "VlWholeOp", "VsWholeOp", "VMvWholeFormat"):
+            assert str(fmt[lf]) != "VConfOp", cls[lf]
+            if str(fmt[lf]) in ("VlWholeOp", "VsWholeOp", "VMvWholeFormat"):
                 assert act == 6, cls[lf]
             if "Float" in str(fmt[lf]):   # no vill check before the SEW = 8 decode, no non-split float op at SEW 8
                 assert act in (2, 5), cls[lf]

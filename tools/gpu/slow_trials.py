@@ -38,4 +38,5 @@ for i in ids:
            "fast_calls": int(st[53]), "fast_insts": int(st[54]), "fast_backs": int(st[55])}
     if os.environ.get("SHREWD_FI_LIB"):
         rec["cycles_per_iter_by_stamp"] = [round(int(st[32 + k]) / max(1, int(st[6])), 1) for k in range(8)]
+        rec["stats_32_40"] = [int(x) for x in st[32:40]]
     print(json.dumps(rec), flush=True)

@@ -32,8 +32,9 @@ sys.path.insert(0, HERE)
 from gen_decode_vectors import run_isa_parser  # noqa: E402
 
 # `[Outer::]Cls::Cls(ExtMachInst machInst[, ...]) : Base("mnem", machInst, XxxOp)`
-CTOR = re.compile(r'(\w+)::\1\(\s*ExtMachInst machInst[^)]*\)\s*:\s*[\w<>:, ]+?\(\s*"([^"]+)",\s*machInst,\s*'
-                  r'(No_OpClass|\w+?Op)\b')
+# (the vector-configuration classes name it _machInst: formats/vector_conf.isa)
+CTOR = re.compile(r'(\w+)::\1\(\s*ExtMachInst _?machInst[^)]*\)\s*:\s*[\w<>:, ]+?\(\s*"([^"]+)",\s*_?machInst,'
+                  r'[^"]*?(No_OpClass|\w+?Op)\b')
 
 
 def opclass_enum(ref: str) -> list[str]:
@@ -88,6 +89,8 @@ def main():
                    "fcvtmod": ["fcvtmod_w_d"],
                    # RVV before any vset*: nothing commits a result (VectorNopMicroInst)
                    "vec": ["ecall"],
+                   # vset* from the start state (vill, vl 0): SimdConfigOp
+                   "vset": ["vsetvli", "vsetvl", "vsetivli"],
                    "crypto": [f"sha256{k}" for k in ("sum0", "sum1", "sig0", "sig1")] +
                              [f"sha512{k}" for k in ("sum0", "sum1", "sig0", "sig1")] +
                              ["sm3p0", "sm3p1", "aes64im", "aes64ks1i", "brev8", "sm4ed", "sm4ks", "aes64es",
