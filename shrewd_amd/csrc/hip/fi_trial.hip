@@ -2162,8 +2162,10 @@ __device__ __noinline__ uint32_t solo_fp_op(KCtx *c, const WaveMem &w, LaneMem &
 // lane's TLB, the six branches, jal, jalr -- with the exact rules of
 // solo_pre_run, and leaves to the C++ loop, before the instruction, at
 // anything else (reason 1): K_SLOW, a decode-cache miss in the rewritten window, a page the TLB
-// does not hold, a page crossing, a misaligned access, a store into the code
-// range or to a page the lane has not copied.  Outcomes are those of the C++
+// does not hold, a page crossing, a misaligned access, the first store that
+// changes bytes of the code range (later ones: the rewrite is marked here as
+// in solo_pre_run -- bounding range, LDS map, decode and entry caches) or a
+// store to a page the lane has not copied.  Outcomes are those of the C++
 // loop bit for bit (every parity test runs through it).
 struct alignas(16) SoloFastIO {
     uint32_t po, steps, budget, xticks;     // 0   in/out (budget in)
@@ -2174,8 +2176,12 @@ struct alignas(16) SoloFastIO {
     uint64_t pre, tlo;                      // 80  pre-decoded text, text base
     uint64_t clo, cvpn;                     // 96  code range base; page cache (in/out)
     uint64_t cpg, npc;                      // 112 its page; out: the pc that left the text (reason 3)
+    uint32_t dl_lds, dsh, pad0, pad1;       // 128 LDS of the rewritten-code map (0: none), its granule shift
 };
-static_assert(sizeof(SoloFastIO) == 128, "SoloFastIO layout");
+static_assert(sizeof(SoloFastIO) == 144, "SoloFastIO layout");
+// a store that rewrites code updates LaneMem::dlo / dhi in place (LDS, from &tv0)
+static_assert(__builtin_offsetof(LaneMem, dlo) == __builtin_offsetof(LaneMem, tv0) + 96 &&
+              __builtin_offsetof(LaneMem, dhi) == __builtin_offsetof(LaneMem, tv0) + 104, "LaneMem dlo / dhi");
 typedef __attribute__((address_space(3))) SoloFastIO lds_fio;
 // reasons: 0 budget spent, 1 the instruction at po is the C++ loop's, 2 a
 // block leader stops the run, 3 a jump left the text (npc), 4 the fall-through
@@ -2953,7 +2959,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_add_u32 s62, s15, s63\n"         // overlaps [clo, clo + csz) iff u < csz + msz - 1
         "s_sub_u32 s62, s62, 1\n"
         "s_cmp_lt_u32 s74, s62\n"
-        "s_cbranch_scc1 L_slow%=\n"
+        "s_cbranch_scc1 L_stc%=\n"
         "L_stok%=:\n"
         "s_add_u32 s10, s10, s63\n"         // data bytes
         "v_mov_b32 v2, s42\n"
@@ -2977,6 +2983,127 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "L_std%=:\n"
         "s_nop 1\n"
         "s_branch L_nowb%=\n"
+        // a store into the code range that writes the bytes already there
+        // changes nothing (solo_pre_run: no rewrite to mark): it commits here
+        // without writing; one that changes them is the C++ loop's
+        "L_stc%=:\n"
+        "s_cmp_eq_u32 s54, 3\n"
+        "s_cbranch_scc1 L_stc8%=\n"
+        "s_cmp_eq_u32 s54, 2\n"
+        "s_cbranch_scc1 L_stc4%=\n"
+        "s_cmp_eq_u32 s54, 1\n"
+        "s_cbranch_scc1 L_stc2%=\n"
+        "global_load_ubyte v2, v[0:1], off\n"
+        "s_and_b32 s62, s42, 0xff\n"
+        "s_branch L_stcw%=\n"
+        "L_stc2%=:\n"
+        "global_load_ushort v2, v[0:1], off\n"
+        "s_and_b32 s62, s42, 0xffff\n"
+        "s_branch L_stcw%=\n"
+        "L_stc4%=:\n"
+        "global_load_dword v2, v[0:1], off\n"
+        "s_mov_b32 s62, s42\n"
+        "L_stcw%=:\n"
+        "s_waitcnt vmcnt(0)\n"
+        "v_readfirstlane_b32 s74, v2\n"
+        "s_cmp_eq_u32 s74, s62\n"
+        "s_cbranch_scc0 L_stdirty%=\n"
+        "s_add_u32 s10, s10, s63\n"         // data bytes
+        "s_branch L_nowb%=\n"
+        "L_stc8%=:\n"
+        "global_load_dwordx2 v[2:3], v[0:1], off\n"
+        "s_waitcnt vmcnt(0)\n"
+        "v_readfirstlane_b32 s74, v2\n"
+        "v_readfirstlane_b32 s75, v3\n"
+        "s_cmp_eq_u64 s[74:75], s[42:43]\n"
+        "s_cbranch_scc0 L_stdirty%=\n"
+        "s_add_u32 s10, s10, s63\n"
+        "s_branch L_nowb%=\n"
+        // a store that rewrites code bytes [ea, ea + msz): mark it as
+        // solo_pre_run does (mark_dirty_solo + its window + cache drops), then
+        // store.  A first rewrite (no window yet: the map starts then) is the
+        // C++ loop's.
+        "L_stdirty%=:\n"
+        "s_cmp_eq_u32 s12, -1\n"
+        "s_cbranch_scc1 L_slow%=\n"
+        // LaneMem dlo = min(dlo, ea), dhi = max(dhi, ea + msz)
+        "ds_read2_b64 v[2:5], v18 offset0:12 offset1:13\n"
+        "s_add_u32 s66, s64, s63\n"         // s[66:67] = ea + msz
+        "s_addc_u32 s67, s65, 0\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_readfirstlane_b32 s68, v2\n"
+        "v_readfirstlane_b32 s69, v3\n"
+        "v_readfirstlane_b32 s40, v4\n"
+        "v_readfirstlane_b32 s41, v5\n"
+        "s_sub_u32 s62, s64, s68\n"         // ea < dlo?
+        "s_subb_u32 s62, s65, s69\n"
+        "s_cselect_b64 s[68:69], s[64:65], s[68:69]\n"
+        "s_sub_u32 s62, s40, s66\n"         // dhi < ea + msz?
+        "s_subb_u32 s62, s41, s67\n"
+        "s_cselect_b64 s[40:41], s[66:67], s[40:41]\n"
+        "v_mov_b32 v2, s68\n"
+        "v_mov_b32 v3, s69\n"
+        "v_mov_b32 v4, s40\n"
+        "v_mov_b32 v5, s41\n"
+        "ds_write2_b64 v18, v[2:3], v[4:5] offset0:12 offset1:13\n"
+        // the window as text offsets: o0 = max(ea, tlo) - tlo, o1 = ea + msz - tlo
+        "s_sub_u32 s68, s64, s22\n"
+        "s_subb_u32 s69, s65, s23\n"
+        "s_cselect_b32 s68, 0, s68\n"       // (ea below the text: 0)
+        "s_sub_u32 s69, s66, s22\n"         // o1
+        "s_min_u32 s12, s12, s68\n"
+        "s_add_u32 s62, s69, 3\n"
+        "s_max_u32 s13, s13, s62\n"
+        // drop the decode-cache and entry-cache entries whose tag t is in
+        // [o0 - 3, o1) -- all 64 at once, every lane of the wave
+        "s_sub_u32 s68, s68, 3\n"           // lo3 = o0 >= 3 ? o0 - 3 : 0
+        "s_cselect_b32 s68, 0, s68\n"
+        "s_sub_u32 s69, s69, s68\n"         // width o1 - lo3
+        "v_readfirstlane_b32 s40, v16\n"    // DCT (LDS)
+        "s_mov_b64 s[74:75], exec\n"
+        "s_mov_b64 exec, -1\n"
+        "v_subrev_u32 v2, s68, v24\n"
+        "v_cmp_gt_u32 vcc, s69, v2\n"
+        "v_cndmask_b32_e64 v24, v24, -1, vcc\n"
+        "v_mbcnt_lo_u32_b32 v4, -1, 0\n"
+        "v_mbcnt_hi_u32_b32 v4, -1, v4\n"
+        "v_lshl_add_u32 v5, v4, 2, s40\n"
+        "ds_read_b32 v6, v5\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_subrev_u32 v7, s68, v6\n"
+        "v_cmp_gt_u32 vcc, s69, v7\n"
+        "s_mov_b64 exec, vcc\n"
+        "v_mov_b32 v6, -1\n"
+        "ds_write_b32 v5, v6\n"
+        "s_mov_b64 exec, s[74:75]\n"
+        // the LDS map: granules (max(ea, clo) - clo) >> sh .. (min(ea + msz, chi) - 1 - clo) >> sh
+        "ds_read2_b32 v[2:3], v31 offset0:32 offset1:33\n"
+        "s_sub_u32 s68, s64, s24\n"         // e0 = ea - clo (0 below the code)
+        "s_subb_u32 s69, s65, s25\n"
+        "s_cselect_b32 s68, 0, s68\n"
+        "s_sub_u32 s69, s66, s24\n"         // e1 = min(ea + msz - clo, csz)
+        "s_min_u32 s69, s69, s15\n"
+        "s_sub_u32 s69, s69, 1\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "v_readfirstlane_b32 s40, v2\n"     // dl (LDS; 0: no map)
+        "v_readfirstlane_b32 s41, v3\n"     // shift
+        "s_cmp_eq_u32 s40, 0\n"
+        "s_cbranch_scc1 L_stok%=\n"
+        "s_lshr_b32 s68, s68, s41\n"
+        "s_lshr_b32 s69, s69, s41\n"
+        "L_dmark%=:\n"
+        "s_lshr_b32 s62, s68, 5\n"
+        "s_lshl_b32 s62, s62, 2\n"
+        "s_add_u32 s62, s62, s40\n"
+        "s_lshl_b32 s41, 1, s68\n"          // (the shift count's low 5 bits: q & 31)
+        "v_mov_b32 v2, s62\n"
+        "v_mov_b32 v3, s41\n"
+        "ds_or_b32 v2, v3\n"
+        "s_add_u32 s68, s68, 1\n"
+        "s_cmp_gt_u32 s68, s69\n"
+        "s_cbranch_scc0 L_dmark%=\n"
+        "s_waitcnt lgkmcnt(0)\n"
+        "s_branch L_stok%=\n"
         // ================================================================ exits
         "L_left%=:\n"
         "s_mov_b32 s19, 3\n"
@@ -3006,6 +3133,9 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "ds_write2_b32 v31, v2, v3 offset0:3 offset1:4\n"
         "ds_write_b32 v31, v4 offset:20\n"
         "ds_write_b32 v31, v5 offset:56\n"
+        "v_mov_b32 v12, s12\n"              // ddlo, ddhi + 3 (a rewrite may have grown them)
+        "v_mov_b32 v13, s13\n"
+        "ds_write2_b32 v31, v12, v13 offset0:7 offset1:8\n"
         "ds_write2_b64 v31, v[6:7], v[8:9] offset0:13 offset1:14\n"
         "ds_write_b64 v31, v[10:11] offset:120\n"
         "ds_write2_b64 v15, v[64:65], v[66:67] offset0:0 offset1:1\n"
@@ -3148,6 +3278,7 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
                 F->r_lds = (uint32_t)(uintptr_t)R; F->dct_lds = (uint32_t)(uintptr_t)DCT;
                 F->dce_lds = (uint32_t)(uintptr_t)DCE; F->tlb_lds = (uint32_t)(uintptr_t)&mp->tv0;
                 F->lc_lds = (uint32_t)(uintptr_t)LC;
+                F->dl_lds = have_dl ? (uint32_t)(uintptr_t)dl : 0u; F->dsh = dsh;
                 F->pre = (uint64_t)(uintptr_t)CX->pre; F->tlo = tlo; F->clo = clo; F->cvpn = cvpn; F->cpg = cpg;
                 solo_fast_run(F);
                 n_fast++;
@@ -3155,6 +3286,7 @@ __device__ __noinline__ void solo_pre_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds
                 po = uni32(F->po); steps = uni32(F->steps); xticks = uni32(F->xticks);
                 fbytes = uni32(F->fbytes); dbytes = uni32(F->dbytes);
                 cvpn = uni64(F->cvpn); cpg = uni64(F->cpg);
+                ddlo = uni32(F->ddlo); ddhi = uni32(F->ddhi3) - 3u;   // (rewrites it marked)
                 const uint32_t why = uni32(F->reason);
                 if (why == 3) { spc = uni64(F->npc); goto leave; }   // a jump left the text
                 if (why == 4) { spc = tlo + po; goto leave; }         // so did the fall-through
@@ -3398,9 +3530,11 @@ leave:
 #endif
 // A trial that leaves the translated blocks after fewer than FI_TX_SHORT
 // instructions four times running stays in the interpreter: if it rewrote
-// code, for the next FI_TX_SKIP (a round trip costs more than the blocks save)
+// code, for the next FI_TX_SKIP (a round trip costs more than the blocks save:
+// qsort 631236 re-entered every 11 instructions, ~5 us per round trip against
+// ~0.2 us per instruction in the assembly interpreter)
 #ifndef FI_TX_SHORT
-#define FI_TX_SHORT 8
+#define FI_TX_SHORT 32
 #endif
 #ifndef FI_TX_SKIP
 #define FI_TX_SKIP 4096
