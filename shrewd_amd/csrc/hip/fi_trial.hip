@@ -2149,20 +2149,24 @@ __device__ __noinline__ uint32_t solo_fp_op(KCtx *c, const WaveMem &w, LaneMem &
 // instruction (a single wave issues one every 4 cycles: ~400 ns); most of it
 // is the guest register file in LDS (address, ds_read, wait, readfirstlane
 // per operand, a ds_write per result) and the compiler's compare tree on the
-// micro-op kind.  Here the 31 guest registers live in VGPRs v64..v127 of the
-// one active lane (x_r = v[64 + 2r] lo, v[65 + 2r] hi), read and written
-// through VGPR index mode (s_set_gpr_idx_on), and everything else is SALU:
+// micro-op kind.  Here the 31 guest registers live in lanes of two VGPRs
+// (x_r = lane r of v28 lo / v29 hi; lane 32 absorbs the writes to x0), read
+// with v_readlane and written with v_writelane (lane select in M0), and
+// everything else is SALU -- two VGPRs instead of 64, so the call saves no
+// callee-saved VGPRs (round 4 kept them in v64..v127 under VGPR index mode:
+// 32 of those are callee-saved, spilled to scratch and back on every call):
 // ~40 instructions for an ALU op, the kind dispatched through a jump table;
 // the entries of the pcs it runs are kept in a 64-entry cache in VGPR lanes
 // (v24..v27, lane (po >> 1) & 63, read with v_readlane), so a loop reads no
 // LDS (rewritten code) after its first iteration.
 // It runs every micro-op but K_SLOW -- add / sub / and / or / xor / slt(u) /
-// shifts / mul / mulh(s)(u) / div(u) / rem(u) (also the W forms), aligned
-// in-page loads and stores through a two-entry page cache in front of the
+// shifts / mul / mulh(s)(u) / div(u) / rem(u) (also the W forms), in-page
+// loads and stores through a two-entry page cache in front of the
 // lane's TLB, the six branches, jal, jalr -- with the exact rules of
 // solo_pre_run, and leaves to the C++ loop, before the instruction, at
 // anything else (reason 1): K_SLOW, a decode-cache miss in the rewritten window, a page the TLB
-// does not hold, a page crossing, a misaligned access, the first store that
+// does not hold, a page crossing (misaligned accesses inside a page go byte by
+// byte, as in solo_pre_run), the first store that
 // changes bytes of the code range (later ones: the rewrite is marked here as
 // in solo_pre_run -- bounding range, LDS map, decode and entry caches) or a
 // store to a page the lane has not copied.  Outcomes are those of the C++
@@ -2189,7 +2193,7 @@ typedef __attribute__((address_space(3))) SoloFastIO lds_fio;
 __device__ __noinline__ void solo_fast_run(lds_fio *io) {
     const uint32_t a = (uint32_t)(uintptr_t)io;
     asm volatile(
-        // ---- state in: the io record (LDS) into SGPRs, R into v64..v127
+        // ---- state in: the io record (LDS) into SGPRs, R into lanes of v28 / v29
         "s_mov_b32 s4, m0\n"
         "v_mov_b32 v31, %[io]\n"
         "ds_read2_b64 v[0:3], v31 offset0:0 offset1:1\n"
@@ -2246,22 +2250,16 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "v_lshl_add_u32 v30, v30, 4, s62\n"
         "ds_read_b128 v[24:27], v30\n"
         "s_mov_b64 exec, s[74:75]\n"
-        "ds_read2_b64 v[64:67], v15 offset0:0 offset1:1\n"
-        "ds_read2_b64 v[68:71], v15 offset0:2 offset1:3\n"
-        "ds_read2_b64 v[72:75], v15 offset0:4 offset1:5\n"
-        "ds_read2_b64 v[76:79], v15 offset0:6 offset1:7\n"
-        "ds_read2_b64 v[80:83], v15 offset0:8 offset1:9\n"
-        "ds_read2_b64 v[84:87], v15 offset0:10 offset1:11\n"
-        "ds_read2_b64 v[88:91], v15 offset0:12 offset1:13\n"
-        "ds_read2_b64 v[92:95], v15 offset0:14 offset1:15\n"
-        "ds_read2_b64 v[96:99], v15 offset0:16 offset1:17\n"
-        "ds_read2_b64 v[100:103], v15 offset0:18 offset1:19\n"
-        "ds_read2_b64 v[104:107], v15 offset0:20 offset1:21\n"
-        "ds_read2_b64 v[108:111], v15 offset0:22 offset1:23\n"
-        "ds_read2_b64 v[112:115], v15 offset0:24 offset1:25\n"
-        "ds_read2_b64 v[116:119], v15 offset0:26 offset1:27\n"
-        "ds_read2_b64 v[120:123], v15 offset0:28 offset1:29\n"
-        "ds_read2_b64 v[124:127], v15 offset0:30 offset1:31\n"
+        // the guest registers: x_r in lane r of v28 (low word) / v29 (high
+        // word), lanes 0..31 (lane 32 takes the writes to x0)
+        "v_readfirstlane_b32 s62, v15\n"
+        "s_mov_b64 s[74:75], exec\n"
+        "s_mov_b32 exec_lo, -1\n"
+        "s_mov_b32 exec_hi, 0\n"
+        "v_mbcnt_lo_u32_b32 v2, -1, 0\n"
+        "v_lshl_add_u32 v2, v2, 3, s62\n"
+        "ds_read_b64 v[28:29], v2\n"
+        "s_mov_b64 exec, s[74:75]\n"
         "s_waitcnt lgkmcnt(0)\n"
         // ================================================================ loop
         "L_top%=:\n"
@@ -2285,18 +2283,13 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "L_nolead%=:\n"
         "s_and_b32 s60, s39, 0xff\n"        // len
         "s_bfe_u32 s57, s37, 0x50008\n"     // rd
-        "s_bfe_u32 s58, s37, 0x6000f\n"     // 2 rs1 (bit 15: the top of the 8-bit rd field, 0)
-        "s_bfe_u32 s59, s37, 0x60017\n"     // 2 rs2 (bit 23: the top of the rs1 field, 0)
-        // a = x[rs1] (av but for U_APC), b = x[rs2]: the index applies to
-        // v_readlane's VGPR source too (lane 0: the solo wave's one lane)
-        "s_set_gpr_idx_on s58, gpr_idx(SRC0)\n"
-        "v_readlane_b32 s44, v64, 0\n"
-        "v_readlane_b32 s45, v65, 0\n"
-        "s_set_gpr_idx_off\n"
-        "s_set_gpr_idx_on s59, gpr_idx(SRC0)\n"
-        "v_readlane_b32 s42, v64, 0\n"
-        "v_readlane_b32 s43, v65, 0\n"
-        "s_set_gpr_idx_off\n"
+        "s_bfe_u32 s58, s37, 0x50010\n"     // rs1
+        "s_bfe_u32 s59, s37, 0x50018\n"     // rs2
+        // a = x[rs1] (av but for U_APC), b = x[rs2]: lane rs of v28 / v29
+        "v_readlane_b32 s44, v28, s58\n"
+        "v_readlane_b32 s45, v29, s58\n"
+        "v_readlane_b32 s42, v28, s59\n"
+        "v_readlane_b32 s43, v29, s59\n"
         "s_ashr_i32 s53, s38, 31\n"         // imm, sign-extended
         "s_mov_b32 s52, s38\n"
         "s_bitcmp1_b32 s39, 25\n"           // U_APC (aux = w >> 16): av = pc (out of line)
@@ -2318,11 +2311,10 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_bitcmp1_b32 s39, 26\n"           // U_W32: sign-extend the low word (out of line)
         "s_cbranch_scc1 L_wbw%=\n"
         "L_wb64%=:\n"
-        "s_lshl_b32 s62, s57, 1\n"
-        "s_set_gpr_idx_on s62, gpr_idx(DST)\n"
-        "v_mov_b64 v[64:65], s[48:49]\n"
-        "s_set_gpr_idx_off\n"
-        "v_mov_b64 v[64:65], 0\n"           // x0 stays zero
+        "s_cmp_eq_u32 s57, 0\n"             // x0 stays zero: its writes go to lane 32
+        "s_cselect_b32 m0, 32, s57\n"
+        "v_writelane_b32 v28, s48, m0\n"
+        "v_writelane_b32 v29, s49, m0\n"
         "L_nowb%=:\n"
         "s_add_u32 s6, s6, 1\n"             // commit (data bytes: in the memory paths)
         "s_bfe_u32 s62, s39, 0x10009\n"     // straddle tick (kPreStraddle)
@@ -2820,11 +2812,10 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_addc_u32 s51, s45, s53\n"
         "s_and_b32 s50, s50, -2\n"
         "L_jwb%=:\n"
-        "s_lshl_b32 s62, s57, 1\n"
-        "s_set_gpr_idx_on s62, gpr_idx(DST)\n"
-        "v_mov_b64 v[64:65], s[48:49]\n"
-        "s_set_gpr_idx_off\n"
-        "v_mov_b64 v[64:65], 0\n"           // x0 stays zero
+        "s_cmp_eq_u32 s57, 0\n"
+        "s_cselect_b32 m0, 32, s57\n"
+        "v_writelane_b32 v28, s48, m0\n"
+        "v_writelane_b32 v29, s49, m0\n"
         "L_jump%=:\n"
         "s_add_u32 s6, s6, 1\n"             // commit
         "s_bfe_u32 s62, s39, 0x10009\n"     // straddle tick (kPreStraddle)
@@ -2902,9 +2893,6 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_add_u32 s62, s78, s63\n"
         "s_cmp_gt_u32 s62, 0x1000\n"
         "s_cbranch_scc1 L_slow%=\n"         // crosses the page
-        "s_sub_u32 s62, s63, 1\n"
-        "s_and_b32 s62, s78, s62\n"
-        "s_cbranch_scc1 L_slow%=\n"         // misaligned
         "s_and_b32 s76, s28, -2\n"          // address in the page
         "s_mov_b32 s77, s29\n"
         "s_add_u32 s76, s76, s78\n"
@@ -2913,8 +2901,13 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "v_mov_b32 v1, s77\n"
         "s_cmp_eq_u32 s56, 13\n"
         "s_cbranch_scc1 L_st%=\n"
-        // load (nothing leaves from here on: its data bytes count)
+        // load (nothing leaves from here on: its data bytes count); a
+        // misaligned one inside the page byte by byte (L_mv)
         "s_add_u32 s10, s10, s63\n"
+        "s_sub_u32 s62, s63, 1\n"
+        "s_and_b32 s62, s78, s62\n"
+        "s_mov_b32 s36, 0\n"
+        "s_cbranch_scc1 L_mv%=\n"
         "s_cmp_eq_u32 s54, 3\n"
         "s_cbranch_scc1 L_ld8%=\n"
         "s_cmp_eq_u32 s54, 2\n"
@@ -2931,6 +2924,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_branch L_ldn%=\n"
         "L_ld8%=:\n"
         "global_load_dwordx2 v[2:3], v[0:1], off\n"
+        "L_ld8w%=:\n"
         "s_waitcnt vmcnt(0)\n"
         "v_readfirstlane_b32 s48, v2\n"
         "v_readfirstlane_b32 s49, v3\n"
@@ -2964,6 +2958,9 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_add_u32 s10, s10, s63\n"         // data bytes
         "v_mov_b32 v2, s42\n"
         "v_mov_b32 v3, s43\n"
+        "s_sub_u32 s62, s63, 1\n"           // misaligned inside the page: bytes
+        "s_and_b32 s62, s78, s62\n"
+        "s_cbranch_scc1 L_stmis%=\n"
         "s_cmp_eq_u32 s54, 3\n"
         "s_cbranch_scc1 L_st8%=\n"
         "s_cmp_eq_u32 s54, 2\n"
@@ -2983,10 +2980,82 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "L_std%=:\n"
         "s_nop 1\n"
         "s_branch L_nowb%=\n"
+        // a misaligned store inside the page, byte by byte
+        "L_stmis%=:\n"
+        "v_lshrrev_b32 v4, 8, v2\n"
+        "v_lshrrev_b32 v5, 16, v2\n"
+        "v_lshrrev_b32 v6, 24, v2\n"
+        "v_lshrrev_b32 v7, 8, v3\n"
+        "v_lshrrev_b32 v8, 16, v3\n"
+        "v_lshrrev_b32 v9, 24, v3\n"
+        "global_store_byte v[0:1], v2, off\n"
+        "global_store_byte v[0:1], v4, off offset:1\n"
+        "s_cmp_eq_u32 s54, 1\n"
+        "s_cbranch_scc1 L_std%=\n"
+        "global_store_byte v[0:1], v5, off offset:2\n"
+        "global_store_byte v[0:1], v6, off offset:3\n"
+        "s_cmp_eq_u32 s54, 2\n"
+        "s_cbranch_scc1 L_std%=\n"
+        "global_store_byte v[0:1], v3, off offset:4\n"
+        "global_store_byte v[0:1], v7, off offset:5\n"
+        "global_store_byte v[0:1], v8, off offset:6\n"
+        "global_store_byte v[0:1], v9, off offset:7\n"
+        "s_branch L_std%=\n"
+        // the value of a misaligned access inside the page (2, 4 or 8 bytes)
+        // byte by byte into v2 (low word) / v3 (high word), zero-extended;
+        // then back to the load (s36 = 0) or the code-store check (s36 = 1)
+        "L_mv%=:\n"
+        "global_load_ubyte v2, v[0:1], off\n"
+        "global_load_ubyte v3, v[0:1], off offset:1\n"
+        "s_cmp_eq_u32 s54, 1\n"
+        "s_cbranch_scc1 L_mv2%=\n"
+        "global_load_ubyte v4, v[0:1], off offset:2\n"
+        "global_load_ubyte v5, v[0:1], off offset:3\n"
+        "s_cmp_eq_u32 s54, 2\n"
+        "s_cbranch_scc1 L_mv4%=\n"
+        "global_load_ubyte v6, v[0:1], off offset:4\n"
+        "global_load_ubyte v7, v[0:1], off offset:5\n"
+        "global_load_ubyte v8, v[0:1], off offset:6\n"
+        "global_load_ubyte v9, v[0:1], off offset:7\n"
+        "s_waitcnt vmcnt(0)\n"
+        "v_lshl_or_b32 v6, v7, 8, v6\n"
+        "v_lshl_or_b32 v6, v8, 16, v6\n"
+        "v_lshl_or_b32 v6, v9, 24, v6\n"
+        "s_branch L_mv4c%=\n"
+        "L_mv4%=:\n"
+        "s_waitcnt vmcnt(0)\n"
+        "v_mov_b32 v6, 0\n"
+        "L_mv4c%=:\n"
+        "v_lshl_or_b32 v2, v3, 8, v2\n"
+        "v_lshl_or_b32 v2, v4, 16, v2\n"
+        "v_lshl_or_b32 v2, v5, 24, v2\n"
+        "v_mov_b32 v3, v6\n"
+        "s_branch L_mvd%=\n"
+        "L_mv2%=:\n"
+        "s_waitcnt vmcnt(0)\n"
+        "v_lshl_or_b32 v2, v3, 8, v2\n"
+        "v_mov_b32 v3, 0\n"
+        "L_mvd%=:\n"
+        "s_cmp_eq_u32 s36, 0\n"
+        "s_cbranch_scc0 L_stcmv%=\n"
+        "s_cmp_eq_u32 s54, 3\n"
+        "s_cbranch_scc1 L_ld8w%=\n"
+        "s_branch L_ldn%=\n"
+        "L_stcmv%=:\n"
+        "s_cmp_eq_u32 s54, 3\n"
+        "s_cbranch_scc1 L_stc8w%=\n"
+        "s_and_b32 s62, s42, 0xffff\n"
+        "s_cmp_eq_u32 s54, 2\n"
+        "s_cselect_b32 s62, s42, s62\n"
+        "s_branch L_stcw%=\n"
         // a store into the code range that writes the bytes already there
         // changes nothing (solo_pre_run: no rewrite to mark): it commits here
-        // without writing; one that changes them is the C++ loop's
+        // without writing; one that changes them marks the rewrite (L_stdirty)
         "L_stc%=:\n"
+        "s_sub_u32 s62, s63, 1\n"
+        "s_and_b32 s62, s78, s62\n"
+        "s_mov_b32 s36, 1\n"
+        "s_cbranch_scc1 L_mv%=\n"
         "s_cmp_eq_u32 s54, 3\n"
         "s_cbranch_scc1 L_stc8%=\n"
         "s_cmp_eq_u32 s54, 2\n"
@@ -3012,6 +3081,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "s_branch L_nowb%=\n"
         "L_stc8%=:\n"
         "global_load_dwordx2 v[2:3], v[0:1], off\n"
+        "L_stc8w%=:\n"
         "s_waitcnt vmcnt(0)\n"
         "v_readfirstlane_b32 s74, v2\n"
         "v_readfirstlane_b32 s75, v3\n"
@@ -3138,22 +3208,14 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
         "ds_write2_b32 v31, v12, v13 offset0:7 offset1:8\n"
         "ds_write2_b64 v31, v[6:7], v[8:9] offset0:13 offset1:14\n"
         "ds_write_b64 v31, v[10:11] offset:120\n"
-        "ds_write2_b64 v15, v[64:65], v[66:67] offset0:0 offset1:1\n"
-        "ds_write2_b64 v15, v[68:69], v[70:71] offset0:2 offset1:3\n"
-        "ds_write2_b64 v15, v[72:73], v[74:75] offset0:4 offset1:5\n"
-        "ds_write2_b64 v15, v[76:77], v[78:79] offset0:6 offset1:7\n"
-        "ds_write2_b64 v15, v[80:81], v[82:83] offset0:8 offset1:9\n"
-        "ds_write2_b64 v15, v[84:85], v[86:87] offset0:10 offset1:11\n"
-        "ds_write2_b64 v15, v[88:89], v[90:91] offset0:12 offset1:13\n"
-        "ds_write2_b64 v15, v[92:93], v[94:95] offset0:14 offset1:15\n"
-        "ds_write2_b64 v15, v[96:97], v[98:99] offset0:16 offset1:17\n"
-        "ds_write2_b64 v15, v[100:101], v[102:103] offset0:18 offset1:19\n"
-        "ds_write2_b64 v15, v[104:105], v[106:107] offset0:20 offset1:21\n"
-        "ds_write2_b64 v15, v[108:109], v[110:111] offset0:22 offset1:23\n"
-        "ds_write2_b64 v15, v[112:113], v[114:115] offset0:24 offset1:25\n"
-        "ds_write2_b64 v15, v[116:117], v[118:119] offset0:26 offset1:27\n"
-        "ds_write2_b64 v15, v[120:121], v[122:123] offset0:28 offset1:29\n"
-        "ds_write2_b64 v15, v[124:125], v[126:127] offset0:30 offset1:31\n"
+        "v_readfirstlane_b32 s62, v15\n"    // the guest registers back to R (lanes 0..31)
+        "s_mov_b64 s[74:75], exec\n"
+        "s_mov_b32 exec_lo, -1\n"
+        "s_mov_b32 exec_hi, 0\n"
+        "v_mbcnt_lo_u32_b32 v14, -1, 0\n"
+        "v_lshl_add_u32 v14, v14, 3, s62\n"
+        "ds_write_b64 v14, v[28:29]\n"
+        "s_mov_b64 exec, s[74:75]\n"
         "v_readfirstlane_b32 s62, v19\n"   // the entry cache back to LDS (all lanes)
         "s_mov_b64 s[74:75], exec\n"
         "s_mov_b64 exec, -1\n"
@@ -3173,11 +3235,7 @@ __device__ __noinline__ void solo_fast_run(lds_fio *io) {
           "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82",
           "v0", "v1", "v2", "v3", "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15",
           "v16", "v17", "v18", "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30",
-          "v31", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77",
-          "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92",
-          "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106",
-          "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119",
-          "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127", "vcc", "memory");
+          "v31", "vcc", "memory");
 }
 
 // 64-bit unsigned / signed compares of uniform values on the scalar unit
