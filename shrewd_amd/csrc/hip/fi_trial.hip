@@ -1937,6 +1937,20 @@ __device__ __forceinline__ uint64_t lp_step(uint32_t e, uint64_t cur) {
 // The recorded pass repeats forever (the rules above).  xe: the integer
 // registers now, at the pass's end; fr: the slot's FP file (stride apart;
 // zeros while it does not exist, fp false).
+// The whole state again: every register equal at the pass's start and end
+// (and the FP file, if any) -- with no store that changed memory in the pass,
+// the next pass is the same pass (a loop whose values converge: x = x & y,
+// shifts that reach zero, a pointer reset at the top).
+__device__ __forceinline__ bool lp_same_state(const lds_lp *P, const uint64_t *xe, const uint64_t *fr, uint64_t stride,
+                                              bool fp) {
+    if ((P->fp0 != 0) != fp) return false;
+    for (uint32_t r = 1; r < 32; r++)
+        if (P->r0[r] != xe[r]) return false;
+    if (fp)
+        for (uint32_t f = 0; f < 32; f++)
+            if (P->f0[f] != fr[(uint64_t)f * stride]) return false;
+    return true;
+}
 __device__ __noinline__ bool lp_prove(const lds_lp *P, const uint64_t *xe, const uint64_t *fr, uint64_t stride,
                                       bool fp) {
     const uint32_t n = P->n;
@@ -1960,7 +1974,7 @@ __device__ __noinline__ bool lp_prove(const lds_lp *P, const uint64_t *xe, const
     uint64_t cur = inv;
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t e = P->e[i], kind = e >> 28;
-        if (kind != kLpPure && kind != kLpConst && !lp_src_ok(e, cur)) return false;
+        if (kind != kLpPure && kind != kLpConst && !lp_src_ok(e, cur)) return lp_same_state(P, xe, fr, stride, fp);
         cur = lp_step(e, cur);
     }
     const uint64_t chk = W & inv;
@@ -1968,7 +1982,7 @@ __device__ __noinline__ bool lp_prove(const lds_lp *P, const uint64_t *xe, const
         if (!((chk >> r) & 1)) continue;
         const uint64_t a = r < 32 ? P->r0[r] : P->f0[r - 32];
         const uint64_t b = r < 32 ? xe[r] : (fp ? fr[(uint64_t)(r - 32) * stride] : 0ULL);
-        if (a != b) return false;
+        if (a != b) return lp_same_state(P, xe, fr, stride, fp);
     }
     return true;
 }
