@@ -4218,7 +4218,19 @@ __device__ __forceinline__ void trial_body() {
                     const uint64_t rem64 = next_ev - L.ninst;
                     const uint32_t rem = rem64 > (1u << 30) ? (1u << 30) : (uint32_t)rem64;
                     const uint32_t wbud = CX->wave_budget ? CX->wave_budget - n_iter : (1u << 30);
-                    const uint32_t bud = rem < wbud ? rem : wbud;
+                    uint32_t bud = rem < wbud ? rem : wbud;
+                    // odd-pc streams: a trial past the golden run's length can only
+                    // end by a crash or at the hang cap, and the static proofs do
+                    // not cover these streams -- its translated instructions count
+                    // toward a loop probe, and a call returns at the golden length and
+                    // when the probe is due (qsort's odd-pc hangs ran 228k translated
+                    // instructions to the cap)
+                    if (kOdd && CX->hang_proof && LP_ELIGIBLE) {
+                        const uint32_t due = L.ninst < CX->gninst
+                                                 ? (uint32_t)(CX->gninst - L.ninst + 1 < bud ? CX->gninst - L.ninst + 1 : bud)
+                                                 : (LP.at > LP.cnt ? LP.at - LP.cnt : 1u);
+                        bud = due < bud ? due : bud;
+                    }
                     // rewritten code bytes as offsets from the text base (empty range if none)
                     const uint64_t tlo = CX->text_lo;
                     __shared__ SoloTxIO sio[1];
@@ -4250,6 +4262,10 @@ __device__ __forceinline__ void trial_body() {
                     n_iter += st;
                     n_tx += st;
                     n_txin++;
+                    if (kOdd && L.ninst > CX->gninst && !uni32(sio->hang)) {
+                        LP.cnt += st;
+                        if (LP.cnt >= LP.at) lp_count((lds_lp *)&LP, CX, (const lds_u64 *)R, slot, L.pc, L.fp, LP_ELIGIBLE, 0u);
+                    }
                     if (uni32(sio->hang)) {   // a loop that cannot leave before the cap
                         uint64_t kf = 0, fva = 0;
                         const uint64_t left = L.ninst < CX->hang_cap ? CX->hang_cap - L.ninst : 0;

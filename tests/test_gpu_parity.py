@@ -914,6 +914,30 @@ def test_odd_pc_kernel(engine_factory, oracle_mod, name):
     compare(a, oracle_for(oracle_mod, name).run_trials(sites, protect_mask=0), sites)
 
 
+def test_odd_stream_loop_proofs(engine_factory, oracle_mod):
+    """pc bit-0 flips that land in a loop of odd-pc instructions run the
+    translated odd-pc streams (solo-odd kernel), which the static proofs do
+    not cover.  Past the golden run's length such a trial can only crash or
+    hang: its translated calls return at the golden length and whenever a
+    loop probe is due, and the probe proves the hang (qsort 80709 / 32646:
+    a store loop whose values converge).  Records equal the engine's own
+    without proofs and the oracle's (which runs them to the cap)."""
+    from shrewd_amd.fi import CFG_NO_HANG_PROOF
+    ids = [80709, 32646, 37937, 68608]
+    on = engine_factory("qsort")
+    off = engine_factory("qsort", flags=CFG_NO_HANG_PROOF)
+    for e in (on, off):
+        e.set_campaign(0x5EED0002, REGS | PC, 1)
+        e.set_protect(0)
+    sites = on.sample(0, max(ids) + 1)[ids]
+    a, _ = on.run_sites(sites)
+    assert int(on.debug_stats()[59]) >= 2
+    b, _ = off.run_sites(sites)
+    assert np.array_equal(a, b)
+    assert (a["cls"][:2] == 3).all()
+    compare(a, oracle_for(oracle_mod, "qsort").run_trials(sites, protect_mask=0), sites)
+
+
 @pytest.mark.parametrize("name,seed,ids", [("qsort", 0x5EED0002, [11487, 46948]),
                                           ("intmix", 0x5EED0002, [64617, 53499, 34535]),
                                           ("qsort", 0x5EED0003, [631236, 934410, 140047, 644543, 802705])])

@@ -36,7 +36,7 @@ for i in ids:
            "ns_per_inst": round(ms * 1e6 / max(xi, 1), 1), "translated": int(st[16]), "tx_entries": int(st[17]),
            "slow_fetches": int(st[8]), "iters": int(st[6]), "trips": int(st[9]),
            "fast_calls": int(st[53]), "fast_insts": int(st[54]), "fast_backs": int(st[55]),
-           "proofs_56_61": [int(x) for x in st[56:62]]}
+           "proofs_56_63": [int(x) for x in st[56:64]]}
     if os.environ.get("SHREWD_FI_LIB"):
         rec["cycles_per_iter_by_stamp"] = [round(int(st[32 + k]) / max(1, int(st[6])), 1) for k in range(8)]
         rec["stats_32_40"] = [int(x) for x in st[32:40]]
