@@ -7,9 +7,7 @@ set -o pipefail
 TAG=${1:-r05}
 mkdir -p gpurun_out
 export SHREWD_FI_JIT_CACHE=$PWD/gpurun_out/jitcache LS_TOP=4
-bash tools/gpu/gpu_tests.sh ${TAG}_chunks "chunking or resource_redo or m5_simulator or smoke or full_size" &&
-timeout -k 10 300 python -u bench.py --workloads "" --no-cpu-baseline --steps 10 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err &&
+bash tools/gpu/gpu_tests.sh ${TAG}_chunks "chunking or resource_redo" &&
 timeout -k 10 200 python -u tools/gpu/launch_size.py qsort 1000000 0x5EED0003 1000000 100000 > gpurun_out/${TAG}_ls.jsonl 2> gpurun_out/${TAG}_ls.err &&
-timeout -k 10 200 python -u tools/gpu/slow_trials.py qsort 0x5EED0003 regs_pc 631236 > gpurun_out/${TAG}_slow631236.jsonl 2>&1 &&
 cd /tmp && export TMPDIR=/tmp &&
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/${TAG}_trace -o run -- python3 -u $GRAFT_REPO_ROOT/tools/gpu/launch_size.py qsort 1000000 0x5EED0003 100000 > $GRAFT_REPO_ROOT/gpurun_out/${TAG}_trace.log 2>&1
