@@ -56,7 +56,7 @@ hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome
                                hipStream_t st);
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
                             uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, uint32_t solo,
-                            uint64_t golden_ninst, hipStream_t st);
+                            uint64_t golden_ninst, uint32_t nb, hipStream_t st);
 hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,
                             hipStream_t st);
 std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
@@ -1551,9 +1551,13 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
             // (fi_surv_keys_kernel; profiles/r04au: intmix -3 %, qsort -3 %
             // per step against the two-tier order)
             const uint32_t skey = (solo && !pack) ? 3u : 0u;
+            // solo keys: tier above numInst, which stays below the hang cap -- a
+            // key of nb + 2 bits (+ 1 for the odd-pc flag) sorts in fewer passes
+            const uint32_t nb = 64u - (uint32_t)__builtin_clzll(std::max<uint64_t>(c.hang_cap, 1));
             HIPCHK(launch_surv_keys(e->d_save, e->d_surv[(ep - 1) & 1], e->d_cnt + ep - 1, k, c.text_lo, e->d_skeys,
-                                    e->d_svals, odd ? e->d_split + 4 * ep : nullptr, skey, e->golden.ninst, st));
-            HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_skeys, e->d_skeys2, e->d_svals, e->d_svals2, k, 64, st));
+                                    e->d_svals, odd ? e->d_split + 4 * ep : nullptr, skey, e->golden.ninst, nb, st));
+            HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_skeys, e->d_skeys2, e->d_svals, e->d_svals2, k,
+                              skey ? (int)std::min(64u, nb + 3u) : 64, st));
             c.resume = e->d_svals2;
             c.resume_n = e->d_cnt + ep - 1;
             if (odd) {   // odd survivors sort last: the solo kernel takes [0, split), the solo-odd kernel the rest

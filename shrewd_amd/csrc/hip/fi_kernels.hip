@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(256) fi_hist_kernel(const fi_site *sites, cons
 // ~20x the cost of translated code) start first, then the rest longest-first.
 __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
                                     uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd,
-                                    uint32_t solo, uint64_t golden_ninst) {
+                                    uint32_t solo, uint64_t golden_ninst, uint32_t nb) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cap) return;
     if (i < *cnt) {
@@ -250,10 +250,12 @@ __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, 
             // (solo bit 1: survivors not yet injected -- their outcome still
             // unknown -- form a tier of their own after the first)
             const bool uninj = (solo & 2u) && ((save[sl].flags >> 1) & 3) == 0;
-            k = ((uint64_t)(first ? 0 : uninj ? 1 : 2) << 61) | (save[sl].ninst & ((1ULL << 46) - 1));
+            // (nb: the bits of the hang cap, above every survivor's numInst --
+            // the key then sorts in nb + 2 (+ 1 odd) bits: fewer radix passes)
+            k = ((uint64_t)(first ? 0 : uninj ? 1 : 2) << nb) | save[sl].ninst;
         }
         if (n_odd) {
-            k = ((pc & 1) << 63) | (k >> 1);
+            k = solo ? (((pc & 1) << (nb + 2)) | k) : (((pc & 1) << 63) | (k >> 1));
             if (pc & 1) atomicAdd(n_odd, 1u);
         }
         keys[i] = k;
@@ -383,9 +385,9 @@ hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome
 }
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
                             uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, uint32_t solo,
-                            uint64_t golden_ninst, hipStream_t st) {
+                            uint64_t golden_ninst, uint32_t nb, hipStream_t st) {
     hipLaunchKernelGGL(fi_surv_keys_kernel, dim3(nblk(cap, 256)), dim3(256), 0, st, save, list, cnt, cap, text_lo,
-                       keys, vals, n_odd, solo, golden_ninst);
+                       keys, vals, n_odd, solo, golden_ninst, nb);
     return hipGetLastError();
 }
 hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,
