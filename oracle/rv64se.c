@@ -273,8 +273,17 @@ typedef struct {
     u64 *dbg_pc, dbg_pc_n, dbg_pc_cap, *dbg_wr, dbg_wr_n, dbg_wr_cap;
     int dbg_raw;   /* or_debug_trace_raw: pc | instruction word << 32 */
     int m5x, m5code;   /* an M5 op that ends the run after it commits: 1 m5_exit, 2 m5_fail, 3 quiesce */
+    /* the vector configuration of the PC state (riscv/pcstate.hh: _vtype, _vl)
+     * as VCFG(vtype, vl) -- 0 is the process start (vtype = vill, vl = 0) */
+    u32 vcfg;
     const or_campaign_t *c;
 } mach_t;
+/* vcfg <-> (vtype, vl): a vtype that getNewVtype produces is vill alone, a
+ * legal vtype8, or (vsetvl's register) a legal vtype8 with bit 63 set */
+#define VILL (1ULL << 63)
+static u32 vcfg_of(u64 vtype, u32 vl) { return ((u32)(vtype & 0xFF) | (u32)(vtype >> 63) << 8 | vl << 9) ^ 0x100u; }
+static u64 vcfg_vtype(u32 vcfg) { vcfg ^= 0x100u; return (u64)(vcfg & 0xFF) | (u64)((vcfg >> 8) & 1) << 63; }
+static u32 vcfg_vl(u32 vcfg) { return vcfg >> 9; }
 
 enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_ESCAPE = 5, F_PGFAULT = 6, F_AMOLINE = 7,
        F_SCLINE = 8, F_M5PANIC = 9, F_UNDEF = 10, F_VSEW = 11 };
@@ -449,13 +458,14 @@ static void decode(u32 raw, dec_t *d) {
     if (d->op == OP_vec && d->imm == VEC_STATE && bits(raw, 6, 0) == 0x57 && bits(raw, 14, 12) == 7) {
         /* vsetvli / vsetvl / vsetivli (decoder.isa:5838-5886): imm = the
          * requested vtype's immediate | form << 16 (0 vsetvli, 1 vsetvl: vtype
-         * from Rs2, 2 vsetivli); Rd written, Rs1 (and Rs2) read */
+         * from Rs2, 2 vsetivli: its uimm << 20); Rd written, Rs1 (and Rs2) read */
         const int form = bits(raw, 31, 31) ? (bits(raw, 30, 30) ? 2 : 1) : 0;
         d->op = OP_vset;
         d->rd = (int)bits(raw, 11, 7);
         d->rs1 = form == 2 ? -1 : (int)bits(raw, 19, 15);
         d->rs2 = form == 1 ? (int)bits(raw, 24, 20) : -1;
-        d->imm = (form == 0 ? (s64)bits(raw, 30, 20) : form == 2 ? (s64)bits(raw, 29, 20) : 0) | ((s64)form << 16);
+        d->imm = (form == 0 ? (s64)bits(raw, 30, 20) : form == 2 ? (s64)bits(raw, 29, 20) : 0) | ((s64)form << 16) |
+                 (form == 2 ? (s64)bits(raw, 19, 15) << 20 : 0);
     }
 }
 /* The executed members of the LOAD-FP / STORE-FP / OP-FP / AMO groups, among
@@ -2224,6 +2234,7 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
 #endif
     /* ---- RVV before any vset* (decode: op vec) */
     case OP_vec:
+        if (m->vcfg) return F_ESCAPE;   /* decoded under another vtype / vl: the vector unit's state */
         switch ((int)imm) {
         case VEC_NOP: goto no_rd;
         case VEC_NOP2: m->num_cycles += 1; goto no_rd;   /* the trailing micro-op's tick */
@@ -2231,27 +2242,43 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
         case VEC_UNDEF: return F_UNDEF;
         default: return F_ESCAPE;
         }
-    /* ---- vset* from the process-start vector state (vtype = vill, vl = 0,
-     * decoder.hh:68-69; every other state escapes, so this is the only
-     * one): VConfOp::execute (formats/vector_conf.isa:115-186).  A request
-     * other than the current vtype is checked by getNewVtype, whose getSew
-     * asserts vsew <= 3 (insts/vector.hh:52-56: gem5.opt aborts); an illegal
-     * one -- LMUL outside [1/8, 8] (vlmul 4: 1/16), SEW > min(LMUL, 1) x ELEN
-     * (ELEN 64, RiscvISA.py:103), reserved bits 62..8 set -- gives vtype =
-     * vill and VLMAX 0, so vl = 0 and the state stays the start state; rd
-     * gets vl.  A legal vtype needs the vector unit's state: escape. */
+    /* ---- vset*: VConfOp::execute (formats/vector_conf.isa:115-186; the
+     * operands at decoder.isa:5838-5886).  getNewVtype: a request other than
+     * the current vtype is checked -- getSew asserts vsew <= 3
+     * (insts/vector.hh:52-56: gem5.opt aborts); LMUL outside [1/8, 8] (vlmul
+     * 4: 1/16), SEW > min(LMUL, 1) x ELEN (ELEN 64, RiscvISA.py:103) or
+     * reserved bits 62..8 set give vtype = vill.  VLMAX = VLEN / SEW x LMUL
+     * (getVlmax, insts/vector.cc:69-76; VLEN 256, RiscvISA.py:98), 0 under
+     * vill.  getNewVL takes the requested vl as uint32_t and picks by the
+     * rd / rs1 register indices (vsetivli: rs1 "-1").  rd gets vl; the new
+     * configuration is the decoder's from the next instruction on
+     * (decoder.cc:155-163). */
     case OP_vset: {
-        const int form = (int)(imm >> 16);
+        const int form = (int)((imm >> 16) & 3);
         const u64 req = form == 1 ? b : (u64)(imm & 0xFFFF);
-        const u64 vill = 1ULL << 63;
-        if (req != vill) {
+        const u64 old = vcfg_vtype(m->vcfg);
+        u64 nt = old;
+        if (req != old) {
             const u32 vsew = (u32)(req >> 3) & 7, vlmul = (u32)req & 7;
             if (vsew > 3) return F_VSEW;
             const u32 lim = vlmul <= 3 ? 64 : vlmul == 5 ? 8 : vlmul == 6 ? 16 : vlmul == 7 ? 32 : 0;
             const int illegal = vlmul == 4 || (8u << vsew) > lim || ((req >> 8) & ((1ULL << 55) - 1)) != 0;
-            if (!illegal) return F_ESCAPE;
+            nt = illegal ? VILL : req;
         }
-        v = 0;
+        u32 vlmax = 0;
+        if (!(nt >> 63)) {
+            const u32 vsew = (u32)(nt >> 3) & 7, vlmul = (u32)nt & 7, per = 32u >> vsew;
+            vlmax = vlmul <= 3 ? per << vlmul : per >> (8 - vlmul);
+        }
+        const u32 rs1_bits = form == 2 ? 1u : (u32)d->rs1, req_vl = form == 2 ? (u32)(imm >> 20) : (u32)a;
+        const u32 cur = vcfg_vl(m->vcfg);
+        u32 nvl = 0;
+        if (vlmax == 0) nvl = 0;
+        else if (d->rd == 0 && rs1_bits == 0) nvl = cur > vlmax ? vlmax : cur;
+        else if (d->rd != 0 && rs1_bits == 0) nvl = vlmax;
+        else nvl = req_vl > vlmax ? vlmax : req_vl;
+        m->vcfg = vcfg_of(nt, nvl);
+        v = nvl;
         break;
     }
     /* ---- privileged SYSTEM / hypervisor load-store from PRV_U (refine_misc) */

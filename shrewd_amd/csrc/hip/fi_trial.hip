@@ -149,6 +149,7 @@ struct LaneMem {
     // lock record stays on the general path, whose stores erase it.
     uint64_t resv, lock;
     bool vm;                       // VmState of the slot is live (the trial made a VM syscall)
+    uint32_t vcfg;                 // vector configuration (vtype, vl) as oracle/rv64se.c vcfg_of; 0 = process start
     uint32_t nmiss;                // diagnostics: full page-table lookups (TLB misses)
     uint32_t *dl;                  // solo kernel: LDS copy of the slot's rewritten-code map (else NULL)
 };
@@ -3730,6 +3731,7 @@ __device__ __forceinline__ void trial_body() {
     m.dlo = m.dhi = 0;
     m.resv = m.lock = kNone;
     m.vm = false;
+    m.vcfg = 0;
     m.nmiss = 0;
     if (CX->ov_blocks && live && !resume) CX->ov_of[slot] = 0xFFFFFFFFu;   // no overflow block yet
     // the solo kernel's LDS copy of the slot's rewritten-code map
@@ -3748,6 +3750,7 @@ __device__ __forceinline__ void trial_body() {
         L.next_chk = SV->next_chk; L.nfail = SV->nfail; L.watch = SV->watch;
         L.out_bad = SV->flags & 1; L.injected = (uint8_t)((SV->flags >> 1) & 3); L.fp = (SV->flags >> 4) & 1;
         L.fflags = (uint8_t)(SV->pad & 0x1F); L.frm = (uint8_t)((SV->pad >> 5) & 7);
+        m.vcfg = SV->pad >> 8;
         m.stack_min = SV->stack_min; m.n_priv = SV->n_priv; m.code_dirty = (SV->flags >> 3) & 1;
         m.dlo = CX->code_lo + SV->dlo; m.dhi = CX->code_lo + SV->dhi;
         m.resv = SV->resv; m.lock = SV->lock;
@@ -3860,7 +3863,7 @@ __device__ __forceinline__ void trial_body() {
                 sv->flags = (L.out_bad ? 1u : 0u) | ((uint32_t)L.injected << 1) | (m.code_dirty ? 8u : 0u) |
                             (L.fp ? 16u : 0u) | (m.vm ? 32u : 0u);
                 sv->resv = m.resv; sv->lock = m.lock;
-                sv->pad = (uint32_t)L.fflags | ((uint32_t)L.frm << 5);
+                sv->pad = (uint32_t)L.fflags | ((uint32_t)L.frm << 5) | (m.vcfg << 8);
                 if (m.dl && m.code_dirty)   // the solo kernel's map lives in LDS
                     for (uint32_t i = 0; i < CX->dmap_words; i++) CX->dmap[slot * CX->dmap_words + i] = m.dl[i];
                 if (kSoloOnce) CX->surv[atomicAdd(CX->surv_n, 1u)] = (uint32_t)slot;
@@ -3959,7 +3962,7 @@ __device__ __forceinline__ void trial_body() {
                 bool eq = grp && L.pc == S->pc && L.out_pos == S->out_pos && L.err_pos == S->err_pos &&
                           (!L.out_bad || (CX->early_exit & 2)) &&
                           m.stack_min == S->stack_min && !L.fp && L.injected != 3 && m.resv == kNone &&
-                          m.lock == kNone && !m.vm &&
+                          m.lock == kNone && !m.vm && !m.vcfg &&
                           // the golden suffix reads curTick: the same future needs the same tick count
                           // too (a path with other non-counting ticks -- ecalls, straddled fetches --
                           // reconverges with the same numInst but would print another time)
@@ -4778,6 +4781,7 @@ __device__ __forceinline__ void trial_body() {
         uint32_t cbo = 0;             // cache-block op: 1 translate only, 2 zero the line
         bool m5 = false;              // M5Op: a1 = 0 at commit
         uint32_t m5x = 0, m5code = 0; // an M5 op that ends the run once it commits: 1 exit, 2 fail, 3 quiesce
+        uint32_t nvcfg = ~0u;         // vset*: the vector configuration from the next instruction on
         bool xdet = false;            // a replica watch read through an M5Op's ABI arguments
 #define FREG_RD(r) (L.fp ? CX->fregs[(uint64_t)(r) * CX->n_slots + slot] : 0ULL)
         // detected-by-replica: the flipped protected register is read before
@@ -5072,29 +5076,48 @@ __device__ __forceinline__ void trial_body() {
                 break;
             }
             case OP_crypto: v = rvk::exec(d.imm, a, b); break;
-            // RVV before any vset* (oracle/rv64se.c VEC_*): no-op (one or two
-            // micro-op ticks), IllegalInst (vill), undefined in gem5, needs vector state
+            // RVV in the process-start vector configuration (oracle/rv64se.c
+            // VEC_*): no-op (one or two micro-op ticks), IllegalInst (vill),
+            // undefined in gem5, needs vector state; under any other
+            // configuration it needs the vector unit's state (escape)
             case OP_vec:
                 wrd = false;
-                if (d.imm == 3) xticks = 1;
+                if (m.vcfg) f = F_ESCAPE;
+                else if (d.imm == 3) xticks = 1;
                 else if (d.imm == 4) f = F_ILLEGAL;
                 else if (d.imm == 5) f = F_UNDEF;
                 else if (d.imm == 6) f = F_ESCAPE;
                 break;
-            // vset* from the start vector state (oracle/rv64se.c OP_vset,
-            // formats/vector_conf.isa:115-186): vsew > 3 trips getSew's assert;
-            // an illegal vtype leaves the start state (vill, vl 0) and rd = 0;
-            // a legal one needs the vector unit's state (escape)
+            // vset* (oracle/rv64se.c OP_vset; formats/vector_conf.isa:115-186):
+            // getNewVtype (a request other than the current vtype: vsew > 3
+            // trips getSew's assert, an illegal one gives vill), VLMAX =
+            // VLEN 256 / SEW x LMUL, getNewVL on the rd / rs1 indices with a
+            // uint32_t requested vl; rd = vl, the configuration from the next
+            // instruction on (committed with the instruction)
             case OP_vset: {
-                const uint32_t form = (uint32_t)d.imm >> 16;
+                const uint32_t form = ((uint32_t)d.imm >> 16) & 3u;
                 const uint64_t req = form == 1 ? b : (uint64_t)((uint32_t)d.imm & 0xFFFFu);
-                if (req != (1ULL << 63)) {
+                const uint32_t vc = m.vcfg ^ 0x100u;
+                const uint64_t old = (uint64_t)(vc & 0xFF) | ((uint64_t)((vc >> 8) & 1) << 63);
+                uint64_t nt = old;
+                if (req != old) {
                     const uint32_t vsew = (uint32_t)(req >> 3) & 7, vlmul = (uint32_t)req & 7;
                     const uint32_t lim = vlmul <= 3 ? 64 : vlmul == 5 ? 8 : vlmul == 6 ? 16 : vlmul == 7 ? 32 : 0;
-                    if (vsew > 3) f = F_VSEW;
-                    else if (vlmul != 4 && (8u << vsew) <= lim && ((req >> 8) & ((1ULL << 55) - 1)) == 0) f = F_ESCAPE;
+                    if (vsew > 3) { f = F_VSEW; break; }
+                    nt = (vlmul == 4 || (8u << vsew) > lim || ((req >> 8) & ((1ULL << 55) - 1)) != 0) ? (1ULL << 63) : req;
                 }
-                v = 0;
+                uint32_t vlmax = 0;
+                if (!(nt >> 63)) {
+                    const uint32_t vsew = (uint32_t)(nt >> 3) & 7, vlmul = (uint32_t)nt & 7, per = 32u >> vsew;
+                    vlmax = vlmul <= 3 ? per << vlmul : per >> (8 - vlmul);
+                }
+                const uint32_t rs1b = form == 2 ? 1u : d.rs1, rqvl = form == 2 ? ((uint32_t)d.imm >> 20) : (uint32_t)a;
+                const uint32_t cur = vc >> 9;
+                const uint32_t nvl = vlmax == 0 ? 0u
+                                   : (d.rd == 0 && rs1b == 0) ? (cur < vlmax ? cur : vlmax)
+                                   : rs1b == 0 ? vlmax : (rqvl < vlmax ? rqvl : vlmax);
+                nvcfg = ((uint32_t)(nt & 0xFF) | ((uint32_t)(nt >> 63) << 8) | (nvl << 9)) ^ 0x100u;
+                v = nvl;
                 break;
             }
             default: f = F_UNKNOWN; break;
@@ -5161,6 +5184,10 @@ __device__ __forceinline__ void trial_body() {
                 if (fpst & 0x200u) { L.fflags = (uint8_t)(fpst & 0x1F); L.frm = (uint8_t)((fpst >> 5) & 7); }
             }
             L.ncyc += xticks;
+            if (nvcfg != ~0u) {
+                m.vcfg = nvcfg;
+                if (CX->record && nvcfg) CX->stats[22] = 1;   // golden vector state is not in the snapshots
+            }
             bool rdet = false;
             if (L.injected == 3) {   // result fault (oracle/rv64se.c:result_fault)
                 if (!(wrd && d.rd)) L.injected = 2;

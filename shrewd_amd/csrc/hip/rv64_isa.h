@@ -573,14 +573,15 @@ __device__ inline Dec rv_decode(uint32_t raw) {
     if ((raw & 3) == 3) rv_refine_misc(raw, d);
     // vsetvli / vsetvl / vsetivli out of the vector-state class (oracle/rv64se.c
     // decode, decoder.isa:5838-5886): imm = the requested vtype's immediate |
-    // form << 16 (0 vsetvli, 1 vsetvl: vtype from Rs2, 2 vsetivli)
+    // form << 16 (0 vsetvli, 1 vsetvl: vtype from Rs2, 2 vsetivli: its uimm << 20)
     if (d.op == OP_vec && d.imm == 6 && (raw & 0x7F) == 0x57 && fbits(raw, 14, 12) == 7) {
         const uint32_t form = fbits(raw, 31, 31) ? (fbits(raw, 30, 30) ? 2u : 1u) : 0u;
         d.op = OP_vset;
         D_RD(fbits(raw, 11, 7));
         if (form != 2) D_RS1(fbits(raw, 19, 15));
         if (form == 1) D_RS2(fbits(raw, 24, 20));
-        d.imm = (int32_t)((form == 0 ? fbits(raw, 30, 20) : form == 2 ? fbits(raw, 29, 20) : 0u) | (form << 16));
+        d.imm = (int32_t)((form == 0 ? fbits(raw, 30, 20) : form == 2 ? fbits(raw, 29, 20) : 0u) | (form << 16) |
+                          (form == 2 ? fbits(raw, 19, 15) << 20 : 0u));
     }
     return d;
 }

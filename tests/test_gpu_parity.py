@@ -581,7 +581,7 @@ def test_native_driver_matches_engine(engine_factory, tmp_path):
 
 
 @pytest.mark.parametrize("prog", ["alu", "mem", "cmp", "rvc", "sys", "lrsc", "vm", "fp", "rnd", "xop", "sys2", "clk",
-                                  "stdin", "vset"])
+                                  "stdin", "vset", "vcfg"])
 def test_known_answer_programs(oracle_mod, prog):
     """Known answers on the device (guest programs of tests/test_isa_vectors.py).
 
@@ -604,7 +604,9 @@ def test_known_answer_programs(oracle_mod, prog):
     xop: scalar crypto, Zfa (fli / fround / fcvtmod.w.d), M5 pseudo-ops, the
     warn-only privileged no-ops and the cache-block ops.
     sys2: read, readlinkat (/proc/self/exe) and riscv_hwprobe.
-    vset: vset* with illegal vtype requests from the start vector state.  The device golden run (general interpreter)
+    vset: vset* with illegal vtype requests from the start vector state.
+    vcfg: vset* chains through legal vector configurations (AVL, VLMAX, the
+    kept vl of x0, x0, uint32_t AVL truncation, vsetvl's vill bit).  The device golden run (general interpreter)
     must print exactly the reference-derived models; no-fault trials
     (pre-decoded and translated paths, from snapshots) must end masked with
     the oracle's records; faulted trials must match the oracle bit for bit."""
@@ -623,7 +625,8 @@ def test_known_answer_programs(oracle_mod, prog):
                      "sys2": (kat.sys2_program_elf, kat.sys2_program_expected),
                      "clk": (kat.clk_program_elf, kat.clk_program_expected),
                      "stdin": (kat.stdin_program_elf, kat.stdin_program_expected),
-                     "vset": (kat.vset_program_elf, kat.vset_program_expected)}[prog]
+                     "vset": (kat.vset_program_elf, kat.vset_program_expected),
+                     "vcfg": (kat.vcfg_program_elf, kat.vcfg_program_expected)}[prog]
     if prog in ("fp", "xop") and not oracle_mod.has_softfloat():
         pytest.skip("oracle without the reference SoftFloat")
     if prog == "xop" and not oracle_mod.has_rvk():

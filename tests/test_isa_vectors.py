@@ -1734,18 +1734,20 @@ def test_fli_probe_matches_reference_table(oracle_mod):
 def test_vector_actions_before_vset(oracle_mod):
     """RVV before any vset* (gen_vector_actions.py): vill-checking classes raise
     IllegalInst, floating-point classes reach GEM5_UNREACHABLE at SEW = 8
-    (escape), vset* and whole-register moves need vector state (escape)."""
+    (escape), whole-register moves need vector state (escape); a legal vset*
+    executes (rd = VLMAX here)."""
     P = oracle_mod.probe
     regs = [0] * 32
     cases = {0x622180d7: ("vector:4", 3),    # vmseq.vv: the first micro-op checks vill
              0x422020d7: ("vector:4", 3),    # vmv.x.s x1, v2 (non-split)
              0x02219057: ("vector:5", 5),    # vfadd.vv: no SEW = 8 instantiation
-             0x0c0071d7: ("vsetvli", 5),     # vsetvli x3, x0, e8, m1, ta, ma: a legal vtype needs vector state
+             0x0c0071d7: ("vsetvli", 0),     # vsetvli x3, x0, e8, m1, ta, ma: rd = VLMAX = 32
              0x02828087: ("vector:6", 5),    # vl1re8.v (whole register)
              0x02218057: ("vector:2", 0)}    # vadd.vv: a no-op at vl = 0
     for w, (name, fault) in cases.items():
         assert oracle_mod.mnemonic(w) == name, (hex(w), oracle_mod.mnemonic(w))
         assert P(w, 0x1000, regs).fault == fault, hex(w)
+    assert P(0x0c0071d7, 0x1000, regs).rd_value == 32
 
 
 def _vsetvli(rd, rs1, zimm):
@@ -1760,31 +1762,79 @@ def _vsetvl(rd, rs1, rs2):
     return (1 << 31) | (rs2 << 20) | (rs1 << 15) | (7 << 12) | (rd << 7) | 0x57
 
 
+VILL = 1 << 63
+
+
+def vset_model(vtype, vl, form, rd, rs1, req, avl):
+    """VConfOp::execute (formats/vector_conf.isa:115-186) restated: the new
+    (vtype, vl), or None where getSew's assert (vsew > 3) aborts.  form 0
+    vsetvli (req = zimm11, avl = x[rs1]), 1 vsetvl (req = x[rs2]), 2 vsetivli
+    (req = zimm10, avl = uimm, rs1 taken as nonzero).  VLEN 256, ELEN 64."""
+    nt = vtype
+    if req != vtype:
+        vsew, vlmul = (req >> 3) & 7, req & 7
+        if vsew > 3:
+            return None
+        lmul = {0: 1, 1: 2, 2: 4, 3: 8, 5: 1 / 8, 6: 1 / 4, 7: 1 / 2}.get(vlmul, 1 / 16)
+        sew = 8 << vsew
+        illegal = not (0.125 <= lmul <= 8) or sew > min(lmul, 1.0) * 64 or (req >> 8) & ((1 << 55) - 1)
+        nt = VILL if illegal else req
+    vlmax = 0 if nt >> 63 else int((256 // (8 << ((nt >> 3) & 7))) *
+                                   {0: 1, 1: 2, 2: 4, 3: 8, 5: 1 / 8, 6: 1 / 4, 7: 1 / 2}[nt & 7])
+    rs1_bits = 1 if form == 2 else rs1
+    req_vl = avl & 0xFFFFFFFF
+    if vlmax == 0:
+        nvl = 0
+    elif rd == 0 and rs1_bits == 0:
+        nvl = min(vl, vlmax)
+    elif rs1_bits == 0:
+        nvl = vlmax
+    else:
+        nvl = min(req_vl, vlmax)
+    return nt, nvl
+
+
+def _vset_word_model(w, regs, vtype=VILL, vl=0):
+    rd, rs1, rs2 = (w >> 7) & 31, (w >> 15) & 31, (w >> 20) & 31
+    form = 0 if not w >> 31 else 2 if (w >> 30) & 1 else 1
+    req = (w >> 20) & 0x7FF if form == 0 else regs[rs2] if form == 1 else (w >> 20) & 0x3FF
+    avl = rs1 if form == 2 else (regs[rs1] if rs1 else 0)
+    return vset_model(vtype, vl, form, rd, rs1, req, avl)
+
+
 def test_vset_from_the_start_state(oracle_mod):
     """vset* (formats/vector_conf.isa:115-186) from the process-start state
-    (vtype = vill, vl = 0): a request equal to the current vtype or an
-    illegal one (LMUL 1/16, SEW > min(LMUL, 1) x ELEN, reserved bits) leaves
-    that state and writes vl = 0 to rd; vsew > 3 trips getSew's assert
-    (abort: fault 11, crash sub-code 14); a legal vtype -- including one whose
-    vill bit came from vsetvl's register -- escapes."""
+    (vtype = vill, vl = 0) against the restated model: a request equal to the
+    current vtype or an illegal one (LMUL 1/16, SEW > min(LMUL, 1) x ELEN,
+    reserved bits) leaves that state and writes vl = 0 to rd; vsew > 3 trips
+    getSew's assert (abort: fault 11, crash sub-code 14); a legal vtype
+    writes rd = the new vl (AVL, VLMAX or the uint32_t truncation of x[rs1])."""
     P = oracle_mod.probe
     regs = [0] * 32
     regs[6], regs[7] = 5, 0x1234
-    for w, fault in ((_vsetvli(7, 6, 0x100), 0), (_vsetvli(7, 0, 0x004), 0), (_vsetvli(7, 6, 0x01D), 0),
-                     (_vsetvli(7, 6, 0x00D), 0), (_vsetivli(7, 31, 0x104), 0), (_vsetivli(7, 5, 0x016), 0),
-                     (_vsetvli(7, 6, 0x005), 5), (_vsetivli(7, 5, 0x00E), 5), (_vsetvli(7, 6, 0x0C0), 5),
-                     (_vsetvli(7, 6, 0x020), 11), (_vsetivli(7, 1, 0x3FF), 11), (_vsetvli(7, 6, 0x13C), 11)):
+    words = [_vsetvli(7, 6, 0x100), _vsetvli(7, 0, 0x004), _vsetvli(7, 6, 0x01D), _vsetvli(7, 6, 0x00D),
+             _vsetivli(7, 31, 0x104), _vsetivli(7, 5, 0x016), _vsetvli(7, 6, 0x005), _vsetivli(7, 5, 0x00E),
+             _vsetvli(7, 6, 0x0C0), _vsetvli(7, 6, 0x020), _vsetivli(7, 1, 0x3FF), _vsetvli(7, 6, 0x13C),
+             _vsetvli(7, 0, 0x018), _vsetvli(0, 0, 0x018), _vsetvli(7, 6, 0x0D3), _vsetivli(7, 31, 0x0C5),
+             _vsetivli(0, 3, 0x01F)]
+    faults = {}
+    for w in words:
         p = P(w, 0x1000, regs)
         assert oracle_mod.mnemonic(w) == ("vsetvli" if w >> 31 == 0 else "vsetivli"), hex(w)
-        assert p.fault == fault, (hex(w), p.fault)
-        if fault == 0:
-            assert p.rd == 7 and p.rd_value == 0, hex(w)
-    for t0, fault in ((1 << 63, 0), (1 << 62, 0), (0x104, 0), ((1 << 63) | 0x8, 5), (0x8, 5), (0x38, 11)):
-        regs[5] = t0
-        p = P(_vsetvl(7, 6, 5), 0x1000, regs)
-        assert p.fault == fault, (hex(t0), p.fault)
-        if fault == 0:
-            assert p.rd == 7 and p.rd_value == 0
+        m = _vset_word_model(w, regs)
+        assert p.fault == (11 if m is None else 0), (hex(w), p.fault)
+        if m is not None and (w >> 7) & 31:
+            assert p.rd == 7 and p.rd_value == m[1], (hex(w), p.rd_value, m)
+        faults[p.fault] = faults.get(p.fault, 0) + 1
+    assert faults == {0: 14, 11: 3}
+    for t0 in (1 << 63, 1 << 62, 0x104, (1 << 63) | 0x8, 0x8, 0x38, 0xC3, 1 << 8):
+        for avl in (0, 3, 1 << 32, (1 << 32) + 7, 1 << 20):
+            regs[5], regs[6] = t0, avl
+            p = P(_vsetvl(7, 6, 5), 0x1000, regs)
+            m = _vset_word_model(_vsetvl(7, 6, 5), regs)
+            assert p.fault == (11 if m is None else 0), (hex(t0), p.fault)
+            if m is not None:
+                assert p.rd == 7 and p.rd_value == m[1], (hex(t0), avl, p.rd_value, m)
 
 
 VSET_WORDS = [_vsetvli(7, 6, 0x100), _vsetvli(7, 0, 0x004), _vsetvli(7, 6, 0x01D), _vsetvli(7, 6, 0x00D),
@@ -1820,6 +1870,66 @@ def test_vset_program_on_oracle(oracle_mod):
     o = oracle_mod.Oracle(vset_program_elf(), "vset")
     g = o.run_golden()
     assert g.exit_code == 0 and o.golden_stdout() == vset_program_expected()
+
+
+# vset* chains through legal configurations: (t0 = vsetvl's vtype, t1 = AVL, word)
+VCFG_STEPS = [(0, 5, _vsetvli(7, 6, 0x000)),             # e8 m1, AVL 5 -> 5
+              (0, 0, _vsetvli(7, 0, 0x009)),             # e16 m2, rd != 0, rs1 = 0 -> VLMAX 32
+              (0, 0, _vsetvli(0, 0, 0x009)),             # the same vtype, x0, x0: vl kept
+              (0, 0, _vsetvli(0, 0, 0x010)),             # e32 m1, x0, x0: vl = min(vl, VLMAX 8)
+              (0, 0, _vsetvli(7, 0, 0x010)),             # -> VLMAX 8
+              (0, 0, _vsetivli(7, 31, 0x01B)),           # e64 m8, uimm 31 -> 31
+              (0xC2, (1 << 32) | 7, _vsetvl(7, 6, 5)),   # ta ma e8 m4, AVL truncated to uint32_t -> 7
+              (0xC2, 1 << 40, _vsetvl(7, 6, 5)),         # the same vtype, AVL truncates to 0 -> 0
+              (0, 1000, _vsetvli(7, 6, 0x005)),          # e8 mf8 -> VLMAX 4
+              (0, 3, _vsetvli(7, 6, 0x01F)),             # e64 mf2: SEW > LMUL x ELEN -> vill, 0
+              (0, 100, _vsetvli(7, 6, 0x003)),           # e8 m8 -> 100
+              (0, 0, _vsetvli(0, 0, 0x00B)),             # e16 m8, x0, x0: vl = min(100, 128)
+              (0, 300, _vsetivli(0, 17, 0x007)),         # e8 mf2, rd = 0: vl = 16 (not written)
+              ((1 << 63) | 3, 50, _vsetvl(7, 6, 5)),     # vsetvl with vill set on a legal vtype8: VLMAX 0
+              ((1 << 63) | 3, 9, _vsetvl(7, 6, 5)),      # the same (vill) vtype: no check, 0
+              (0, 9, _vsetvli(7, 6, 0x000)),             # e8 m1 -> 9
+              (0, 200, _vsetvli(7, 6, 0x0D1)),           # ta ma e16 m2 -> 32
+              (0, 9, _vsetvli(7, 6, 0x100))]             # reserved bit: vill, vl 0 (the start state again)
+
+
+def vcfg_program_source() -> str:
+    """vset* chains through legal vector configurations (each rd printed, -1
+    where rd = x0), then back to the start state and an RVV op that is a
+    no-op there."""
+    L = ["    .text", "_start:", "    la    s2, out", "    mv    s3, s2"]
+    for t0, t1, w in VCFG_STEPS:
+        L += [f"    li    t0, {t0 - (1 << 64) if t0 >> 63 else t0}", f"    li    t1, {t1}", "    li    t2, -1",
+              f"    .word {w:#x}", "    sd    t2, 0(s2)", "    addi  s2, s2, 8"]
+    L += ["    .word 0x02218057",                    # vadd.vv: a no-op in the start state
+          "    li    a0, 1", "    mv    a1, s3", "    sub   a2, s2, s3", "    li    a7, 64", "    ecall",
+          "    li    a0, 0", "    li    a7, 93", "    ecall", "    .bss", "    .balign 8", "out:", "    .zero 512"]
+    return "\n".join(L) + "\n"
+
+
+def vcfg_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(vcfg_program_source(), compress=False)
+
+
+def vcfg_program_expected() -> bytes:
+    vtype, vl, out = VILL, 0, b""
+    for t0, t1, w in VCFG_STEPS:
+        regs = [0] * 32
+        regs[5], regs[6], regs[7] = t0, t1, (1 << 64) - 1
+        vtype, vl = _vset_word_model(w, regs, vtype, vl)
+        out += (vl if (w >> 7) & 31 else (1 << 64) - 1).to_bytes(8, "little")
+    assert (vtype, vl) == (VILL, 0)
+    return out
+
+
+def test_vcfg_program_on_oracle(oracle_mod):
+    exp = vcfg_program_expected()
+    assert [int.from_bytes(exp[k:k + 8], "little") for k in range(0, len(exp), 8)][:9] == \
+        [5, 32, (1 << 64) - 1, (1 << 64) - 1, 8, 31, 7, 0, 4]
+    o = oracle_mod.Oracle(vcfg_program_elf(), "vcfg")
+    g = o.run_golden()
+    assert g.exit_code == 0 and o.golden_stdout() == exp
 
 
 # ---------------------------------------------------------------- m5end program
