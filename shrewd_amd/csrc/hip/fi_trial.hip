@@ -3605,9 +3605,12 @@ leave:
 // instructions four times running stays in the interpreter: if it rewrote
 // code, for the next FI_TX_SKIP (a round trip costs more than the blocks save:
 // qsort 631236 re-entered every 11 instructions, ~5 us per round trip against
-// ~0.2 us per instruction in the assembly interpreter)
+// ~0.2 us per instruction in the assembly interpreter).  64, not 32: intmix
+// 53499 (a loop that rewrites its head every iteration) leaves after 32-63
+// instructions; the intmix step 319 -> 252 ms, qsort +1.5 %, crc32 even
+// (profiles/ab_bench_r05tm_*.jsonl)
 #ifndef FI_TX_SHORT
-#define FI_TX_SHORT 32
+#define FI_TX_SHORT 64
 #endif
 #ifndef FI_TX_SKIP
 #define FI_TX_SKIP 4096
