@@ -123,7 +123,7 @@ typedef struct {
     uint32_t max_trials_per_launch; /* 0 -> auto: as many as half the free device memory holds (65536 .. 2M) */
     uint32_t snapshot_interval;     /* golden snapshot every N committed insts (0 -> auto, >= 256) */
     uint32_t flags;                 /* FI_CFG_* */
-    uint32_t epoch_iters;           /* first epoch's loop iterations per wave (0 -> 1024; then x4, x16, unbounded) */
+    uint32_t epoch_iters;           /* first epoch's loop iterations per wave (0 -> 384; then x4, x16, unbounded) */
     uint32_t lanes_per_wave;        /* trials per 64-lane wave in the first epoch: 1, 2, 4, ..., 64 (0 -> 64) */
     uint32_t resume_lanes;          /* trials per wave in resumed epochs (0 -> default): survivors have diverged, and
                                        a wave serialises its lanes' distinct control flows, so fewer per wave */

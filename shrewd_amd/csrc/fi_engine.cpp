@@ -1518,11 +1518,13 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
     if (e->cfg.flags & FI_CFG_NO_EPOCHS) {
         budgets = {0};
     } else {
-        const uint32_t b = e->cfg.epoch_iters ? e->cfg.epoch_iters : 1024;
+        const uint32_t b = e->cfg.epoch_iters ? e->cfg.epoch_iters : 384;
         // default: one 64-lane epoch, then every survivor to completion on the
         // solo kernel (profiles/r02c epoch_sweep: 2 epochs beat 3 and 4; with
-        // first-access forwarding a 1024-iteration first epoch beats 4096:
-        // crc32 12.7M vs 9.8M, qsort +3 %, intmix even, profiles/r02l_ab.txt)
+        // first-access forwarding a 1024-iteration first epoch beat 4096:
+        // crc32 12.7M vs 9.8M, qsort +3 %, intmix even, profiles/r02l_ab.txt;
+        // with the round-5 solo kernel 384 beats 1024: crc32 4.77 vs 4.96 ms,
+        // qsort 30.9 vs 32.2 ms, intmix 257 vs 253 ms, profiles/ep_sweep_r05*.jsonl)
         const uint32_t n_ep = e->cfg.epochs ? std::max(2u, std::min(e->cfg.epochs, 14u)) : 2u;
         for (uint32_t i = 0; i + 1 < n_ep; i++) budgets.push_back(b << (2 * std::min(i, 2u)));
         budgets.push_back(0);
