@@ -121,8 +121,9 @@ def load_traffic(path, workload, trials, lanes):
             tj = json.load(f)
     except (OSError, ValueError):
         return {}
-    if tj.get("workload") == workload and tj.get("trials") == trials and tj.get("lanes_per_wave", 64) == lanes:
-        return tj
+    for ent in [tj] + list(tj.get("workloads", {}).values()):
+        if ent.get("workload") == workload and ent.get("trials") == trials and ent.get("lanes_per_wave", 64) == lanes:
+            return ent
     return {}
 
 

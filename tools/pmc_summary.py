@@ -91,12 +91,26 @@ def main():
             "sq": sq, "issue": issue}
     with open(os.path.join(p, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
-    with open(os.path.join(p, "pmc_traffic.json"), "w") as f:
-        json.dump({"tag": tag, "workload": wl, "trials": bench["config"]["trials_per_gpu"],
-                   "lanes_per_wave": bench["config"].get("lanes_per_wave", 64),
-                   "per_kernel": {k: {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "issue": v["issue"]}
-                                  for k, v in out["per_kernel"].items()},
-                   "source": f"profiles/{tag}_pmc.json"}, f, indent=1)
+    # one entry per workload (bench.py looks its own up); the headline
+    # workload's entry also stays at the top level
+    path = os.path.join(p, "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        tj = {}
+    ent = {"tag": tag, "workload": wl, "trials": bench["config"]["trials_per_gpu"],
+           "lanes_per_wave": bench["config"].get("lanes_per_wave", 64),
+           "per_kernel": {k: {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"], "issue": v["issue"]}
+                          for k, v in out["per_kernel"].items()},
+           "source": f"profiles/{tag}_pmc.json"}
+    wls = tj.get("workloads", {})
+    if tj.get("workload"):
+        wls.setdefault(tj["workload"], {k: v for k, v in tj.items() if k != "workloads"})
+    wls[wl] = ent
+    top = ent if wl == "crc32" or not tj.get("workload") else {k: v for k, v in tj.items() if k != "workloads"}
+    with open(path, "w") as f:
+        json.dump(dict(top, workloads=wls), f, indent=1)
     print(json.dumps(out, indent=1))
 
 
