@@ -42,6 +42,9 @@ def parse(argv=None):
     ap.add_argument("--priority-to-shadow", action="store_true", help="BaseO3CPU.priorityToShadow")
     ap.add_argument("--issue-width", type=int, default=8)
     ap.add_argument("--load-latency", type=int, default=2)
+    ap.add_argument("--cpu-type", default="atomic", choices=["atomic", "timing"],
+                    help="fault-site time coordinate: numInst (AtomicSimpleCPU) or ticks (TimingSimpleCPU on the "
+                         "NoCache + SingleChannelDDR3_1600 board of simple_binary_run.py)")
     ap.add_argument("--num-gpus", type=int, default=1)
     ap.add_argument("--max-insts-factor", type=float, default=2.0)
     ap.add_argument("--private-pages", type=int, default=16)
@@ -64,6 +67,7 @@ def run_gem5(a):
                          protect_opclasses=_split(a.protect_opclasses), shadow_fu_model=a.shadow_fu_model,
                          priority_to_shadow=a.priority_to_shadow, issue_width=a.issue_width,
                          load_latency=a.load_latency, num_gpus=a.num_gpus, max_insts_factor=a.max_insts_factor,
+                         cpu_type=a.cpu_type,
                          private_pages=a.private_pages, output=a.output)
     root = Root(full_system=False, campaign=camp)
     m5.instantiate()
@@ -93,7 +97,7 @@ def run_ctypes(a):
                       protect_opclasses=_split(a.protect_opclasses), bits=a.bits or None,
                       shadow_fu_model=a.shadow_fu_model, priority_to_shadow=a.priority_to_shadow, checkpoint=a.checkpoint,
                       issue_params={"issue_width": a.issue_width, "load_latency": a.load_latency},
-                      input=a.input, executable=a.executable or None)
+                      input=a.input, executable=a.executable or None, cpu_type=a.cpu_type)
     t0 = time.perf_counter()
     c.run(first_trial=a.first_trial)
     dt = time.perf_counter() - t0

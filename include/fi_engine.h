@@ -92,6 +92,23 @@ typedef int32_t fi_status;
 #define FI_ESC_RESOURCE 5   /* an engine bound: exit_code 0 = private pages (re-run with more before the
                               histogram), 1 = the VMA list / getrandom table (bounded in the oracle too) */
 #define FI_ESC_UNDEF 6      /* gem5's own behaviour is undefined (GEM5_UNREACHABLE: an RVV floating-point op at SEW = 8) */
+#define FI_ESC_TIMING 7     /* a tick-domain site (fi_run_tick_trials) whose TimingSimpleCPU effect is not a
+                               numInst injection; exit_code = FI_TK_* (the reason), detail = the pc in flight */
+/* FI_ESC_TIMING reasons.  A flip at tick t lands inside the instruction in
+ * flight; most such flips equal a numInst injection (fi_run_tick_trials
+ * maps them), these do not: */
+#define FI_TK_NONCOUNT 1    /* after an ecall / a page-fault retry (no numInst step) that reads or writes the
+                               flipped register (ecall: a0..a7; retry: rs1, rs2), or any pc flip there */
+#define FI_TK_STRADDLE1 2   /* pc flip while the first half of a 32-bit instruction at pc % 4 == 2 is fetched,
+                               to another word: the second fetch reads a third word */
+#define FI_TK_ALIGN 3       /* pc flip that changes the fetch word and pc % 4 (the decoder re-slices the word) */
+#define FI_TK_STRADDLE2 4   /* pc flip to a 4-aligned pc while the decoder holds a first half (Decoder::moreBytes
+                               takes the aligned path with mid still set, arch/riscv/decoder.cc:63-116) */
+#define FI_TK_TWO 5         /* pc flip while auipc / jal with a link is fetched: rd and the next pc both change */
+#define FI_TK_FAULTOP 6     /* pc flip to another word on an ecall / page-fault attempt */
+#define FI_TK_MACRO 7       /* pc flip while an AMO / LR / SC (a macro-op) has its access outstanding */
+#define FI_TK_CLOCK 8       /* the trial reads curTick (clock_gettime, rpns): the engine keeps AtomicSimpleCPU's
+                               clock */
 
 /* Fault-site structures: 1..31 = x1..x31, 32 = pc, 33 = 8-byte memory word,
  * 34 = the result of an instruction: the value the first instruction that
@@ -385,6 +402,130 @@ fi_status fi_set_issue_model(fi_engine *e, const fi_issue_params *p);
  * (numInst index; ecalls, which numInst does not count, are left out).
  * *n = golden ninst; stats may be NULL. */
 fi_status fi_shadow_map(fi_engine *e, uint8_t *shadow, uint64_t cap, uint64_t *n, fi_issue_stats *stats);
+
+/* ---- Tick-domain injection under TimingSimpleCPU.
+ *
+ * The reference's own SE run script offers CPUTypes.TIMING on a NoCache board
+ * (SystemXBar, width 64) with SingleChannelDDR3_1600 memory at 3 GHz
+ * (tests/gem5/se_mode/hello_se/configs/simple_binary_run.py:61-64,113-126;
+ * components/cachehierarchies/classic/no_cache.py;
+ * components/memory/single_channel.py:45-51, dram_interfaces/ddr3.py).  Under
+ * that CPU an instruction's architectural effect is the AtomicSimpleCPU one
+ * (same numInst, same results) but it takes a data-dependent number of ticks:
+ * TimingSimpleCPU::fetch/sendFetch/completeIfetch/completeDataAccess
+ * (src/cpu/simple/timing.cc:677-1077) send one request at a time through the
+ * CoherentXBar (src/mem/coherent_xbar.cc:150-507, xbar.cc:108-330) to the
+ * MemCtrl (src/mem/mem_ctrl.cc) and its DRAMInterface (src/mem/
+ * dram_interface.cc: banks, refresh, FR-FCFS).  The engine replays the golden
+ * run's requests through a restatement of those components (an event queue
+ * with gem5's same-tick LIFO order, src/sim/eventq.cc:91-158) and maps a fault
+ * at tick t to the numInst injection the trial kernels already run.
+ *
+ * fi_timing_model_run is the model as a pure host function (no device, no
+ * engine); fi_set_cpu_model(FI_CPU_TIMING) builds the golden request list
+ * from the golden run and runs it; fi_run_tick_trials runs a tick-domain
+ * campaign. */
+typedef struct {
+    uint64_t fetch[2];   /* physical address of each 4-byte instruction fetch ((pc & ~3) + fetchOffset,
+                            BaseSimpleCPU::setupFetchRequest, src/cpu/simple/base.cc:304-318) */
+    uint64_t addr[2];    /* physical address of each data fragment (split at a 64-byte line,
+                            TimingSimpleCPU::initiateMemRead/writeMem, timing.cc:451-586) */
+    uint16_t size[2];    /* fragment bytes */
+    uint8_t nfetch;      /* 1, or 2 for a 32-bit instruction at pc % 4 == 2 (the decoder needs more bytes) */
+    uint8_t nfrag;       /* data requests: 0 (none; also a failed SC), 1 or 2 */
+    uint8_t kind;        /* FI_TOP_* */
+    uint8_t cmd;         /* FI_TCMD_*: the request command of the data fragments */
+    uint8_t pad[8];
+} fi_timing_op;
+#define FI_TOP_EXEC 0    /* executes at its completeIfetch; with data fragments it completes (commits) at the
+                            completeDataAccess of the last response, else at once */
+#define FI_TOP_FAULT 1   /* execute returns a fault (ecall, a page-table fault the SE fixup resolves): the next
+                            fetch is the fetchEvent rescheduled at clockEdge() (timing.cc:782-797) */
+#define FI_TOP_END 2     /* the exit syscall: the run ends at its execute */
+#define FI_TCMD_READ 0   /* ReadReq */
+#define FI_TCMD_WRITE 1  /* WriteReq */
+#define FI_TCMD_SWAP 2   /* SwapReq (AMO: the memory controller's write path, a response with data) */
+#define FI_TCMD_LL 3     /* LoadLockedReq (LR) */
+#define FI_TCMD_SC 4     /* StoreCondReq (a successful SC) */
+
+typedef struct {
+    uint64_t fetch_send[2];   /* tick each fetch request was sent */
+    uint64_t fetch_done[2];   /* tick of its completeIfetch (the CPU clock edge after the response) */
+    uint64_t exec;            /* tick the instruction executes (initiateAcc for a data access) */
+    uint64_t done;            /* tick it completes (completeDataAccess; == exec without data requests) */
+} fi_timing_ticks;
+
+typedef struct {
+    uint64_t cpu_period;      /* CPU and crossbar clock period in ticks (1 ps): SimpleBoard clk_freq 3 GHz -> 333 */
+    uint32_t xbar_frontend, xbar_forward, xbar_response, xbar_header, xbar_width, xbar_sf_lookup;
+                              /* SystemXBar (src/mem/XBar.py): 3, 4, 2 cycles, header 1, NoCache width 64 B,
+                                 snoop-filter lookup 1 cycle */
+    uint64_t mc_frontend, mc_backend, mc_command_window;   /* MemCtrl.py: 10 ns, 10 ns, 10 ns */
+    uint32_t read_buffer, write_buffer;                    /* DRAMInterface read/write_buffer_size: 32, 64 */
+    uint32_t write_high_pct, write_low_pct;                /* 85, 50 */
+    uint32_t min_writes_per_switch, min_reads_per_switch;  /* 16, 16 */
+    uint64_t tCK, tBURST, tRCD, tCL, tRP, tRAS, tRRD, tXAW, tRFC, tWR, tWTR, tRTP, tRTW, tCS, tREFI;
+                              /* DDR3_1600_8x8 (components/memory/dram_interfaces/ddr3.py) */
+    uint32_t activation_limit, ranks, banks, burst_bytes, row_buffer_bytes, max_accesses_per_row;
+                              /* 4, 2, 8, 64, 8 KiB (8 x 1 KiB devices), 16 */
+    uint64_t mem_bytes;       /* channel capacity: 8 GiB (rows per bank) */
+} fi_timing_params;
+
+typedef struct {
+    uint64_t ops, ticks;                       /* ops replayed; tick of the last op's execute (the run's end) */
+    uint64_t reads, writes, write_queue_hits;  /* DRAM read / write bursts; reads the write queue serviced */
+    uint64_t row_hits, activates, refreshes;
+    uint64_t xbar_retries, mc_retries;         /* requests a busy crossbar layer / full controller queue refused */
+} fi_timing_stats;
+
+/* The reference board's parameters (listed above). */
+void fi_timing_default_params(fi_timing_params *p);
+/* Pure host function: replay ops[0..n) (the last one FI_TOP_END) through the
+ * TimingSimpleCPU + SystemXBar + MemCtrl/DDR3 model; out[i] = op i's ticks. */
+fi_status fi_timing_model_run(const fi_timing_op *ops, uint64_t n, const fi_timing_params *p, fi_timing_ticks *out,
+                              fi_timing_stats *stats);
+
+/* The campaign's time coordinate: FI_CPU_ATOMIC (the default: sites at a
+ * numInst) or FI_CPU_TIMING (tick-domain sites, fi_run_tick_trials: the golden
+ * run's requests are rebuilt and timed by fi_golden_run).  Before fi_golden_run
+ * (FI_E_STATE after); p = NULL: the reference board (fi_timing_default_params). */
+#define FI_CPU_ATOMIC 0
+#define FI_CPU_TIMING 1
+fi_status fi_set_cpu_model(fi_engine *e, int model, const fi_timing_params *p);
+
+typedef struct {
+    uint64_t golden_ticks;    /* tick of the golden run's exit (its last attempt's execute) */
+    uint64_t attempts;        /* fetch-execute attempts: commits + ecalls + page-fault retries */
+    fi_timing_stats stats;
+    char status[160];         /* "" when tick campaigns can run, else why not (a golden run that reads curTick,
+                                 unmaps memory, has a failed SC, a prefetch / cache-block / vector op; a checkpoint
+                                 start; the atomic CPU model) */
+} fi_tick_info;
+fi_status fi_tick_golden(fi_engine *e, fi_tick_info *out);
+/* The golden run's attempts as requests and their ticks (copies up to cap; *n = count). */
+fi_status fi_tick_trace(fi_engine *e, fi_timing_op *ops, fi_timing_ticks *ticks, uint64_t cap, uint64_t *n);
+
+typedef struct {
+    uint64_t tick;      /* the flip happens before every event of this tick (tick < golden_ticks) */
+    uint64_t mask;      /* xor mask */
+    uint32_t target;    /* 1..31 = x_r, FI_T_PC, FI_T_RESULT (memory words: not in the tick domain) */
+    uint32_t trial;
+} fi_tick_site;
+/* fi_sample_sites' SplitMix64 draw keyed by (seed, trial) with tick = mulhi(r0,
+ * golden_ticks) in place of numInst (fi_set_campaign / fi_set_bits settings). */
+fi_status fi_sample_tick_sites(fi_engine *e, uint64_t first_trial, uint64_t n, fi_tick_site *out);
+/* The map to the kernels' numInst sites: disp[i] = 0 run sites[i]; 1 the trial
+ * is the golden run (the flip does not persist: the completion of the load in
+ * flight overwrites the register; a pc flip while a link-free jalr is fetched);
+ * 2 escape (FI_ESC_TIMING, FI_TK_* in exit_code).  host_out (may be NULL)
+ * receives the outcome of the disp 1 / 2 trials. */
+fi_status fi_map_tick_sites(fi_engine *e, const fi_tick_site *ts, uint64_t n, fi_site *sites, uint8_t *disp,
+                            fi_outcome *host_out);
+/* A tick-domain campaign (explicit sites / sampled): map, run, classify.  The
+ * histogram counts each trial under its tick site's structure and first bit.
+ * Needs fi_set_protect / fi_set_protect_opclasses off. */
+fi_status fi_run_tick_sites(fi_engine *e, const fi_tick_site *ts, uint64_t n, fi_outcome *out, fi_histogram *hist);
+fi_status fi_run_tick_trials(fi_engine *e, uint64_t first_trial, uint64_t n, fi_outcome *out, fi_histogram *hist);
 
 fi_status fi_sample_sites(fi_engine *e, uint64_t first_trial, uint64_t n, fi_site *out);
 /* out (n entries, trial order) and hist may be NULL. hist is accumulated into (+=). */

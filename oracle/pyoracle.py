@@ -44,6 +44,51 @@ class IssueStats(C.Structure):
 
 
 ISSUE_OP_DT = np.dtype([("src", "<u8"), ("dst", "<u8"), ("opclass", "u1"), ("kind", "u1"), ("pad", "u1", (6,))])
+# tick-domain injection (timing_se.h; layouts == include/fi_engine.h fi_timing_*)
+TIMING_OP_DT = np.dtype([("fetch", "<u8", (2,)), ("addr", "<u8", (2,)), ("size", "<u2", (2,)), ("nfetch", "u1"),
+                         ("nfrag", "u1"), ("kind", "u1"), ("cmd", "u1"), ("pad", "u1", (8,))])
+TIMING_TICKS_DT = np.dtype([("fetch_send", "<u8", (2,)), ("fetch_done", "<u8", (2,)), ("exec", "<u8"),
+                            ("done", "<u8")])
+TICK_SITE_DT = np.dtype([("tick", "<u8"), ("mask", "<u8"), ("target", "<u4"), ("trial", "<u4")])
+
+
+class TimingParams(C.Structure):
+    _fields_ = ([("cpu_period", C.c_uint64)] +
+                [(n, C.c_uint32) for n in ("xbar_frontend", "xbar_forward", "xbar_response", "xbar_header",
+                                           "xbar_width", "xbar_sf_lookup")] +
+                [(n, C.c_uint64) for n in ("mc_frontend", "mc_backend", "mc_command_window")] +
+                [(n, C.c_uint32) for n in ("read_buffer", "write_buffer", "write_high_pct", "write_low_pct",
+                                           "min_writes_per_switch", "min_reads_per_switch")] +
+                [(n, C.c_uint64) for n in ("tCK", "tBURST", "tRCD", "tCL", "tRP", "tRAS", "tRRD", "tXAW", "tRFC",
+                                           "tWR", "tWTR", "tRTP", "tRTW", "tCS", "tREFI")] +
+                [(n, C.c_uint32) for n in ("activation_limit", "ranks", "banks", "burst_bytes",
+                                           "row_buffer_bytes", "max_accesses_per_row")] +
+                [("mem_bytes", C.c_uint64)])
+
+
+class TimingStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("ops", "ticks", "reads", "writes", "write_queue_hits", "row_hits",
+                                          "activates", "refreshes", "xbar_retries", "mc_retries")]
+
+
+def timing_params(**kw) -> TimingParams:
+    """The reference board's timing parameters (timing_se.c), with overrides."""
+    p = TimingParams()
+    lib().or_timing_default_params(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, int(v))
+    return p
+
+
+def timing_model(ops: np.ndarray, params: TimingParams | None = None):
+    """or_timing_model -> (ticks TIMING_TICKS_DT[n], TimingStats)"""
+    ops = np.ascontiguousarray(ops, TIMING_OP_DT)
+    out = np.zeros(len(ops), TIMING_TICKS_DT)
+    st = TimingStats()
+    if lib().or_timing_model(ops.ctypes.data, len(ops), C.byref(params or timing_params()), out.ctypes.data,
+                             C.byref(st)) != 0:
+        raise RuntimeError("or_timing_model: rejected")
+    return out, st
 FU_NAMES = ("IntALU", "IntMultDiv", "FP_ALU", "FP_MultDiv", "RdWrPort", "IprPort")
 
 
@@ -122,6 +167,17 @@ def lib():
         L.or_shadow_map.restype = C.c_uint64
         L.or_shadow_map.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(IssueStats)]
         L.or_rvk.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+        L.or_timing_default_params.argtypes = [C.c_void_p]
+        L.or_timing_model.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.or_tick_setup.argtypes = [C.c_void_p, C.c_void_p]
+        L.or_tick_golden_ticks.restype = C.c_uint64
+        L.or_tick_golden_ticks.argtypes = [C.c_void_p]
+        L.or_tick_trace.restype = C.c_uint64
+        L.or_tick_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]
+        L.or_tick_sample.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32,
+                                     C.c_uint64, C.c_void_p]
+        L.or_run_tick_trials.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p,
+                                         C.c_int]
         L.or_sf_ref.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
                                 C.c_void_p, C.c_void_p]
         _lib = L
@@ -227,6 +283,41 @@ class Oracle:
 
     def set_clock(self, period_ticks=500, random_seed=5489):
         self.L.or_set_clock(self.h, period_ticks, random_seed)
+
+    # ---- tick-domain injection under TimingSimpleCPU (rv64se.h)
+    def tick_setup(self, params: TimingParams | None = None) -> int:
+        """Record the golden run's requests and run the timing model; returns
+        the golden run's length in ticks."""
+        if self.L.or_tick_setup(self.h, C.byref(params) if params is not None else None) != 0:
+            raise RuntimeError(self.L.or_error(self.h).decode())
+        return int(self.L.or_tick_golden_ticks(self.h))
+
+    def tick_trace(self):
+        """(ops TIMING_OP_DT, ticks TIMING_TICKS_DT) of the golden run's attempts."""
+        n = self.L.or_tick_trace(self.h, None, None, 0)
+        ops = np.zeros(n, TIMING_OP_DT)
+        ticks = np.zeros(n, TIMING_TICKS_DT)
+        self.L.or_tick_trace(self.h, ops.ctypes.data, ticks.ctypes.data, n)
+        return ops, ticks
+
+    def tick_sample(self, seed, first, n, structures, burst=1, bits=2**64 - 1) -> np.ndarray:
+        out = np.zeros(n, TICK_SITE_DT)
+        if self.L.or_tick_sample(self.h, seed, first, n, structures, burst, bits & (2**64 - 1),
+                                 out.ctypes.data) != 0:
+            raise RuntimeError(self.L.or_error(self.h).decode())
+        return out
+
+    def run_tick_trials(self, sites: np.ndarray, hang_x16=0, threads=None, truth=False):
+        """-> outcomes (the contract's escapes reported, not run), or
+        (outcomes, literal outcomes of every trial) with truth=True"""
+        sites = np.ascontiguousarray(sites, TICK_SITE_DT)
+        out = np.zeros(len(sites), OUTCOME_DT)
+        tr = np.zeros(len(sites), OUTCOME_DT) if truth else None
+        threads = threads or os.cpu_count() or 1
+        if self.L.or_run_tick_trials(self.h, sites.ctypes.data, len(sites), hang_x16, out.ctypes.data,
+                                     tr.ctypes.data if truth else None, threads) != 0:
+            raise RuntimeError(self.L.or_error(self.h).decode())
+        return (out, tr) if truth else out
 
     def run_one(self, site=None, protect_mask=0, hang_x16=0):
         out = np.zeros(1, OUTCOME_DT)

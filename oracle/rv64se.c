@@ -10,6 +10,7 @@
  */
 #define _GNU_SOURCE
 #include "rv64se.h"
+#include "timing_se.h"
 #include "../shrewd_amd/csrc/gem5_decode_table.h"
 #include "../shrewd_amd/csrc/gem5_opclass_table.h"
 
@@ -195,6 +196,8 @@ static void by_push(bytes_t *b, const uint8_t *p, u64 n) {
 
 struct or_campaign {
     pmap_t image;          /* initial process image pages (shared, read-only) */
+    u64 *alloc_vpn; u64 n_alloc, cap_alloc;   /* image pages in the order the image write allocated them */
+    struct tkgold *tk;     /* tick-domain injection (or_tick_setup): the golden run's requests and ticks */
     u64 entry, sp0, stack_min0;
     u64 regs0[32], pc0;    /* initial architectural state (process start or a checkpoint) */
     u64 text_lo, text_hi;  /* page-aligned executable range (PT_LOAD with PF_X) */
@@ -245,6 +248,7 @@ typedef struct {
     /* fault injection */
     const or_site_t *site; int injected; int watch; /* watch = protected flipped reg, -1 none */
     int rarm, wrote;      /* result fault armed (OR_T_RESULT); the executing instruction wrote x[rd] */
+    u64 rmask;            /* the armed result fault's mask */
     /* golden trace recording for the issue model (or_set_issue_model) */
     or_issue_op_t *rec; u64 rec_n, rec_cap;
     /* LR/SC: the ISA's load reservation (isa.cc:1006-1064) and this context's
@@ -276,6 +280,13 @@ typedef struct {
     /* the vector configuration of the PC state (riscv/pcstate.hh: _vtype, _vl)
      * as VCFG(vtype, vl) -- 0 is the process start (vtype = vill, vl = 0) */
     u32 vcfg;
+    /* tick-domain injection (TimingSimpleCPU, include/fi_engine.h "Tick-domain
+     * injection"): tkr records the golden run's requests, tki applies a trial's
+     * flip inside the instruction in flight; fo = the next fetch reads fo_addr
+     * (a request sent before a pc flip); tk_cpu = a CPU access is executing */
+    struct tkrec *tkr;
+    const struct tkinj *tki;
+    int fo, tk_cpu; u64 fo_addr;
     const or_campaign_t *c;
 } mach_t;
 /* vcfg <-> (vtype, vl): a vtype that getNewVtype produces is vill alone, a
@@ -286,7 +297,7 @@ static u64 vcfg_vtype(u32 vcfg) { vcfg ^= 0x100u; return (u64)(vcfg & 0xFF) | (u
 static u32 vcfg_vl(u32 vcfg) { return vcfg >> 9; }
 
 enum { F_NONE = 0, F_SYSCALL = 1, F_BREAK = 2, F_ILLEGAL = 3, F_UNKNOWN = 4, F_ESCAPE = 5, F_PGFAULT = 6, F_AMOLINE = 7,
-       F_SCLINE = 8, F_M5PANIC = 9, F_UNDEF = 10, F_VSEW = 11 };
+       F_SCLINE = 8, F_M5PANIC = 9, F_UNDEF = 10, F_VSEW = 11, F_TKCLOCK = 12 };
 
 /* -------------------------------------------------------------- decode */
 /* Op ids.  Names follow gem5's mnemonics (arch/riscv/isa/decoder.isa). */
@@ -985,6 +996,12 @@ const char *or_mnemonic(u32 inst) {
     return n;
 }
 
+/* ------------------------------------------------- tick-domain hooks (decl) */
+static void tk_page(mach_t *m, u64 vpn);
+static void tk_frag(mach_t *m, u64 addr, unsigned size, int cmd);
+static void tk_unsupported(mach_t *m, const char *why);
+static void tk_fetch(mach_t *m, u64 fetch_pc);
+
 /* ---------------------------------------------------------- memory access */
 /* SE translation: arch/riscv/tlb.cc:573-604 -> EmulationPageTable::translate
  * (mem/page_table.cc:143-153).  Returns page data or NULL (page-table fault). */
@@ -1009,6 +1026,7 @@ static void alloc_page(mach_t *m, u64 vaddr) {
     if (pm_find(&m->mem, vpn)) return;
     uint8_t *n = (uint8_t *)calloc(1, PAGE);
     pm_insert(&m->mem, vpn, n, 1);
+    if (m->tkr) tk_page(m, vpn);   /* seWorkload->allocPhysPages: the next free frame */
 }
 
 /* MemState::fixupFault, sim/mem_state.cc:387-447.  Returns 1 handled, 0 not
@@ -1047,6 +1065,7 @@ static int mem_read(mach_t *m, u64 addr, unsigned size, u64 *val, u64 *fault_va)
             u64 b = a + i;   /* fragment lies within one page (64-byte line) */
             buf[done + i] = pg[b & (PAGE - 1)];
         }
+        if (m->tkr) tk_frag(m, a, frag, OR_TCMD_READ);
         done += frag; a += frag;
     }
     u64 v = 0;
@@ -1067,6 +1086,7 @@ static int mem_write(mach_t *m, u64 addr, unsigned size, u64 val, u64 *fault_va)
         uint8_t *pg = translate_w(m, a);
         if (!pg) { *fault_va = a; return F_PGFAULT; }
         for (unsigned i = 0; i < frag; i++) pg[(a + i) & (PAGE - 1)] = (uint8_t)(val >> (8 * (done + i)));
+        if (m->tkr) tk_frag(m, a, frag, OR_TCMD_WRITE);
         /* AbstractMemory::checkLockedAddrList: a store erases the lock records
          * of its fragment's 16-byte granule (abstract_mem.cc:290-345) */
         if (m->lock == (a & ~0xFULL)) m->lock = OR_NONE;
@@ -1086,6 +1106,7 @@ static int mem_write_zero64(mach_t *m, u64 ea, u64 *fault_va) {
     uint8_t *pg = translate_w(m, ea);
     if (!pg) { *fault_va = ea; return F_PGFAULT; }
     memset(pg + (ea & (PAGE - 1)), 0, 64);
+    if (m->tkr) tk_frag(m, ea, 64, OR_TCMD_WRITE);
     if (m->lock == ea) m->lock = OR_NONE;
     m->data_bytes += 64;
     return F_NONE;
@@ -1134,6 +1155,7 @@ static int vma_add(mach_t *m, u64 lo, u64 hi) {
  * mapped (zeroed on deallocation: zeroPages=True, Process.py:55-58). */
 static int vma_unmap(mach_t *m, u64 lo, u64 hi) {
     int n = m->nvma;
+    if (m->tkr) tk_unsupported(m, "the golden run unmaps memory (freed frames are reused)");
     for (int i = 0; i < n; i++) {
         u64 a = m->vma[i].lo, b = m->vma[i].hi;
         if (!(a < hi && lo < b)) continue;
@@ -1625,6 +1647,8 @@ static void do_syscall(mach_t *m) {
         const u64 tp = m->x[11];
         if (!tp) { se_panic(m); return; }
         if (!proxy_readable(m, tp, 16)) { finish(m, OR_CRASH, OR_CRASH_PROXY, 1); return; }
+        if (m->tkr) tk_unsupported(m, "the golden run reads curTick (clock_gettime)");
+        if (m->tki) { finish(m, OR_ESCAPE, OR_ESC_TIMING, OR_TK_CLOCK); return; }
         const u64 ns = (m->c->tick0 + (m->num_cycles - 1) * m->c->clk_period) / 1000;
         const u64 sec = ns / 1000000000ULL + 1000000000ULL, nsec = ns % 1000000000ULL;
         uint8_t b[16];
@@ -1783,6 +1807,7 @@ static int lr_read(mach_t *m, u64 addr, unsigned size, u64 *val, u64 *fault_va) 
         uint8_t *pg = translate(m, a);
         if (!pg) { *fault_va = a; return F_PGFAULT; }
         for (unsigned i = 0; i < frag; i++) v |= (u64)pg[(a + i) & (PAGE - 1)] << (8 * (done + i));
+        if (m->tkr) tk_frag(m, a, frag, OR_TCMD_LL);
         m->resv = a;
         m->lock = a & ~0xFULL;
         done += frag; a += frag;
@@ -1816,6 +1841,10 @@ static int sc_write(mach_t *m, u64 addr, unsigned size, u64 val, int *ok, u64 *f
         u64 a2 = addr + frag;
         if (a2 + (size - frag) - 1 < a2 || !translate(m, a2)) { *fault_va = a2; return F_PGFAULT; }
         return F_SCLINE;
+    }
+    if (m->tkr) {   /* a failed SC: whether it reached memory is not in the golden record */
+        if (*ok) tk_frag(m, addr, size, OR_TCMD_SC);
+        else tk_unsupported(m, "the golden run has a failed SC");
     }
     if (*ok) m->data_bytes += size;
     return F_NONE;
@@ -2172,6 +2201,7 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
         for (unsigned i = 0; i < sz; i++) old |= (u64)pg[(ea + i) & (PAGE - 1)] << (8 * i);
         u64 nw = amo_apply(d->op - (w ? OP_amoadd_w : OP_amoadd_d), old, b, w);
         for (unsigned i = 0; i < sz; i++) pg[(ea + i) & (PAGE - 1)] = (uint8_t)(nw >> (8 * i));
+        if (m->tkr) tk_frag(m, ea, sz, OR_TCMD_SWAP);
         m->data_bytes += 2 * sz;
         m->num_cycles += (d->funct3 & 1) + (d->funct3 >> 1);   /* rl / aq fence micro-ops: one tick each */
         v = w ? sx32(old) : old;
@@ -2301,7 +2331,11 @@ static int execute(mach_t *m, const dec_t *d, u64 *fault_va) {
     case OP_m5op: {
         u64 res = 0;
         switch (imm) {
-        case 0x07: res = (m->c->tick0 + (m->num_cycles - 1) * m->c->clk_period) / 1000; break;   /* rpns: curTick() / ns */
+        case 0x07:   /* rpns: curTick() / ns */
+            if (m->tkr) tk_unsupported(m, "the golden run reads curTick (rpns)");
+            if (m->tki) return F_TKCLOCK;
+            res = (m->c->tick0 + (m->num_cycles - 1) * m->c->clk_period) / 1000;
+            break;
         case 0x23:   /* m5sum(a0..a5) */
             if (m->watch >= 10 && m->watch <= 15) return 100;
             for (int k = 10; k <= 15; k++) res += m->x[k];
@@ -2386,6 +2420,7 @@ static void inject(mach_t *m) {
         if ((m->protect_mask >> 32) & 1) { finish(m, OR_DETECTED, 0, 0); }
     } else if (s->target == OR_T_RESULT) {
         m->rarm = 1;   /* the next instruction that commits is the target */
+        m->rmask = s->mask;
     } else if (s->target == OR_T_MEM) {
         /* flip the 8-byte word if its page is mapped at inject time */
         uint8_t *pg = translate_w(m, s->addr);
@@ -2408,6 +2443,7 @@ static void invoke_fault(mach_t *m, int f, u64 fault_va, const dec_t *d) {
         do_syscall(m);
         return;
     case F_BREAK: finish(m, OR_CRASH, OR_CRASH_SIGTRAP, 133); return;
+    case F_TKCLOCK: finish(m, OR_ESCAPE, OR_ESC_TIMING, OR_TK_CLOCK); return;
     case F_ILLEGAL: finish(m, OR_CRASH, OR_CRASH_ILLEGAL_INST, 134); return;
     case F_UNKNOWN: finish(m, OR_CRASH, OR_CRASH_UNKNOWN_INST, 134); return;
     case F_ESCAPE: finish(m, OR_ESCAPE, OR_ESC_INST, 0); m->res.detail = d->raw; return;
@@ -2716,13 +2752,25 @@ static int result_fault(mach_t *m, const dec_t *d) {
     m->rarm = 0;
     if (!m->wrote) { m->injected = 2; return 0; }
     if (replicated(m->c, op_class(d->op), m->num_inst - 1)) { finish(m, OR_DETECTED, 0, 0); return 1; }
-    m->x[d->rd] ^= m->site->mask;
+    m->x[d->rd] ^= m->rmask;
     return 0;
 }
 
 /* One AtomicSimpleCPU::tick() with width=1 (cpu/simple/atomic.cc:611-739). */
+static void tk_open(mach_t *m, u64 tick_index);
+static void tk_close(mach_t *m, int f, const dec_t *d);
+static void tk_inject_top(mach_t *m);
+static void tk_inject_data(mach_t *m, const dec_t *d);
+static int tk_here(const mach_t *m, u64 tick_index, int data);
+
 static void tick(mach_t *m, u64 cap) {
+    const u64 tick_index = m->num_cycles;
     m->num_cycles++;
+    if (m->tkr) tk_open(m, tick_index);
+    if (m->tki && !m->injected && tk_here(m, tick_index, 0)) {
+        tk_inject_top(m);
+        if (m->done) return;
+    }
     /* serviceInstCountEvents (base.cc:321-325): fault injection and the
      * max-insts exit both fire at the top of the first tick with numInst >= n */
     if (m->site && !m->injected && m->num_inst >= m->site->inst) {
@@ -2734,7 +2782,9 @@ static void tick(mach_t *m, u64 cap) {
     if (m->num_inst >= cap) { finish(m, OR_HANG, OR_HANG_INSTS, 0); m->res.detail = 0; return; }
     /* setupFetchRequest: 4 bytes at (pc & ~3) + fetchOffset (base.cc:304-318) */
     u64 fetch_pc = (m->pc & ~3ULL) + m->fetch_offset;
+    if (m->fo) { fetch_pc = m->fo_addr; m->fo = 0; }   /* a request sent before the pc flip */
     uint8_t *pg = translate(m, fetch_pc);
+    if (pg && m->tkr) tk_fetch(m, fetch_pc);
     int f = F_NONE; u64 fva = 0;
     dec_t d; memset(&d, 0, sizeof d);
     int have_inst = 0;
@@ -2771,7 +2821,10 @@ static void tick(mach_t *m, u64 cap) {
         }
         if (have_inst) {
             m->wrote = 0;
+            m->tk_cpu = 1;
             f = execute(m, &d, &fva);
+            m->tk_cpu = 0;
+            if (m->tki && !m->injected && f == F_NONE && tk_here(m, tick_index, 1)) tk_inject_data(m, &d);
             if (m->rec && (f == F_NONE || f == F_SYSCALL)) {
                 if (m->rec_n == m->rec_cap) {
                     m->rec_cap = m->rec_cap ? 2 * m->rec_cap : 4096;
@@ -2798,6 +2851,7 @@ static void tick(mach_t *m, u64 cap) {
         }
     }
     if (m->m5x && !m->done) {   /* the M5 op that ends the run has committed */
+        if (m->tkr) tk_close(m, F_NONE + 100, &d);
         if (m->m5x == 3) {
             finish(m, OR_HANG, OR_HANG_QUIESCE, 0);
         } else {
@@ -2809,6 +2863,7 @@ static void tick(mach_t *m, u64 cap) {
             finish(m, same ? OR_MASKED : OR_SDC, m->m5x == 1 ? OR_END_M5_EXIT : OR_END_M5_FAIL, m->m5code);
         }
     }
+    if (m->tkr && (f != F_NONE || !m->stay_at_pc)) tk_close(m, f, &d);
 }
 
 /* --------------------------------------------------------- ELF + image */
@@ -2821,7 +2876,16 @@ static void image_write(or_campaign_t *c, u64 addr, const uint8_t *src, u64 n) {
     for (u64 i = 0; i < n; i++) {
         u64 a = addr + i;
         pte_t *p = pm_find(&c->image, a >> 12);
-        if (!p) p = pm_insert(&c->image, a >> 12, (uint8_t *)calloc(1, PAGE), 1);
+        if (!p) {
+            p = pm_insert(&c->image, a >> 12, (uint8_t *)calloc(1, PAGE), 1);
+            /* SETranslatingPortProxy::fixupRange (Always): allocateMem per page
+             * in write order, each the next free frame (mem_pool.cc:96-102) */
+            if (c->n_alloc == c->cap_alloc) {
+                c->cap_alloc = c->cap_alloc ? 2 * c->cap_alloc : 64;
+                c->alloc_vpn = (u64 *)realloc(c->alloc_vpn, c->cap_alloc * sizeof(u64));
+            }
+            c->alloc_vpn[c->n_alloc++] = a >> 12;
+        }
         p->data[a & (PAGE - 1)] = src ? src[i] : 0;
     }
 }
@@ -2957,9 +3021,12 @@ or_campaign_t *or_create(const uint8_t *elf, size_t len, const char *argv0) {
     return c;
 }
 
+static void tkgold_free(struct tkgold *g);
 void or_destroy(or_campaign_t *c) {
     if (!c) return;
     pm_free(&c->image);
+    tkgold_free(c->tk);
+    free(c->alloc_vpn);
     free(c->mem_pages); free(c->gout.buf); free(c->gerr.buf); free(c->shadow); free(c->in_data);
     free(c);
 }
@@ -3529,4 +3596,340 @@ or_campaign_t *or_create_checkpoint(const char *dir, const uint8_t *elf, size_t 
     if (!ok) snprintf(c->err, sizeof c->err, "memory store truncated");
     free(va); free(pa); cpt_free(&t);
     return c;
+}
+
+/* =================================================== tick-domain injection
+ * (TimingSimpleCPU on the reference's SE board; rv64se.h "Tick-domain
+ * injection").  One attempt = one fetch-execute of TimingSimpleCPU
+ * (timing.cc:819-898): its fetch words, then either an execute that commits
+ * (with its data requests, completing at completeDataAccess), or a fault
+ * (ecall, a page-table fault SE fixes up) after which fetchEvent refetches. */
+typedef struct {
+    u64 pc, n, cyc0, next_pc;   /* pc, numInst before it, first atomic tick index, the next attempt's pc */
+    int op, rd, rs1, rs2;       /* the oracle's decode of the instruction */
+    uint8_t len, nfetch, kind;  /* kind: 0 commits, 1 ecall, 2 page-fault retry, 3 the run's end */
+} tk_info_t;
+enum { TK_COMMIT = 0, TK_ECALL = 1, TK_PGFAULT = 2, TK_END = 3 };
+
+typedef struct tkrec {
+    or_timing_op_t *ops; tk_info_t *info; u64 n, cap;
+    int open;
+    u64 *pv, *pp; u64 np, capp;   /* vpn -> frame, allocation order */
+    char why[160];
+} tkrec_t;
+
+typedef struct tkgold {
+    or_timing_op_t *ops; tk_info_t *info; or_timing_ticks_t *ticks; u64 n;
+    u64 golden_ticks;
+} tkgold_t;
+
+enum { TKP_FETCH1 = 0, TKP_FETCH2 = 1, TKP_DATA = 2 };
+typedef struct tkinj {
+    u64 cyc;          /* atomic tick index of the attempt's tick the flip lands in */
+    int phase;        /* TKP_* */
+    uint32_t target; u64 mask;
+} tkinj_t;
+
+static void tk_unsupported(mach_t *m, const char *why) {
+    if (m->tkr && !m->tkr->why[0]) snprintf(m->tkr->why, sizeof m->tkr->why, "%s", why);
+}
+static u64 tk_frame(tkrec_t *r, u64 vpn) {
+    for (u64 i = 0; i < r->np; i++) if (r->pv[i] == vpn) return r->pp[i];
+    return OR_NONE;
+}
+static void tk_page(mach_t *m, u64 vpn) {
+    tkrec_t *r = m->tkr;
+    if (tk_frame(r, vpn) != OR_NONE) return;
+    if (r->np == r->capp) {
+        r->capp = r->capp ? 2 * r->capp : 256;
+        r->pv = (u64 *)realloc(r->pv, r->capp * 8); r->pp = (u64 *)realloc(r->pp, r->capp * 8);
+    }
+    r->pv[r->np] = vpn; r->pp[r->np] = r->np; r->np++;
+}
+static u64 tk_paddr(mach_t *m, u64 va) {
+    u64 f = tk_frame(m->tkr, va >> 12);
+    if (f == OR_NONE) { tk_unsupported(m, "an access to a page with no frame"); return 0; }
+    return (f << 12) | (va & (PAGE - 1));
+}
+static void tk_open(mach_t *m, u64 tick_index) {
+    tkrec_t *r = m->tkr;
+    if (r->open) return;
+    if (r->n == r->cap) {
+        r->cap = r->cap ? 2 * r->cap : 4096;
+        r->ops = (or_timing_op_t *)realloc(r->ops, r->cap * sizeof *r->ops);
+        r->info = (tk_info_t *)realloc(r->info, r->cap * sizeof *r->info);
+    }
+    memset(&r->ops[r->n], 0, sizeof r->ops[0]);
+    memset(&r->info[r->n], 0, sizeof r->info[0]);
+    if (r->n) r->info[r->n - 1].next_pc = m->pc;
+    r->info[r->n].pc = m->pc; r->info[r->n].n = m->num_inst; r->info[r->n].cyc0 = tick_index;
+    r->open = 1;
+}
+static void tk_fetch(mach_t *m, u64 fetch_pc) {
+    tkrec_t *r = m->tkr;
+    or_timing_op_t *o = &r->ops[r->n];
+    if (o->nfetch >= 2) { tk_unsupported(m, "more than two fetches for one instruction"); return; }
+    o->fetch[o->nfetch++] = tk_paddr(m, fetch_pc);
+}
+static void tk_frag(mach_t *m, u64 addr, unsigned size, int cmd) {
+    if (!m->tk_cpu) return;   /* syscall proxies move no CPU requests */
+    tkrec_t *r = m->tkr;
+    or_timing_op_t *o = &r->ops[r->n];
+    if (o->nfrag >= 2) { tk_unsupported(m, "more than two data requests"); return; }
+    o->addr[o->nfrag] = tk_paddr(m, addr); o->size[o->nfrag] = (uint16_t)size; o->cmd = (uint8_t)cmd;
+    o->nfrag++;
+}
+static void tk_close(mach_t *m, int f, const dec_t *d) {
+    tkrec_t *r = m->tkr;
+    or_timing_op_t *o = &r->ops[r->n];
+    tk_info_t *I = &r->info[r->n];
+    I->op = d->op; I->rd = d->rd; I->rs1 = d->rs1; I->rs2 = d->rs2; I->len = (uint8_t)d->len;
+    I->nfetch = o->nfetch;
+    if (f == F_NONE + 100) {                     /* m5_exit / m5_fail ends the run after it commits */
+        o->kind = OR_TOP_END; I->kind = TK_END;
+    } else if (f == F_NONE) {
+        o->kind = OR_TOP_EXEC; I->kind = TK_COMMIT;
+        if (d->op == OP_prefetch_i || d->op == OP_prefetch_r || d->op == OP_prefetch_w)
+            tk_unsupported(m, "a prefetch (a PREFETCH request) in the golden run");
+        if (d->op == OP_cbo && d->imm != 4) tk_unsupported(m, "a cache-block management op in the golden run");
+        if (d->op == OP_vec || d->op == OP_vset) tk_unsupported(m, "a vector op in the golden run");
+    } else if (f == F_SYSCALL) {
+        o->nfrag = 0;
+        if (m->done) { o->kind = OR_TOP_END; I->kind = TK_END; }
+        else { o->kind = OR_TOP_FAULT; I->kind = TK_ECALL; }
+    } else if (f == F_PGFAULT && !m->done) {
+        o->nfrag = 0; o->kind = OR_TOP_FAULT; I->kind = TK_PGFAULT;
+    } else {
+        tk_unsupported(m, "the golden run faults");
+    }
+    r->n++;
+    r->open = 0;
+}
+
+/* the attempt's tick that a flip at phase lands in */
+static int tk_here(const mach_t *m, u64 tick_index, int data) {
+    const tkinj_t *k = m->tki;
+    if (data) return k->phase == TKP_DATA && tick_index == k->cyc;
+    return k->phase != TKP_DATA && tick_index == k->cyc;
+}
+/* before the attempt's tick: its (next) fetch request went out with the old pc */
+static void tk_inject_top(mach_t *m) {
+    const tkinj_t *k = m->tki;
+    m->injected = 1;
+    if (k->target >= 1 && k->target <= 31) {
+        m->x[k->target] ^= k->mask;
+    } else if (k->target == OR_T_PC) {
+        m->fo = 1;
+        m->fo_addr = (m->pc & ~3ULL) + m->fetch_offset;
+        m->pc ^= k->mask;   /* PCState::set: npc = pc + 4 -- decode sets it again */
+    } else if (k->target == OR_T_RESULT) {
+        m->rarm = 1; m->rmask = k->mask;
+    }
+}
+/* between initiateAcc and completeAcc: the completion writes rd afterwards,
+ * then advancePC takes npc, which PCState::set made pc + 4 */
+static void tk_inject_data(mach_t *m, const dec_t *d) {
+    const tkinj_t *k = m->tki;
+    m->injected = 1;
+    if (k->target >= 1 && k->target <= 31) {
+        if (!(m->wrote && d->rd == (int)k->target)) m->x[k->target] ^= k->mask;
+    } else if (k->target == OR_T_PC) {
+        m->npc = (m->pc ^ k->mask) + 4;
+    } else if (k->target == OR_T_RESULT) {
+        m->rarm = 1; m->rmask = k->mask;
+    }
+}
+
+static int tk_is_macro(int op) {
+    return (op >= OP_amoadd_w && op <= OP_amomaxu_d) || op == OP_lr_w || op == OP_lr_d || op == OP_sc_w || op == OP_sc_d;
+}
+/* The contract: which tick sites the numInst engine does not reproduce
+ * (include/fi_engine.h FI_TK_*).  0 = reproduced. */
+static int tk_contract(const tkgold_t *g, u64 j, int phase, uint32_t target, u64 mask) {
+    const tk_info_t *I = &g->info[j];
+    if (target == OR_T_RESULT) return 0;
+    u64 gs = j;
+    while (gs > 0 && (g->info[gs - 1].kind == TK_ECALL || g->info[gs - 1].kind == TK_PGFAULT)) gs--;
+    if (target <= 31) {
+        if (phase == TKP_DATA) return 0;
+        for (u64 k = gs; k < j; k++) {
+            const tk_info_t *K = &g->info[k];
+            if (K->kind == TK_ECALL && target >= 10 && target <= 17) return OR_TK_NONCOUNT;
+            if (K->kind == TK_PGFAULT && ((int)target == K->rs1 || (int)target == K->rs2)) return OR_TK_NONCOUNT;
+        }
+        return 0;
+    }
+    /* pc */
+    if (gs != j) return OR_TK_NONCOUNT;
+    const u64 pc = I->pc, npc = pc ^ mask;
+    const int same_word = ((pc ^ npc) & ~3ULL) == 0;
+    if (phase == TKP_DATA) return tk_is_macro(I->op) ? OR_TK_MACRO : 0;
+    if (I->kind != TK_COMMIT) return (phase == TKP_FETCH1 && same_word) ? 0 : OR_TK_FAULTOP;
+    const int two = I->op == OP_auipc || (I->op == OP_jal && I->rd > 0);
+    if (phase == TKP_FETCH1) {
+        if (same_word) return 0;
+        if (I->nfetch == 2) return OR_TK_STRADDLE1;
+        if ((pc & 3) != (npc & 3)) return OR_TK_ALIGN;
+        return two ? OR_TK_TWO : 0;
+    }
+    if ((npc & 3) == 0) return OR_TK_STRADDLE2;
+    return two ? OR_TK_TWO : 0;
+}
+
+static void tkgold_free(tkgold_t *g) {
+    if (!g) return;
+    free(g->ops); free(g->info); free(g->ticks); free(g);
+}
+
+int or_tick_setup(or_campaign_t *c, const or_timing_params_t *p) {
+    if (!c->have_golden) { snprintf(c->err, sizeof c->err, "or_tick_setup: golden run required"); return -1; }
+    tkgold_free(c->tk); c->tk = NULL;
+    or_timing_params_t dp;
+    if (!p) { or_timing_default_params(&dp); p = &dp; }
+    tkrec_t r; memset(&r, 0, sizeof r);
+    mach_t m; mach_init(&m, c);
+    m.tkr = &r;
+    for (u64 i = 0; i < c->n_alloc; i++) tk_page(&m, c->alloc_vpn[i]);   /* the image, as initState wrote it */
+    run(&m, c->golden.ninst + 1);
+    int rc = 0;
+    if (!r.why[0] && (m.res.cls != OR_MASKED || m.num_inst != c->golden.ninst || r.n == 0 ||
+                      r.ops[r.n - 1].kind != OR_TOP_END))
+        snprintf(r.why, sizeof r.why, "the recorded golden run does not end with its exit");
+    if (r.why[0]) {
+        snprintf(c->err, sizeof c->err, "tick model: %s", r.why);
+        rc = -1;
+    } else {
+        tkgold_t *g = (tkgold_t *)calloc(1, sizeof *g);
+        g->ops = r.ops; g->info = r.info; g->n = r.n; r.ops = NULL; r.info = NULL;
+        g->ticks = (or_timing_ticks_t *)calloc(g->n, sizeof *g->ticks);
+        or_timing_stats_t st;
+        if (or_timing_model(g->ops, g->n, p, g->ticks, &st) != 0) {
+            snprintf(c->err, sizeof c->err, "tick model: a state gem5 asserts on");
+            tkgold_free(g);
+            rc = -1;
+        } else {
+            g->golden_ticks = st.ticks;
+            c->tk = g;
+        }
+    }
+    m.tkr = NULL;
+    free(r.ops); free(r.info); free(r.pv); free(r.pp);
+    mach_free(&m);
+    return rc;
+}
+
+uint64_t or_tick_golden_ticks(or_campaign_t *c) { return c->tk ? c->tk->golden_ticks : 0; }
+
+uint64_t or_tick_trace(or_campaign_t *c, or_timing_op_t *ops, or_timing_ticks_t *ticks, uint64_t cap) {
+    if (!c->tk) return 0;
+    u64 n = c->tk->n < cap ? c->tk->n : cap;
+    if (ops) memcpy(ops, c->tk->ops, n * sizeof *ops);
+    if (ticks) memcpy(ticks, c->tk->ticks, n * sizeof *ticks);
+    return c->tk->n;
+}
+
+int or_tick_sample(or_campaign_t *c, u64 seed, u64 first, u64 n, u64 structures, u32 burst, u64 bits,
+                   or_tick_site_t *out) {
+    if (!c->tk) { snprintf(c->err, sizeof c->err, "or_tick_sample: or_tick_setup first"); return -1; }
+    if (burst < 1 || burst > 64) burst = 1;
+    structures &= ((1ULL << 32) - 2) | (1ULL << OR_T_PC) | (1ULL << OR_T_RESULT);
+    int nt = __builtin_popcountll(structures);
+    if (nt == 0) { snprintf(c->err, sizeof c->err, "no fault structures"); return -1; }
+    for (u64 i = 0; i < n; i++) {
+        u64 id = first + i;
+        u64 st = seed ^ (id * 0xD6E8FEB86659FD93ULL);
+        u64 r0 = splitmix(&st), r1 = splitmix(&st), r2 = splitmix(&st);
+        or_tick_site_t *s = &out[i];
+        s->tick = mulhi(r0, c->tk->golden_ticks);
+        u64 k = mulhi(r1, (u64)nt), mm = structures;
+        for (u64 j = 0; j < k; j++) mm &= mm - 1;
+        s->target = (u32)__builtin_ctzll(mm);
+        const u64 valid = burst == 1 ? ~0ULL : ((2ULL << (64 - burst)) - 1);
+        u64 b;
+        if ((bits & valid) == valid) {
+            b = mulhi(r2, 65 - burst);
+        } else {
+            u64 bb = bits & valid;
+            const u64 kk = mulhi(r2, (u64)__builtin_popcountll(bb));
+            for (u64 j = 0; j < kk; j++) bb &= bb - 1;
+            b = (u64)__builtin_ctzll(bb);
+        }
+        s->mask = (burst == 64 ? ~0ULL : ((1ULL << burst) - 1)) << b;
+        s->trial = (u32)id;
+    }
+    return 0;
+}
+
+/* the attempt in flight at tick t (the first whose last event is at or after
+ * t: a flip at t precedes every event of tick t) and the phase within it */
+static void tk_locate(const tkgold_t *g, u64 t, u64 *j_out, int *phase) {
+    u64 lo = 0, hi = g->n - 1;
+    while (lo < hi) {
+        u64 mid = (lo + hi) / 2;
+        if (g->ticks[mid].done < t) lo = mid + 1; else hi = mid;
+    }
+    const or_timing_ticks_t *T = &g->ticks[lo];
+    *j_out = lo;
+    if (g->ops[lo].nfetch == 2 && t <= T->fetch_done[0]) *phase = TKP_FETCH1;
+    else if (t <= T->exec) *phase = g->ops[lo].nfetch == 2 ? TKP_FETCH2 : TKP_FETCH1;
+    else *phase = TKP_DATA;
+}
+
+static void tk_trial(const or_campaign_t *c, const or_tick_site_t *s, u64 cap, or_outcome_t *o, or_outcome_t *truth) {
+    const tkgold_t *g = c->tk;
+    u64 j; int phase;
+    tk_locate(g, s->tick, &j, &phase);
+    const tk_info_t *I = &g->info[j];
+    tkinj_t k;
+    k.phase = phase; k.target = s->target; k.mask = s->mask;
+    /* the tick of the attempt the flip lands in: its first (fetch 1), its
+     * second (straddle: fetch 2, and the execute that then follows) */
+    k.cyc = I->cyc0 + ((phase == TKP_FETCH2 || (phase == TKP_DATA && I->nfetch == 2)) ? 1 : 0);
+    const int why = tk_contract(g, j, phase, s->target, s->mask);
+    or_outcome_t lit;
+    memset(&lit, 0, sizeof lit);
+    if (truth || !why) {
+        mach_t m; mach_init(&m, c);
+        m.tki = &k;
+        run(&m, cap);
+        lit = m.res;
+        mach_free(&m);
+    }
+    if (truth) *truth = lit;
+    if (why) {
+        memset(o, 0, sizeof *o);
+        o->cls = OR_ESCAPE; o->sub = OR_ESC_TIMING; o->exit_code = (uint8_t)why; o->flags = 1;
+        o->detail = (u32)I->pc; o->ninst = I->n;
+    } else {
+        *o = lit;
+    }
+}
+
+typedef struct {
+    const or_campaign_t *c; const or_tick_site_t *s; u64 n, cap; or_outcome_t *out, *truth; int tid, nth;
+} tkjob_t;
+static void *tk_worker(void *arg) {
+    tkjob_t *j = (tkjob_t *)arg;
+    for (u64 i = (u64)j->tid; i < j->n; i += (u64)j->nth)
+        tk_trial(j->c, &j->s[i], j->cap, &j->out[i], j->truth ? &j->truth[i] : NULL);
+    return NULL;
+}
+
+int or_run_tick_trials(or_campaign_t *c, const or_tick_site_t *sites, u64 n, u64 f16, or_outcome_t *out,
+                       or_outcome_t *truth, int nth) {
+    if (!c->tk) { snprintf(c->err, sizeof c->err, "or_run_tick_trials: or_tick_setup first"); return -1; }
+    u64 cap = hang_cap(c, f16);
+    if (nth <= 1) {
+        for (u64 i = 0; i < n; i++) tk_trial(c, &sites[i], cap, &out[i], truth ? &truth[i] : NULL);
+        return 0;
+    }
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nth);
+    tkjob_t *jobs = (tkjob_t *)malloc(sizeof(tkjob_t) * nth);
+    for (int t = 0; t < nth; t++) {
+        jobs[t] = (tkjob_t){c, sites, n, cap, out, truth, t, nth};
+        pthread_create(&th[t], NULL, tk_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nth; t++) pthread_join(th[t], NULL);
+    free(th); free(jobs);
+    return 0;
 }

@@ -19,6 +19,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "timing_se.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -49,7 +51,19 @@ enum {
     OR_ESC_CSR = 3,             /* U-mode-accessible CSR */
     OR_ESC_HOST = 4,            /* behaviour that depends on the host (fd 0, huge buffers) */
     OR_ESC_RESOURCE = 5,        /* engine resource limit (private pages) -- device only */
-    OR_ESC_UNDEF = 6            /* gem5's own behaviour is undefined (GEM5_UNREACHABLE reached) */
+    OR_ESC_UNDEF = 6,           /* gem5's own behaviour is undefined (GEM5_UNREACHABLE reached) */
+    OR_ESC_TIMING = 7           /* tick-domain site the numInst engine does not reproduce (exit_code = OR_TK_*) */
+};
+/* OR_ESC_TIMING reasons (exit_code), the contract of include/fi_engine.h FI_TK_* */
+enum {
+    OR_TK_NONCOUNT = 1,   /* flip after an ecall / page-fault retry (same numInst) that the tick touches */
+    OR_TK_STRADDLE1 = 2,  /* pc flip while a straddling instruction's first half is fetched: another second word */
+    OR_TK_ALIGN = 3,      /* pc flip changes both the fetch word and pc % 4 */
+    OR_TK_STRADDLE2 = 4,  /* pc flip to a 4-aligned pc while the decoder holds a first half */
+    OR_TK_TWO = 5,        /* pc flip on auipc / jal with a link: two values change */
+    OR_TK_FAULTOP = 6,    /* pc flip (another word) on an ecall / page-fault attempt */
+    OR_TK_MACRO = 7,      /* pc flip while a macro-op's (AMO / LR / SC) access is outstanding */
+    OR_TK_CLOCK = 8       /* the trial reads curTick (clock_gettime / rpns) */
 };
 enum { OR_HANG_INSTS = 1,         /* the max-insts cap (scheduleInstStop, cpu/base.cc:764-770) */
        OR_HANG_QUIESCE = 2 };      /* m5_quiesce: the only context suspends for good (thread_context.cc:167) */
@@ -160,6 +174,36 @@ void or_set_clock(or_campaign_t *c, uint64_t period_ticks, uint64_t random_seed)
 int or_run_trials(or_campaign_t *c, const or_site_t *sites, uint64_t n,
                   uint64_t protect_mask, uint64_t hang_factor_x16,
                   or_outcome_t *out, int n_threads);
+
+/* ---- Tick-domain injection under TimingSimpleCPU (include/fi_engine.h):
+ * the golden run again, recording every fetch / execute attempt's requests
+ * (physical addresses: frames in allocation order from 0) -> timing_se.c ->
+ * the tick of each attempt.  A trial's flip at tick t is applied inside the
+ * attempt in flight, as the gem5 components would see it: before its fetch
+ * response (the decoder then reads the word fetched before the flip), between
+ * the two fetches of a straddling instruction, or while its data access is
+ * outstanding (a load's completion overwrites its rd; a pc flip resets npc to
+ * pc + 4).  Returns 0, or -1 with or_error() giving the reason (unsupported
+ * golden run: unmaps, clock reads, failed SC, prefetch / cache-block ops,
+ * vector ops). */
+int or_tick_setup(or_campaign_t *c, const or_timing_params_t *p);
+uint64_t or_tick_golden_ticks(or_campaign_t *c);
+/* copies up to cap attempts (requests and ticks); returns the count */
+uint64_t or_tick_trace(or_campaign_t *c, or_timing_op_t *ops, or_timing_ticks_t *ticks, uint64_t cap);
+typedef struct {
+    uint64_t tick;      /* flip applied before every event of this tick */
+    uint64_t mask;
+    uint32_t target;    /* 1..31, OR_T_PC, OR_T_RESULT */
+    uint32_t trial;
+} or_tick_site_t;
+/* SplitMix64 keyed by (seed, trial), as or_sample, with tick = mulhi(r0, golden ticks) */
+int or_tick_sample(or_campaign_t *c, uint64_t seed, uint64_t first, uint64_t n, uint64_t structures, uint32_t burst,
+                   uint64_t bits, or_tick_site_t *out);
+/* out[i] = the trial's outcome (an escape the contract names is reported as
+ * OR_ESC_TIMING without running it); truth (may be NULL) = the literal outcome
+ * of every trial, escapes included */
+int or_run_tick_trials(or_campaign_t *c, const or_tick_site_t *sites, uint64_t n, uint64_t hang_factor_x16,
+                       or_outcome_t *out, or_outcome_t *truth, int n_threads);
 
 /* Diagnostics: run one trial and return its full stdout in buf. */
 int or_run_one_capture(or_campaign_t *c, const or_site_t *site, uint64_t protect_mask,

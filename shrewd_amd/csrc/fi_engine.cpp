@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "fi_checkpoint.h"
+#include "fi_tick.h"
 #include "fi_types.h"
 #include "rv64_isa.h"
 
@@ -221,6 +222,17 @@ struct fi_engine {
     uint32_t *d_shadow = nullptr;    // the same as a bitmap, [ninst / 32 + 1]
     std::vector<PreInst> g_pre;      // golden pre-decoded text and trace (empty: unavailable)
     std::vector<uint32_t> g_trace;
+    // tick-domain injection (fi_set_cpu_model FI_CPU_TIMING; fi_tick.cpp, fi_timing.cpp)
+    int cpu_model = FI_CPU_ATOMIC;
+    fi_timing_params tparams{};
+    std::vector<uint64_t> alloc_order;   // process-start pages in allocation order (fi_load_elf's writes)
+    bool golden_unmapped = false;        // the golden run freed frames (munmap / brk shrink)
+    std::vector<fi_timing_op> t_ops;     // the golden run's attempts as requests
+    std::vector<TickAttempt> t_att;
+    std::vector<fi_timing_ticks> t_ticks;
+    fi_timing_stats t_stats{};
+    std::string t_status = "no golden run";
+    uint32_t clk_esc = 0;                // DevCtx::clk_esc while tick trials run
 
     // work buffers, sized for `cap` trials per launch
     uint64_t cap = 0;
@@ -496,7 +508,12 @@ static void img_write(fi_engine *e, uint64_t addr, const uint8_t *src, uint64_t 
     for (uint64_t i = 0; i < n;) {
         const uint64_t a = addr + i;
         auto &pg = e->pages[a >> 12];
-        if (pg.empty()) pg.assign(kPage, 0);
+        if (pg.empty()) {
+            pg.assign(kPage, 0);
+            // SETranslatingPortProxy (Always) allocates the frame on this first
+            // write: frames go out in this order (sim/process.cc:318-343)
+            e->alloc_order.push_back(a >> 12);
+        }
         const uint64_t off = a & (kPage - 1);
         const uint64_t k = std::min<uint64_t>(n - i, kPage - off);
         if (src) memcpy(pg.data() + off, src + i, k);
@@ -591,6 +608,7 @@ fi_status fi_load_elf(fi_engine *e, const uint8_t *elf, size_t len, const char *
     e->pages.clear();
     e->mem_pages.clear();
     e->segs.clear();
+    e->alloc_order.clear();
     if (len < 64 || memcmp(elf, "\x7f" "ELF", 4) || elf[4] != 2 || elf[5] != 1 || le16(elf + 18) != 243)
         return fail(e, FI_E_ELF, "not an ELF64 little-endian RISC-V executable");
     e->entry = le64(elf + 24);
@@ -752,6 +770,7 @@ fi_status fi_load_checkpoint(fi_engine *e, const char *cpt_dir, const uint8_t *e
     const std::vector<fi_engine::Seg> segs = e->segs;   // (fi_load_elf's; free_image keeps them)
     free_image(e);
     e->pages.clear();
+    e->alloc_order.clear();   // a checkpoint's frames: not in process-start order (no tick model)
     for (auto &kv : img.pages) e->pages[kv.first] = kv.second;
     // memory-fault candidates, as at process start (the ELF's writable
     // segments and the stack): every mapped page no read-only PT_LOAD covers
@@ -910,6 +929,7 @@ static DevCtx base_ctx(fi_engine *e) {
     c.exe_path = e->d_exe; c.exe_len = e->d_exe ? e->exe_path.size() : 0;
     c.tick0 = e->tick0;
     c.clk_until = e->clk_until;
+    c.clk_esc = e->clk_esc;
     c.stdin_data = e->stdin_on ? e->d_stdin : nullptr;
     c.stdin_len = e->stdin_on ? e->stdin_data.size() : 0;
     c.in_pos = e->d_inpos;
@@ -993,7 +1013,8 @@ static fi_status build_mem_index(fi_engine *e, const std::vector<MemEv> &mev, bo
             const uint64_t wd = a & ~7ULL, we = std::min(end, wd + 8);
             uint64_t bm = 0;
             for (uint64_t b = a; b < we; b++) bm |= 1ULL << (b - wd);
-            ent.emplace_back(wd, ((uint64_t)ev.t << 16) | ((kind & 1) ? bm << 8 : 0) | ((kind & 2) ? bm : 0));
+            ent.emplace_back(wd, ((uint64_t)(ev.t & ~kMemEvProxy) << 16) | ((kind & 1) ? bm << 8 : 0) |
+                                     ((kind & 2) ? bm : 0));
             if (ent.size() > kMaxEnt) return FI_OK;
             a = we;
         }
@@ -1021,6 +1042,31 @@ static fi_status build_mem_index(fi_engine *e, const std::vector<MemEv> &mev, bo
     return FI_OK;
 }
 
+// The golden run under TimingSimpleCPU (fi_tick.cpp, fi_timing.cpp): its
+// attempts as requests, then their ticks.  t_status says why not, if not.
+static void tick_prepare(fi_engine *e, const std::vector<MemEv> &mev, bool mev_ok) {
+    e->t_ops.clear(); e->t_att.clear(); e->t_ticks.clear(); e->t_stats = fi_timing_stats{};
+    if (e->cpu_model != FI_CPU_TIMING) { e->t_status = "the CPU model is AtomicSimpleCPU (fi_set_cpu_model)"; return; }
+    if (e->alloc_order.empty()) { e->t_status = "a checkpoint start: its frame order is not known"; return; }
+    if (e->clk_until) { e->t_status = "the golden run reads curTick: its output depends on the CPU model"; return; }
+    if (e->golden_unmapped) { e->t_status = "the golden run unmaps memory: freed frames are reused"; return; }
+    if (!mev_ok || e->g_trace.empty()) { e->t_status = "the golden access record is incomplete"; return; }
+    TickGoldenIn in{&e->g_trace, &e->g_pre, e->text_lo, &mev, &e->alloc_order, e->stack_min0, e->svma_lo,
+                    e->svma_hi, kStackBase, kMaxStack, e->golden.ninst, e->golden.ncycles};
+    std::string why = build_tick_attempts(in, e->t_ops, e->t_att);
+    if (why.empty()) {
+        e->t_ticks.resize(e->t_ops.size());
+        if (fi_timing_model_run(e->t_ops.data(), e->t_ops.size(), &e->tparams, e->t_ticks.data(), &e->t_stats))
+            why = "the timing model rejected the golden requests (a state gem5 asserts on)";
+    }
+    if (!why.empty()) {
+        e->t_ops.clear(); e->t_att.clear(); e->t_ticks.clear();
+        e->t_status = why;
+        return;
+    }
+    e->t_status = "";
+}
+
 fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     if (!e) return FI_E_ARG;
     if (!e->loaded) return fail(e, FI_E_STATE, "fi_golden_run: no workload loaded");
@@ -1028,6 +1074,8 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     fi_status st = ensure_work(e, 64);
     if (st) return st;
     // back to the process-start image only
+    e->t_status = "no golden run";
+    e->t_ops.clear(); e->t_att.clear(); e->t_ticks.clear();
     e->snaps.resize(1);
     e->tab.resize(e->n_start_frames);
     e->pool.resize((uint64_t)e->n_start_frames * kPage);
@@ -1246,6 +1294,8 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
     if (st) return st;
     st = build_mem_index(e, mev, live_ok && n_mem <= mem_cap);
     if (st) return st;
+    e->golden_unmapped = stats[62] != 0;
+    tick_prepare(e, mev, !trace.empty() && n_mem <= mem_cap);
 
     // ---- translate the golden basic blocks and build the trial kernel with
     // them (hipRTC); the static kernel stays the fallback
@@ -1765,6 +1815,164 @@ fi_status fi_run_trials(fi_engine *e, uint64_t first, uint64_t n, fi_outcome *ou
 fi_status fi_run_sites(fi_engine *e, const fi_site *sites, uint64_t n, fi_outcome *out, fi_histogram *hist) {
     if (!sites && n) return FI_E_ARG;
     return run_common(e, 0, sites, n, out, hist);
+}
+
+// ---------------------------------------------------- tick-domain injection
+fi_status fi_set_cpu_model(fi_engine *e, int model, const fi_timing_params *p) {
+    if (!e) return FI_E_ARG;
+    if (model != FI_CPU_ATOMIC && model != FI_CPU_TIMING) return fail(e, FI_E_ARG, "unknown CPU model %d", model);
+    if (e->have_golden) return fail(e, FI_E_STATE, "fi_set_cpu_model: set before fi_golden_run");
+    e->cpu_model = model;
+    if (p) e->tparams = *p; else fi_timing_default_params(&e->tparams);
+    return FI_OK;
+}
+
+fi_status fi_tick_golden(fi_engine *e, fi_tick_info *out) {
+    if (!e || !out) return FI_E_ARG;
+    *out = fi_tick_info{};
+    snprintf(out->status, sizeof out->status, "%s", e->t_status.c_str());
+    out->attempts = e->t_ops.size();
+    out->golden_ticks = e->t_stats.ticks;
+    out->stats = e->t_stats;
+    return FI_OK;
+}
+
+fi_status fi_tick_trace(fi_engine *e, fi_timing_op *ops, fi_timing_ticks *ticks, uint64_t cap, uint64_t *n) {
+    if (!e) return FI_E_ARG;
+    if (!e->t_status.empty()) return fail(e, FI_E_STATE, "tick model: %s", e->t_status.c_str());
+    const uint64_t k = std::min<uint64_t>(cap, e->t_ops.size());
+    if (ops && k) memcpy(ops, e->t_ops.data(), k * sizeof *ops);
+    if (ticks && k) memcpy(ticks, e->t_ticks.data(), k * sizeof *ticks);
+    if (n) *n = e->t_ops.size();
+    return FI_OK;
+}
+
+static uint64_t splitmix_host(uint64_t &s) {   // the sampler's SplitMix64 (fi_kernels.hip)
+    uint64_t z = (s += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+static uint64_t mulhi64(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
+
+static fi_status tick_ready(fi_engine *e) {
+    if (!e->have_golden) return fail(e, FI_E_STATE, "golden run required");
+    if (!e->t_status.empty()) return fail(e, FI_E_STATE, "tick model: %s", e->t_status.c_str());
+    return FI_OK;
+}
+
+fi_status fi_sample_tick_sites(fi_engine *e, uint64_t first, uint64_t n, fi_tick_site *out) {
+    if (!e || (!out && n)) return FI_E_ARG;
+    fi_status st = tick_ready(e);
+    if (st) return st;
+    if (!e->structures) return fail(e, FI_E_STATE, "fi_set_campaign first");
+    if (e->structures & (1ULL << FI_T_MEM)) return fail(e, FI_E_ARG, "tick sites: memory words are not supported");
+    const uint64_t structures = e->structures;
+    const uint32_t nt = (uint32_t)__builtin_popcountll(structures), burst = e->burst;
+    const uint64_t valid = burst == 1 ? ~0ULL : ((2ULL << (64 - burst)) - 1);
+    for (uint64_t i = 0; i < n; i++) {   // fi_sample_kernel's draw with the golden run's ticks for numInst
+        const uint64_t id = first + i;
+        uint64_t s = e->seed ^ (id * 0xD6E8FEB86659FD93ULL);
+        const uint64_t r0 = splitmix_host(s), r1 = splitmix_host(s), r2 = splitmix_host(s);
+        fi_tick_site &o = out[i];
+        o.tick = mulhi64(r0, e->t_stats.ticks);
+        const uint64_t k = mulhi64(r1, nt);
+        uint64_t m = structures;
+        for (uint64_t j = 0; j < k; j++) m &= m - 1;
+        o.target = (uint32_t)__builtin_ctzll(m);
+        uint64_t b;
+        if ((e->bits & valid) == valid) {
+            b = mulhi64(r2, 65 - burst);
+        } else {
+            uint64_t mm = e->bits & valid;
+            const uint64_t kk = mulhi64(r2, (uint64_t)__builtin_popcountll(mm));
+            for (uint64_t j = 0; j < kk; j++) mm &= mm - 1;
+            b = (uint64_t)__builtin_ctzll(mm);
+        }
+        o.mask = (burst == 64 ? ~0ULL : ((1ULL << burst) - 1)) << b;
+        o.trial = (uint32_t)id;
+    }
+    return FI_OK;
+}
+
+fi_status fi_map_tick_sites(fi_engine *e, const fi_tick_site *ts, uint64_t n, fi_site *sites, uint8_t *disp,
+                            fi_outcome *host_out) {
+    if (!e || (n && (!ts || !sites || !disp))) return FI_E_ARG;
+    fi_status st = tick_ready(e);
+    if (st) return st;
+    for (uint64_t i = 0; i < n; i++) {
+        const fi_tick_site &t = ts[i];
+        const bool target_ok = (t.target >= 1 && t.target <= FI_T_PC) || t.target == FI_T_RESULT;
+        if (!t.mask || !target_ok || t.tick >= e->t_stats.ticks)
+            return fail(e, FI_E_ARG, "tick site %llu: target %u, tick %llu (golden run %llu ticks)",
+                        (unsigned long long)i, t.target, (unsigned long long)t.tick,
+                        (unsigned long long)e->t_stats.ticks);
+        const TickMapped m = map_tick_site(e->t_att, e->t_ticks, e->golden.ninst, t.tick, t.target, t.mask, t.trial);
+        disp[i] = (uint8_t)m.disp;
+        sites[i] = m.site;
+        if (host_out) {
+            fi_outcome o{};
+            if (m.disp == 1) {   // the golden run itself
+                o.cls = FI_MASKED; o.sub = (uint8_t)e->gsub; o.exit_code = (uint8_t)e->golden.exit_code;
+                o.flags = 1; o.detail = e->gdetail; o.ninst = e->golden.ninst;
+            } else if (m.disp == 2) {
+                const TickAttempt &A = e->t_att[m.attempt];
+                o.cls = FI_ESCAPE; o.sub = FI_ESC_TIMING; o.exit_code = (uint8_t)m.reason;
+                o.flags = 1; o.detail = (uint32_t)A.pc; o.ninst = A.n;
+            }
+            host_out[i] = o;
+        }
+    }
+    return FI_OK;
+}
+
+fi_status fi_run_tick_sites(fi_engine *e, const fi_tick_site *ts, uint64_t n, fi_outcome *out, fi_histogram *hist) {
+    if (!e || (n && !ts)) return FI_E_ARG;
+    fi_status st = tick_ready(e);
+    if (st) return st;
+    if (e->protect || e->protect_opc)
+        return fail(e, FI_E_ARG, "tick sites: selective replication (fi_set_protect*) is not supported");
+    std::vector<fi_site> sites(n);
+    std::vector<uint8_t> disp(n);
+    std::vector<fi_outcome> res(n);
+    st = fi_map_tick_sites(e, ts, n, sites.data(), disp.data(), res.data());
+    if (st) return st;
+    std::vector<fi_site> run;
+    std::vector<uint64_t> idx;
+    for (uint64_t i = 0; i < n; i++)
+        if (disp[i] == 0) { run.push_back(sites[i]); idx.push_back(i); }
+    fi_histogram dh{};
+    if (!run.empty()) {
+        std::vector<fi_outcome> ro(run.size());
+        e->clk_esc = 1;   // this engine's clock is AtomicSimpleCPU's: a curTick read escapes
+        st = run_common(e, 0, run.data(), run.size(), ro.data(), &dh);
+        e->clk_esc = 0;
+        if (st) return st;
+        for (size_t q = 0; q < idx.size(); q++) res[idx[q]] = ro[q];
+    }
+    if (out) memcpy(out, res.data(), n * sizeof *out);
+    if (hist) {   // by the tick site's own structure and bit (fi_hist_kernel's layout)
+        for (uint64_t i = 0; i < n; i++) {
+            const fi_outcome &o = res[i];
+            const uint32_t cls = o.cls < FI_N_CLASS ? o.cls : FI_ESCAPE;
+            hist->counts[ts[i].target][__builtin_ctzll(ts[i].mask)][cls]++;
+            if (cls == FI_CRASH) hist->crash_sub[o.sub & 15]++;
+            if (cls == FI_ESCAPE) hist->escape_sub[o.sub & 7]++;
+            hist->trials++;
+            hist->guest_insts += o.ninst;
+        }
+        hist->fetch_bytes += dh.fetch_bytes; hist->data_bytes += dh.data_bytes;
+        hist->cow_pages += dh.cow_pages; hist->device_insts += dh.device_insts;
+    }
+    return FI_OK;
+}
+
+fi_status fi_run_tick_trials(fi_engine *e, uint64_t first, uint64_t n, fi_outcome *out, fi_histogram *hist) {
+    if (!e) return FI_E_ARG;
+    std::vector<fi_tick_site> ts(n);
+    fi_status st = fi_sample_tick_sites(e, first, n, ts.data());
+    if (st) return st;
+    return fi_run_tick_sites(e, ts.data(), n, out, hist);
 }
 
 fi_status fi_run_trials_device(fi_engine *e, uint64_t first, uint64_t n, void *d_out, void *d_hist, void *stream) {

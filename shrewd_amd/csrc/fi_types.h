@@ -92,9 +92,10 @@ struct VmState {
 // instruction (or syscall) at numInst == t.
 struct MemEv {
     uint64_t addr;
-    uint32_t t;
+    uint32_t t;                      // numInst | kMemEvProxy for an access of a syscall (not a CPU request)
     uint32_t len_kind;               // len (< 2^30) | kind << 30
 };
+constexpr uint32_t kMemEvProxy = 0x80000000u;
 
 // First-access forwarding (fi_forward_kernel): the golden run's register
 // accesses (always) and its memory accesses (when complete and the golden
@@ -206,6 +207,10 @@ struct DevCtx {
     const uint8_t *exe_path;         // realpath of the executable (readlinkat /proc/self/exe), exe_len bytes
     uint64_t exe_len;                // 0: unknown (that call escapes as host)
     uint64_t clk_period;             // ticks per CPU cycle (clock_gettime)
+    uint32_t clk_esc;                // tick-domain trials (fi_run_tick_trials): a curTick read (clock_gettime,
+                                     // rpns) ends the trial as FI_ESC_TIMING / FI_TK_CLOCK -- the engine's
+                                     // clock is AtomicSimpleCPU's, not TimingSimpleCPU's
+    uint32_t clk_esc_pad;
     uint64_t tick0;                  // curTick at the campaign start (a checkpoint's [Globals] curTick; else 0)
     const uint8_t *stdin_data;       // Process.input as a file: its bytes (NULL: "cin", reads of fd 0 escape)
     uint64_t stdin_len;
@@ -241,6 +246,7 @@ struct DevCtx {
                                      // [27] register faults dead at injection [30] trials re-run with more private
                                      // pages (FI_ESC_RESOURCE, fi_engine.cpp run_chunk)
                                      // [52] record mode: 1 + numInst of the golden run's last curTick read
+                                     // [62] record mode: the golden run unmapped memory (munmap, brk shrink)
                                      // [53] solo_fast_run calls [54] instructions they ran [55] hand-backs
                                      // [56] hangs proved by the clean body's counted-loop test
                                      // [57] page-fault crashes proved in run-off loops [58] loop proofs undecided

@@ -451,6 +451,7 @@ __device__ bool vm_add(VmState *v, uint64_t lo, uint64_t hi) {
 // stack page gets one).  0 ok, 1 no private page left, 2 the VMA list is full
 // (resource escapes; exit code kEscTable for the latter, vm_esc).
 __device__ int vm_unmap(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot, VmState *v, uint64_t lo, uint64_t hi) {
+    if (c->record) c->stats[62] = 1;   // frames freed: the tick model's frame order no longer holds
     const uint32_t n = v->nvma;
     for (uint32_t i = 0; i < n; i++) {
         const uint64_t a = v->vma[i][0], b = v->vma[i][1];
@@ -531,7 +532,7 @@ __device__ bool proxy_write(KCtx *c, const WaveMem &w, LaneMem &m, uint64_t slot
 }
 
 enum { F_NONE = 0, F_SYSCALL, F_BREAK, F_ILLEGAL, F_UNKNOWN, F_ESCAPE, F_ESCCSR, F_PGFAULT, F_NEEDPAGE, F_DETECT,
-       F_AMOLINE, F_SCLINE, F_M5PANIC, F_UNDEF, F_VSEW };
+       F_AMOLINE, F_SCLINE, F_M5PANIC, F_UNDEF, F_VSEW, F_TKCLOCK };
 
 // AtomicSimpleCPU::readMem/writeMem (atomic.cc:331-544): the access is split
 // at 64-byte line boundaries, each fragment translated on its own; faults are
@@ -932,7 +933,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         uint8_t *rec = fd == 1 ? c->rec_out : c->rec_err;
         uint64_t cur_vpn = kNone;
         const uint8_t *pg = nullptr;
-        if (c->record) rec_mem(c, buf, n, L.ninst, 1u);
+        if (c->record) rec_mem(c, buf, n, L.ninst | kMemEvProxy, 1u);
         for (uint64_t i = 0; i < n; i++) {
             const uint64_t a = buf + i;
             if ((a >> 12) != cur_vpn) { cur_vpn = a >> 12; pg = page_of(lookup(c, w, m, slot, cur_vpn)); }
@@ -947,14 +948,14 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         pos += n;
     };
     auto rd64 = [&](uint64_t a) {
-        if (c->record) rec_mem(c, a, 8, L.ninst, 1u);
+        if (c->record) rec_mem(c, a, 8, L.ninst | kMemEvProxy, 1u);
         uint64_t v = 0;
         for (int k = 0; k < 8; k++) v |= (uint64_t)proxy_byte(c, w, m, slot, a + k) << (8 * k);
         return v;
     };
     auto set_ret = [&](int64_t v) { RREG(10) = (uint64_t)v; };
     auto pwrite = [&](uint64_t a, const char *src, uint64_t n) {
-        if (c->record) rec_mem(c, a, n, L.ninst, 2u);
+        if (c->record) rec_mem(c, a, n, L.ninst | kMemEvProxy, 2u);
         return proxy_write(c, w, m, slot, a, src, n);
     };
     switch (num) {
@@ -1114,6 +1115,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         return a0 < c->code_hi && a0 + a1 > c->code_lo;
     }
     case 113: {   // clock_gettimeFunc (syscall_emul.hh:2266-2278): curTick() in ns + 1e9 s
+        if (c->clk_esc) { finish(L, FI_ESCAPE, FI_ESC_TIMING, FI_TK_CLOCK, pc32); return false; }
         if (!a1) { finish(L, FI_CRASH, FI_CRASH_SE_PANIC, 134, pc32); return false; }
         if (!proxy_readable(c, w, m, slot, a1, 16)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
         const uint64_t ns = (c->tick0 + (L.ncyc - 1) * c->clk_period) / 1000;
@@ -1201,7 +1203,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
             if (n == 4096) { finish(L, FI_ESCAPE, FI_ESC_HOST, 0, pc32); return false; }
             if (a1 + n < a1 || !proxy_readable(c, w, m, slot, a1 + n, 1)) { set_ret(-14); return false; }
             const uint8_t ch = proxy_byte(c, w, m, slot, a1 + n);
-            if (c->record) rec_mem(c, a1 + n, 1, L.ninst, 1u);
+            if (c->record) rec_mem(c, a1 + n, 1, L.ninst | kMemEvProxy, 1u);
             if (n == 0) first = ch;
             if (n < 15) exe = exe && ch == (uint8_t)want[n];
             if (!ch) break;
@@ -1264,12 +1266,12 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
             if (!proxy_readable(c, w, m, slot, cpus_user, usz)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
             uint64_t ub = 0;
             for (uint64_t q = 0; q < usz; q++) ub |= (uint64_t)proxy_byte(c, w, m, slot, cpus_user + q) << (8 * q);
-            if (c->record) rec_mem(c, cpus_user, usz, L.ninst, 1u);
+            if (c->record) rec_mem(c, cpus_user, usz, L.ninst | kMemEvProxy, 1u);
             uint64_t cpus = ub ? ub : 1;
             if (!ub) cpusetsize = 8;
             cpus &= 1;
             if (psz && !proxy_readable(c, w, m, slot, pairs, psz)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
-            if (c->record) rec_mem(c, pairs, psz, L.ninst, 1u);
+            if (c->record) rec_mem(c, pairs, psz, L.ninst | kMemEvProxy, 1u);
             int64_t bad = -1;   // the first invalid key's index
             for (uint64_t i = 0; i < count; i++) {
                 const int64_t key = (int64_t)rd64(pairs + 16 * i);
@@ -1304,11 +1306,11 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
         if (cpusetsize > 8) cpusetsize = 8;
         if (!(cpusetsize == 0 && !cpus_user)) {
             if (!proxy_readable(c, w, m, slot, cpus_user, cpusetsize)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
-            if (c->record) rec_mem(c, cpus_user, cpusetsize, L.ninst, 1u);
+            if (c->record) rec_mem(c, cpus_user, cpusetsize, L.ninst | kMemEvProxy, 1u);
             if (cpusetsize < 8 || !(proxy_byte(c, w, m, slot, cpus_user) & 1)) { set_ret(-22); return false; }
         }
         if (psz && !proxy_readable(c, w, m, slot, pairs, psz)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
-        if (c->record) rec_mem(c, pairs, psz, L.ninst, 1u);
+        if (c->record) rec_mem(c, pairs, psz, L.ninst | kMemEvProxy, 1u);
         if (!copy_out_ok(pairs, psz)) return false;
         for (uint64_t i = 0; i < count; i++) {
             int64_t key = (int64_t)rd64(pairs + 16 * i);
@@ -1335,7 +1337,7 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
     if (n) {
         if (!proxy_readable(c, w, m, slot, buf, n)) { finish(L, FI_CRASH, FI_CRASH_PROXY, 1, pc32); return false; }
         if (fd == 0) {   // the input file, opened O_RDONLY (fd_array.cc:69-75): host write() -> EBADF
-            if (c->record) rec_mem(c, buf, n, L.ninst, 1u);
+            if (c->record) rec_mem(c, buf, n, L.ninst | kMemEvProxy, 1u);
         } else {
             emit(fd, buf, n);
         }
@@ -5038,6 +5040,7 @@ __device__ __forceinline__ void trial_body() {
                 // rpns: curTick() in ns during this instruction's execute -- its
                 // fetch tick(s) already elapsed (the commit adds them to ncyc)
                 case 0x07:
+                    if (CX->clk_esc) { f = F_TKCLOCK; break; }
                     v = (CX->tick0 + (L.ncyc + ticks - 1) * CX->clk_period) / 1000;
                     if (CX->record) CX->stats[52] = L.ninst + 1;
                     break;
@@ -5261,6 +5264,7 @@ __device__ __forceinline__ void trial_body() {
         case F_M5PANIC: finish(L, FI_CRASH, FI_CRASH_M5_PANIC, 134, (uint32_t)pc); break;
         case F_VSEW: finish(L, FI_CRASH, FI_CRASH_VSET_SEW, 134, (uint32_t)pc); break;
         case F_UNDEF: finish(L, FI_ESCAPE, FI_ESC_UNDEF, 0, d.raw); break;
+        case F_TKCLOCK: finish(L, FI_ESCAPE, FI_ESC_TIMING, FI_TK_CLOCK, (uint32_t)pc); break;
         case F_PGFAULT: {   // GenericPageTableFault::invoke -> fixupFault (sim/faults.cc:95-105)
             int h;
             OOL(h = fixup_fault(CX, mc_, slot, fva));

@@ -23,7 +23,12 @@ CRASH_NAMES = {1: "panic_unknown_inst", 2: "panic_illegal_inst", 3: "panic_page_
                4: "fatal_syscall_range", 5: "fatal_syscall_unimpl", 6: "fatal_proxy", 7: "abort_fd_assert",
                8: "sigtrap", 9: "fatal_stack_limit", 10: "panic_amo_line", 11: "abort_sc_line", 12: "panic_se_handler",
                13: "panic_m5op", 14: "abort_vset_sew"}
-ESCAPE_NAMES = {1: "inst", 2: "syscall", 3: "csr", 4: "host", 5: "resource", 6: "undefined"}
+ESCAPE_NAMES = {1: "inst", 2: "syscall", 3: "csr", 4: "host", 5: "resource", 6: "undefined", 7: "timing"}
+# FI_ESC_TIMING reasons (exit_code): tick sites that are not a numInst injection (include/fi_engine.h FI_TK_*)
+TICK_ESCAPE_NAMES = {1: "after_noncounting_tick", 2: "pc_straddle_first_fetch", 3: "pc_word_and_alignment",
+                     4: "pc_aligned_mid_decode", 5: "pc_two_values", 6: "pc_on_fault_attempt",
+                     7: "pc_macro_op_access", 8: "reads_curtick"}
+CPU_ATOMIC, CPU_TIMING = 0, 1
 HANG_NAMES = {1: "max_insts", 2: "m5_quiesce"}
 END_NAMES = {0: "exit", 1: "m5_exit", 2: "m5_fail"}     # sub-codes of masked / sdc: how the run ended
 T_PC, T_MEM, T_RESULT, N_STRUCT = 32, 33, 34, 35
@@ -145,6 +150,66 @@ class IssueStats(C.Structure):
 
 
 ISSUE_OP_DT = np.dtype([("src", "<u8"), ("dst", "<u8"), ("opclass", "u1"), ("kind", "u1"), ("pad", "u1", (6,))])
+
+# ---- tick-domain injection under TimingSimpleCPU (include/fi_engine.h)
+TIMING_OP_DT = np.dtype([("fetch", "<u8", (2,)), ("addr", "<u8", (2,)), ("size", "<u2", (2,)), ("nfetch", "u1"),
+                         ("nfrag", "u1"), ("kind", "u1"), ("cmd", "u1"), ("pad", "u1", (8,))])
+TIMING_TICKS_DT = np.dtype([("fetch_send", "<u8", (2,)), ("fetch_done", "<u8", (2,)), ("exec", "<u8"),
+                            ("done", "<u8")])
+TICK_SITE_DT = np.dtype([("tick", "<u8"), ("mask", "<u8"), ("target", "<u4"), ("trial", "<u4")])
+TOP_EXEC, TOP_FAULT, TOP_END = 0, 1, 2
+TCMD_READ, TCMD_WRITE, TCMD_SWAP, TCMD_LL, TCMD_SC = 0, 1, 2, 3, 4
+
+
+class TimingParams(C.Structure):
+    """fi_timing_params: the reference SE board (NoCache SystemXBar, DDR3-1600, 3 GHz)."""
+    _fields_ = ([("cpu_period", C.c_uint64)] +
+                [(n, C.c_uint32) for n in ("xbar_frontend", "xbar_forward", "xbar_response", "xbar_header",
+                                           "xbar_width", "xbar_sf_lookup")] +
+                [(n, C.c_uint64) for n in ("mc_frontend", "mc_backend", "mc_command_window")] +
+                [(n, C.c_uint32) for n in ("read_buffer", "write_buffer", "write_high_pct", "write_low_pct",
+                                           "min_writes_per_switch", "min_reads_per_switch")] +
+                [(n, C.c_uint64) for n in ("tCK", "tBURST", "tRCD", "tCL", "tRP", "tRAS", "tRRD", "tXAW", "tRFC",
+                                           "tWR", "tWTR", "tRTP", "tRTW", "tCS", "tREFI")] +
+                [(n, C.c_uint32) for n in ("activation_limit", "ranks", "banks", "burst_bytes",
+                                           "row_buffer_bytes", "max_accesses_per_row")] +
+                [("mem_bytes", C.c_uint64)])
+
+
+class TimingStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("ops", "ticks", "reads", "writes", "write_queue_hits", "row_hits",
+                                          "activates", "refreshes", "xbar_retries", "mc_retries")]
+
+    def as_dict(self) -> dict:
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+class TickInfo(C.Structure):
+    _fields_ = [("golden_ticks", C.c_uint64), ("attempts", C.c_uint64), ("stats", TimingStats),
+                ("status", C.c_char * 160)]
+
+
+def timing_params(**kw) -> TimingParams:
+    """The reference board's timing parameters with overrides by field name."""
+    p = TimingParams()
+    lib().fi_timing_default_params(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, int(v))
+    return p
+
+
+def timing_model_run(ops: np.ndarray, params: TimingParams | None = None):
+    """fi_timing_model_run (pure host code): -> (ticks TIMING_TICKS_DT[n], TimingStats)."""
+    ops = np.ascontiguousarray(ops, TIMING_OP_DT)
+    out = np.zeros(len(ops), TIMING_TICKS_DT)
+    st = TimingStats()
+    rc = lib().fi_timing_model_run(ops.ctypes.data, len(ops), C.byref(params or timing_params()),
+                                   out.ctypes.data, C.byref(st))
+    if rc != FI_OK:
+        raise EngineError(f"fi_timing_model_run: {rc}")
+    return out, st
+
+
 ISSUE_PLAIN, ISSUE_LOAD, ISSUE_STORE, ISSUE_SERIAL = 0, 1, 2, 3
 FU_NAMES = ("IntALU", "IntMultDiv", "FP_ALU", "FP_MultDiv", "RdWrPort", "IprPort")
 
@@ -240,6 +305,15 @@ def lib():
         L.fi_issue_model_run.argtypes = [vp, C.c_uint64, C.POINTER(IssueParams), vp, C.POINTER(IssueStats)]
         L.fi_set_issue_model.argtypes = [vp, C.POINTER(IssueParams)]
         L.fi_shadow_map.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(IssueStats)]
+        L.fi_timing_default_params.argtypes = [C.POINTER(TimingParams)]
+        L.fi_timing_model_run.argtypes = [vp, C.c_uint64, C.POINTER(TimingParams), vp, C.POINTER(TimingStats)]
+        L.fi_set_cpu_model.argtypes = [vp, C.c_int, C.POINTER(TimingParams)]
+        L.fi_tick_golden.argtypes = [vp, C.POINTER(TickInfo)]
+        L.fi_tick_trace.argtypes = [vp, vp, vp, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.fi_sample_tick_sites.argtypes = [vp, C.c_uint64, C.c_uint64, vp]
+        L.fi_map_tick_sites.argtypes = [vp, vp, C.c_uint64, vp, vp, vp]
+        L.fi_run_tick_sites.argtypes = [vp, vp, C.c_uint64, vp, vp]
+        L.fi_run_tick_trials.argtypes = [vp, C.c_uint64, C.c_uint64, vp, vp]
         L.fi_translate_status.restype = C.c_char_p
         L.fi_translate_status.argtypes = [vp]
         _lib = L
@@ -367,6 +441,61 @@ class Engine:
         out = np.zeros(n.value, np.uint8)
         self._chk(self.L.fi_shadow_map(self.h, out.ctypes.data, n.value, C.byref(n), C.byref(st)), "fi_shadow_map")
         return out, st
+
+    # ---- tick-domain injection under TimingSimpleCPU
+    def set_cpu_model(self, model: int | str, params: TimingParams | None = None):
+        """fi_set_cpu_model: 'atomic' (numInst sites) or 'timing' (tick sites on
+        the reference board); before golden_run()."""
+        if isinstance(model, str):
+            model = {"atomic": CPU_ATOMIC, "timing": CPU_TIMING}[model.lower().removesuffix("simplecpu")]
+        self._chk(self.L.fi_set_cpu_model(self.h, model, C.byref(params) if params is not None else None),
+                  "fi_set_cpu_model")
+
+    def tick_info(self) -> dict:
+        t = TickInfo()
+        self._chk(self.L.fi_tick_golden(self.h, C.byref(t)), "fi_tick_golden")
+        return {"golden_ticks": int(t.golden_ticks), "attempts": int(t.attempts), "stats": t.stats.as_dict(),
+                "status": t.status.decode()}
+
+    def tick_trace(self):
+        """(ops TIMING_OP_DT, ticks TIMING_TICKS_DT): the golden run's attempts."""
+        n = C.c_uint64()
+        self._chk(self.L.fi_tick_trace(self.h, None, None, 0, C.byref(n)), "fi_tick_trace")
+        ops = np.zeros(n.value, TIMING_OP_DT)
+        ticks = np.zeros(n.value, TIMING_TICKS_DT)
+        self._chk(self.L.fi_tick_trace(self.h, ops.ctypes.data, ticks.ctypes.data, n.value, C.byref(n)),
+                  "fi_tick_trace")
+        return ops, ticks
+
+    def sample_tick_sites(self, first: int, n: int) -> np.ndarray:
+        out = np.zeros(n, TICK_SITE_DT)
+        self._chk(self.L.fi_sample_tick_sites(self.h, first, n, out.ctypes.data), "fi_sample_tick_sites")
+        return out
+
+    def map_tick_sites(self, ts: np.ndarray):
+        """-> (numInst sites, disposition 0 run / 1 golden / 2 escape, host outcomes)"""
+        ts = np.ascontiguousarray(ts, TICK_SITE_DT)
+        sites = np.zeros(len(ts), SITE_DT)
+        disp = np.zeros(len(ts), np.uint8)
+        ho = np.zeros(len(ts), OUTCOME_DT)
+        self._chk(self.L.fi_map_tick_sites(self.h, ts.ctypes.data, len(ts), sites.ctypes.data, disp.ctypes.data,
+                                           ho.ctypes.data), "fi_map_tick_sites")
+        return sites, disp, ho
+
+    def run_tick_sites(self, ts: np.ndarray):
+        ts = np.ascontiguousarray(ts, TICK_SITE_DT)
+        out = np.zeros(len(ts), OUTCOME_DT)
+        hist = np.zeros(1, HIST_DT)
+        self._chk(self.L.fi_run_tick_sites(self.h, ts.ctypes.data, len(ts), out.ctypes.data, hist.ctypes.data),
+                  "fi_run_tick_sites")
+        return out, hist[0]
+
+    def run_tick_trials(self, first: int, n: int, want_outcomes: bool = True):
+        out = np.zeros(n, OUTCOME_DT) if want_outcomes else None
+        hist = np.zeros(1, HIST_DT)
+        self._chk(self.L.fi_run_tick_trials(self.h, first, n, out.ctypes.data if out is not None else None,
+                                            hist.ctypes.data), "fi_run_tick_trials")
+        return out, hist[0]
 
     def sample(self, first: int, n: int) -> np.ndarray:
         out = np.zeros(n, SITE_DT)
@@ -564,7 +693,11 @@ class FaultCampaign:
     file, opened relative to the working directory, that fd 0 reads);
     checkpoint (a gem5 SE checkpoint directory to start from),
     shadow_fu_model (SHREWD FU contention for result faults, off by default),
-    priority_to_shadow and issue_params (the O3 issue model's parameters).
+    priority_to_shadow and issue_params (the O3 issue model's parameters);
+    cpu_type ("atomic": sites at a committed-instruction count, the default;
+    "timing": sites at a tick of a TimingSimpleCPU run on the reference run
+    script's NoCache + SingleChannelDDR3_1600 board -- simple_binary_run.py's
+    CPUTypes.TIMING -- mapped to the instruction in flight) and timing_params.
     """
 
     def __init__(self, workload: str, cmd: Sequence[str] | None = None, env: Sequence[str] | None = None,
@@ -572,7 +705,8 @@ class FaultCampaign:
                  protect_mask: int = 0, num_gpus: int = 1, max_insts_factor: float = 2.0, output: str = "",
                  device: int = 0, private_pages: int = 16, protect_opclasses=(), bits=None,
                  shadow_fu_model: bool = False, priority_to_shadow: bool = False, issue_params: dict | None = None,
-                 checkpoint: str = "", executable: str | None = None, input: str = "cin"):
+                 checkpoint: str = "", executable: str | None = None, input: str = "cin",
+                 cpu_type: str = "atomic", timing_params: TimingParams | None = None):
         self.workload, self.cmd, self.env = workload, list(cmd or [workload]), list(env or [])
         self.trials, self.seed, self.structures, self.burst = trials, seed, structures, burst
         self.protect_mask, self.num_gpus, self.output = protect_mask, num_gpus, output
@@ -601,8 +735,14 @@ class FaultCampaign:
                 raise ValueError("input='': gem5 polls fd -1 and retries read(0) forever")
             with open(input, "rb") as f:
                 self.engine.set_stdin(f.read())
+        self.cpu_type = cpu_type.lower().removesuffix("simplecpu")
+        if self.cpu_type not in ("atomic", "timing"):
+            raise ValueError(f"cpu_type {cpu_type!r}: 'atomic' or 'timing'")
+        self.engine.set_cpu_model(self.cpu_type, timing_params)
         # trials start at once; the translated kernels join when their build lands
         self.golden = self.engine.golden_run(wait_translation=False)
+        if self.cpu_type == "timing" and self.engine.tick_info()["status"]:
+            raise EngineError(f"cpu_type='timing': {self.engine.tick_info()['status']}")
         self.engine.set_campaign(seed, structures, burst)
         self.bits = bits_mask(bits)
         self.engine.set_bits(self.bits)
@@ -638,7 +778,10 @@ class FaultCampaign:
                 rank, world = dist.get_rank(), dist.get_world_size()
         lo, cnt = shard_range(n, world, rank)
         self.first = first_trial + lo
-        self.outcomes, self._hist = self.engine.run_trials(self.first, cnt)
+        if self.cpu_type == "timing":
+            self.outcomes, self._hist = self.engine.run_tick_trials(self.first, cnt)
+        else:
+            self.outcomes, self._hist = self.engine.run_trials(self.first, cnt)
         if world > 1:
             import torch
             import torch.distributed as dist

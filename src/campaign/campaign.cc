@@ -25,10 +25,10 @@ const char *kCrash[] = {"", "panic_unknown_inst", "panic_illegal_inst", "panic_p
                         "fatal_syscall_unimpl", "fatal_proxy", "abort_fd_assert", "sigtrap", "fatal_stack_limit",
                         "panic_amo_line", "abort_sc_line", "panic_se_handler", "panic_m5op",
                         "abort_vset_sew"};
-const char *kEscape[] = {"", "inst", "syscall", "csr", "host", "resource", "undefined"};
+const char *kEscape[] = {"", "inst", "syscall", "csr", "host", "resource", "undefined", "timing"};
 constexpr int kNCrash = sizeof(kCrash) / sizeof(kCrash[0]);
 constexpr int kNEscape = sizeof(kEscape) / sizeof(kEscape[0]);
-static_assert(kNCrash == FI_CRASH_VSET_SEW + 1 && kNEscape == FI_ESC_UNDEF + 1, "sub-code names");
+static_assert(kNCrash == FI_CRASH_VSET_SEW + 1 && kNEscape == FI_ESC_TIMING + 1, "sub-code names");
 
 void check(fi_engine *e, fi_status s, const char *what) {
     if (s != FI_OK) {
@@ -145,6 +145,9 @@ Campaign::Campaign(const CampaignParams &p) : p_(p) {
         const std::string x = p_.executable.empty() ? p_.workload : p_.executable;
         if (char *rp = realpath(x.c_str(), nullptr)) { exe = rp; free(rp); }
     }
+    if (p_.cpu_type != "atomic" && p_.cpu_type != "timing")
+        throw std::runtime_error("cpu_type: 'atomic' or 'timing', not '" + p_.cpu_type + "'");
+    const bool timing = p_.cpu_type == "timing";
     std::vector<int32_t> devs = p_.devices;
     if (devs.empty())
         for (uint32_t g = 0; g < p_.num_gpus; g++) devs.push_back((int32_t)(p_.first_device + g));
@@ -167,8 +170,14 @@ Campaign::Campaign(const CampaignParams &p) : p_(p) {
             check(e, fi_load_checkpoint(e, p_.checkpoint.c_str(), elf.data(), elf.size()), "fi_load_checkpoint");
         if (!exe.empty()) check(e, fi_set_exe_path(e, exe.c_str()), "fi_set_exe_path");
         if (input_file) check(e, fi_set_stdin(e, input.data(), input.size()), "fi_set_stdin");
+        check(e, fi_set_cpu_model(e, timing ? FI_CPU_TIMING : FI_CPU_ATOMIC, nullptr), "fi_set_cpu_model");
         fi_golden_info gi{};
         check(e, fi_golden_run(e, &gi), "fi_golden_run");
+        if (timing) {
+            fi_tick_info ti{};
+            check(e, fi_tick_golden(e, &ti), "fi_tick_golden");
+            if (ti.status[0]) throw std::runtime_error(std::string("cpu_type timing: ") + ti.status);
+        }
         check(e, fi_set_campaign(e, p_.seed, smask, p_.burst), "fi_set_campaign");
         check(e, fi_set_bits(e, bits_mask(p_.bits)), "fi_set_bits");
         check(e, fi_set_protect(e, p_.protect_mask), "fi_set_protect");
@@ -224,7 +233,9 @@ void Campaign::run() {
         th.emplace_back([&, g] {
             const uint64_t lo = T * g / G, hi = T * (g + 1) / G;
             memset(&h[g], 0, sizeof(fi_histogram));
-            fi_status s = fi_run_trials(engines_[g], p_.first_trial + lo, hi - lo, out_.data() + lo, &h[g]);
+            fi_status s = p_.cpu_type == "timing"
+                              ? fi_run_tick_trials(engines_[g], p_.first_trial + lo, hi - lo, out_.data() + lo, &h[g])
+                              : fi_run_trials(engines_[g], p_.first_trial + lo, hi - lo, out_.data() + lo, &h[g]);
             if (s != FI_OK) err[g] = fi_last_error(engines_[g]);
         });
     }

@@ -49,6 +49,8 @@ struct CampaignParams {
     double max_insts_factor = 2.0;        // hang cap = golden * f + 1000
     uint32_t private_pages = 16;
     std::string output;                   // prefix: <output>.outcomes.bin + <output>.json
+    std::string cpu_type = "atomic";      // "atomic": sites at a numInst; "timing": at a tick of a
+                                          // TimingSimpleCPU run on the reference board (fi_set_cpu_model)
 };
 
 // 'int_reg' (x1..x31), 'pc', 'mem', 'xN' or ABI register names -> bitmask

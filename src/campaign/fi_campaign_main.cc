@@ -57,6 +57,7 @@ int main(int argc, char **argv) {
         else if (k == "--shadow-fu-model") p.shadow_fu_model = strtoul(v.c_str(), nullptr, 0) != 0;
         else if (k == "--priority-to-shadow") p.priority_to_shadow = strtoul(v.c_str(), nullptr, 0) != 0;
         else if (k == "--issue-width") p.issue_width = (uint32_t)strtoul(v.c_str(), nullptr, 0);
+        else if (k == "--cpu-type") p.cpu_type = v;
         else if (k == "--load-latency") p.load_latency = (uint32_t)strtoul(v.c_str(), nullptr, 0);
         else if (k == "--num-gpus") p.num_gpus = (uint32_t)strtoul(v.c_str(), nullptr, 0);
         else if (k == "--device") p.first_device = (uint32_t)strtoul(v.c_str(), nullptr, 0);

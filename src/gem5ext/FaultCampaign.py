@@ -56,6 +56,10 @@ class FaultCampaign(SimObject):
         False, "shadows claim units before younger primaries (BaseO3CPU.priorityToShadow)")
     issue_width = Param.UInt32(8, "issue model: instructions issued per cycle (BaseO3CPU.issueWidth)")
     load_latency = Param.UInt32(2, "issue model: cycles from a load's issue to its value")
+    cpu_type = Param.String(
+        "atomic", "time coordinate of the fault sites: 'atomic' (a committed-instruction count, "
+        "AtomicSimpleCPU) or 'timing' (a tick of a TimingSimpleCPU run on the NoCache + "
+        "SingleChannelDDR3_1600 board of the SE run script)")
     num_gpus = Param.UInt32(1, "MI355X devices used by this process")
     first_gpu = Param.UInt32(0, "first HIP device ordinal")
     max_insts_factor = Param.Float(

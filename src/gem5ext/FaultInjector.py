@@ -9,6 +9,11 @@
 # mechanism of BaseCPU::scheduleInstStop, src/cpu/base.cc:764-770), which
 # AtomicSimpleCPU services at the top of the first tick with numInst >= inst
 # (src/cpu/simple/base.cc:321-325) -- the engine's injection point.
+# Tick mode (tick > 0; a TimingSimpleCPU on the reference SE board, the
+# engine's fi_run_tick_sites): the flip is an event on the main queue at that
+# tick with the lowest priority value, so it precedes every other event of the
+# tick -- the state it sees is the one after all events of earlier ticks,
+# which is what the engine's map to the instruction in flight assumes.
 from m5.params import *
 from m5.proxy import *
 from m5.SimObject import SimObject
@@ -24,3 +29,5 @@ class FaultInjector(SimObject):
     target = Param.UInt32("1..31 = x1..x31, 32 = pc, 33 = 8-byte memory word (fi_site.target)")
     mask = Param.UInt64("xor mask (fi_site.mask)")
     addr = Param.Addr(0, "memory sites: 8-byte aligned guest virtual address (fi_site.addr)")
+    tick = Param.UInt64(
+        0, "tick mode: the flip happens before every event of this tick (fi_tick_site.tick); 0 = at inst")

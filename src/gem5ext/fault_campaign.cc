@@ -33,6 +33,7 @@ FaultCampaign::init()
     cp.shadow_fu_model = params().shadow_fu_model;
     cp.priority_to_shadow = params().priority_to_shadow;
     cp.issue_width = params().issue_width;
+    cp.cpu_type = params().cpu_type;
     cp.load_latency = params().load_latency;
     cp.num_gpus = params().num_gpus;
     cp.first_device = params().first_gpu;

@@ -11,16 +11,25 @@
 namespace gem5 {
 
 FaultInjector::FaultInjector(const Params &p)
-    : SimObject(p), cpu(p.cpu), event([this] { inject(); }, name() + ".inject")
+    : SimObject(p), cpu(p.cpu), event([this] { inject(); }, name() + ".inject"),
+      tick_event([this] { inject(); }, name() + ".inject_tick", false, Event::Minimum_Pri)
 {
     if (p.target < 1 || p.target > 33)
         fatal("FaultInjector %s: target %u is not x1..x31, pc or memory", name(), p.target);
+    if (p.tick && p.target == 33)
+        fatal("FaultInjector %s: memory words have no tick mode", name());
 }
 
 void
 FaultInjector::startup()
 {
     SimObject::startup();
+    if (params().tick) {
+        // tick mode: before every other event of the tick (the flip lands in
+        // whatever the TimingSimpleCPU has in flight: its fetch or data access)
+        schedule(tick_event, params().tick);
+        return;
+    }
     // fires at the top of the first tick with numInst >= inst (the engine's
     // injection point; site.inst < golden numInst, so it is always reached)
     cpu->getContext(0)->scheduleInstCountEvent(&event, params().inst);

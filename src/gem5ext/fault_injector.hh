@@ -26,7 +26,8 @@ class FaultInjector : public SimObject
     void inject();
 
     BaseCPU *cpu;
-    EventFunctionWrapper event;
+    EventFunctionWrapper event;       // instruction-count mode
+    EventFunctionWrapper tick_event;  // tick mode: Minimum_Pri, ahead of every event of its tick
 };
 
 } // namespace gem5
