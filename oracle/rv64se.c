@@ -3918,6 +3918,13 @@ static void *tk_worker(void *arg) {
 int or_run_tick_trials(or_campaign_t *c, const or_tick_site_t *sites, u64 n, u64 f16, or_outcome_t *out,
                        or_outcome_t *truth, int nth) {
     if (!c->tk) { snprintf(c->err, sizeof c->err, "or_run_tick_trials: or_tick_setup first"); return -1; }
+    for (u64 i = 0; i < n; i++)   /* a site lies inside the golden run: [0, golden_ticks) */
+        if (sites[i].tick >= c->tk->golden_ticks) {
+            snprintf(c->err, sizeof c->err, "or_run_tick_trials: site %llu at tick %llu, the run ends at %llu",
+                     (unsigned long long)i, (unsigned long long)sites[i].tick,
+                     (unsigned long long)c->tk->golden_ticks);
+            return -1;
+        }
     u64 cap = hang_cap(c, f16);
     if (nth <= 1) {
         for (u64 i = 0; i < n; i++) tk_trial(c, &sites[i], cap, &out[i], truth ? &truth[i] : NULL);

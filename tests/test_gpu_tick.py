@@ -109,6 +109,7 @@ def _boundary_sites(o, rng, n):
     """Tick sites on the edges of attempts (first / last tick of each phase),
     every target kind, across the run."""
     ops, ticks = o.tick_trace()
+    end = int(ticks["exec"][-1])   # sites lie in [0, golden ticks)
     out = []
     for j in rng.integers(0, len(ops), n):
         T = ticks[j]
@@ -119,7 +120,7 @@ def _boundary_sites(o, rng, n):
         t = int(rng.choice(cand))
         tgt = int(rng.choice([32, 32, 34, int(rng.integers(1, 32))]))
         b = int(rng.integers(0, 64)) if tgt != 32 else int(rng.choice([1, 2, 3, 5, 12, 20, 40]))
-        out.append((max(t, 0), 1 << b, tgt, len(out)))
+        out.append((min(t, end - 1), 1 << b, tgt, len(out)))
     return np.array(out, dtype=[("tick", "<u8"), ("mask", "<u8"), ("target", "<u4"), ("trial", "<u4")])
 
 
@@ -133,7 +134,7 @@ def test_tick_boundary_sites_match_oracle(tick_pair, name):
     ref = o.run_tick_trials(ts, threads=16)
     _compare(dev, ref, ts)
     esc = (ref["cls"] == 5) & (ref["sub"] == 7)
-    assert esc.any() and (~esc).sum() > 0.8 * len(ts)
+    assert esc.any() and (~esc).sum() > 0.5 * len(ts)
 
 
 def test_tick_map_dispositions(tick_pair):
@@ -141,6 +142,14 @@ def test_tick_map_dispositions(tick_pair):
     their host outcomes are the oracle's."""
     e, o = tick_pair("crc32")
     ts = _boundary_sites(o, np.random.default_rng(9), 3000)
+    # flips of a load's destination while its data is outstanding: golden-equal
+    ops, ticks = o.tick_trace()
+    gops = o.golden_ops()
+    loads = np.nonzero((ops["kind"] == 0) & (ops["nfrag"] > 0) & (ops["cmd"] == 0))[0]
+    extra = [(int(ticks["done"][j]), 1 << 7, (int(gops["dst"][j]) & 0xFFFFFFFE).bit_length() - 1, 0)
+             for j in loads[::max(1, len(loads) // 200)] if bin(int(gops["dst"][j]) & 0xFFFFFFFE).count("1") == 1]
+    ts = np.concatenate([ts, np.array(extra, ts.dtype)])
+    ts["trial"] = np.arange(len(ts))
     sites, disp, ho = e.map_tick_sites(ts)
     ref = o.run_tick_trials(ts, threads=16)
     assert set(np.unique(disp).tolist()) <= {0, 1, 2}

@@ -233,3 +233,14 @@ def test_tick_setup_refuses_clock_readers(oracle_mod):
     with pytest.raises(RuntimeError, match="curTick"):
         o.tick_setup()
     o.close()
+
+
+def test_tick_sites_lie_inside_the_run(oracle_mod):
+    o = _tick_setup(oracle_mod, "hello")
+    T = oracle_mod.Oracle.tick_setup(o)
+    bad = np.array([(T, 1, 5, 0)], oracle_mod.TICK_SITE_DT)
+    with pytest.raises(RuntimeError, match="ends at"):
+        o.run_tick_trials(bad)
+    ok = o.run_tick_trials(np.array([(T - 1, 1, 5, 0)], oracle_mod.TICK_SITE_DT))
+    assert ok["cls"][0] == 0
+    o.close()
