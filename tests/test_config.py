@@ -25,7 +25,8 @@ def _load_config():
 
 
 ARGS = ["--workload", "w.elf", "--cmd", "w,x", "--input", "in.txt", "--executable", "/opt/w", "--trials", "7",
-        "--seed", "0x1234", "--structures", "int_reg,pc", "--protect-mask", "0x6", "--max-insts-factor", "3"]
+        "--seed", "0x1234", "--structures", "int_reg,pc", "--protect-mask", "0x6", "--max-insts-factor", "3",
+        "--cpu-type", "timing"]
 
 
 def test_arguments_reach_the_simobject(monkeypatch):
@@ -62,11 +63,11 @@ def test_arguments_reach_the_simobject(monkeypatch):
     assert seen["input"] == "in.txt" and seen["executable"] == "/opt/w"
     assert seen["workload"] == "w.elf" and seen["cmd"] == ["w", "x"] and seen["trials"] == 7
     assert seen["seed"] == 0x1234 and seen["structures"] == ["int_reg", "pc"] and seen["protect_mask"] == 6
-    assert seen["max_insts_factor"] == 3.0
-    # defaults: the host's stdin, the workload path
+    assert seen["max_insts_factor"] == 3.0 and seen["cpu_type"] == "timing"
+    # defaults: the host's stdin, the workload path, numInst sites
     seen.clear()
     cfg.run_gem5(cfg.parse(["--workload", "w.elf"]))
-    assert seen["input"] == "cin" and seen["executable"] == ""
+    assert seen["input"] == "cin" and seen["executable"] == "" and seen["cpu_type"] == "atomic"
 
 
 def test_arguments_reach_the_ctypes_mirror(monkeypatch):
@@ -90,9 +91,10 @@ def test_arguments_reach_the_ctypes_mirror(monkeypatch):
     cfg.run_ctypes(cfg.parse(ARGS))
     assert seen["input"] == "in.txt" and seen["executable"] == "/opt/w"
     assert seen["workload"] == "w.elf" and seen["cmd"] == ["w", "x"] and seen["trials"] == 7
+    assert seen["cpu_type"] == "timing"
     seen.clear()
     cfg.run_ctypes(cfg.parse(["--workload", "w.elf"]))
-    assert seen["input"] == "cin" and seen["executable"] is None
+    assert seen["input"] == "cin" and seen["executable"] is None and seen["cpu_type"] == "atomic"
 
 
 @pytest.mark.gpu

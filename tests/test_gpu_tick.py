@@ -186,3 +186,30 @@ def test_timing_refuses_clock_reader(tmp_path):
     with pytest.raises(EngineError, match="curTick"):
         FaultCampaign(str(path), cmd=["clk"], trials=10, cpu_type="timing")
     FaultCampaign(str(path), cmd=["clk"], trials=10, cpu_type="atomic").run()
+
+
+def test_native_cli_timing(tick_pair, tmp_path):
+    """fi_campaign --cpu-type timing (one engine and two on device 0): the
+    engine's tick campaign, outcome for outcome."""
+    import os
+    import subprocess
+    from conftest import ROOT
+    from shrewd_amd import HIST_DT, OUTCOME_DT
+    from shrewd_amd import build as b
+    exe = b.build_cli()
+    e, _ = tick_pair("crc32")
+    n = 4000
+    e.set_campaign(SEED, REGS | PC, 1)
+    e.set_bits(2**64 - 1)
+    ref, rh = e.run_tick_trials(0, n)
+    for devices in ("0", "0,0"):
+        prefix = str(tmp_path / f"t{devices.count(',')}")
+        r = subprocess.run([exe, "--workload", os.path.join(ROOT, "workloads", "crc32.elf"), "--cmd", "crc32",
+                            "--trials", str(n), "--seed", hex(SEED), "--structures", "int_reg,pc",
+                            "--cpu-type", "timing", "--devices", devices, "--output", prefix],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        out = np.fromfile(prefix + ".outcomes.bin", OUTCOME_DT)
+        hist = np.fromfile(prefix + ".hist.bin", HIST_DT)[0]
+        assert out.tobytes() == ref.tobytes()
+        assert hist["counts"].tobytes() == rh["counts"].tobytes()

@@ -18,6 +18,12 @@ abort and the message naming the site (sub-codes of fi_engine.h).  Compared
 fields: class, crash sub-code, exit code and committed instructions
 (fi_outcome.detail, the final pc, is not observable from outside gem5).
 Result faults (structure 34) have no gem5 hook and are skipped.
+
+Tick-domain sites (fi_tick_site records, from Engine.sample_tick_sites /
+run_tick_sites of an engine with cpu_type "timing"): each trial runs on
+TimingSimpleCPU with the fault at its tick (--cpu timing --tick); trials the
+engine reports as FI_ESC_TIMING are skipped, and --golden-ticks (the engine's
+fi_tick_info.golden_ticks) is compared with the fault-free run's final tick.
 """
 import argparse
 import json
@@ -32,7 +38,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from shrewd_amd.fi import OUTCOME_DT, SITE_DT  # noqa: E402
+from shrewd_amd.fi import OUTCOME_DT, SITE_DT, TICK_SITE_DT  # noqa: E402
 
 # gem5 message -> fi_engine.h crash sub-code (the sites named in fi_engine.h)
 CRASH_PATTERNS = [
@@ -54,7 +60,12 @@ def run_one(args, site, tag):
     d = tempfile.mkdtemp(prefix=f"fi_{tag}_")
     cmd = [args.gem5, "-d", d, os.path.join(ROOT, "configs", "fi_gem5_trial.py"), "--workload", args.workload,
            "--cmd", args.cmd, "--max-insts", str(args.max_insts), "--clock", args.clock]
-    if site is not None:
+    if args.tick_sites:
+        cmd += ["--cpu", "timing"]
+    if site is not None and args.tick_sites:
+        cmd += ["--tick", str(int(site["tick"])), "--target", str(int(site["target"])),
+                "--mask", hex(int(site["mask"]))]
+    elif site is not None:
         cmd += ["--inst", str(int(site["inst"])), "--target", str(int(site["target"])),
                 "--mask", hex(int(site["mask"])), "--addr", hex(int(site["addr"]))]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=args.timeout)
@@ -101,13 +112,18 @@ def main():
     ap.add_argument("--clock", default="2GHz")
     ap.add_argument("--timeout", type=float, default=3600)
     ap.add_argument("--max-insts", type=int, default=0, help="0: 2 x golden numInst + 1000 (engine default)")
+    ap.add_argument("--golden-ticks", type=int, default=0,
+                    help="tick sites: the engine's golden run length in ticks, checked against gem5's")
     args = ap.parse_args()
-    sites = np.load(args.sites).astype(SITE_DT)
+    raw = np.load(args.sites)
+    args.tick_sites = "tick" in (raw.dtype.names or ())
+    sites = raw.astype(TICK_SITE_DT if args.tick_sites else SITE_DT)
     eng = np.load(args.outcomes).astype(OUTCOME_DT)
     golden = run_one(args, None, "golden")
     if args.max_insts == 0:
         args.max_insts = 2 * golden["ninst"] + 1000
-    keep = [i for i in range(len(sites)) if sites[i]["target"] <= 33]
+    keep = [i for i in range(len(sites)) if sites[i]["target"] <= 33
+            and not (args.tick_sites and eng[i]["cls"] == 5 and eng[i]["sub"] == 7)]
     with ThreadPoolExecutor(args.jobs) as ex:
         recs = list(ex.map(lambda i: run_one(args, sites[i], str(i)), keep))
     bad = []
@@ -119,7 +135,12 @@ def main():
         if want != got or (rec["ninst"] >= 0 and rec["ninst"] != int(e["ninst"])):
             bad.append({"trial": int(sites[i]["trial"]), "engine": want, "gem5": got,
                         "engine_ninst": int(e["ninst"]), "gem5_ninst": rec["ninst"]})
-    print(json.dumps({"checked": len(keep), "mismatches": len(bad), "first": bad[:20]}))
+    res = {"checked": len(keep), "mismatches": len(bad), "first": bad[:20]}
+    if args.tick_sites and args.golden_ticks:
+        res["golden_ticks"] = {"engine": args.golden_ticks, "gem5": golden.get("tick", -1)}
+        if golden.get("tick", -1) != args.golden_ticks:
+            bad.append("golden_ticks")
+    print(json.dumps(res))
     return 1 if bad else 0
 
 
