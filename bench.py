@@ -58,6 +58,11 @@ def parse():
     ap.add_argument("--epochs", type=int, default=0, help="epochs per chunk (0: default)")
     ap.add_argument("--epoch-iters", type=int, default=0, help="first epoch's iterations per wave (0: default)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: the histogram reduce's backend (nccl = RCCL; gloo reduces a host copy -- tests)")
+    ap.add_argument("--device-index", type=int, default=-1,
+                    help="HIP device of this rank (default LOCAL_RANK; tests run two ranks on device 0)")
+    ap.add_argument("--hist-out", default="", help="rank 0: save the headline workload's node histogram (.npy)")
     return ap.parse_args()
 
 
@@ -171,12 +176,18 @@ def run_workload(a, name, T, steps, warmup, rank, world, dev, cpu_seconds, min_p
     torch.cuda.set_stream(tstream)
     stream = tstream.cuda_stream
 
+    gloo = world > 1 and dist.get_backend() == "gloo"
+
     def step():
         d_hist.zero_()
         eng.run_trials_device(rank * T, T, d_out.data_ptr(), d_hist.data_ptr(), stream)
         d_hist_node.copy_(d_hist)
-        if world > 1:
+        if world > 1 and not gloo:
             dist.all_reduce(d_hist_node)      # RCCL over xGMI: outcome histogram only
+        elif gloo:                            # (tests: a host copy through gloo)
+            h = d_hist_node.cpu()
+            dist.all_reduce(h)
+            d_hist_node.copy_(h)
 
     for _ in range(warmup):
         step()
@@ -194,10 +205,12 @@ def run_workload(a, name, T, steps, warmup, rank, world, dev, cpu_seconds, min_p
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=None if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     node_h = np.frombuffer(d_hist_node.cpu().numpy().tobytes(), HIST_DT)[0]
+    if rank == 0 and a.hist_out and name == a.workload:
+        np.save(a.hist_out, np.array([node_h], HIST_DT))
     if rank != 0:
         eng.close()
         return None
@@ -286,10 +299,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    if a.device_index >= 0:
+        local = a.device_index
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)

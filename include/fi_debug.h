@@ -58,6 +58,28 @@ fi_status fi_debug_jit_compile(const char *body, const char *arch, void *code, u
  * device needed; *len the code object's size, *cached 1 when it was loaded. */
 fi_status fi_debug_jit_build(const char *body, const char *arch, int part, int use_cache, uint64_t *len,
                              int *cached, char *err, uint64_t err_cap);
+
+/* A run-off loop as the translated solo body reports it (SoloTxIO lp_*,
+ * fi_translate.cpp): counter | compared register << 8 | (int8) step << 16,
+ * instructions per iteration, loads, per load {reg | kind << 8 | size << 12 |
+ * position << 16, offset, span}; the registers at the loop's first
+ * instruction and `left`, the instructions to the hang cap (64-bit). */
+typedef struct {
+    uint64_t regs[32];
+    uint64_t left;
+    uint32_t lp_cnt, lp_m, lp_n;
+    uint32_t lp_ld[4][3];
+    uint32_t pad;
+} fi_debug_loop;
+typedef struct {
+    int32_t verdict;      /* loop_outcome: 0 undecided, 1 hang, 2 page-fault crash after k instructions at fva */
+    uint32_t body_proof;  /* the body's own proof against left capped at 2^32 - 1 (tx_hang_proof) */
+    uint64_t k, fva;
+} fi_debug_loop_out;
+/* loop_outcome (fi_trial.hip) on device, for each record, against the
+ * process-start page set of the loaded workload (after fi_golden_run) --
+ * the function the solo kernel calls whenever the body claims a hang. */
+fi_status fi_debug_loop_outcome(fi_engine *e, const fi_debug_loop *in, uint64_t n, fi_debug_loop_out *out);
 #ifdef __cplusplus
 }
 #endif

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "fi_checkpoint.h"
+#include "fi_debug.h"
 #include "fi_tick.h"
 #include "fi_types.h"
 #include "rv64_isa.h"
@@ -43,6 +44,8 @@ hipError_t launch_predecode(const uint8_t *text, uint64_t code_off, uint64_t cod
 hipError_t launch_debug_decode(const uint32_t *raws, uint64_t n, PreInst *out, hipStream_t st);
 hipError_t launch_trials(const DevCtx &c, hipStream_t st);
 hipError_t launch_trials_solo(const DevCtx &c, hipStream_t st);
+hipError_t launch_debug_loop(const DevCtx &c, const fi_debug_loop *in, uint64_t n, fi_debug_loop_out *out,
+                             hipStream_t st);
 hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, fi_histogram *h,
                        const unsigned long long *stats, hipStream_t st);
 hipError_t launch_hist_stats(const unsigned long long *stats, fi_histogram *h, hipStream_t st);
@@ -2154,6 +2157,25 @@ fi_status fi_debug_decode(fi_engine *e, const uint32_t *raws, uint64_t n, void *
     HIPCHK(hipMemcpy(out16, d_o, n * sizeof(PreInst), hipMemcpyDeviceToHost));
     (void)hipFree(d_raw);
     (void)hipFree(d_o);
+    return FI_OK;
+}
+
+fi_status fi_debug_loop_outcome(fi_engine *e, const fi_debug_loop *in, uint64_t n, fi_debug_loop_out *out) {
+    if (!e || (n && (!in || !out))) return FI_E_ARG;
+    if (e->snaps.empty()) return fail(e, FI_E_STATE, "fi_debug_loop_outcome: fi_golden_run first");
+    if (!n) return FI_OK;
+    HIPCHK(hipSetDevice(e->dev));
+    fi_debug_loop *d_in = nullptr;
+    fi_debug_loop_out *d_out = nullptr;
+    HIPCHK(hipMalloc(&d_in, n * sizeof *in));
+    HIPCHK(hipMalloc(&d_out, n * sizeof *out));
+    HIPCHK(hipMemcpy(d_in, in, n * sizeof *in, hipMemcpyHostToDevice));
+    DevCtx c = base_ctx(e);
+    HIPCHK(launch_debug_loop(c, d_in, n, d_out, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    HIPCHK(hipMemcpy(out, d_out, n * sizeof *out, hipMemcpyDeviceToHost));
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
     return FI_OK;
 }
 

@@ -27,6 +27,9 @@
 #include "gem5_opclass_table.h"
 #include "fi_softfp.h"
 #include "fi_crypto.h"
+#ifndef __HIPCC_RTC__
+#include "fi_debug.h"   // (the static library's test hooks)
+#endif
 
 namespace fi {
 
@@ -1649,7 +1652,8 @@ S_out:
 }
 #endif
 
-#ifdef FI_TX
+// (loop proofs: unconditional, so the static library's test hook
+// fi_debug_loop_outcome runs the same code the translated kernels do)
 // A counted loop (fi_translate.cpp) whose counter x steps by c = +-1 and ends
 // it at zero passes its branch n more times, x + n c = 0 (mod 2^64; 2^64 for
 // x = 0), at least m instructions apart: it commits (n - 1) m of them before
@@ -1692,8 +1696,9 @@ __device__ __forceinline__ bool page_mapped(KCtx *c, const WaveMem &w, const Lan
 //   0: undecided (a page the fault handler would map, a table page outside
 //      the set, a counter load that could straddle a line, many pages, or
 //      the loop leaves before the cap): the trial runs on.
-__device__ __noinline__ int loop_outcome(KCtx *c, const WaveMem &w, const LaneMem &m, uint64_t slot, const lds_u64 *R,
-                                         const lds_io *io, uint64_t left, uint64_t &k, uint64_t &fva) {
+template <typename RegP, typename IoP>
+__device__ __noinline__ int loop_outcome(KCtx *c, const WaveMem &w, const LaneMem &m, uint64_t slot, RegP R, IoP io,
+                                         uint64_t left, uint64_t &k, uint64_t &fva) {
     const uint32_t cnt = io->lp_cnt, mm = io->lp_m, nl = io->lp_n;
     const uint32_t cr = cnt & 0xFF, tr = (cnt >> 8) & 0xFF;
     const int cs = (int)(int8_t)(uint8_t)(cnt >> 16);
@@ -1745,6 +1750,7 @@ __device__ __noinline__ int loop_outcome(KCtx *c, const WaveMem &w, const LaneMe
     return n - 1 >= (left + mm - 1) / mm ? 1 : 0;
 }
 
+#ifdef FI_TX
 // The clean solo body (fi_translate.cpp): for a trial that rewrote no code and
 // watches no register, blocks without those checks (a store into the code
 // range leaves before itself).  Same calling convention as solo_tx_run.
@@ -5413,6 +5419,42 @@ hipError_t launch_trials(const DevCtx &c, hipStream_t st) {
 // one trial per single-lane workgroup (surplus workgroups of a resume grid exit at once)
 hipError_t launch_trials_solo(const DevCtx &c, hipStream_t st) {
     hipLaunchKernelGGL(fi_trial_kernel_solo, dim3((unsigned)c.n), dim3(kSoloLanes), 0, st, c);
+    return hipGetLastError();
+}
+
+// Test hook (include/fi_debug.h fi_debug_loop_outcome): loop_outcome and the
+// body's capped proof on synthetic loop records, one per lane, against the
+// process-start page set (snapshot 0, no private pages, the start VMAs).
+__global__ void __launch_bounds__(64) fi_debug_loop_kernel(DevCtx, const fi_debug_loop *in, uint64_t n,
+                                                           fi_debug_loop_out *out) {
+    KCtx *const kx = (KCtx *)__builtin_amdgcn_kernarg_segment_ptr();
+    const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const fi_debug_loop *d = in + i;
+    const SnapState *S0 = kx->snaps;
+    WaveMem w;
+    w.tab = kx->snap_tab + S0->tab_off;
+    w.tab_n = S0->tab_n;
+    LaneMem m;
+    m.stack_min = S0->stack_min;
+    tlb_flush(m);
+    m.tp0 = m.tp1 = m.tp2 = m.tp3 = 0;
+    m.tnext = 0; m.n_priv = 0; m.req_vpn = kNone; m.req_src = nullptr; m.code_dirty = false;
+    m.dlo = m.dhi = 0; m.resv = m.lock = kNone; m.vm = false; m.vcfg = 0; m.nmiss = 0; m.dl = nullptr;
+    uint64_t k = 0, fva = 0;
+    const int r = loop_outcome(kx, w, m, 0, d->regs, d, d->left, k, fva);
+    // the body's proof (TXHANG in solo_tx_clean_run) against hleft capped as the kernel caps it
+    const uint32_t cnt = d->lp_cnt, cr = cnt & 0xFF, tr = (cnt >> 8) & 0xFF;
+    const uint32_t hl = d->left > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d->left;
+    const bool body = cr && d->lp_m && tx_hang_proof(d->regs[cr] - (tr ? d->regs[tr] : 0ULL),
+                                                     (int)(int8_t)(uint8_t)(cnt >> 16), d->lp_m, hl);
+    fi_debug_loop_out o;
+    o.verdict = r; o.body_proof = body ? 1u : 0u; o.k = k; o.fva = fva;
+    out[i] = o;
+}
+hipError_t launch_debug_loop(const DevCtx &c, const fi_debug_loop *in, uint64_t n, fi_debug_loop_out *out,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(fi_debug_loop_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, st, c, in, n, out);
     return hipGetLastError();
 }
 #endif

@@ -156,6 +156,10 @@ TIMING_OP_DT = np.dtype([("fetch", "<u8", (2,)), ("addr", "<u8", (2,)), ("size",
                          ("nfrag", "u1"), ("kind", "u1"), ("cmd", "u1"), ("pad", "u1", (8,))])
 TIMING_TICKS_DT = np.dtype([("fetch_send", "<u8", (2,)), ("fetch_done", "<u8", (2,)), ("exec", "<u8"),
                             ("done", "<u8")])
+# include/fi_debug.h fi_debug_loop / fi_debug_loop_out
+DEBUG_LOOP_DT = np.dtype([("regs", "<u8", (32,)), ("left", "<u8"), ("lp_cnt", "<u4"), ("lp_m", "<u4"), ("lp_n", "<u4"),
+                          ("lp_ld", "<u4", (4, 3)), ("pad", "<u4")])
+DEBUG_LOOP_OUT_DT = np.dtype([("verdict", "<i4"), ("body_proof", "<u4"), ("k", "<u8"), ("fva", "<u8")])
 TICK_SITE_DT = np.dtype([("tick", "<u8"), ("mask", "<u8"), ("target", "<u4"), ("trial", "<u4")])
 TOP_EXEC, TOP_FAULT, TOP_END = 0, 1, 2
 TCMD_READ, TCMD_WRITE, TCMD_SWAP, TCMD_LL, TCMD_SC = 0, 1, 2, 3, 4
@@ -286,6 +290,7 @@ def lib():
         L.fi_last_kernel_ms.restype = C.c_double
         L.fi_last_kernel_ms.argtypes = [vp]
         L.fi_debug_decode.argtypes = [vp, vp, C.c_uint64, vp]
+        L.fi_debug_loop_outcome.argtypes = [vp, vp, C.c_uint64, vp]
         L.fi_kernel_timer_reset.argtypes = [vp]
         L.fi_get_config.argtypes = [vp, C.POINTER(_Config)]
         L.fi_debug_stats.argtypes = [vp, vp]
@@ -594,6 +599,15 @@ class Engine:
                        ("len", "u1"), ("flags", "u1"), ("aux", "<u2")])
         out = np.zeros(len(raws), dt)
         self._chk(self.L.fi_debug_decode(self.h, raws.ctypes.data, len(raws), out.ctypes.data), "fi_debug_decode")
+        return out
+
+    def debug_loop_outcome(self, loops: np.ndarray) -> np.ndarray:
+        """fi_debug_loop_outcome: loop_outcome (and the body's capped proof)
+        on DEBUG_LOOP_DT records -> DEBUG_LOOP_OUT_DT."""
+        loops = np.ascontiguousarray(loops, DEBUG_LOOP_DT)
+        out = np.zeros(len(loops), DEBUG_LOOP_OUT_DT)
+        self._chk(self.L.fi_debug_loop_outcome(self.h, loops.ctypes.data, len(loops), out.ctypes.data),
+                  "fi_debug_loop_outcome")
         return out
 
 
