@@ -67,3 +67,8 @@ for i in order:
                       "start_us": round(float(start[i]), 1), "end_us": round(float(end[i]), 1),
                       "insts": int(ins[i]), "ninst0": int(n0[i]), "ns_per_inst": round(1e3 * float(end[i] - start[i]) / max(1, int(ins[i])), 1),
                       "tx_entries": int(w[i, 8]), "tx_insts": int(w[i, 2])}), flush=True)
+# every solo trial, for offline scheduling studies (SOLO_TL_DUMP=path.npz)
+if os.environ.get("SOLO_TL_DUMP"):
+    np.savez(os.environ["SOLO_TL_DUMP"], tid=tids, start_us=start, end_us=end, insts=ins, n0=n0,
+             cls=out["cls"][tids], ninst=out["ninst"][tids], target=sites["target"][tids], mask=sites["mask"][tids],
+             inst=sites["inst"][tids], golden_ninst=int(e.golden.ninst))
