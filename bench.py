@@ -226,6 +226,7 @@ def run_workload(a, name, T, steps, warmup, rank, world, dev, cpu_seconds, min_p
     # stream); the dominant kernel is the one with the most device time.
     st = eng.debug_stats()
     kinds, dms = eng.debug_dispatch_kinds(), eng.debug_dispatch_ms()
+    spans = eng.debug_dispatch_span_ms()
     tx = eng.translate_status() == ""
     names = (["fi_trial_kernel_tx", "fi_trial_kernel_tx_solo", "fi_trial_kernel_tx_solo_odd"] if tx
              else ["fi_trial_kernel", "fi_trial_kernel_solo", "fi_trial_kernel_solo_odd"])
@@ -235,6 +236,7 @@ def run_workload(a, name, T, steps, warmup, rank, world, dev, cpu_seconds, min_p
         ms_k = [m for m, kk in zip(dms, kinds) if kk == k]
         if not ms_k:
             continue
+        busy_k = [m for m, kk in zip(spans, kinds) if kk == k]
         disp = len(ms_k) / steps
         b = int(st[40 + 4 * k]) + int(st[41 + 4 * k]) + 4096 * int(st[42 + 4 * k]) + (T * (264 + 16) if k == 0 else 0)
         avg_ms = sum(ms_k) / len(ms_k)
@@ -245,7 +247,12 @@ def run_workload(a, name, T, steps, warmup, rank, world, dev, cpu_seconds, min_p
                              "ms_per_step": avg_ms * disp, "algorithmic_bytes_per_launch": per_launch,
                              "achieved": ach, "frac": ach / HBM_PEAK_GBS,
                              "device_insts_per_launch": int(st[43 + 4 * k]) / disp,
-                             "traffic": tk.get("hbm_bytes_per_launch"), "issue": tk.get("issue")}
+                             "traffic": tk.get("hbm_bytes_per_launch"), "issue": tk.get("issue"),
+                             # the dispatch's own work on the device (first to last stamp of
+                             # the waves that ran a trial): the HIP-event / trace time of the
+                             # solo-odd kernel also holds its wait for CU slots the solo
+                             # kernel on the other stream occupies
+                             "device_busy_ms": sum(busy_k) / len(busy_k) if busy_k else None}
     dom = max(per_kernel, key=lambda n: per_kernel[n]["ms_per_step"])
     D = per_kernel[dom]
     cls = node_h["counts"].sum(axis=(0, 1))

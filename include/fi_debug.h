@@ -29,6 +29,11 @@ fi_status fi_debug_waves(fi_engine *e, uint64_t *out, uint64_t n_waves);
 /* Device time of each interpreter dispatch since fi_kernel_timer_reset, in
  * launch order (epochs of each chunk); *n = dispatches (at most cap written). */
 fi_status fi_debug_dispatch_ms(fi_engine *e, float *ms, uint32_t cap, uint32_t *n);
+/* Device busy span of each of those dispatches (ms): from the first to the
+ * last s_memrealtime stamp of the waves that ran a trial -- the dispatch's own
+ * work, without the time its waves waited for CU slots held by the other
+ * stream's kernel (0: no trial ran).  Needs fi_kernel_timer_reset first. */
+fi_status fi_debug_dispatch_span_ms(fi_engine *e, float *ms, uint32_t cap, uint32_t *n);
 /* The kernel of each of those dispatches: 0 fi_trial_kernel_tx (64 lanes; the
  * static fi_trial_kernel without a load-time build), 1 the solo kernel, 2 the
  * solo-odd kernel (odd-pc survivors, on a second stream beside the solo one). */

@@ -44,6 +44,7 @@ hipError_t launch_predecode(const uint8_t *text, uint64_t code_off, uint64_t cod
 hipError_t launch_debug_decode(const uint32_t *raws, uint64_t n, PreInst *out, hipStream_t st);
 hipError_t launch_trials(const DevCtx &c, hipStream_t st);
 hipError_t launch_trials_solo(const DevCtx &c, hipStream_t st);
+hipError_t launch_span_init(unsigned long long *span, uint64_t n, hipStream_t st);
 hipError_t launch_debug_loop(const DevCtx &c, const fi_debug_loop *in, uint64_t n, fi_debug_loop_out *out,
                              hipStream_t st);
 hipError_t launch_hist(const fi_site *sites, const fi_outcome *out, uint64_t n, fi_histogram *h,
@@ -138,6 +139,7 @@ struct fi_engine {
     double last_ms = 0;
     // per-launch timing of the interpreter kernel (bench roofline)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> tpool;
+    unsigned long long *d_span = nullptr;   // per timer slot: [min wave start, max wave end] (kSpanSlots pairs)
     std::vector<uint32_t> tkind;
     size_t tused = 0;
 
@@ -485,6 +487,7 @@ void fi_destroy(fi_engine *e) {
     free_image(e);
     dfree(e->d_rnd); dfree(e->d_exe); dfree(e->d_stdin);
     for (auto &tp : e->tpool) { (void)hipEventDestroy(tp.first); (void)hipEventDestroy(tp.second); }
+    dfree(e->d_span);
     if (e->ev0) (void)hipEventDestroy(e->ev0);
     if (e->ev1) (void)hipEventDestroy(e->ev1);
     if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -1514,7 +1517,9 @@ static hipError_t launch_trial_kernel(fi_engine *e, DevCtx &c, hipStream_t st, b
 
 // The event pair of the next trial-kernel dispatch (kind: 0 the 64-lane
 // kernel, 1 solo, 2 solo-odd; fi_debug_dispatch_ms).
+static constexpr size_t kTimerSlots = 4096;   // dispatch timers kept between fi_kernel_timer_reset calls (a ring)
 static std::pair<hipEvent_t, hipEvent_t> &timer_slot(fi_engine *e, uint32_t kind) {
+    if (e->tused == kTimerSlots) e->tused = 0;
     if (e->tused == e->tpool.size()) {
         hipEvent_t a = nullptr, b = nullptr;
         (void)hipEventCreate(&a);
@@ -1625,6 +1630,7 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
                 HIPCHK(hipEventRecord(e->ev_fork, st));
                 HIPCHK(hipStreamWaitEvent(e->stream_odd, e->ev_fork, 0));
                 auto &tq = timer_slot(e, 2);
+                co.span = e->d_span ? e->d_span + 2 * (e->tused - 1) : nullptr;
                 HIPCHK(hipEventRecord(tq.first, e->stream_odd));
                 void *args[] = {&co};
                 HIPCHK(hipModuleLaunchKernel(e->tx_fn_odd, grid, 1, 1, kSoloLanes, 1, 1, 0, e->stream_odd, args, nullptr));
@@ -1644,6 +1650,7 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
         // every dispatch of the trial kernel is bracketed by its own event
         // pair on the launch stream (the bench's per-dispatch kernel time)
         auto &tp = timer_slot(e, solo ? 1 : 0);
+        c.span = e->d_span ? e->d_span + 2 * (e->tused - 1) : nullptr;
         HIPCHK(hipEventRecord(tp.first, st));
         if (solo) { c.lanes = 1; c.resume_waves = 0; c.wrange = nullptr; c.n_waves = nullptr; }
         HIPCHK(launch_trial_kernel(e, c, st, solo));
@@ -2109,6 +2116,13 @@ fi_status fi_get_config(fi_engine *e, fi_config *out) {
 fi_status fi_kernel_timer_reset(fi_engine *e) {
     if (!e) return FI_E_ARG;
     e->tused = 0;
+    if (!e->d_span) {
+        HIPCHK(hipSetDevice(e->dev));
+        HIPCHK(hipMalloc(&e->d_span, kTimerSlots * 2 * sizeof(unsigned long long)));
+    }
+    // every slot's min starts at ~0, its max at 0 (layout: slot i at [2i, 2i + 1])
+    HIPCHK(hipMemsetAsync(e->d_span, 0, kTimerSlots * 2 * sizeof(unsigned long long), e->stream));
+    HIPCHK(launch_span_init(e->d_span, kTimerSlots, e->stream));
     return FI_OK;
 }
 
@@ -2137,6 +2151,21 @@ fi_status fi_debug_dispatch_ms(fi_engine *e, float *ms, uint32_t cap, uint32_t *
     return FI_OK;
 }
 
+fi_status fi_debug_dispatch_span_ms(fi_engine *e, float *ms, uint32_t cap, uint32_t *n) {
+    if (!e || (!ms && cap)) return FI_E_ARG;
+    const size_t k = std::min<size_t>(e->tused, cap);
+    if (k) {
+        if (!e->d_span) return fail(e, FI_E_STATE, "fi_debug_dispatch_span_ms: fi_kernel_timer_reset first");
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipStreamSynchronize(e->stream_odd));
+        std::vector<unsigned long long> h(2 * k);
+        HIPCHK(hipMemcpy(h.data(), e->d_span, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < k; i++)   // (s_memrealtime runs at 100 MHz; no trial ran: 0)
+            ms[i] = h[2 * i + 1] > h[2 * i] ? (float)((h[2 * i + 1] - h[2 * i]) * 1e-5) : 0.0f;
+    }
+    if (n) *n = (uint32_t)e->tused;
+    return FI_OK;
+}
 fi_status fi_debug_dispatch_kinds(fi_engine *e, uint32_t *kinds, uint32_t cap, uint32_t *n) {
     if (!e || (!kinds && cap)) return FI_E_ARG;
     for (size_t i = 0; i < e->tused && i < cap; i++) kinds[i] = e->tkind[i];

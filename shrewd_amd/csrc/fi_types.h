@@ -186,6 +186,8 @@ struct DevCtx {
     const uint32_t *resume;          // NULL = fresh launch: lane slot = global lane index
     const uint32_t *resume_n;        // number of entries in resume[]
     const uint32_t *resume_lo;       // solo-odd launch: its entries are resume[*resume_lo .. *resume_n) (else NULL)
+    unsigned long long *span;        // this dispatch's [min wave start, max wave end] (s_memrealtime, 100 MHz)
+                                     // over the waves that ran a trial; NULL = not recorded
     const uint32_t *wrange;          // packed resume (FI_CFG_PACK_RUNS): wave b runs resume[wrange[2b] .. wrange[2b+1])
     const uint32_t *n_waves;         //   number of valid wrange pairs (waves b >= it exit at once)
     uint32_t *surv;                  // suspended lanes' slots are appended here

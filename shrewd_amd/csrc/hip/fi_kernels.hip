@@ -166,6 +166,11 @@ __global__ void fi_predecode_kernel(const uint8_t *text, uint64_t code_off, uint
     pre[h] = p;
 }
 
+// dispatch busy spans (DevCtx::span): every slot's min at ~0 (its max is zeroed by a memset)
+__global__ void fi_span_init_kernel(unsigned long long *span, uint64_t n) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) span[2 * i] = ~0ULL;
+}
 __global__ void fi_debug_decode_kernel(const uint32_t *raws, uint64_t n, PreInst *out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -352,6 +357,10 @@ hipError_t launch_predecode(const uint8_t *text, uint64_t code_off, uint64_t cod
                            hipStream_t st) {
     hipLaunchKernelGGL(fi_predecode_kernel, dim3(nblk(nhalf, 256)), dim3(256), 0, st, text, code_off, code_end, nhalf,
                        pre);
+    return hipGetLastError();
+}
+hipError_t launch_span_init(unsigned long long *span, uint64_t n, hipStream_t st) {
+    hipLaunchKernelGGL(fi_span_init_kernel, dim3(nblk(n, 256)), dim3(256), 0, st, span, n);
     return hipGetLastError();
 }
 hipError_t launch_debug_decode(const uint32_t *raws, uint64_t n, PreInst *out, hipStream_t st) {

@@ -5341,6 +5341,12 @@ __device__ __forceinline__ void trial_body() {
         wd[8] = n_txin;                                  // translated-code entries
         wd[9] = m.nmiss;                                 // lane 0's full page-table lookups
     }
+    // the dispatch's busy span: waves that ran a trial (a surplus wave of a
+    // resume grid returned above; one lane's vector atomics)
+    if (CX->span && wballot<kNL>(live) != 0 && lane == 0) {
+        atomicMin(&CX->span[0], (unsigned long long)rt_start);
+        atomicMax(&CX->span[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
     if (blockIdx.x == 0 && lane == 0) {
         CX->stats[20] = __builtin_amdgcn_s_memtime() - t_start;
         CX->stats[21] = __builtin_amdgcn_s_memrealtime() - rt_start;

@@ -301,6 +301,7 @@ def lib():
         L.fi_debug_epochs.argtypes = [vp, vp]
         L.fi_debug_dispatch_ms.argtypes = [vp, vp, C.c_uint32, C.POINTER(C.c_uint32)]
         L.fi_debug_dispatch_kinds.argtypes = [vp, vp, C.c_uint32, C.POINTER(C.c_uint32)]
+        L.fi_debug_dispatch_span_ms.argtypes = [vp, vp, C.c_uint32, C.POINTER(C.c_uint32)]
         L.fi_debug_golden_trace.argtypes = [vp, vp, C.c_uint64, C.POINTER(C.c_uint64), vp, C.c_uint64,
                                             C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.fi_debug_translate.argtypes = [vp, C.c_uint64, C.c_uint64, vp, C.c_uint64, C.c_char_p, C.c_uint64,
@@ -546,6 +547,15 @@ class Engine:
         ms = np.zeros(256, np.float32)
         n = C.c_uint32()
         self._chk(self.L.fi_debug_dispatch_ms(self.h, ms.ctypes.data, 256, C.byref(n)), "fi_debug_dispatch_ms")
+        return [round(float(x), 3) for x in ms[:min(n.value, 256)]]
+
+    def debug_dispatch_span_ms(self) -> list:
+        """Device busy span of each dispatch since kernel_timer_reset (ms):
+        first to last stamp of the waves that ran a trial."""
+        ms = np.zeros(256, np.float32)
+        n = C.c_uint32()
+        self._chk(self.L.fi_debug_dispatch_span_ms(self.h, ms.ctypes.data, 256, C.byref(n)),
+                  "fi_debug_dispatch_span_ms")
         return [round(float(x), 3) for x in ms[:min(n.value, 256)]]
 
     def debug_dispatch_kinds(self) -> list:
