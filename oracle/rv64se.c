@@ -226,6 +226,7 @@ struct or_campaign {
     /* golden */
     int have_golden;
     or_golden_t golden;
+    int gsub;                        /* the golden run's end sub-code (OR_END_*) */
     bytes_t gout, gerr;
     char err[256];
 };
@@ -1545,7 +1546,8 @@ static void do_syscall(mach_t *m) {
         }
         int code = status & 0xff;
         const or_campaign_t *c = m->c;
-        int same = c->have_golden && code == (int)c->golden.exit_code &&
+        /* masked: the golden output and exit code, ended the way the golden run ended */
+        int same = c->have_golden && code == (int)c->golden.exit_code && c->gsub == OR_END_EXIT &&
                    m->out.len == c->gout.len && m->err.len == c->gerr.len &&
                    (m->out.len == 0 || !memcmp(m->out.buf, c->gout.buf, m->out.len)) &&
                    (m->err.len == 0 || !memcmp(m->err.buf, c->gerr.buf, m->err.len));
@@ -2857,6 +2859,7 @@ static void tick(mach_t *m, u64 cap) {
         } else {
             const or_campaign_t *c = m->c;
             int same = c->have_golden && m->m5code == (int)c->golden.exit_code &&
+                       c->gsub == (m->m5x == 1 ? OR_END_M5_EXIT : OR_END_M5_FAIL) &&
                        m->out.len == c->gout.len && m->err.len == c->gerr.len &&
                        (m->out.len == 0 || !memcmp(m->out.buf, c->gout.buf, m->out.len)) &&
                        (m->err.len == 0 || !memcmp(m->err.buf, c->gerr.buf, m->err.len));
@@ -3067,6 +3070,7 @@ int or_golden(or_campaign_t *c, u64 max_inst, or_golden_t *out) {
     }
     c->golden.ninst = m.num_inst; c->golden.ncycles = m.num_cycles;
     c->golden.exit_code = m.res.exit_code; c->golden.cls = 0;
+    c->gsub = m.res.sub;   /* how it ended: exit, m5_exit or m5_fail */
     c->golden.stdout_len = m.out.len; c->golden.stderr_len = m.err.len;
     c->golden.fetch_bytes = m.fetch_bytes; c->golden.data_bytes = m.data_bytes;
     free(c->gout.buf); free(c->gerr.buf);

@@ -187,7 +187,9 @@ struct fi_engine {
     // load-time build of the trial kernel with the translated golden blocks
     hipModule_t tx_mod[3] = {nullptr, nullptr, nullptr};
     std::shared_ptr<JitJob> jit;     // the build in flight (nullptr: none)
-    std::vector<std::thread> jit_threads;   // every build this engine started: joined by fi_destroy
+    // builds this engine started: a finished one is joined when a build is
+    // installed (jit_install), one still running by fi_destroy
+    std::vector<std::pair<std::thread, std::shared_ptr<JitJob>>> jit_threads;
     std::vector<PreInst> jit_pre;    // golden pre-decoded text with the leader flags, uploaded when it lands
     uint64_t jit_blocks = 0, jit_insts = 0;
     hipFunction_t tx_fn = nullptr, tx_fn_solo = nullptr;
@@ -333,6 +335,9 @@ static fi_status upload_rnd(fi_engine *e) {
     return FI_OK;
 }
 
+// private pages per slot of the second pass (and so the overflow blocks): 16 P, at least 256
+static uint64_t redo_pages(uint64_t P) { return std::max<uint64_t>(P * 16ull, 256); }
+
 fi_status fi_create(const fi_config *cfg, fi_engine **out) {
     if (!out) { g_create_err = "fi_create: out is NULL"; return FI_E_ARG; }
     *out = nullptr;
@@ -378,9 +383,15 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
     if (e->cfg.max_trials_per_launch == 0) {
         // auto: a campaign's trials in as few launches as half the free HBM
         // holds (each launch ends in its own serial tail of long trials), at
-        // ~(4 KiB + 8 B) per private page + ~2.5 KiB of per-trial state
+        // (4 KiB + 8 B) per private page, the per-slot buffers of ensure_work
+        // (both site / outcome buffers of the chunks in flight, the redo
+        // lists, the rewritten-code map) and the overflow pool's share
+        // (one block of P' - P pages per 2048 slots)
         size_t free_b = 0, total_b = 0;
-        const uint64_t per = (uint64_t)e->cfg.private_pages * (kPage + 8) + 2560 + kDmapWords * 4;
+        const uint64_t P = e->cfg.private_pages, P2 = redo_pages(P);
+        const uint64_t slot_b = 3 * sizeof(fi_site) + 3 * sizeof(fi_outcome) + 8 * 8 + 8 * 4 + 10 * 8 +
+                                sizeof(LaneSave) + sizeof(VmState) + 33 * 8 + kDmapWords * 4 + 4 + 64;
+        const uint64_t per = P * (kPage + 8) + slot_b + (P2 > P ? (P2 - P) * (kPage + 8) / 2048 + 1 : 0);
         uint64_t cap = 65536;
         if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = (uint64_t)free_b / 2 / per;
         e->cfg.max_trials_per_launch = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(cap, 65536), 1u << 21);
@@ -434,6 +445,21 @@ static void jit_install(fi_engine *e, hipStream_t st, bool wait) {
         if (!j->done) return;
     }
     e->jit.reset();
+    // join the builds that have finished (this one, and any an earlier golden
+    // run left behind): a long-lived engine keeps no finished threads
+    for (size_t i = 0; i < e->jit_threads.size();) {
+        bool fin;
+        {
+            std::lock_guard<std::mutex> lk(e->jit_threads[i].second->mu);
+            fin = e->jit_threads[i].second->done;
+        }
+        if (fin) {
+            if (e->jit_threads[i].first.joinable()) e->jit_threads[i].first.join();
+            e->jit_threads.erase(e->jit_threads.begin() + (long)i);
+        } else {
+            i++;
+        }
+    }
     if (!j->err.empty()) {
         e->tx_status = j->err;
         return;
@@ -481,7 +507,7 @@ void fi_destroy(fi_engine *e) {
     // is left behind -- exiting under a running build races the static
     // destructors of the JIT cache and of hipRTC
     for (auto &t : e->jit_threads)
-        if (t.joinable()) t.join();
+        if (t.first.joinable()) t.first.join();
     (void)hipSetDevice(e->dev);
     free_work(e);
     free_image(e);
@@ -823,7 +849,6 @@ fi_status fi_load_checkpoint(fi_engine *e, const char *cpt_dir, const uint8_t *e
 
 // Private pages per trial of the second pass (chunk_end) and, with the
 // overflow pool, a trial's capacity in the first: 16 P, at least 256.
-static uint64_t redo_pages(uint64_t P) { return std::max<uint64_t>(P * 16ull, 256); }
 
 static fi_status ensure_work(fi_engine *e, uint64_t n) {
     if (n <= e->cap) return FI_OK;
@@ -867,10 +892,10 @@ static fi_status ensure_work(fi_engine *e, uint64_t n) {
     if (!e->h_redo_cnt) HIPCHK(hipHostMalloc(&e->h_redo_cnt, 16));
     for (auto &ev : e->ev_cnt)
         if (!ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    for (int i = 0; i < 2; i++) {
-        HIPCHK(hipHostMalloc(&e->h_stage[i], c * sizeof(fi_outcome)));
+    // (the pinned staging of host-bound outcomes is made on first use:
+    // chunk_end; device-resident runs never need it)
+    for (int i = 0; i < 2; i++)
         if (!e->ev_stage[i]) HIPCHK(hipEventCreateWithFlags(&e->ev_stage[i], hipEventDisableTiming));
-    }
     // overflow pool: a trial past P pages takes a block of P' - P more (P' the
     // redo pass's page count), one block per 2048 slots (at least 64)
     {
@@ -1343,7 +1368,7 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
             e->jit_insts = n_tx;
             e->jit = j;
             e->tx_status = "compiling";
-            e->jit_threads.emplace_back(jit_job_run, j);
+            e->jit_threads.emplace_back(std::thread(jit_job_run, j), j);
         }
     }
     e->last_ms = golden_ms;
@@ -1712,6 +1737,7 @@ static fi_status chunk_end(fi_engine *e, const Chunk &ch, fi_histogram *d_hist, 
     }
     HIPCHK(launch_hist(ch.sites, ch.out, ch.k, d_hist, nullptr, st));
     if (ch.host_out) {
+        if (!e->h_stage[ch.slot]) HIPCHK(hipHostMalloc(&e->h_stage[ch.slot], e->cap * sizeof(fi_outcome)));
         HIPCHK(hipMemcpyAsync(e->h_stage[ch.slot], ch.out, ch.k * sizeof(fi_outcome), hipMemcpyDeviceToHost, st));
         HIPCHK(hipEventRecord(e->ev_stage[ch.slot], st));
     }

@@ -974,7 +974,10 @@ __device__ __noinline__ bool do_syscall(KCtx *c, WaveMem w, Lane &L, LaneMem &m,
             finish(L, FI_MASKED, 0, code, pc32);
             return false;
         }
-        const bool same = !L.out_bad && L.out_pos == c->gout_len && L.err_pos == c->gerr_len && code == (int)c->gexit;
+        // masked: the golden run's output and exit code, ended the way it ended
+        // (an exit syscall, not m5_exit / m5_fail: INTEGRATION.md, outcome classes)
+        const bool same = !L.out_bad && L.out_pos == c->gout_len && L.err_pos == c->gerr_len && code == (int)c->gexit &&
+                          c->gsub == FI_END_EXIT;
         finish(L, same ? FI_MASKED : FI_SDC, 0, code, pc32);
         return false;
     }
@@ -3888,6 +3891,9 @@ __device__ __forceinline__ void trial_body() {
             // (a lane past its P pages takes its overflow block first: priv_room)
             const bool room = !L.done && m.req_vpn != kNone && priv_room(CX, slot, m.n_priv);
             uint64_t wl = wballot<kNL>(room);
+            // (priv_room may have handed a lane its overflow block, ov_of[slot] in
+            // global memory, which the other lanes read back in priv_frame below)
+            if (wl) __threadfence_block();
             while (wl) {
                 const int l = __ffsll((unsigned long long)wl) - 1;
                 wl &= wl - 1;
@@ -5219,7 +5225,7 @@ __device__ __forceinline__ void trial_body() {
                     finish(L, FI_MASKED, m5x == 1 ? FI_END_M5_EXIT : FI_END_M5_FAIL, (int)m5code, (uint32_t)L.pc);
                 } else {
                     const bool same = !L.out_bad && L.out_pos == CX->gout_len && L.err_pos == CX->gerr_len &&
-                                      m5code == CX->gexit;
+                                      m5code == CX->gexit && CX->gsub == (m5x == 1 ? FI_END_M5_EXIT : FI_END_M5_FAIL);
                     finish(L, same ? FI_MASKED : FI_SDC, m5x == 1 ? FI_END_M5_EXIT : FI_END_M5_FAIL, (int)m5code,
                            (uint32_t)L.pc);
                 }

@@ -732,6 +732,27 @@ def test_m5_simulator_control_ops(oracle_mod, flags):
     e.close()
 
 
+@pytest.mark.parametrize("golden_m5", [False, True])
+@pytest.mark.parametrize("flags", [0, 128 | 4 | 1 | 2])
+def test_end_kind_decides_masked(oracle_mod, golden_m5, flags):
+    """Same output and exit code by another end (exit syscall vs m5_exit,
+    test_isa_vectors.endkind_program_source): SDC with the trial's own end
+    sub-code, on the device as in the oracle."""
+    from shrewd_amd import Engine
+    import test_isa_vectors as kat
+    elf = kat.endkind_program_elf(golden_m5)
+    e = Engine(private_pages=64, flags=flags)
+    e.load_elf(elf, ["endkind"])
+    e.golden_run()
+    o = oracle_mod.Oracle(elf, "endkind")
+    o.run_golden()
+    sites = kat.endkind_sites()
+    dev, _ = e.run_sites(sites)
+    compare(dev, o.run_trials(sites, protect_mask=0), sites)
+    assert (dev["cls"] == 1).any() and (dev["cls"] == 0).any()
+    e.close()
+
+
 def test_clock_read_blocks_tick_blind_early_exit(oracle_mod):
     """Exact early exit when the golden suffix reads curTick: the clk program's
     branch-register faults take an arm with 16 extra non-counting ticks

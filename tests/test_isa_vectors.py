@@ -1994,6 +1994,53 @@ def test_m5end_program_on_oracle(oracle_mod):
     assert last == [(5, 1, 0), (1, 2, 5), (0, 2, 7)], last
 
 
+# ---------------------------------------------------------------- endkind programs
+# The same output and exit code, reached by another end: the golden run ends
+# with exit(0) (endkind_exit) or m5_exit(0) (endkind_m5); a dead branch on t0
+# ends the other way after the same output.  A trial is masked only if it
+# ends the way the golden run did (an exit syscall's "exiting with last
+# active thread context" vs "m5_exit instruction encountered",
+# syscall_emul.cc:120-248, sim/pseudo_inst.cc:178): otherwise SDC, with the
+# trial's own end sub-code.  (No reference fixture decides this: parity
+# unpinned.)
+def endkind_program_source(golden_m5: bool) -> str:
+    m5_end = ["    li    a0, 0", _m5(0x21)]
+    exit_end = ["    li    a0, 0", "    li    a7, 93", "    ecall"]
+    L = ["    .text", "_start:", "    li    a0, 1", "    la    a1, msg", "    li    a2, 3", "    li    a7, 64", "    ecall",
+         "    li    t0, 0", "    bnez  t0, other"]
+    L += m5_end if golden_m5 else exit_end
+    L += ["other:"] + (exit_end if golden_m5 else m5_end)
+    L += ["    .data", "msg:", "    .ascii \"hi\\n\""]
+    return "\n".join(L) + "\n"
+
+
+def endkind_program_elf(golden_m5: bool) -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(endkind_program_source(golden_m5), compress=False)
+
+
+def endkind_sites():
+    import numpy as np
+    from shrewd_amd.fi import SITE_DT
+    L = [(i, 1 << b, 0, 5, 0) for i in range(8) for b in (0, 7, 40)]
+    s = np.array(L, dtype=SITE_DT)
+    s["trial"] = np.arange(len(s))
+    return s
+
+
+@pytest.mark.parametrize("golden_m5", [False, True])
+def test_endkind_program_on_oracle(oracle_mod, golden_m5):
+    o = oracle_mod.Oracle(endkind_program_elf(golden_m5), "endkind")
+    g = o.run_golden()
+    assert g.exit_code == 0 and o.golden_stdout() == b"hi\n"
+    r = o.run_trials(endkind_sites(), protect_mask=0)
+    got = {(int(c), int(s), int(x)) for c, s, x in zip(r["cls"], r["sub"], r["exit_code"])}
+    gsub, osub = (1, 0) if golden_m5 else (0, 1)
+    assert (0, gsub, 0) in got           # masked: t0 flipped after its last use, the golden end
+    assert (1, osub, 0) in got           # the other end, same output and code: SDC
+    assert got <= {(0, gsub, 0), (1, osub, 0)}, got
+
+
 # ---------------------------------------------------------------- sys2 program
 # read (63), readlinkat (78) and riscv_hwprobe (258) (oracle/rv64se.c:
 # sys_readlinkat / sys_hwprobe; se_workload.cc:221-527, syscall_emul.hh:
