@@ -212,6 +212,12 @@ typedef struct {
  * the fallback when the pool is spent) (A/B and parity checks; outcomes are
  * identical) */
 #define FI_CFG_NO_OVERFLOW 32768u
+/* The solo epoch starts its trials longest-first by the work left: the golden
+ * run's remaining length, or -- for a trial inside a counted loop of the
+ * golden text -- the loop's remaining passes times its length, if larger (a
+ * flipped bound or pointer).  This flag drops the loop term (A/B; the order
+ * never changes an outcome). */
+#define FI_CFG_NO_LOOP_ORDER 65536u
 
 typedef struct {
     uint64_t ninst, ncycles;

@@ -61,12 +61,13 @@ hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome
                                hipStream_t st);
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
                             uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, uint32_t solo,
-                            uint64_t golden_ninst, uint32_t nb, hipStream_t st);
+                            uint64_t golden_ninst, uint32_t nb, const LoopEst *loops, uint32_t n_loops,
+                            uint64_t hang_cap, hipStream_t st);
 hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,
                             hipStream_t st);
 std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, const std::vector<uint32_t> &trace,
                              const std::vector<uint64_t> &extra_pcs, std::vector<uint32_t> &leaders_out,
-                             uint32_t &n_insts, bool odd_streams);
+                             uint32_t &n_insts, bool odd_streams, std::vector<LoopEst> *loops_out = nullptr);
 std::vector<fi_issue_op> issue_ops_from_trace(const std::vector<PreInst> &pre, const std::vector<uint32_t> &trace);
 std::string jit_compile(const std::string &body, const char *arch, std::vector<char> &code, bool &cached, int part,
                         bool use_cache);
@@ -272,6 +273,8 @@ struct fi_engine {
     uint32_t *d_svals = nullptr, *d_svals2 = nullptr;
     uint32_t *d_wrange = nullptr, *d_nwaves = nullptr;   // packed resume (FI_CFG_PACK_RUNS)
     uint32_t *d_split = nullptr;   // per epoch: odd-pc survivors, then the solo kernel's share of the list
+    LoopEst *d_loops = nullptr;    // counted loops of the golden text (the solo order's work-left estimate)
+    uint32_t n_loops = 0;
     uint32_t *d_dmap = nullptr;    // per slot: rewritten-code map (DevCtx::dmap, kDmapWords words)
     // second pass of the trials that ran out of private pages (chunk_end)
     uint32_t *d_redo_idx = nullptr, *d_redo_cnt = nullptr, *h_redo_cnt = nullptr;   // two of each: a chunk and its predecessor
@@ -349,6 +352,8 @@ fi_status fi_create(const fi_config *cfg, fi_engine **out) {
     if (getenv("SHREWD_FI_TRACE")) signal(SIGSEGV, segv_trace);
     fi_engine *e = new fi_engine();
     if (cfg) e->cfg = *cfg;
+    // diagnostics (A/B runs of an unchanged caller): FI_CFG_* bits to add
+    if (const char *x = getenv("SHREWD_FI_EXTRA_FLAGS")) e->cfg.flags |= (uint32_t)strtoul(x, nullptr, 0);
     if (e->cfg.private_pages == 0) e->cfg.private_pages = 16;
     if (e->cfg.hang_factor_x16 == 0) e->cfg.hang_factor_x16 = 32;
     if (e->cfg.lanes_per_wave == 0) e->cfg.lanes_per_wave = kDefaultLanes;
@@ -421,8 +426,9 @@ static void free_mem_index(fi_engine *e) {
     e->mem_live = false;
 }
 static void free_fw(fi_engine *e) {
-    dfree(e->d_fw_off); dfree(e->d_fw_ev);
+    dfree(e->d_fw_off); dfree(e->d_fw_ev); dfree(e->d_loops);
     e->fw_ok = false;
+    e->n_loops = 0;
 }
 static void free_tx(fi_engine *e) {
     for (auto &m : e->tx_mod) {
@@ -1340,11 +1346,18 @@ fi_status fi_golden_run(fi_engine *e, fi_golden_info *out) {
         // mid-block steps to the next leader in the interpreter)
         const std::vector<uint64_t> pcs;
         std::vector<uint32_t> leaders;
+        std::vector<LoopEst> loops;
         uint32_t n_tx = 0;
-        std::string body = translate_blocks(pre, e->text_lo, trace, pcs, leaders, n_tx, true);
+        std::string body = translate_blocks(pre, e->text_lo, trace, pcs, leaders, n_tx, true, &loops);
         if (n_tx > 24000) {   // the odd-pc streams make it too large: without them
             leaders.clear();
-            body = translate_blocks(pre, e->text_lo, trace, pcs, leaders, n_tx, false);
+            loops.clear();
+            body = translate_blocks(pre, e->text_lo, trace, pcs, leaders, n_tx, false, &loops);
+        }
+        if (!loops.empty() && !(e->cfg.flags & FI_CFG_NO_LOOP_ORDER)) {
+            HIPCHK(hipMalloc(&e->d_loops, loops.size() * sizeof(LoopEst)));
+            HIPCHK(hipMemcpy(e->d_loops, loops.data(), loops.size() * sizeof(LoopEst), hipMemcpyHostToDevice));
+            e->n_loops = (uint32_t)loops.size();
         }
         e->tx_body = body;
         hipDeviceProp_t prop;
@@ -1640,7 +1653,8 @@ static fi_status run_pass(fi_engine *e, fi_site *sites, uint64_t k, fi_outcome *
             // key of nb + 2 bits (+ 1 for the odd-pc flag) sorts in fewer passes
             const uint32_t nb = 64u - (uint32_t)__builtin_clzll(std::max<uint64_t>(c.hang_cap, 1));
             HIPCHK(launch_surv_keys(e->d_save, e->d_surv[(ep - 1) & 1], e->d_cnt + ep - 1, k, c.text_lo, e->d_skeys,
-                                    e->d_svals, odd ? e->d_split + 4 * ep : nullptr, skey, e->golden.ninst, nb, st));
+                                    e->d_svals, odd ? e->d_split + 4 * ep : nullptr, skey, e->golden.ninst, nb,
+                                    e->d_loops, e->n_loops, c.hang_cap, st));
             HIPCHK(sort_pairs(e->d_tmp, e->tmp_bytes, e->d_skeys, e->d_skeys2, e->d_svals, e->d_svals2, k,
                               skey ? (int)std::min(64u, nb + 3u) : 64, st));
             c.resume = e->d_svals2;

@@ -74,6 +74,19 @@ struct LaneSave {
     uint64_t resv, lock;             // LR/SC: load reservation and lock record (~0 = none)
 };
 
+// A counted loop of the golden text (fi_translate.cpp, the hang proofs' loops),
+// for the solo order's work-left estimate: a survivor whose pc offset from
+// text_lo lies in [lo, hi) has about loop_passes(x[reg] - x[treg], step) * m
+// instructions left in that loop.  Only the order of the trials uses it.
+struct LoopEst {
+    uint32_t lo, hi;
+    uint8_t reg, treg;
+    int8_t step;
+    uint8_t pad;
+    uint32_t m;
+};
+constexpr uint32_t kMaxLoopEst = 64;
+
 // A trial's SE memory-map state once it made a VM syscall (brk, mmap, munmap,
 // close, set_tid_address): gem5's MemState VMA list, brk point and mmap end
 // (src/sim/mem_state.hh), the fd entries 0-2 it closed and childClearTID.

@@ -234,9 +234,35 @@ __global__ void __launch_bounds__(256) fi_hist_kernel(const fi_site *sites, cons
 // solo != 0: the next epoch runs one trial per wave, where the order only
 // decides when a trial starts: trials that rewrote their code (interpreted at
 // ~20x the cost of translated code) start first, then the rest longest-first.
+// The work-left estimate of a solo trial: the golden run's remaining length
+// (the trial follows its path, the usual case: a wrong value carried to the
+// end), or, when the trial stands in a counted loop of the golden text, that
+// loop's remaining passes times its length if larger (a flipped bound, counter
+// or pointer that stretches the loop: profiles/r05tl_solo_timeline_crc32.jsonl,
+// the late starters); capped at the hang cap.
+__device__ __forceinline__ uint64_t solo_work_left(const LaneSave &s, uint64_t text_lo, uint64_t golden_ninst,
+                                                  const LoopEst *loops, uint32_t n_loops, uint64_t hang_cap) {
+    uint64_t w = s.ninst < golden_ninst ? golden_ninst - s.ninst : 0;
+    const uint64_t off = s.pc - text_lo;
+    for (uint32_t i = 0; i < n_loops; i++) {
+        const LoopEst L = loops[i];
+        if (off < L.lo || off >= L.hi) continue;
+        const uint64_t x = s.regs[L.reg] - (L.treg ? s.regs[L.treg] : 0ULL);
+        const uint64_t d = L.step < 0 ? x : 0 - x;
+        const uint32_t a = (uint32_t)(L.step < 0 ? -L.step : L.step);
+        const uint64_t n = (d & (a - 1)) ? ~0ULL : (d / a ? d / a : ~0ULL);   // (fi_trial.hip loop_passes)
+        const uint64_t e = n > (hang_cap / (L.m ? L.m : 1)) ? hang_cap : n * L.m;
+        w = e > w ? e : w;
+        break;
+    }
+    const uint64_t left = s.ninst < hang_cap ? hang_cap - s.ninst : 0;
+    return w < left ? w : left;
+}
+
 __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
                                     uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd,
-                                    uint32_t solo, uint64_t golden_ninst, uint32_t nb) {
+                                    uint32_t solo, uint64_t golden_ninst, uint32_t nb, const LoopEst *loops,
+                                    uint32_t n_loops, uint64_t hang_cap) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= cap) return;
     if (i < *cnt) {
@@ -257,7 +283,12 @@ __global__ void fi_surv_keys_kernel(const LaneSave *save, const uint32_t *list, 
             const bool uninj = (solo & 2u) && ((save[sl].flags >> 1) & 3) == 0;
             // (nb: the bits of the hang cap, above every survivor's numInst --
             // the key then sorts in nb + 2 (+ 1 odd) bits: fewer radix passes)
-            k = ((uint64_t)(first ? 0 : uninj ? 1 : 2) << nb) | save[sl].ninst;
+            // (tier 2: the most work left first, by the estimate below the cap)
+            const uint64_t low = (first || uninj || !n_loops)
+                                     ? save[sl].ninst
+                                     : ((1ULL << nb) - 1) - solo_work_left(save[sl], text_lo, golden_ninst, loops,
+                                                                          n_loops, hang_cap);
+            k = ((uint64_t)(first ? 0 : uninj ? 1 : 2) << nb) | low;
         }
         if (n_odd) {
             k = solo ? (((pc & 1) << (nb + 2)) | k) : (((pc & 1) << 63) | (k >> 1));
@@ -394,9 +425,10 @@ hipError_t launch_redo_scatter(const uint32_t *idx, uint64_t n, const fi_outcome
 }
 hipError_t launch_surv_keys(const LaneSave *save, const uint32_t *list, const uint32_t *cnt, uint64_t cap,
                             uint64_t text_lo, uint64_t *keys, uint32_t *vals, uint32_t *n_odd, uint32_t solo,
-                            uint64_t golden_ninst, uint32_t nb, hipStream_t st) {
+                            uint64_t golden_ninst, uint32_t nb, const LoopEst *loops, uint32_t n_loops,
+                            uint64_t hang_cap, hipStream_t st) {
     hipLaunchKernelGGL(fi_surv_keys_kernel, dim3(nblk(cap, 256)), dim3(256), 0, st, save, list, cnt, cap, text_lo,
-                       keys, vals, n_odd, solo, golden_ninst, nb);
+                       keys, vals, n_odd, solo, golden_ninst, nb, loops, n_loops, hang_cap);
     return hipGetLastError();
 }
 hipError_t launch_odd_split(const uint32_t *cnt, const uint32_t *n_odd, uint32_t *split, uint32_t grid,

@@ -1554,6 +1554,12 @@ __device__ __forceinline__ bool ult64(uint64_t a, uint64_t b) {
     return ah < bh || (ah == bh && (uint32_t)a < (uint32_t)b);
 }
 
+#ifndef FI_SOLO_VLOAD   // clean solo body: vector loads from shared frames too (0: scalar loads there; profiles/r06 A/B)
+#define FI_SOLO_VLOAD 1
+#endif
+#ifndef FI_SOLO_CPB     // clean solo body: site caches hold frame - page address (0: the TLB entry)
+#define FI_SOLO_CPB 1
+#endif
 typedef __attribute__((address_space(3))) uint64_t lds_u64;
 typedef __attribute__((address_space(3))) LaneMem lds_mem;
 
@@ -1790,6 +1796,30 @@ __device__ __noinline__ void solo_tx_clean_run(KCtx *CX, lds_u64 *R, lds_mem *mp
     TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
     TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
 #undef TXR
+    // the site caches (fi_translate.cpp): the page number CV of the last page a
+    // site touched and its TLB entry CP (frame | private bit) -- or, with
+    // FI_SOLO_CPB, the frame minus the page's own address (a hit is one add)
+    // and the private bit apart in CQ
+#if FI_SOLO_CPB
+#define SC_SET(i, vp, e) (CV##i = (vp), CP##i = ((e) & ~1ULL) - ((vp) << 12), CQ##i = (uint32_t)(e) & 1u)
+#define SC_PTR(i, ea) ((uint8_t *)(uintptr_t)(CP##i + (ea)))
+#define SC_PRIV(i) (CQ##i != 0u)
+#else
+#define SC_SET(i, vp, e) (CV##i = (vp), CP##i = (e))
+#define SC_PTR(i, ea) ((uint8_t *)(uintptr_t)((CP##i & ~1ULL) + ((ea) & 4095u)))
+#define SC_PRIV(i) ((CP##i & 1u) != 0)
+#endif
+#if FI_SOLO_VLOAD
+    // every translated load through the vector memory path (shared frames are
+    // read-only during a launch: either path reads the same bytes)
+#undef SPRIV
+#define SPRIV(x) ((x) || true)
+#endif
+    // the clean body's temporaries (fi_translate.cpp: no block-scope variables)
+    uint8_t *p_;
+    bool pv_;
+    uint64_t v_, ea_, vp_, e_, t_, off_;
+    (void)p_; (void)pv_; (void)v_; (void)ea_; (void)vp_; (void)e_; (void)t_; (void)off_;
     goto S_entry;
     /*@TX_SOLO_CLEAN@*/
 S_out:
@@ -3606,6 +3636,9 @@ leave:
 // crc32 (tools/gpu/solo_ab.sh, profiles/r02j_solo_ab.txt): 1 (no bound, 136-140
 // VGPRs, 3 waves) 6.44M, 4: 7.06M trials/s; VGPR-pinned guest registers
 // 3.2-3.7M.
+#ifndef FI_SOLO_AGE   // solo waves raise their priority at 2^k, 2^(k+1), 2^(k+2) instructions (0: off)
+#define FI_SOLO_AGE 0
+#endif
 #ifndef FI_SOLO_WAVES_PER_EU
 #define FI_SOLO_WAVES_PER_EU 4
 #endif
@@ -4282,6 +4315,14 @@ __device__ __forceinline__ void trial_body() {
                     n_iter += st;
                     n_tx += st;
                     n_txin++;
+#if FI_SOLO_AGE
+                    // ageing: a solo trial that has run long is likely to run long
+                    // still (the campaign's tail); it gets the issue arbiter's
+                    // preference over the younger waves of its CU
+                    if (n_iter >= (4u << FI_SOLO_AGE)) __builtin_amdgcn_s_setprio(3);
+                    else if (n_iter >= (2u << FI_SOLO_AGE)) __builtin_amdgcn_s_setprio(2);
+                    else if (n_iter >= (1u << FI_SOLO_AGE)) __builtin_amdgcn_s_setprio(1);
+#endif
                     if (kOdd && L.ninst > CX->gninst && !uni32(sio->hang)) {
                         LP.cnt += st;
                         if (LP.cnt >= LP.at) lp_count((lds_lp *)&LP, CX, (const lds_u64 *)R, slot, L.pc, L.fp, LP_ELIGIBLE, 0u);
