@@ -1221,21 +1221,29 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     sc_head += "S_entry:\n";
     for (uint32_t i = 0; i < kSiteCaches; i++) sc_head += sfmt("  CV%u = ~0ULL; CP%u = 0; CQ%u = 0;\n", i, i, i);
     sc_head += "  goto S_dispatch;\n";
-    // the clean body's temporaries live at function scope (solo_tx_clean_run
-    // declares them): a goto out of a block that declares a variable leaves
+    // the bodies' temporaries live at function scope (fi_trial.hip declares
+    // them, TX_TEMPS): a goto out of a block that declares a variable leaves
     // through clang's lifetime cleanup switch -- a flag set, compared and
-    // branched on at every exit test (crc32's loop: 38 -> 23 scalar
+    // branched on at every exit test (crc32's clean loop: 38 -> 23 scalar
     // instructions per iteration, and loaded values stay in VGPRs)
-    std::string body_c = sc.out;
-    for (const auto &[from, to] : std::vector<std::pair<std::string, std::string>>{
-             {"uint8_t *p_; ", ""}, {"bool pv_; ", ""}, {"uint64_t v_; ", ""},
-             {", vp_ = ea_ >> 12;", "; vp_ = ea_ >> 12;"}, {"const uint64_t ea_ = ", "ea_ = "},
-             {"const uint64_t e_ = ", "e_ = "}, {"const uint64_t t_ = ", "t_ = "},
-             {"const uint64_t off_ = ", "off_ = "}}) {
-        for (size_t at = body_c.find(from); at != std::string::npos; at = body_c.find(from, at + to.size()))
-            body_c.replace(at, from.size(), to);
-    }
-    return g.out + FI_TX_SPLIT + so.out + FI_TX_SPLIT + sq.out + FI_TX_SPLIT + sc_head + body_c;
+    auto hoist = [](std::string t) {
+        for (const auto &[from, to] : std::vector<std::pair<std::string, std::string>>{
+                 {"uint8_t *p_; ", ""}, {"bool pv_; ", ""}, {"uint64_t v_; ", ""},
+                 {", vp_ = ea_ >> 12;", "; vp_ = ea_ >> 12;"}, {"const uint64_t ea_ = ", "ea_ = "},
+                 {"const uint64_t e_ = ", "e_ = "}, {"const uint64_t t_ = ", "t_ = "},
+                 {"const uint64_t t0_ = ", "t0_ = "}, {"const uint64_t off_ = ", "off_ = "},
+                 {"const uint32_t cs_ = ", "cs_ = "}, {"const bool chg_ = ", "chg_ = "},
+                 {"const bool ok_ = ", "ok_ = "}, {"const bool c_ = ", "c_ = "},
+                 {"const uint64_t tk_ = ", "tk_ = "}, {"const uint32_t mm_ = ", "mm_ = "}}) {
+            for (size_t at = t.find(from); at != std::string::npos; at = t.find(from, at + to.size()))
+                t.replace(at, from.size(), to);
+        }
+        return t;
+    };
+    // (the clean body only: hoisting the 64-lane body's doubles its spills
+    // (intmix 183 -> 985 VGPRs), the full solo body's costs crc32 +3 % and
+    // saves qsort 7 %: profiles/r06h_ab_hoist_scope_*.jsonl)
+    return g.out + FI_TX_SPLIT + so.out + FI_TX_SPLIT + sq.out + FI_TX_SPLIT + sc_head + hoist(sc.out);
 }
 
 }  // namespace fi

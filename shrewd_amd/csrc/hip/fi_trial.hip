@@ -1441,6 +1441,15 @@ typedef __attribute__((address_space(1), aligned(1))) uint64_t g_u64;
 #define SUNI(x) (x)
 #define SUNI32(x) (x)
 #define SX(r, e) X##r = (uint64_t)(e)
+// the translated bodies' temporaries, at function scope (fi_translate.cpp:
+// no block-scope variables in the generated text)
+#define TX_TEMPS()                                                                       \
+    uint8_t *p_;                                                                         \
+    bool pv_, ok_, c_, chg_;                                                             \
+    uint64_t v_, ea_, vp_, e_, t_, t0_, tk_, off_;                                       \
+    uint32_t cs_, mm_;                                                                   \
+    (void)p_; (void)pv_; (void)ok_; (void)c_; (void)chg_; (void)v_; (void)ea_; (void)vp_; \
+    (void)e_; (void)t_; (void)t0_; (void)tk_; (void)off_; (void)cs_; (void)mm_
 // cycle headers: the pending-route flag as an opaque scalar (fi_translate.cpp)
 #define ETGT_OPAQUE() __asm__ volatile("" : "+s"(eon))
 
@@ -1634,6 +1643,7 @@ __device__ __noinline__ void solo_tx_run(KCtx *CX, lds_u64 *R, lds_mem *mp, lds_
     TXR(14) TXR(15) TXR(16) TXR(17) TXR(18) TXR(19) TXR(20) TXR(21) TXR(22) TXR(23) TXR(24) TXR(25)
     TXR(26) TXR(27) TXR(28) TXR(29) TXR(30) TXR(31)
 #undef TXR
+    TX_TEMPS();
 #ifdef FI_TX_SOLO_ODD
     if constexpr (kOdd) {
         goto Q_dispatch;
@@ -1815,11 +1825,7 @@ __device__ __noinline__ void solo_tx_clean_run(KCtx *CX, lds_u64 *R, lds_mem *mp
 #undef SPRIV
 #define SPRIV(x) ((x) || true)
 #endif
-    // the clean body's temporaries (fi_translate.cpp: no block-scope variables)
-    uint8_t *p_;
-    bool pv_;
-    uint64_t v_, ea_, vp_, e_, t_, off_;
-    (void)p_; (void)pv_; (void)v_; (void)ea_; (void)vp_; (void)e_; (void)t_; (void)off_;
+    TX_TEMPS();
     goto S_entry;
     /*@TX_SOLO_CLEAN@*/
 S_out:
@@ -4417,6 +4423,7 @@ __device__ __forceinline__ void trial_body() {
         pmin = uni64(pend ? wmin64<kNL>(((pend >> lane) & 1) ? lp : kNone) : kNone);         \
         wmin = uni64(ult64(pmin, owm) ? pmin : owm);                                         \
     } while (0)
+                TX_TEMPS();
                 goto tx_dispatch;
                 /*@TX_BODY@*/
 #undef TXMERGE
