@@ -141,7 +141,7 @@ typedef struct {
     uint32_t snapshot_interval;     /* golden snapshot every N committed insts (0 -> auto, >= 256) */
     uint32_t flags;                 /* FI_CFG_* */
     uint32_t epoch_iters;           /* first epoch's loop iterations per wave (0 -> 384; then x4, x16, unbounded) */
-    uint32_t lanes_per_wave;        /* trials per 64-lane wave in the first epoch: 1, 2, 4, ..., 64 (0 -> 64) */
+    uint32_t lanes_per_wave;        /* trials per 64-lane wave in the first epoch: 1, 2, 4, ..., 64 (0 -> 32) */
     uint32_t resume_lanes;          /* trials per wave in resumed epochs (0 -> default): survivors have diverged, and
                                        a wave serialises its lanes' distinct control flows, so fewer per wave */
     uint32_t epochs;                /* epochs per chunk (0 -> 2): budgets b, 4b, 16b, 16b, ..., unbounded */

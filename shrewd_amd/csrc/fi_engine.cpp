@@ -79,8 +79,12 @@ hipError_t sort_pairs(void *tmp, size_t bytes, const uint64_t *kin, uint64_t *ko
 
 using namespace fi;
 
-// trials per wave when fi_config.lanes_per_wave is 0
-static constexpr uint32_t kDefaultLanes = 64;
+// trials per wave when fi_config.lanes_per_wave is 0: 32 of
+// a wave's 64 lanes -- twice the waves in the first epoch (3,125 for 100k
+// trials: ~3 per SIMD instead of 1.5) and half the divergence per wave;
+// profiles/r06w_sweep_lanes_*.jsonl: crc32 4.37 -> 4.13 ms, intmix 243 ->
+// 225 ms, qsort even against 64; 16 loses on crc32
+static constexpr uint32_t kDefaultLanes = 32;
 static constexpr uint32_t kPreTail = 4;   // zero PreInst entries past the text (fi_trial.hip solo_pre_run)
 static constexpr uint32_t kDefaultResumeLanes = 8;   // measured: profiles/README.md (r01b sweep)
 // trials per launch while the translated kernels are still being built, so
