@@ -20,7 +20,10 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/prof_write_$TAG -o write --ou
     python $R/bench.py --steps 2 --warmup 0 --no-cpu-baseline --workloads "" > $O/prof_write_$TAG.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
     -d $O/prof_sq_$TAG -o sq --output-format csv -- \
-    python $R/bench.py --steps 2 --warmup 0 --no-cpu-baseline --workloads "" > $O/prof_sq_$TAG.log 2>&1
+    python $R/bench.py --steps 2 --warmup 0 --no-cpu-baseline --workloads "" > $O/prof_sq_$TAG.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SMEM SQ_INSTS_VMEM GRBM_GUI_ACTIVE \
+    -d $O/prof_sqb_$TAG -o sqb --output-format csv -- \
+    python $R/bench.py --steps 2 --warmup 0 --no-cpu-baseline --workloads "" > $O/prof_sqb_$TAG.log 2>&1
 rc=$?
 echo "profile rc=$rc"
 exit $rc

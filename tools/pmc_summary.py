@@ -23,6 +23,8 @@ KERNELS = ("fi_trial_kernel_tx", "fi_trial_kernel_tx_solo", "fi_trial_kernel_tx_
            "fi_trial_kernel", "fi_trial_kernel_solo")
 SQ = ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
       "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE")
+SQB = ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_VALU",
+       "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_SMEM", "SQ_INSTS_VMEM")
 
 
 def rows(path):
@@ -55,6 +57,9 @@ def main():
     fr = rows(os.path.join(g, f"prof_fetch_{tag}", "fetch_counter_collection.csv"))
     wr = rows(os.path.join(g, f"prof_write_{tag}", "write_counter_collection.csv"))
     sr = rows(os.path.join(g, f"prof_sq_{tag}", "sq_counter_collection.csv"))
+    # the wait / active-instruction pass (tools/gpu_profile.sh), when taken
+    sqb_path = os.path.join(g, f"prof_sqb_{tag}", "sqb_counter_collection.csv")
+    sbr = rows(sqb_path) if os.path.exists(sqb_path) else []
     trace = rows(os.path.join(g, f"prof_trace_{tag}", "trace_kernel_trace.csv"))
     wl = bench["config"]["workload"].split()[0]
     bk = bench["roofline"].get("per_kernel", {})
@@ -67,6 +72,15 @@ def main():
         fetch, nf = per_launch(fr, "FETCH_SIZE", kn)
         write, nw = per_launch(wr, "WRITE_SIZE", kn)
         sq = {name: per_launch(sr, name, kn)[0] for name in SQ}
+        for name in SQB:
+            if sbr:
+                sq[name] = per_launch(sbr, name, kn)[0]
+        if sq.get("SQ_WAIT_INST_ANY") is not None and sq.get("SQ_WAVE_CYCLES"):
+            # shares of wave-cycles (both counted in quad-cycles per wave)
+            sq["share_wait_inst_any"] = sq["SQ_WAIT_INST_ANY"] / sq["SQ_WAVE_CYCLES"]
+            sq["share_wait_any"] = sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"]
+        if sq.get("GRBM_GUI_ACTIVE") and sq.get("SQ_INSTS_SALU") is not None:
+            sq["salu_per_cu_cycle"] = sq["SQ_INSTS_SALU"] / (256 * sq["GRBM_GUI_ACTIVE"] / 8)
         hbm = (2 * fetch + write) * 1024 if fetch is not None and write is not None else None
         # issue roof: instructions issued per SIMD-cycle (MI355X: 256 CUs x 4
         # SIMDs; GRBM_GUI_ACTIVE sums the 8 XCDs, SQ_WAVE_CYCLES counts quad-cycles)
