@@ -48,6 +48,12 @@ fi_status fi_debug_golden_trace(fi_engine *e, void *pre_out, uint64_t pre_cap, u
 /* Run the translator on given inputs (no device): the generated C++. */
 fi_status fi_debug_translate(const void *pre, uint64_t n_pre, uint64_t text_lo, const uint32_t *trace,
                              uint64_t n_trace, char *out, uint64_t cap, uint64_t *len);
+/* The translator's counted loops on given inputs (no device): the solo
+ * order's work-left estimates (fi_types.h LoopEst: text span lo, hi as
+ * offsets from text_lo, counter reg, compared treg, step, instructions per
+ * pass m; 16 bytes each).  *n = their number, out gets up to cap of them. */
+fi_status fi_debug_loop_est(const void *pre, uint64_t n_pre, uint64_t text_lo, const uint32_t *trace,
+                            uint64_t n_trace, void *out, uint64_t cap, uint64_t *n);
 /* The C++ generated for the golden blocks by the last fi_golden_run
  * (fi_translate.cpp); *len = its length, buf gets up to cap-1 bytes + NUL. */
 fi_status fi_debug_translation(fi_engine *e, char *buf, uint64_t cap, uint64_t *len);

@@ -2116,6 +2116,20 @@ fi_status fi_debug_golden_trace(fi_engine *e, void *pre_out, uint64_t pre_cap, u
     return FI_OK;
 }
 
+fi_status fi_debug_loop_est(const void *pre, uint64_t n_pre, uint64_t text_lo, const uint32_t *trace,
+                            uint64_t n_trace, void *out, uint64_t cap, uint64_t *n) {
+    if (!pre || !trace) return FI_E_ARG;
+    std::vector<PreInst> p((const PreInst *)pre, (const PreInst *)pre + n_pre);
+    std::vector<uint32_t> t(trace, trace + n_trace), leaders;
+    std::vector<LoopEst> loops;
+    uint32_t n_tx = 0;
+    (void)translate_blocks(p, text_lo, t, {}, leaders, n_tx, true, &loops);
+    static_assert(sizeof(LoopEst) == 16, "LoopEst is 16 bytes (fi_debug.h)");
+    if (out) memcpy(out, loops.data(), std::min<uint64_t>(cap, loops.size()) * sizeof(LoopEst));
+    if (n) *n = loops.size();
+    return FI_OK;
+}
+
 fi_status fi_debug_translate(const void *pre, uint64_t n_pre, uint64_t text_lo, const uint32_t *trace,
                              uint64_t n_trace, char *out, uint64_t cap, uint64_t *len) {
     if (!pre || !trace) return FI_E_ARG;

@@ -118,6 +118,7 @@ CFG_NO_ODD_KERNEL = 4096
 CFG_JIT_NO_CACHE = 8192
 CFG_NO_HANG_PROOF = 16384
 CFG_NO_OVERFLOW = 32768
+CFG_NO_LOOP_ORDER = 65536
 
 
 class GoldenInfo(C.Structure):

@@ -325,6 +325,7 @@ PATH_FLAGS = {
     "simt_no_solo_interp": 256 | 64 | 4,    # the step loop for every epoch, no translated blocks
     "no_odd_kernel": 4096,                  # FI_CFG_NO_ODD_KERNEL: odd-pc survivors on the solo kernel
     "no_redo": 2048,                        # FI_CFG_NO_REDO: no second pass for private-page exhaustion
+    "no_loop_order": 65536,                 # FI_CFG_NO_LOOP_ORDER: solo order by the golden remainder only
 }
 _PATH_REF = {}
 

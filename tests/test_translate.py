@@ -65,3 +65,48 @@ def test_clean_body_shape():
     assert "#define SADD(n_) (brem -= (n_))" in clean and "#define SCOLD(x)" in clean
     assert "SCOLD(" in clean and "SPRIV(x) __builtin_expect" not in clean
     assert _translate({"SHREWD_FI_TXV": "47"}) == base
+
+
+def test_crc32_loop_estimates():
+    """The counted loops the translator exports for the solo order's work-left
+    estimate (fi_types.h LoopEst, fi_kernels.hip solo_work_left): the loops
+    its hang proofs recognise -- crc32's table inner bit loop (t6 counts
+    down) and the crc loop (a0 runs up to a1) -- each with its instructions
+    per pass and a text span around its blocks."""
+    from shrewd_amd.fi import lib
+    L = lib()
+    L.fi_debug_loop_est.restype = C.c_int
+    L.fi_debug_loop_est.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                    C.POINTER(C.c_uint64)]
+    z = np.load(os.path.join(ROOT, "tests", "golden", "tx_inputs_crc32.npz"))
+    pre, tr = np.ascontiguousarray(z["pre"]), np.ascontiguousarray(z["trace"])
+    dt = np.dtype([("lo", "<u4"), ("hi", "<u4"), ("reg", "u1"), ("treg", "u1"), ("step", "i1"), ("pad", "u1"),
+                   ("m", "<u4")])
+    n = C.c_uint64()
+    assert L.fi_debug_loop_est(pre.ctypes.data, len(pre), int(z["text_lo"]), tr.ctypes.data, len(tr), None, 0,
+                               C.byref(n)) == 0
+    out = np.zeros(n.value, dt)
+    L.fi_debug_loop_est(pre.ctypes.data, len(pre), int(z["text_lo"]), tr.ctypes.data, len(tr), out.ctypes.data,
+                        n.value, C.byref(n))
+    loops = {(int(r["reg"]), int(r["treg"]), int(r["step"]), int(r["m"])): (int(r["lo"]), int(r["hi"])) for r in out}
+    assert (10, 11, 1, 10) in loops     # crc_loop: lbu .. addi a0, a0, 1; bne a0, a1
+    assert (31, 0, -1, 5) in loops      # tbl_inner: addi t6, t6, -1; bnez t6 (shortest pass: 5)
+    # the buffer fill (gen: sw t0, 0(t2) .. addi s1, s1, -1; bnez s1) stores:
+    # no proof, no estimate (the golden remainder stands)
+    assert not any(k[0] == 9 for k in loops) and len(loops) == 2
+    lo, hi = loops[(10, 11, 1, 10)]
+    assert lo == 0x16C and hi == 0x16C + 0x22   # the crc loop's one block (pc 0x1016c, 34 bytes)
+
+
+def test_clean_body_temporaries_at_function_scope():
+    """The clean body declares no block-scope temporaries (a goto out of such
+    a block leaves through clang's lifetime cleanup switch: DESIGN.md 4h);
+    solo_tx_clean_run declares them (TX_TEMPS)."""
+    clean = _translate().split("/*@TX_SPLIT@*/")[-1]
+    for decl in ("uint8_t *p_;", "bool pv_;", "uint64_t v_;", "const uint64_t ea_", "const uint64_t e_ ",
+                 "const uint64_t t_ ", "const uint64_t off_"):
+        assert decl not in clean, decl
+    assert "ea_ = X10 + " in clean
+    src = open(os.path.join(ROOT, "shrewd_amd", "csrc", "hip", "fi_trial.hip")).read()
+    fn = src[src.index("void solo_tx_clean_run("):src.index("/*@TX_SOLO_CLEAN@*/")]
+    assert "TX_TEMPS();" in fn
