@@ -649,12 +649,15 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     // test, the exit also against a register the block does not write (bne
     // a0, a1), steps of +-1, 2, 4, 8, and plain loads whose address is either
     // the counter plus a constant or a register the block does not write plus
-    // a bounded offset (andi / slli / shNadd chains: a table lookup).  Such a
-    // loop that cannot leave before the cap either faults on a counter load's
-    // first page that is not mapped (a crash at an exact instruction) or
-    // reaches the cap; the kernel decides which from the lane's page set
-    // (loop_outcome, fi_trial.hip), so the body only passes the loads on.
-    struct ProofLoad { uint32_t reg, kind, size, pos; int64_t off; uint64_t span; };   // kind 0 counter, 1 bounded
+    // a bounded offset (andi / slli / shNadd chains: a table lookup), and
+    // stores at the counter plus a constant (round 6: the data they write
+    // never steers the loop).  Such a loop that cannot leave before the cap
+    // either faults on a counter access's first page that is not mapped (a
+    // crash at an exact instruction) or reaches the cap; the kernel decides
+    // which from the lane's page set (loop_outcome, fi_trial.hip; a store walk
+    // that would reach the code range stays undecided), so the body only
+    // passes the accesses on.
+    struct ProofLoad { uint32_t reg, kind, size, pos; int64_t off; uint64_t span; };   // kind 0 counter, 1 bounded, 2 counter store
     struct HangProof { uint32_t reg, treg; int step; uint32_t m; std::vector<ProofLoad> loads; };
     std::map<uint32_t, HangProof> hang_proof;
     // abstract value of a register inside a run-off block: TOP unknown; CNT the
@@ -709,7 +712,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 const PreInst &p = pre[b.insts[i]];
                 const uint64_t pc = text_lo + 2ULL * b.insts[i];
                 const Cls k = classify(p, e, sz, sx, cond);
-                if (k == C_STORE || k == C_JALR || k == C_STOP || (k == C_LOAD && in.size() != 1)) ok = false;
+                if (k == C_JALR || k == C_STOP || ((k == C_LOAD || k == C_STORE) && in.size() != 1)) ok = false;
                 if ((k == C_ALU || k == C_JAL || k == C_LOAD) && p.rd) writes[p.rd]++;
                 if (k == C_BR) { to(pc + (int64_t)p.imm, true); to(pc + p.len, false); }
                 if (k == C_JAL) to(pc + (int64_t)p.imm, true);
@@ -761,6 +764,15 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                     else if (A.k == AV_BND) loads.push_back({A.base, 1u, sz, (uint32_t)i, A.lo + imm, (uint64_t)(A.hi - A.lo)});
                     else ok = false;
                     if (p.rd) av[p.rd] = AVal{AV_TOP, 0, 0, 0};
+                    continue;
+                }
+                // a store at the counter plus a constant walks memory like a
+                // counter load (kind 2: loop_outcome also keeps it out of the
+                // code range); its data never steers the loop, whose exit
+                // depends on the counter alone.  Any other store: no proof.
+                if (k == C_STORE) {
+                    if (A.k == AV_CNT) loads.push_back({reg, 2u, sz, (uint32_t)i, A.lo + imm, 0u});
+                    else ok = false;
                     continue;
                 }
                 if (!p.rd || (k != C_ALU && k != C_JAL)) continue;

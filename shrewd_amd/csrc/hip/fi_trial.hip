@@ -1704,10 +1704,11 @@ __device__ __forceinline__ bool page_mapped(KCtx *c, const WaveMem &w, const Lan
 // before the hang cap (fi_translate.cpp; the registers are the ones at the
 // loop's first instruction, `left` the instructions to the cap).  Iteration i
 // runs the block's instruction at position p as the (i m + p)-th from here,
-// if i < n (the n-th pass of the branch leaves) and i m + p < left.  Loads at
-// the counter plus a constant walk through memory; bounded loads (a table
-// lookup) stay inside [base + off, base + off + span + size).
-//   2: a counter load first touches a page outside the lane's set that
+// if i < n (the n-th pass of the branch leaves) and i m + p < left.  Loads and
+// stores (kind 2) at the counter plus a constant walk through memory -- a
+// store walk that could reach the code range is undecided --; bounded loads
+// (a table lookup) stay inside [base + off, base + off + span + size).
+//   2: a counter access first touches a page outside the lane's set that
 //      MemState::fixupFault would not map (mem_state.cc:387-447) -- the
 //      process dies there with GenericPageTableFault (sim/faults.cc:95-105):
 //      *k instructions commit first, *fva is the address;
@@ -1739,6 +1740,12 @@ __device__ __noinline__ int loop_outcome(KCtx *c, const WaveMem &w, const LaneMe
         if (pos >= left) continue;
         uint64_t ilim = (left - pos + mm - 1) / mm;   // iterations in which it runs
         if (n < ilim) ilim = n;
+        if (kind == 2) {   // a store walk: undecided if it could reach the code range (it would rewrite code)
+            const uint64_t span = (ilim - 1) * ac;
+            if (ilim > 1 && span / ac != ilim - 1) return 0;
+            const uint64_t lo = cs > 0 ? a0 : a0 - span, hi = (cs > 0 ? a0 + span : a0) + size;
+            if ((cs > 0 ? hi < a0 : lo > a0) || !(hi <= c->code_lo || lo >= c->code_hi)) return 0;
+        }
         uint64_t i = 0;
         for (uint32_t pg = 0; i < ilim; pg++) {
             if (pg > 512) return 0;

@@ -463,6 +463,38 @@ def test_runoff_loop_proofs(oracle_mod):
     assert ins_on < ins_off
 
 
+def test_storeoff_loop_proofs(oracle_mod):
+    """Run-off loops that store at their counter (round 6: fi_translate.cpp
+    kind 2, fi_trial.hip loop_outcome): store walks off a .bss buffer end as
+    page-fault crashes proved at the loop's entry (stats[57]); walks that
+    could reach the code range or go into heap pages the fault handler maps
+    stay undecided (stats[58]) and run on.  Every record equals the oracle's
+    (reference semantics: mem_state.cc:387-447, sim/faults.cc:95-105), with
+    the proofs on and off."""
+    from shrewd_amd import Engine
+    from shrewd_amd.fi import CFG_NO_HANG_PROOF
+    import test_isa_vectors as kat
+    elf = kat.storeoff_program_elf()
+    o = oracle_mod.Oracle(elf, "storeoff")
+    g = o.run_golden()
+    sites = kat.storeoff_sites(g.ninst, 3000)
+    ref = o.run_trials(sites, protect_mask=0)
+    got = []
+    for flags in (0, CFG_NO_HANG_PROOF):
+        e = Engine(flags=flags)
+        e.load_elf(elf, ["storeoff"])
+        e.golden_run()
+        dev, h = e.run_sites(sites)
+        assert e.translate_status() == ""
+        compare(dev, ref, sites)
+        st = e.debug_stats()
+        got.append((int(st[57]), int(st[58]), int(h["device_insts"])))
+        e.close()
+    (crash_on, und_on, ins_on), (crash_off, und_off, ins_off) = got
+    assert crash_on > 10 and und_on > 0 and crash_off == 0 and und_off == 0
+    assert ins_on < ins_off
+
+
 def test_run_trials_equals_run_sites(engine_factory):
     e = engine_factory("crc32")
     e.set_campaign(4242, REGS | PC, 1)

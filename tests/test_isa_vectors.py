@@ -2268,6 +2268,142 @@ def runoff_sites(ninst, n=3000, seed=11):
     return s
 
 
+# ------------------------------------------------------------ storeoff program
+# Store walks whose faulted trials run off their buffers (the run-off proofs'
+# counter stores, round 6: fi_translate.cpp kind 2, fi_trial.hip loop_outcome):
+# a forward byte store over a .bss buffer (past its end: outside every VMA, a
+# page-fault crash -- mem_state.cc:387-447, sim/faults.cc:95-105), a backward
+# read-modify-write word walk (down through .data into the text: a store walk
+# that could rewrite code stays undecided and runs on), and a byte store over
+# the first brk page (past it: heap pages the fault handler maps, undecided).
+STOREOFF_BUF = 4096
+
+
+def storeoff_program_source() -> str:
+    return f"""    .text
+_start:
+    la    s0, buf
+    li    s5, 3
+    li    t4, 1
+passA:
+    mv    a0, s0
+    li    t0, {STOREOFF_BUF}
+    add   a1, s0, t0
+storeA:
+    sb    t4, 0(a0)
+    addi  a0, a0, 1
+    bne   a0, a1, storeA
+    addi  t4, t4, 7
+    addi  s5, s5, -1
+    bnez  s5, passA
+    li    s5, 2
+passB:
+    li    t0, {STOREOFF_BUF - 4}
+    add   a0, s0, t0
+    addi  a1, s0, -4
+storeB:
+    lw    t1, 0(a0)
+    addi  t1, t1, 3
+    sw    t1, 0(a0)
+    addi  a0, a0, -4
+    bne   a0, a1, storeB
+    addi  s5, s5, -1
+    bnez  s5, passB
+    li    a0, 0
+    li    a7, 214
+    ecall
+    mv    s7, a0
+    li    t0, 0x10000
+    add   a0, s7, t0
+    li    a7, 214
+    ecall
+    li    s5, 4
+passC:
+    mv    a0, s7
+    addi  a1, s7, 64
+storeC:
+    sb    s5, 0(a0)
+    addi  a0, a0, 1
+    bne   a0, a1, storeC
+    addi  s5, s5, -1
+    bnez  s5, passC
+    li    s6, 0
+    li    t0, 0
+    li    t1, {STOREOFF_BUF}
+sum:
+    add   t2, s0, t0
+    lbu   t3, 0(t2)
+    slli  s6, s6, 1
+    xor   s6, s6, t3
+    addi  t0, t0, 1
+    bne   t0, t1, sum
+    li    t0, 0
+    li    t1, 64
+hsum:
+    add   t2, s7, t0
+    lbu   t3, 0(t2)
+    add   s6, s6, t3
+    addi  t0, t0, 1
+    bne   t0, t1, hsum
+    la    a1, out
+    sd    s6, 0(a1)
+    li    a0, 1
+    li    a2, 8
+    li    a7, 64
+    ecall
+    li    a0, 0
+    li    a7, 93
+    ecall
+    .bss
+    .balign 8
+out:
+    .zero 8
+buf:
+    .zero {STOREOFF_BUF}
+"""
+
+
+def storeoff_program_elf() -> bytes:
+    from tools.rvasm.rvasm import assemble
+    return assemble(storeoff_program_source(), compress=False)
+
+
+def storeoff_program_expected() -> bytes:
+    M = (1 << 64) - 1
+    buf = bytearray([1 + 7 * 2] * STOREOFF_BUF)   # the third pass's byte
+    for _ in range(2):                               # two read-modify-write passes, word by word
+        for k in range(0, STOREOFF_BUF, 4):
+            w = (int.from_bytes(buf[k:k + 4], "little") + 3) & 0xFFFFFFFF
+            buf[k:k + 4] = w.to_bytes(4, "little")
+    s6 = 0
+    for b in buf:
+        s6 = ((s6 << 1) ^ b) & M
+    s6 = (s6 + 64 * 1) & M                           # the last heap pass stores 1
+    return s6.to_bytes(8, "little")
+
+
+def storeoff_sites(ninst, n=3000, seed=12):
+    """Single-bit faults on the store pointer (a0) and the walk's end (a1)."""
+    import numpy as np
+    from oracle.pyoracle import SITE_DT
+    r = np.random.default_rng(seed)
+    s = np.zeros(n, SITE_DT)
+    s["inst"] = r.integers(1, ninst, n)
+    s["mask"] = np.uint64(1) << r.integers(0, 64, n).astype(np.uint64)
+    s["target"] = r.choice([10, 11], n)
+    s["trial"] = np.arange(n)
+    return s
+
+
+def test_storeoff_program_on_oracle(oracle_mod):
+    o = oracle_mod.Oracle(storeoff_program_elf(), "storeoff")
+    g = o.run_golden()
+    assert g.exit_code == 0, g
+    assert o.golden_stdout() == storeoff_program_expected()
+    res = o.run_trials(storeoff_sites(g.ninst, 400), protect_mask=0)
+    assert (res["cls"] == 2).sum() > 20 and (res["sub"][res["cls"] == 2] == 3).any()
+
+
 def test_runoff_program_on_oracle(oracle_mod):
     o = oracle_mod.Oracle(runoff_program_elf(), "runoff")
     g = o.run_golden()
