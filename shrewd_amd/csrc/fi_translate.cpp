@@ -657,14 +657,16 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     // which from the lane's page set (loop_outcome, fi_trial.hip; a store walk
     // that would reach the code range stays undecided), so the body only
     // passes the accesses on.
-    struct ProofLoad { uint32_t reg, kind, size, pos; int64_t off; uint64_t span; };   // kind 0 counter, 1 bounded, 2 counter store
+    // kind 0 counter load, 1 bounded load, 2 counter store, 3 / 4 load / store
+    // at another induction register (span = its step per iteration, int32)
+    struct ProofLoad { uint32_t reg, kind, size, pos; int64_t off; uint64_t span; };
     struct HangProof { uint32_t reg, treg; int step; uint32_t m; std::vector<ProofLoad> loads; };
     std::map<uint32_t, HangProof> hang_proof;
     // abstract value of a register inside a run-off block: TOP unknown; CNT the
     // counter's value at the iteration's start + lo; BND base register (0: none)
     // plus an offset in [lo, hi]
     struct AVal { int k; uint32_t base; int64_t lo, hi; };
-    enum { AV_TOP, AV_CNT, AV_BND };
+    enum { AV_TOP, AV_CNT, AV_BND, AV_IND };   // AV_IND: another induction register base, + lo
     const int64_t kAvLim = (int64_t)1 << 40;
     auto av_ok = [&](AVal v) { return v.k == AV_BND && v.lo > -kAvLim && v.hi < kAvLim && v.lo <= v.hi ? v : AVal{AV_TOP, 0, 0, 0}; };
     auto av_add = [&](AVal a, AVal b) -> AVal {
@@ -749,6 +751,18 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         if (in.size() == 1) {
             AVal av[32];
             for (uint32_t r = 0; r < 32; r++) av[r] = writes[r] ? AVal{AV_TOP, 0, 0, 0} : AVal{AV_BND, r, 0, 0};
+            // other induction registers: written once per iteration, by
+            // addi r, r, c -- an access at r walks memory with its own step
+            // (kinds 3 / 4: the step travels in the span field)
+            int ind_step[32] = {0};
+            for (size_t i = 0; i < E.insts.size(); i++) {
+                const PreInst &p = pre[E.insts[i]];
+                if ((p.op == OP_addi || p.op == OP_c_addi) && p.rd && p.rd == p.rs1 && p.rd != reg && writes[p.rd] == 1 &&
+                    p.imm != 0 && p.imm >= -2048 && p.imm <= 2048) {
+                    ind_step[p.rd] = p.imm;
+                    av[p.rd] = AVal{AV_IND, p.rd, 0, 0};
+                }
+            }
             av[reg] = AVal{AV_CNT, 0, 0, 0};
             for (size_t i = 0; i < E.insts.size() && ok; i++) {
                 std::string e;
@@ -761,6 +775,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 const int64_t imm = p.imm;
                 if (k == C_LOAD) {
                     if (A.k == AV_CNT) loads.push_back({reg, 0u, sz, (uint32_t)i, A.lo + imm, 0u});
+                    else if (A.k == AV_IND)
+                        loads.push_back({A.base, 3u, sz, (uint32_t)i, A.lo + imm, (uint64_t)(uint32_t)ind_step[A.base]});
                     else if (A.k == AV_BND) loads.push_back({A.base, 1u, sz, (uint32_t)i, A.lo + imm, (uint64_t)(A.hi - A.lo)});
                     else ok = false;
                     if (p.rd) av[p.rd] = AVal{AV_TOP, 0, 0, 0};
@@ -772,6 +788,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 // depends on the counter alone.  Any other store: no proof.
                 if (k == C_STORE) {
                     if (A.k == AV_CNT) loads.push_back({reg, 2u, sz, (uint32_t)i, A.lo + imm, 0u});
+                    else if (A.k == AV_IND)
+                        loads.push_back({A.base, 4u, sz, (uint32_t)i, A.lo + imm, (uint64_t)(uint32_t)ind_step[A.base]});
                     else ok = false;
                     continue;
                 }
@@ -780,6 +798,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 if (k == C_ALU) switch (p.op) {
                 case OP_addi: case OP_c_addi: case OP_c_addi4spn: case OP_c_addi16sp:
                     if (A.k == AV_CNT) v = AVal{AV_CNT, 0, A.lo + imm, A.lo + imm};
+                    else if (A.k == AV_IND && p.rd == A.base) v = AVal{AV_IND, A.base, A.lo + imm, A.lo + imm};
                     else v = av_add(A, av_const(imm, imm));
                     break;
                 case OP_add: case OP_c_add: v = av_add(A, B); break;
@@ -798,7 +817,8 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                 av[p.rd] = v;
             }
             for (const ProofLoad &l : loads)
-                if (l.off <= -((int64_t)1 << 31) || l.off >= ((int64_t)1 << 31) || l.span >= (1u << 20)) ok = false;
+                if (l.off <= -((int64_t)1 << 31) || l.off >= ((int64_t)1 << 31) || (l.kind < 3 && l.span >= (1u << 20)))
+                    ok = false;
             if (!ok || loads.size() > 4) continue;
         }
         // m: the fewest instructions from E's successor in the cycle around to E's end

@@ -1705,8 +1705,9 @@ __device__ __forceinline__ bool page_mapped(KCtx *c, const WaveMem &w, const Lan
 // loop's first instruction, `left` the instructions to the cap).  Iteration i
 // runs the block's instruction at position p as the (i m + p)-th from here,
 // if i < n (the n-th pass of the branch leaves) and i m + p < left.  Loads and
-// stores (kind 2) at the counter plus a constant walk through memory -- a
-// store walk that could reach the code range is undecided --; bounded loads
+// stores (kind 2) at the counter plus a constant walk through memory, and so
+// do those at another induction register (kinds 3 / 4, with its own step) --
+// a store walk that could reach the code range is undecided --; bounded loads
 // (a table lookup) stay inside [base + off, base + off + span + size).
 //   2: a counter access first touches a page outside the lane's set that
 //      MemState::fixupFault would not map (mem_state.cc:387-447) -- the
@@ -1735,27 +1736,31 @@ __device__ __noinline__ int loop_outcome(KCtx *c, const WaveMem &w, const LaneMe
                 if (!page_mapped(c, w, m, slot, v)) return 0;
             continue;
         }
-        const uint64_t a0 = x + (uint64_t)off, ac = (uint64_t)(cs < 0 ? -cs : cs);
+        // kinds 0 / 2 walk with the counter, 3 / 4 with another induction
+        // register (its value at the loop's first instruction, its own step)
+        const int64_t st = kind >= 3 ? (int64_t)(int32_t)io->lp_ld[j][2] : (int64_t)cs;
+        if (kind > 4 || st == 0) return 0;
+        const uint64_t a0 = (kind >= 3 ? (br ? R[br] : 0ULL) : x) + (uint64_t)off, ac = (uint64_t)(st < 0 ? -st : st);
         if (size > 1 && ((a0 & (size - 1)) || (ac & (size - 1)))) return 0;   // could straddle a 64-byte line
         if (pos >= left) continue;
         uint64_t ilim = (left - pos + mm - 1) / mm;   // iterations in which it runs
         if (n < ilim) ilim = n;
-        if (kind == 2) {   // a store walk: undecided if it could reach the code range (it would rewrite code)
+        if (kind == 2 || kind == 4) {   // a store walk: undecided if it could reach the code range (it would rewrite code)
             const uint64_t span = (ilim - 1) * ac;
             if (ilim > 1 && span / ac != ilim - 1) return 0;
-            const uint64_t lo = cs > 0 ? a0 : a0 - span, hi = (cs > 0 ? a0 + span : a0) + size;
-            if ((cs > 0 ? hi < a0 : lo > a0) || !(hi <= c->code_lo || lo >= c->code_hi)) return 0;
+            const uint64_t lo = st > 0 ? a0 : a0 - span, hi = (st > 0 ? a0 + span : a0) + size;
+            if ((st > 0 ? hi < a0 : lo > a0) || !(hi <= c->code_lo || lo >= c->code_hi)) return 0;
         }
         uint64_t i = 0;
         for (uint32_t pg = 0; i < ilim; pg++) {
             if (pg > 512) return 0;
-            const uint64_t a = a0 + i * (uint64_t)(int64_t)cs, vpn = a >> 12;
+            const uint64_t a = a0 + i * (uint64_t)st, vpn = a >> 12;
             if (!page_mapped(c, w, m, slot, vpn)) {
                 const uint64_t kj = i * mm + pos;
                 if (kj < best_k) { best_k = kj; best_a = a; }
                 break;
             }
-            if (cs > 0) {   // the first iteration past this page
+            if (st > 0) {   // the first iteration past this page
                 const uint64_t nx = (vpn + 1) << 12;
                 if (!nx) return 0;
                 i = (nx - a0 + ac - 1) / ac;

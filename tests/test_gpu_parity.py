@@ -5,6 +5,8 @@ committed-instruction count) on the same seeded sites.
 """
 import os
 
+import re
+
 import numpy as np
 import pytest
 
@@ -486,6 +488,9 @@ def test_storeoff_loop_proofs(oracle_mod):
         e.golden_run()
         dev, h = e.run_sites(sites)
         assert e.translate_status() == ""
+        if flags == 0:   # proofs for counter stores (kind 2) and induction-pointer stores / loads (4 / 3)
+            kinds = {(int(d) >> 8) & 15 for d in re.findall(r"TXLD\(\d+, (\d+)u", e.debug_translation())}
+            assert {0, 2, 3, 4} <= kinds, kinds
         compare(dev, ref, sites)
         st = e.debug_stats()
         got.append((int(st[57]), int(st[58]), int(h["device_insts"])))

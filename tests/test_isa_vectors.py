@@ -2275,7 +2275,9 @@ def runoff_sites(ninst, n=3000, seed=11):
 # page-fault crash -- mem_state.cc:387-447, sim/faults.cc:95-105), a backward
 # read-modify-write word walk (down through .data into the text: a store walk
 # that could rewrite code stays undecided and runs on), and a byte store over
-# the first brk page (past it: heap pages the fault handler maps, undecided).
+# the first brk page (past it: heap pages the fault handler maps, undecided);
+# then a word store and a byte load at a pointer that steps beside a separate
+# down-counter (kinds 3 / 4: another induction register).
 STOREOFF_BUF = 4096
 
 
@@ -2309,6 +2311,14 @@ storeB:
     bne   a0, a1, storeB
     addi  s5, s5, -1
     bnez  s5, passB
+    li    s1, {STOREOFF_BUF // 4}
+    mv    t2, s0
+    li    t4, 0x01020304
+storeD:
+    sw    t4, 0(t2)
+    addi  t2, t2, 4
+    addi  s1, s1, -1
+    bnez  s1, storeD
     li    a0, 0
     li    a7, 214
     ecall
@@ -2328,15 +2338,15 @@ storeC:
     addi  s5, s5, -1
     bnez  s5, passC
     li    s6, 0
-    li    t0, 0
+    mv    t2, s0
     li    t1, {STOREOFF_BUF}
 sum:
-    add   t2, s0, t0
     lbu   t3, 0(t2)
     slli  s6, s6, 1
     xor   s6, s6, t3
-    addi  t0, t0, 1
-    bne   t0, t1, sum
+    addi  t2, t2, 1
+    addi  t1, t1, -1
+    bnez  t1, sum
     li    t0, 0
     li    t1, 64
 hsum:
@@ -2375,6 +2385,7 @@ def storeoff_program_expected() -> bytes:
         for k in range(0, STOREOFF_BUF, 4):
             w = (int.from_bytes(buf[k:k + 4], "little") + 3) & 0xFFFFFFFF
             buf[k:k + 4] = w.to_bytes(4, "little")
+    buf = bytearray(bytes([4, 3, 2, 1]) * (STOREOFF_BUF // 4))   # storeD: every word 0x01020304
     s6 = 0
     for b in buf:
         s6 = ((s6 << 1) ^ b) & M
@@ -2383,14 +2394,15 @@ def storeoff_program_expected() -> bytes:
 
 
 def storeoff_sites(ninst, n=3000, seed=12):
-    """Single-bit faults on the store pointer (a0) and the walk's end (a1)."""
+    """Single-bit faults on the walks' pointers (a0, t2), ends (a1) and
+    counters (s1, t1)."""
     import numpy as np
     from oracle.pyoracle import SITE_DT
     r = np.random.default_rng(seed)
     s = np.zeros(n, SITE_DT)
     s["inst"] = r.integers(1, ninst, n)
     s["mask"] = np.uint64(1) << r.integers(0, 64, n).astype(np.uint64)
-    s["target"] = r.choice([10, 11], n)
+    s["target"] = r.choice([10, 11, 9, 7, 6], n)
     s["trial"] = np.arange(n)
     return s
 

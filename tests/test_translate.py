@@ -54,6 +54,12 @@ def test_crc32_loop_proofs():
     assert cnt == 10 | 11 << 8 | 1 << 16
     assert (d0 & 0xFF, (d0 >> 8) & 15, (d0 >> 12) & 15, d0 >> 16, o0, s0) == (10, 0, 1, 0, 0, 0)   # lbu at a0
     assert (d1 & 0xFF, (d1 >> 8) & 15, (d1 >> 12) & 15, d1 >> 16, o1, s1) == (18, 1, 4, 5, 0, 1020)   # lwu at s2+
+    # the buffer fill: sw t0, 0(t2) walks with t2 (+4 per pass), a store at
+    # another induction register (kind 4, the step in the span field)
+    m = re.search(r"TXHANG\(X9, -1, 10u\).*?TXLOOP\((\d+)u, 10u, 1u\); TXLD\(0, (\d+)u, (-?\d+), (\d+)u\);", body)
+    assert m, "buffer fill has no run-off proof"
+    d, o, st = int(m.group(2)), int(m.group(3)), int(m.group(4))
+    assert (d & 0xFF, (d >> 8) & 15, (d >> 12) & 15, o, st) == (7, 4, 4, 0, 4)
 
 
 def test_clean_body_shape():
@@ -70,9 +76,9 @@ def test_clean_body_shape():
 def test_crc32_loop_estimates():
     """The counted loops the translator exports for the solo order's work-left
     estimate (fi_types.h LoopEst, fi_kernels.hip solo_work_left): the loops
-    its hang proofs recognise -- crc32's table inner bit loop (t6 counts
-    down) and the crc loop (a0 runs up to a1) -- each with its instructions
-    per pass and a text span around its blocks."""
+    its hang proofs recognise -- crc32's buffer fill (s1 counts down), table
+    inner bit loop (t6 counts down) and crc loop (a0 runs up to a1) -- each
+    with its instructions per pass and a text span around its blocks."""
     from shrewd_amd.fi import lib
     L = lib()
     L.fi_debug_loop_est.restype = C.c_int
@@ -91,9 +97,10 @@ def test_crc32_loop_estimates():
     loops = {(int(r["reg"]), int(r["treg"]), int(r["step"]), int(r["m"])): (int(r["lo"]), int(r["hi"])) for r in out}
     assert (10, 11, 1, 10) in loops     # crc_loop: lbu .. addi a0, a0, 1; bne a0, a1
     assert (31, 0, -1, 5) in loops      # tbl_inner: addi t6, t6, -1; bnez t6 (shortest pass: 5)
-    # the buffer fill (gen: sw t0, 0(t2) .. addi s1, s1, -1; bnez s1) stores:
-    # no proof, no estimate (the golden remainder stands)
-    assert not any(k[0] == 9 for k in loops) and len(loops) == 2
+    # the buffer fill (gen: sw t0, 0(t2); addi t2, t2, 4; addi s1, s1, -1;
+    # bnez s1): its store walks with the pointer t2, an induction register of
+    # its own (round 6: run-off proofs with stores)
+    assert (9, 0, -1, 10) in loops and len(loops) == 3
     lo, hi = loops[(10, 11, 1, 10)]
     assert lo == 0x16C and hi == 0x16C + 0x22   # the crc loop's one block (pc 0x1016c, 34 bytes)
 
