@@ -660,7 +660,7 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
     // kind 0 counter load, 1 bounded load, 2 counter store, 3 / 4 load / store
     // at another induction register (span = its step per iteration, int32)
     struct ProofLoad { uint32_t reg, kind, size, pos; int64_t off; uint64_t span; };
-    struct HangProof { uint32_t reg, treg; int step; uint32_t m; std::vector<ProofLoad> loads; };
+    struct HangProof { uint32_t reg, treg; int step; uint32_t m; std::vector<ProofLoad> loads; bool rel = false; };
     std::map<uint32_t, HangProof> hang_proof;
     // abstract value of a register inside a run-off block: TOP unknown; CNT the
     // counter's value at the iteration's start + lo; BND base register (0: none)
@@ -852,6 +852,211 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         }
     }
 
+    // ---- region proofs (round 6): an outer counted loop that calls a leaf
+    // function and reads / writes bounded tables.  Block E ends with
+    // `bltu rc, rl, H` back to a header H (the loop runs while rc < rl,
+    // unsigned), E holds the region's only write of rc, `addi rc, rc, c`
+    // (0 < c <= 8), and rl is written nowhere in the region.  The region is
+    // every block reachable from H by direct edges, a call (`jal ra, f`) into
+    // f's blocks, and f's `ret` back to the call's return site, without
+    // passing E's fall-through (the exit).  Every block of it must be
+    // translated code (no ecall, CSR, indirect jump other than that ret, no
+    // nested call, ra written only by the calls) and every load / store
+    // address a register the region never writes plus a bounded offset (a
+    // table).  Then nothing in the region can leave it but E's exit test,
+    // nothing in it can fault once the tables' pages are in the lane's set
+    // and the stores miss the code range (loop_outcome, kinds 1 / 5), and rc
+    // grows by at most c per pass -- E runs once per pass --, so from any
+    // point of the region the loop passes E at least k = ceil((rl - rc) / c)
+    // more times, at least m instructions apart (m: the shortest pass, callee
+    // included): it commits (k - 1) m instructions before it can leave.  Data
+    // (the hash, the tables' contents, the callee's inner loops) never matter:
+    // a pass that spins inside the region only makes the trial longer.  The
+    // test runs at the dispatch entries of the loop's own blocks (not the
+    // callee's, which other call sites share), including the return site that
+    // every `ret` enters through the dispatch.
+    {
+        std::map<uint32_t, const Block *> blk;
+        for (const Block &b : blocks)
+            if (b.opc == 0 && !b.insts.empty()) blk[b.h0] = &b;
+        for (const Block &E : blocks) {
+            if (E.opc != 0 || E.insts.empty() || !E.term) continue;
+            const PreInst &br = pre[E.insts.back()];
+            if (br.op != OP_bltu || !br.rs1 || !br.rs2 || br.rs1 == br.rs2) continue;
+            const uint64_t epc = g.pc_of(E.insts.back()), hpc = epc + (int64_t)br.imm;
+            uint32_t H;
+            if (!hof(hpc, H) || !blk.count(H) || hpc > epc) continue;
+            const uint32_t rc = br.rs1, rl = br.rs2;
+            int c = 0;
+            for (size_t i = 0; i + 1 < E.insts.size(); i++) {
+                const PreInst &p = pre[E.insts[i]];
+                if ((p.op == OP_addi || p.op == OP_c_addi) && p.rd == rc && p.rs1 == rc && p.imm > 0 && p.imm <= 8) c = p.imm;
+            }
+            if (!c || hang_proof.count(H)) continue;
+            // the region: blocks by direct edges, calls and their returns
+            std::set<uint32_t> own, callee, ret_sites;
+            std::vector<std::pair<uint32_t, bool>> work{{H, false}};
+            std::map<uint32_t, std::vector<uint32_t>> nxt;   // region edges (for the shortest pass)
+            bool ok = true;
+            std::set<std::pair<uint32_t, bool>> seen;
+            while (!work.empty() && ok) {
+                const auto [h, in_f] = work.back();
+                work.pop_back();
+                if (!seen.insert({h, in_f}).second) continue;
+                if (seen.size() > 256) { ok = false; break; }
+                auto bi = blk.find(h);
+                if (bi == blk.end()) { ok = false; break; }
+                const Block &b = *bi->second;
+                (in_f ? callee : own).insert(h);
+                auto go = [&](uint64_t pc, bool f) {
+                    uint32_t t;
+                    if (!hof(pc, t) || !blk.count(t)) { ok = false; return; }
+                    nxt[h].push_back(t);
+                    work.push_back({t, f});
+                };
+                for (size_t i = 0; i < b.insts.size() && ok; i++) {
+                    std::string e;
+                    uint32_t sz;
+                    int sx;
+                    const char *cond;
+                    const PreInst &p = pre[b.insts[i]];
+                    const uint64_t pc = g.pc_of(b.insts[i]);
+                    const Cls k = classify(p, e, sz, sx, cond);
+                    if (k == C_STOP) ok = false;
+                    else if (k == C_BR) {
+                        if (&b == &E && i + 1 == b.insts.size()) { go(hpc, false); continue; }   // the exit: not followed
+                        go(pc + (int64_t)p.imm, in_f);
+                        go(pc + p.len, in_f);
+                    } else if (k == C_JAL) {
+                        if (p.rd == 0) go(pc + (int64_t)p.imm, in_f);
+                        else if (p.rd == 1 && !in_f) {   // a call: the callee, and the return site after it
+                            uint32_t rs;
+                            if (!hof(pc + p.len, rs) || !blk.count(rs)) { ok = false; continue; }
+                            ret_sites.insert(rs);
+                            go(pc + (int64_t)p.imm, true);
+                            work.push_back({rs, false});   // (no edge: a pass goes through the callee)
+                        }
+                        else ok = false;   // another link register, or a nested call
+                    } else if (k == C_JALR) {
+                        // only a callee's `ret` (jalr x0, 0(ra)), back to the return sites
+                        if (!(in_f && p.rd == 0 && p.rs1 == 1 && p.imm == 0)) ok = false;
+                    }
+                }
+                if (ok && !b.term) go(g.pc_of(b.insts.back()) + pre[b.insts.back()].len, in_f);
+            }
+            if (!ok || own.empty() || !own.count(E.h0)) continue;
+            for (uint32_t r : ret_sites) {   // each ret continues at the return sites
+                for (uint32_t f : callee) {
+                    const Block &fb = *blk[f];
+                    const PreInst &lp = pre[fb.insts.back()];
+                    std::string e;
+                    uint32_t sz;
+                    int sx;
+                    const char *cond;
+                    if (classify(lp, e, sz, sx, cond) == C_JALR) nxt[f].push_back(r);
+                }
+            }
+            // writes, accesses: every block of the region (own and callee)
+            std::set<uint32_t> all(own);
+            all.insert(callee.begin(), callee.end());
+            uint32_t writes[32] = {0};
+            for (uint32_t h : all) {
+                const Block &b = *blk[h];
+                for (uint32_t hh : b.insts) {
+                    std::string e;
+                    uint32_t sz;
+                    int sx;
+                    const char *cond;
+                    const PreInst &p = pre[hh];
+                    const Cls k = classify(p, e, sz, sx, cond);
+                    if ((k == C_ALU || k == C_LOAD || k == C_JAL) && p.rd) writes[p.rd]++;
+                }
+            }
+            if (writes[rc] != 1 || writes[rl] != 0) continue;
+            {   // ra: written only by the calls (one jal per call site)
+                uint32_t jals = 0;
+                for (uint32_t h : own) {
+                    const Block &b = *blk[h];
+                    const PreInst &lp = pre[b.insts.back()];
+                    if (lp.op == OP_jal && lp.rd == 1) jals++;
+                }
+                if (writes[1] != jals) continue;
+            }
+            // the accesses: a register the region never writes + a bounded offset
+            std::vector<ProofLoad> acc;
+            for (uint32_t h : all) {
+                const Block &b = *blk[h];
+                AVal av[32];
+                for (uint32_t r = 0; r < 32; r++) av[r] = writes[r] ? AVal{AV_TOP, 0, 0, 0} : AVal{AV_BND, r, 0, 0};
+                for (size_t i = 0; i < b.insts.size() && ok; i++) {
+                    std::string e;
+                    uint32_t sz;
+                    int sx;
+                    const char *cond;
+                    const PreInst &p = pre[b.insts[i]];
+                    const Cls k = classify(p, e, sz, sx, cond);
+                    const AVal A = av[p.rs1], B = av[p.rs2];
+                    const int64_t imm = p.imm;
+                    if (k == C_LOAD || k == C_STORE) {
+                        if (A.k != AV_BND || !A.base || A.hi - A.lo >= (1 << 20) || A.lo + imm <= -((int64_t)1 << 31) ||
+                            A.lo + imm >= ((int64_t)1 << 31)) { ok = false; break; }
+                        const ProofLoad l{A.base, k == C_STORE ? 5u : 1u, sz, 0u, A.lo + imm, (uint64_t)(A.hi - A.lo)};
+                        bool dup = false;
+                        for (ProofLoad &q : acc)
+                            if (q.reg == l.reg && q.kind == l.kind && q.off == l.off && q.span == l.span) {
+                                q.size = std::max(q.size, l.size);
+                                dup = true;
+                            }
+                        if (!dup) acc.push_back(l);
+                        if (k == C_LOAD && p.rd) av[p.rd] = AVal{AV_TOP, 0, 0, 0};
+                        continue;
+                    }
+                    if (!p.rd || (k != C_ALU && k != C_JAL)) continue;
+                    AVal v{AV_TOP, 0, 0, 0};
+                    if (k == C_ALU) switch (p.op) {
+                    case OP_addi: case OP_c_addi: case OP_c_addi4spn: case OP_c_addi16sp: v = av_add(A, av_const(imm, imm)); break;
+                    case OP_add: case OP_c_add: v = av_add(A, B); break;
+                    case OP_c_mv: v = B; break;
+                    case OP_andi: case OP_c_andi: if (imm >= 0) v = av_const(0, imm); break;
+                    case OP_c_zext_b: v = av_const(0, 0xFF); break;
+                    case OP_c_zext_h: v = av_const(0, 0xFFFF); break;
+                    case OP_slli: case OP_c_slli: v = av_shl(A, imm); break;
+                    case OP_srli: case OP_c_srli: if (imm >= 44 && imm < 64) v = av_const(0, (int64_t)((1ULL << (64 - imm)) - 1)); break;
+                    case OP_sh1add: v = av_add(av_shl(A, 1), B); break;
+                    case OP_sh2add: v = av_add(av_shl(A, 2), B); break;
+                    case OP_sh3add: v = av_add(av_shl(A, 3), B); break;
+                    case OP_c_li: case OP_lui: v = av_const(imm, imm); break;
+                    default: break;
+                    }
+                    av[p.rd] = v;
+                }
+                if (!ok) break;
+            }
+            if (!ok || acc.empty() || acc.size() > 4) continue;
+            // m: the shortest pass, H around to E's end (callee included)
+            std::map<uint32_t, uint32_t> dist;
+            std::set<std::pair<uint32_t, uint32_t>> q;
+            dist[H] = (uint32_t)blk[H]->insts.size();
+            q.insert({dist[H], H});
+            uint32_t m = 0;
+            while (!q.empty()) {
+                const auto [d, v] = *q.begin();
+                q.erase(q.begin());
+                if (d != dist[v]) continue;
+                if (v == E.h0) { m = d; break; }
+                for (uint32_t t : nxt[v]) {
+                    if (t == H) continue;
+                    const uint32_t nd = d + (uint32_t)blk[t]->insts.size();
+                    if (!dist.count(t) || nd < dist[t]) { dist[t] = nd; q.insert({nd, t}); }
+                }
+            }
+            if (!m) continue;
+            HangProof P{rc, rl, c, m, acc, true};
+            for (uint32_t h : own)
+                if (!hang_proof.count(h)) hang_proof[h] = P;
+        }
+    }
+
     // ---- clean body budget tests.  Only a check point tests the budget: a
     // top-level block or a cycle header (the dispatch and the back edges enter
     // those), or a block routed to through its headers (the routing tests it).
@@ -925,9 +1130,11 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
         if (hp == hang_proof.end()) return std::string();
         const HangProof &P = hp->second;
         const std::string x = P.treg ? sfmt("X%u - X%u", P.reg, P.treg) : sfmt("X%u", P.reg);
-        std::string r = sfmt("if (TXHANG(%s, %d, %uu)) { spc = %s; hang = 1u; TXLOOP(%uu, %uu, %uu); ", x.c_str(), P.step,
-                             P.m, hex(g.pc_of(h)).c_str(), P.reg | P.treg << 8 | (uint32_t)(uint8_t)(int8_t)P.step << 16,
-                             P.m, (uint32_t)P.loads.size());
+        const uint32_t lp = P.reg | P.treg << 8 | (uint32_t)(uint8_t)(int8_t)P.step << 16 | (P.rel ? 1u << 24 : 0u);
+        std::string r = P.rel ? sfmt("if (TXHANGU(X%u, X%u, %d, %uu)) { spc = %s; hang = 1u; TXLOOP(%uu, %uu, %uu); ", P.reg,
+                                     P.treg, P.step, P.m, hex(g.pc_of(h)).c_str(), lp, P.m, (uint32_t)P.loads.size())
+                              : sfmt("if (TXHANG(%s, %d, %uu)) { spc = %s; hang = 1u; TXLOOP(%uu, %uu, %uu); ", x.c_str(),
+                                     P.step, P.m, hex(g.pc_of(h)).c_str(), lp, P.m, (uint32_t)P.loads.size());
         for (size_t j = 0; j < P.loads.size(); j++) {
             const ProofLoad &l = P.loads[j];
             r += sfmt("TXLD(%u, %uu, %d, %uu); ", (uint32_t)j, l.reg | l.kind << 8 | l.size << 12 | l.pos << 16,

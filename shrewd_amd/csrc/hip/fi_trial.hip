@@ -1690,6 +1690,16 @@ __device__ __forceinline__ bool tx_hang_proof(uint64_t x, int c, uint32_t m, uin
     const uint64_t n = loop_passes(x, c);
     return n - 1 >= ((uint64_t)left + m - 1) / m;
 }
+// A region loop (fi_translate.cpp region proofs) that runs while x < l
+// (unsigned), x growing by c per pass: it passes its exit test at least
+// ceil((l - x) / c) more times (x >= l: it may leave at the next test).
+__device__ __forceinline__ uint64_t loop_passes_u(uint64_t x, uint64_t l, int c) {
+    return x < l ? (l - x - 1) / (uint64_t)c + 1 : 0;
+}
+__device__ __forceinline__ bool tx_hang_proof_u(uint64_t x, uint64_t l, int c, uint32_t m, uint32_t left) {
+    const uint64_t n = loop_passes_u(x, l, c);
+    return n != 0 && n - 1 >= ((uint64_t)left + m - 1) / m;
+}
 
 // Is vpn in the lane's page set?  (lookup_full without the TLB insert)
 __device__ __forceinline__ bool page_mapped(KCtx *c, const WaveMem &w, const LaneMem &m, uint64_t slot, uint64_t vpn) {
@@ -1723,19 +1733,23 @@ __device__ __noinline__ int loop_outcome(KCtx *c, const WaveMem &w, const LaneMe
     const uint32_t cnt = io->lp_cnt, mm = io->lp_m, nl = io->lp_n;
     const uint32_t cr = cnt & 0xFF, tr = (cnt >> 8) & 0xFF;
     const int cs = (int)(int8_t)(uint8_t)(cnt >> 16);
-    if (!mm || nl > 4 || !cr) return 0;
-    const uint64_t x = R[cr], n = loop_passes(x - (tr ? R[tr] : 0ULL), cs);
+    const bool rel = (cnt >> 24) & 1;   // a region loop: runs while x < R[tr] (bounded accesses only)
+    if (!mm || nl > 4 || !cr || (rel && (!tr || cs <= 0))) return 0;
+    const uint64_t x = R[cr], n = rel ? loop_passes_u(x, R[tr], cs) : loop_passes(x - (tr ? R[tr] : 0ULL), cs);
+    if (rel && n == 0) return 0;
     uint64_t best_k = ~0ULL, best_a = 0;
     for (uint32_t j = 0; j < nl; j++) {
         const uint32_t d = io->lp_ld[j][0], br = d & 0xFF, kind = (d >> 8) & 15, size = (d >> 12) & 15, pos = d >> 16;
         const int64_t off = (int64_t)(int32_t)io->lp_ld[j][1];
-        if (kind == 1) {   // bounded: every page of its range in the set
+        if (kind == 1 || kind == 5) {   // bounded (5: a store): every page of its range in the set
             const uint64_t lo = (br ? R[br] : 0ULL) + (uint64_t)off, hi = lo + io->lp_ld[j][2] + size - 1;
             if (hi < lo || (hi >> 12) - (lo >> 12) > 8) return 0;
             for (uint64_t v = lo >> 12; v <= (hi >> 12); v++)
                 if (!page_mapped(c, w, m, slot, v)) return 0;
+            if (kind == 5 && !(hi < c->code_lo || lo >= c->code_hi)) return 0;   // it could rewrite code
             continue;
         }
+        if (rel) return 0;   // (region proofs pass bounded accesses only)
         // kinds 0 / 2 walk with the counter, 3 / 4 with another induction
         // register (its value at the loop's first instruction, its own step)
         const int64_t st = kind >= 3 ? (int64_t)(int32_t)io->lp_ld[j][2] : (int64_t)cs;
@@ -1811,6 +1825,7 @@ __device__ __noinline__ void solo_tx_clean_run(KCtx *CX, lds_u64 *R, lds_mem *mp
 #define SOVER(n_) (st + (n_) > bud)
 #define SDONE() (st)
 #define TXHANG(x_, c_, m_) (hok && tx_hang_proof((x_), (c_), (m_), hleft - SDONE()))
+#define TXHANGU(x_, l_, c_, m_) (hok && tx_hang_proof_u((x_), (l_), (c_), (m_), hleft - SDONE()))
 #define TXLOOP(c_, m_, n_) (io->lp_cnt = (c_), io->lp_m = (m_), io->lp_n = (n_))
 #define TXLD(j_, d_, o_, s_) (io->lp_ld[j_][0] = (d_), io->lp_ld[j_][1] = (uint32_t)(o_), io->lp_ld[j_][2] = (s_))
 #define TXR(r) uint64_t X##r = R[r];

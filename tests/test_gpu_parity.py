@@ -500,6 +500,35 @@ def test_storeoff_loop_proofs(oracle_mod):
     assert ins_on < ins_off
 
 
+def test_region_loop_proofs(engine_factory, oracle_mod):
+    """intmix's loop bound s3 flipped high: the main loop (a call and table
+    stores per pass) runs to the hang cap.  The region proof (fi_translate.cpp,
+    fi_trial.hip loop_outcome: bounded accesses, kinds 1 / 5) ends those
+    trials as hangs at their next dispatch entry into the loop (stats[56]);
+    every record equals the oracle's, with the proofs on and off."""
+    from oracle.pyoracle import SITE_DT
+    from shrewd_amd.fi import CFG_NO_HANG_PROOF
+    o = oracle_for(oracle_mod, "intmix")
+    g = o.run_golden()
+    r = np.random.default_rng(21)
+    n = 256
+    s = np.zeros(n, SITE_DT)
+    s["inst"] = r.integers(1000, g.ninst - 1000, n)
+    s["mask"] = np.uint64(1) << r.integers(0, 64, n).astype(np.uint64)
+    s["target"] = 19
+    s["trial"] = np.arange(n)
+    ref = o.run_trials(s, protect_mask=0)
+    got = []
+    for flags in (0, CFG_NO_HANG_PROOF):
+        e = engine_factory("intmix", flags=flags)
+        dev, h = e.run_sites(s)
+        compare(dev, ref, s)
+        got.append((int(e.debug_stats()[56]), int(h["device_insts"])))
+    (hang_on, ins_on), (hang_off, ins_off) = got
+    assert (ref["cls"] == 3).sum() > 50
+    assert hang_on > 20 and hang_off == 0 and ins_on < ins_off // 2, got
+
+
 def test_run_trials_equals_run_sites(engine_factory):
     e = engine_factory("crc32")
     e.set_campaign(4242, REGS | PC, 1)

@@ -1,8 +1,8 @@
 """The load-time translator's loop proofs on the CPU (fi_translate.cpp; no GPU:
 fi_debug_translate runs on the host).  Inputs: crc32's pre-decoded text and
 golden block trace, as the engine dumps them (tools/gpu/dump_golden.py ->
-tests/golden/tx_inputs_crc32.npz, the engine's own output, not reference
-data).  The device side of the same proofs is tested against the oracle in
+tests/golden/tx_inputs_{crc32,intmix}.npz, the engine's own output, not
+reference data).  The device side of the same proofs is tested against the oracle in
 tests/test_gpu_parity.py (test_counted_loop_hang_proofs,
 test_runoff_loop_proofs)."""
 import ctypes as C
@@ -14,14 +14,14 @@ import numpy as np
 from conftest import ROOT
 
 
-def _translate(env=None):
+def _translate(env=None, name="crc32"):
     from shrewd_amd.fi import lib
     old = {k: os.environ.get(k) for k in (env or {})}
     os.environ.update(env or {})
     try:
         L = lib()
         L.fi_debug_translate.restype = C.c_int
-        z = np.load(os.path.join(ROOT, "tests", "golden", "tx_inputs_crc32.npz"))
+        z = np.load(os.path.join(ROOT, "tests", "golden", f"tx_inputs_{name}.npz"))
         pre, tr = np.ascontiguousarray(z["pre"]), np.ascontiguousarray(z["trace"])
         n = C.c_uint64()
         L.fi_debug_translate(pre.ctypes.data, len(pre), int(z["text_lo"]), tr.ctypes.data, len(tr), None, 0, C.byref(n))
@@ -117,3 +117,23 @@ def test_clean_body_temporaries_at_function_scope():
     src = open(os.path.join(ROOT, "shrewd_amd", "csrc", "hip", "fi_trial.hip")).read()
     fn = src[src.index("void solo_tx_clean_run("):src.index("/*@TX_SOLO_CLEAN@*/")]
     assert "TX_TEMPS();" in fn
+
+
+def test_intmix_region_proof():
+    """intmix's main loop (loop: ... call popcnt ... sd t3, 0(t2) ... skip:
+    addi s2, s2, 1; bltu s2, s3, loop) is a region proof (round 6,
+    fi_translate.cpp): it runs while s2 < s3, s2 grows by one per pass, the
+    pass calls a leaf (popcnt, its own counted inner loop) and reads / writes
+    the acc table at s1 + [0, 4088] and pctab at s0 + [0, 255] -- bounded
+    accesses at registers the region never writes (kinds 1 and 5).  The
+    shortest pass (callee included) is 30 instructions; the test sits at the
+    loop's own blocks only (the callee's are shared with its other callers)."""
+    body = _translate(name="intmix")
+    clean = body.split("/*@TX_SPLIT@*/")[-1]
+    tests = re.findall(r"case (\d+): if \(TXHANGU\(X18, X19, 1, 30u\)\).*?TXLOOP\((\d+)u, 30u, 3u\); "
+                       r"TXLD\(0, (\d+)u, 0, 4088u\); TXLD\(1, (\d+)u, 0, 4088u\); TXLD\(2, (\d+)u, 0, 255u\);", clean)
+    assert len(tests) == 4, tests
+    for _, lp, d0, d1, d2 in tests:
+        assert int(lp) == 18 | 19 << 8 | 1 << 16 | 1 << 24
+        assert [(int(d) & 0xFF, (int(d) >> 8) & 15, (int(d) >> 12) & 15) for d in (d0, d1, d2)] == [(9, 1, 8), (9, 5, 8), (8, 1, 1)]
+    assert "TXHANGU" not in body.split("/*@TX_SPLIT@*/")[1]   # the full solo body has no proofs
