@@ -3669,6 +3669,9 @@ leave:
 // crc32 (tools/gpu/solo_ab.sh, profiles/r02j_solo_ab.txt): 1 (no bound, 136-140
 // VGPRs, 3 waves) 6.44M, 4: 7.06M trials/s; VGPR-pinned guest registers
 // 3.2-3.7M.
+#ifndef FI_SOLO_DIRTY_PRIO   // solo waves of trials that rewrote code run at this priority (0: no change)
+#define FI_SOLO_DIRTY_PRIO 0
+#endif
 #ifndef FI_SOLO_AGE   // solo waves raise their priority at 2^k, 2^(k+1), 2^(k+2) instructions (0: off)
 #define FI_SOLO_AGE 0
 #endif
@@ -4109,6 +4112,13 @@ __device__ __forceinline__ void trial_body() {
             next_snap += CX->rec_interval;
         }
 
+#if FI_SOLO_DIRTY_PRIO
+        // a solo trial that rewrote its code runs interpreted, ~10x slower per
+        // instruction than translated code: the issue arbiter prefers it
+        if constexpr (kNL == 1) {
+            if (m.code_dirty) __builtin_amdgcn_s_setprio(FI_SOLO_DIRTY_PRIO);
+        }
+#endif
         const bool ready = !L.done && m.req_vpn == kNone;
         const uint64_t act = wballot<kNL>(ready);
         if (act == 0) {
