@@ -938,8 +938,9 @@ std::string translate_blocks(const std::vector<PreInst> &pre, uint64_t text_lo, 
                         }
                         else ok = false;   // another link register, or a nested call
                     } else if (k == C_JALR) {
-                        // only a callee's `ret` (jalr x0, 0(ra)), back to the return sites
-                        if (!(in_f && p.rd == 0 && p.rs1 == 1 && p.imm == 0)) ok = false;
+                        // only a callee's `ret` (jalr x0, 0(ra) or c.jr ra), back to the
+                        // return sites (c.jalr links ra: no)
+                        if (!(in_f && p.op != OP_c_jalr && p.rd == 0 && p.rs1 == 1 && p.imm == 0)) ok = false;
                     }
                 }
                 if (ok && !b.term) go(g.pc_of(b.insts.back()) + pre[b.insts.back()].len, in_f);
